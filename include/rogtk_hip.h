@@ -1,0 +1,194 @@
+/*
+ * rogtk_hip.h — C ABI of librogtk_hip.so, the MI355X-native (gfx950) engine for
+ * rogtk's UMI score + cluster hot path.
+ *
+ * Boundary. In the reference (tzeitim/rogtk) this path is reached through polars
+ * plugin calls into Rust (pyo3-polars #[polars_expr]); the per-row loops live in
+ *   src/expressions.rs:1234-1284   umi_complexity_all_expr      (H1, struct of 7)
+ *   src/expressions.rs:1286-1410   umi_*_expr single fields     (H1, 7 exprs)
+ *   src/expressions.rs:1048-1073   hamming_distance_expr        (H2)
+ *   src/expressions.rs:1075-1101   hamming_within_expr          (H2)
+ *   src/umi_score.rs:17-200        calculate_umi_complexity     (H1 arithmetic)
+ *   rogtk/__init__.py:206-214      caller-side group_by('umi')  (H3 semantics)
+ * Each entry point below cites the reference interface it replaces. The plain-C
+ * signatures (pointers + sizes, no torch / no HIP types) are what a Rust
+ * `extern "C"` block, cgo, JNI or ctypes binds.
+ *
+ * Conventions
+ *  - Every function returns ROGTK_OK (0) or an error code; the message of the
+ *    last failure on the calling thread is rogtk_last_error(). No C++ exception
+ *    and no abort ever crosses this boundary.
+ *  - Strings use the Arrow C Data layout: offsets (int32 or int64, n+1 entries),
+ *    values (UTF-8 bytes), optional validity bitmap (LSB bit order) with a bit
+ *    offset. Null in -> null out (the caller reuses the input validity).
+ *  - "Packed SoA": codes[i] holds a regular UMI 2 bits per base, FIRST base in the
+ *    most significant bits, A=0 C=1 G=2 T=3 (code order == lexicographic order).
+ *    regular_bits[i/64] bit (i%64) = row i is valid, has byte length umi_len
+ *    (1..16) and contains only 'A','C','G','T'. All other valid rows are
+ *    "irregular" and are computed by the byte-path kernels (same results).
+ *  - Level-1 functions take DEVICE pointers and a hipStream_t passed as void*
+ *    (NULL = legacy default stream); they only enqueue work (graph-capturable,
+ *    no allocation, no synchronisation) unless documented otherwise.
+ *  - Level-2 functions (*_host) take HOST Arrow buffers, run on a per-thread
+ *    device context and return when the results are in the host buffers.
+ */
+#ifndef ROGTK_HIP_H
+#define ROGTK_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ROGTK_OK 0
+#define ROGTK_E_INVALID 1     /* bad argument */
+#define ROGTK_E_HIP 2         /* HIP runtime failure */
+#define ROGTK_E_UNSUPPORTED 3 /* valid input outside what this build supports */
+#define ROGTK_E_NODEVICE 4    /* no usable gfx950 device */
+#define ROGTK_E_OVERFLOW 5    /* a capacity given by the caller was exceeded */
+
+/* ------------------------------------------------------------------ basics */
+const char* rogtk_version(void);
+const char* rogtk_last_error(void);
+/* Number of visible HIP devices (0 when none). */
+int rogtk_device_count(int* out_count);
+
+/*
+ * Output set of UMI complexity scoring: ComplexityScore (umi_score.rs:5-13)
+ * exported in the field order of umi_complexity_struct_output_type
+ * (expressions.rs:1219-1232). NULL members are neither computed nor written,
+ * which is how the seven single-field expressions (expressions.rs:1286-1410)
+ * avoid the reference's 7x recomputation.
+ */
+typedef struct rogtk_umi_scores {
+    double* shannon_entropy;
+    double* linguistic_complexity;
+    double* homopolymer_fraction;
+    double* dinucleotide_entropy;
+    uint32_t* longest_homopolymer_run;
+    double* dust_score;
+    double* combined_score;
+} rogtk_umi_scores;
+
+/* ============================ Level 1: device ============================ */
+
+/*
+ * Stage a device-resident Arrow string column into the packed SoA.
+ * Writes codes[n] (0 for non-regular rows), regular_bits[ceil(n/64)], and the
+ * indices of valid irregular rows to irregular_rows[0 .. *n_irregular) (order
+ * unspecified; capacity n). *n_irregular is a DEVICE int64 zeroed by this call.
+ * Replaces the per-row `ca.iter()` string walk of expressions.rs:1246/1054.
+ */
+int rogtk_stage_strings(const void* offsets, int offset_width, const uint8_t* values,
+                        const uint8_t* validity, int64_t validity_offset, int64_t n,
+                        int umi_len, uint32_t* codes, uint64_t* regular_bits,
+                        int64_t* irregular_rows, int64_t* n_irregular, void* stream);
+
+/*
+ * Fused per-read pass over the packed SoA (the hot kernel):
+ *   H1 scores   -> scores  (NULL = skip)            umi_complexity_all_expr, expressions.rs:1234
+ *   H2 Hamming  -> hamming_distance[n] (u32, u32::MAX on length mismatch) and/or
+ *                  hamming_within_bits[ceil(n/64)] (bit-packed Arrow boolean, LSB
+ *                  order, distance <= max_distance)    expressions.rs:1048-1101
+ *                  target = host bytes (any UTF-8); target == NULL skips H2
+ *   H3 mark     -> cluster_ws presence table (NULL = skip), see rogtk_cluster_*
+ * Rows whose regular bit is 0 get zeros everywhere (fix irregular rows up with
+ * rogtk_umi_score_rows; null rows stay behind the caller's validity bitmap).
+ * regular_bits == NULL means every row is regular.
+ */
+int rogtk_umi_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
+                           int umi_len, const rogtk_umi_scores* scores,
+                           const uint8_t* target, int64_t target_len, uint32_t max_distance,
+                           uint32_t* hamming_distance, uint64_t* hamming_within_bits,
+                           void* cluster_ws, int64_t cluster_max_distinct, void* stream);
+
+/*
+ * Byte path: the same outputs for an explicit list of rows of a device Arrow
+ * string column (rows[0 .. *n_rows_dev), at most max_rows), computed straight
+ * from the UTF-8 bytes with the reference's byte semantics (umi_score.rs: every
+ * byte counts toward totals; 'N'/lowercase are ordinary bytes; DUST for len>=64;
+ * empty string -> combined NaN). max_len >= the byte length of every listed row
+ * (sizes the entropy table). hamming_within_bits is updated with atomic OR.
+ * Replaces calculate_umi_complexity (umi_score.rs:17) for non-packable UMIs.
+ */
+int rogtk_umi_score_rows(const void* offsets, int offset_width, const uint8_t* values,
+                         const int64_t* rows, const int64_t* n_rows_dev, int64_t max_rows,
+                         int64_t max_len, const rogtk_umi_scores* scores,
+                         const uint8_t* target, int64_t target_len, uint32_t max_distance,
+                         uint32_t* hamming_distance, uint64_t* hamming_within_bits,
+                         void* stream);
+
+/*
+ * H3 — UMI cluster assignment over the packed SoA (spec: DESIGN.md §H3; the
+ * reference groups in the caller, rogtk/__init__.py:206-214). Regular UMIs of
+ * length umi_len (1..16) are clustered exactly (max_distance 0) or as connected
+ * components of the Hamming<=1 graph (max_distance 1). Cluster ids are dense,
+ * in order of each cluster's smallest code. The workspace is a device buffer of
+ * rogtk_cluster_workspace_size() bytes, zeroed once by rogtk_cluster_init().
+ * max_distinct bounds the distinct regular UMIs across all shards
+ * (<= min(4^umi_len, total rows)).
+ *
+ * Single GPU:  init (once) -> mark (or score_packed with cluster_ws)
+ *              -> local_bitmap -> resolve(bitmap, 1) -> assign
+ * N GPUs:      each rank: mark -> local_bitmap -> all-gather the bitmaps (RCCL)
+ *              -> resolve(gathered, N) -> assign. Every rank resolves the same
+ *              global components, so ids are identical for any GPU count.
+ */
+int rogtk_cluster_workspace_size(int umi_len, int64_t max_distinct, int64_t* bytes);
+int rogtk_cluster_bitmap_words(int umi_len, int64_t* words);
+int rogtk_cluster_init(void* ws, int umi_len, int64_t max_distinct, void* stream);
+int rogtk_cluster_mark(const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
+                       int umi_len, void* ws, int64_t max_distinct, void* stream);
+/* presence table -> bitmap words (rogtk_cluster_bitmap_words); clears presence */
+int rogtk_cluster_local_bitmap(void* ws, int umi_len, int64_t max_distinct,
+                               uint64_t* bitmap_out, void* stream);
+/* bitmaps: n_bitmaps bitmaps laid out back to back (all-gather output layout) */
+int rogtk_cluster_resolve(void* ws, int umi_len, int64_t max_distinct,
+                          const uint64_t* bitmaps, int n_bitmaps, int max_distance,
+                          void* stream);
+/* cluster_id[i] for regular rows; 0xFFFFFFFF for the others */
+int rogtk_cluster_assign(const void* ws, int umi_len, int64_t max_distinct,
+                         const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
+                         uint32_t* cluster_id, void* stream);
+/* Copies {n_distinct, n_clusters, overflow, error} (int64 each) to host; syncs the stream. */
+int rogtk_cluster_stats(const void* ws, int umi_len, int64_t max_distinct, int64_t* out4,
+                        void* stream);
+
+/* ========================= Level 2: host buffers ========================= */
+
+/* umi_complexity_all_expr + the 7 single-field exprs (expressions.rs:1234-1410). */
+int rogtk_umi_complexity_host(const void* offsets, int offset_width, const uint8_t* values,
+                              int64_t values_len, const uint8_t* validity,
+                              int64_t validity_offset, int64_t n, const rogtk_umi_scores* out);
+
+/* hamming_distance_expr / hamming_within_expr (expressions.rs:1048-1101).
+ * within_bits: Arrow bit-packed (LSB order), ceil(n/8) bytes; either output NULL = skip. */
+int rogtk_hamming_host(const void* offsets, int offset_width, const uint8_t* values,
+                       int64_t values_len, const uint8_t* validity, int64_t validity_offset,
+                       int64_t n, const uint8_t* target, int64_t target_len,
+                       uint32_t max_distance, uint32_t* distance, uint8_t* within_bits);
+
+/* H3 over a host column: regular rows clustered on the GPU (umi_len <= 0:
+ * length of the first non-null row); irregular non-null rows grouped by exact
+ * bytes and numbered after the regular clusters in byte-lexicographic order.
+ * cluster_id of null rows = 0xFFFFFFFF. */
+int rogtk_umi_cluster_host(const void* offsets, int offset_width, const uint8_t* values,
+                           int64_t values_len, const uint8_t* validity, int64_t validity_offset,
+                           int64_t n, int umi_len, int max_distance, uint32_t* cluster_id,
+                           int64_t* n_clusters, int* resolved_umi_len);
+
+/* ============================== profiling ================================ */
+/* When enabled, every kernel launch is bracketed by HIP events on its stream. */
+int rogtk_profile_enable(int on);
+int rogtk_profile_reset(void);
+/* Total device milliseconds and launch count recorded for `kernel` (synchronises
+ * the recorded events). Kernel names: "stage", "score_packed", "score_rows",
+ * "cluster_mark", "cluster_bitmap", "cluster_scan", "cluster_compact",
+ * "cluster_union", "cluster_flatten", "cluster_label", "cluster_assign". */
+int rogtk_profile_read(const char* kernel, double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ROGTK_HIP_H */

@@ -1,0 +1,391 @@
+// =============================================================================
+// rogtk_oracle.cpp — TEST INFRASTRUCTURE ONLY. NOT PART OF THE PRODUCT PATH.
+//
+// CPU restatement of the reference (tzeitim/rogtk) algorithms on the UMI
+// score + cluster hot path. Only tests/, __graft_entry__.smoke() and bench.py's
+// cpu_baseline leg may load this library, and only as the checker / the CPU
+// baseline; the product (rogtk_amd + librogtk_hip.so) never links or calls it.
+//
+// Parity pinning: the reference is Rust (no cargo/rustc in this image) and has
+// no tests or golden vectors for these functions. The
+// restatement is pinned by (1) the hand-derived known answers of SURVEY.md
+// Appendix A, (2) an independent pure-Python restatement (oracle/pyoracle.py),
+// and (3) the golden vectors it generated, committed under tests/golden/.
+//
+// Data structures deliberately mirror the reference (per-UMI hash maps, serial
+// row loop) so this also serves as the "port" CPU baseline of bench.py.
+//
+// Deliberate, documented deviation: dinucleotide_entropy sums its terms in
+// ascending (byte0, byte1) order. The reference sums in Rust HashMap
+// iteration order (RandomState, different in every process), so the reference
+// itself is not bit-reproducible there (≤2 ULP spread).
+// `dinuc_order = 1` selects first-occurrence order (the order Appendix A's
+// printed values used) for the KAT check.
+//
+// Build: see oracle/Makefile (g++ -O2 -ffp-contract=off, glibc log2).
+// =============================================================================
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+namespace {
+
+// ---- umi_score.rs:45-73 ------------------------------------------------------
+double shannon_entropy(const uint8_t* s, size_t n) {
+    uint32_t counts[4] = {0, 0, 0, 0};
+    uint32_t total = 0;
+    for (size_t i = 0; i < n; ++i) {
+        total += 1;  // every byte counts toward total (:50), incl. N / lowercase
+        switch (s[i]) {
+            case 'A': counts[0] += 1; break;
+            case 'C': counts[1] += 1; break;
+            case 'G': counts[2] += 1; break;
+            case 'T': counts[3] += 1; break;
+            default: break;
+        }
+    }
+    if (total == 0) return 0.0;
+    double entropy = 0.0;
+    for (int b = 0; b < 4; ++b) {  // fixed A,C,G,T order (:65)
+        if (counts[b] > 0) {
+            double p = (double)counts[b] / (double)total;
+            entropy -= p * std::log2(p);
+        }
+    }
+    return entropy;
+}
+
+// ---- umi_score.rs:77-93 ------------------------------------------------------
+double linguistic_complexity(const uint8_t* s, size_t n) {
+    if (n < 3) return 0.0;
+    const size_t k = 3;
+    std::unordered_map<uint32_t, int> kmers;  // key = the 3-byte window
+    for (size_t i = 0; i + k <= n; ++i) {
+        uint32_t key = ((uint32_t)s[i] << 16) | ((uint32_t)s[i + 1] << 8) | s[i + 2];
+        kmers[key] += 1;
+    }
+    double unique_kmers = (double)kmers.size();
+    double max_possible = (double)std::min<size_t>(n - k + 1, 64);  // 4^3 (:90)
+    return unique_kmers / max_possible;
+}
+
+// ---- umi_score.rs:96-121 -----------------------------------------------------
+double homopolymer_fraction(const uint8_t* s, size_t n) {
+    if (n == 0) return 0.0;
+    size_t in_homopolymer = 0, i = 0;
+    while (i < n) {
+        uint8_t current = s[i];
+        size_t run_length = 1;
+        while (i + run_length < n && s[i + run_length] == current) run_length += 1;
+        if (run_length >= 3) in_homopolymer += run_length;
+        i += run_length;
+    }
+    return (double)in_homopolymer / (double)n;
+}
+
+// ---- umi_score.rs:124-146 ----------------------------------------------------
+double dinucleotide_entropy(const uint8_t* s, size_t n, int order) {
+    if (n < 2) return 0.0;
+    const double total = (double)(n - 1);
+    double entropy = 0.0;
+    if (order == 0) {
+        // canonical: ascending (byte0, byte1) — std::map iterates in key order
+        std::map<std::pair<uint8_t, uint8_t>, int> counts;
+        for (size_t i = 0; i + 2 <= n; ++i) counts[{s[i], s[i + 1]}] += 1;
+        for (const auto& kv : counts) {
+            double p = (double)kv.second / total;
+            entropy -= p * std::log2(p);
+        }
+    } else {
+        // first-occurrence order (SURVEY.md Appendix A convention)
+        std::vector<std::pair<uint16_t, int>> counts;
+        for (size_t i = 0; i + 2 <= n; ++i) {
+            uint16_t key = (uint16_t)((s[i] << 8) | s[i + 1]);
+            auto it = std::find_if(counts.begin(), counts.end(),
+                                   [&](const std::pair<uint16_t, int>& e) { return e.first == key; });
+            if (it == counts.end()) counts.push_back({key, 1});
+            else it->second += 1;
+        }
+        for (const auto& kv : counts) {
+            double p = (double)kv.second / total;
+            entropy -= p * std::log2(p);
+        }
+    }
+    return entropy / 4.0;
+}
+
+// ---- umi_score.rs:149-168 ----------------------------------------------------
+size_t longest_homopolymer_run(const uint8_t* s, size_t n) {
+    if (n == 0) return 0;
+    size_t max_run = 1, current_run = 1;
+    for (size_t i = 1; i < n; ++i) {
+        if (s[i] == s[i - 1]) {
+            current_run += 1;
+            max_run = std::max(max_run, current_run);
+        } else {
+            current_run = 1;
+        }
+    }
+    return max_run;
+}
+
+// ---- umi_score.rs:171-200 ----------------------------------------------------
+double dust_score(const uint8_t* s, size_t n, size_t window_size) {
+    if (n < window_size) return 0.0;
+    double total_score = 0.0;
+    for (size_t i = 0; i + window_size <= n; ++i) {
+        const uint8_t* w = s + i;
+        std::unordered_map<uint32_t, int> triplet_counts;
+        for (size_t j = 0; j + 3 <= window_size; ++j) {
+            uint32_t key = ((uint32_t)w[j] << 16) | ((uint32_t)w[j + 1] << 8) | w[j + 2];
+            triplet_counts[key] += 1;
+        }
+        double window_score = 0.0;
+        for (const auto& kv : triplet_counts) {
+            int count = kv.second;
+            if (count > 1) window_score += (double)(count * (count - 1)) / 2.0;
+        }
+        total_score += window_score;
+    }
+    return total_score / (double)(n - window_size + 1);
+}
+
+struct Score {
+    double shannon, linguistic, homopolymer, dinuc, dust, combined;
+    uint32_t longest;
+};
+
+// ---- umi_score.rs:17-43 ------------------------------------------------------
+Score calculate_umi_complexity(const uint8_t* s, size_t n, int order) {
+    Score r;
+    r.shannon = shannon_entropy(s, n);
+    r.linguistic = linguistic_complexity(s, n);
+    r.homopolymer = homopolymer_fraction(s, n);
+    r.dinuc = dinucleotide_entropy(s, n, order);
+    size_t longest = longest_homopolymer_run(s, n);
+    r.dust = dust_score(s, n, 64);
+    // evaluated left to right, no contraction (built with -ffp-contract=off)
+    r.combined = 0.25 * r.shannon
+               + 0.25 * r.linguistic
+               + 0.15 * (1.0 - r.homopolymer)
+               + 0.15 * r.dinuc
+               + 0.10 * (1.0 - ((double)longest / (double)n))
+               + 0.10 * (1.0 - std::fmin(r.dust, 1.0));
+    r.longest = (uint32_t)longest;  // exported as UInt32 (expressions.rs:1254)
+    return r;
+}
+
+inline bool row_valid(const uint8_t* validity, int64_t bit_offset, int64_t i) {
+    if (!validity) return true;
+    int64_t b = bit_offset + i;
+    return (validity[b >> 3] >> (b & 7)) & 1;
+}
+
+inline void row_span(const void* offsets, int offset_width, int64_t i, int64_t* start, int64_t* len) {
+    if (offset_width == 4) {
+        const int32_t* o = (const int32_t*)offsets;
+        *start = o[i];
+        *len = (int64_t)o[i + 1] - o[i];
+    } else {
+        const int64_t* o = (const int64_t*)offsets;
+        *start = o[i];
+        *len = o[i + 1] - o[i];
+    }
+}
+
+// Decode one UTF-8 scalar (input is a valid Rust &str / Arrow utf8 value).
+inline size_t utf8_next(const uint8_t* s, size_t n, size_t i, uint32_t* cp) {
+    uint8_t c = s[i];
+    size_t w = c < 0x80 ? 1 : (c >> 5) == 0x6 ? 2 : (c >> 4) == 0xE ? 3 : 4;
+    if (i + w > n) w = n - i;
+    uint32_t v = w == 1 ? c : w == 2 ? (c & 0x1F) : w == 3 ? (c & 0x0F) : (c & 0x07);
+    for (size_t k = 1; k < w; ++k) v = (v << 6) | (s[i + k] & 0x3F);
+    *cp = v;
+    return i + w;
+}
+
+// ---- expressions.rs:1054-1069: byte-length check, then chars().zip() ----------
+uint32_t hamming_one(const uint8_t* s, size_t n, const uint8_t* t, size_t tn) {
+    if (n != tn) return UINT32_MAX;
+    uint32_t d = 0;
+    size_t i = 0, j = 0;
+    while (i < n && j < tn) {
+        uint32_t a, b;
+        i = utf8_next(s, n, i, &a);
+        j = utf8_next(t, tn, j, &b);
+        if (a != b) d += 1;
+    }
+    return d;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* oracle_version(void) { return "rogtk-oracle 1 (umi_score.rs/expressions.rs restatement)"; }
+
+// One UMI. out6 = {shannon, linguistic, homopolymer, dinuc, dust, combined}.
+void oracle_umi_complexity(const uint8_t* s, int64_t n, int dinuc_order, double* out6, uint32_t* longest) {
+    Score r = calculate_umi_complexity(s, (size_t)n, dinuc_order);
+    out6[0] = r.shannon; out6[1] = r.linguistic; out6[2] = r.homopolymer;
+    out6[3] = r.dinuc;   out6[4] = r.dust;       out6[5] = r.combined;
+    *longest = r.longest;
+}
+
+// Row loop of umi_complexity_all_expr (expressions.rs:1246-1268). Null rows are
+// skipped (their outputs are left untouched; validity = input validity).
+void oracle_umi_complexity_batch(const void* offsets, int offset_width, const uint8_t* values,
+                                 const uint8_t* validity, int64_t validity_offset, int64_t n,
+                                 int dinuc_order, double* shannon, double* linguistic,
+                                 double* homopolymer, double* dinuc, uint32_t* longest,
+                                 double* dust, double* combined) {
+    for (int64_t i = 0; i < n; ++i) {
+        if (!row_valid(validity, validity_offset, i)) continue;
+        int64_t st, len;
+        row_span(offsets, offset_width, i, &st, &len);
+        Score r = calculate_umi_complexity(values + st, (size_t)len, dinuc_order);
+        if (shannon) shannon[i] = r.shannon;
+        if (linguistic) linguistic[i] = r.linguistic;
+        if (homopolymer) homopolymer[i] = r.homopolymer;
+        if (dinuc) dinuc[i] = r.dinuc;
+        if (longest) longest[i] = r.longest;
+        if (dust) dust[i] = r.dust;
+        if (combined) combined[i] = r.combined;
+    }
+}
+
+// hamming_distance_expr (expressions.rs:1048-1073) / hamming_within_expr
+// (:1075-1101). dist: u32::MAX on byte-length mismatch; within: dist <= max.
+void oracle_hamming_batch(const void* offsets, int offset_width, const uint8_t* values,
+                          const uint8_t* validity, int64_t validity_offset, int64_t n,
+                          const uint8_t* target, int64_t target_len, uint32_t max_distance,
+                          uint32_t* dist, uint8_t* within) {
+    for (int64_t i = 0; i < n; ++i) {
+        if (!row_valid(validity, validity_offset, i)) continue;
+        int64_t st, len;
+        row_span(offsets, offset_width, i, &st, &len);
+        uint32_t d = hamming_one(values + st, (size_t)len, target, (size_t)target_len);
+        if (dist) dist[i] = d;
+        if (within) within[i] = (d != UINT32_MAX && d <= max_distance) ? 1 : 0;
+    }
+}
+
+// ---- H3: UMI cluster assignment (spec owned by this build) ----
+// Regular rows (byte length == L, all of A/C/G/T) are packed 2 bits/base, first
+// base most significant (A=0,C=1,G=2,T=3), so code order == lexicographic order.
+// max_distance 0: clusters = distinct regular UMIs. max_distance 1: connected
+// components of the graph with an edge between distinct UMIs at Hamming 1.
+// Representative = smallest code of the component. Irregular non-null rows are
+// grouped by exact byte equality. Cluster ids are dense: regular clusters in
+// representative-code order, then irregular clusters in byte-lexicographic
+// order. Null rows get no id (out_valid = 0).
+// umi_len <= 0: L = byte length of the first non-null row.
+// Returns the number of clusters, or -1 on bad arguments.
+int64_t oracle_umi_cluster(const void* offsets, int offset_width, const uint8_t* values,
+                           const uint8_t* validity, int64_t validity_offset, int64_t n,
+                           int umi_len, int max_distance, uint32_t* cluster_id, uint8_t* out_valid,
+                           int* resolved_len) {
+    if (max_distance < 0 || max_distance > 1) return -1;
+    int L = umi_len;
+    if (L <= 0) {
+        L = 0;
+        for (int64_t i = 0; i < n; ++i)
+            if (row_valid(validity, validity_offset, i)) {
+                int64_t st, len;
+                row_span(offsets, offset_width, i, &st, &len);
+                L = (int)len;
+                break;
+            }
+    }
+    if (resolved_len) *resolved_len = L;
+    const bool packable = L >= 1 && L <= 32;
+    std::vector<uint64_t> codes((size_t)n, 0);
+    std::vector<uint8_t> cls((size_t)n, 0);  // 0 null, 1 regular, 2 irregular
+    std::vector<uint64_t> distinct;
+    for (int64_t i = 0; i < n; ++i) {
+        if (!row_valid(validity, validity_offset, i)) continue;
+        int64_t st, len;
+        row_span(offsets, offset_width, i, &st, &len);
+        const uint8_t* s = values + st;
+        bool reg = packable && len == L;
+        uint64_t c = 0;
+        for (int64_t j = 0; reg && j < len; ++j) {
+            int b = s[j] == 'A' ? 0 : s[j] == 'C' ? 1 : s[j] == 'G' ? 2 : s[j] == 'T' ? 3 : -1;
+            if (b < 0) reg = false;
+            c = (c << 2) | (uint64_t)(b & 3);
+        }
+        cls[i] = reg ? 1 : 2;
+        if (reg) {
+            codes[i] = c;
+            distinct.push_back(c);
+        }
+    }
+    std::sort(distinct.begin(), distinct.end());
+    distinct.erase(std::unique(distinct.begin(), distinct.end()), distinct.end());
+    const size_t D = distinct.size();
+    std::vector<uint32_t> parent(D);
+    for (size_t i = 0; i < D; ++i) parent[i] = (uint32_t)i;
+    auto find = [&](uint32_t x) {
+        while (parent[x] != x) { parent[x] = parent[parent[x]]; x = parent[x]; }
+        return x;
+    };
+    if (max_distance == 1) {
+        for (size_t i = 0; i < D; ++i) {
+            const uint64_t c = distinct[i];
+            for (int p = 0; p < L; ++p)
+                for (uint64_t d = 1; d <= 3; ++d) {
+                    uint64_t nb = c ^ (d << (2 * p));
+                    if (nb >= c) continue;
+                    auto it = std::lower_bound(distinct.begin(), distinct.end(), nb);
+                    if (it == distinct.end() || *it != nb) continue;
+                    uint32_t a = find((uint32_t)i), b = find((uint32_t)(it - distinct.begin()));
+                    if (a == b) continue;
+                    if (a < b) std::swap(a, b);
+                    parent[a] = b;  // hook larger root under smaller: root = min index
+                }
+        }
+    }
+    std::vector<uint32_t> label(D);
+    uint32_t n_regular = 0;
+    for (size_t i = 0; i < D; ++i) {  // roots in ascending code order
+        uint32_t r = find((uint32_t)i);
+        if (r == i) label[i] = n_regular++;
+        else label[i] = label[r];  // r < i already labelled
+    }
+    std::map<std::string, uint32_t> irregular;
+    for (int64_t i = 0; i < n; ++i)
+        if (cls[i] == 2) {
+            int64_t st, len;
+            row_span(offsets, offset_width, i, &st, &len);
+            irregular.emplace(std::string((const char*)values + st, (size_t)len), 0);
+        }
+    uint32_t next = n_regular;
+    for (auto& kv : irregular) kv.second = next++;
+    for (int64_t i = 0; i < n; ++i) {
+        if (out_valid) out_valid[i] = cls[i] != 0;
+        if (cls[i] == 0) { cluster_id[i] = 0; continue; }
+        if (cls[i] == 1) {
+            size_t idx = (size_t)(std::lower_bound(distinct.begin(), distinct.end(), codes[i]) - distinct.begin());
+            cluster_id[i] = label[idx];
+        } else {
+            int64_t st, len;
+            row_span(offsets, offset_width, i, &st, &len);
+            cluster_id[i] = irregular[std::string((const char*)values + st, (size_t)len)];
+        }
+    }
+    return (int64_t)next;
+}
+
+// Entropy term table entry as the reference computes it: p = c/t; p*log2(p).
+double oracle_plogp(uint32_t c, uint32_t t) {
+    double p = (double)c / (double)t;
+    return p * std::log2(p);
+}
+
+}  // extern "C"

@@ -1,0 +1,37 @@
+"""rogtk_amd — MI355X-native (gfx950) engine for rogtk's UMI score + cluster hot path.
+
+Drop-in surface (mirrors rogtk/__init__.py's `umi` / `hamming` namespaces):
+
+    import rogtk_amd as rg
+    rg.col(umis).umi.complexity_all()            # Struct of 7 (umi_score.rs)
+    rg.col(umis).umi.shannon_entropy()           # ... and the other 6 fields
+    rg.col(umis).hamming.distance("ACGTACGTACGT")
+    rg.col(umis).hamming.within("ACGTACGTACGT", max_distance=1)
+    rg.umi_complexity_scores(umis)
+    rg.umi_cluster(umis, max_distance=1)         # H3 (caller-side group_by('umi'))
+
+Device-resident pipeline (packed SoA in HBM, torch tensors as plumbing):
+    rogtk_amd.device (PackedBatch, score_packed, ClusterEngine, cluster_batch)
+Multi-GPU exchange: rogtk_amd.dist. Synthetic data: rogtk_amd.synth.
+C ABI: include/rogtk_hip.h (librogtk_hip.so, in-tree).
+"""
+from ._lib import RogtkError, device_count, version  # noqa: F401
+from .api import (  # noqa: F401
+    FIELDS,
+    STRUCT_TYPE,
+    Col,
+    HammingExpr,
+    UmiNamespace,
+    col,
+    hamming_distance,
+    hamming_within,
+    umi_cluster,
+    umi_complexity,
+    umi_complexity_scores,
+)
+
+__all__ = [
+    "RogtkError", "device_count", "version", "FIELDS", "STRUCT_TYPE", "Col", "HammingExpr",
+    "UmiNamespace", "col", "hamming_distance", "hamming_within", "umi_cluster", "umi_complexity",
+    "umi_complexity_scores",
+]

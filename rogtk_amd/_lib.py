@@ -1,0 +1,162 @@
+"""ctypes binding of the in-tree C-ABI libraries (include/rogtk_hip.h).
+
+The product path has no fallback: if ``librogtk_hip.so`` is missing the import of
+anything that computes raises ``RogtkError`` with the build instruction. There is
+no CPU implementation of the kernels anywhere in this package.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+HIP_LIB_PATH = os.path.join(_HERE, "librogtk_hip.so")
+SYNTH_LIB_PATH = os.path.join(_HERE, "librogtk_synth.so")
+
+ROGTK_OK = 0
+ROGTK_E_INVALID = 1
+ROGTK_E_HIP = 2
+ROGTK_E_UNSUPPORTED = 3
+ROGTK_E_NODEVICE = 4
+ROGTK_E_OVERFLOW = 5
+
+
+class RogtkError(RuntimeError):
+    """Raised for every non-zero status returned across the C ABI."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(f"[rogtk status {code}] {message}")
+        self.code = code
+
+
+class UmiScores(ctypes.Structure):
+    """rogtk_umi_scores (include/rogtk_hip.h): field order of
+    umi_complexity_struct_output_type (reference src/expressions.rs:1219-1232)."""
+
+    _fields_ = [
+        ("shannon_entropy", ctypes.c_void_p),
+        ("linguistic_complexity", ctypes.c_void_p),
+        ("homopolymer_fraction", ctypes.c_void_p),
+        ("dinucleotide_entropy", ctypes.c_void_p),
+        ("longest_homopolymer_run", ctypes.c_void_p),
+        ("dust_score", ctypes.c_void_p),
+        ("combined_score", ctypes.c_void_p),
+    ]
+
+
+_vp, _i64, _i32, _u32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_uint32
+_P_SCORES = ctypes.POINTER(UmiScores)
+_P_I64 = ctypes.POINTER(ctypes.c_int64)
+_P_I32 = ctypes.POINTER(ctypes.c_int)
+_P_F64 = ctypes.POINTER(ctypes.c_double)
+
+# name -> (argtypes) ; every function returns int status except the two strings
+SIGNATURES = {
+    "rogtk_device_count": [_P_I32],
+    "rogtk_stage_strings": [_vp, _i32, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp],
+    "rogtk_umi_score_packed": [_vp, _vp, _i64, _i32, _P_SCORES, _vp, _i64, _u32, _vp, _vp, _vp,
+                               _i64, _vp],
+    "rogtk_umi_score_rows": [_vp, _i32, _vp, _vp, _vp, _i64, _i64, _P_SCORES, _vp, _i64, _u32, _vp,
+                             _vp, _vp],
+    "rogtk_cluster_workspace_size": [_i32, _i64, _P_I64],
+    "rogtk_cluster_bitmap_words": [_i32, _P_I64],
+    "rogtk_cluster_init": [_vp, _i32, _i64, _vp],
+    "rogtk_cluster_mark": [_vp, _vp, _i64, _i32, _vp, _i64, _vp],
+    "rogtk_cluster_local_bitmap": [_vp, _i32, _i64, _vp, _vp],
+    "rogtk_cluster_resolve": [_vp, _i32, _i64, _vp, _i32, _i32, _vp],
+    "rogtk_cluster_assign": [_vp, _i32, _i64, _vp, _vp, _i64, _vp, _vp],
+    "rogtk_cluster_stats": [_vp, _i32, _i64, _P_I64, _vp],
+    "rogtk_umi_complexity_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _P_SCORES],
+    "rogtk_hamming_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _u32, _vp, _vp],
+    "rogtk_umi_cluster_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _P_I64,
+                               _P_I32],
+    "rogtk_profile_enable": [_i32],
+    "rogtk_profile_reset": [],
+    "rogtk_profile_read": [ctypes.c_char_p, _P_F64, _P_I64],
+}
+
+_lock = threading.Lock()
+_hip = None
+_synth = None
+
+
+def _bind_one_hip_runtime() -> None:
+    """Make the process use ONE HIP runtime.
+
+    The torch wheel ships its own libamdhip64 (SONAME libamdhip64.so.7) that its
+    libc10_hip NEEDs as "libamdhip64.so" through torch/lib's RPATH; librogtk_hip
+    NEEDs "libamdhip64.so.7". Loading torch first makes the dynamic linker satisfy
+    our dependency with torch's already-loaded runtime (SONAME match), so device
+    pointers and streams from torch tensors are valid in our calls. Loading ours
+    first would pull /opt/rocm's runtime AND later torch's second copy.
+    """
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # plain C-ABI use without torch: /opt/rocm's runtime
+        pass
+
+
+def hip() -> ctypes.CDLL:
+    """Load librogtk_hip.so (fails loudly when the extension was not built)."""
+    global _hip
+    with _lock:
+        if _hip is None:
+            _bind_one_hip_runtime()
+            if not os.path.exists(HIP_LIB_PATH):
+                raise RogtkError(ROGTK_E_NODEVICE,
+                                 f"{HIP_LIB_PATH} is missing: build it with "
+                                 "`python -c 'import __graft_entry__ as g; g.build()'` "
+                                 "(make -C rogtk_amd/csrc). There is no CPU fallback.")
+            lib = ctypes.CDLL(HIP_LIB_PATH)
+            for name, argtypes in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.argtypes = argtypes
+                fn.restype = ctypes.c_int
+            lib.rogtk_version.restype = ctypes.c_char_p
+            lib.rogtk_version.argtypes = []
+            lib.rogtk_last_error.restype = ctypes.c_char_p
+            lib.rogtk_last_error.argtypes = []
+            _hip = lib
+    return _hip
+
+
+def synth() -> ctypes.CDLL:
+    global _synth
+    with _lock:
+        if _synth is None:
+            if not os.path.exists(SYNTH_LIB_PATH):
+                raise RogtkError(ROGTK_E_NODEVICE, f"{SYNTH_LIB_PATH} is missing: run make -C rogtk_amd/csrc")
+            lib = ctypes.CDLL(SYNTH_LIB_PATH)
+            u64, f64 = ctypes.c_uint64, ctypes.c_double
+            lib.rogtk_synth_umis_ascii.argtypes = [u64, _i32, u64, f64, f64, f64, u64, u64, _vp]
+            lib.rogtk_synth_umis_ascii.restype = None
+            lib.rogtk_synth_umis_codes.argtypes = [u64, _i32, u64, f64, u64, u64, _vp]
+            lib.rogtk_synth_umis_codes.restype = ctypes.c_int
+            lib.rogtk_synth_reads.argtypes = [u64, _i32, u64, f64, u64, u64, _vp]
+            lib.rogtk_synth_reads.restype = None
+            lib.rogtk_synth_molecules.argtypes = [u64, u64, u64, u64, _vp]
+            lib.rogtk_synth_molecules.restype = None
+            _synth = lib
+    return _synth
+
+
+def check(status: int) -> None:
+    """Raise RogtkError carrying rogtk_last_error() for a non-zero status."""
+    if status != ROGTK_OK:
+        msg = hip().rogtk_last_error()
+        raise RogtkError(status, msg.decode("utf-8", "replace") if msg else "unknown error")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(hip(), name)(*args))
+
+
+def version() -> str:
+    return hip().rogtk_version().decode()
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    check(hip().rogtk_device_count(ctypes.byref(n)))
+    return n.value

@@ -1,0 +1,696 @@
+// capi.hip — extern "C" surface of librogtk_hip.so (declared in include/rogtk_hip.h).
+//
+// Host-side responsibilities: argument validation, thread-local last-error,
+// the glibc-log2 entropy tables (bit-exact with the reference's f64::log2),
+// Hamming target encoding, the per-thread device context of the level-2
+// (host Arrow buffer) entry points, and launch-bracketing profiling events.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "rogtk_internal.h"
+
+namespace rogtk {
+
+// ------------------------------------------------------------------ errors
+static thread_local char t_err[1024] = "";
+
+void set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(t_err, sizeof(t_err), fmt, ap);
+    va_end(ap);
+}
+
+// --------------------------------------------------------------- profiling
+const char* const kKernelNames[K_COUNT_] = {
+    "stage",          "score_packed",   "score_rows",    "cluster_mark",
+    "cluster_bitmap", "cluster_scan",   "cluster_compact", "cluster_union",
+    "cluster_flatten", "cluster_label", "cluster_assign", "cluster_irregular"};
+
+namespace {
+std::atomic<bool> g_prof{false};
+std::mutex g_prof_mu;
+struct ProfRec {
+    KernelId id;
+    hipEvent_t a, b;
+};
+std::vector<ProfRec> g_prof_pending;
+double g_prof_ms[K_COUNT_] = {0};
+int64_t g_prof_n[K_COUNT_] = {0};
+
+void prof_drain_locked() {
+    for (auto& r : g_prof_pending) {
+        float ms = 0.f;
+        if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+            g_prof_ms[r.id] += ms;
+            g_prof_n[r.id] += 1;
+        }
+        hipEventDestroy(r.a);
+        hipEventDestroy(r.b);
+    }
+    g_prof_pending.clear();
+}
+}  // namespace
+
+ProfScope::ProfScope(KernelId id, hipStream_t stream) : id_(id), stream_(stream) {
+    if (!g_prof.load(std::memory_order_relaxed)) return;
+    if (hipEventCreate(&start_) != hipSuccess) {
+        start_ = nullptr;
+        return;
+    }
+    hipEventRecord(start_, stream_);
+}
+
+ProfScope::~ProfScope() {
+    if (!start_) return;
+    hipEvent_t stop = nullptr;
+    if (hipEventCreate(&stop) != hipSuccess) {
+        hipEventDestroy(start_);
+        return;
+    }
+    hipEventRecord(stop, stream_);
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof_pending.push_back({id_, start_, stop});
+}
+
+// ------------------------------------------------------------ entropy LUT
+double plogp_host(uint32_t c, uint32_t t) {
+    // umi_score.rs:67-68 / :140-141: p = count as f64 / total as f64; p * p.log2()
+    const double p = (double)c / (double)t;
+    return p * std::log2(p);
+}
+
+namespace {
+struct DevLut {
+    double* dev = nullptr;
+    int64_t covered = -1;
+};
+std::mutex g_lut_mu;
+std::map<int, DevLut> g_luts;
+}  // namespace
+
+int lut_ensure(int64_t max_total, const double** dev, int64_t* covered) {
+    int device = 0;
+    ROGTK_HIP_CHECK(hipGetDevice(&device));
+    std::lock_guard<std::mutex> lk(g_lut_mu);
+    DevLut& L = g_luts[device];
+    if (L.covered < max_total) {
+        int64_t want = std::max<int64_t>(std::max<int64_t>(max_total, 256), L.covered * 2);
+        // 4096 covers every UMI/read-length string; the table is 8.4M doubles (67 MB).
+        ROGTK_REQUIRE(max_total <= 4096, ROGTK_E_UNSUPPORTED,
+                      "byte path: strings longer than 4096 bytes are not supported");
+        want = std::min<int64_t>(want, 4096);
+        const int64_t entries = lut_index(want + 1, 0);
+        std::vector<double> h((size_t)entries, 0.0);
+        for (int64_t t = 1; t <= want; ++t)
+            for (int64_t c = 1; c <= t; ++c) h[(size_t)lut_index(t, c)] = plogp_host((uint32_t)c, (uint32_t)t);
+        double* d = nullptr;
+        ROGTK_HIP_CHECK(hipMalloc(&d, (size_t)entries * sizeof(double)));
+        ROGTK_HIP_CHECK(hipMemcpy(d, h.data(), (size_t)entries * sizeof(double), hipMemcpyHostToDevice));
+        if (L.dev) {
+            ROGTK_HIP_CHECK(hipDeviceSynchronize());
+            hipFree(L.dev);
+        }
+        L.dev = d;
+        L.covered = want;
+    }
+    *dev = L.dev;
+    *covered = L.covered;
+    return ROGTK_OK;
+}
+
+int build_packed_params(int L, PackedParams* p) {
+    std::memset(p, 0, sizeof(*p));
+    p->L = L;
+    for (int c = 1; c <= L; ++c) p->sh[c] = plogp_host((uint32_t)c, (uint32_t)L);
+    if (L >= 2)
+        for (int c = 1; c <= L - 1; ++c) p->di[c] = plogp_host((uint32_t)c, (uint32_t)(L - 1));
+    if (L >= 3) {
+        const double denom = (double)std::min(L - 2, 64);  // umi_score.rs:90
+        for (int u = 0; u <= kMaxPackedLen; ++u) p->ling[u] = (double)u / denom;
+    }
+    for (int k = 0; k <= L; ++k) p->frac[k] = (double)k / (double)L;  // :120, :31
+    return ROGTK_OK;
+}
+
+static size_t utf8_next_host(const uint8_t* s, size_t n, size_t i, uint32_t* cp) {
+    const uint8_t c = s[i];
+    size_t w = c < 0x80 ? 1 : (c >> 5) == 0x6 ? 2 : (c >> 4) == 0xE ? 3 : 4;
+    if (i + w > n) w = n - i;
+    uint32_t v = w == 1 ? c : w == 2 ? (c & 0x1Fu) : w == 3 ? (c & 0x0Fu) : (c & 0x07u);
+    for (size_t k = 1; k < w; ++k) v = (v << 6) | (s[i + k] & 0x3Fu);
+    *cp = v;
+    return i + w;
+}
+
+void encode_target(const uint8_t* target, int64_t tlen, int L, uint32_t maxd, PackedParams* p) {
+    p->max_distance = maxd;
+    p->tcode = p->cmplo = p->always_mismatch = 0;
+    if (!target) {
+        p->ham_mode = 0;
+        return;
+    }
+    if (tlen != L) {  // expressions.rs:1057: seq.len() != target.len() -> u32::MAX / false
+        p->ham_mode = 2;
+        return;
+    }
+    p->ham_mode = 1;
+    // chars().zip(): a packed row is L ASCII chars; the target may hold fewer chars
+    // (multi-byte UTF-8) — only the first min(k, L) positions are compared.
+    size_t i = 0;
+    int j = 0;
+    while (i < (size_t)tlen && j < L) {
+        uint32_t cp;
+        i = utf8_next_host(target, (size_t)tlen, i, &cp);
+        const int sh = 2 * (L - 1 - j);
+        const int b = cp == 'A' ? 0 : cp == 'C' ? 1 : cp == 'G' ? 2 : cp == 'T' ? 3 : -1;
+        if (b < 0) {
+            p->always_mismatch += 1;  // a non-ACGT target char never equals a packed base
+        } else {
+            p->tcode |= (uint32_t)b << sh;
+            p->cmplo |= 1u << sh;
+        }
+        ++j;
+    }
+}
+
+}  // namespace rogtk
+
+using namespace rogtk;
+
+namespace {
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+int check_offset_width(int ow) {
+    ROGTK_REQUIRE(ow == 4 || ow == 8, ROGTK_E_INVALID, "offset_width must be 4 or 8, got %d", ow);
+    return ROGTK_OK;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+int check_packed_alignment(const uint32_t* codes, const ScoreOut& o, const uint32_t* hd) {
+    const void* ps[] = {codes, o.sh, o.ling, o.homo, o.di, o.dust, o.comb, o.longest, hd};
+    for (const void* p : ps)
+        ROGTK_REQUIRE(!p || aligned16(p), ROGTK_E_INVALID,
+                      "packed SoA buffers must be 16-byte aligned (device allocations are)");
+    return ROGTK_OK;
+}
+
+// --------------------------------------------- per-thread level-2 context
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    ~DevBuf() {
+        if (p) hipFree(p);
+    }
+    int ensure(size_t bytes) {
+        if (bytes <= cap && p) return ROGTK_OK;
+        if (p) {
+            hipFree(p);
+            p = nullptr;
+            cap = 0;
+        }
+        size_t want = std::max<size_t>(bytes, 256);
+        want = (want + 255) / 256 * 256;
+        ROGTK_HIP_CHECK(hipMalloc(&p, want));
+        cap = want;
+        return ROGTK_OK;
+    }
+    template <class T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct HostCtx {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    DevBuf offsets, values, validity, codes, regbits, irr, nirr, target, out[8], ws, bitmap;
+    int64_t ws_L = -1, ws_maxd = -1;
+    ~HostCtx() {
+        if (stream) hipStreamDestroy(stream);
+    }
+};
+
+thread_local std::unique_ptr<HostCtx> t_ctx;
+
+int host_ctx(HostCtx** out) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        set_error("no HIP device available (librogtk_hip needs an MI355X / gfx950 GPU)");
+        return ROGTK_E_NODEVICE;
+    }
+    int dev = 0;
+    ROGTK_HIP_CHECK(hipGetDevice(&dev));
+    if (!t_ctx || t_ctx->device != dev) {
+        t_ctx.reset(new HostCtx());
+        t_ctx->device = dev;
+        ROGTK_HIP_CHECK(hipStreamCreateWithFlags(&t_ctx->stream, hipStreamNonBlocking));
+    }
+    *out = t_ctx.get();
+    return ROGTK_OK;
+}
+
+struct HostCol {
+    const void* offsets;
+    int ow;
+    const uint8_t* values;
+    int64_t values_len;
+    const uint8_t* validity;
+    int64_t voff;
+    int64_t n;
+    int64_t off0() const { return ow == 4 ? ((const int32_t*)offsets)[0] : ((const int64_t*)offsets)[0]; }
+    int64_t off(int64_t i) const {
+        return ow == 4 ? ((const int32_t*)offsets)[i] : ((const int64_t*)offsets)[i];
+    }
+    bool valid(int64_t i) const {
+        if (!validity) return true;
+        const int64_t b = voff + i;
+        return (validity[b >> 3] >> (b & 7)) & 1;
+    }
+    int first_len() const {
+        for (int64_t i = 0; i < n; ++i)
+            if (valid(i)) return (int)std::min<int64_t>(off(i + 1) - off(i), 1 << 30);
+        return 0;
+    }
+    int64_t max_len() const {
+        int64_t m = 0;
+        for (int64_t i = 0; i < n; ++i) m = std::max<int64_t>(m, off(i + 1) - off(i));
+        return m;
+    }
+};
+
+// Upload a host column and stage it; returns the resolved packed length in *L.
+int upload_and_stage(HostCtx* c, const HostCol& h, int L_req, int* L_out, int64_t* n_irr_host) {
+    const int64_t n = h.n;
+    const int ow = h.ow;
+    ROGTK_REQUIRE(c->offsets.ensure((size_t)(n + 1) * ow) == ROGTK_OK, ROGTK_E_HIP, "%s", rogtk_last_error());
+    ROGTK_HIP_CHECK(hipMemcpyAsync(c->offsets.p, h.offsets, (size_t)(n + 1) * ow, hipMemcpyHostToDevice, c->stream));
+    // values: upload [0, off(n)) so the device offsets stay valid as given
+    const int64_t vbytes = std::max<int64_t>(h.off(n), 1);
+    ROGTK_REQUIRE(h.off(n) <= h.values_len || h.values_len < 0, ROGTK_E_INVALID,
+                  "offsets reference %lld bytes but values_len is %lld", (long long)h.off(n),
+                  (long long)h.values_len);
+    if (c->values.ensure((size_t)vbytes) != ROGTK_OK) return ROGTK_E_HIP;
+    if (h.off(n) > 0)
+        ROGTK_HIP_CHECK(hipMemcpyAsync(c->values.p, h.values, (size_t)h.off(n), hipMemcpyHostToDevice, c->stream));
+    const uint8_t* dvalid = nullptr;
+    if (h.validity) {
+        const size_t vb = (size_t)((h.voff + n + 7) / 8);
+        if (c->validity.ensure(vb) != ROGTK_OK) return ROGTK_E_HIP;
+        ROGTK_HIP_CHECK(hipMemcpyAsync(c->validity.p, h.validity, vb, hipMemcpyHostToDevice, c->stream));
+        dvalid = c->validity.as<uint8_t>();
+    }
+    int L = L_req > 0 ? L_req : h.first_len();
+    *L_out = L;
+    const int64_t words = (n + 63) / 64;
+    if (c->codes.ensure((size_t)std::max<int64_t>(n, 4) * 4) != ROGTK_OK ||
+        c->regbits.ensure((size_t)std::max<int64_t>(words, 1) * 8) != ROGTK_OK ||
+        c->irr.ensure((size_t)std::max<int64_t>(n, 1) * 8) != ROGTK_OK ||
+        c->nirr.ensure(8) != ROGTK_OK)
+        return ROGTK_E_HIP;
+    ROGTK_HIP_CHECK(hipMemsetAsync(c->nirr.p, 0, 8, c->stream));
+    int rc = launch_stage(c->offsets.p, ow, c->values.as<uint8_t>(), dvalid, h.voff, n, L,
+                          c->codes.as<uint32_t>(), c->regbits.as<uint64_t>(), c->irr.as<int64_t>(),
+                          c->nirr.as<unsigned long long>(), c->stream);
+    if (rc) return rc;
+    if (n_irr_host) {
+        ROGTK_HIP_CHECK(hipMemcpyAsync(n_irr_host, c->nirr.p, 8, hipMemcpyDeviceToHost, c->stream));
+        ROGTK_HIP_CHECK(hipStreamSynchronize(c->stream));
+    }
+    return ROGTK_OK;
+}
+
+int check_host_col(const HostCol& h) {
+    if (int rc = check_offset_width(h.ow)) return rc;
+    ROGTK_REQUIRE(h.n >= 0, ROGTK_E_INVALID, "n must be >= 0");
+    ROGTK_REQUIRE(h.offsets != nullptr, ROGTK_E_INVALID, "offsets must not be NULL");
+    ROGTK_REQUIRE(h.values != nullptr || h.off(h.n) == h.off0(), ROGTK_E_INVALID, "values must not be NULL");
+    ROGTK_REQUIRE(h.off0() == 0, ROGTK_E_INVALID,
+                  "offsets[0] must be 0 (slice the values buffer instead of the offsets)");
+    return ROGTK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rogtk_version(void) { return "rogtk-amd 0.1.0 (gfx950)"; }
+
+const char* rogtk_last_error(void) { return t_err; }
+
+int rogtk_device_count(int* out) {
+    ROGTK_REQUIRE(out, ROGTK_E_INVALID, "out_count is NULL");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *out = n;
+    return ROGTK_OK;
+}
+
+int rogtk_stage_strings(const void* offsets, int offset_width, const uint8_t* values,
+                        const uint8_t* validity, int64_t validity_offset, int64_t n, int umi_len,
+                        uint32_t* codes, uint64_t* regular_bits, int64_t* irregular_rows,
+                        int64_t* n_irregular, void* stream) {
+    if (int rc = check_offset_width(offset_width)) return rc;
+    ROGTK_REQUIRE(n >= 0, ROGTK_E_INVALID, "n must be >= 0");
+    ROGTK_REQUIRE(n == 0 || (offsets && codes && regular_bits && irregular_rows && n_irregular),
+                  ROGTK_E_INVALID, "stage: NULL buffer");
+    hipStream_t s = as_stream(stream);
+    if (n_irregular) ROGTK_HIP_CHECK(hipMemsetAsync(n_irregular, 0, 8, s));
+    return launch_stage(offsets, offset_width, values, validity, validity_offset, n, umi_len, codes,
+                        regular_bits, irregular_rows, (unsigned long long*)n_irregular, s);
+}
+
+int rogtk_umi_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
+                           int umi_len, const rogtk_umi_scores* scores, const uint8_t* target,
+                           int64_t target_len, uint32_t max_distance, uint32_t* hamming_distance,
+                           uint64_t* hamming_within_bits, void* cluster_ws,
+                           int64_t cluster_max_distinct, void* stream) {
+    ROGTK_REQUIRE(umi_len >= 1 && umi_len <= kMaxPackedLen, ROGTK_E_UNSUPPORTED,
+                  "packed path: umi_len %d outside 1..%d", umi_len, kMaxPackedLen);
+    ROGTK_REQUIRE(n >= 0, ROGTK_E_INVALID, "n must be >= 0");
+    ROGTK_REQUIRE(n == 0 || codes, ROGTK_E_INVALID, "codes is NULL");
+    ROGTK_REQUIRE(target_len >= 0, ROGTK_E_INVALID, "target_len must be >= 0");
+    const ScoreOut o = to_score_out(scores);
+    if (int rc = check_packed_alignment(codes, o, hamming_distance)) return rc;
+    PackedParams p;
+    build_packed_params(umi_len, &p);
+    encode_target(target, target_len, umi_len, max_distance, &p);
+    uint8_t* presence = nullptr;
+    if (cluster_ws) {
+        ClusterLayout cl;
+        if (int rc = cluster_layout(umi_len, cluster_max_distinct, &cl)) return rc;
+        presence = (uint8_t*)cluster_ws + cl.off_presence;
+    }
+    return launch_score_packed(codes, regular_bits, n, p, o, hamming_distance, hamming_within_bits,
+                               presence, as_stream(stream));
+}
+
+int rogtk_umi_score_rows(const void* offsets, int offset_width, const uint8_t* values,
+                         const int64_t* rows, const int64_t* n_rows_dev, int64_t max_rows,
+                         int64_t max_len, const rogtk_umi_scores* scores, const uint8_t* target,
+                         int64_t target_len, uint32_t max_distance, uint32_t* hamming_distance,
+                         uint64_t* hamming_within_bits, void* stream) {
+    if (int rc = check_offset_width(offset_width)) return rc;
+    ROGTK_REQUIRE(max_rows >= 0 && max_len >= 0 && target_len >= 0, ROGTK_E_INVALID,
+                  "score_rows: negative size");
+    if (max_rows == 0) return ROGTK_OK;
+    ROGTK_REQUIRE(offsets && rows, ROGTK_E_INVALID, "score_rows: NULL offsets/rows");
+    const double* lut = nullptr;
+    int64_t covered = 0;
+    if (int rc = lut_ensure(std::max<int64_t>(max_len, 1), &lut, &covered)) return rc;
+    hipStream_t s = as_stream(stream);
+    const uint8_t* tdev = nullptr;
+    thread_local DevBuf t_target;
+    if (target) {
+        if (int rc = t_target.ensure((size_t)std::max<int64_t>(target_len, 1))) return rc;
+        if (target_len)
+            ROGTK_HIP_CHECK(hipMemcpyAsync(t_target.p, target, (size_t)target_len, hipMemcpyHostToDevice, s));
+        tdev = t_target.as<uint8_t>();
+    }
+    return launch_score_rows(offsets, offset_width, values, rows, n_rows_dev, max_rows, lut, covered,
+                             to_score_out(scores), tdev, target_len, target ? 1 : 0, max_distance,
+                             hamming_distance, hamming_within_bits, s);
+}
+
+int rogtk_cluster_workspace_size(int umi_len, int64_t max_distinct, int64_t* bytes) {
+    ROGTK_REQUIRE(bytes, ROGTK_E_INVALID, "bytes is NULL");
+    ClusterLayout cl;
+    if (int rc = cluster_layout(umi_len, max_distinct, &cl)) return rc;
+    *bytes = cl.total;
+    return ROGTK_OK;
+}
+
+int rogtk_cluster_bitmap_words(int umi_len, int64_t* words) {
+    ROGTK_REQUIRE(words, ROGTK_E_INVALID, "words is NULL");
+    ClusterLayout cl;
+    if (int rc = cluster_layout(umi_len, 1, &cl)) return rc;
+    *words = cl.words;
+    return ROGTK_OK;
+}
+
+int rogtk_cluster_init(void* ws, int umi_len, int64_t max_distinct, void* stream) {
+    ClusterLayout cl;
+    if (int rc = cluster_layout(umi_len, max_distinct, &cl)) return rc;
+    ROGTK_REQUIRE(ws, ROGTK_E_INVALID, "ws is NULL");
+    ROGTK_HIP_CHECK(hipMemsetAsync(ws, 0, (size_t)cl.total, as_stream(stream)));
+    return ROGTK_OK;
+}
+
+int rogtk_cluster_mark(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
+                       void* ws, int64_t max_distinct, void* stream) {
+    ROGTK_REQUIRE(ws, ROGTK_E_INVALID, "ws is NULL");
+    return rogtk_umi_score_packed(codes, regular_bits, n, umi_len, nullptr, nullptr, 0, 0, nullptr,
+                                  nullptr, ws, max_distinct, stream);
+}
+
+int rogtk_cluster_local_bitmap(void* ws, int umi_len, int64_t max_distinct, uint64_t* bitmap_out,
+                               void* stream) {
+    ClusterLayout cl;
+    if (int rc = cluster_layout(umi_len, max_distinct, &cl)) return rc;
+    ROGTK_REQUIRE(ws && bitmap_out, ROGTK_E_INVALID, "ws/bitmap_out is NULL");
+    return launch_cluster_local_bitmap(cl, (uint8_t*)ws, bitmap_out, as_stream(stream));
+}
+
+int rogtk_cluster_resolve(void* ws, int umi_len, int64_t max_distinct, const uint64_t* bitmaps,
+                          int n_bitmaps, int max_distance, void* stream) {
+    ClusterLayout cl;
+    if (int rc = cluster_layout(umi_len, max_distinct, &cl)) return rc;
+    ROGTK_REQUIRE(ws && bitmaps, ROGTK_E_INVALID, "ws/bitmaps is NULL");
+    ROGTK_REQUIRE(n_bitmaps >= 1, ROGTK_E_INVALID, "n_bitmaps must be >= 1");
+    ROGTK_REQUIRE(max_distance == 0 || max_distance == 1, ROGTK_E_UNSUPPORTED,
+                  "max_distance %d: only 0 (exact) and 1 (Hamming<=1 components) are supported",
+                  max_distance);
+    return launch_cluster_resolve(cl, (uint8_t*)ws, bitmaps, n_bitmaps, max_distance, as_stream(stream));
+}
+
+int rogtk_cluster_assign(const void* ws, int umi_len, int64_t max_distinct, const uint32_t* codes,
+                         const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id,
+                         void* stream) {
+    ClusterLayout cl;
+    if (int rc = cluster_layout(umi_len, max_distinct, &cl)) return rc;
+    ROGTK_REQUIRE(ws && (n == 0 || (codes && cluster_id)), ROGTK_E_INVALID, "assign: NULL buffer");
+    ROGTK_REQUIRE(aligned16(codes) && aligned16(cluster_id), ROGTK_E_INVALID,
+                  "assign: codes/cluster_id must be 16-byte aligned");
+    return launch_cluster_assign(cl, (const uint8_t*)ws, codes, regular_bits, n, cluster_id,
+                                 as_stream(stream));
+}
+
+int rogtk_cluster_stats(const void* ws, int umi_len, int64_t max_distinct, int64_t* out4,
+                        void* stream) {
+    ClusterLayout cl;
+    if (int rc = cluster_layout(umi_len, max_distinct, &cl)) return rc;
+    ROGTK_REQUIRE(ws && out4, ROGTK_E_INVALID, "stats: NULL buffer");
+    hipStream_t s = as_stream(stream);
+    ROGTK_HIP_CHECK(hipMemcpyAsync(out4, (const uint8_t*)ws + cl.off_stats, 32, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    return ROGTK_OK;
+}
+
+// ----------------------------------------------------------------- level 2
+int rogtk_umi_complexity_host(const void* offsets, int offset_width, const uint8_t* values,
+                              int64_t values_len, const uint8_t* validity, int64_t validity_offset,
+                              int64_t n, const rogtk_umi_scores* out) {
+    HostCol h{offsets, offset_width, values, values_len, validity, validity_offset, n};
+    if (int rc = check_host_col(h)) return rc;
+    ROGTK_REQUIRE(out, ROGTK_E_INVALID, "out is NULL");
+    if (n == 0) return ROGTK_OK;
+    HostCtx* c;
+    if (int rc = host_ctx(&c)) return rc;
+    int L = 0;
+    int64_t n_irr = 0;
+    const int64_t max_len = h.max_len();
+    if (int rc = upload_and_stage(c, h, 0, &L, &n_irr)) return rc;
+    const ScoreOut ho = to_score_out(out);
+    // device outputs
+    double* dptr[6] = {nullptr};
+    const double* hptr[6] = {ho.sh, ho.ling, ho.homo, ho.di, ho.dust, ho.comb};
+    for (int k = 0; k < 6; ++k)
+        if (hptr[k]) {
+            if (int rc = c->out[k].ensure((size_t)n * 8)) return rc;
+            dptr[k] = c->out[k].as<double>();
+        }
+    uint32_t* dlong = nullptr;
+    if (ho.longest) {
+        if (int rc = c->out[6].ensure((size_t)n * 4)) return rc;
+        dlong = c->out[6].as<uint32_t>();
+    }
+    rogtk_umi_scores ds{dptr[0], dptr[1], dptr[2], dptr[3], dlong, dptr[4], dptr[5]};
+    const bool packable = L >= 1 && L <= kMaxPackedLen;
+    if (packable) {
+        int rc = rogtk_umi_score_packed(c->codes.as<uint32_t>(), c->regbits.as<uint64_t>(), n, L, &ds,
+                                        nullptr, 0, 0, nullptr, nullptr, nullptr, 0, c->stream);
+        if (rc) return rc;
+    }
+    if (n_irr > 0) {
+        int rc = rogtk_umi_score_rows(c->offsets.p, offset_width, c->values.as<uint8_t>(),
+                                      c->irr.as<int64_t>(), nullptr, n_irr, max_len, &ds, nullptr, 0,
+                                      0, nullptr, nullptr, c->stream);
+        if (rc) return rc;
+    }
+    for (int k = 0; k < 6; ++k)
+        if (hptr[k])
+            ROGTK_HIP_CHECK(hipMemcpyAsync((void*)hptr[k], dptr[k], (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+    if (ho.longest)
+        ROGTK_HIP_CHECK(hipMemcpyAsync(ho.longest, dlong, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return ROGTK_OK;
+}
+
+int rogtk_hamming_host(const void* offsets, int offset_width, const uint8_t* values,
+                       int64_t values_len, const uint8_t* validity, int64_t validity_offset,
+                       int64_t n, const uint8_t* target, int64_t target_len, uint32_t max_distance,
+                       uint32_t* distance, uint8_t* within_bits) {
+    HostCol h{offsets, offset_width, values, values_len, validity, validity_offset, n};
+    if (int rc = check_host_col(h)) return rc;
+    ROGTK_REQUIRE(target || target_len == 0, ROGTK_E_INVALID, "target is NULL");
+    ROGTK_REQUIRE(target_len >= 0, ROGTK_E_INVALID, "target_len must be >= 0");
+    if (n == 0) return ROGTK_OK;
+    static const uint8_t kEmpty = 0;
+    const uint8_t* tg = target ? target : &kEmpty;
+    HostCtx* c;
+    if (int rc = host_ctx(&c)) return rc;
+    int L = 0;
+    int64_t n_irr = 0;
+    const int64_t max_len = h.max_len();
+    if (int rc = upload_and_stage(c, h, 0, &L, &n_irr)) return rc;
+    uint32_t* dd = nullptr;
+    uint64_t* dw = nullptr;
+    if (distance) {
+        if (int rc = c->out[0].ensure((size_t)n * 4)) return rc;
+        dd = c->out[0].as<uint32_t>();
+    }
+    const int64_t words = (n + 63) / 64;
+    if (within_bits) {
+        if (int rc = c->out[1].ensure((size_t)words * 8)) return rc;
+        dw = c->out[1].as<uint64_t>();
+    }
+    if (L >= 1 && L <= kMaxPackedLen) {
+        int rc = rogtk_umi_score_packed(c->codes.as<uint32_t>(), c->regbits.as<uint64_t>(), n, L,
+                                        nullptr, tg, target_len, max_distance, dd, dw, nullptr, 0,
+                                        c->stream);
+        if (rc) return rc;
+    } else if (dw) {
+        ROGTK_HIP_CHECK(hipMemsetAsync(dw, 0, (size_t)words * 8, c->stream));
+    }
+    if (n_irr > 0) {
+        int rc = rogtk_umi_score_rows(c->offsets.p, offset_width, c->values.as<uint8_t>(),
+                                      c->irr.as<int64_t>(), nullptr, n_irr, max_len, nullptr, tg,
+                                      target_len, max_distance, dd, dw, c->stream);
+        if (rc) return rc;
+    }
+    if (distance)
+        ROGTK_HIP_CHECK(hipMemcpyAsync(distance, dd, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    if (within_bits)
+        ROGTK_HIP_CHECK(hipMemcpyAsync(within_bits, dw, (size_t)(n + 7) / 8, hipMemcpyDeviceToHost, c->stream));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return ROGTK_OK;
+}
+
+int rogtk_umi_cluster_host(const void* offsets, int offset_width, const uint8_t* values,
+                           int64_t values_len, const uint8_t* validity, int64_t validity_offset,
+                           int64_t n, int umi_len, int max_distance, uint32_t* cluster_id,
+                           int64_t* n_clusters, int* resolved_umi_len) {
+    HostCol h{offsets, offset_width, values, values_len, validity, validity_offset, n};
+    if (int rc = check_host_col(h)) return rc;
+    ROGTK_REQUIRE(cluster_id || n == 0, ROGTK_E_INVALID, "cluster_id is NULL");
+    ROGTK_REQUIRE(max_distance == 0 || max_distance == 1, ROGTK_E_UNSUPPORTED,
+                  "max_distance %d: only 0 and 1 are supported", max_distance);
+    int L = umi_len > 0 ? umi_len : h.first_len();
+    if (resolved_umi_len) *resolved_umi_len = L;
+    if (n_clusters) *n_clusters = 0;
+    if (n == 0) return ROGTK_OK;
+    HostCtx* c;
+    if (int rc = host_ctx(&c)) return rc;
+    int64_t n_irr = 0;
+    if (int rc = upload_and_stage(c, h, L, &L, &n_irr)) return rc;
+    if (int rc = c->out[0].ensure((size_t)std::max<int64_t>(n, 4) * 4)) return rc;
+    uint32_t* did = c->out[0].as<uint32_t>();
+    int64_t n_reg_clusters = 0;
+    const int64_t* stats_dev = nullptr;
+    if (L >= 1 && L <= kMaxPackedLen) {
+        const int64_t space = (int64_t)1 << std::min(2 * L, 40);
+        const int64_t maxd = std::max<int64_t>(1, std::min<int64_t>(space, n));
+        ClusterLayout cl;
+        if (int rc = cluster_layout(L, maxd, &cl)) return rc;
+        if (c->ws_L != L || c->ws_maxd < cl.max_distinct) {
+            if (int rc = c->ws.ensure((size_t)cl.total)) return rc;
+            if (int rc = rogtk_cluster_init(c->ws.p, L, cl.max_distinct, c->stream)) return rc;
+            c->ws_L = L;
+            c->ws_maxd = cl.max_distinct;
+        }
+        ClusterLayout use;
+        cluster_layout(L, c->ws_maxd, &use);
+        if (int rc = c->bitmap.ensure((size_t)use.words * 8)) return rc;
+        int rc = rogtk_cluster_mark(c->codes.as<uint32_t>(), c->regbits.as<uint64_t>(), n, L, c->ws.p,
+                                    use.max_distinct, c->stream);
+        if (!rc) rc = rogtk_cluster_local_bitmap(c->ws.p, L, use.max_distinct, c->bitmap.as<uint64_t>(), c->stream);
+        if (!rc) rc = rogtk_cluster_resolve(c->ws.p, L, use.max_distinct, c->bitmap.as<uint64_t>(), 1,
+                                            max_distance, c->stream);
+        if (!rc) rc = rogtk_cluster_assign(c->ws.p, L, use.max_distinct, c->codes.as<uint32_t>(),
+                                           c->regbits.as<uint64_t>(), n, did, c->stream);
+        if (rc) {
+            c->ws_L = -1;  // presence may be dirty: re-initialise on the next call
+            return rc;
+        }
+        int64_t st[4];
+        if (int rc2 = rogtk_cluster_stats(c->ws.p, L, use.max_distinct, st, c->stream)) return rc2;
+        ROGTK_REQUIRE(st[2] == 0, ROGTK_E_OVERFLOW, "cluster: distinct UMIs exceeded max_distinct");
+        n_reg_clusters = st[1];
+        stats_dev = (const int64_t*)((uint8_t*)c->ws.p + use.off_stats);
+    } else {
+        ROGTK_HIP_CHECK(hipMemsetAsync(did, 0xFF, (size_t)n * 4, c->stream));
+    }
+    int64_t n_irr_clusters = 0;
+    if (n_irr > 0) {
+        int rc = irregular_cluster(c->offsets.p, offset_width, c->values.as<uint8_t>(),
+                                   c->irr.as<int64_t>(), n_irr, h.max_len(), stats_dev, did,
+                                   &n_irr_clusters, c->stream);
+        if (rc) return rc;
+    }
+    ROGTK_HIP_CHECK(hipMemcpyAsync(cluster_id, did, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(c->stream));
+    if (n_clusters) *n_clusters = n_reg_clusters + n_irr_clusters;
+    return ROGTK_OK;
+}
+
+// --------------------------------------------------------------- profiling
+int rogtk_profile_enable(int on) {
+    g_prof.store(on != 0);
+    return ROGTK_OK;
+}
+
+int rogtk_profile_reset(void) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    prof_drain_locked();
+    for (int k = 0; k < K_COUNT_; ++k) {
+        g_prof_ms[k] = 0;
+        g_prof_n[k] = 0;
+    }
+    return ROGTK_OK;
+}
+
+int rogtk_profile_read(const char* kernel, double* total_ms, int64_t* launches) {
+    ROGTK_REQUIRE(kernel && total_ms && launches, ROGTK_E_INVALID, "profile_read: NULL argument");
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    prof_drain_locked();
+    for (int k = 0; k < K_COUNT_; ++k)
+        if (std::strcmp(kernel, kKernelNames[k]) == 0) {
+            *total_ms = g_prof_ms[k];
+            *launches = g_prof_n[k];
+            return ROGTK_OK;
+        }
+    set_error("profile_read: unknown kernel '%s'", kernel);
+    return ROGTK_E_INVALID;
+}
+
+}  // extern "C"

@@ -1,0 +1,156 @@
+// rogtk_internal.h — shared declarations of librogtk_hip.so (not installed).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/rogtk_hip.h"
+
+namespace rogtk {
+
+// ---------------------------------------------------------------- errors
+void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+
+#define ROGTK_HIP_CHECK(expr)                                                                    \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess) {                                                                  \
+            ::rogtk::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                               __LINE__);                                                        \
+            return ROGTK_E_HIP;                                                                  \
+        }                                                                                        \
+    } while (0)
+
+#define ROGTK_REQUIRE(cond, code, ...)        \
+    do {                                      \
+        if (!(cond)) {                        \
+            ::rogtk::set_error(__VA_ARGS__);  \
+            return (code);                    \
+        }                                     \
+    } while (0)
+
+// ------------------------------------------------------------- profiling
+enum KernelId {
+    K_STAGE = 0,
+    K_SCORE_PACKED,
+    K_SCORE_ROWS,
+    K_MARK,
+    K_BITMAP,
+    K_SCAN,
+    K_COMPACT,
+    K_UNION,
+    K_FLATTEN,
+    K_LABEL,
+    K_ASSIGN,
+    K_IRREGULAR,
+    K_COUNT_
+};
+extern const char* const kKernelNames[K_COUNT_];
+
+// Brackets one launch with HIP events on `stream` when profiling is enabled.
+class ProfScope {
+   public:
+    ProfScope(KernelId id, hipStream_t stream);
+    ~ProfScope();
+
+   private:
+    KernelId id_;
+    hipStream_t stream_;
+    hipEvent_t start_ = nullptr;
+};
+
+// ------------------------------------------------- entropy / ratio tables
+// Triangular table T[t][c] = fl(fl(c/t) * log2(fl(c/t))) computed on the host
+// with glibc log2 (the function Rust's f64::log2 resolves to), T[t][0] = 0.
+__host__ __device__ inline int64_t lut_index(int64_t t, int64_t c) { return t * (t + 1) / 2 + c; }
+double plogp_host(uint32_t c, uint32_t t);
+// Device copy covering totals 0..max_total on the current device.
+int lut_ensure(int64_t max_total, const double** dev, int64_t* covered);
+
+constexpr int kMaxPackedLen = 16;
+
+// Per-call constants of the packed kernel (passed by value as a kernel argument).
+struct PackedParams {
+    double sh[kMaxPackedLen + 1];    // plogp(c, L)
+    double di[kMaxPackedLen + 1];    // plogp(c, L-1)
+    double ling[kMaxPackedLen + 1];  // u / min(L-2, 64)
+    double frac[kMaxPackedLen + 1];  // k / L
+    int L;
+    int ham_mode;  // 0 none, 1 compare, 2 byte-length mismatch (u32::MAX / false)
+    uint32_t tcode, cmplo, always_mismatch, max_distance;
+};
+
+struct ScoreOut {
+    double* sh;
+    double* ling;
+    double* homo;
+    double* di;
+    uint32_t* longest;
+    double* dust;
+    double* comb;
+};
+
+inline ScoreOut to_score_out(const rogtk_umi_scores* s) {
+    if (!s) return ScoreOut{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    return ScoreOut{s->shannon_entropy,      s->linguistic_complexity, s->homopolymer_fraction,
+                    s->dinucleotide_entropy, s->longest_homopolymer_run, s->dust_score,
+                    s->combined_score};
+}
+inline bool any_score(const ScoreOut& o) {
+    return o.sh || o.ling || o.homo || o.di || o.longest || o.dust || o.comb;
+}
+
+// Host-side encoding of a Hamming target against packed UMIs of length L
+// (expressions.rs:1057-1063 byte-length check + chars().zip()).
+void encode_target(const uint8_t* target, int64_t target_len, int L, uint32_t max_distance,
+                   PackedParams* p);
+int build_packed_params(int L, PackedParams* p);
+
+// ------------------------------------------------------ kernel launchers
+int launch_stage(const void* offsets, int offset_width, const uint8_t* values,
+                 const uint8_t* validity, int64_t validity_offset, int64_t n, int L,
+                 uint32_t* codes, uint64_t* regular_bits, int64_t* irregular_rows,
+                 unsigned long long* n_irregular, hipStream_t s);
+int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
+                        const PackedParams& p, const ScoreOut& o, uint32_t* hd, uint64_t* hw,
+                        uint8_t* presence, hipStream_t s);
+int launch_score_rows(const void* offsets, int offset_width, const uint8_t* values,
+                      const int64_t* rows, const int64_t* n_rows_dev, int64_t max_rows,
+                      const double* lut, int64_t lut_max, const ScoreOut& o,
+                      const uint8_t* target_dev, int64_t target_len, int ham, uint32_t max_distance,
+                      uint32_t* hd, uint64_t* hw, hipStream_t s);
+
+// Cluster workspace layout: a pure function of (L, max_distinct).
+struct ClusterLayout {
+    int L;
+    int64_t max_distinct;
+    uint64_t nbits;      // 4^L codes
+    int64_t words;       // bitmap words over code space
+    int64_t blocks;      // scan blocks over code-space words (1024 words each)
+    int64_t rwords;      // root-bitmap words over index space
+    int64_t rblocks;     // scan blocks over index-space words
+    bool label_by_code;  // dense label table indexed by code (L <= 13)
+    // byte offsets into the workspace
+    int64_t off_stats, off_presence, off_bitmap, off_wpref, off_blksum, off_blkoff, off_D,
+        off_parent, off_rbits, off_rpref, off_rblksum, off_rblkoff, off_labelcode, total;
+};
+int cluster_layout(int L, int64_t max_distinct, ClusterLayout* out);
+
+int launch_cluster_mark(const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
+                        uint8_t* presence, hipStream_t s);
+int launch_cluster_local_bitmap(const ClusterLayout& cl, uint8_t* ws, uint64_t* bitmap_out,
+                                hipStream_t s);
+int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t* bitmaps,
+                           int n_bitmaps, int max_distance, hipStream_t s);
+int launch_cluster_assign(const ClusterLayout& cl, const uint8_t* ws, const uint32_t* codes,
+                          const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id,
+                          hipStream_t s);
+
+// Irregular rows grouped by exact bytes (any length <= max_len); ids continue after
+// stats_dev[1] (the regular cluster count) or from 0 when stats_dev is NULL.
+int irregular_cluster(const void* offsets, int offset_width, const uint8_t* values,
+                      const int64_t* rows, int64_t n_rows, int64_t max_len, const int64_t* stats_dev,
+                      uint32_t* cluster_id, int64_t* n_irregular_clusters, hipStream_t s);
+
+}  // namespace rogtk

@@ -1,0 +1,512 @@
+// umi_kernels.hip — H1 (UMI complexity) + H2 (Hamming vs target) on gfx950.
+//
+// Kernels
+//   k_stage         Arrow strings -> packed 2-bit SoA + regular bitmap + irregular list
+//   k_score_packed  THE hot kernel: one pass over the packed SoA computing all seven
+//                   complexity fields (umi_score.rs:17-43), Hamming distance/within
+//                   (expressions.rs:1048-1101) and the H3 presence mark. 4 rows per
+//                   lane: 16-B code loads, 2x16-B stores per f64 field, ballot-free
+//                   16-lane OR-reduction for the bit-packed Boolean output.
+//   k_score_rows    byte path for irregular rows (N, lowercase, other lengths, empty),
+//                   the reference's byte semantics restated per lane.
+//
+// Bit-exactness: entropy terms come from a host table of fl(p*log2(p)) built with
+// glibc log2 (what Rust f64::log2 calls); sums run in the reference order (A,C,G,T
+// for Shannon; ascending byte pair for dinucleotides = the oracle's canonical
+// order); the file is compiled with -ffp-contract=off so `e -= t` and the combined
+// score are never fused into FMAs; f64 division is IEEE (correctly rounded).
+#include "rogtk_internal.h"
+
+namespace rogtk {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kRowsPerLane = 4;
+
+__device__ __forceinline__ double x86_default_nan() {
+    // 0.0/0.0 on x86-64 SSE2 yields the "real indefinite" QNaN 0xFFF8000000000000;
+    // the reference computes combined = ... longest/len with len == 0 (umi_score.rs:31).
+    return __longlong_as_double((long long)0xFFF8000000000000ull);
+}
+
+// --------------------------------------------------------------- staging
+template <int OW>
+__device__ __forceinline__ void span(const void* offs, int64_t i, int64_t& st, int64_t& len) {
+    if (OW == 4) {
+        const int32_t* o = (const int32_t*)offs;
+        st = o[i];
+        len = (int64_t)o[i + 1] - o[i];
+    } else {
+        const int64_t* o = (const int64_t*)offs;
+        st = o[i];
+        len = o[i + 1] - o[i];
+    }
+}
+
+__device__ __forceinline__ int base_code(uint8_t ch) {
+    return ch == 'A' ? 0 : ch == 'C' ? 1 : ch == 'G' ? 2 : ch == 'T' ? 3 : -1;
+}
+
+template <int OW>
+__global__ __launch_bounds__(kBlock) void k_stage(const void* __restrict__ offs,
+                                                   const uint8_t* __restrict__ vals,
+                                                   const uint8_t* __restrict__ validity,
+                                                   int64_t voff, int64_t n, int L,
+                                                   uint32_t* __restrict__ codes,
+                                                   uint64_t* __restrict__ regbits,
+                                                   int64_t* __restrict__ irr,
+                                                   unsigned long long* __restrict__ nirr) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    bool valid = false, regular = false;
+    uint32_t code = 0;
+    if (i < n) {
+        valid = true;
+        if (validity) {
+            const int64_t b = voff + i;
+            valid = (validity[b >> 3] >> (b & 7)) & 1;
+        }
+        if (valid) {
+            int64_t st, len;
+            span<OW>(offs, i, st, len);
+            regular = (len == L) && L >= 1 && L <= kMaxPackedLen;
+            for (int j = 0; regular && j < L; ++j) {
+                const int b = base_code(vals[st + j]);
+                regular = b >= 0;
+                code = (code << 2) | (uint32_t)(b & 3);
+            }
+        }
+        codes[i] = regular ? code : 0u;
+    }
+    const uint64_t rmask = __ballot(regular);
+    const uint64_t imask = __ballot(valid && !regular);
+    const int lane = threadIdx.x & 63;
+    if (lane == 0 && i < n) regbits[i >> 6] = rmask;
+    if (imask) {
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(nirr, (unsigned long long)__popcll(imask));
+        base = __shfl(base, 0);
+        if (valid && !regular) {
+            const uint64_t below = imask & ((1ull << lane) - 1ull);
+            irr[base + __popcll(below)] = i;
+        }
+    }
+}
+
+// ------------------------------------------------------ packed scoring
+struct RowScore {
+    double sh, ling, homo, di, comb;
+    uint32_t longest;
+};
+
+__device__ __forceinline__ RowScore score_code(uint32_t code, int L, const double* __restrict__ t_sh,
+                                               const double* __restrict__ t_di,
+                                               const double* __restrict__ t_ling,
+                                               const double* __restrict__ t_frac) {
+    RowScore r;
+    // shannon_entropy (umi_score.rs:45-73): base counts from the 2-bit planes,
+    // terms subtracted in A,C,G,T order; t_sh[0] == 0.0 stands for a skipped term.
+    const uint32_t lowmask = 0x55555555u >> (32 - 2 * L);
+    const uint32_t lo = code & lowmask, hi = (code >> 1) & lowmask;
+    const int nT = __popc(lo & hi), nG = __popc(hi & ~lo), nC = __popc(lo & ~hi);
+    const int nA = L - nT - nG - nC;
+    double e = 0.0;
+    e = e - t_sh[nA];
+    e = e - t_sh[nC];
+    e = e - t_sh[nG];
+    e = e - t_sh[nT];
+    r.sh = e;
+
+    // homopolymer_fraction (:96-121) + longest_homopolymer_run (:149-168)
+    int in_homo = 0, longest = 1, run = 1;
+    uint32_t prev = (code >> (2 * (L - 1))) & 3u;
+    for (int j = 1; j < L; ++j) {
+        const uint32_t b = (code >> (2 * (L - 1 - j))) & 3u;
+        if (b == prev) {
+            ++run;
+        } else {
+            if (run >= 3) in_homo += run;
+            longest = max(longest, run);
+            run = 1;
+        }
+        prev = b;
+    }
+    if (run >= 3) in_homo += run;
+    longest = max(longest, run);
+    r.homo = t_frac[in_homo];
+    r.longest = (uint32_t)longest;
+
+    // linguistic_complexity (:77-93): distinct 3-mers as a 64-bit occupancy mask
+    double ling = 0.0;
+    if (L >= 3) {
+        uint64_t occ = 0;
+        for (int j = 0; j <= L - 3; ++j) occ |= 1ull << ((code >> (2 * (L - 3 - j))) & 63u);
+        ling = t_ling[__popcll(occ)];
+    }
+    r.ling = ling;
+
+    // dinucleotide_entropy (:124-146): 16 nibble counters in one u64, summed in
+    // ascending pair order (A<C<G<T == ASCII order, the oracle's canonical order).
+    double di = 0.0;
+    if (L >= 2) {
+        uint64_t cnt = 0;
+        for (int j = 0; j <= L - 2; ++j) cnt += 1ull << (4 * ((code >> (2 * (L - 2 - j))) & 15u));
+        double d = 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) d = d - t_di[(cnt >> (4 * k)) & 15ull];
+        di = d / 4.0;
+    }
+    r.di = di;
+
+    // calculate_umi_complexity (:27-32); dust_score == 0 for len < 64 (:172)
+    const double dust = 0.0;
+    r.comb = 0.25 * r.sh + 0.25 * r.ling + 0.15 * (1.0 - r.homo) + 0.15 * r.di +
+             0.10 * (1.0 - t_frac[longest]) + 0.10 * (1.0 - fmin(dust, 1.0));
+    return r;
+}
+
+__device__ __forceinline__ uint32_t hamming_code(uint32_t code, const PackedParams& P) {
+    const uint32_t x = code ^ P.tcode;
+    return (uint32_t)__popc((x | (x >> 1)) & P.cmplo) + P.always_mismatch;
+}
+
+template <bool SCORE, bool HAMD, bool HAMW, bool MARK>
+__global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restrict__ codes,
+                                                          const uint64_t* __restrict__ regbits,
+                                                          int64_t n, const PackedParams P,
+                                                          const ScoreOut O,
+                                                          uint32_t* __restrict__ hd,
+                                                          uint64_t* __restrict__ hw,
+                                                          uint8_t* __restrict__ pres) {
+    __shared__ double s_tab[4][kMaxPackedLen + 1];
+    if (SCORE) {
+        for (int t = threadIdx.x; t < 4 * (kMaxPackedLen + 1); t += kBlock) {
+            const int a = t / (kMaxPackedLen + 1), c = t % (kMaxPackedLen + 1);
+            s_tab[a][c] = a == 0 ? P.sh[c] : a == 1 ? P.di[c] : a == 2 ? P.ling[c] : P.frac[c];
+        }
+        __syncthreads();
+    }
+    const int L = P.L;
+    const int64_t row0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * kRowsPerLane;
+    const bool full = row0 + kRowsPerLane <= n;
+
+    uint32_t c[kRowsPerLane] = {0, 0, 0, 0};
+    uint32_t reg = 0;
+    if (row0 < n) {
+        if (full) {
+            const uint4 v = *reinterpret_cast<const uint4*>(codes + row0);
+            c[0] = v.x; c[1] = v.y; c[2] = v.z; c[3] = v.w;
+        } else {
+            for (int k = 0; k < kRowsPerLane; ++k)
+                if (row0 + k < n) c[k] = codes[row0 + k];
+        }
+        reg = regbits ? (uint32_t)(regbits[row0 >> 6] >> (row0 & 63)) & 0xFu : 0xFu;
+        if (!full) reg &= (1u << (uint32_t)(n - row0)) - 1u;
+    }
+
+    uint32_t wnib = 0;
+    if (row0 < n) {
+        if (SCORE) {
+            double sh[4], li[4], ho[4], di[4], du[4], co[4];
+            uint32_t lg[4];
+#pragma unroll
+            for (int k = 0; k < kRowsPerLane; ++k) {
+                if ((reg >> k) & 1u) {
+                    const RowScore r = score_code(c[k], L, s_tab[0], s_tab[1], s_tab[2], s_tab[3]);
+                    sh[k] = r.sh; li[k] = r.ling; ho[k] = r.homo; di[k] = r.di; co[k] = r.comb;
+                    lg[k] = r.longest;
+                } else {
+                    sh[k] = li[k] = ho[k] = di[k] = co[k] = 0.0;
+                    lg[k] = 0;
+                }
+                du[k] = 0.0;
+            }
+            if (full) {
+                auto st2 = [&](double* p, const double* v) {
+                    if (!p) return;
+                    reinterpret_cast<double2*>(p + row0)[0] = make_double2(v[0], v[1]);
+                    reinterpret_cast<double2*>(p + row0)[1] = make_double2(v[2], v[3]);
+                };
+                st2(O.sh, sh); st2(O.ling, li); st2(O.homo, ho); st2(O.di, di);
+                st2(O.dust, du); st2(O.comb, co);
+                if (O.longest)
+                    *reinterpret_cast<uint4*>(O.longest + row0) = make_uint4(lg[0], lg[1], lg[2], lg[3]);
+            } else {
+                for (int k = 0; k < kRowsPerLane; ++k) {
+                    if (row0 + k >= n) break;
+                    if (O.sh) O.sh[row0 + k] = sh[k];
+                    if (O.ling) O.ling[row0 + k] = li[k];
+                    if (O.homo) O.homo[row0 + k] = ho[k];
+                    if (O.di) O.di[row0 + k] = di[k];
+                    if (O.dust) O.dust[row0 + k] = du[k];
+                    if (O.comb) O.comb[row0 + k] = co[k];
+                    if (O.longest) O.longest[row0 + k] = lg[k];
+                }
+            }
+        }
+        if (HAMD || HAMW) {
+            uint32_t d[4];
+#pragma unroll
+            for (int k = 0; k < kRowsPerLane; ++k) {
+                d[k] = 0;
+                if ((reg >> k) & 1u) {
+                    d[k] = P.ham_mode == 1 ? hamming_code(c[k], P) : 0xFFFFFFFFu;
+                    if (P.ham_mode == 1 && d[k] <= P.max_distance) wnib |= 1u << k;
+                }
+            }
+            if (HAMD) {
+                if (full) {
+                    *reinterpret_cast<uint4*>(hd + row0) = make_uint4(d[0], d[1], d[2], d[3]);
+                } else {
+                    for (int k = 0; k < kRowsPerLane; ++k)
+                        if (row0 + k < n) hd[row0 + k] = d[k];
+                }
+            }
+        }
+        if (MARK) {
+#pragma unroll
+            for (int k = 0; k < kRowsPerLane; ++k)
+                if ((reg >> k) & 1u) pres[c[k]] = 1;  // benign same-value race
+        }
+    }
+    if (HAMW) {
+        // 16 lanes x 4 rows = one 64-row word (LSB = first row): OR-reduce in-wave.
+        uint64_t w = (uint64_t)wnib << (4 * (threadIdx.x & 15));
+        w |= __shfl_xor(w, 1);
+        w |= __shfl_xor(w, 2);
+        w |= __shfl_xor(w, 4);
+        w |= __shfl_xor(w, 8);
+        if ((threadIdx.x & 15) == 0 && row0 < n) hw[row0 >> 6] = w;
+    }
+}
+
+// ------------------------------------------------------------ byte path
+__device__ __forceinline__ uint32_t utf8_next(const uint8_t* s, int64_t n, int64_t& i) {
+    const uint8_t c = s[i];
+    int64_t w = c < 0x80 ? 1 : (c >> 5) == 0x6 ? 2 : (c >> 4) == 0xE ? 3 : 4;
+    if (i + w > n) w = n - i;
+    uint32_t v = w == 1 ? c : w == 2 ? (c & 0x1Fu) : w == 3 ? (c & 0x0Fu) : (c & 0x07u);
+    for (int64_t k = 1; k < w; ++k) v = (v << 6) | (s[i + k] & 0x3Fu);
+    i += w;
+    return v;
+}
+
+__device__ uint32_t hamming_bytes(const uint8_t* s, int64_t n, const uint8_t* t, int64_t tn) {
+    if (n != tn) return 0xFFFFFFFFu;
+    uint32_t d = 0;
+    int64_t i = 0, j = 0;
+    while (i < n && j < tn) d += utf8_next(s, n, i) != utf8_next(t, tn, j) ? 1u : 0u;
+    return d;
+}
+
+__device__ __forceinline__ uint32_t trip(const uint8_t* s, int64_t j) {
+    return ((uint32_t)s[j] << 16) | ((uint32_t)s[j + 1] << 8) | s[j + 2];
+}
+
+__device__ void score_bytes(const uint8_t* s, int64_t n, const double* __restrict__ lut,
+                            int64_t lut_max, RowScore& r, double& dust) {
+    const double qnan = __longlong_as_double(0x7FF8000000000001ll);
+    // shannon_entropy (umi_score.rs:45-73): total counts every byte
+    uint32_t cnt[4] = {0, 0, 0, 0};
+    for (int64_t i = 0; i < n; ++i) {
+        const int b = base_code(s[i]);
+        if (b >= 0) cnt[b] += 1;
+    }
+    double e = 0.0;
+    if (n > 0) {
+        if (n > lut_max) e = qnan;
+        else
+            for (int b = 0; b < 4; ++b)
+                if (cnt[b]) e = e - lut[lut_index(n, cnt[b])];
+    }
+    r.sh = e;
+    // linguistic_complexity (:77-93): distinct byte 3-mers / min(len-2, 64)
+    double ling = 0.0;
+    if (n >= 3) {
+        int64_t u = 0;
+        for (int64_t i = 0; i + 3 <= n; ++i) {
+            const uint32_t k = trip(s, i);
+            bool dup = false;
+            for (int64_t j = 0; j < i && !dup; ++j) dup = trip(s, j) == k;
+            u += dup ? 0 : 1;
+        }
+        ling = (double)u / (double)min<int64_t>(n - 2, 64);
+    }
+    r.ling = ling;
+    // homopolymer_fraction (:96-121) + longest_homopolymer_run (:149-168)
+    int64_t in_homo = 0, longest = n ? 1 : 0, run = 1;
+    for (int64_t i = 1; i < n; ++i) {
+        if (s[i] == s[i - 1]) {
+            ++run;
+        } else {
+            if (run >= 3) in_homo += run;
+            longest = max(longest, run);
+            run = 1;
+        }
+    }
+    if (n) {
+        if (run >= 3) in_homo += run;
+        longest = max(longest, run);
+    }
+    r.homo = n ? (double)in_homo / (double)n : 0.0;
+    r.longest = (uint32_t)longest;
+    // dinucleotide_entropy (:124-146), canonical ascending (byte0, byte1) order
+    double di = 0.0;
+    if (n >= 2) {
+        const int64_t t = n - 1;
+        double d = 0.0;
+        int32_t prev = -1;
+        if (t > lut_max) d = qnan;
+        else
+            for (;;) {
+                int32_t cur = 0x10000;
+                for (int64_t i = 0; i + 2 <= n; ++i) {
+                    const int32_t k = ((int32_t)s[i] << 8) | s[i + 1];
+                    if (k > prev && k < cur) cur = k;
+                }
+                if (cur == 0x10000) break;
+                int64_t c = 0;
+                for (int64_t i = 0; i + 2 <= n; ++i) c += (((int32_t)s[i] << 8) | s[i + 1]) == cur;
+                d = d - lut[lut_index(t, c)];
+                prev = cur;
+            }
+        di = d / 4.0;
+    }
+    r.di = di;
+    // dust_score(seq, 64) (:171-200): pairs of equal triplets per 64-byte window,
+    // slid incrementally; integer sums are exact in f64, so order is immaterial.
+    dust = 0.0;
+    if (n >= 64) {
+        constexpr int64_t kT = 62;  // triplets per window
+        uint64_t score = 0;
+        for (int64_t j = 0; j < kT; ++j)
+            for (int64_t k = j + 1; k < kT; ++k) score += trip(s, j) == trip(s, k);
+        uint64_t total = score;
+        for (int64_t i = 0; i + 64 < n; ++i) {
+            const uint32_t out = trip(s, i), in = trip(s, i + kT);
+            for (int64_t k = i + 1; k < i + kT; ++k) {
+                const uint32_t tk = trip(s, k);
+                score -= tk == out;
+                score += tk == in;
+            }
+            total += score;
+        }
+        dust = (double)total / (double)(n - 64 + 1);
+    }
+    if (n == 0) {
+        r.comb = x86_default_nan();
+    } else {
+        r.comb = 0.25 * r.sh + 0.25 * r.ling + 0.15 * (1.0 - r.homo) + 0.15 * r.di +
+                 0.10 * (1.0 - ((double)longest / (double)n)) + 0.10 * (1.0 - fmin(dust, 1.0));
+    }
+}
+
+template <int OW>
+__global__ __launch_bounds__(kBlock) void k_score_rows(
+    const void* __restrict__ offs, const uint8_t* __restrict__ vals,
+    const int64_t* __restrict__ rows, const int64_t* __restrict__ n_rows_dev, int64_t max_rows,
+    const double* __restrict__ lut, int64_t lut_max, const ScoreOut O,
+    const uint8_t* __restrict__ tgt, int64_t tlen, int ham, uint32_t maxd,
+    uint32_t* __restrict__ hd, unsigned long long* __restrict__ hw) {
+    int64_t nr = max_rows;
+    if (n_rows_dev) nr = min<int64_t>(nr, *n_rows_dev);
+    const bool score = O.sh || O.ling || O.homo || O.di || O.longest || O.dust || O.comb;
+    for (int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x; k < nr;
+         k += (int64_t)gridDim.x * kBlock) {
+        const int64_t row = rows[k];
+        int64_t st, len;
+        span<OW>(offs, row, st, len);
+        const uint8_t* s = vals + st;
+        if (score) {
+            RowScore r;
+            double dust;
+            score_bytes(s, len, lut, lut_max, r, dust);
+            if (O.sh) O.sh[row] = r.sh;
+            if (O.ling) O.ling[row] = r.ling;
+            if (O.homo) O.homo[row] = r.homo;
+            if (O.di) O.di[row] = r.di;
+            if (O.longest) O.longest[row] = r.longest;
+            if (O.dust) O.dust[row] = dust;
+            if (O.comb) O.comb[row] = r.comb;
+        }
+        if (ham) {
+            const uint32_t d = hamming_bytes(s, len, tgt, tlen);
+            if (hd) hd[row] = d;
+            if (hw && d != 0xFFFFFFFFu && d <= maxd) atomicOr(hw + (row >> 6), 1ull << (row & 63));
+        }
+    }
+}
+
+inline int grid_for(int64_t lanes) {
+    const int64_t g = (lanes + kBlock - 1) / kBlock;
+    return (int)(g < 1 ? 1 : g);
+}
+
+}  // namespace
+
+int launch_stage(const void* offsets, int offset_width, const uint8_t* values,
+                 const uint8_t* validity, int64_t validity_offset, int64_t n, int L,
+                 uint32_t* codes, uint64_t* regular_bits, int64_t* irregular_rows,
+                 unsigned long long* n_irregular, hipStream_t s) {
+    if (n <= 0) return ROGTK_OK;
+    ProfScope prof(K_STAGE, s);
+    const int g = grid_for(n);
+    if (offset_width == 4)
+        hipLaunchKernelGGL(k_stage<4>, dim3(g), dim3(kBlock), 0, s, offsets, values, validity,
+                           validity_offset, n, L, codes, regular_bits, irregular_rows, n_irregular);
+    else
+        hipLaunchKernelGGL(k_stage<8>, dim3(g), dim3(kBlock), 0, s, offsets, values, validity,
+                           validity_offset, n, L, codes, regular_bits, irregular_rows, n_irregular);
+    ROGTK_HIP_CHECK(hipGetLastError());
+    return ROGTK_OK;
+}
+
+int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
+                        const PackedParams& p, const ScoreOut& o, uint32_t* hd, uint64_t* hw,
+                        uint8_t* presence, hipStream_t s) {
+    if (n <= 0) return ROGTK_OK;
+    const bool score = any_score(o), hamd = p.ham_mode && hd, hamw = p.ham_mode && hw,
+               mark = presence != nullptr;
+    if (!score && !hamd && !hamw && !mark) return ROGTK_OK;
+    ProfScope prof(K_SCORE_PACKED, s);
+    const int g = grid_for((n + kRowsPerLane - 1) / kRowsPerLane);
+    const int sel = (score ? 8 : 0) | (hamd ? 4 : 0) | (hamw ? 2 : 0) | (mark ? 1 : 0);
+#define ROGTK_SP(S, D, W, M)                                                                    \
+    case (S * 8 + D * 4 + W * 2 + M):                                                          \
+        hipLaunchKernelGGL((k_score_packed<S, D, W, M>), dim3(g), dim3(kBlock), 0, s, codes, \
+                           regular_bits, n, p, o, hd, hw, presence);                          \
+        break;
+    switch (sel) {
+        ROGTK_SP(0, 0, 0, 1) ROGTK_SP(0, 0, 1, 0) ROGTK_SP(0, 0, 1, 1) ROGTK_SP(0, 1, 0, 0)
+        ROGTK_SP(0, 1, 0, 1) ROGTK_SP(0, 1, 1, 0) ROGTK_SP(0, 1, 1, 1) ROGTK_SP(1, 0, 0, 0)
+        ROGTK_SP(1, 0, 0, 1) ROGTK_SP(1, 0, 1, 0) ROGTK_SP(1, 0, 1, 1) ROGTK_SP(1, 1, 0, 0)
+        ROGTK_SP(1, 1, 0, 1) ROGTK_SP(1, 1, 1, 0) ROGTK_SP(1, 1, 1, 1)
+        default: break;
+    }
+#undef ROGTK_SP
+    ROGTK_HIP_CHECK(hipGetLastError());
+    return ROGTK_OK;
+}
+
+int launch_score_rows(const void* offsets, int offset_width, const uint8_t* values,
+                      const int64_t* rows, const int64_t* n_rows_dev, int64_t max_rows,
+                      const double* lut, int64_t lut_max, const ScoreOut& o,
+                      const uint8_t* target_dev, int64_t target_len, int ham, uint32_t max_distance,
+                      uint32_t* hd, uint64_t* hw, hipStream_t s) {
+    if (max_rows <= 0) return ROGTK_OK;
+    if (!any_score(o) && !(ham && (hd || hw))) return ROGTK_OK;
+    ProfScope prof(K_SCORE_ROWS, s);
+    int g = grid_for(max_rows);
+    if (g > 4096) g = 4096;
+    if (offset_width == 4)
+        hipLaunchKernelGGL(k_score_rows<4>, dim3(g), dim3(kBlock), 0, s, offsets, values, rows,
+                           n_rows_dev, max_rows, lut, lut_max, o, target_dev, target_len, ham,
+                           max_distance, hd, (unsigned long long*)hw);
+    else
+        hipLaunchKernelGGL(k_score_rows<8>, dim3(g), dim3(kBlock), 0, s, offsets, values, rows,
+                           n_rows_dev, max_rows, lut, lut_max, o, target_dev, target_len, ham,
+                           max_distance, hd, (unsigned long long*)hw);
+    ROGTK_HIP_CHECK(hipGetLastError());
+    return ROGTK_OK;
+}
+
+}  // namespace rogtk

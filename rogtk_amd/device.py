@@ -1,0 +1,184 @@
+"""Device-resident pipeline over the packed 2-bit SoA (level-1 C ABI).
+
+PyTorch is only plumbing here: tensors provide HBM allocations and the HIP
+stream (torch's current stream) whose handle is passed through the C ABI; every
+byte of compute happens in librogtk_hip's kernels.
+
+Layout in HBM for a batch of n reads (DESIGN.md §Data layout):
+  codes         uint32[n]        2 bits/base, first base most significant
+  regular_bits  uint64[ceil(n/64)]  row is packable (else: byte path / null)
+  scores        6 x float64[n] + uint32[n]   (SoA, one array per field)
+  hamming       uint32[n] distance and/or uint64[ceil(n/64)] within bits
+  cluster_id    uint32[n]
+  cluster ws    presence u8[4^L] | bitmap u64[4^L/64] | rank tables | D/parent u32[max_distinct] | labels
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional
+
+import torch
+
+from . import _lib
+
+_FIELDS = ("shannon_entropy", "linguistic_complexity", "homopolymer_fraction",
+           "dinucleotide_entropy", "longest_homopolymer_run", "dust_score", "combined_score")
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _s(stream: Optional[torch.cuda.Stream] = None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class PackedBatch:
+    """The packed SoA of one batch (device tensors)."""
+
+    def __init__(self, codes: torch.Tensor, umi_len: int, regular_bits: Optional[torch.Tensor] = None):
+        if codes.dtype != torch.int32 or not codes.is_cuda or not codes.is_contiguous():
+            raise TypeError("codes must be a contiguous int32 (bit pattern of uint32) CUDA tensor")
+        if not 1 <= umi_len <= 16:
+            raise ValueError("packed path supports umi_len 1..16")
+        self.codes = codes
+        self.umi_len = int(umi_len)
+        self.regular_bits = regular_bits
+        self.n = codes.numel()
+
+
+def alloc_scores(n: int, device, fields=_FIELDS) -> Dict[str, torch.Tensor]:
+    out = {}
+    for f in fields:
+        dt = torch.int32 if f == "longest_homopolymer_run" else torch.float64
+        out[f] = torch.empty(max(n, 4), dtype=dt, device=device)
+    return out
+
+
+def _scores_struct(scores: Optional[Dict[str, torch.Tensor]]):
+    if not scores:
+        return None
+    return ctypes.byref(_lib.UmiScores(*[_p(scores.get(f)) for f in _FIELDS]))
+
+
+def stage_strings(offsets: torch.Tensor, values: torch.Tensor, n: int, umi_len: int,
+                  validity: Optional[torch.Tensor] = None, validity_offset: int = 0, stream=None):
+    """Arrow strings already in HBM -> (PackedBatch, irregular_rows int64[n], n_irregular int64[1])."""
+    dev = offsets.device
+    codes = torch.empty(max(n, 4), dtype=torch.int32, device=dev)
+    regbits = torch.empty(max((n + 63) // 64, 1), dtype=torch.int64, device=dev)
+    irr = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    nirr = torch.zeros(1, dtype=torch.int64, device=dev)
+    ow = offsets.element_size()
+    _lib.call("rogtk_stage_strings", _p(offsets), ow, _p(values), _p(validity), validity_offset, n, umi_len,
+              _p(codes), _p(regbits), _p(irr), _p(nirr), _s(stream))
+    batch = PackedBatch(codes[:n] if n else codes[:0], umi_len if 1 <= umi_len <= 16 else 16, regbits)
+    batch.n = n
+    return batch, irr, nirr
+
+
+def score_packed(batch: PackedBatch, scores: Optional[Dict[str, torch.Tensor]] = None,
+                 target: Optional[bytes] = None, max_distance: int = 1,
+                 hamming_distance: Optional[torch.Tensor] = None,
+                 hamming_within_bits: Optional[torch.Tensor] = None,
+                 cluster: Optional["ClusterEngine"] = None, stream=None) -> None:
+    """The fused hot kernel: H1 scores + H2 Hamming + H3 presence mark in one pass."""
+    t = None
+    tl = 0
+    if target is not None:
+        tb = target.encode() if isinstance(target, str) else bytes(target)
+        t = ctypes.create_string_buffer(tb, max(len(tb), 1))
+        tl = len(tb)
+    _lib.call("rogtk_umi_score_packed", _p(batch.codes), _p(batch.regular_bits), batch.n, batch.umi_len,
+              _scores_struct(scores), t, tl, max_distance, _p(hamming_distance), _p(hamming_within_bits),
+              _p(cluster.ws) if cluster is not None else None,
+              cluster.max_distinct if cluster is not None else 0, _s(stream))
+
+
+def score_rows(offsets: torch.Tensor, values: torch.Tensor, rows: torch.Tensor,
+               n_rows_dev: Optional[torch.Tensor], max_rows: int, max_len: int,
+               scores: Optional[Dict[str, torch.Tensor]] = None, target: Optional[bytes] = None,
+               max_distance: int = 1, hamming_distance=None, hamming_within_bits=None, stream=None):
+    """Byte path for listed rows (irregular UMIs) of a device Arrow string column."""
+    t = None
+    tl = 0
+    if target is not None:
+        tb = target.encode() if isinstance(target, str) else bytes(target)
+        t = ctypes.create_string_buffer(tb, max(len(tb), 1))
+        tl = len(tb)
+    _lib.call("rogtk_umi_score_rows", _p(offsets), offsets.element_size(), _p(values), _p(rows),
+              _p(n_rows_dev), max_rows, max_len, _scores_struct(scores), t, tl, max_distance,
+              _p(hamming_distance), _p(hamming_within_bits), _s(stream))
+
+
+class ClusterEngine:
+    """H3 over the packed SoA: workspace + the mark/bitmap/resolve/assign phases."""
+
+    def __init__(self, umi_len: int, max_distinct: int, device, stream=None):
+        self.umi_len = int(umi_len)
+        self.max_distinct = int(min(max_distinct, 4 ** self.umi_len))
+        nbytes = ctypes.c_int64(0)
+        _lib.call("rogtk_cluster_workspace_size", self.umi_len, self.max_distinct, ctypes.byref(nbytes))
+        words = ctypes.c_int64(0)
+        _lib.call("rogtk_cluster_bitmap_words", self.umi_len, ctypes.byref(words))
+        self.words = int(words.value)
+        self.ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=device)
+        self.local_bitmap = torch.empty(self.words, dtype=torch.int64, device=device)
+        _lib.call("rogtk_cluster_init", _p(self.ws), self.umi_len, self.max_distinct, _s(stream))
+
+    @property
+    def workspace_bytes(self) -> int:
+        return self.ws.numel()
+
+    def mark(self, batch: PackedBatch, stream=None) -> None:
+        _lib.call("rogtk_cluster_mark", _p(batch.codes), _p(batch.regular_bits), batch.n, self.umi_len,
+                  _p(self.ws), self.max_distinct, _s(stream))
+
+    def build_local_bitmap(self, stream=None) -> torch.Tensor:
+        _lib.call("rogtk_cluster_local_bitmap", _p(self.ws), self.umi_len, self.max_distinct,
+                  _p(self.local_bitmap), _s(stream))
+        return self.local_bitmap
+
+    def resolve(self, bitmaps: torch.Tensor, n_bitmaps: int, max_distance: int, stream=None) -> None:
+        if bitmaps.numel() != n_bitmaps * self.words:
+            raise ValueError("bitmaps must hold n_bitmaps * words int64 words")
+        _lib.call("rogtk_cluster_resolve", _p(self.ws), self.umi_len, self.max_distinct, _p(bitmaps),
+                  int(n_bitmaps), int(max_distance), _s(stream))
+
+    def assign(self, batch: PackedBatch, cluster_id: torch.Tensor, stream=None) -> None:
+        _lib.call("rogtk_cluster_assign", _p(self.ws), self.umi_len, self.max_distinct, _p(batch.codes),
+                  _p(batch.regular_bits), batch.n, _p(cluster_id), _s(stream))
+
+    def stats(self, stream=None) -> Dict[str, int]:
+        out = (ctypes.c_int64 * 4)()
+        _lib.call("rogtk_cluster_stats", _p(self.ws), self.umi_len, self.max_distinct, out, _s(stream))
+        return {"n_distinct": out[0], "n_clusters": out[1], "overflow": out[2], "error": out[3]}
+
+
+def cluster_batch(engine: ClusterEngine, batch: PackedBatch, cluster_id: torch.Tensor,
+                  max_distance: int = 1, group=None, marked: bool = False, stream=None) -> None:
+    """mark -> local bitmap -> (all-gather over ranks) -> resolve -> assign."""
+    from .dist import gather_bitmaps
+
+    if not marked:
+        engine.mark(batch, stream)
+    local = engine.build_local_bitmap(stream)
+    bitmaps, nb = gather_bitmaps(local, group)
+    engine.resolve(bitmaps, nb, max_distance, stream)
+    engine.assign(batch, cluster_id, stream)
+
+
+def profile_enable(on: bool = True) -> None:
+    _lib.call("rogtk_profile_enable", 1 if on else 0)
+
+
+def profile_reset() -> None:
+    _lib.call("rogtk_profile_reset")
+
+
+def profile_read(kernel: str):
+    ms = ctypes.c_double(0)
+    n = ctypes.c_int64(0)
+    _lib.call("rogtk_profile_read", kernel.encode(), ctypes.byref(ms), ctypes.byref(n))
+    return ms.value, n.value
