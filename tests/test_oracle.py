@@ -1,0 +1,156 @@
+"""CPU: the oracle pinned against SURVEY.md Appendix A, the pure-Python restatement,
+the committed golden vectors, and (for H3) an O(n^2) brute force."""
+from __future__ import annotations
+
+import math
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import pyoracle as P
+
+# hand-derived known answers (dinucleotide terms summed in
+# first-occurrence order, as printed there). Fields: shannon, linguistic,
+# homopolymer, dinuc, longest, dust, combined.
+APPENDIX_A = {
+    b"AAAAAAAAAAAA": (0.0, 0.1, 1.0, 0.0, 12, 0.0, 0.125),
+    b"ACGTACGTACGT": (2.0, 0.4, 0.0, 0.49520648405726964, 1, 0.0, 1.015947639275257),
+    b"AACCGGTTAACC": (1.9182958340544893, 0.8, 0.0, 0.7284942682956881, 2, 0.0, 1.122181432091309),
+    b"ACGTTGCAACGT": (2.0, 0.8, 0.0, 0.7284942682956881, 2, 0.0, 1.1426074735776865),
+    b"GATTACAGATTA": (1.7841591278514217, 0.7, 0.0, 0.6830397228411426, 2, 0.0, 1.0568290737223602),
+    b"NNNNNNNNNNNN": (0.0, 0.1, 1.0, 0.0, 12, 0.0, 0.125),
+    b"ACGTNACGTACG": (1.930827083453526, 0.7, 0.0, 0.6032721091064395, 1, 0.0, 1.0898642538960142),
+    b"acgtacgtacgt": (0.0, 0.4, 0.0, 0.49520648405726964, 1, 0.0, 0.5159476392752571),
+}
+
+
+def _ulp_diff(a: float, b: float) -> int:
+    ia = np.array([a]).view(np.int64)[0]
+    ib = np.array([b]).view(np.int64)[0]
+    return abs(int(ia) - int(ib))
+
+
+@pytest.mark.parametrize("umi", list(APPENDIX_A))
+def test_appendix_a_first_occurrence_order_exact(umi):
+    got = P.umi_complexity_one(umi, dinuc_order=1)
+    exp = APPENDIX_A[umi]
+    for f, e in zip(P.FIELDS, exp):
+        assert got[f] == e, (umi, f, got[f], e)
+
+
+@pytest.mark.parametrize("umi", list(APPENDIX_A))
+def test_appendix_a_canonical_order_within_2ulp(umi):
+    """The canonical (ascending pair) order differs from any HashMap order by <= 2 ULP
+    on dinucleotide/combined only; all other fields exact."""
+    got = P.umi_complexity_one(umi, dinuc_order=0)
+    exp = APPENDIX_A[umi]
+    for f, e in zip(P.FIELDS, exp):
+        if f in ("dinucleotide_entropy", "combined_score"):
+            assert _ulp_diff(got[f], e) <= 2, (umi, f)
+        else:
+            assert got[f] == e, (umi, f)
+
+
+def test_empty_umi_is_x86_default_nan():
+    r = P.umi_complexity_one(b"", 0)
+    assert math.isnan(r["combined_score"])
+    assert np.array([r["combined_score"]]).view(np.uint64)[0] == 0xFFF8000000000000
+    assert r["longest_homopolymer_run"] == 0 and r["shannon_entropy"] == 0.0
+
+
+def _random_bytes(rng, n, lengths, alphabet):
+    return [bytes(rng.choice(list(alphabet), size=int(rng.choice(lengths))).astype(np.uint8)) for _ in range(n)]
+
+
+@pytest.mark.parametrize("order", [0, 1])
+def test_cpp_oracle_matches_python_restatement(order):
+    rng = np.random.default_rng(1)
+    umis = _random_bytes(rng, 300, list(range(0, 30)), b"ACGTNacgt")
+    umis += _random_bytes(rng, 20, [64, 65, 80, 130], b"ACGT")  # DUST windows
+    umis += _random_bytes(rng, 10, [100], b"AC")
+    for u in umis:
+        a = P.umi_complexity_one(u, order)
+        b = P.py_umi_complexity(u, order)
+        for f in P.FIELDS:
+            va, vb = a[f], b[f]
+            if isinstance(vb, float) and math.isnan(vb):
+                assert math.isnan(va)
+            else:
+                assert va == vb, (u, f, va, vb)
+
+
+def test_dust_nonzero_for_long_reads():
+    r = P.umi_complexity_one(b"A" * 100, 0)
+    # every 64-byte window holds 62 identical triplets: 62*61/2 pairs
+    assert r["dust_score"] == 62 * 61 / 2
+    assert r["combined_score"] == P.py_umi_complexity(b"A" * 100)["combined_score"]
+
+
+def test_hamming_semantics():
+    t = b"ACGTACGTACGT"
+    assert P.py_hamming(b"ACGTACGTACGT", t) == 0
+    assert P.py_hamming(b"ACGTACGTACGA", t) == 1
+    assert P.py_hamming(b"ACGT", t) == 0xFFFFFFFF  # byte-length mismatch -> u32::MAX
+    # same byte length, fewer chars: zip stops at the shorter char sequence
+    assert P.py_hamming("ACGTACGTACé".encode(), t) == 1
+    col = P.StrCol.from_list([b"ACGTACGTACGT", None, b"ACGTNCGTACGT", b"ACG", "ACGTACGTACé".encode()])
+    d, w, valid = P.hamming(col, t, 1)
+    assert list(valid) == [True, False, True, True, True]
+    assert d[0] == 0 and d[2] == 1 and d[3] == 0xFFFFFFFF and d[4] == 1
+    assert list(w[[0, 2, 3, 4]]) == [True, True, False, True]
+
+
+@pytest.mark.parametrize("fixture", ["c1_clean", "c1_stress"])
+def test_golden_vectors_reproduce(fixture):
+    """The committed fixtures are exactly what the oracle computes (no drift)."""
+    z = np.load(os.path.join(GOLDEN, fixture + ".npz"), allow_pickle=False)
+    offs, vals, valid = z["offsets"], z["values"], z["valid"]
+    n = len(valid)
+    validity = None if valid.all() else np.packbits(valid, bitorder="little")
+    col = P.StrCol(offs, vals, validity, n)
+    res = P.umi_complexity(col)
+    for f in P.FIELDS:
+        a = res[f].view(np.uint64) if res[f].dtype == np.float64 else res[f]
+        assert np.array_equal(a[valid], z["f_" + f][valid]), f
+    for md in (0, 1):
+        cid, cv, k, _ = P.umi_cluster(col, 12, md)
+        assert k == int(z[f"n_clusters_{md}"][0])
+        assert np.array_equal(cid[cv], z[f"cluster_{md}"][cv])
+
+
+def test_golden_stress_covers_edge_cases():
+    z = np.load(os.path.join(GOLDEN, "c1_stress.npz"), allow_pickle=False)
+    lens = np.diff(z["offsets"])
+    valid = z["valid"]
+    assert (~valid).sum() >= 1  # nulls
+    assert (lens[valid] == 0).any()  # empty string
+    assert (lens[valid] >= 64).any()  # DUST windows
+    assert (lens[valid] < 3).any()  # below the 3-mer window
+    vals = z["values"]
+    assert (vals == ord("N")).any() and (vals >= 0x80).any() and ((vals >= ord("a")) & (vals <= ord("z"))).any()
+
+
+@pytest.mark.parametrize("md", [0, 1])
+def test_cluster_oracle_vs_bruteforce(md):
+    rng = np.random.default_rng(4 + md)
+    umis = _random_bytes(rng, 1500, [5], b"ACGT")
+    umis += [None, b"ACGTN", b"acgta", b"ACGT", b"ACGTAC", b"ACGTN"]
+    ref, rk = P.py_cluster_bruteforce(umis, 5, md)
+    cid, valid, k, L = P.umi_cluster(P.StrCol.from_list(umis), 5, md)
+    assert L == 5 and k == rk
+    assert [int(c) if v else None for c, v in zip(cid, valid)] == ref
+
+
+def test_cluster_spec_properties():
+    """Ids are dense, ordered by each cluster's smallest UMI, transitive for d=1."""
+    umis = [b"AAAA", b"AAAC", b"AACC", b"TTTT", b"GGGG", b"GGGA", b"CCCC", b"AAAN", b"AAAN", None]
+    cid, valid, k, _ = P.umi_cluster(P.StrCol.from_list(umis), 4, 1)
+    ids = dict(zip(umis, cid))
+    assert ids[b"AAAA"] == ids[b"AAAC"] == ids[b"AACC"] == 0  # chain AAAA-AAAC-AACC
+    assert ids[b"CCCC"] == 1 and ids[b"GGGA"] == ids[b"GGGG"] == 2 and ids[b"TTTT"] == 3
+    assert ids[b"AAAN"] == 4  # irregular rows after the regular clusters
+    assert k == 5 and not valid[-1]
+    cid0, _, k0, _ = P.umi_cluster(P.StrCol.from_list(umis), 4, 0)
+    assert k0 == 8  # 7 distinct regular + 1 irregular
