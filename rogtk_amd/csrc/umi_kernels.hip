@@ -467,7 +467,7 @@ int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int
     const bool score = any_score(o), hamd = p.ham_mode && hd, hamw = p.ham_mode && hw,
                mark = presence != nullptr;
     if (!score && !hamd && !hamw && !mark) return ROGTK_OK;
-    ProfScope prof(K_SCORE_PACKED, s);
+    ProfScope prof(score || hamd || hamw ? K_SCORE_PACKED : K_MARK, s);
     const int g = grid_for((n + kRowsPerLane - 1) / kRowsPerLane);
     const int sel = (score ? 8 : 0) | (hamd ? 4 : 0) | (hamw ? 2 : 0) | (mark ? 1 : 0);
 #define ROGTK_SP(S, D, W, M)                                                                    \
