@@ -3,10 +3,13 @@
 
 One step = one pass of the hot path over one batch of synthetic reads already
 resident in HBM as the packed 2-bit SoA (BASELINE config C2: 10M reads per GPU,
-12-bp UMI, Hamming<=1):
-  k_score_packed  H1 all 7 complexity fields + H2 Hamming-within bits + H3 presence mark
-  cluster         presence -> bitmap -> [all-gather over ranks, RCCL] -> scan ->
-                  compact -> union-find -> flatten -> labels -> assign cluster ids
+12-bp UMI, Hamming<=1), through rogtk_amd.pipeline (three HIP streams, --depth
+batches in flight; the timed region ends after every submitted batch is done):
+  main     k_score_packed: H1 all 7 complexity fields + H2 Hamming-within bits +
+           H3 presence mark; presence -> bitmap
+  resolve  [all-gather over ranks, RCCL] -> scan -> rank tables -> LDS-local CC ->
+           global hook/jump rounds -> labels
+  assign   cluster ids per read
 Weak scaling: every rank owns reads_per_gpu records of one global dataset
 (shard by record); value = all ranks' reads / max-over-ranks wall time.
 
@@ -32,6 +35,7 @@ sys.path.insert(0, ROOT)
 from rogtk_amd import device as D  # noqa: E402
 from rogtk_amd import dist as RD  # noqa: E402
 from rogtk_amd import synth  # noqa: E402
+from rogtk_amd.pipeline import UmiPipeline  # noqa: E402
 
 METRIC = "reads/s UMI score+cluster, 150 bp/12 bp UMI, 1→8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -49,6 +53,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip in-run HIP-event kernel timing")
+    ap.add_argument("--depth", type=int, default=3, help="batches in flight (1 = no cross-batch overlap)")
     return ap.parse_args()
 
 
@@ -115,17 +120,15 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     codes = torch.from_numpy(codes_h.view(np.int32)).to(dev)
     batch = D.PackedBatch(codes, L)
-    scores = D.alloc_scores(count, dev)
-    within = torch.empty((count + 63) // 64, dtype=torch.int64, device=dev)
-    cid = torch.empty(count, dtype=torch.int32, device=dev)
-    eng = D.ClusterEngine(L, min(n_total, 4 ** L), dev)
+    pipe = UmiPipeline(L, min(n_total, 4 ** L), count, dev, depth=args.depth, target=TARGET,
+                       max_distance=md, group=None)
 
     def step():
-        D.score_packed(batch, scores, TARGET, 1, None, within, cluster=eng)
-        D.cluster_batch(eng, batch, cid, md, marked=True)
+        pipe.submit(batch)
 
     for _ in range(args.warmup):
         step()
+    pipe.drain()
     torch.cuda.synchronize()
     if not args.no_profile:
         D.profile_reset()
@@ -135,6 +138,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    pipe.drain()
     torch.cuda.synchronize()
     barrier(world)
     el = time.perf_counter() - t0
@@ -144,7 +148,7 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    stats = eng.stats()
+    stats = pipe.slots[0].eng.stats()
 
     kernels = {}
     if not args.no_profile:

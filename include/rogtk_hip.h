@@ -143,17 +143,24 @@ int rogtk_cluster_mark(const uint32_t* codes, const uint64_t* regular_bits, int6
 /* presence table -> bitmap words (rogtk_cluster_bitmap_words); clears presence */
 int rogtk_cluster_local_bitmap(void* ws, int umi_len, int64_t max_distinct,
                                uint64_t* bitmap_out, void* stream);
-/* bitmaps: n_bitmaps bitmaps laid out back to back (all-gather output layout) */
+/* bitmaps: n_bitmaps bitmaps laid out back to back (all-gather output layout).
+ * Enqueue-only: the global union rounds run speculatively and their convergence
+ * flags are copied asynchronously to pinned host memory; rogtk_cluster_assign /
+ * rogtk_cluster_stats check them (normally already complete) and finish the
+ * resolve on their own stream in the rare case more rounds are needed. */
 int rogtk_cluster_resolve(void* ws, int umi_len, int64_t max_distinct,
                           const uint64_t* bitmaps, int n_bitmaps, int max_distance,
                           void* stream);
-/* cluster_id[i] for regular rows; 0xFFFFFFFF for the others */
+/* cluster_id[i] for regular rows; 0xFFFFFFFF for the others. Completes a pending
+ * resolve of this workspace first (host waits on that resolve's event). */
 int rogtk_cluster_assign(const void* ws, int umi_len, int64_t max_distinct,
                          const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
                          uint32_t* cluster_id, void* stream);
 /* Copies {n_distinct, n_clusters, overflow, error} (int64 each) to host; syncs the stream. */
 int rogtk_cluster_stats(const void* ws, int umi_len, int64_t max_distinct, int64_t* out4,
                         void* stream);
+/* Releases the host-side resolve state kept for ws (call before freeing ws). */
+int rogtk_cluster_release(const void* ws);
 
 /* ========================= Level 2: host buffers ========================= */
 

@@ -442,6 +442,7 @@ int rogtk_cluster_init(void* ws, int umi_len, int64_t max_distinct, void* stream
     ClusterLayout cl;
     if (int rc = cluster_layout(umi_len, max_distinct, &cl)) return rc;
     ROGTK_REQUIRE(ws, ROGTK_E_INVALID, "ws is NULL");
+    cluster_release(ws);  // a reused address must not inherit a stale pending resolve
     ROGTK_HIP_CHECK(hipMemsetAsync(ws, 0, (size_t)cl.total, as_stream(stream)));
     return ROGTK_OK;
 }
@@ -491,8 +492,14 @@ int rogtk_cluster_stats(const void* ws, int umi_len, int64_t max_distinct, int64
     if (int rc = cluster_layout(umi_len, max_distinct, &cl)) return rc;
     ROGTK_REQUIRE(ws && out4, ROGTK_E_INVALID, "stats: NULL buffer");
     hipStream_t s = as_stream(stream);
+    if (int rc = cluster_finish(ws, s)) return rc;
     ROGTK_HIP_CHECK(hipMemcpyAsync(out4, (const uint8_t*)ws + cl.off_stats, 32, hipMemcpyDeviceToHost, s));
     ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    return ROGTK_OK;
+}
+
+int rogtk_cluster_release(const void* ws) {
+    if (ws) cluster_release(ws);
     return ROGTK_OK;
 }
 

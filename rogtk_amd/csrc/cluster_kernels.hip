@@ -33,6 +33,10 @@
 //   roots   ballot root flags into an index-space bitmap; scan = dense cluster ids
 //   label   labelcode[D[i]] (L <= 13) or f[i] := dense id (index space)
 //   assign  cluster_id[row] = label(code[row])
+#include <algorithm>
+#include <map>
+#include <mutex>
+
 #include "rogtk_internal.h"
 
 namespace rogtk {
@@ -637,11 +641,72 @@ int launch_cluster_local_bitmap(const ClusterLayout& cl, uint8_t* ws, uint64_t* 
     return ROGTK_OK;
 }
 
+namespace {
+
+constexpr int kSpecRounds = 4;  // speculative global rounds (synth-v1 needs 3-4)
+
+// Host-side state of an in-flight resolve, keyed by workspace: the round flags are
+// copied asynchronously to pinned host memory so resolve never blocks the host;
+// assign (or rogtk_cluster_stats) checks them and only then, if the speculative
+// rounds were not enough, runs more rounds and relabels.
+struct ResolveState {
+    hipEvent_t ev = nullptr;
+    unsigned int* hflags = nullptr;  // pinned, kMaxRounds entries
+    int launched = 0;
+    bool pending = false;
+    ClusterLayout cl{};
+};
+std::mutex g_rs_mu;
+std::map<const void*, ResolveState> g_rs;
+
+int enqueue_rounds(const ClusterLayout& cl, const WsPtrs& p, int from, int to, hipStream_t s) {
+    const int pg = grid_for(cl.max_distinct, kPersistentGrid);
+    const int64_t tasks = (int64_t)(cl.L - kLocalPos) * (cl.words >> 2);
+    for (int k = from; k < to; ++k) {
+        hipLaunchKernelGGL(k_hook_g, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words, cl.L,
+                           kLocalPos, p.f, p.flags, k);
+        hipLaunchKernelGGL(k_jump, dim3(pg), dim3(kBlock), 0, s, p.f, cl.max_distinct, p.stats, p.flags, k);
+    }
+    ROGTK_HIP_CHECK(hipGetLastError());
+    return ROGTK_OK;
+}
+
+int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s) {
+    const int pg = grid_for(cl.max_distinct, kPersistentGrid);
+    {
+        ProfScope prof(K_FLATTEN, s);
+        hipLaunchKernelGGL(k_roots, dim3(pg), dim3(kBlock), 0, s, p.f, cl.max_distinct, p.rbits, p.stats);
+        hipLaunchKernelGGL(k_scan_words, dim3((unsigned)cl.rblocks), dim3(kBlock), 0, s, p.rbits, 1,
+                           cl.rwords, p.stats + S_NDISTINCT, (uint64_t*)nullptr, p.rpref, p.rblksum);
+        hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, p.rblksum, cl.rblocks, p.rblkoff,
+                           p.stats, (int)S_NCLUSTERS, -1);
+        ROGTK_HIP_CHECK(hipGetLastError());
+    }
+    {
+        ProfScope prof(K_LABEL, s);
+        hipLaunchKernelGGL(k_label, dim3(pg), dim3(kBlock), 0, s, p.f, p.D, p.rbits, p.rpref, p.rblkoff,
+                           p.labelcode, cl.max_distinct, p.stats);
+        ROGTK_HIP_CHECK(hipGetLastError());
+    }
+    return ROGTK_OK;
+}
+
+bool any_zero(const unsigned int* f, int from, int to) {
+    for (int k = from; k < to; ++k)
+        if (f[k] == 0) return true;
+    return false;
+}
+
+}  // namespace
+
 int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t* bitmaps,
                            int n_bitmaps, int max_distance, hipStream_t s) {
     WsPtrs p = ws_ptrs(cl, ws);
+    std::lock_guard<std::mutex> lk(g_rs_mu);
+    ResolveState& st = g_rs[ws];
+    st.pending = false;
+    st.cl = cl;
     ROGTK_HIP_CHECK(hipMemsetAsync(p.stats, 0, kStatsBytes, s));
-    const int pg = grid_for(cl.max_distinct, kPersistentGrid);
     {
         ProfScope prof(K_SCAN, s);
         hipLaunchKernelGGL(k_scan_words, dim3((unsigned)cl.blocks), dim3(kBlock), 0, s, bitmaps,
@@ -670,50 +735,68 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
                            p.f, p.UR, cl.max_distinct, p.stats);
         ROGTK_HIP_CHECK(hipGetLastError());
         if (cl.L > kLocalPos) {
-            const int64_t tasks = (int64_t)(cl.L - kLocalPos) * (cl.words >> 2);
-            bool converged = false;
-            unsigned int hflags[kRoundBatch];
-            for (int base = 0; base < kMaxRounds && !converged; base += kRoundBatch) {
-                for (int k = base; k < base + kRoundBatch; ++k) {
-                    hipLaunchKernelGGL(k_hook_g, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words,
-                                       cl.L, kLocalPos, p.f, p.flags, k);
-                    hipLaunchKernelGGL(k_jump, dim3(pg), dim3(kBlock), 0, s, p.f, cl.max_distinct, p.stats,
-                                       p.flags, k);
-                }
-                ROGTK_HIP_CHECK(hipGetLastError());
-                ROGTK_HIP_CHECK(hipMemcpyAsync(hflags, p.flags + base, sizeof(hflags), hipMemcpyDeviceToHost, s));
-                ROGTK_HIP_CHECK(hipStreamSynchronize(s));
-                for (int k = 0; k < kRoundBatch; ++k)
-                    if (hflags[k] == 0) {
-                        converged = true;
-                        break;
-                    }
+            if (int rc = enqueue_rounds(cl, p, 0, kSpecRounds, s)) return rc;
+            if (!st.ev) {
+                ROGTK_HIP_CHECK(hipEventCreateWithFlags(&st.ev, hipEventDisableTiming));
+                ROGTK_HIP_CHECK(hipHostMalloc((void**)&st.hflags, kMaxRounds * sizeof(unsigned int),
+                                              hipHostMallocDefault));
             }
-            ROGTK_REQUIRE(converged, ROGTK_E_HIP, "cluster: union rounds did not converge in %d rounds",
-                          kMaxRounds);
+            ROGTK_HIP_CHECK(hipMemcpyAsync(st.hflags, p.flags, kSpecRounds * sizeof(unsigned int),
+                                           hipMemcpyDeviceToHost, s));
+            ROGTK_HIP_CHECK(hipEventRecord(st.ev, s));
+            st.launched = kSpecRounds;
+            st.pending = true;
         }
     }
-    {
-        ProfScope prof(K_FLATTEN, s);
-        hipLaunchKernelGGL(k_roots, dim3(pg), dim3(kBlock), 0, s, p.f, cl.max_distinct, p.rbits, p.stats);
-        hipLaunchKernelGGL(k_scan_words, dim3((unsigned)cl.rblocks), dim3(kBlock), 0, s, p.rbits, 1,
-                           cl.rwords, p.stats + S_NDISTINCT, (uint64_t*)nullptr, p.rpref, p.rblksum);
-        hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, p.rblksum, cl.rblocks, p.rblkoff,
-                           p.stats, (int)S_NCLUSTERS, -1);
-        ROGTK_HIP_CHECK(hipGetLastError());
+    return enqueue_labels(cl, p, s);
+}
+
+int cluster_finish(const void* ws, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_rs_mu);
+    auto it = g_rs.find(ws);
+    if (it == g_rs.end() || !it->second.pending) return ROGTK_OK;
+    ResolveState& st = it->second;
+    ROGTK_HIP_CHECK(hipEventSynchronize(st.ev));
+    if (any_zero(st.hflags, 0, st.launched)) {
+        st.pending = false;
+        return ROGTK_OK;
     }
-    {
-        ProfScope prof(K_LABEL, s);
-        hipLaunchKernelGGL(k_label, dim3(pg), dim3(kBlock), 0, s, p.f, p.D, p.rbits, p.rpref, p.rblkoff,
-                           p.labelcode, cl.max_distinct, p.stats);
-        ROGTK_HIP_CHECK(hipGetLastError());
+    // the speculative rounds were not enough: continue synchronously, then relabel
+    WsPtrs p = ws_ptrs(st.cl, const_cast<uint8_t*>((const uint8_t*)ws));
+    bool converged = false;
+    while (!converged && st.launched < kMaxRounds) {
+        const int to = std::min(st.launched + kRoundBatch, kMaxRounds);
+        {
+            ProfScope prof(K_UNION, s);
+            if (int rc = enqueue_rounds(st.cl, p, st.launched, to, s)) return rc;
+        }
+        ROGTK_HIP_CHECK(hipMemcpyAsync(st.hflags + st.launched, p.flags + st.launched,
+                                       (to - st.launched) * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+        ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+        converged = any_zero(st.hflags, st.launched, to);
+        st.launched = to;
     }
-    return ROGTK_OK;
+    st.pending = false;
+    ROGTK_REQUIRE(converged, ROGTK_E_HIP, "cluster: union rounds did not converge in %d rounds", kMaxRounds);
+    return enqueue_labels(st.cl, p, s);
+}
+
+void cluster_release(const void* ws) {
+    std::lock_guard<std::mutex> lk(g_rs_mu);
+    auto it = g_rs.find(ws);
+    if (it == g_rs.end()) return;
+    if (it->second.ev) {
+        hipEventSynchronize(it->second.ev);
+        hipEventDestroy(it->second.ev);
+    }
+    if (it->second.hflags) hipHostFree(it->second.hflags);
+    g_rs.erase(it);
 }
 
 int launch_cluster_assign(const ClusterLayout& cl, const uint8_t* ws, const uint32_t* codes,
                           const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id,
                           hipStream_t s) {
+    if (int rc = cluster_finish(ws, s)) return rc;
     if (n <= 0) return ROGTK_OK;
     WsPtrs p = ws_ptrs(cl, const_cast<uint8_t*>(ws));
     ProfScope prof(K_ASSIGN, s);

@@ -143,6 +143,9 @@ int launch_cluster_local_bitmap(const ClusterLayout& cl, uint8_t* ws, uint64_t* 
                                 hipStream_t s);
 int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t* bitmaps,
                            int n_bitmaps, int max_distance, hipStream_t s);
+// Waits for an asynchronous resolve's round flags and completes it if needed.
+int cluster_finish(const void* ws, hipStream_t s);
+void cluster_release(const void* ws);
 int launch_cluster_assign(const ClusterLayout& cl, const uint8_t* ws, const uint32_t* codes,
                           const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id,
                           hipStream_t s);

@@ -127,6 +127,12 @@ class ClusterEngine:
         self.local_bitmap = torch.empty(self.words, dtype=torch.int64, device=device)
         _lib.call("rogtk_cluster_init", _p(self.ws), self.umi_len, self.max_distinct, _s(stream))
 
+    def __del__(self):
+        try:
+            _lib.call("rogtk_cluster_release", _p(self.ws))
+        except Exception:
+            pass
+
     @property
     def workspace_bytes(self) -> int:
         return self.ws.numel()

@@ -1,0 +1,89 @@
+"""Streaming pipeline over packed batches: three HIP streams, `depth` batches in flight.
+
+The hot path has three phases with different limits on MI355X:
+  main stream     k_score_packed (H1 scores + H2 Hamming + H3 presence mark) and
+                  the presence->bitmap pass: HBM-bandwidth bound
+  resolve stream  [RCCL all-gather of the bitmaps] + rank tables + LDS-local and
+                  global connected components: latency bound (small tables, many
+                  dependent steps)
+  assign stream   cluster_id[row] = label(code): random-gather bound
+Batch k's resolve overlaps batch k+1's scoring and batch k-1's assign, so a
+steady-state step costs max(phase) instead of the sum. Each slot owns its
+workspace and outputs; events order every cross-stream hand-off:
+  main(k)   waits assign(k - depth) (slot reuse)   -> records marked(k)
+  resolve(k) waits marked(k)                        -> records resolved(k)
+  assign(k)  waits resolved(k)                      -> records assigned(k)
+Resolve is enqueue-only (rogtk_cluster_resolve); assign completes a resolve whose
+speculative rounds were not enough, so results never depend on timing.
+"""
+from __future__ import annotations
+
+from collections import deque
+from typing import Optional
+
+import torch
+
+from . import device as D
+from .dist import gather_bitmaps
+
+
+class _Slot:
+    def __init__(self, umi_len, max_distinct, n_max, dev, with_scores):
+        self.eng = D.ClusterEngine(umi_len, max_distinct, dev)
+        self.scores = D.alloc_scores(n_max, dev) if with_scores else None
+        self.within = torch.empty(max((n_max + 63) // 64, 1), dtype=torch.int64, device=dev)
+        self.cid = torch.empty(max(n_max, 4), dtype=torch.int32, device=dev)
+        self.assigned: Optional[torch.cuda.Event] = None
+
+
+class UmiPipeline:
+    def __init__(self, umi_len: int, max_distinct: int, n_max: int, device=None, depth: int = 3,
+                 target: Optional[bytes] = b"ACGTACGTACGT", max_hamming: int = 1, max_distance: int = 1,
+                 group=None, with_scores: bool = True):
+        dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
+        self.group = group
+        self.slots = [_Slot(umi_len, max_distinct, n_max, dev, with_scores) for _ in range(depth)]
+        self.main = torch.cuda.current_stream(dev)
+        self.s_resolve = torch.cuda.Stream(dev)
+        self.s_assign = torch.cuda.Stream(dev)
+        self.queue = deque()
+        self.k = 0
+        self.last_assigned: Optional[torch.cuda.Event] = None
+
+    def submit(self, batch: D.PackedBatch):
+        """Enqueue one batch; returns its slot (outputs valid after drain() or a later event)."""
+        slot = self.slots[self.k % len(self.slots)]
+        if slot.assigned is not None:
+            self.main.wait_event(slot.assigned)
+        D.score_packed(batch, slot.scores, self.target, self.max_hamming, None, slot.within,
+                       cluster=slot.eng, stream=self.main)
+        slot.eng.build_local_bitmap(stream=self.main)
+        marked = torch.cuda.Event()
+        marked.record(self.main)
+        with torch.cuda.stream(self.s_resolve):
+            self.s_resolve.wait_event(marked)
+            bitmaps, nb = gather_bitmaps(slot.eng.local_bitmap, self.group)
+            slot.eng.resolve(bitmaps, nb, self.max_distance, stream=self.s_resolve)
+            resolved = torch.cuda.Event()
+            resolved.record(self.s_resolve)
+        self.queue.append((slot, batch, resolved))
+        while len(self.queue) > 1:  # assign lags resolve by one batch
+            self._assign_oldest()
+        self.k += 1
+        return slot
+
+    def _assign_oldest(self):
+        slot, batch, resolved = self.queue.popleft()
+        self.s_assign.wait_event(resolved)
+        slot.eng.assign(batch, slot.cid, stream=self.s_assign)
+        slot.assigned = torch.cuda.Event()
+        slot.assigned.record(self.s_assign)
+        self.last_assigned = slot.assigned
+
+    def drain(self):
+        """Finish every submitted batch; the main stream waits for the last assign."""
+        while self.queue:
+            self._assign_oldest()
+        if self.last_assigned is not None:
+            self.main.wait_event(self.last_assigned)

@@ -335,3 +335,78 @@ def test_full_size_c2_properties(rg):
     assert np.array_equal(cid2.cpu().numpy(), cid.cpu().numpy())
     assert np.array_equal(scores2["combined_score"][:n].cpu().numpy().view(np.uint64),
                           scores["combined_score"][:n].cpu().numpy().view(np.uint64))
+
+
+@pytest.mark.parametrize("depth,nb", [(4, 4), (2, 5), (1, 3)])
+def test_streaming_pipeline_matches_sequential(rg, depth, nb):
+    """rogtk_amd.pipeline (3 streams, `depth` batches in flight) == the sequential device path."""
+    import torch
+
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+    from rogtk_amd.pipeline import UmiPipeline
+
+    n, L = 300_001, 12
+    seeds = [synth.DEFAULT_SEED + 17 * k for k in range(nb)]
+    pipe = UmiPipeline(L, n, n, "cuda", depth=depth, target=b"ACGTACGTACGT", max_distance=1)
+    keep = []
+    for s in seeds:
+        codes = torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda()
+        keep.append(D.PackedBatch(codes, L))
+        pipe.submit(keep[-1])
+    pipe.drain()
+    torch.cuda.synchronize()
+    for k in range(nb - depth, nb):
+        slot = pipe.slots[k % depth]
+        _, scores, _, hw, cid, _ = _device_run(n, seed=seeds[k])
+        assert np.array_equal(slot.cid[:n].cpu().numpy(), cid.cpu().numpy()), k
+        assert np.array_equal(slot.within.cpu().numpy(), hw.cpu().numpy()), k
+        for f in ("combined_score", "dust_score", "longest_homopolymer_run"):
+            assert np.array_equal(slot.scores[f][:n].cpu().numpy(), scores[f][:n].cpu().numpy()), (k, f)
+
+
+def _chain_codes(rng, L, length, high_bases):
+    """Self-avoiding walk that changes one of the first `high_bases` bases per step (low bases
+    fixed): every edge crosses LDS-local groups, so the global rounds carry the whole merge."""
+    shift0 = 2 * (L - high_bases)
+    low = int(rng.integers(1 << shift0))
+    cur = int(rng.integers(4 ** high_bases))
+    seen, path = {cur}, [cur]
+    while len(path) < length:
+        for _ in range(64):
+            j = int(rng.integers(high_bases))
+            b = int(rng.integers(1, 4))
+            nxt = cur ^ (b << (2 * j))
+            if nxt not in seen:
+                break
+        else:
+            break
+        seen.add(nxt)
+        path.append(nxt)
+        cur = nxt
+    return np.array([(c << shift0) | low for c in path], dtype=np.uint32)
+
+
+@pytest.mark.parametrize("L", [12, 16])
+def test_long_chains_need_extra_rounds(rg, L):
+    """Long Hamming-1 paths (diameter >> speculative rounds) resolve exactly: the deferred
+    completion in assign must finish them."""
+    import torch
+
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+
+    rng = np.random.default_rng(L)
+    parts = [_chain_codes(rng, L, 3000, min(L - 7, 8)) for _ in range(4)]
+    codes_h = np.unique(np.concatenate(parts))
+    codes_h = codes_h[rng.permutation(len(codes_h))]
+    n = len(codes_h)
+    codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
+    batch = D.PackedBatch(codes, L)
+    eng = D.ClusterEngine(L, n, "cuda")
+    cid = torch.empty(n, dtype=torch.int32, device="cuda")
+    D.cluster_batch(eng, batch, cid, 1)
+    stats = eng.stats()
+    rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L)), L, 1)
+    assert stats["n_clusters"] == rk
+    assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc)
