@@ -53,7 +53,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip in-run HIP-event kernel timing")
-    ap.add_argument("--depth", type=int, default=3, help="batches in flight (1 = no cross-batch overlap)")
+    ap.add_argument("--depth", type=int, default=1, help="batches in flight (1 = no cross-batch overlap)")
+    ap.add_argument("--prio", type=str, default="0,0,0", help="stream priorities main,resolve,assign (-1 = high)")
     return ap.parse_args()
 
 
@@ -121,7 +122,8 @@ def main():
     codes = torch.from_numpy(codes_h.view(np.int32)).to(dev)
     batch = D.PackedBatch(codes, L)
     pipe = UmiPipeline(L, min(n_total, 4 ** L), count, dev, depth=args.depth, target=TARGET,
-                       max_distance=md, group=None)
+                       max_distance=md, group=None,
+                       priorities=tuple(int(x) for x in args.prio.split(",")))
 
     def step():
         pipe.submit(batch)

@@ -39,14 +39,17 @@ class _Slot:
 class UmiPipeline:
     def __init__(self, umi_len: int, max_distinct: int, n_max: int, device=None, depth: int = 3,
                  target: Optional[bytes] = b"ACGTACGTACGT", max_hamming: int = 1, max_distance: int = 1,
-                 group=None, with_scores: bool = True):
+                 group=None, with_scores: bool = True, priorities=(0, 0, 0)):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
         self.slots = [_Slot(umi_len, max_distinct, n_max, dev, with_scores) for _ in range(depth)]
-        self.main = torch.cuda.current_stream(dev)
-        self.s_resolve = torch.cuda.Stream(dev)
-        self.s_assign = torch.cuda.Stream(dev)
+        # priorities: (main, resolve, assign); lower = higher priority (torch convention)
+        self.caller = torch.cuda.current_stream(dev)
+        self.main = torch.cuda.Stream(dev, priority=priorities[0])
+        self.main.wait_stream(self.caller)
+        self.s_resolve = torch.cuda.Stream(dev, priority=priorities[1])
+        self.s_assign = torch.cuda.Stream(dev, priority=priorities[2])
         self.queue = deque()
         self.k = 0
         self.last_assigned: Optional[torch.cuda.Event] = None
@@ -54,6 +57,7 @@ class UmiPipeline:
     def submit(self, batch: D.PackedBatch):
         """Enqueue one batch; returns its slot (outputs valid after drain() or a later event)."""
         slot = self.slots[self.k % len(self.slots)]
+        self.main.wait_stream(torch.cuda.current_stream(self.main.device))  # batch producer -> main
         if slot.assigned is not None:
             self.main.wait_event(slot.assigned)
         D.score_packed(batch, slot.scores, self.target, self.max_hamming, None, slot.within,
@@ -87,3 +91,4 @@ class UmiPipeline:
             self._assign_oldest()
         if self.last_assigned is not None:
             self.main.wait_event(self.last_assigned)
+        torch.cuda.current_stream(self.main.device).wait_stream(self.main)
