@@ -53,7 +53,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip in-run HIP-event kernel timing")
-    ap.add_argument("--depth", type=int, default=1, help="batches in flight (1 = no cross-batch overlap)")
+    ap.add_argument("--iso-launches", type=int, default=10, help="isolated score-kernel launches after timing")
+    ap.add_argument("--depth", type=int, default=3, help="batches in flight (1 = no cross-batch overlap)")
+    ap.add_argument("--mark", choices=("xcd", "fused"), default="xcd",
+                    help="H3 presence mark: XCD-partitioned kernel or fused into k_score_packed")
     ap.add_argument("--prio", type=str, default="0,0,0", help="stream priorities main,resolve,assign (-1 = high)")
     return ap.parse_args()
 
@@ -123,7 +126,7 @@ def main():
     batch = D.PackedBatch(codes, L)
     pipe = UmiPipeline(L, min(n_total, 4 ** L), count, dev, depth=args.depth, target=TARGET,
                        max_distance=md, group=None,
-                       priorities=tuple(int(x) for x in args.prio.split(",")))
+                       priorities=tuple(int(x) for x in args.prio.split(",")), mark=args.mark)
 
     def step():
         pipe.submit(batch)
@@ -144,21 +147,35 @@ def main():
     torch.cuda.synchronize()
     barrier(world)
     el = time.perf_counter() - t0
+    kernels = {}
     if not args.no_profile:
         D.profile_enable(False)
+        for k in ("score_packed", "cluster_mark", "cluster_bitmap", "cluster_scan", "cluster_compact", "cluster_union",
+                  "cluster_flatten", "cluster_label", "cluster_assign"):
+            ms, launches = D.profile_read(k)
+            if launches:
+                kernels[k] = {"avg_us": 1000.0 * ms / launches, "launches": launches}
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     stats = pipe.slots[0].eng.stats()
 
-    kernels = {}
+    # Outside the timed region: the same score kernel launched alone (nothing else on
+    # the GPU), so its duration is the kernel's own, not the pipeline-shared one.
+    iso = None
     if not args.no_profile:
-        for k in ("score_packed", "cluster_bitmap", "cluster_scan", "cluster_compact", "cluster_union",
-                  "cluster_flatten", "cluster_label", "cluster_assign"):
-            ms, launches = D.profile_read(k)
-            if launches:
-                kernels[k] = {"avg_us": 1000.0 * ms / launches, "launches": launches}
+        slot = pipe.slots[0]
+        torch.cuda.synchronize()
+        D.profile_reset()
+        D.profile_enable(True)
+        for _ in range(args.iso_launches):
+            D.score_packed(batch, slot.scores, TARGET, 1, None, slot.within)
+        torch.cuda.synchronize()
+        D.profile_enable(False)
+        ms, launches = D.profile_read("score_packed")
+        if launches:
+            iso = 1000.0 * ms / launches
 
     if rank != 0:
         if world > 1:
@@ -177,7 +194,14 @@ def main():
         roof = {"kernel": "k_score_packed", "bound": "hbm", "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "traffic_source": src,
-                "algorithmic_bytes_per_launch": int(count * bpr), "bytes_per_read": bpr}
+                "algorithmic_bytes_per_launch": int(count * bpr), "bytes_per_read": bpr,
+                "measured_over": f"timed region, {args.depth} batches in flight (kernel shares the GPU with "
+                                 f"mark/resolve/assign of neighbouring batches)"}
+        if iso:
+            a_iso = count * bpr / (iso * 1e-6) / 1e9
+            roof["isolated"] = {"avg_us": round(iso, 2), "achieved": round(a_iso, 1),
+                                "frac": round(a_iso / HBM_PEAK_GBS, 4), "launches": args.iso_launches,
+                                "note": "same kernel, same batch, launched alone after the timed region"}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(codes_h, L, md, args.cpu_seconds)

@@ -450,8 +450,12 @@ int rogtk_cluster_init(void* ws, int umi_len, int64_t max_distinct, void* stream
 int rogtk_cluster_mark(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
                        void* ws, int64_t max_distinct, void* stream) {
     ROGTK_REQUIRE(ws, ROGTK_E_INVALID, "ws is NULL");
-    return rogtk_umi_score_packed(codes, regular_bits, n, umi_len, nullptr, nullptr, 0, 0, nullptr,
-                                  nullptr, ws, max_distinct, stream);
+    ClusterLayout cl;
+    if (int rc = cluster_layout(umi_len, max_distinct, &cl)) return rc;
+    ROGTK_REQUIRE(n >= 0 && (n == 0 || codes), ROGTK_E_INVALID, "mark: bad codes/n");
+    ROGTK_REQUIRE(aligned16(codes), ROGTK_E_INVALID, "mark: codes must be 16-byte aligned");
+    return launch_cluster_mark(codes, regular_bits, n, umi_len, (uint8_t*)ws + cl.off_presence,
+                               as_stream(stream));
 }
 
 int rogtk_cluster_local_bitmap(void* ws, int umi_len, int64_t max_distinct, uint64_t* bitmap_out,

@@ -43,6 +43,8 @@ namespace rogtk {
 namespace {
 
 constexpr int kBlock = 256;
+constexpr int kMarkParts = 8;     // XCD partitions of the code space (mark)
+constexpr int kMarkChunks = 256;  // row chunks of the XCD-partitioned kernels; grid = 8 * chunks
 constexpr int kScanWords = 1024;  // words per scan block (4 per thread)
 constexpr int kMaxRounds = 64;
 constexpr int kRoundBatch = 4;
@@ -507,7 +509,7 @@ __global__ __launch_bounds__(kBlock) void k_label(uint32_t* __restrict__ f, cons
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nd; i += (int64_t)gridDim.x * kBlock) {
         const uint32_t lab = root_label(f[i], rbits, rpref, rblkoff);
         if (labelcode) labelcode[D[i]] = lab;
-        else f[i] = lab;
+        f[i] = lab;  // in place: lane i only ever reads its own f[i]
     }
 }
 
@@ -625,6 +627,52 @@ int cluster_layout(int L, int64_t max_distinct, ClusterLayout* o) {
     c.off_labelcode = c.label_by_code ? take((int64_t)c.nbits * 4) : off;
     c.total = off;
     *o = c;
+    return ROGTK_OK;
+}
+
+// ------------------------------------------------------------------ mark
+// presence[code] = 1 for every regular row, partitioned by XCD: block b marks only
+// the codes of partition b % 8 (code range [p, p+1) * 4^L / 8) from its chunk of
+// rows. Under the observed round-robin placement blocks b and b + 8 share an XCD,
+// so each XCD's scattered byte stores land in its own 1/8 of the table (2 MB at
+// L = 12), which stays resident in that XCD's 4 MB L2 until the kernel ends; the
+// 8x re-read of the codes is served by the Infinity Cache. Placement only affects
+// speed: every (partition, chunk) pair is handled by exactly one block.
+
+__global__ __launch_bounds__(kBlock) void k_mark_xcd(const uint32_t* __restrict__ codes,
+                                                      const uint64_t* __restrict__ regbits, int64_t n,
+                                                      int two_l, int64_t chunk, uint8_t* __restrict__ pres) {
+    const uint32_t part = blockIdx.x % kMarkParts;
+    const int64_t c0 = (int64_t)(blockIdx.x / kMarkParts) * chunk;
+    const int64_t c1 = c0 + chunk < n ? c0 + chunk : n;
+    for (int64_t r = c0 + 4 * (int64_t)threadIdx.x; r < c1; r += 4 * kBlock) {
+        uint32_t c[4];
+        uint32_t reg = regbits ? (uint32_t)(regbits[r >> 6] >> (r & 63)) & 0xFu : 0xFu;
+        if (r + 4 <= n) {
+            const uint4 v = *reinterpret_cast<const uint4*>(codes + r);
+            c[0] = v.x; c[1] = v.y; c[2] = v.z; c[3] = v.w;
+        } else {
+            reg &= (1u << (uint32_t)(n - r)) - 1u;
+            for (int k = 0; k < 4; ++k) c[k] = r + k < n ? codes[r + k] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (((reg >> k) & 1u) && (uint32_t)(((uint64_t)c[k] * kMarkParts) >> two_l) == part)
+                pres[c[k]] = 1;  // benign same-value race
+    }
+}
+
+int launch_cluster_mark(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int L,
+                        uint8_t* presence, hipStream_t s) {
+    if (n <= 0) return ROGTK_OK;
+    ProfScope prof(K_MARK, s);
+    // chunk: a multiple of 4 * kBlock rows (keeps r 4-aligned for the uint4 loads)
+    int64_t chunk = (n + kMarkChunks - 1) / kMarkChunks;
+    chunk = (chunk + 4 * kBlock - 1) / (4 * kBlock) * (4 * kBlock);
+    const int64_t chunks = (n + chunk - 1) / chunk;
+    hipLaunchKernelGGL(k_mark_xcd, dim3((unsigned)(chunks * kMarkParts)), dim3(kBlock), 0, s, codes, regular_bits,
+                       n, 2 * L, chunk, presence);
+    ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
 }
 

@@ -137,7 +137,8 @@ struct ClusterLayout {
 };
 int cluster_layout(int L, int64_t max_distinct, ClusterLayout* out);
 
-int launch_cluster_mark(const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
+// XCD-partitioned presence mark (standalone; k_score_packed<..., MARK> is the fused form).
+int launch_cluster_mark(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int L,
                         uint8_t* presence, hipStream_t s);
 int launch_cluster_local_bitmap(const ClusterLayout& cl, uint8_t* ws, uint64_t* bitmap_out,
                                 hipStream_t s);

@@ -186,25 +186,35 @@ __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restr
         __syncthreads();
     }
     const int L = P.L;
-    const int64_t row0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * kRowsPerLane;
-    const bool full = row0 + kRowsPerLane <= n;
+    // Wave tile of 256 rows; lane l owns rows {2l, 2l+1, 128+2l, 129+2l} so that every
+    // 16-B (double2) store instruction of the wave writes 1 KB of contiguous output.
+    const int lane = threadIdx.x & 63;
+    const int64_t base = ((int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63)) * kRowsPerLane;
+    const int64_t rA = base + 2 * lane, rB = rA + 128;
+    const bool full = base + 64 * kRowsPerLane <= n;
 
     uint32_t c[kRowsPerLane] = {0, 0, 0, 0};
     uint32_t reg = 0;
-    if (row0 < n) {
-        if (full) {
-            const uint4 v = *reinterpret_cast<const uint4*>(codes + row0);
-            c[0] = v.x; c[1] = v.y; c[2] = v.z; c[3] = v.w;
-        } else {
-            for (int k = 0; k < kRowsPerLane; ++k)
-                if (row0 + k < n) c[k] = codes[row0 + k];
+    if (full) {
+        const uint2 va = *reinterpret_cast<const uint2*>(codes + rA);
+        const uint2 vb = *reinterpret_cast<const uint2*>(codes + rB);
+        c[0] = va.x; c[1] = va.y; c[2] = vb.x; c[3] = vb.y;
+        reg = regbits ? ((uint32_t)(regbits[rA >> 6] >> (rA & 63)) & 3u) |
+                            (((uint32_t)(regbits[rB >> 6] >> (rB & 63)) & 3u) << 2)
+                      : 0xFu;
+    } else {
+        const int64_t rr[4] = {rA, rA + 1, rB, rB + 1};
+#pragma unroll
+        for (int k = 0; k < kRowsPerLane; ++k) {
+            if (rr[k] < n) {
+                c[k] = codes[rr[k]];
+                if (!regbits || ((regbits[rr[k] >> 6] >> (rr[k] & 63)) & 1u)) reg |= 1u << k;
+            }
         }
-        reg = regbits ? (uint32_t)(regbits[row0 >> 6] >> (row0 & 63)) & 0xFu : 0xFu;
-        if (!full) reg &= (1u << (uint32_t)(n - row0)) - 1u;
     }
 
     uint32_t wnib = 0;
-    if (row0 < n) {
+    if (rA < n) {
         if (SCORE) {
             double sh[4], li[4], ho[4], di[4], du[4], co[4];
             uint32_t lg[4];
@@ -223,23 +233,27 @@ __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restr
             if (full) {
                 auto st2 = [&](double* p, const double* v) {
                     if (!p) return;
-                    reinterpret_cast<double2*>(p + row0)[0] = make_double2(v[0], v[1]);
-                    reinterpret_cast<double2*>(p + row0)[1] = make_double2(v[2], v[3]);
+                    *reinterpret_cast<double2*>(p + rA) = make_double2(v[0], v[1]);
+                    *reinterpret_cast<double2*>(p + rB) = make_double2(v[2], v[3]);
                 };
                 st2(O.sh, sh); st2(O.ling, li); st2(O.homo, ho); st2(O.di, di);
                 st2(O.dust, du); st2(O.comb, co);
-                if (O.longest)
-                    *reinterpret_cast<uint4*>(O.longest + row0) = make_uint4(lg[0], lg[1], lg[2], lg[3]);
+                if (O.longest) {
+                    *reinterpret_cast<uint2*>(O.longest + rA) = make_uint2(lg[0], lg[1]);
+                    *reinterpret_cast<uint2*>(O.longest + rB) = make_uint2(lg[2], lg[3]);
+                }
             } else {
+                const int64_t rr[4] = {rA, rA + 1, rB, rB + 1};
                 for (int k = 0; k < kRowsPerLane; ++k) {
-                    if (row0 + k >= n) break;
-                    if (O.sh) O.sh[row0 + k] = sh[k];
-                    if (O.ling) O.ling[row0 + k] = li[k];
-                    if (O.homo) O.homo[row0 + k] = ho[k];
-                    if (O.di) O.di[row0 + k] = di[k];
-                    if (O.dust) O.dust[row0 + k] = du[k];
-                    if (O.comb) O.comb[row0 + k] = co[k];
-                    if (O.longest) O.longest[row0 + k] = lg[k];
+                    const int64_t r = rr[k];
+                    if (r >= n) continue;
+                    if (O.sh) O.sh[r] = sh[k];
+                    if (O.ling) O.ling[r] = li[k];
+                    if (O.homo) O.homo[r] = ho[k];
+                    if (O.di) O.di[r] = di[k];
+                    if (O.dust) O.dust[r] = du[k];
+                    if (O.comb) O.comb[r] = co[k];
+                    if (O.longest) O.longest[r] = lg[k];
                 }
             }
         }
@@ -255,10 +269,12 @@ __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restr
             }
             if (HAMD) {
                 if (full) {
-                    *reinterpret_cast<uint4*>(hd + row0) = make_uint4(d[0], d[1], d[2], d[3]);
+                    *reinterpret_cast<uint2*>(hd + rA) = make_uint2(d[0], d[1]);
+                    *reinterpret_cast<uint2*>(hd + rB) = make_uint2(d[2], d[3]);
                 } else {
+                    const int64_t rr[4] = {rA, rA + 1, rB, rB + 1};
                     for (int k = 0; k < kRowsPerLane; ++k)
-                        if (row0 + k < n) hd[row0 + k] = d[k];
+                        if (rr[k] < n) hd[rr[k]] = d[k];
                 }
             }
         }
@@ -269,13 +285,21 @@ __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restr
         }
     }
     if (HAMW) {
-        // 16 lanes x 4 rows = one 64-row word (LSB = first row): OR-reduce in-wave.
-        uint64_t w = (uint64_t)wnib << (4 * (threadIdx.x & 15));
-        w |= __shfl_xor(w, 1);
-        w |= __shfl_xor(w, 2);
-        w |= __shfl_xor(w, 4);
-        w |= __shfl_xor(w, 8);
-        if ((threadIdx.x & 15) == 0 && row0 < n) hw[row0 >> 6] = w;
+        // 32 lanes x 2 rows = one 64-row word (LSB = first row): OR-reduce per half-wave.
+        // Lanes 0..31 hold words 0 (rows 0..63) and 2 (rows 128..191) of the tile,
+        // lanes 32..63 words 1 and 3.
+        uint64_t w01 = (uint64_t)(wnib & 3u) << (2 * (lane & 31));
+        uint64_t w23 = (uint64_t)((wnib >> 2) & 3u) << (2 * (lane & 31));
+#pragma unroll
+        for (int m = 1; m < 32; m <<= 1) {
+            w01 |= __shfl_xor(w01, m);
+            w23 |= __shfl_xor(w23, m);
+        }
+        if ((lane & 31) == 0) {
+            const int64_t wa = (base >> 6) + (lane >> 5), wb = wa + 2;
+            if (wa * 64 < n) hw[wa] = w01;
+            if (wb * 64 < n) hw[wb] = w23;
+        }
     }
 }
 

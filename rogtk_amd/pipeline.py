@@ -1,8 +1,9 @@
 """Streaming pipeline over packed batches: three HIP streams, `depth` batches in flight.
 
 The hot path has three phases with different limits on MI355X:
-  main stream     k_score_packed (H1 scores + H2 Hamming + H3 presence mark) and
-                  the presence->bitmap pass: HBM-bandwidth bound
+  main stream     k_score_packed (H1 scores + H2 Hamming), the XCD-partitioned
+                  presence mark (or the mark fused into k_score_packed) and the
+                  presence->bitmap pass: HBM-bandwidth bound
   resolve stream  [RCCL all-gather of the bitmaps] + rank tables + LDS-local and
                   global connected components: latency bound (small tables, many
                   dependent steps)
@@ -39,10 +40,14 @@ class _Slot:
 class UmiPipeline:
     def __init__(self, umi_len: int, max_distinct: int, n_max: int, device=None, depth: int = 3,
                  target: Optional[bytes] = b"ACGTACGTACGT", max_hamming: int = 1, max_distance: int = 1,
-                 group=None, with_scores: bool = True, priorities=(0, 0, 0)):
+                 group=None, with_scores: bool = True, priorities=(0, 0, 0), mark: str = "xcd",
+                 on_assigned=None):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
+        if mark not in ("xcd", "fused"):
+            raise ValueError("mark must be 'xcd' (XCD-partitioned mark kernel) or 'fused' (inside k_score_packed)")
+        self.fused_mark = mark == "fused"
         self.slots = [_Slot(umi_len, max_distinct, n_max, dev, with_scores) for _ in range(depth)]
         # priorities: (main, resolve, assign); lower = higher priority (torch convention)
         self.caller = torch.cuda.current_stream(dev)
@@ -51,6 +56,12 @@ class UmiPipeline:
         self.s_resolve = torch.cuda.Stream(dev, priority=priorities[1])
         self.s_assign = torch.cuda.Stream(dev, priority=priorities[2])
         self.queue = deque()
+        # assign lags resolve by one batch only when a second slot exists: with one
+        # slot the next batch's resolve would overwrite the tables assign reads
+        self.lag = 1 if depth > 1 else 0
+        # on_assigned(slot, batch): called with the assign stream current, after the
+        # batch's assign and before its slot may be reused (e.g. to copy outputs out)
+        self.on_assigned = on_assigned
         self.k = 0
         self.last_assigned: Optional[torch.cuda.Event] = None
 
@@ -61,7 +72,9 @@ class UmiPipeline:
         if slot.assigned is not None:
             self.main.wait_event(slot.assigned)
         D.score_packed(batch, slot.scores, self.target, self.max_hamming, None, slot.within,
-                       cluster=slot.eng, stream=self.main)
+                       cluster=slot.eng if self.fused_mark else None, stream=self.main)
+        if not self.fused_mark:
+            slot.eng.mark(batch, stream=self.main)
         slot.eng.build_local_bitmap(stream=self.main)
         marked = torch.cuda.Event()
         marked.record(self.main)
@@ -72,7 +85,7 @@ class UmiPipeline:
             resolved = torch.cuda.Event()
             resolved.record(self.s_resolve)
         self.queue.append((slot, batch, resolved))
-        while len(self.queue) > 1:  # assign lags resolve by one batch
+        while len(self.queue) > self.lag:
             self._assign_oldest()
         self.k += 1
         return slot
@@ -81,6 +94,9 @@ class UmiPipeline:
         slot, batch, resolved = self.queue.popleft()
         self.s_assign.wait_event(resolved)
         slot.eng.assign(batch, slot.cid, stream=self.s_assign)
+        if self.on_assigned is not None:
+            with torch.cuda.stream(self.s_assign):
+                self.on_assigned(slot, batch)
         slot.assigned = torch.cuda.Event()
         slot.assigned.record(self.s_assign)
         self.last_assigned = slot.assigned

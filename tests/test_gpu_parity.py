@@ -337,9 +337,11 @@ def test_full_size_c2_properties(rg):
                           scores["combined_score"][:n].cpu().numpy().view(np.uint64))
 
 
-@pytest.mark.parametrize("depth,nb", [(4, 4), (2, 5), (1, 3)])
-def test_streaming_pipeline_matches_sequential(rg, depth, nb):
-    """rogtk_amd.pipeline (3 streams, `depth` batches in flight) == the sequential device path."""
+@pytest.mark.parametrize("depth,nb", [(4, 4), (2, 5), (1, 3), (3, 7)])
+@pytest.mark.parametrize("mark", ["xcd", "fused"])
+def test_streaming_pipeline_matches_sequential(rg, depth, nb, mark):
+    """rogtk_amd.pipeline (3 streams, `depth` batches in flight) == the sequential device
+    path for EVERY batch (outputs copied out by the on_assigned hook before slot reuse)."""
     import torch
 
     from rogtk_amd import device as D
@@ -348,7 +350,14 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb):
 
     n, L = 300_001, 12
     seeds = [synth.DEFAULT_SEED + 17 * k for k in range(nb)]
-    pipe = UmiPipeline(L, n, n, "cuda", depth=depth, target=b"ACGTACGTACGT", max_distance=1)
+    outs = []
+
+    def grab(slot, batch):
+        outs.append((slot.cid[:n].clone(), slot.within.clone(), slot.scores["combined_score"][:n].clone(),
+                     slot.scores["longest_homopolymer_run"][:n].clone()))
+
+    pipe = UmiPipeline(L, n, n, "cuda", depth=depth, target=b"ACGTACGTACGT", max_distance=1, mark=mark,
+                       on_assigned=grab)
     keep = []
     for s in seeds:
         codes = torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda()
@@ -356,13 +365,14 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb):
         pipe.submit(keep[-1])
     pipe.drain()
     torch.cuda.synchronize()
-    for k in range(nb - depth, nb):
-        slot = pipe.slots[k % depth]
+    assert len(outs) == nb
+    for k in range(nb):
         _, scores, _, hw, cid, _ = _device_run(n, seed=seeds[k])
-        assert np.array_equal(slot.cid[:n].cpu().numpy(), cid.cpu().numpy()), k
-        assert np.array_equal(slot.within.cpu().numpy(), hw.cpu().numpy()), k
-        for f in ("combined_score", "dust_score", "longest_homopolymer_run"):
-            assert np.array_equal(slot.scores[f][:n].cpu().numpy(), scores[f][:n].cpu().numpy()), (k, f)
+        g_cid, g_w, g_comb, g_long = (t.cpu().numpy() for t in outs[k])
+        assert np.array_equal(g_cid, cid.cpu().numpy()), k
+        assert np.array_equal(g_w, hw.cpu().numpy()), k
+        assert np.array_equal(g_comb.view(np.uint64), scores["combined_score"][:n].cpu().numpy().view(np.uint64)), k
+        assert np.array_equal(g_long, scores["longest_homopolymer_run"][:n].cpu().numpy()), k
 
 
 def _chain_codes(rng, L, length, high_bases):

@@ -5,7 +5,11 @@ profiles/<tag>_pmc.json           per-kernel HBM traffic from separate FETCH_SIZ
                                   WRITE_SIZE passes, corrected as MI355X_MICROARCH.md
                                   prescribes (units KB; gfx950 FETCH_SIZE x2 for wide
                                   streaming reads), per launch
-Usage: python tools/summarize_profiles.py <tag> [reads_per_launch]
+profiles/<tag>_score_split.json   k_score_packed dispatch durations from the trace, split into
+                                  the bench's phases (warmup+timed pipeline vs the isolated
+                                  launches after the timed region) so they can be compared with
+                                  the bench line's roofline.avg and roofline.isolated
+Usage: python tools/summarize_profiles.py <tag> [reads_per_launch] [isolated_launches]
 """
 import csv
 import json
@@ -35,6 +39,7 @@ def counters(kind, counter):
 def main():
     tag = sys.argv[1]
     reads = int(sys.argv[2]) if len(sys.argv) > 2 else 10_000_000
+    n_iso = int(sys.argv[3]) if len(sys.argv) > 3 else 10
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     shutil.copy(os.path.join(SRC, "trace", "run_kernel_stats.csv"),
                 os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
@@ -62,6 +67,19 @@ def main():
     if sp:
         out["score_packed_hbm_bytes_per_launch"] = kernels[sp[0]]["hbm_bytes"]
         out["score_packed_bytes_per_read"] = round(kernels[sp[0]]["hbm_bytes"] / reads, 2)
+    tr = [r for r in csv.DictReader(open(os.path.join(SRC, "trace", "run_kernel_trace.csv")))
+          if short(r["Kernel_Name"]).startswith("k_score_packed")]
+    tr.sort(key=lambda r: int(r["Start_Timestamp"]))
+    d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0 for r in tr]
+    if d:
+        pipe, iso = d[:-n_iso] if len(d) > n_iso else d, d[-n_iso:] if len(d) > n_iso else []
+        split = {"kernel": short(tr[0]["Kernel_Name"]), "dispatches": len(d),
+                 "pipeline_avg_us": round(sum(pipe) / len(pipe), 2), "pipeline_dispatches": len(pipe),
+                 "isolated_avg_us": round(sum(iso) / len(iso), 2) if iso else None, "isolated_dispatches": len(iso),
+                 "all_avg_us": round(sum(d) / len(d), 2)}
+        with open(os.path.join(ROOT, "profiles", f"{tag}_score_split.json"), "w") as f:
+            json.dump(split, f, indent=1)
+        print(json.dumps(split))
     with open(os.path.join(ROOT, "profiles", f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1)[:3000])
