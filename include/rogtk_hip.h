@@ -185,6 +185,31 @@ int rogtk_umi_cluster_host(const void* offsets, int offset_width, const uint8_t*
                            int64_t n, int umi_len, int max_distance, uint32_t* cluster_id,
                            int64_t* n_clusters, int* resolved_umi_len);
 
+/* ================ H4: k-mer spectra of read groups (host buffers) ================
+ * Replaces, per polars group (group_by(...).agg), the k-mer front end of fracture
+ * assembly: expressions.rs:739-744 (nulls skipped), fracture.rs:200-256 (auto_k via
+ * estimate_k, k > 64 -> nothing, uppercase, drop sequences with a non-ACGT byte,
+ * effective k = 4/8/16/32/64) and fracture.rs:105-146 (debruijn 0.3.4
+ * filter_kmers + CountFilter(min_coverage) + remove_censored_exts, stranded; node /
+ * terminal / isolated counts). Spec: oracle/kmer_oracle.cpp.
+ * Groups are contiguous row ranges: group_offsets[0] = 0 ... group_offsets[n_groups]
+ * = n_rows (NULL / 0 groups = one group of all rows).
+ * Output, per group in group order (entry_offsets[n_groups + 1]): its valid k-mers
+ * in ascending order (the crate's pre-MPHF order; its MPHF order is not
+ * reproducible), kmers[2 i] = high 64 bits (k_eff = 64 only), kmers[2 i + 1] = low
+ * 64 bits (2-bit codes, first base most significant, A0 C1 G2 T3); exts[i] = the
+ * censored Exts byte (low nibble left bases, high nibble right); counts[i] =
+ * occurrences (u16, saturating). group_stats[5 g ..] = {k_eff (0 when k > 64),
+ * n_sequences, node_count, terminal_count, isolated_count}.
+ * capacity >= rogtk_kmer_capacity() always suffices (ROGTK_E_OVERFLOW otherwise). */
+int rogtk_kmer_capacity(const void* offsets, int offset_width, int64_t n_rows, int64_t* capacity);
+int rogtk_kmer_spectrum_host(const void* offsets, int offset_width, const uint8_t* values,
+                             int64_t values_len, const uint8_t* validity, int64_t validity_offset,
+                             int64_t n_rows, const int64_t* group_offsets, int64_t n_groups, int k,
+                             int auto_k, int64_t min_coverage, int64_t capacity, uint64_t* kmers,
+                             uint8_t* exts, uint16_t* counts, int64_t* entry_offsets,
+                             int64_t* group_stats);
+
 /* ============================== profiling ================================ */
 /* When enabled, every kernel launch is bracketed by HIP events on its stream. */
 int rogtk_profile_enable(int on);

@@ -32,8 +32,8 @@ _lib = None
 
 def build() -> str:
     """Compile the oracle (g++) in-tree if it is missing or stale."""
-    src = os.path.join(_HERE, "rogtk_oracle.cpp")
-    if (not os.path.exists(_LIB_PATH)) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, f) for f in ("rogtk_oracle.cpp", "kmer_oracle.cpp")]
+    if (not os.path.exists(_LIB_PATH)) or os.path.getmtime(_LIB_PATH) < max(map(os.path.getmtime, srcs)):
         import subprocess
         subprocess.check_call(["make", "-s", "-C", _HERE])
     return _LIB_PATH
@@ -56,6 +56,10 @@ def lib():
         L.oracle_plogp.argtypes = [u32, u32]
         L.oracle_plogp.restype = ctypes.c_double
         L.oracle_version.restype = ctypes.c_char_p
+        L.oracle_kmer_spectrum.argtypes = [vp, i32, vp, vp, i64, i64, i64, i32, i32, i64, vp, vp, vp, i64, vp]
+        L.oracle_kmer_spectrum.restype = i64
+        L.oracle_kmer_observations.argtypes = [vp, i32, i64, i64, i32]
+        L.oracle_kmer_observations.restype = i64
         _lib = L
     return _lib
 
@@ -303,3 +307,101 @@ def py_cluster_bruteforce(items: Sequence[Optional[bytes]], umi_len: int = 0, ma
         else:
             out.append(irr_id[x])
     return out, len(roots) + len(irregular)
+
+
+# --------------------------------------------------------------------------
+# H4: k-mer spectra of read groups (oracle/kmer_oracle.cpp)
+# --------------------------------------------------------------------------
+def effective_k(k: int) -> int:
+    """fracture.rs:246-256: Kmer4 / Kmer8 / Kmer16 / Kmer32 / Kmer64."""
+    return 4 if k <= 4 else 8 if k <= 8 else 16 if k <= 16 else 32 if k <= 32 else 64
+
+
+def kmer_spectrum(col: StrCol, k: int, min_cov: int, auto_k: bool = False, group_offsets=None):
+    """Per-group spectra, concatenated in group order. Returns a dict with
+    kmer_hi, kmer_lo (u64), exts (u8), counts (u16), group_offsets (n_groups+1, int64)
+    and stats (n_groups x 5: k_eff, n_sequences, node_count, terminal_count, isolated_count)."""
+    L = lib()
+    go = np.array([0, col.n], dtype=np.int64) if group_offsets is None else np.asarray(group_offsets, np.int64)
+    G = len(go) - 1
+    offs, vals, valid = col._ptrs()
+    his, los, exs, cns = [], [], [], []
+    stats = np.zeros((G, 5), dtype=np.int64)
+    out_off = np.zeros(G + 1, dtype=np.int64)
+    for g in range(G):
+        cap = int(L.oracle_kmer_observations(offs, 8, int(go[g]), int(go[g + 1]), 4)) + 1
+        km = np.zeros(2 * cap, dtype=np.uint64)
+        ex = np.zeros(cap, dtype=np.uint8)
+        cn = np.zeros(cap, dtype=np.uint16)
+        st = np.zeros(5, dtype=np.int64)
+        m = L.oracle_kmer_spectrum(offs, 8, vals, valid, 0, int(go[g]), int(go[g + 1]), int(k), int(bool(auto_k)),
+                                   int(min_cov), km.ctypes.data_as(ctypes.c_void_p), ex.ctypes.data_as(ctypes.c_void_p),
+                                   cn.ctypes.data_as(ctypes.c_void_p), cap, st.ctypes.data_as(ctypes.c_void_p))
+        assert m >= 0
+        his.append(km[0:2 * m:2])
+        los.append(km[1:2 * m:2])
+        exs.append(ex[:m])
+        cns.append(cn[:m])
+        stats[g] = st
+        out_off[g + 1] = out_off[g] + m
+    cat = lambda xs, dt: np.concatenate(xs).astype(dt) if xs else np.zeros(0, dt)
+    return {"kmer_hi": cat(his, np.uint64), "kmer_lo": cat(los, np.uint64), "exts": cat(exs, np.uint8),
+            "counts": cat(cns, np.uint16), "group_offsets": out_off, "stats": stats}
+
+
+def py_kmer_spectrum(items: Sequence[Optional[bytes]], k: int, min_cov: int, auto_k: bool = False):
+    """Independent pure-Python restatement of the same path (small inputs only):
+    returns ([(kmer_str, exts, count)] sorted, (k_eff, n_seq, node, terminal, isolated))."""
+    raw = [bytes(x) for x in items if x is not None]
+    if auto_k:
+        lens = [len(x) for x in raw if len(x) > 0]
+        if not raw or not lens:
+            k = 31
+        else:
+            mean = sum(lens) / len(lens)
+            q = mean / 3.0
+            kk = int(q + 0.5) if q >= 0 else -int(-q + 0.5)  # round half away from zero
+            kk = 63 if kk == 0 else (kk - 1 if kk % 2 == 0 else kk)
+            k = min(max(kk, 11), 63)
+    if k > 64:
+        return [], (0, 0, 0, 0, 0)
+    seqs = []
+    for x in raw:
+        u = bytes(c - 32 if 97 <= c <= 122 else c for c in x)
+        if all(c in b"ACGT" for c in u):
+            seqs.append(u.decode())
+    K = effective_k(k)
+    if not seqs:
+        return [], (K, 0, 0, 0, 0)
+    obs = {}
+    for s in seqs:
+        for i in range(len(s) - K + 1):
+            km = s[i:i + K]
+            e = 0
+            if i > 0:
+                e |= 1 << "ACGT".index(s[i - 1])
+            if i + K < len(s):
+                e |= 1 << (4 + "ACGT".index(s[i + K]))
+            c, ee = obs.get(km, (0, 0))
+            obs[km] = (min(c + 1, 0xFFFF), ee | e)
+    valid = {km: v for km, v in obs.items() if v[0] >= min_cov}
+    out = []
+    term = iso = 0
+    for km in sorted(valid):
+        c, e = valid[km]
+        ne = 0
+        for b in range(4):
+            if (e >> b) & 1 and ("ACGT"[b] + km[:-1]) in valid:
+                ne |= 1 << b
+            if (e >> (4 + b)) & 1 and (km[1:] + "ACGT"[b]) in valid:
+                ne |= 1 << (4 + b)
+        out.append((km, ne, c))
+        l0, r0 = (ne & 0xF) == 0, (ne >> 4) == 0
+        term += int(l0 or r0)
+        iso += int(l0 and r0)
+    return out, (K, len(seqs), len(out), term, iso)
+
+
+def kmer_to_str(hi: int, lo: int, K: int) -> str:
+    v = (int(hi) << 64) | int(lo)
+    return "".join("ACGT"[(v >> (2 * (K - 1 - i))) & 3] for i in range(K))

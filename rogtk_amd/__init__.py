@@ -9,6 +9,7 @@ Drop-in surface (mirrors rogtk/__init__.py's `umi` / `hamming` namespaces):
     rg.col(umis).hamming.within("ACGTACGTACGT", max_distance=1)
     rg.umi_complexity_scores(umis)
     rg.umi_cluster(umis, max_distance=1)         # H3 (caller-side group_by('umi'))
+    rg.kmer_spectrum(reads, k=17, min_coverage=20, group_offsets=...)  # H4 (fracture.rs)
 
 Device-resident pipeline (packed SoA in HBM, torch tensors as plumbing):
     rogtk_amd.device (PackedBatch, score_packed, ClusterEngine, cluster_batch)
@@ -18,6 +19,7 @@ C ABI: include/rogtk_hip.h (librogtk_hip.so, in-tree).
 from ._lib import RogtkError, device_count, version  # noqa: F401
 from .api import (  # noqa: F401
     FIELDS,
+    KMER_STATS,
     STRUCT_TYPE,
     Col,
     HammingExpr,
@@ -25,6 +27,7 @@ from .api import (  # noqa: F401
     col,
     hamming_distance,
     hamming_within,
+    kmer_spectrum,
     umi_cluster,
     umi_complexity,
     umi_complexity_scores,
@@ -33,5 +36,5 @@ from .api import (  # noqa: F401
 __all__ = [
     "RogtkError", "device_count", "version", "FIELDS", "STRUCT_TYPE", "Col", "HammingExpr",
     "UmiNamespace", "col", "hamming_distance", "hamming_within", "umi_cluster", "umi_complexity",
-    "umi_complexity_scores",
+    "umi_complexity_scores", "kmer_spectrum", "KMER_STATS",
 ]

@@ -72,6 +72,9 @@ SIGNATURES = {
     "rogtk_hamming_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _u32, _vp, _vp],
     "rogtk_umi_cluster_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _P_I64,
                                _P_I32],
+    "rogtk_kmer_capacity": [_vp, _i32, _i64, _P_I64],
+    "rogtk_kmer_spectrum_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i32, _i32, _i64, _i64, _vp,
+                                 _vp, _vp, _vp, _vp],
     "rogtk_profile_enable": [_i32],
     "rogtk_profile_reset": [],
     "rogtk_profile_read": [ctypes.c_char_p, _P_F64, _P_I64],

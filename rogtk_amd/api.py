@@ -13,6 +13,9 @@ reference                                          rogtk_amd
 ``pl.col(c).hamming.distance(target)`` (:331)      ``col(c).hamming.distance(target)``
 ``pl.col(c).hamming.within(target, 1)`` (:341)     ``col(c).hamming.within(target, 1)``
 ``df.group_by('umi')`` (caller, :206-214)          ``umi_cluster(c, max_distance=0|1)``
+k-mer front end of ``assemble_sequences*`` per     ``kmer_spectrum(c, k, min_coverage,
+group (fracture.rs:105-256, debruijn                auto_k, group_offsets)``
+filter_kmers)
 ================================================  ==========================================
 
 polars is not part of this build's image, so an "expression" is evaluated eagerly
@@ -153,6 +156,44 @@ def umi_cluster(column: ColumnLike, umi_len: int = 0, max_distance: int = 1):
               n, int(umi_len), int(max_distance), _ptr(cid), ctypes.byref(nclu), ctypes.byref(rl))
     out = pa.Array.from_buffers(pa.uint32(), n, [validity_buffer(ch), pa.py_buffer(cid[:n].copy())])
     return out, int(nclu.value), int(rl.value)
+
+
+KMER_STATS = ("k_eff", "n_sequences", "node_count", "terminal_count", "isolated_count")
+
+
+def kmer_spectrum(column: ColumnLike, k: int, min_coverage: int, auto_k: bool = False, group_offsets=None):
+    """H4: k-mer spectra of read groups (include/rogtk_hip.h, rogtk_kmer_spectrum_host).
+
+    ``group_offsets`` (n_groups + 1 row offsets, contiguous groups; None = one group)
+    plays the role of polars' group_by: each group is what one call of the
+    reference's assemble_sequences_expr sees. Returns a dict of numpy arrays:
+    kmer_hi / kmer_lo (u64; hi only for k_eff 64), exts (u8), counts (u16),
+    entry_offsets (n_groups + 1) and stats (n_groups x 5, columns KMER_STATS).
+    """
+    arr = column
+    if isinstance(arr, pa.ChunkedArray):
+        arr = arr.combine_chunks() if arr.num_chunks else pa.array([], type=arr.type)
+    chs = list(chunks(arr))
+    assert len(chs) == 1
+    ch = chs[0]
+    n = ch.n
+    o, v, val = ch.ptrs()
+    cap = ctypes.c_int64(0)
+    _lib.call("rogtk_kmer_capacity", o, ch.offset_width, n, ctypes.byref(cap))
+    capn = max(int(cap.value), 1)
+    go = None if group_offsets is None else np.ascontiguousarray(group_offsets, dtype=np.int64)
+    G = 1 if go is None else len(go) - 1
+    km = np.empty(2 * capn, dtype=np.uint64)
+    ex = np.empty(capn, dtype=np.uint8)
+    cn = np.empty(capn, dtype=np.uint16)
+    eo = np.empty(G + 1, dtype=np.int64)
+    st = np.empty(5 * G, dtype=np.int64)
+    _lib.call("rogtk_kmer_spectrum_host", o, ch.offset_width, v, ch.values.size, val, ch.validity_offset, n,
+              _ptr(go), 0 if go is None else G, int(k), int(bool(auto_k)), int(min_coverage), capn,
+              _ptr(km), _ptr(ex), _ptr(cn), _ptr(eo), _ptr(st))
+    m = int(eo[G])
+    return {"kmer_hi": km[0:2 * m:2].copy(), "kmer_lo": km[1:2 * m:2].copy(), "exts": ex[:m].copy(),
+            "counts": cn[:m].copy(), "entry_offsets": eo, "stats": st.reshape(G, 5)}
 
 
 # ------------------------------------------------------------ namespaces

@@ -208,29 +208,6 @@ int check_packed_alignment(const uint32_t* codes, const ScoreOut& o, const uint3
 }
 
 // --------------------------------------------- per-thread level-2 context
-struct DevBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-    ~DevBuf() {
-        if (p) hipFree(p);
-    }
-    int ensure(size_t bytes) {
-        if (bytes <= cap && p) return ROGTK_OK;
-        if (p) {
-            hipFree(p);
-            p = nullptr;
-            cap = 0;
-        }
-        size_t want = std::max<size_t>(bytes, 256);
-        want = (want + 255) / 256 * 256;
-        ROGTK_HIP_CHECK(hipMalloc(&p, want));
-        cap = want;
-        return ROGTK_OK;
-    }
-    template <class T>
-    T* as() const { return reinterpret_cast<T*>(p); }
-};
-
 struct HostCtx {
     int device = -1;
     hipStream_t stream = nullptr;

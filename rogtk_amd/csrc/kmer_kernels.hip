@@ -1,0 +1,670 @@
+// kmer_kernels.hip — H4: k-mer spectra of read groups on gfx950.
+//
+// Replaces, per polars group, the k-mer front end of rogtk's fracture assembly:
+//   expressions.rs:739-744  sequences = column.into_iter().flatten()
+//   fracture.rs:200-229     auto_k (estimate_k :24-54), k > 64 -> nothing, uppercase,
+//                           drop sequences with any non-ACGT byte
+//   fracture.rs:246-256     effective k = 4 / 8 / 16 / 32 / 64
+//   fracture.rs:105-116     debruijn 0.3.4 filter_kmers(CountFilter(min_cov), stranded,
+//                           report_all) + remove_censored_exts
+//   fracture.rs:118-146     node / terminal / isolated counts
+// Output per group: its valid k-mers in ascending order (the crate's pre-MPHF order)
+// with the censored Exts byte (low nibble = left bases, high = right) and the
+// saturating u16 count. Spec and the oracle: oracle/kmer_oracle.cpp.
+//
+// Device pipeline for one effective k (groups of other k are skipped):
+//   rows    one wave per row: group lookup, ACGT check (ballot), observation count
+//   emit    one wave per row: every k-mer observation -> (key lo[, hi], ext, group)
+//   sort    LSD radix passes (hipcub, stable): key lo, [key hi], group -> permutation
+//   runs    run heads -> run count (saturating) + OR of exts -> CountFilter
+//   censor  binary search of each extension's neighbour inside the group's valid run
+//   out     entries at the group's capacity offset; host packs them densely
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+#include <memory>
+#include <vector>
+
+#include "rogtk_internal.h"
+
+namespace rogtk {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / 64;
+constexpr int64_t kMaxObsPerLaunch = int64_t(1) << 30;  // u32 permutation indices
+
+__device__ __forceinline__ uint32_t base2(uint8_t c) { return (uint32_t)((c >> 1) ^ (c >> 2)) & 3u; }
+__device__ __forceinline__ bool acgt(uint8_t c) {
+    const uint8_t u = c & 0xDF;  // ASCII upper case for letters; other bytes stay non-ACGT
+    return u == 'A' || u == 'C' || u == 'G' || u == 'T';
+}
+
+template <int OW>
+__device__ __forceinline__ void span(const void* offsets, int64_t r, int64_t& st, int64_t& len) {
+    if (OW == 4) {
+        const int32_t* o = (const int32_t*)offsets;
+        st = o[r];
+        len = (int64_t)o[r + 1] - o[r];
+    } else {
+        const int64_t* o = (const int64_t*)offsets;
+        st = o[r];
+        len = o[r + 1] - o[r];
+    }
+}
+
+// last g with go[g] <= r (groups cover [go[0], go[G]) = [0, n_rows))
+__device__ __forceinline__ int64_t group_of(const int64_t* go, int64_t G, int64_t r) {
+    int64_t lo = 0, hi = G - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (go[mid] <= r) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+template <int OW>
+__global__ __launch_bounds__(kBlock) void k_kmer_rows(const void* offsets, const uint8_t* __restrict__ values,
+                                                      const uint8_t* __restrict__ validity, int64_t voff,
+                                                      int64_t n_rows, const int64_t* __restrict__ go, int64_t G,
+                                                      const uint8_t* __restrict__ gk, int K,
+                                                      uint32_t* __restrict__ row_group, int64_t* __restrict__ row_obs,
+                                                      unsigned long long* __restrict__ gstat) {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
+    for (int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); r < n_rows; r += waves) {
+        const int64_t g = group_of(go, G, r);
+        bool valid = gk[g] == K;
+        if (valid && validity) {
+            const int64_t b = voff + r;
+            valid = (validity[b >> 3] >> (b & 7)) & 1;
+        }
+        int64_t st = 0, len = 0;
+        bool ok = false;
+        if (valid) {
+            span<OW>(offsets, r, st, len);
+            bool bad = false;
+            for (int64_t j = lane; j < len; j += 64) bad |= !acgt(values[st + j]);
+            ok = __ballot(bad) == 0;
+        }
+        if (lane == 0) {
+            row_group[r] = (uint32_t)g;
+            row_obs[r] = ok && len >= K ? len - K + 1 : 0;
+            if (ok) atomicAdd(gstat + 5 * g + 1, 1ull);  // n_sequences
+        }
+    }
+}
+
+template <int OW, bool WIDE>
+__global__ __launch_bounds__(kBlock) void k_kmer_emit(const void* offsets, const uint8_t* __restrict__ values,
+                                                      int64_t n_rows, int K, const uint32_t* __restrict__ row_group,
+                                                      const int64_t* __restrict__ row_obs,
+                                                      const int64_t* __restrict__ obs_off,
+                                                      uint64_t* __restrict__ key_lo, uint64_t* __restrict__ key_hi,
+                                                      uint8_t* __restrict__ ext, uint32_t* __restrict__ grp,
+                                                      uint32_t* __restrict__ idx) {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
+    for (int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); r < n_rows; r += waves) {
+        const int64_t nobs = row_obs[r];
+        if (nobs == 0) continue;
+        int64_t st, len;
+        span<OW>(offsets, r, st, len);
+        const uint8_t* s = values + st;
+        const int64_t o0 = obs_off[r];
+        const uint32_t g = row_group[r];
+        for (int64_t p = lane; p < nobs; p += 64) {
+            uint64_t lo = 0, hi = 0;
+            if (WIDE) {
+                for (int j = 0; j < 32; ++j) hi = (hi << 2) | base2(s[p + j]);
+                for (int j = 32; j < 64; ++j) lo = (lo << 2) | base2(s[p + j]);
+            } else {
+                for (int j = 0; j < K; ++j) lo = (lo << 2) | base2(s[p + j]);
+            }
+            uint8_t e = 0;
+            if (p > 0) e |= (uint8_t)(1u << base2(s[p - 1]));
+            if (p + K < len) e |= (uint8_t)(1u << (4 + base2(s[p + K])));
+            const int64_t o = o0 + p;
+            key_lo[o] = lo;
+            if (WIDE) key_hi[o] = hi;
+            ext[o] = e;
+            grp[o] = g;
+            idx[o] = (uint32_t)o;
+        }
+    }
+}
+
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_gather(const T* __restrict__ src, const uint32_t* __restrict__ perm,
+                                                   int64_t n, T* __restrict__ dst) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+        dst[i] = src[perm[i]];
+}
+
+template <bool WIDE>
+__device__ __forceinline__ bool same_key(const uint64_t* lo, const uint64_t* hi, const uint32_t* grp, int64_t a,
+                                         int64_t b) {
+    return grp[a] == grp[b] && lo[a] == lo[b] && (!WIDE || hi[a] == hi[b]);
+}
+
+template <bool WIDE>
+__global__ __launch_bounds__(kBlock) void k_heads(const uint64_t* __restrict__ lo, const uint64_t* __restrict__ hi,
+                                                  const uint32_t* __restrict__ grp, int64_t n,
+                                                  uint32_t* __restrict__ head) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+        head[i] = (i == 0 || !same_key<WIDE>(lo, hi, grp, i, i - 1)) ? 1u : 0u;
+}
+
+// One lane per run head: count (u16 saturating), OR of exts, CountFilter.
+template <bool WIDE>
+__global__ __launch_bounds__(kBlock) void k_runs(const uint64_t* __restrict__ lo, const uint64_t* __restrict__ hi,
+                                                 const uint32_t* __restrict__ grp, const uint8_t* __restrict__ ext,
+                                                 const uint32_t* __restrict__ head, const uint32_t* __restrict__ rid,
+                                                 int64_t n, int64_t min_cov, uint32_t* __restrict__ r_valid,
+                                                 uint32_t* __restrict__ r_first, uint8_t* __restrict__ r_ext,
+                                                 uint16_t* __restrict__ r_cnt) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        if (!head[i]) continue;
+        uint32_t count = 0;
+        uint8_t e = 0;
+        int64_t j = i;
+        do {
+            if (count < 0xFFFFu) ++count;
+            e |= ext[j];
+            ++j;
+        } while (j < n && !head[j]);
+        const uint32_t r = rid[i];
+        r_valid[r] = (int64_t)count >= min_cov ? 1u : 0u;
+        r_first[r] = (uint32_t)i;
+        r_ext[r] = e;
+        r_cnt[r] = (uint16_t)count;
+    }
+}
+
+template <bool WIDE>
+__global__ __launch_bounds__(kBlock) void k_compact_valid(const uint32_t* __restrict__ r_valid,
+                                                          const uint32_t* __restrict__ vpos,
+                                                          const uint32_t* __restrict__ r_first,
+                                                          const uint8_t* __restrict__ r_ext,
+                                                          const uint16_t* __restrict__ r_cnt, int64_t n_runs,
+                                                          const uint64_t* __restrict__ lo,
+                                                          const uint64_t* __restrict__ hi,
+                                                          const uint32_t* __restrict__ grp,
+                                                          uint64_t* __restrict__ v_lo, uint64_t* __restrict__ v_hi,
+                                                          uint32_t* __restrict__ v_grp, uint8_t* __restrict__ v_ext,
+                                                          uint16_t* __restrict__ v_cnt) {
+    for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < n_runs; r += (int64_t)gridDim.x * kBlock) {
+        if (!r_valid[r]) continue;
+        const uint32_t j = vpos[r], f = r_first[r];
+        v_lo[j] = lo[f];
+        if (WIDE) v_hi[j] = hi[f];
+        v_grp[j] = grp[f];
+        v_ext[j] = r_ext[r];
+        v_cnt[j] = r_cnt[r];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_group_ranges(const uint32_t* __restrict__ v_grp, int64_t nv,
+                                                         int64_t* __restrict__ gstart, int64_t* __restrict__ gcount) {
+    for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < nv; j += (int64_t)gridDim.x * kBlock) {
+        const uint32_t g = v_grp[j];
+        if (j == 0 || v_grp[j - 1] != g) gstart[g] = j;
+        if (j == nv - 1 || v_grp[j + 1] != g) gcount[g] = j + 1;  // end; made a count below
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_group_counts(const uint8_t* __restrict__ gk, int K, int64_t G,
+                                                         const int64_t* __restrict__ gstart,
+                                                         int64_t* __restrict__ gcount) {
+    for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < G; g += (int64_t)gridDim.x * kBlock)
+        if (gk[g] == K && gcount[g] > 0) gcount[g] -= gstart[g];
+}
+
+// remove_censored_exts + terminal / isolated counts + output at the group's capacity offset
+template <bool WIDE>
+__global__ __launch_bounds__(kBlock) void k_censor(const uint64_t* __restrict__ v_lo, const uint64_t* __restrict__ v_hi,
+                                                   const uint32_t* __restrict__ v_grp,
+                                                   const uint8_t* __restrict__ v_ext,
+                                                   const uint16_t* __restrict__ v_cnt, int64_t nv, int K,
+                                                   const int64_t* __restrict__ gstart,
+                                                   const int64_t* __restrict__ gcount,
+                                                   const int64_t* __restrict__ cap_off,
+                                                   uint64_t* __restrict__ o_kmer, uint8_t* __restrict__ o_ext,
+                                                   uint16_t* __restrict__ o_cnt,
+                                                   unsigned long long* __restrict__ gstat) {
+    const uint64_t mask = (WIDE || K == 32) ? ~0ull : ((1ull << (2 * K)) - 1ull);
+    for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < nv; j += (int64_t)gridDim.x * kBlock) {
+        const uint32_t g = v_grp[j];
+        const int64_t a0 = gstart[g], b0 = a0 + gcount[g];
+        const uint64_t lo = v_lo[j], hi = WIDE ? v_hi[j] : 0ull;
+        const uint8_t e = v_ext[j];
+        uint8_t ne = 0;
+        for (int bit = 0; bit < 8; ++bit) {
+            if (!((e >> bit) & 1u)) continue;
+            const uint64_t b = (uint64_t)(bit & 3);
+            uint64_t nlo, nhi = 0;
+            if (bit < 4) {  // extend_left: b + kmer[0..K-1]
+                if (WIDE) {
+                    nlo = (lo >> 2) | ((hi & 3ull) << 62);
+                    nhi = (hi >> 2) | (b << 62);
+                } else {
+                    nlo = (lo >> 2) | (b << (2 * K - 2));
+                }
+            } else {  // extend_right: kmer[1..K] + b
+                if (WIDE) {
+                    nhi = (hi << 2) | (lo >> 62);
+                    nlo = (lo << 2) | b;
+                } else {
+                    nlo = ((lo << 2) | b) & mask;
+                }
+            }
+            int64_t a = a0, c = b0;
+            while (a < c) {
+                const int64_t m = (a + c) >> 1;
+                const bool less = WIDE ? (v_hi[m] < nhi || (v_hi[m] == nhi && v_lo[m] < nlo)) : v_lo[m] < nlo;
+                if (less) a = m + 1;
+                else c = m;
+            }
+            const bool found = a < b0 && v_lo[a] == nlo && (!WIDE || v_hi[a] == nhi);
+            if (found) ne |= (uint8_t)(1u << bit);
+        }
+        const int64_t o = cap_off[g] + (j - a0);
+        o_kmer[2 * o] = hi;
+        o_kmer[2 * o + 1] = lo;
+        o_ext[o] = ne;
+        o_cnt[o] = v_cnt[j];
+        const bool l0 = (ne & 0xF) == 0, r0 = (ne >> 4) == 0;
+        if (l0 || r0) atomicAdd(gstat + 5 * g + 3, 1ull);
+        if (l0 && r0) atomicAdd(gstat + 5 * g + 4, 1ull);
+    }
+}
+
+// dense packing: one wave per group copies its entries to the final offsets
+__global__ __launch_bounds__(kBlock) void k_pack(const uint64_t* __restrict__ t_kmer, const uint8_t* __restrict__ t_ext,
+                                                 const uint16_t* __restrict__ t_cnt, int64_t G,
+                                                 const int64_t* __restrict__ cap_off,
+                                                 const int64_t* __restrict__ gcount,
+                                                 const int64_t* __restrict__ out_off, uint64_t* __restrict__ kmer,
+                                                 uint8_t* __restrict__ ext, uint16_t* __restrict__ cnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
+    for (int64_t g = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); g < G; g += waves) {
+        const int64_t n = gcount[g], s = cap_off[g], d = out_off[g];
+        for (int64_t t = lane; t < n; t += 64) {
+            kmer[2 * (d + t)] = t_kmer[2 * (s + t)];
+            kmer[2 * (d + t) + 1] = t_kmer[2 * (s + t) + 1];
+            ext[d + t] = t_ext[s + t];
+            cnt[d + t] = t_cnt[s + t];
+        }
+    }
+}
+
+int grid_for(int64_t n, int cap = 8192) {
+    int64_t g = (n + kBlock - 1) / kBlock;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+// ---------------------------------------------------------------- host side
+int estimate_k_host(const std::vector<int64_t>& lens) {  // fracture.rs:24-54 over the non-null rows
+    if (lens.empty()) return 31;
+    uint64_t total = 0, count = 0;
+    for (int64_t l : lens)
+        if (l > 0) {
+            total += (uint64_t)l;
+            count += 1;
+        }
+    if (count == 0) return 31;
+    const double mean = (double)total / (double)count;
+    const int64_t k = (int64_t)std::round(mean / 3.0);
+    uint64_t ku = (k % 2 == 0) ? (uint64_t)k - 1 : (uint64_t)k;  // 0 - 1 wraps (release build)
+    if (ku < 11) ku = 11;
+    if (ku > 63) ku = 63;
+    return (int)ku;
+}
+
+int effective_k(int k) { return k <= 4 ? 4 : k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : 64; }
+
+struct KmerCtx {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    DevBuf offsets, values, validity, go, gk, cap_off, gstat, gstart, gcount, out_off;
+    DevBuf row_group, row_obs, obs_off;
+    DevBuf key_lo, key_hi, ext, grp, idx, perm_a, perm_b, tmp_u64, tmp_u32;
+    DevBuf s_lo, s_hi, s_ext, s_grp, head, rid, r_valid, r_first, r_ext, r_cnt, vpos;
+    DevBuf v_lo, v_hi, v_grp, v_ext, v_cnt, t_kmer, t_ext, t_cnt, o_kmer, o_ext, o_cnt, cub;
+    ~KmerCtx() {
+        if (stream) hipStreamDestroy(stream);
+    }
+};
+thread_local std::unique_ptr<KmerCtx> t_kctx;
+
+int kmer_ctx(KmerCtx** out) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        set_error("no HIP device available (librogtk_hip needs an MI355X / gfx950 GPU)");
+        return ROGTK_E_NODEVICE;
+    }
+    int dev = 0;
+    ROGTK_HIP_CHECK(hipGetDevice(&dev));
+    if (!t_kctx || t_kctx->device != dev) {
+        t_kctx.reset(new KmerCtx());
+        t_kctx->device = dev;
+        ROGTK_HIP_CHECK(hipStreamCreateWithFlags(&t_kctx->stream, hipStreamNonBlocking));
+    }
+    *out = t_kctx.get();
+    return ROGTK_OK;
+}
+
+// hipcub helpers with grow-only temp storage
+int cub_exsum_i64(KmerCtx* c, const int64_t* in, int64_t* out, int64_t n, hipStream_t s) {
+    size_t bytes = 0;
+    ROGTK_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, (int)n, s));
+    if (int rc = c->cub.ensure(bytes)) return rc;
+    ROGTK_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(c->cub.p, bytes, in, out, (int)n, s));
+    return ROGTK_OK;
+}
+int cub_exsum_u32(KmerCtx* c, const uint32_t* in, uint32_t* out, int64_t n, hipStream_t s) {
+    size_t bytes = 0;
+    ROGTK_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, (int)n, s));
+    if (int rc = c->cub.ensure(bytes)) return rc;
+    ROGTK_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(c->cub.p, bytes, in, out, (int)n, s));
+    return ROGTK_OK;
+}
+template <class K>
+int cub_sort(KmerCtx* c, const K* kin, K* kout, const uint32_t* vin, uint32_t* vout, int64_t n, int end_bit,
+             hipStream_t s) {
+    size_t bytes = 0;
+    ROGTK_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kin, kout, vin, vout, (int)n, 0, end_bit, s));
+    if (int rc = c->cub.ensure(bytes)) return rc;
+    ROGTK_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(c->cub.p, bytes, kin, kout, vin, vout, (int)n, 0, end_bit, s));
+    return ROGTK_OK;
+}
+
+int bits_for(uint64_t v) {
+    int b = 1;
+    while (b < 64 && (v >> b)) ++b;
+    return b;
+}
+
+template <int OW, bool WIDE>
+int run_class(KmerCtx* c, const uint8_t* validity, int64_t n_rows, int64_t G, int K, int64_t min_cov,
+              hipStream_t s) {
+    const int64_t* go = c->go.as<int64_t>();
+    unsigned long long* gstat = c->gstat.as<unsigned long long>();
+    if (int rc = c->row_group.ensure(n_rows * 4)) return rc;
+    if (int rc = c->row_obs.ensure(n_rows * 8)) return rc;
+    if (int rc = c->obs_off.ensure(n_rows * 8)) return rc;
+    const int wgrid = grid_for((n_rows + kWavesPerBlock - 1) / kWavesPerBlock * kBlock, 16384);
+    hipLaunchKernelGGL((k_kmer_rows<OW>), dim3(wgrid), dim3(kBlock), 0, s, c->offsets.p, c->values.as<uint8_t>(),
+                       validity, (int64_t)0, n_rows, go, G,
+                       c->gk.as<uint8_t>(), K, c->row_group.as<uint32_t>(), c->row_obs.as<int64_t>(), gstat);
+    ROGTK_HIP_CHECK(hipGetLastError());
+    if (int rc = cub_exsum_i64(c, c->row_obs.as<int64_t>(), c->obs_off.as<int64_t>(), n_rows, s)) return rc;
+    int64_t last[2] = {0, 0};
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&last[0], c->obs_off.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&last[1], c->row_obs.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    const int64_t T = last[0] + last[1];
+    if (T == 0) return ROGTK_OK;
+    ROGTK_REQUIRE(T <= kMaxObsPerLaunch, ROGTK_E_UNSUPPORTED,
+                  "kmer: %lld k-mer observations in one call (max %lld); split the groups over calls",
+                  (long long)T, (long long)kMaxObsPerLaunch);
+    for (DevBuf* b : {&c->key_lo, &c->key_hi, &c->tmp_u64, &c->s_lo, &c->s_hi, &c->v_lo, &c->v_hi})
+        if (int rc = b->ensure((size_t)T * 8)) return rc;
+    for (DevBuf* b : {&c->grp, &c->idx, &c->perm_a, &c->perm_b, &c->tmp_u32, &c->s_grp, &c->head, &c->rid,
+                      &c->r_valid, &c->r_first, &c->vpos, &c->v_grp})
+        if (int rc = b->ensure((size_t)T * 4)) return rc;
+    for (DevBuf* b : {&c->ext, &c->s_ext, &c->r_ext, &c->v_ext})
+        if (int rc = b->ensure((size_t)T)) return rc;
+    for (DevBuf* b : {&c->r_cnt, &c->v_cnt})
+        if (int rc = b->ensure((size_t)T * 2)) return rc;
+
+    hipLaunchKernelGGL((k_kmer_emit<OW, WIDE>), dim3(wgrid), dim3(kBlock), 0, s, c->offsets.p,
+                       c->values.as<uint8_t>(), n_rows, K, c->row_group.as<uint32_t>(), c->row_obs.as<int64_t>(),
+                       c->obs_off.as<int64_t>(), c->key_lo.as<uint64_t>(), c->key_hi.as<uint64_t>(),
+                       c->ext.as<uint8_t>(), c->grp.as<uint32_t>(), c->idx.as<uint32_t>());
+    ROGTK_HIP_CHECK(hipGetLastError());
+    // LSD: key lo, [key hi], group (hipcub radix sort is stable)
+    const int g = grid_for(T);
+    const int lo_bits = WIDE ? 64 : 2 * K;
+    if (int rc = cub_sort<uint64_t>(c, c->key_lo.as<uint64_t>(), c->tmp_u64.as<uint64_t>(), c->idx.as<uint32_t>(),
+                                    c->perm_a.as<uint32_t>(), T, lo_bits, s))
+        return rc;
+    uint32_t* perm = c->perm_a.as<uint32_t>();
+    uint32_t* other = c->perm_b.as<uint32_t>();
+    if (WIDE) {
+        hipLaunchKernelGGL(k_gather<uint64_t>, dim3(g), dim3(kBlock), 0, s, c->key_hi.as<uint64_t>(), perm, T,
+                           c->s_hi.as<uint64_t>());
+        if (int rc = cub_sort<uint64_t>(c, c->s_hi.as<uint64_t>(), c->tmp_u64.as<uint64_t>(), perm, other, T, 64, s))
+            return rc;
+        std::swap(perm, other);
+    }
+    if (G > 1) {
+        hipLaunchKernelGGL(k_gather<uint32_t>, dim3(g), dim3(kBlock), 0, s, c->grp.as<uint32_t>(), perm, T,
+                           c->s_grp.as<uint32_t>());
+        if (int rc = cub_sort<uint32_t>(c, c->s_grp.as<uint32_t>(), c->tmp_u32.as<uint32_t>(), perm, other, T,
+                                        bits_for((uint64_t)G - 1), s))
+            return rc;
+        std::swap(perm, other);
+    }
+    hipLaunchKernelGGL(k_gather<uint64_t>, dim3(g), dim3(kBlock), 0, s, c->key_lo.as<uint64_t>(), perm, T,
+                       c->s_lo.as<uint64_t>());
+    if (WIDE)
+        hipLaunchKernelGGL(k_gather<uint64_t>, dim3(g), dim3(kBlock), 0, s, c->key_hi.as<uint64_t>(), perm, T,
+                           c->s_hi.as<uint64_t>());
+    hipLaunchKernelGGL(k_gather<uint8_t>, dim3(g), dim3(kBlock), 0, s, c->ext.as<uint8_t>(), perm, T,
+                       c->s_ext.as<uint8_t>());
+    hipLaunchKernelGGL(k_gather<uint32_t>, dim3(g), dim3(kBlock), 0, s, c->grp.as<uint32_t>(), perm, T,
+                       c->s_grp.as<uint32_t>());
+    ROGTK_HIP_CHECK(hipGetLastError());
+    // runs + CountFilter
+    hipLaunchKernelGGL((k_heads<WIDE>), dim3(g), dim3(kBlock), 0, s, c->s_lo.as<uint64_t>(), c->s_hi.as<uint64_t>(),
+                       c->s_grp.as<uint32_t>(), T, c->head.as<uint32_t>());
+    if (int rc = cub_exsum_u32(c, c->head.as<uint32_t>(), c->rid.as<uint32_t>(), T, s)) return rc;
+    uint32_t lastu[2] = {0, 0};
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&lastu[0], c->rid.as<uint32_t>() + T - 1, 4, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&lastu[1], c->head.as<uint32_t>() + T - 1, 4, hipMemcpyDeviceToHost, s));
+    hipLaunchKernelGGL((k_runs<WIDE>), dim3(g), dim3(kBlock), 0, s, c->s_lo.as<uint64_t>(), c->s_hi.as<uint64_t>(),
+                       c->s_grp.as<uint32_t>(), c->s_ext.as<uint8_t>(), c->head.as<uint32_t>(),
+                       c->rid.as<uint32_t>(), T, min_cov, c->r_valid.as<uint32_t>(), c->r_first.as<uint32_t>(),
+                       c->r_ext.as<uint8_t>(), c->r_cnt.as<uint16_t>());
+    ROGTK_HIP_CHECK(hipGetLastError());
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    const int64_t n_runs = (int64_t)lastu[0] + lastu[1];
+    if (int rc = cub_exsum_u32(c, c->r_valid.as<uint32_t>(), c->vpos.as<uint32_t>(), n_runs, s)) return rc;
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&lastu[0], c->vpos.as<uint32_t>() + n_runs - 1, 4, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&lastu[1], c->r_valid.as<uint32_t>() + n_runs - 1, 4, hipMemcpyDeviceToHost, s));
+    const int gr = grid_for(n_runs);
+    hipLaunchKernelGGL((k_compact_valid<WIDE>), dim3(gr), dim3(kBlock), 0, s, c->r_valid.as<uint32_t>(),
+                       c->vpos.as<uint32_t>(), c->r_first.as<uint32_t>(), c->r_ext.as<uint8_t>(),
+                       c->r_cnt.as<uint16_t>(), n_runs, c->s_lo.as<uint64_t>(), c->s_hi.as<uint64_t>(),
+                       c->s_grp.as<uint32_t>(), c->v_lo.as<uint64_t>(), c->v_hi.as<uint64_t>(),
+                       c->v_grp.as<uint32_t>(), c->v_ext.as<uint8_t>(), c->v_cnt.as<uint16_t>());
+    ROGTK_HIP_CHECK(hipGetLastError());
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    const int64_t nv = (int64_t)lastu[0] + lastu[1];
+    if (nv == 0) return ROGTK_OK;
+    const int gv = grid_for(nv);
+    hipLaunchKernelGGL(k_group_ranges, dim3(gv), dim3(kBlock), 0, s, c->v_grp.as<uint32_t>(), nv,
+                       c->gstart.as<int64_t>(), c->gcount.as<int64_t>());
+    hipLaunchKernelGGL(k_group_counts, dim3(grid_for(G)), dim3(kBlock), 0, s, c->gk.as<uint8_t>(), K, G,
+                       c->gstart.as<int64_t>(), c->gcount.as<int64_t>());
+    hipLaunchKernelGGL((k_censor<WIDE>), dim3(gv), dim3(kBlock), 0, s, c->v_lo.as<uint64_t>(),
+                       c->v_hi.as<uint64_t>(), c->v_grp.as<uint32_t>(), c->v_ext.as<uint8_t>(),
+                       c->v_cnt.as<uint16_t>(), nv, K, c->gstart.as<int64_t>(), c->gcount.as<int64_t>(),
+                       c->cap_off.as<int64_t>(), c->t_kmer.as<uint64_t>(), c->t_ext.as<uint8_t>(),
+                       c->t_cnt.as<uint16_t>(), gstat);
+    ROGTK_HIP_CHECK(hipGetLastError());
+    return ROGTK_OK;
+}
+
+template <int OW>
+int run_any(KmerCtx* c, const uint8_t* validity, int64_t n_rows, int64_t G, int K, int64_t min_cov,
+            hipStream_t s) {
+    return K == 64 ? run_class<OW, true>(c, validity, n_rows, G, K, min_cov, s)
+                   : run_class<OW, false>(c, validity, n_rows, G, K, min_cov, s);
+}
+
+}  // namespace
+}  // namespace rogtk
+
+using namespace rogtk;
+
+extern "C" {
+
+int rogtk_kmer_capacity(const void* offsets, int offset_width, int64_t n_rows, int64_t* capacity) {
+    ROGTK_REQUIRE(capacity && (n_rows == 0 || offsets), ROGTK_E_INVALID, "kmer_capacity: NULL argument");
+    ROGTK_REQUIRE(offset_width == 4 || offset_width == 8, ROGTK_E_INVALID, "offset_width must be 4 or 8");
+    int64_t t = 0;
+    for (int64_t r = 0; r < n_rows; ++r) {
+        const int64_t len = offset_width == 4
+                                ? (int64_t)((const int32_t*)offsets)[r + 1] - ((const int32_t*)offsets)[r]
+                                : ((const int64_t*)offsets)[r + 1] - ((const int64_t*)offsets)[r];
+        if (len >= 4) t += len - 3;
+    }
+    *capacity = t;
+    return ROGTK_OK;
+}
+
+int rogtk_kmer_spectrum_host(const void* offsets, int offset_width, const uint8_t* values, int64_t values_len,
+                             const uint8_t* validity, int64_t validity_offset, int64_t n_rows,
+                             const int64_t* group_offsets, int64_t n_groups, int k, int auto_k,
+                             int64_t min_coverage, int64_t capacity, uint64_t* kmers, uint8_t* exts,
+                             uint16_t* counts, int64_t* entry_offsets, int64_t* group_stats) {
+    ROGTK_REQUIRE(offset_width == 4 || offset_width == 8, ROGTK_E_INVALID, "offset_width must be 4 or 8");
+    ROGTK_REQUIRE(n_rows >= 0 && (n_rows == 0 || offsets), ROGTK_E_INVALID, "kmer: bad offsets / n_rows");
+    ROGTK_REQUIRE(values_len >= 0 && (values_len == 0 || values), ROGTK_E_INVALID, "kmer: bad values");
+    ROGTK_REQUIRE(entry_offsets && group_stats, ROGTK_E_INVALID, "kmer: entry_offsets / group_stats are NULL");
+    ROGTK_REQUIRE(capacity >= 0 && (capacity == 0 || (kmers && exts && counts)), ROGTK_E_INVALID,
+                  "kmer: output arrays are NULL");
+    ROGTK_REQUIRE(min_coverage >= 0, ROGTK_E_INVALID, "kmer: min_coverage must be >= 0");
+    // groups: contiguous row ranges covering [0, n_rows)
+    std::vector<int64_t> go;
+    if (group_offsets && n_groups > 0) {
+        go.assign(group_offsets, group_offsets + n_groups + 1);
+        ROGTK_REQUIRE(go.front() == 0 && go.back() == n_rows, ROGTK_E_INVALID,
+                      "kmer: group_offsets must start at 0 and end at n_rows");
+        for (int64_t g = 0; g < n_groups; ++g)
+            ROGTK_REQUIRE(go[g] <= go[g + 1], ROGTK_E_INVALID, "kmer: group_offsets must be non-decreasing");
+    } else {
+        go = {0, n_rows};
+    }
+    const int64_t G = (int64_t)go.size() - 1;
+    ROGTK_REQUIRE(G < (int64_t)0xFFFFFFFF, ROGTK_E_UNSUPPORTED, "kmer: too many groups");
+    auto row_len = [&](int64_t r) -> int64_t {
+        return offset_width == 4 ? (int64_t)((const int32_t*)offsets)[r + 1] - ((const int32_t*)offsets)[r]
+                                 : ((const int64_t*)offsets)[r + 1] - ((const int64_t*)offsets)[r];
+    };
+    auto row_ok = [&](int64_t r) -> bool {
+        if (!validity) return true;
+        const int64_t b = validity_offset + r;
+        return (validity[b >> 3] >> (b & 7)) & 1;
+    };
+    // per-group effective k (0 = no output: k > 64), capacity offsets
+    std::vector<uint8_t> gk(G);
+    std::vector<int64_t> cap_off(G + 1, 0);
+    bool present[65] = {false};
+    for (int64_t g = 0; g < G; ++g) {
+        int kg = k;
+        if (auto_k) {
+            std::vector<int64_t> lens;
+            for (int64_t r = go[g]; r < go[g + 1]; ++r)
+                if (row_ok(r)) lens.push_back(row_len(r));
+            kg = estimate_k_host(lens);
+        }
+        gk[g] = (uint8_t)(kg > 64 ? 0 : effective_k(kg));
+        if (gk[g]) present[gk[g]] = true;
+        int64_t cap = 0;
+        for (int64_t r = go[g]; r < go[g + 1]; ++r) {
+            const int64_t len = row_len(r);
+            if (len >= 4) cap += len - 3;
+        }
+        cap_off[g + 1] = cap_off[g] + cap;
+    }
+    KmerCtx* c = nullptr;
+    if (int rc = kmer_ctx(&c)) return rc;
+    hipStream_t s = c->stream;
+    // normalise offsets to start at 0 so only the referenced values travel
+    const int64_t base = n_rows ? (offset_width == 4 ? ((const int32_t*)offsets)[0] : ((const int64_t*)offsets)[0]) : 0;
+    const int64_t vend = n_rows ? (offset_width == 4 ? ((const int32_t*)offsets)[n_rows] : ((const int64_t*)offsets)[n_rows]) : 0;
+    ROGTK_REQUIRE(vend <= values_len, ROGTK_E_INVALID, "kmer: offsets exceed values_len");
+    std::vector<int64_t> offs(n_rows + 1);
+    for (int64_t r = 0; r <= n_rows; ++r)
+        offs[r] = (offset_width == 4 ? (int64_t)((const int32_t*)offsets)[r] : ((const int64_t*)offsets)[r]) - base;
+    std::vector<uint8_t> vbits;
+    if (validity) {
+        vbits.assign((size_t)(n_rows + 7) / 8, 0);
+        for (int64_t r = 0; r < n_rows; ++r)
+            if (row_ok(r)) vbits[r >> 3] |= (uint8_t)(1u << (r & 7));
+    }
+    if (int rc = c->offsets.ensure((size_t)(n_rows + 1) * 8)) return rc;
+    if (int rc = c->values.ensure((size_t)std::max<int64_t>(vend - base, 1))) return rc;
+    if (int rc = c->go.ensure((size_t)(G + 1) * 8)) return rc;
+    if (int rc = c->gk.ensure((size_t)G)) return rc;
+    if (int rc = c->cap_off.ensure((size_t)(G + 1) * 8)) return rc;
+    if (int rc = c->gstat.ensure((size_t)G * 5 * 8)) return rc;
+    if (int rc = c->gstart.ensure((size_t)G * 8)) return rc;
+    if (int rc = c->gcount.ensure((size_t)G * 8)) return rc;
+    if (int rc = c->out_off.ensure((size_t)(G + 1) * 8)) return rc;
+    const int64_t tcap = std::max<int64_t>(cap_off[G], 1);
+    if (int rc = c->t_kmer.ensure((size_t)tcap * 16)) return rc;
+    if (int rc = c->t_ext.ensure((size_t)tcap)) return rc;
+    if (int rc = c->t_cnt.ensure((size_t)tcap * 2)) return rc;
+    if (validity) {
+        if (int rc = c->validity.ensure(vbits.size())) return rc;
+    }
+    ROGTK_HIP_CHECK(hipMemcpyAsync(c->offsets.p, offs.data(), (n_rows + 1) * 8, hipMemcpyHostToDevice, s));
+    if (vend > base)
+        ROGTK_HIP_CHECK(hipMemcpyAsync(c->values.p, values + base, vend - base, hipMemcpyHostToDevice, s));
+    if (validity)
+        ROGTK_HIP_CHECK(hipMemcpyAsync(c->validity.p, vbits.data(), vbits.size(), hipMemcpyHostToDevice, s));
+    ROGTK_HIP_CHECK(hipMemcpyAsync(c->go.p, go.data(), (G + 1) * 8, hipMemcpyHostToDevice, s));
+    ROGTK_HIP_CHECK(hipMemcpyAsync(c->gk.p, gk.data(), G, hipMemcpyHostToDevice, s));
+    ROGTK_HIP_CHECK(hipMemcpyAsync(c->cap_off.p, cap_off.data(), (G + 1) * 8, hipMemcpyHostToDevice, s));
+    ROGTK_HIP_CHECK(hipMemsetAsync(c->gstat.p, 0, G * 5 * 8, s));
+    ROGTK_HIP_CHECK(hipMemsetAsync(c->gcount.p, 0, G * 8, s));
+    for (int K : {4, 8, 16, 32, 64}) {
+        if (!present[K] || n_rows == 0) continue;
+        if (int rc = run_any<8>(c, validity ? c->validity.as<uint8_t>() : nullptr, n_rows, G, K, min_coverage, s))
+            return rc;
+    }
+    // dense packing by group
+    std::vector<int64_t> gcount(G);
+    ROGTK_HIP_CHECK(hipMemcpyAsync(gcount.data(), c->gcount.p, G * 8, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    entry_offsets[0] = 0;
+    for (int64_t g = 0; g < G; ++g) entry_offsets[g + 1] = entry_offsets[g] + gcount[g];
+    const int64_t total = entry_offsets[G];
+    ROGTK_REQUIRE(total <= capacity, ROGTK_E_OVERFLOW, "kmer: %lld entries exceed capacity %lld",
+                  (long long)total, (long long)capacity);
+    if (total > 0) {
+        if (int rc = c->o_kmer.ensure((size_t)total * 16)) return rc;
+        if (int rc = c->o_ext.ensure((size_t)total)) return rc;
+        if (int rc = c->o_cnt.ensure((size_t)total * 2)) return rc;
+        ROGTK_HIP_CHECK(hipMemcpyAsync(c->out_off.p, entry_offsets, (G + 1) * 8, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_pack, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, c->t_kmer.as<uint64_t>(),
+                           c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), G, c->cap_off.as<int64_t>(),
+                           c->gcount.as<int64_t>(), c->out_off.as<int64_t>(), c->o_kmer.as<uint64_t>(),
+                           c->o_ext.as<uint8_t>(), c->o_cnt.as<uint16_t>());
+        ROGTK_HIP_CHECK(hipGetLastError());
+        ROGTK_HIP_CHECK(hipMemcpyAsync(kmers, c->o_kmer.p, total * 16, hipMemcpyDeviceToHost, s));
+        ROGTK_HIP_CHECK(hipMemcpyAsync(exts, c->o_ext.p, total, hipMemcpyDeviceToHost, s));
+        ROGTK_HIP_CHECK(hipMemcpyAsync(counts, c->o_cnt.p, total * 2, hipMemcpyDeviceToHost, s));
+    }
+    std::vector<unsigned long long> st((size_t)G * 5);
+    ROGTK_HIP_CHECK(hipMemcpyAsync(st.data(), c->gstat.p, G * 5 * 8, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    for (int64_t g = 0; g < G; ++g) {
+        group_stats[5 * g + 0] = gk[g];
+        group_stats[5 * g + 1] = (int64_t)st[5 * g + 1];
+        group_stats[5 * g + 2] = gcount[g];
+        group_stats[5 * g + 3] = (int64_t)st[5 * g + 3];
+        group_stats[5 * g + 4] = (int64_t)st[5 * g + 4];
+    }
+    return ROGTK_OK;
+}
+
+}  // extern "C"

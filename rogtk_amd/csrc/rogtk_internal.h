@@ -3,6 +3,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstddef>
 #include <cstdint>
 
 #include "../../include/rogtk_hip.h"
@@ -136,6 +138,31 @@ struct ClusterLayout {
         off_rbits, off_rpref, off_rblksum, off_rblkoff, off_labelcode, total;
 };
 int cluster_layout(int L, int64_t max_distinct, ClusterLayout* out);
+
+// Grow-only device buffer owned by a host-side context.
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    ~DevBuf() {
+        if (p) hipFree(p);
+    }
+    int ensure(size_t bytes) {
+        if (bytes <= cap && p) return ROGTK_OK;
+        if (p) {
+            hipFree(p);
+            p = nullptr;
+            cap = 0;
+        }
+        size_t want = std::max<size_t>(bytes, 256);
+        want = (want + 255) / 256 * 256;
+        ROGTK_HIP_CHECK(hipMalloc(&p, want));
+        cap = want;
+        return ROGTK_OK;
+    }
+    template <class T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+};
+
 
 // XCD-partitioned presence mark (standalone; k_score_packed<..., MARK> is the fused form).
 int launch_cluster_mark(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int L,

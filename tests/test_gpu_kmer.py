@@ -1,0 +1,121 @@
+"""H4 k-mer spectra on the GPU vs the oracle (oracle/kmer_oracle.cpp), bit-exact.
+
+Every output array (k-mer codes, censored exts, saturating counts, per-group entry
+offsets and the 5 per-group stats) must equal the oracle's for the same column and
+groups: effective k 4/8/16/32/64, auto_k, min_coverage, nulls, lowercase, N and
+other bytes (row dropped), empty rows, rows shorter than k, k > 64, many groups.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pyarrow as pa
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rg():
+    import rogtk_amd
+    return rogtk_amd
+
+
+def P():
+    from oracle import pyoracle
+    return pyoracle
+
+
+def _check(rg, items, k, min_cov, auto_k=False, group_offsets=None):
+    col = P().StrCol.from_list(items)
+    ref = P().kmer_spectrum(col, k, min_cov, auto_k, group_offsets)
+    got = rg.kmer_spectrum(pa.array(items, type=pa.large_binary()), k, min_cov, auto_k, group_offsets)
+    assert np.array_equal(got["entry_offsets"], ref["group_offsets"])
+    assert np.array_equal(got["stats"], ref["stats"])
+    for f in ("kmer_hi", "kmer_lo", "exts", "counts"):
+        assert np.array_equal(got[f], ref[f]), f
+    return got
+
+
+def _reads(rng, n, lo, hi, alphabet=b"ACGT"):
+    out = []
+    for _ in range(n):
+        L = int(rng.integers(lo, hi + 1))
+        out.append(bytes(rng.choice(np.frombuffer(alphabet, np.uint8), L)))
+    return out
+
+
+def test_reference_fixture_sequences(rg):
+    """fracture.rs:611-626 test sequences (their 44-bp assembly = 29 16-mers for k=13)."""
+    seqs = [b"GAGACTGCATGGGCTGGTGGGCGTCCGTCTGC", b"GGGCTGGTGGGCGTCCGTCTGCTTTAGTGAGGGT"]
+    for k in (4, 13, 20, 33):
+        _check(rg, seqs, k, 1)
+    got = _check(rg, seqs, 13, 1)
+    contig = b"GAGACTGCATGGGCTGGTGGGCGTCCGTCTGCTTTAGTGAGGGT"
+    want = sorted({contig[i:i + 16] for i in range(len(contig) - 15)})
+    have = [P().kmer_to_str(h, l, 16).encode() for h, l in zip(got["kmer_hi"], got["kmer_lo"])]
+    assert have == want
+
+
+@pytest.mark.parametrize("k", [1, 4, 5, 8, 11, 16, 17, 31, 32, 33, 47, 64, 65, 100])
+@pytest.mark.parametrize("min_cov", [1, 2, 5])
+def test_single_group_all_k(rg, k, min_cov):
+    rng = np.random.default_rng(k * 10 + min_cov)
+    template = _reads(rng, 1, 200, 200)[0]
+    items = []
+    for _ in range(30):  # overlapping fragments of one template -> real coverage
+        a = int(rng.integers(0, 120))
+        items.append(template[a:a + int(rng.integers(20, 80))])
+    items += [None, b"", b"ACGTNACGT" * 4, b"acgtacgtacgtacgtacgtACGTACGTAAACCC", b"AC"]
+    _check(rg, items, k, min_cov)
+
+
+def test_auto_k(rg):
+    rng = np.random.default_rng(5)
+    for lens in ((10, 20), (30, 40), (90, 150), (150, 150), (1, 3), (0, 0)):
+        items = _reads(rng, 12, *lens) + [None]
+        _check(rg, items, 0, 1, auto_k=True)
+    _check(rg, [], 0, 1, auto_k=True)
+    _check(rg, [None, None], 0, 1, auto_k=True)
+
+
+def test_many_groups_mixed(rg):
+    """Many groups, each one polars group: sizes 0..40 rows, mixed validity and bytes."""
+    rng = np.random.default_rng(11)
+    items, go = [], [0]
+    for g in range(300):
+        m = int(rng.integers(0, 40))
+        tpl = _reads(rng, 1, 150, 150)[0]
+        for _ in range(m):
+            r = rng.random()
+            if r < 0.03:
+                items.append(None)
+            elif r < 0.06:
+                items.append(b"ACGTN" + tpl[:40])
+            elif r < 0.09:
+                items.append(tpl[:60].lower())
+            else:
+                a = int(rng.integers(0, 60))
+                items.append(tpl[a:a + int(rng.integers(30, 91))])
+        go.append(len(items))
+    for k, mc in ((17, 3), (13, 1), (31, 2), (33, 2), (7, 4)):
+        _check(rg, items, k, mc, group_offsets=go)
+    _check(rg, items, 0, 2, auto_k=True, group_offsets=go)
+
+
+def test_saturating_count(rg):
+    """> 65535 observations of one k-mer: the count saturates at u16::MAX (CountFilter)."""
+    items = [b"A" * 80] * 1200  # 77 observations of AAAA..(k=4) per row -> 92,400
+    got = _check(rg, items, 4, 1)
+    assert int(got["counts"][0]) == 0xFFFF
+    _check(rg, items, 4, 70000)  # saturated count never reaches min_cov > 65535
+
+
+def test_large_group(rg):
+    """One group of 20k reads (2.4M observations at k_eff 32)."""
+    rng = np.random.default_rng(3)
+    tpl = _reads(rng, 1, 2000, 2000)[0]
+    items = []
+    for _ in range(20000):
+        a = int(rng.integers(0, 1850))
+        items.append(tpl[a:a + 150])
+    _check(rg, items, 17, 20)

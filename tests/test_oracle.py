@@ -154,3 +154,43 @@ def test_cluster_spec_properties():
     assert k == 5 and not valid[-1]
     cid0, _, k0, _ = P.umi_cluster(P.StrCol.from_list(umis), 4, 0)
     assert k0 == 8  # 7 distinct regular + 1 irregular
+
+
+# ---------------------------------------------------------------- H4 k-mer oracle
+def test_kmer_oracle_matches_python_restatement():
+    """oracle/kmer_oracle.cpp vs the independent Python restatement (pyoracle.py)."""
+    import random
+
+    rng = random.Random(1)
+    for trial in range(300):
+        items = []
+        for _ in range(rng.randint(0, 12)):
+            if rng.random() < 0.1:
+                items.append(None)
+                continue
+            alpha = b"ACGTacgtN" if rng.random() < 0.2 else b"ACGT"
+            items.append(bytes(rng.choice(alpha) for _ in range(rng.randint(0, 40))))
+        k = rng.choice([0, 1, 3, 4, 5, 8, 9, 16, 17, 31, 32, 33, 64, 65])
+        mc = rng.choice([0, 1, 1, 2, 3])
+        ak = rng.random() < 0.2
+        r = P.kmer_spectrum(P.StrCol.from_list(items), k, mc, ak)
+        py, st = P.py_kmer_spectrum(items, k, mc, ak)
+        got = [(P.kmer_to_str(h, l, st[0]), int(e), int(c))
+               for h, l, e, c in zip(r["kmer_hi"], r["kmer_lo"], r["exts"], r["counts"])]
+        assert got == py and tuple(r["stats"][0]) == st, (trial, items, k, mc, ak)
+
+
+def test_kmer_oracle_reference_fixture():
+    """fracture.rs:611-626: the two test reads assemble to the 44-bp contig in the
+    comment; at k=13 (effective 16) their valid k-mers are exactly its 29 16-mers,
+    forming one unbranched path (2 terminal ends, 0 isolated)."""
+    seqs = [b"GAGACTGCATGGGCTGGTGGGCGTCCGTCTGC", b"GGGCTGGTGGGCGTCCGTCTGCTTTAGTGAGGGT"]
+    r = P.kmer_spectrum(P.StrCol.from_list(seqs), 13, 1)
+    contig = "GAGACTGCATGGGCTGGTGGGCGTCCGTCTGCTTTAGTGAGGGT"
+    want = sorted({contig[i:i + 16] for i in range(len(contig) - 15)})
+    have = [P.kmer_to_str(h, l, 16) for h, l in zip(r["kmer_hi"], r["kmer_lo"])]
+    assert have == want
+    assert tuple(r["stats"][0]) == (16, 2, 29, 2, 0)
+    # k=4 (fracture.rs:685 test_compare_assembly_methods): non-empty spectrum
+    r4 = P.kmer_spectrum(P.StrCol.from_list(seqs), 4, 1)
+    assert r4["stats"][0][0] == 4 and r4["stats"][0][2] > 0
