@@ -203,6 +203,14 @@ int rogtk_umi_cluster_host(const void* offsets, int offset_width, const uint8_t*
  * n_sequences, node_count, terminal_count, isolated_count}.
  * capacity >= rogtk_kmer_capacity() always suffices (ROGTK_E_OVERFLOW otherwise). */
 int rogtk_kmer_capacity(const void* offsets, int offset_width, int64_t n_rows, int64_t* capacity);
+/* Path selection for the calling thread (default 1): groups with <= 2048 k-mer
+ * observations, rows <= 2048 bases and k_eff <= 32 run entirely in LDS (one
+ * workgroup per group); 0 sends every group through the global radix-sort path.
+ * Results are identical; tests use this to cover both paths. */
+int rogtk_kmer_set_path(int lds_small_groups);
+/* Groups of the calling thread's last rogtk_kmer_spectrum_host call per path:
+ * out2[0] = LDS path, out2[1] = global path (groups with k > 64 count in neither). */
+int rogtk_kmer_path_stats(int64_t* out2);
 int rogtk_kmer_spectrum_host(const void* offsets, int offset_width, const uint8_t* values,
                              int64_t values_len, const uint8_t* validity, int64_t validity_offset,
                              int64_t n_rows, const int64_t* group_offsets, int64_t n_groups, int k,

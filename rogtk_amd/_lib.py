@@ -73,6 +73,8 @@ SIGNATURES = {
     "rogtk_umi_cluster_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _P_I64,
                                _P_I32],
     "rogtk_kmer_capacity": [_vp, _i32, _i64, _P_I64],
+    "rogtk_kmer_set_path": [_i32],
+    "rogtk_kmer_path_stats": [_P_I64],
     "rogtk_kmer_spectrum_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i32, _i32, _i64, _i64, _vp,
                                  _vp, _vp, _vp, _vp],
     "rogtk_profile_enable": [_i32],

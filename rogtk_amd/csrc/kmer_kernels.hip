@@ -215,10 +215,11 @@ __global__ __launch_bounds__(kBlock) void k_group_ranges(const uint32_t* __restr
 }
 
 __global__ __launch_bounds__(kBlock) void k_group_counts(const uint8_t* __restrict__ gk, int K, int64_t G,
+                                                         const uint8_t* __restrict__ gsmall,
                                                          const int64_t* __restrict__ gstart,
                                                          int64_t* __restrict__ gcount) {
     for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < G; g += (int64_t)gridDim.x * kBlock)
-        if (gk[g] == K && gcount[g] > 0) gcount[g] -= gstart[g];
+        if (gk[g] == K && !(gsmall && gsmall[g]) && gcount[g] > 0) gcount[g] -= gstart[g];
 }
 
 // remove_censored_exts + terminal / isolated counts + output at the group's capacity offset
@@ -300,6 +301,223 @@ __global__ __launch_bounds__(kBlock) void k_pack(const uint64_t* __restrict__ t_
     }
 }
 
+// ----------------------------------------------------------- LDS fast path
+// One workgroup per small group (<= kLdsObs observations, rows <= kLdsRowBases,
+// k_eff <= 32): reads are packed to 2-bit words in LDS, every observation is
+// inserted into an LDS hash table (64-bit CAS on the key; the count and the OR of
+// exts share one u32: count in bits 0..23, exts in 24..31), the valid entries are
+// compacted, bitonic-sorted and censored by binary search, all in LDS. The all-ones
+// key (TTT..T at k = 32) equals the empty marker and gets a dedicated slot.
+constexpr int kLdsObs = 2048;
+constexpr int kLdsSlots = 2 * kLdsObs;   // power of two, load factor <= 0.5
+constexpr int kLdsRowBases = 2048;       // per-wave packed row buffer
+constexpr int kLdsRowWords = kLdsRowBases / 32 + 1;
+constexpr unsigned long long kEmpty = ~0ull;
+
+__device__ __forceinline__ uint32_t pk_base(const uint64_t* pk, int64_t p) {
+    return (uint32_t)(pk[p >> 5] >> (62 - 2 * (p & 31))) & 3u;
+}
+
+__device__ __forceinline__ bool kless(uint64_t ka, uint32_t ia, uint64_t kb, uint32_t ib) {
+    return ka < kb || (ka == kb && (ia >> 31) < (ib >> 31));  // real entries before pads
+}
+
+template <int OW>
+__global__ __launch_bounds__(kBlock) void k_kmer_lds(const void* offsets, const uint8_t* __restrict__ values,
+                                                     const int64_t* __restrict__ go, int64_t G,
+                                                     const uint8_t* __restrict__ gsmall, int K, int64_t min_cov,
+                                                     const int64_t* __restrict__ row_obs,
+                                                     const int64_t* __restrict__ cap_off,
+                                                     uint64_t* __restrict__ t_kmer, uint8_t* __restrict__ t_ext,
+                                                     uint16_t* __restrict__ t_cnt, int64_t* __restrict__ gcount,
+                                                     unsigned long long* __restrict__ gstat) {
+    __shared__ unsigned long long tkey[kLdsSlots + 1];
+    __shared__ uint32_t tinfo[kLdsSlots + 1];
+    __shared__ uint64_t pk[kWavesPerBlock][kLdsRowWords];
+    __shared__ uint64_t vkey[kLdsObs];
+    __shared__ uint32_t vinfo[kLdsObs];  // count | exts << 16 | pad << 31
+    __shared__ uint32_t scan[kBlock];
+    __shared__ uint32_t s_term, s_iso;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int hbits = 31 - __clz(kLdsSlots);
+    const uint64_t kmask = K == 32 ? ~0ull : ((1ull << (2 * K)) - 1ull);
+    for (int64_t g = blockIdx.x; g < G; g += gridDim.x) {
+        if (!gsmall[g]) continue;  // uniform per block
+        for (int i = tid; i <= kLdsSlots; i += kBlock) {
+            tkey[i] = kEmpty;
+            tinfo[i] = 0;
+        }
+        if (tid == 0) {
+            s_term = 0;
+            s_iso = 0;
+        }
+        __syncthreads();
+        const int64_t r0 = go[g], r1 = go[g + 1];
+        for (int64_t rb = r0; rb < r1; rb += kWavesPerBlock) {  // uniform trip count
+            const int64_t r = rb + wave;
+            int64_t nobs = 0, st = 0, len = 0;
+            if (r < r1) {
+                nobs = row_obs[r];
+                if (nobs) span<OW>(offsets, r, st, len);
+            }
+            const int nw = (int)((len + 31) >> 5) + 1;
+            for (int w = lane; w < nw; w += 64) pk[wave][w] = 0;
+            __syncthreads();
+            for (int64_t j = lane; j < len && nobs; j += 64)
+                atomicOr((unsigned long long*)&pk[wave][j >> 5],
+                         (unsigned long long)base2(values[st + j]) << (62 - 2 * (j & 31)));
+            __syncthreads();
+            for (int64_t p = lane; p < nobs; p += 64) {
+                const int b = (int)(2 * (p & 31));
+                const uint64_t w0 = pk[wave][p >> 5], w1 = pk[wave][(p >> 5) + 1];
+                const uint64_t top = b ? (w0 << b) | (w1 >> (64 - b)) : w0;
+                const uint64_t key = (top >> (64 - 2 * K)) & kmask;
+                uint32_t e = 0;
+                if (p > 0) e |= 1u << pk_base(pk[wave], p - 1);
+                if (p + K < len) e |= 1u << (4 + pk_base(pk[wave], p + K));
+                uint32_t slot;
+                if (key == kEmpty) {
+                    slot = kLdsSlots;
+                } else {
+                    slot = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - hbits));
+                    while (true) {
+                        const unsigned long long prev = atomicCAS(&tkey[slot], kEmpty, (unsigned long long)key);
+                        if (prev == kEmpty || prev == key) break;
+                        slot = (slot + 1) & (kLdsSlots - 1);
+                    }
+                }
+                atomicAdd(&tinfo[slot], 1u);
+                if (e) atomicOr(&tinfo[slot], e << 24);
+            }
+            __syncthreads();
+        }
+        // CountFilter + compaction (slot ranges per thread keep the pass simple)
+        constexpr int per = (kLdsSlots + 1 + kBlock - 1) / kBlock;
+        const int s0 = tid * per, s1 = min(s0 + per, kLdsSlots + 1);
+        uint32_t mine = 0;
+        for (int i = s0; i < s1; ++i) {
+            const uint32_t c = tinfo[i] & 0xFFFFFFu;
+            if (c && (int64_t)min(c, 0xFFFFu) >= min_cov) ++mine;
+        }
+        scan[tid] = mine;
+        __syncthreads();
+        for (int off = 1; off < kBlock; off <<= 1) {  // inclusive Hillis-Steele scan
+            const uint32_t v = tid >= off ? scan[tid - off] : 0u;
+            __syncthreads();
+            scan[tid] += v;
+            __syncthreads();
+        }
+        const uint32_t nv = scan[kBlock - 1];
+        uint32_t w = scan[tid] - mine;
+        for (int i = s0; i < s1; ++i) {
+            const uint32_t c = tinfo[i] & 0xFFFFFFu;
+            if (c && (int64_t)min(c, 0xFFFFu) >= min_cov) {
+                vkey[w] = i == kLdsSlots ? kEmpty : tkey[i];
+                vinfo[w] = min(c, 0xFFFFu) | ((tinfo[i] >> 24) << 16);
+                ++w;
+            }
+        }
+        uint32_t P = 2;
+        while (P < nv) P <<= 1;
+        for (uint32_t i = nv + tid; i < P; i += kBlock) {
+            vkey[i] = kEmpty;
+            vinfo[i] = 1u << 31;
+        }
+        __syncthreads();
+        for (uint32_t k2 = 2; k2 <= P; k2 <<= 1) {  // bitonic sort, ascending
+            for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = tid; i < P; i += kBlock) {
+                    const uint32_t ij = i ^ j;
+                    if (ij > i) {
+                        const uint64_t ka = vkey[i], kb = vkey[ij];
+                        const uint32_t ia = vinfo[i], ib = vinfo[ij];
+                        const bool up = (i & k2) == 0;
+                        if (kless(kb, ib, ka, ia) == up) {
+                            vkey[i] = kb;
+                            vkey[ij] = ka;
+                            vinfo[i] = ib;
+                            vinfo[ij] = ia;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        // remove_censored_exts + output at the group's capacity offset
+        const int64_t base = cap_off[g];
+        for (uint32_t i = tid; i < nv; i += kBlock) {
+            const uint64_t key = vkey[i];
+            const uint32_t info = vinfo[i];
+            const uint32_t e = (info >> 16) & 0xFFu;
+            uint32_t ne = 0;
+            for (int bit = 0; bit < 8; ++bit) {
+                if (!((e >> bit) & 1u)) continue;
+                const uint64_t b = (uint64_t)(bit & 3);
+                const uint64_t nb = bit < 4 ? (key >> 2) | (b << (2 * K - 2)) : ((key << 2) | b) & kmask;
+                uint32_t a = 0, c = nv;
+                while (a < c) {
+                    const uint32_t m = (a + c) >> 1;
+                    if (vkey[m] < nb) a = m + 1;
+                    else c = m;
+                }
+                if (a < nv && vkey[a] == nb) ne |= 1u << bit;
+            }
+            const int64_t o = base + i;
+            t_kmer[2 * o] = 0;
+            t_kmer[2 * o + 1] = key;
+            t_ext[o] = (uint8_t)ne;
+            t_cnt[o] = (uint16_t)(info & 0xFFFFu);
+            const bool l0 = (ne & 0xFu) == 0, r0 = (ne >> 4) == 0;
+            if (l0 || r0) atomicAdd(&s_term, 1u);
+            if (l0 && r0) atomicAdd(&s_iso, 1u);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            gcount[g] = nv;
+            gstat[5 * g + 3] = s_term;
+            gstat[5 * g + 4] = s_iso;
+        }
+        __syncthreads();
+    }
+}
+
+// Per group of effective k K: observation total and longest row decide the path.
+__global__ __launch_bounds__(kBlock) void k_group_classify(const void* offsets, int ow, const int64_t* __restrict__ go,
+                                                           int64_t G, const uint8_t* __restrict__ gk, int K,
+                                                           const int64_t* __restrict__ row_obs,
+                                                           uint8_t* __restrict__ gsmall) {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
+    for (int64_t g = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); g < G; g += waves) {
+        if (gk[g] != K) {
+            if (lane == 0) gsmall[g] = 0;
+            continue;
+        }
+        int64_t obs = 0, maxlen = 0;
+        for (int64_t r = go[g] + lane; r < go[g + 1]; r += 64) {
+            obs += row_obs[r];
+            if (row_obs[r]) {
+                const int64_t len = ow == 4 ? (int64_t)((const int32_t*)offsets)[r + 1] - ((const int32_t*)offsets)[r]
+                                            : ((const int64_t*)offsets)[r + 1] - ((const int64_t*)offsets)[r];
+                maxlen = max(maxlen, len);
+            }
+        }
+        for (int m = 32; m > 0; m >>= 1) {
+            obs += __shfl_xor(obs, m);
+            maxlen = max(maxlen, __shfl_xor(maxlen, m));
+        }
+        if (lane == 0) gsmall[g] = (K <= 32 && obs <= kLdsObs && maxlen <= kLdsRowBases) ? 1 : 0;
+    }
+}
+
+// rows of LDS-path groups leave the global path
+__global__ __launch_bounds__(kBlock) void k_drop_small_rows(const uint32_t* __restrict__ row_group,
+                                                            const uint8_t* __restrict__ gsmall, int64_t n_rows,
+                                                            int64_t* __restrict__ row_obs) {
+    for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < n_rows; r += (int64_t)gridDim.x * kBlock)
+        if (gsmall[row_group[r]]) row_obs[r] = 0;
+}
+
 int grid_for(int64_t n, int cap = 8192) {
     int64_t g = (n + kBlock - 1) / kBlock;
     if (g < 1) g = 1;
@@ -334,7 +552,9 @@ struct KmerCtx {
     DevBuf row_group, row_obs, obs_off;
     DevBuf key_lo, key_hi, ext, grp, idx, perm_a, perm_b, tmp_u64, tmp_u32;
     DevBuf s_lo, s_hi, s_ext, s_grp, head, rid, r_valid, r_first, r_ext, r_cnt, vpos;
-    DevBuf v_lo, v_hi, v_grp, v_ext, v_cnt, t_kmer, t_ext, t_cnt, o_kmer, o_ext, o_cnt, cub;
+    DevBuf v_lo, v_hi, v_grp, v_ext, v_cnt, t_kmer, t_ext, t_cnt, o_kmer, o_ext, o_cnt, cub, gsmall;
+    bool lds_path = true;  // rogtk_kmer_set_path(): tests force the global path
+    int64_t last_lds_groups = 0, last_global_groups = 0;  // rogtk_kmer_path_stats()
     ~KmerCtx() {
         if (stream) hipStreamDestroy(stream);
     }
@@ -391,7 +611,7 @@ int bits_for(uint64_t v) {
 
 template <int OW, bool WIDE>
 int run_class(KmerCtx* c, const uint8_t* validity, int64_t n_rows, int64_t G, int K, int64_t min_cov,
-              hipStream_t s) {
+              hipStream_t s, const std::vector<uint8_t>& gk_host) {
     const int64_t* go = c->go.as<int64_t>();
     unsigned long long* gstat = c->gstat.as<unsigned long long>();
     if (int rc = c->row_group.ensure(n_rows * 4)) return rc;
@@ -402,11 +622,33 @@ int run_class(KmerCtx* c, const uint8_t* validity, int64_t n_rows, int64_t G, in
                        validity, (int64_t)0, n_rows, go, G,
                        c->gk.as<uint8_t>(), K, c->row_group.as<uint32_t>(), c->row_obs.as<int64_t>(), gstat);
     ROGTK_HIP_CHECK(hipGetLastError());
+    if (c->lds_path && K <= 32) {
+        if (int rc = c->gsmall.ensure((size_t)G)) return rc;
+        hipLaunchKernelGGL(k_group_classify, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, c->offsets.p, OW, go,
+                           G, c->gk.as<uint8_t>(), K, c->row_obs.as<int64_t>(), c->gsmall.as<uint8_t>());
+        hipLaunchKernelGGL((k_kmer_lds<OW>), dim3((unsigned)std::min<int64_t>(G, 65536)), dim3(kBlock), 0, s,
+                           c->offsets.p, c->values.as<uint8_t>(), go, G, c->gsmall.as<uint8_t>(), K, min_cov,
+                           c->row_obs.as<int64_t>(), c->cap_off.as<int64_t>(), c->t_kmer.as<uint64_t>(),
+                           c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), c->gcount.as<int64_t>(), gstat);
+        hipLaunchKernelGGL(k_drop_small_rows, dim3(grid_for(n_rows)), dim3(kBlock), 0, s, c->row_group.as<uint32_t>(),
+                           c->gsmall.as<uint8_t>(), n_rows, c->row_obs.as<int64_t>());
+        ROGTK_HIP_CHECK(hipGetLastError());
+    }
     if (int rc = cub_exsum_i64(c, c->row_obs.as<int64_t>(), c->obs_off.as<int64_t>(), n_rows, s)) return rc;
+    std::vector<uint8_t> small;
+    if (c->lds_path && K <= 32) {
+        small.resize(G);
+        ROGTK_HIP_CHECK(hipMemcpyAsync(small.data(), c->gsmall.p, G, hipMemcpyDeviceToHost, s));
+    }
     int64_t last[2] = {0, 0};
     ROGTK_HIP_CHECK(hipMemcpyAsync(&last[0], c->obs_off.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
     ROGTK_HIP_CHECK(hipMemcpyAsync(&last[1], c->row_obs.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
     ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    for (int64_t g = 0; g < G; ++g) {
+        if (gk_host[g] != K) continue;
+        if (!small.empty() && small[g]) ++c->last_lds_groups;
+        else ++c->last_global_groups;
+    }
     const int64_t T = last[0] + last[1];
     if (T == 0) return ROGTK_OK;
     ROGTK_REQUIRE(T <= kMaxObsPerLaunch, ROGTK_E_UNSUPPORTED,
@@ -491,7 +733,8 @@ int run_class(KmerCtx* c, const uint8_t* validity, int64_t n_rows, int64_t G, in
     hipLaunchKernelGGL(k_group_ranges, dim3(gv), dim3(kBlock), 0, s, c->v_grp.as<uint32_t>(), nv,
                        c->gstart.as<int64_t>(), c->gcount.as<int64_t>());
     hipLaunchKernelGGL(k_group_counts, dim3(grid_for(G)), dim3(kBlock), 0, s, c->gk.as<uint8_t>(), K, G,
-                       c->gstart.as<int64_t>(), c->gcount.as<int64_t>());
+                       (c->lds_path && K <= 32) ? c->gsmall.as<uint8_t>() : nullptr, c->gstart.as<int64_t>(),
+                       c->gcount.as<int64_t>());
     hipLaunchKernelGGL((k_censor<WIDE>), dim3(gv), dim3(kBlock), 0, s, c->v_lo.as<uint64_t>(),
                        c->v_hi.as<uint64_t>(), c->v_grp.as<uint32_t>(), c->v_ext.as<uint8_t>(),
                        c->v_cnt.as<uint16_t>(), nv, K, c->gstart.as<int64_t>(), c->gcount.as<int64_t>(),
@@ -503,9 +746,9 @@ int run_class(KmerCtx* c, const uint8_t* validity, int64_t n_rows, int64_t G, in
 
 template <int OW>
 int run_any(KmerCtx* c, const uint8_t* validity, int64_t n_rows, int64_t G, int K, int64_t min_cov,
-            hipStream_t s) {
-    return K == 64 ? run_class<OW, true>(c, validity, n_rows, G, K, min_cov, s)
-                   : run_class<OW, false>(c, validity, n_rows, G, K, min_cov, s);
+            hipStream_t s, const std::vector<uint8_t>& gk) {
+    return K == 64 ? run_class<OW, true>(c, validity, n_rows, G, K, min_cov, s, gk)
+                   : run_class<OW, false>(c, validity, n_rows, G, K, min_cov, s, gk);
 }
 
 }  // namespace
@@ -514,6 +757,22 @@ int run_any(KmerCtx* c, const uint8_t* validity, int64_t n_rows, int64_t G, int 
 using namespace rogtk;
 
 extern "C" {
+
+int rogtk_kmer_set_path(int lds_small_groups) {
+    KmerCtx* c = nullptr;
+    if (int rc = kmer_ctx(&c)) return rc;
+    c->lds_path = lds_small_groups != 0;
+    return ROGTK_OK;
+}
+
+int rogtk_kmer_path_stats(int64_t* out2) {
+    ROGTK_REQUIRE(out2, ROGTK_E_INVALID, "kmer_path_stats: NULL");
+    KmerCtx* c = nullptr;
+    if (int rc = kmer_ctx(&c)) return rc;
+    out2[0] = c->last_lds_groups;
+    out2[1] = c->last_global_groups;
+    return ROGTK_OK;
+}
 
 int rogtk_kmer_capacity(const void* offsets, int offset_width, int64_t n_rows, int64_t* capacity) {
     ROGTK_REQUIRE(capacity && (n_rows == 0 || offsets), ROGTK_E_INVALID, "kmer_capacity: NULL argument");
@@ -626,9 +885,10 @@ int rogtk_kmer_spectrum_host(const void* offsets, int offset_width, const uint8_
     ROGTK_HIP_CHECK(hipMemcpyAsync(c->cap_off.p, cap_off.data(), (G + 1) * 8, hipMemcpyHostToDevice, s));
     ROGTK_HIP_CHECK(hipMemsetAsync(c->gstat.p, 0, G * 5 * 8, s));
     ROGTK_HIP_CHECK(hipMemsetAsync(c->gcount.p, 0, G * 8, s));
+    c->last_lds_groups = c->last_global_groups = 0;
     for (int K : {4, 8, 16, 32, 64}) {
         if (!present[K] || n_rows == 0) continue;
-        if (int rc = run_any<8>(c, validity ? c->validity.as<uint8_t>() : nullptr, n_rows, G, K, min_coverage, s))
+        if (int rc = run_any<8>(c, validity ? c->validity.as<uint8_t>() : nullptr, n_rows, G, K, min_coverage, s, gk))
             return rc;
     }
     // dense packing by group

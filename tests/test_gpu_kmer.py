@@ -12,12 +12,20 @@ import pyarrow as pa
 import pytest
 
 pytestmark = pytest.mark.gpu
+_LAST_MODE = [1]
 
 
-@pytest.fixture(scope="module")
-def rg():
+@pytest.fixture(scope="module", params=["lds", "global"])
+def rg(request):
+    """Every test runs twice: small groups in LDS (default) and all groups through
+    the global radix-sort path (rogtk_kmer_set_path(0))."""
     import rogtk_amd
-    return rogtk_amd
+    from rogtk_amd import _lib
+
+    _LAST_MODE[0] = 1 if request.param == "lds" else 0
+    _lib.call("rogtk_kmer_set_path", _LAST_MODE[0])
+    yield rogtk_amd
+    _lib.call("rogtk_kmer_set_path", 1)
 
 
 def P():
@@ -79,11 +87,12 @@ def test_auto_k(rg):
 
 
 def test_many_groups_mixed(rg):
-    """Many groups, each one polars group: sizes 0..40 rows, mixed validity and bytes."""
+    """Many groups, each one polars group: sizes 0..100 rows (small ones take the LDS
+    path, the larger ones the global path in the same call), mixed validity and bytes."""
     rng = np.random.default_rng(11)
     items, go = [], [0]
     for g in range(300):
-        m = int(rng.integers(0, 40))
+        m = int(rng.integers(0, 40)) if rng.random() < 0.85 else int(rng.integers(60, 100))
         tpl = _reads(rng, 1, 150, 150)[0]
         for _ in range(m):
             r = rng.random()
@@ -97,8 +106,18 @@ def test_many_groups_mixed(rg):
                 a = int(rng.integers(0, 60))
                 items.append(tpl[a:a + int(rng.integers(30, 91))])
         go.append(len(items))
+    import ctypes
+
+    from rogtk_amd import _lib
+
     for k, mc in ((17, 3), (13, 1), (31, 2), (33, 2), (7, 4)):
         _check(rg, items, k, mc, group_offsets=go)
+        paths = (ctypes.c_int64 * 2)()
+        _lib.call("rogtk_kmer_path_stats", paths)
+        if k > 32 or _LAST_MODE[0] == 0:
+            assert paths[0] == 0 and paths[1] == 300
+        else:
+            assert paths[0] > 100 and paths[1] > 10 and paths[0] + paths[1] == 300, tuple(paths)
     _check(rg, items, 0, 2, auto_k=True, group_offsets=go)
 
 
