@@ -208,6 +208,24 @@ int rogtk_kmer_capacity(const void* offsets, int offset_width, int64_t n_rows, i
  * workgroup per group); 0 sends every group through the global radix-sort path.
  * Results are identical; tests use this to cover both paths. */
 int rogtk_kmer_set_path(int lds_small_groups);
+/* Device-resident form (Level 1): the column (int64 offsets, values, optional
+ * validity), the optional grouping permutation rows[n_rows] (grouped row r is
+ * column row rows[r]; NULL = identity) and group_offsets[n_groups + 1] over the
+ * grouped rows are DEVICE buffers, as are the outputs (layout as above; kmers 2
+ * words per entry). One requested k for all groups (no auto_k). Work is enqueued on
+ * `stream`, but the call synchronises it: the global path sizes its buffers from
+ * the data. *n_entries (host) = total entries; ROGTK_E_OVERFLOW if > capacity
+ * (which rogtk_kmer_capacity over the same rows bounds). */
+int rogtk_kmer_spectrum_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* validity,
+                            int64_t validity_offset, const int64_t* rows, int64_t n_rows,
+                            const int64_t* group_offsets, int64_t n_groups, int k, int64_t min_coverage,
+                            int64_t capacity, uint64_t* kmers, uint8_t* exts, uint16_t* counts,
+                            int64_t* entry_offsets, int64_t* group_stats, int64_t* n_entries, void* stream);
+/* polars group_by over u32 keys on the device (e.g. H3 cluster ids): rows_out[n] =
+ * row indices ordered by key (stable), group_offsets_out[0 .. *n_groups] their
+ * group boundaries (capacity n + 1). Synchronises the stream. */
+int rogtk_group_by_key(const uint32_t* keys, int64_t n, int64_t* rows_out, int64_t* group_offsets_out,
+                       int64_t* n_groups, void* stream);
 /* Groups of the calling thread's last rogtk_kmer_spectrum_host call per path:
  * out2[0] = LDS path, out2[1] = global path (groups with k > 64 count in neither). */
 int rogtk_kmer_path_stats(int64_t* out2);

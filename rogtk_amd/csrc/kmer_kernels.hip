@@ -67,6 +67,7 @@ __device__ __forceinline__ int64_t group_of(const int64_t* go, int64_t G, int64_
 template <int OW>
 __global__ __launch_bounds__(kBlock) void k_kmer_rows(const void* offsets, const uint8_t* __restrict__ values,
                                                       const uint8_t* __restrict__ validity, int64_t voff,
+                                                      const int64_t* __restrict__ rows,
                                                       int64_t n_rows, const int64_t* __restrict__ go, int64_t G,
                                                       const uint8_t* __restrict__ gk, int K,
                                                       uint32_t* __restrict__ row_group, int64_t* __restrict__ row_obs,
@@ -75,15 +76,16 @@ __global__ __launch_bounds__(kBlock) void k_kmer_rows(const void* offsets, const
     const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
     for (int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); r < n_rows; r += waves) {
         const int64_t g = group_of(go, G, r);
+        const int64_t pr = rows ? rows[r] : r;  // physical row of grouped row r
         bool valid = gk[g] == K;
         if (valid && validity) {
-            const int64_t b = voff + r;
+            const int64_t b = voff + pr;
             valid = (validity[b >> 3] >> (b & 7)) & 1;
         }
         int64_t st = 0, len = 0;
         bool ok = false;
         if (valid) {
-            span<OW>(offsets, r, st, len);
+            span<OW>(offsets, pr, st, len);
             bool bad = false;
             for (int64_t j = lane; j < len; j += 64) bad |= !acgt(values[st + j]);
             ok = __ballot(bad) == 0;
@@ -98,7 +100,7 @@ __global__ __launch_bounds__(kBlock) void k_kmer_rows(const void* offsets, const
 
 template <int OW, bool WIDE>
 __global__ __launch_bounds__(kBlock) void k_kmer_emit(const void* offsets, const uint8_t* __restrict__ values,
-                                                      int64_t n_rows, int K, const uint32_t* __restrict__ row_group,
+                                                      const int64_t* __restrict__ rows, int64_t n_rows, int K, const uint32_t* __restrict__ row_group,
                                                       const int64_t* __restrict__ row_obs,
                                                       const int64_t* __restrict__ obs_off,
                                                       uint64_t* __restrict__ key_lo, uint64_t* __restrict__ key_hi,
@@ -110,7 +112,7 @@ __global__ __launch_bounds__(kBlock) void k_kmer_emit(const void* offsets, const
         const int64_t nobs = row_obs[r];
         if (nobs == 0) continue;
         int64_t st, len;
-        span<OW>(offsets, r, st, len);
+        span<OW>(offsets, rows ? rows[r] : r, st, len);
         const uint8_t* s = values + st;
         const int64_t o0 = obs_off[r];
         const uint32_t g = row_group[r];
@@ -324,6 +326,7 @@ __device__ __forceinline__ bool kless(uint64_t ka, uint32_t ia, uint64_t kb, uin
 
 template <int OW>
 __global__ __launch_bounds__(kBlock) void k_kmer_lds(const void* offsets, const uint8_t* __restrict__ values,
+                                                     const int64_t* __restrict__ rows,
                                                      const int64_t* __restrict__ go, int64_t G,
                                                      const uint8_t* __restrict__ gsmall, int K, int64_t min_cov,
                                                      const int64_t* __restrict__ row_obs,
@@ -358,7 +361,7 @@ __global__ __launch_bounds__(kBlock) void k_kmer_lds(const void* offsets, const 
             int64_t nobs = 0, st = 0, len = 0;
             if (r < r1) {
                 nobs = row_obs[r];
-                if (nobs) span<OW>(offsets, r, st, len);
+                if (nobs) span<OW>(offsets, rows ? rows[r] : r, st, len);
             }
             const int nw = (int)((len + 31) >> 5) + 1;
             for (int w = lane; w < nw; w += 64) pk[wave][w] = 0;
@@ -482,7 +485,9 @@ __global__ __launch_bounds__(kBlock) void k_kmer_lds(const void* offsets, const 
 }
 
 // Per group of effective k K: observation total and longest row decide the path.
-__global__ __launch_bounds__(kBlock) void k_group_classify(const void* offsets, int ow, const int64_t* __restrict__ go,
+__global__ __launch_bounds__(kBlock) void k_group_classify(const void* offsets, int ow,
+                                                           const int64_t* __restrict__ rows,
+                                                           const int64_t* __restrict__ go,
                                                            int64_t G, const uint8_t* __restrict__ gk, int K,
                                                            const int64_t* __restrict__ row_obs,
                                                            uint8_t* __restrict__ gsmall) {
@@ -497,8 +502,9 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const void* offsets, 
         for (int64_t r = go[g] + lane; r < go[g + 1]; r += 64) {
             obs += row_obs[r];
             if (row_obs[r]) {
-                const int64_t len = ow == 4 ? (int64_t)((const int32_t*)offsets)[r + 1] - ((const int32_t*)offsets)[r]
-                                            : ((const int64_t*)offsets)[r + 1] - ((const int64_t*)offsets)[r];
+                const int64_t pr = rows ? rows[r] : r;
+                const int64_t len = ow == 4 ? (int64_t)((const int32_t*)offsets)[pr + 1] - ((const int32_t*)offsets)[pr]
+                                            : ((const int64_t*)offsets)[pr + 1] - ((const int64_t*)offsets)[pr];
                 maxlen = max(maxlen, len);
             }
         }
@@ -516,6 +522,61 @@ __global__ __launch_bounds__(kBlock) void k_drop_small_rows(const uint32_t* __re
                                                             int64_t* __restrict__ row_obs) {
     for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < n_rows; r += (int64_t)gridDim.x * kBlock)
         if (gsmall[row_group[r]]) row_obs[r] = 0;
+}
+
+// per-group capacity: sum over its rows of max(0, len - 3) (k_eff >= 4)
+__global__ __launch_bounds__(kBlock) void k_group_caps(const int64_t* __restrict__ offsets,
+                                                       const int64_t* __restrict__ rows,
+                                                       const int64_t* __restrict__ go, int64_t G,
+                                                       int64_t* __restrict__ caps) {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
+    for (int64_t g = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); g < G; g += waves) {
+        int64_t t = 0;
+        for (int64_t r = go[g] + lane; r < go[g + 1]; r += 64) {
+            const int64_t pr = rows ? rows[r] : r;
+            const int64_t len = offsets[pr + 1] - offsets[pr];
+            if (len >= 4) t += len - 3;
+        }
+        for (int m = 32; m > 0; m >>= 1) t += __shfl_xor(t, m);
+        if (lane == 0) caps[g] = t;
+    }
+}
+
+__global__ void k_tail_sum(const int64_t* __restrict__ pre, const int64_t* __restrict__ vals, int64_t G,
+                           int64_t* __restrict__ out_last) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *out_last = G ? pre[G - 1] + vals[G - 1] : 0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_group_stats_out(const unsigned long long* __restrict__ gstat,
+                                                            const int64_t* __restrict__ gcount, int64_t G, int K,
+                                                            int64_t* __restrict__ out) {
+    for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < G; g += (int64_t)gridDim.x * kBlock) {
+        out[5 * g + 0] = K;
+        out[5 * g + 1] = K ? (int64_t)gstat[5 * g + 1] : 0;
+        out[5 * g + 2] = gcount[g];
+        out[5 * g + 3] = (int64_t)gstat[5 * g + 3];
+        out[5 * g + 4] = (int64_t)gstat[5 * g + 4];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_iota64(int64_t* __restrict__ out, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) out[i] = i;
+}
+
+__global__ __launch_bounds__(kBlock) void k_key_heads(const uint32_t* __restrict__ k, int64_t n,
+                                                      uint32_t* __restrict__ head) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+        head[i] = (i == 0 || k[i] != k[i - 1]) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void k_key_offsets(const uint32_t* __restrict__ head,
+                                                        const uint32_t* __restrict__ gid, int64_t n,
+                                                        int64_t* __restrict__ go) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        if (head[i]) go[gid[i]] = i;                    // exclusive scan: a head's group = gid
+        if (i == n - 1) go[gid[i] + head[i]] = n;       // row i's group = gid + head - 1
+    }
 }
 
 int grid_for(int64_t n, int cap = 8192) {
@@ -552,7 +613,7 @@ struct KmerCtx {
     DevBuf row_group, row_obs, obs_off;
     DevBuf key_lo, key_hi, ext, grp, idx, perm_a, perm_b, tmp_u64, tmp_u32;
     DevBuf s_lo, s_hi, s_ext, s_grp, head, rid, r_valid, r_first, r_ext, r_cnt, vpos;
-    DevBuf v_lo, v_hi, v_grp, v_ext, v_cnt, t_kmer, t_ext, t_cnt, o_kmer, o_ext, o_cnt, cub, gsmall;
+    DevBuf v_lo, v_hi, v_grp, v_ext, v_cnt, t_kmer, t_ext, t_cnt, o_kmer, o_ext, o_cnt, cub, gsmall, caps, scal;
     bool lds_path = true;  // rogtk_kmer_set_path(): tests force the global path
     int64_t last_lds_groups = 0, last_global_groups = 0;  // rogtk_kmer_path_stats()
     ~KmerCtx() {
@@ -609,27 +670,42 @@ int bits_for(uint64_t v) {
     return b;
 }
 
+// Inputs / per-group outputs of one spectrum call (device pointers). Offsets are
+// int64; rows (optional) maps grouped row r to its physical row.
+struct KIn {
+    const int64_t* offsets;
+    const uint8_t* values;
+    const uint8_t* validity;
+    int64_t voff;
+    const int64_t* rows;
+    const int64_t* go;
+    const uint8_t* gk;
+    const int64_t* cap_off;
+    unsigned long long* gstat;  // G x 5
+    int64_t* gcount;            // G
+};
+
 template <int OW, bool WIDE>
-int run_class(KmerCtx* c, const uint8_t* validity, int64_t n_rows, int64_t G, int K, int64_t min_cov,
-              hipStream_t s, const std::vector<uint8_t>& gk_host) {
-    const int64_t* go = c->go.as<int64_t>();
-    unsigned long long* gstat = c->gstat.as<unsigned long long>();
+int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64_t min_cov, hipStream_t s,
+              const std::vector<uint8_t>* gk_host) {
+    const int64_t* go = in.go;
+    unsigned long long* gstat = in.gstat;
     if (int rc = c->row_group.ensure(n_rows * 4)) return rc;
     if (int rc = c->row_obs.ensure(n_rows * 8)) return rc;
     if (int rc = c->obs_off.ensure(n_rows * 8)) return rc;
     const int wgrid = grid_for((n_rows + kWavesPerBlock - 1) / kWavesPerBlock * kBlock, 16384);
-    hipLaunchKernelGGL((k_kmer_rows<OW>), dim3(wgrid), dim3(kBlock), 0, s, c->offsets.p, c->values.as<uint8_t>(),
-                       validity, (int64_t)0, n_rows, go, G,
-                       c->gk.as<uint8_t>(), K, c->row_group.as<uint32_t>(), c->row_obs.as<int64_t>(), gstat);
+    hipLaunchKernelGGL((k_kmer_rows<OW>), dim3(wgrid), dim3(kBlock), 0, s, in.offsets, in.values, in.validity,
+                       in.voff, in.rows, n_rows, go, G, in.gk, K, c->row_group.as<uint32_t>(),
+                       c->row_obs.as<int64_t>(), gstat);
     ROGTK_HIP_CHECK(hipGetLastError());
     if (c->lds_path && K <= 32) {
         if (int rc = c->gsmall.ensure((size_t)G)) return rc;
-        hipLaunchKernelGGL(k_group_classify, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, c->offsets.p, OW, go,
-                           G, c->gk.as<uint8_t>(), K, c->row_obs.as<int64_t>(), c->gsmall.as<uint8_t>());
+        hipLaunchKernelGGL(k_group_classify, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, in.offsets, OW,
+                           in.rows, go, G, in.gk, K, c->row_obs.as<int64_t>(), c->gsmall.as<uint8_t>());
         hipLaunchKernelGGL((k_kmer_lds<OW>), dim3((unsigned)std::min<int64_t>(G, 65536)), dim3(kBlock), 0, s,
-                           c->offsets.p, c->values.as<uint8_t>(), go, G, c->gsmall.as<uint8_t>(), K, min_cov,
-                           c->row_obs.as<int64_t>(), c->cap_off.as<int64_t>(), c->t_kmer.as<uint64_t>(),
-                           c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), c->gcount.as<int64_t>(), gstat);
+                           in.offsets, in.values, in.rows, go, G, c->gsmall.as<uint8_t>(), K, min_cov,
+                           c->row_obs.as<int64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
+                           c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
         hipLaunchKernelGGL(k_drop_small_rows, dim3(grid_for(n_rows)), dim3(kBlock), 0, s, c->row_group.as<uint32_t>(),
                            c->gsmall.as<uint8_t>(), n_rows, c->row_obs.as<int64_t>());
         ROGTK_HIP_CHECK(hipGetLastError());
@@ -645,7 +721,7 @@ int run_class(KmerCtx* c, const uint8_t* validity, int64_t n_rows, int64_t G, in
     ROGTK_HIP_CHECK(hipMemcpyAsync(&last[1], c->row_obs.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
     ROGTK_HIP_CHECK(hipStreamSynchronize(s));
     for (int64_t g = 0; g < G; ++g) {
-        if (gk_host[g] != K) continue;
+        if (gk_host && (*gk_host)[g] != K) continue;
         if (!small.empty() && small[g]) ++c->last_lds_groups;
         else ++c->last_global_groups;
     }
@@ -664,8 +740,8 @@ int run_class(KmerCtx* c, const uint8_t* validity, int64_t n_rows, int64_t G, in
     for (DevBuf* b : {&c->r_cnt, &c->v_cnt})
         if (int rc = b->ensure((size_t)T * 2)) return rc;
 
-    hipLaunchKernelGGL((k_kmer_emit<OW, WIDE>), dim3(wgrid), dim3(kBlock), 0, s, c->offsets.p,
-                       c->values.as<uint8_t>(), n_rows, K, c->row_group.as<uint32_t>(), c->row_obs.as<int64_t>(),
+    hipLaunchKernelGGL((k_kmer_emit<OW, WIDE>), dim3(wgrid), dim3(kBlock), 0, s, in.offsets, in.values, in.rows,
+                       n_rows, K, c->row_group.as<uint32_t>(), c->row_obs.as<int64_t>(),
                        c->obs_off.as<int64_t>(), c->key_lo.as<uint64_t>(), c->key_hi.as<uint64_t>(),
                        c->ext.as<uint8_t>(), c->grp.as<uint32_t>(), c->idx.as<uint32_t>());
     ROGTK_HIP_CHECK(hipGetLastError());
@@ -731,24 +807,24 @@ int run_class(KmerCtx* c, const uint8_t* validity, int64_t n_rows, int64_t G, in
     if (nv == 0) return ROGTK_OK;
     const int gv = grid_for(nv);
     hipLaunchKernelGGL(k_group_ranges, dim3(gv), dim3(kBlock), 0, s, c->v_grp.as<uint32_t>(), nv,
-                       c->gstart.as<int64_t>(), c->gcount.as<int64_t>());
-    hipLaunchKernelGGL(k_group_counts, dim3(grid_for(G)), dim3(kBlock), 0, s, c->gk.as<uint8_t>(), K, G,
+                       c->gstart.as<int64_t>(), in.gcount);
+    hipLaunchKernelGGL(k_group_counts, dim3(grid_for(G)), dim3(kBlock), 0, s, in.gk, K, G,
                        (c->lds_path && K <= 32) ? c->gsmall.as<uint8_t>() : nullptr, c->gstart.as<int64_t>(),
-                       c->gcount.as<int64_t>());
+                       in.gcount);
     hipLaunchKernelGGL((k_censor<WIDE>), dim3(gv), dim3(kBlock), 0, s, c->v_lo.as<uint64_t>(),
                        c->v_hi.as<uint64_t>(), c->v_grp.as<uint32_t>(), c->v_ext.as<uint8_t>(),
-                       c->v_cnt.as<uint16_t>(), nv, K, c->gstart.as<int64_t>(), c->gcount.as<int64_t>(),
-                       c->cap_off.as<int64_t>(), c->t_kmer.as<uint64_t>(), c->t_ext.as<uint8_t>(),
+                       c->v_cnt.as<uint16_t>(), nv, K, c->gstart.as<int64_t>(), in.gcount,
+                       in.cap_off, c->t_kmer.as<uint64_t>(), c->t_ext.as<uint8_t>(),
                        c->t_cnt.as<uint16_t>(), gstat);
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
 }
 
 template <int OW>
-int run_any(KmerCtx* c, const uint8_t* validity, int64_t n_rows, int64_t G, int K, int64_t min_cov,
-            hipStream_t s, const std::vector<uint8_t>& gk) {
-    return K == 64 ? run_class<OW, true>(c, validity, n_rows, G, K, min_cov, s, gk)
-                   : run_class<OW, false>(c, validity, n_rows, G, K, min_cov, s, gk);
+int run_any(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64_t min_cov, hipStream_t s,
+            const std::vector<uint8_t>* gk) {
+    return K == 64 ? run_class<OW, true>(c, in, n_rows, G, K, min_cov, s, gk)
+                   : run_class<OW, false>(c, in, n_rows, G, K, min_cov, s, gk);
 }
 
 }  // namespace
@@ -886,10 +962,12 @@ int rogtk_kmer_spectrum_host(const void* offsets, int offset_width, const uint8_
     ROGTK_HIP_CHECK(hipMemsetAsync(c->gstat.p, 0, G * 5 * 8, s));
     ROGTK_HIP_CHECK(hipMemsetAsync(c->gcount.p, 0, G * 8, s));
     c->last_lds_groups = c->last_global_groups = 0;
+    const KIn in{c->offsets.as<int64_t>(), c->values.as<uint8_t>(), validity ? c->validity.as<uint8_t>() : nullptr,
+                 0, nullptr, c->go.as<int64_t>(), c->gk.as<uint8_t>(), c->cap_off.as<int64_t>(),
+                 c->gstat.as<unsigned long long>(), c->gcount.as<int64_t>()};
     for (int K : {4, 8, 16, 32, 64}) {
         if (!present[K] || n_rows == 0) continue;
-        if (int rc = run_any<8>(c, validity ? c->validity.as<uint8_t>() : nullptr, n_rows, G, K, min_coverage, s, gk))
-            return rc;
+        if (int rc = run_any<8>(c, in, n_rows, G, K, min_coverage, s, &gk)) return rc;
     }
     // dense packing by group
     std::vector<int64_t> gcount(G);
@@ -923,6 +1001,101 @@ int rogtk_kmer_spectrum_host(const void* offsets, int offset_width, const uint8_
         group_stats[5 * g + 2] = gcount[g];
         group_stats[5 * g + 3] = (int64_t)st[5 * g + 3];
         group_stats[5 * g + 4] = (int64_t)st[5 * g + 4];
+    }
+    return ROGTK_OK;
+}
+
+int rogtk_group_by_key(const uint32_t* keys, int64_t n, int64_t* rows_out, int64_t* group_offsets_out,
+                       int64_t* n_groups, void* stream) {
+    ROGTK_REQUIRE(n_groups && (n == 0 || (keys && rows_out && group_offsets_out)), ROGTK_E_INVALID,
+                  "group_by_key: NULL argument");
+    ROGTK_REQUIRE(n >= 0 && n < (int64_t)0x7FFFFFFF, ROGTK_E_UNSUPPORTED, "group_by_key: n must be < 2^31");
+    *n_groups = 0;
+    if (n == 0) return ROGTK_OK;
+    KmerCtx* c = nullptr;
+    if (int rc = kmer_ctx(&c)) return rc;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (int rc = c->tmp_u32.ensure((size_t)n * 4)) return rc;
+    if (int rc = c->head.ensure((size_t)n * 4)) return rc;
+    if (int rc = c->rid.ensure((size_t)n * 4)) return rc;
+    if (int rc = c->obs_off.ensure((size_t)n * 8)) return rc;
+    const int g = grid_for(n);
+    hipLaunchKernelGGL(k_iota64, dim3(g), dim3(kBlock), 0, s, c->obs_off.as<int64_t>(), n);
+    size_t bytes = 0;
+    ROGTK_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, keys, c->tmp_u32.as<uint32_t>(),
+                                                       c->obs_off.as<int64_t>(), rows_out, (int)n, 0, 32, s));
+    if (int rc = c->cub.ensure(bytes)) return rc;
+    ROGTK_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(c->cub.p, bytes, keys, c->tmp_u32.as<uint32_t>(),
+                                                       c->obs_off.as<int64_t>(), rows_out, (int)n, 0, 32, s));
+    hipLaunchKernelGGL(k_key_heads, dim3(g), dim3(kBlock), 0, s, c->tmp_u32.as<uint32_t>(), n, c->head.as<uint32_t>());
+    if (int rc = cub_exsum_u32(c, c->head.as<uint32_t>(), c->rid.as<uint32_t>(), n, s)) return rc;
+    hipLaunchKernelGGL(k_key_offsets, dim3(g), dim3(kBlock), 0, s, c->head.as<uint32_t>(), c->rid.as<uint32_t>(), n,
+                       group_offsets_out);
+    ROGTK_HIP_CHECK(hipGetLastError());
+    uint32_t last[2];
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&last[0], c->rid.as<uint32_t>() + n - 1, 4, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&last[1], c->head.as<uint32_t>() + n - 1, 4, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    *n_groups = (int64_t)last[0] + last[1];
+    return ROGTK_OK;
+}
+
+int rogtk_kmer_spectrum_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* validity,
+                            int64_t validity_offset, const int64_t* rows, int64_t n_rows,
+                            const int64_t* group_offsets, int64_t n_groups, int k, int64_t min_coverage,
+                            int64_t capacity, uint64_t* kmers, uint8_t* exts, uint16_t* counts,
+                            int64_t* entry_offsets, int64_t* group_stats, int64_t* n_entries, void* stream) {
+    ROGTK_REQUIRE(offsets && values && group_offsets && entry_offsets && group_stats && n_entries, ROGTK_E_INVALID,
+                  "kmer_dev: NULL argument");
+    ROGTK_REQUIRE(n_rows >= 0 && n_groups >= 1 && min_coverage >= 0, ROGTK_E_INVALID,
+                  "kmer_dev: n_rows >= 0, n_groups >= 1, min_coverage >= 0");
+    ROGTK_REQUIRE(n_groups < (int64_t)0xFFFFFFFF, ROGTK_E_UNSUPPORTED, "kmer_dev: too many groups");
+    KmerCtx* c = nullptr;
+    if (int rc = kmer_ctx(&c)) return rc;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int64_t G = n_groups;
+    const int K = k > 64 ? 0 : effective_k(k);
+    for (DevBuf* b : {&c->caps, &c->cap_off, &c->gcount, &c->gstart})
+        if (int rc = b->ensure((size_t)(G + 1) * 8)) return rc;
+    if (int rc = c->gk.ensure((size_t)G)) return rc;
+    if (int rc = c->gstat.ensure((size_t)G * 5 * 8)) return rc;
+    if (int rc = c->scal.ensure(64)) return rc;
+    ROGTK_HIP_CHECK(hipMemsetAsync(c->gk.p, K, G, s));
+    ROGTK_HIP_CHECK(hipMemsetAsync(c->gstat.p, 0, G * 5 * 8, s));
+    ROGTK_HIP_CHECK(hipMemsetAsync(c->gcount.p, 0, G * 8, s));
+    hipLaunchKernelGGL(k_group_caps, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, offsets, rows,
+                       group_offsets, G, c->caps.as<int64_t>());
+    if (int rc = cub_exsum_i64(c, c->caps.as<int64_t>(), c->cap_off.as<int64_t>(), G, s)) return rc;
+    hipLaunchKernelGGL(k_tail_sum, dim3(1), dim3(64), 0, s, c->cap_off.as<int64_t>(), c->caps.as<int64_t>(), G,
+                       c->cap_off.as<int64_t>() + G);
+    int64_t tcap = 0;
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&tcap, c->cap_off.as<int64_t>() + G, 8, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    tcap = std::max<int64_t>(tcap, 1);
+    if (int rc = c->t_kmer.ensure((size_t)tcap * 16)) return rc;
+    if (int rc = c->t_ext.ensure((size_t)tcap)) return rc;
+    if (int rc = c->t_cnt.ensure((size_t)tcap * 2)) return rc;
+    c->last_lds_groups = c->last_global_groups = 0;
+    if (K && n_rows > 0) {
+        const KIn in{offsets, values, validity, validity_offset, rows, group_offsets, c->gk.as<uint8_t>(),
+                     c->cap_off.as<int64_t>(), c->gstat.as<unsigned long long>(), c->gcount.as<int64_t>()};
+        if (int rc = run_any<8>(c, in, n_rows, G, K, min_coverage, s, nullptr)) return rc;
+    }
+    if (int rc = cub_exsum_i64(c, c->gcount.as<int64_t>(), entry_offsets, G, s)) return rc;
+    hipLaunchKernelGGL(k_tail_sum, dim3(1), dim3(64), 0, s, entry_offsets, c->gcount.as<int64_t>(), G,
+                       entry_offsets + G);
+    ROGTK_HIP_CHECK(hipMemcpyAsync(n_entries, entry_offsets + G, 8, hipMemcpyDeviceToHost, s));
+    hipLaunchKernelGGL(k_group_stats_out, dim3(grid_for(G)), dim3(kBlock), 0, s, c->gstat.as<unsigned long long>(),
+                       c->gcount.as<int64_t>(), G, K, group_stats);
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    ROGTK_REQUIRE(*n_entries <= capacity, ROGTK_E_OVERFLOW, "kmer_dev: %lld entries exceed capacity %lld",
+                  (long long)*n_entries, (long long)capacity);
+    if (*n_entries > 0) {
+        ROGTK_REQUIRE(kmers && exts && counts, ROGTK_E_INVALID, "kmer_dev: output arrays are NULL");
+        hipLaunchKernelGGL(k_pack, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, c->t_kmer.as<uint64_t>(),
+                           c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), G, c->cap_off.as<int64_t>(),
+                           c->gcount.as<int64_t>(), entry_offsets, kmers, exts, counts);
+        ROGTK_HIP_CHECK(hipGetLastError());
     }
     return ROGTK_OK;
 }

@@ -175,6 +175,41 @@ def cluster_batch(engine: ClusterEngine, batch: PackedBatch, cluster_id: torch.T
     engine.assign(batch, cluster_id, stream)
 
 
+def group_by_key(keys: torch.Tensor, stream=None):
+    """polars group_by on the device (e.g. H3 cluster ids, int32/uint32 tensor):
+    returns (rows int64[n] ordered by key (stable), group_offsets int64[G + 1], G)."""
+    n = keys.numel()
+    rows = torch.empty(max(n, 1), dtype=torch.int64, device=keys.device)
+    go = torch.empty(n + 1, dtype=torch.int64, device=keys.device)
+    ng = ctypes.c_int64(0)
+    _lib.call("rogtk_group_by_key", _p(keys), n, _p(rows), _p(go), ctypes.byref(ng), _s(stream))
+    G = int(ng.value)
+    return rows[:n], go[:G + 1] if n else go[:1].zero_(), G
+
+
+def kmer_spectrum_dev(offsets: torch.Tensor, values: torch.Tensor, group_offsets: torch.Tensor, k: int,
+                      min_coverage: int, capacity: int, rows: Optional[torch.Tensor] = None,
+                      validity: Optional[torch.Tensor] = None, validity_offset: int = 0, stream=None):
+    """H4 on a device-resident column (int64 offsets, uint8 values). Returns a dict of
+    device tensors: kmers (int64 [m, 2]: hi, lo words), exts (uint8), counts (int16 bits
+    of u16), entry_offsets (int64 G + 1), stats (int64 G x 5)."""
+    dev = values.device
+    G = group_offsets.numel() - 1
+    n_rows = rows.numel() if rows is not None else offsets.numel() - 1
+    cap = max(int(capacity), 1)
+    km = torch.empty((cap, 2), dtype=torch.int64, device=dev)
+    ex = torch.empty(cap, dtype=torch.uint8, device=dev)
+    cn = torch.empty(cap, dtype=torch.int16, device=dev)
+    eo = torch.empty(G + 1, dtype=torch.int64, device=dev)
+    st = torch.empty((G, 5), dtype=torch.int64, device=dev)
+    m = ctypes.c_int64(0)
+    _lib.call("rogtk_kmer_spectrum_dev", _p(offsets), _p(values), _p(validity), int(validity_offset), _p(rows),
+              n_rows, _p(group_offsets), G, int(k), int(min_coverage), cap, _p(km), _p(ex), _p(cn), _p(eo),
+              _p(st), ctypes.byref(m), _s(stream))
+    n = int(m.value)
+    return {"kmers": km[:n], "exts": ex[:n], "counts": cn[:n], "entry_offsets": eo, "stats": st}
+
+
 def profile_enable(on: bool = True) -> None:
     _lib.call("rogtk_profile_enable", 1 if on else 0)
 

@@ -138,3 +138,61 @@ def test_large_group(rg):
         a = int(rng.integers(0, 1850))
         items.append(tpl[a:a + 150])
     _check(rg, items, 17, 20)
+
+
+def test_group_by_key_device(rg):
+    """rogtk_group_by_key == numpy stable argsort + run boundaries."""
+    import torch
+
+    from rogtk_amd import device as D
+
+    rng = np.random.default_rng(2)
+    for n, hi in ((1, 5), (1000, 7), (100_003, 50_000), (300_000, 0xFFFFFFFF)):
+        keys = rng.integers(0, hi, n, dtype=np.uint64).astype(np.uint32)
+        if n > 10:
+            keys[:5] = 0xFFFFFFFF  # null ids group last
+        rows, go, G = D.group_by_key(torch.from_numpy(keys.view(np.int32)).cuda())
+        order = np.argsort(keys, kind="stable")
+        sk = keys[order]
+        heads = np.flatnonzero(np.r_[True, sk[1:] != sk[:-1]])
+        assert G == len(heads)
+        assert np.array_equal(rows.cpu().numpy(), order)
+        assert np.array_equal(go.cpu().numpy(), np.r_[heads, n])
+
+
+@pytest.mark.parametrize("k,min_cov", [(17, 3), (13, 1), (33, 2), (70, 1)])
+def test_device_spectrum_with_grouping(rg, k, min_cov):
+    """Level-1 path: device column + device group_by permutation == host path on the
+    same column physically regrouped (and so == the oracle)."""
+    import torch
+
+    from rogtk_amd import device as D
+
+    rng = np.random.default_rng(k)
+    n_mol = 400
+    tpls = _reads(rng, n_mol, 150, 150)
+    mol = rng.integers(0, n_mol, 6000)
+    items = []
+    for m in mol:
+        t = tpls[m]
+        a = int(rng.integers(0, 40))
+        r = bytearray(t[a:a + 110])
+        if rng.random() < 0.02:
+            r[5] = ord("N")
+        items.append(bytes(r))
+    lens = np.array([len(x) for x in items], dtype=np.int64)
+    offs = np.r_[0, np.cumsum(lens)].astype(np.int64)
+    vals = np.frombuffer(b"".join(items), dtype=np.uint8)
+    rows, go, G = D.group_by_key(torch.from_numpy(mol.astype(np.uint32).view(np.int32)).cuda())
+    cap = int(sum(max(0, L - 3) for L in lens))
+    out = D.kmer_spectrum_dev(torch.from_numpy(offs).cuda(), torch.from_numpy(vals.copy()).cuda(), go, k, min_cov,
+                              cap, rows=rows)
+    order = rows.cpu().numpy()
+    grouped = [items[i] for i in order]
+    ref = P().kmer_spectrum(P().StrCol.from_list(grouped), k, min_cov, False, go.cpu().numpy())
+    assert np.array_equal(out["entry_offsets"].cpu().numpy(), ref["group_offsets"])
+    assert np.array_equal(out["stats"].cpu().numpy(), ref["stats"])
+    km = out["kmers"].cpu().numpy().view(np.uint64)
+    assert np.array_equal(km[:, 0], ref["kmer_hi"]) and np.array_equal(km[:, 1], ref["kmer_lo"])
+    assert np.array_equal(out["exts"].cpu().numpy(), ref["exts"])
+    assert np.array_equal(out["counts"].cpu().numpy().view(np.uint16), ref["counts"])
