@@ -22,6 +22,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cmath>
+#include <cstdlib>
 #include <memory>
 #include <vector>
 
@@ -53,49 +54,92 @@ __device__ __forceinline__ void span(const void* offsets, int64_t r, int64_t& st
     }
 }
 
-// last g with go[g] <= r (groups cover [go[0], go[G]) = [0, n_rows))
-__device__ __forceinline__ int64_t group_of(const int64_t* go, int64_t G, int64_t r) {
-    int64_t lo = 0, hi = G - 1;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi + 1) >> 1;
-        if (go[mid] <= r) lo = mid;
-        else hi = mid - 1;
-    }
-    return lo;
-}
-
+// Grouped row r -> its span in the column (one thread per row: the rows[] ->
+// offsets[] chain runs 64x wider than per wave). raw_len = -1 for rows that take no
+// part (null, or a group of another effective k); words = 2-bit words to stage.
 template <int OW>
-__global__ __launch_bounds__(kBlock) void k_kmer_rows(const void* offsets, const uint8_t* __restrict__ values,
-                                                      const uint8_t* __restrict__ validity, int64_t voff,
-                                                      const int64_t* __restrict__ rows,
-                                                      int64_t n_rows, const int64_t* __restrict__ go, int64_t G,
-                                                      const uint8_t* __restrict__ gk, int K,
-                                                      uint32_t* __restrict__ row_group, int64_t* __restrict__ row_obs,
-                                                      unsigned long long* __restrict__ gstat) {
-    const int lane = threadIdx.x & 63;
-    const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
-    for (int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); r < n_rows; r += waves) {
-        const int64_t g = group_of(go, G, r);
-        const int64_t pr = rows ? rows[r] : r;  // physical row of grouped row r
-        bool valid = gk[g] == K;
+__global__ __launch_bounds__(kBlock) void k_row_meta(const void* offsets, const uint8_t* __restrict__ validity,
+                                                     int64_t voff, const int64_t* __restrict__ rows, int64_t n_rows,
+                                                     const uint8_t* __restrict__ gk, int K,
+                                                     const uint32_t* __restrict__ row_group,
+                                                     int64_t* __restrict__ row_st, int32_t* __restrict__ raw_len,
+                                                     int64_t* __restrict__ row_words) {
+    for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < n_rows; r += (int64_t)gridDim.x * kBlock) {
+        const int64_t pr = rows ? rows[r] : r;
+        bool valid = gk[row_group[r]] == K;
         if (valid && validity) {
             const int64_t b = voff + pr;
             valid = (validity[b >> 3] >> (b & 7)) & 1;
         }
         int64_t st = 0, len = 0;
-        bool ok = false;
-        if (valid) {
-            span<OW>(offsets, pr, st, len);
-            bool bad = false;
-            for (int64_t j = lane; j < len; j += 64) bad |= !acgt(values[st + j]);
-            ok = __ballot(bad) == 0;
+        if (valid) span<OW>(offsets, pr, st, len);
+        row_st[r] = st;
+        raw_len[r] = valid ? (int32_t)len : -1;
+        row_words[r] = valid ? (len + 31) >> 5 : 0;
+    }
+}
+
+// One wave per grouped row, bytes loaded once: the ACGT check of fracture.rs:217-229
+// (ballot), the observation count, n_sequences, and the packed 2-bit staging
+// (packed[woff[r] ..], base j in word j / 32 at bits 62 - 2 (j % 32)).
+__global__ __launch_bounds__(kBlock) void k_row_stage(const uint8_t* __restrict__ values, int64_t n_rows, int K,
+                                                      const uint32_t* __restrict__ row_group,
+                                                      const int64_t* __restrict__ row_st,
+                                                      const int32_t* __restrict__ raw_len,
+                                                      const int64_t* __restrict__ woff,
+                                                      uint64_t* __restrict__ packed,
+                                                      int64_t* __restrict__ row_obs, int32_t* __restrict__ row_len,
+                                                      unsigned long long* __restrict__ gstat) {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
+    for (int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); r < n_rows; r += waves) {
+        const int64_t len = raw_len[r];
+        if (len < 0) {
+            if (lane == 0) {
+                row_obs[r] = 0;
+                row_len[r] = 0;
+            }
+            continue;
         }
+        const int64_t st = row_st[r];
+        const int iters = (int)((len + 63) >> 6);
+        uint64_t* out = packed + woff[r];
+        bool bad = false;
+        for (int it0 = 0; it0 < iters; it0 += 4) {
+            uint8_t cb[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t j = (int64_t)(it0 + u) * 64 + lane;
+                cb[u] = j < len ? values[st + j] : (uint8_t)'A';
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (it0 + u >= iters) break;
+                bad |= !acgt(cb[u]);
+                uint64_t v = (uint64_t)base2(cb[u]) << (62 - 2 * (lane & 31));
+#pragma unroll
+                for (int m = 1; m < 32; m <<= 1) v |= __shfl_xor(v, m);
+                const int64_t w = 2 * (int64_t)(it0 + u) + (lane >> 5);
+                if ((lane & 31) == 0 && w * 32 < len) out[w] = v;
+            }
+        }
+        const bool ok = __ballot(bad) == 0;
         if (lane == 0) {
-            row_group[r] = (uint32_t)g;
-            row_obs[r] = ok && len >= K ? len - K + 1 : 0;
-            if (ok) atomicAdd(gstat + 5 * g + 1, 1ull);  // n_sequences
+            const bool use = ok && len >= K;
+            row_obs[r] = use ? len - K + 1 : 0;
+            row_len[r] = use ? (int32_t)len : 0;
+            if (ok) atomicAdd(gstat + 5 * row_group[r] + 1, 1ull);  // n_sequences
         }
     }
+}
+
+// row -> group map: one wave per group writes its rows' group id (coalesced)
+__global__ __launch_bounds__(kBlock) void k_row_groups(const int64_t* __restrict__ go, int64_t G,
+                                                       uint32_t* __restrict__ row_group) {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
+    for (int64_t g = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); g < G; g += waves)
+        for (int64_t r = go[g] + lane; r < go[g + 1]; r += 64) row_group[r] = (uint32_t)g;
 }
 
 template <int OW, bool WIDE>
@@ -304,16 +348,26 @@ __global__ __launch_bounds__(kBlock) void k_pack(const uint64_t* __restrict__ t_
 }
 
 // ----------------------------------------------------------- LDS fast path
-// One workgroup per small group (<= kLdsObs observations, rows <= kLdsRowBases,
-// k_eff <= 32): reads are packed to 2-bit words in LDS, every observation is
+// One workgroup per small group (size class CLS: observations, rows and packed
+// words within LdsCfg<CLS>, k_eff <= 32): the group's rows, already packed to 2-bit
+// words in HBM by k_kmer_pack, are loaded into LDS in one coalesced pass; every observation is
 // inserted into an LDS hash table (64-bit CAS on the key; the count and the OR of
 // exts share one u32: count in bits 0..23, exts in 24..31), the valid entries are
 // compacted, bitonic-sorted and censored by binary search, all in LDS. The all-ones
 // key (TTT..T at k = 32) equals the empty marker and gets a dedicated slot.
-constexpr int kLdsObs = 2048;
-constexpr int kLdsSlots = 2 * kLdsObs;   // power of two, load factor <= 0.5
-constexpr int kLdsRowBases = 2048;       // per-wave packed row buffer
-constexpr int kLdsRowWords = kLdsRowBases / 32 + 1;
+// Two size classes: class 1 (<= 2048 observations, ~78 KB LDS, 2 workgroups per CU)
+// and class 2 (<= 4096 observations, ~155 KB, 1 per CU). Larger groups take the
+// global radix-sort path.
+template <int CLS>
+struct LdsCfg {
+    static constexpr int kObs = CLS == 1 ? 2048 : 4096;
+    static constexpr int kSlots = 2 * kObs;                  // power of two, load factor <= 0.5
+    static constexpr int kRows = CLS == 1 ? 256 : 512;       // rows of one group
+    static constexpr int kWords = CLS == 1 ? 768 : 1536;     // packed words of one group
+    // insert phase (packed words + row metadata) and sort phase (valid entries) share LDS
+    static constexpr int kUnionWords = (kObs * 12 + 7) / 8;
+    static_assert((kWords + 1) * 8 + kRows * 12 <= kUnionWords * 8, "LDS union too small");
+};
 constexpr unsigned long long kEmpty = ~0ull;
 
 __device__ __forceinline__ uint32_t pk_base(const uint64_t* pk, int64_t p) {
@@ -324,60 +378,71 @@ __device__ __forceinline__ bool kless(uint64_t ka, uint32_t ia, uint64_t kb, uin
     return ka < kb || (ka == kb && (ia >> 31) < (ib >> 31));  // real entries before pads
 }
 
-template <int OW>
-__global__ __launch_bounds__(kBlock) void k_kmer_lds(const void* offsets, const uint8_t* __restrict__ values,
-                                                     const int64_t* __restrict__ rows,
-                                                     const int64_t* __restrict__ go, int64_t G,
+template <int CLS>
+__global__ __launch_bounds__(kBlock) void k_kmer_lds(const int64_t* __restrict__ go, int64_t G,
                                                      const uint8_t* __restrict__ gsmall, int K, int64_t min_cov,
                                                      const int64_t* __restrict__ row_obs,
+                                                     const int32_t* __restrict__ row_len,
+                                                     const int64_t* __restrict__ woff,
+                                                     const uint64_t* __restrict__ packed,
                                                      const int64_t* __restrict__ cap_off,
                                                      uint64_t* __restrict__ t_kmer, uint8_t* __restrict__ t_ext,
                                                      uint16_t* __restrict__ t_cnt, int64_t* __restrict__ gcount,
                                                      unsigned long long* __restrict__ gstat) {
+    using C = LdsCfg<CLS>;
+    constexpr int kLdsObs = C::kObs, kLdsSlots = C::kSlots, kLdsRows = C::kRows, kLdsWords = C::kWords;
     __shared__ unsigned long long tkey[kLdsSlots + 1];
-    __shared__ uint32_t tinfo[kLdsSlots + 1];
-    __shared__ uint64_t pk[kWavesPerBlock][kLdsRowWords];
-    __shared__ uint64_t vkey[kLdsObs];
-    __shared__ uint32_t vinfo[kLdsObs];  // count | exts << 16 | pad << 31
-    __shared__ uint32_t scan[kBlock];
-    __shared__ uint32_t s_term, s_iso;
+    __shared__ uint32_t tinfo[kLdsSlots + 1];  // count (bits 0..23) | exts << 24
+    __shared__ uint16_t claimed[kLdsObs + 1];  // slots first touched by this group
+    __shared__ uint64_t ubuf[C::kUnionWords];
+    uint64_t* const words = ubuf;                                      // the group's packed rows
+    int32_t* const m_len = reinterpret_cast<int32_t*>(ubuf + kLdsWords + 1);
+    int32_t* const m_nobs = m_len + kLdsRows;
+    int32_t* const m_w = m_nobs + kLdsRows;
+    uint64_t* const vkey = ubuf;                                       // after the inserts
+    uint32_t* const vinfo = reinterpret_cast<uint32_t*>(ubuf + kLdsObs);  // count | exts << 16 | pad << 31
+    __shared__ uint32_t scan[kWavesPerBlock];
+    __shared__ uint32_t s_claimed, s_term, s_iso;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int hbits = 31 - __clz(kLdsSlots);
     const uint64_t kmask = K == 32 ? ~0ull : ((1ull << (2 * K)) - 1ull);
+    for (int i = tid; i <= kLdsSlots; i += kBlock) {  // once; groups reset only what they touch
+        tkey[i] = kEmpty;
+        tinfo[i] = 0;
+    }
+    if (tid == 0) s_claimed = 0;
     for (int64_t g = blockIdx.x; g < G; g += gridDim.x) {
-        if (!gsmall[g]) continue;  // uniform per block
-        for (int i = tid; i <= kLdsSlots; i += kBlock) {
-            tkey[i] = kEmpty;
-            tinfo[i] = 0;
+        if (gsmall[g] != CLS) continue;  // uniform per block
+        const int64_t r0 = go[g], r1 = go[g + 1];
+        const int nrows = (int)(r1 - r0);  // <= kLdsRows (classification)
+        const int64_t w0 = woff[r0];
+        const int nwords = (int)(woff[r1 - 1] + ((row_len[r1 - 1] + 31) >> 5) - w0);  // <= kLdsWords
+        for (int i = tid; i < nrows; i += kBlock) {
+            m_len[i] = row_len[r0 + i];
+            m_nobs[i] = (int32_t)row_obs[r0 + i];
+            m_w[i] = (int32_t)(woff[r0 + i] - w0);
         }
+        for (int i = tid; i < nwords; i += kBlock) words[i] = packed[w0 + i];
         if (tid == 0) {
+            words[nwords] = 0;
             s_term = 0;
             s_iso = 0;
         }
         __syncthreads();
-        const int64_t r0 = go[g], r1 = go[g + 1];
-        for (int64_t rb = r0; rb < r1; rb += kWavesPerBlock) {  // uniform trip count
-            const int64_t r = rb + wave;
-            int64_t nobs = 0, st = 0, len = 0;
-            if (r < r1) {
-                nobs = row_obs[r];
-                if (nobs) span<OW>(offsets, rows ? rows[r] : r, st, len);
-            }
-            const int nw = (int)((len + 31) >> 5) + 1;
-            for (int w = lane; w < nw; w += 64) pk[wave][w] = 0;
-            __syncthreads();
-            for (int64_t j = lane; j < len && nobs; j += 64)
-                atomicOr((unsigned long long*)&pk[wave][j >> 5],
-                         (unsigned long long)base2(values[st + j]) << (62 - 2 * (j & 31)));
-            __syncthreads();
-            for (int64_t p = lane; p < nobs; p += 64) {
-                const int b = (int)(2 * (p & 31));
-                const uint64_t w0 = pk[wave][p >> 5], w1 = pk[wave][(p >> 5) + 1];
-                const uint64_t top = b ? (w0 << b) | (w1 >> (64 - b)) : w0;
+        // every k-mer observation of the group, straight from the packed words in LDS
+        for (int ri = wave; ri < nrows; ri += kWavesPerBlock) {
+            const int nobs = m_nobs[ri];
+            if (nobs == 0) continue;
+            const int len = m_len[ri];
+            const uint64_t* rw = words + m_w[ri];
+            for (int p = lane; p < nobs; p += 64) {
+                const int b = 2 * (p & 31);
+                const uint64_t x0 = rw[p >> 5], x1 = rw[(p >> 5) + 1];
+                const uint64_t top = b ? (x0 << b) | (x1 >> (64 - b)) : x0;
                 const uint64_t key = (top >> (64 - 2 * K)) & kmask;
                 uint32_t e = 0;
-                if (p > 0) e |= 1u << pk_base(pk[wave], p - 1);
-                if (p + K < len) e |= 1u << (4 + pk_base(pk[wave], p + K));
+                if (p > 0) e |= 1u << pk_base(rw, p - 1);
+                if (p + K < len) e |= 1u << (4 + pk_base(rw, p + K));
                 uint32_t slot;
                 if (key == kEmpty) {
                     slot = kLdsSlots;
@@ -389,36 +454,114 @@ __global__ __launch_bounds__(kBlock) void k_kmer_lds(const void* offsets, const 
                         slot = (slot + 1) & (kLdsSlots - 1);
                     }
                 }
-                atomicAdd(&tinfo[slot], 1u);
+                if ((atomicAdd(&tinfo[slot], 1u) & 0xFFFFFFu) == 0) claimed[atomicAdd(&s_claimed, 1u)] = (uint16_t)slot;
                 if (e) atomicOr(&tinfo[slot], e << 24);
             }
-            __syncthreads();
         }
-        // CountFilter + compaction (slot ranges per thread keep the pass simple)
-        constexpr int per = (kLdsSlots + 1 + kBlock - 1) / kBlock;
-        const int s0 = tid * per, s1 = min(s0 + per, kLdsSlots + 1);
-        uint32_t mine = 0;
-        for (int i = s0; i < s1; ++i) {
-            const uint32_t c = tinfo[i] & 0xFFFFFFu;
-            if (c && (int64_t)min(c, 0xFFFFu) >= min_cov) ++mine;
-        }
-        scan[tid] = mine;
         __syncthreads();
-        for (int off = 1; off < kBlock; off <<= 1) {  // inclusive Hillis-Steele scan
-            const uint32_t v = tid >= off ? scan[tid - off] : 0u;
-            __syncthreads();
-            scan[tid] += v;
-            __syncthreads();
+        // CountFilter + compaction over the claimed slots: wave-shuffle scan, one
+        // barrier for the per-wave totals
+        const uint32_t ncl = s_claimed;
+        const uint32_t per = (ncl + kBlock - 1) / kBlock;
+        const uint32_t c0 = min(ncl, tid * per), c1 = min(ncl, c0 + per);
+        uint32_t mine = 0;
+        for (uint32_t i = c0; i < c1; ++i) {
+            const uint32_t c = tinfo[claimed[i]] & 0xFFFFFFu;
+            if ((int64_t)min(c, 0xFFFFu) >= min_cov) ++mine;
         }
-        const uint32_t nv = scan[kBlock - 1];
-        uint32_t w = scan[tid] - mine;
-        for (int i = s0; i < s1; ++i) {
-            const uint32_t c = tinfo[i] & 0xFFFFFFu;
-            if (c && (int64_t)min(c, 0xFFFFu) >= min_cov) {
-                vkey[w] = i == kLdsSlots ? kEmpty : tkey[i];
-                vinfo[w] = min(c, 0xFFFFu) | ((tinfo[i] >> 24) << 16);
+        uint32_t incl = mine;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t v = __shfl_up(incl, off);
+            if (lane >= off) incl += v;
+        }
+        if (lane == 63) scan[wave] = incl;
+        __syncthreads();
+        uint32_t wbase = 0, nv = 0;
+#pragma unroll
+        for (int w2 = 0; w2 < kWavesPerBlock; ++w2) {
+            if (w2 < wave) wbase += scan[w2];
+            nv += scan[w2];
+        }
+        uint32_t w = wbase + incl - mine;
+        for (uint32_t i = c0; i < c1; ++i) {
+            const uint32_t sl = claimed[i];
+            const uint32_t info = tinfo[sl];
+            const uint32_t c = info & 0xFFFFFFu;
+            if ((int64_t)min(c, 0xFFFFu) >= min_cov) {
+                vkey[w] = sl == kLdsSlots ? kEmpty : tkey[sl];
+                vinfo[w] = min(c, 0xFFFFu) | ((info >> 24) << 16);
                 ++w;
             }
+        }
+        __syncthreads();
+        // reset the touched slots for the next group (the table is not read again here)
+        for (uint32_t i = tid; i < ncl; i += kBlock) {
+            const uint32_t sl = claimed[i];
+            tkey[sl] = kEmpty;
+            tinfo[sl] = 0;
+        }
+        const int64_t base = cap_off[g];
+        if (nv <= 64) {
+            // small valid set: wave 0 sorts it in registers (bitonic over shuffles),
+            // censors and writes it
+            if (wave == 0) {
+                uint64_t key = lane < (int)nv ? vkey[lane] : kEmpty;
+                uint32_t info = lane < (int)nv ? vinfo[lane] : (1u << 31);
+#pragma unroll
+                for (int k2 = 2; k2 <= 64; k2 <<= 1) {
+#pragma unroll
+                    for (int j = k2 >> 1; j > 0; j >>= 1) {
+                        const uint64_t ok = __shfl_xor(key, j);
+                        const uint32_t oi = __shfl_xor(info, j);
+                        const bool lower = (lane & j) == 0, up = (lane & k2) == 0;
+                        const bool other_less = kless(ok, oi, key, info);
+                        const bool take = (lower == up) ? other_less : !other_less && !(ok == key && oi == info);
+                        if (take) {
+                            key = ok;
+                            info = oi;
+                        }
+                    }
+                }
+                vkey[lane] = key;  // sorted (pads last) for the neighbour searches
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                uint32_t term = 0, iso = 0;
+                if (lane < (int)nv) {
+                    const uint32_t e = (info >> 16) & 0xFFu;
+                    uint32_t ne = 0;
+                    for (int bit = 0; bit < 8; ++bit) {
+                        if (!((e >> bit) & 1u)) continue;
+                        const uint64_t bb = (uint64_t)(bit & 3);
+                        const uint64_t nb = bit < 4 ? (key >> 2) | (bb << (2 * K - 2)) : ((key << 2) | bb) & kmask;
+                        uint32_t a = 0, c = nv;
+                        while (a < c) {
+                            const uint32_t m = (a + c) >> 1;
+                            if (vkey[m] < nb) a = m + 1;
+                            else c = m;
+                        }
+                        if (a < nv && vkey[a] == nb) ne |= 1u << bit;
+                    }
+                    const int64_t o = base + lane;
+                    t_kmer[2 * o] = 0;
+                    t_kmer[2 * o + 1] = key;
+                    t_ext[o] = (uint8_t)ne;
+                    t_cnt[o] = (uint16_t)(info & 0xFFFFu);
+                    const bool l0 = (ne & 0xFu) == 0, r0b = (ne >> 4) == 0;
+                    term = (l0 || r0b) ? 1u : 0u;
+                    iso = (l0 && r0b) ? 1u : 0u;
+                }
+                const uint64_t tb = __ballot(term), ib = __ballot(iso);
+                if (lane == 0) {
+                    gcount[g] = nv;
+                    gstat[5 * g + 3] = (unsigned long long)__popcll(tb);
+                    gstat[5 * g + 4] = (unsigned long long)__popcll(ib);
+                    s_claimed = 0;
+                }
+            }
+            __syncthreads();
+            continue;
         }
         uint32_t P = 2;
         while (P < nv) P <<= 1;
@@ -447,7 +590,6 @@ __global__ __launch_bounds__(kBlock) void k_kmer_lds(const void* offsets, const 
             }
         }
         // remove_censored_exts + output at the group's capacity offset
-        const int64_t base = cap_off[g];
         for (uint32_t i = tid; i < nv; i += kBlock) {
             const uint64_t key = vkey[i];
             const uint32_t info = vinfo[i];
@@ -455,8 +597,8 @@ __global__ __launch_bounds__(kBlock) void k_kmer_lds(const void* offsets, const 
             uint32_t ne = 0;
             for (int bit = 0; bit < 8; ++bit) {
                 if (!((e >> bit) & 1u)) continue;
-                const uint64_t b = (uint64_t)(bit & 3);
-                const uint64_t nb = bit < 4 ? (key >> 2) | (b << (2 * K - 2)) : ((key << 2) | b) & kmask;
+                const uint64_t bb = (uint64_t)(bit & 3);
+                const uint64_t nb = bit < 4 ? (key >> 2) | (bb << (2 * K - 2)) : ((key << 2) | bb) & kmask;
                 uint32_t a = 0, c = nv;
                 while (a < c) {
                     const uint32_t m = (a + c) >> 1;
@@ -470,26 +612,26 @@ __global__ __launch_bounds__(kBlock) void k_kmer_lds(const void* offsets, const 
             t_kmer[2 * o + 1] = key;
             t_ext[o] = (uint8_t)ne;
             t_cnt[o] = (uint16_t)(info & 0xFFFFu);
-            const bool l0 = (ne & 0xFu) == 0, r0 = (ne >> 4) == 0;
-            if (l0 || r0) atomicAdd(&s_term, 1u);
-            if (l0 && r0) atomicAdd(&s_iso, 1u);
+            const bool l0 = (ne & 0xFu) == 0, r0b = (ne >> 4) == 0;
+            if (l0 || r0b) atomicAdd(&s_term, 1u);
+            if (l0 && r0b) atomicAdd(&s_iso, 1u);
         }
         __syncthreads();
         if (tid == 0) {
             gcount[g] = nv;
             gstat[5 * g + 3] = s_term;
             gstat[5 * g + 4] = s_iso;
+            s_claimed = 0;
         }
         __syncthreads();
     }
 }
 
-// Per group of effective k K: observation total and longest row decide the path.
-__global__ __launch_bounds__(kBlock) void k_group_classify(const void* offsets, int ow,
-                                                           const int64_t* __restrict__ rows,
-                                                           const int64_t* __restrict__ go,
-                                                           int64_t G, const uint8_t* __restrict__ gk, int K,
+// Per group of effective k K: observation, row and packed-word totals decide the path.
+__global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __restrict__ go, int64_t G,
+                                                           const uint8_t* __restrict__ gk, int K,
                                                            const int64_t* __restrict__ row_obs,
+                                                           const int64_t* __restrict__ row_words,
                                                            uint8_t* __restrict__ gsmall) {
     const int lane = threadIdx.x & 63;
     const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
@@ -498,21 +640,24 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const void* offsets, 
             if (lane == 0) gsmall[g] = 0;
             continue;
         }
-        int64_t obs = 0, maxlen = 0;
+        int64_t obs = 0, words = 0;
         for (int64_t r = go[g] + lane; r < go[g + 1]; r += 64) {
             obs += row_obs[r];
-            if (row_obs[r]) {
-                const int64_t pr = rows ? rows[r] : r;
-                const int64_t len = ow == 4 ? (int64_t)((const int32_t*)offsets)[pr + 1] - ((const int32_t*)offsets)[pr]
-                                            : ((const int64_t*)offsets)[pr + 1] - ((const int64_t*)offsets)[pr];
-                maxlen = max(maxlen, len);
-            }
+            words += row_words[r];
         }
         for (int m = 32; m > 0; m >>= 1) {
             obs += __shfl_xor(obs, m);
-            maxlen = max(maxlen, __shfl_xor(maxlen, m));
+            words += __shfl_xor(words, m);
         }
-        if (lane == 0) gsmall[g] = (K <= 32 && obs <= kLdsObs && maxlen <= kLdsRowBases) ? 1 : 0;
+        const int64_t nrows = go[g + 1] - go[g];
+        if (lane == 0) {
+            uint8_t cls = 0;
+            if (K <= 32 && obs > 0) {
+                if (obs <= LdsCfg<1>::kObs && nrows <= LdsCfg<1>::kRows && words <= LdsCfg<1>::kWords) cls = 1;
+                else if (obs <= LdsCfg<2>::kObs && nrows <= LdsCfg<2>::kRows && words <= LdsCfg<2>::kWords) cls = 2;
+            }
+            gsmall[g] = cls;
+        }
     }
 }
 
@@ -610,7 +755,7 @@ struct KmerCtx {
     int device = -1;
     hipStream_t stream = nullptr;
     DevBuf offsets, values, validity, go, gk, cap_off, gstat, gstart, gcount, out_off;
-    DevBuf row_group, row_obs, obs_off;
+    DevBuf row_group, row_obs, obs_off, row_len, row_words, woff, packed, row_st, raw_len;
     DevBuf key_lo, key_hi, ext, grp, idx, perm_a, perm_b, tmp_u64, tmp_u32;
     DevBuf s_lo, s_hi, s_ext, s_grp, head, rid, r_valid, r_first, r_ext, r_cnt, vpos;
     DevBuf v_lo, v_hi, v_grp, v_ext, v_cnt, t_kmer, t_ext, t_cnt, o_kmer, o_ext, o_cnt, cub, gsmall, caps, scal;
@@ -692,19 +837,43 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
     unsigned long long* gstat = in.gstat;
     if (int rc = c->row_group.ensure(n_rows * 4)) return rc;
     if (int rc = c->row_obs.ensure(n_rows * 8)) return rc;
+    if (int rc = c->row_len.ensure(n_rows * 4)) return rc;
+    if (int rc = c->row_words.ensure(n_rows * 8)) return rc;
+    if (int rc = c->woff.ensure(n_rows * 8)) return rc;
+    if (int rc = c->row_st.ensure(n_rows * 8)) return rc;
+    if (int rc = c->raw_len.ensure(n_rows * 4)) return rc;
     if (int rc = c->obs_off.ensure(n_rows * 8)) return rc;
     const int wgrid = grid_for((n_rows + kWavesPerBlock - 1) / kWavesPerBlock * kBlock, 16384);
-    hipLaunchKernelGGL((k_kmer_rows<OW>), dim3(wgrid), dim3(kBlock), 0, s, in.offsets, in.values, in.validity,
-                       in.voff, in.rows, n_rows, go, G, in.gk, K, c->row_group.as<uint32_t>(),
-                       c->row_obs.as<int64_t>(), gstat);
+    hipLaunchKernelGGL(k_row_groups, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, go, G,
+                       c->row_group.as<uint32_t>());
+    // stage: row spans -> word offsets -> one pass over the bytes (check + pack + counts)
+    hipLaunchKernelGGL((k_row_meta<OW>), dim3(grid_for(n_rows)), dim3(kBlock), 0, s, in.offsets, in.validity, in.voff,
+                       in.rows, n_rows, in.gk, K, c->row_group.as<uint32_t>(), c->row_st.as<int64_t>(),
+                       c->raw_len.as<int32_t>(), c->row_words.as<int64_t>());
+    if (int rc = cub_exsum_i64(c, c->row_words.as<int64_t>(), c->woff.as<int64_t>(), n_rows, s)) return rc;
+    {
+        int64_t wl[2] = {0, 0};
+        ROGTK_HIP_CHECK(hipMemcpyAsync(&wl[0], c->woff.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
+        ROGTK_HIP_CHECK(hipMemcpyAsync(&wl[1], c->row_words.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
+        ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+        if (int rc = c->packed.ensure((size_t)std::max<int64_t>(wl[0] + wl[1], 1) * 8)) return rc;
+    }
+    hipLaunchKernelGGL(k_row_stage, dim3(wgrid), dim3(kBlock), 0, s, in.values, n_rows, K, c->row_group.as<uint32_t>(),
+                       c->row_st.as<int64_t>(), c->raw_len.as<int32_t>(), c->woff.as<int64_t>(),
+                       c->packed.as<uint64_t>(), c->row_obs.as<int64_t>(), c->row_len.as<int32_t>(), gstat);
     ROGTK_HIP_CHECK(hipGetLastError());
     if (c->lds_path && K <= 32) {
+        // one workgroup per small group, straight from the packed rows
         if (int rc = c->gsmall.ensure((size_t)G)) return rc;
-        hipLaunchKernelGGL(k_group_classify, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, in.offsets, OW,
-                           in.rows, go, G, in.gk, K, c->row_obs.as<int64_t>(), c->gsmall.as<uint8_t>());
-        hipLaunchKernelGGL((k_kmer_lds<OW>), dim3((unsigned)std::min<int64_t>(G, 65536)), dim3(kBlock), 0, s,
-                           in.offsets, in.values, in.rows, go, G, c->gsmall.as<uint8_t>(), K, min_cov,
-                           c->row_obs.as<int64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
+        hipLaunchKernelGGL(k_group_classify, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, go, G, in.gk, K,
+                           c->row_obs.as<int64_t>(), c->row_words.as<int64_t>(), c->gsmall.as<uint8_t>());
+        hipLaunchKernelGGL(k_kmer_lds<1>, dim3((unsigned)std::min<int64_t>(G, 65536)), dim3(kBlock), 0, s, go, G,
+                           c->gsmall.as<uint8_t>(), K, min_cov, c->row_obs.as<int64_t>(), c->row_len.as<int32_t>(),
+                           c->woff.as<int64_t>(), c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
+                           c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
+        hipLaunchKernelGGL(k_kmer_lds<2>, dim3((unsigned)std::min<int64_t>(G, 8192)), dim3(kBlock), 0, s, go, G,
+                           c->gsmall.as<uint8_t>(), K, min_cov, c->row_obs.as<int64_t>(), c->row_len.as<int32_t>(),
+                           c->woff.as<int64_t>(), c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
                            c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
         hipLaunchKernelGGL(k_drop_small_rows, dim3(grid_for(n_rows)), dim3(kBlock), 0, s, c->row_group.as<uint32_t>(),
                            c->gsmall.as<uint8_t>(), n_rows, c->row_obs.as<int64_t>());

@@ -87,12 +87,14 @@ def test_auto_k(rg):
 
 
 def test_many_groups_mixed(rg):
-    """Many groups, each one polars group: sizes 0..100 rows (small ones take the LDS
-    path, the larger ones the global path in the same call), mixed validity and bytes."""
+    """Many groups, each one polars group: sizes 0..200 rows (small and medium ones take
+    the two LDS size classes, the largest the global path, all in the same call), mixed
+    validity and bytes."""
     rng = np.random.default_rng(11)
     items, go = [], [0]
     for g in range(300):
-        m = int(rng.integers(0, 40)) if rng.random() < 0.85 else int(rng.integers(60, 100))
+        u = rng.random()  # LDS class 1 (<= 2048 obs), class 2 (<= 4096) and global-path groups
+        m = int(rng.integers(0, 40)) if u < 0.8 else int(rng.integers(60, 100)) if u < 0.9 else int(rng.integers(120, 200))
         tpl = _reads(rng, 1, 150, 150)[0]
         for _ in range(m):
             r = rng.random()

@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""C3 measurement (BASELINE.json configs[2]): UMI grouping + k-mer front end on 1 MI355X.
+
+One step = one batch of synthetic 150-bp reads with 12-bp UMIs, resident in HBM:
+  H3 exact UMI ids    (mark -> bitmap -> resolve(max_distance 0) -> assign; the
+                       caller-side group_by('umi') of rogtk/__init__.py:206-214)
+  group_by            rogtk_group_by_key: stable radix sort of the ids -> row
+                       permutation + group offsets
+  k-mer spectra       rogtk_kmer_spectrum_dev, k = 17 (effective 32), min_coverage
+                       20 (rogtk/__init__.py:212): filter_kmers + CountFilter +
+                       censored exts per group (LDS path for small groups)
+Prints one JSON line: reads/s over the timed steps, per-phase HIP-event times and
+the LDS / global path split. Not the driver's bench (bench.py is C2).
+
+Usage: python tools/bench_kmer.py [--reads 10000000 --steps 5 --warmup 1]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from rogtk_amd import _lib  # noqa: E402
+from rogtk_amd import device as D  # noqa: E402
+from rogtk_amd import synth  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=10_000_000)
+    ap.add_argument("--read-len", type=int, default=150)
+    ap.add_argument("--k", type=int, default=17)
+    ap.add_argument("--min-coverage", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--global-only", action="store_true", help="route every group through the radix-sort path")
+    args = ap.parse_args()
+    n, RL, L = args.reads, args.read_len, 12
+    dev = torch.device("cuda", 0)
+    t0 = time.time()
+    codes = torch.from_numpy(synth.umi_codes(n, L).view(np.int32)).to(dev)
+    reads = torch.empty(n * RL, dtype=torch.uint8, device=dev)
+    chunk = 2_000_000
+    for a in range(0, n, chunk):  # host generator (OpenMP), streamed to HBM
+        b = min(n, a + chunk)
+        reads[a * RL:b * RL] = torch.from_numpy(synth.reads(n, RL, start=a, count=b - a).reshape(-1)).to(dev)
+    offsets = torch.arange(0, (n + 1) * RL, RL, dtype=torch.int64, device=dev)
+    gen_s = time.time() - t0
+    batch = D.PackedBatch(codes, L)
+    eng = D.ClusterEngine(L, min(n, 4 ** L), dev)
+    cid = torch.empty(n, dtype=torch.int32, device=dev)
+    cap = n * max(0, RL - 3)
+    _lib.call("rogtk_kmer_set_path", 0 if args.global_only else 1)
+    ev = lambda: torch.cuda.Event(enable_timing=True)
+    phases = {"cluster": 0.0, "group_by": 0.0, "kmer": 0.0}
+    out = None
+
+    def step(record):
+        nonlocal out
+        e0, e1, e2, e3 = ev(), ev(), ev(), ev()
+        e0.record()
+        D.cluster_batch(eng, batch, cid, 0)
+        e1.record()
+        rows, go, G = D.group_by_key(cid)
+        e2.record()
+        out = D.kmer_spectrum_dev(offsets, reads, go, args.k, args.min_coverage, cap, rows=rows)
+        e3.record()
+        torch.cuda.synchronize()
+        if record:
+            phases["cluster"] += e0.elapsed_time(e1)
+            phases["group_by"] += e1.elapsed_time(e2)
+            phases["kmer"] += e2.elapsed_time(e3)
+        return G
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        G = step(True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t
+    paths = (ctypes.c_int64 * 2)()
+    _lib.call("rogtk_kmer_path_stats", paths)
+    st = out["stats"].cpu().numpy()
+    line = {
+        "metric": "reads/s UMI group_by + k-mer spectra (C3 front end), 150 bp reads, 12 bp UMI, 1 MI355X",
+        "value": round(n * args.steps / el, 1), "unit": "reads/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 3),
+        "config": {"workload": "C3: H3 exact UMI ids -> group_by -> k-mer spectra per group",
+                   "reads": n, "read_len": RL, "umi_len": L, "k": args.k, "k_eff": int(st[:, 0].max()),
+                   "min_coverage": args.min_coverage, "groups": G, "lds_groups": paths[0],
+                   "global_groups": paths[1], "valid_kmers": int(out["entry_offsets"][-1].item()),
+                   "sequences": int(st[:, 1].sum())},
+        "phases_ms": {k: round(v / args.steps, 3) for k, v in phases.items()},
+        "observations_per_s": round(n * (RL - int(st[:, 0].max()) + 1) * args.steps / el, 1),
+        "data": f"synthetic (synth-v1 reads + UMIs, {n // 10} molecules), generated in {gen_s:.1f} s, resident in HBM",
+    }
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
