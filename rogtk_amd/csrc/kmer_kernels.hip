@@ -355,6 +355,8 @@ __global__ __launch_bounds__(kBlock) void k_pack(const uint64_t* __restrict__ t_
 // exts share one u32: count in bits 0..23, exts in 24..31), the valid entries are
 // compacted, bitonic-sorted and censored by binary search, all in LDS. The all-ones
 // key (TTT..T at k = 32) equals the empty marker and gets a dedicated slot.
+constexpr int kLdsBlock = 512;  // 8 waves per group workgroup (16 per CU for class 1; 1024 measured slower)
+
 // Two size classes: class 1 (<= 2048 observations, ~78 KB LDS, 2 workgroups per CU)
 // and class 2 (<= 4096 observations, ~155 KB, 1 per CU). Larger groups take the
 // global radix-sort path.
@@ -378,10 +380,16 @@ __device__ __forceinline__ bool kless(uint64_t ka, uint32_t ia, uint64_t kb, uin
     return ka < kb || (ka == kb && (ia >> 31) < (ib >> 31));  // real entries before pads
 }
 
-template <int CLS>
-__global__ __launch_bounds__(kBlock) void k_kmer_lds(const int64_t* __restrict__ go, int64_t G,
+// What an LDS-path group needs to start: its first grouped row, first packed word,
+// row count and packed word count (written by k_group_classify).
+struct GroupDesc {
+    int64_t r0, w0;
+    int32_t nrows, nwords;
+};
+
+template <int CLS, int TB>
+__global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ gdesc, int64_t G,
                                                      const uint8_t* __restrict__ gsmall, int K, int64_t min_cov,
-                                                     const int64_t* __restrict__ row_obs,
                                                      const int32_t* __restrict__ row_len,
                                                      const int64_t* __restrict__ woff,
                                                      const uint64_t* __restrict__ packed,
@@ -390,6 +398,7 @@ __global__ __launch_bounds__(kBlock) void k_kmer_lds(const int64_t* __restrict__
                                                      uint16_t* __restrict__ t_cnt, int64_t* __restrict__ gcount,
                                                      unsigned long long* __restrict__ gstat) {
     using C = LdsCfg<CLS>;
+    constexpr int kWaves = TB / 64;
     constexpr int kLdsObs = C::kObs, kLdsSlots = C::kSlots, kLdsRows = C::kRows, kLdsWords = C::kWords;
     __shared__ unsigned long long tkey[kLdsSlots + 1];
     __shared__ uint32_t tinfo[kLdsSlots + 1];  // count (bits 0..23) | exts << 24
@@ -401,28 +410,40 @@ __global__ __launch_bounds__(kBlock) void k_kmer_lds(const int64_t* __restrict__
     int32_t* const m_w = m_nobs + kLdsRows;
     uint64_t* const vkey = ubuf;                                       // after the inserts
     uint32_t* const vinfo = reinterpret_cast<uint32_t*>(ubuf + kLdsObs);  // count | exts << 16 | pad << 31
-    __shared__ uint32_t scan[kWavesPerBlock];
+    __shared__ uint32_t scan[kWaves];
     __shared__ uint32_t s_claimed, s_term, s_iso;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int hbits = 31 - __clz(kLdsSlots);
     const uint64_t kmask = K == 32 ? ~0ull : ((1ull << (2 * K)) - 1ull);
-    for (int i = tid; i <= kLdsSlots; i += kBlock) {  // once; groups reset only what they touch
+    for (int i = tid; i <= kLdsSlots; i += TB) {  // once; groups reset only what they touch
         tkey[i] = kEmpty;
         tinfo[i] = 0;
     }
     if (tid == 0) s_claimed = 0;
-    for (int64_t g = blockIdx.x; g < G; g += gridDim.x) {
-        if (gsmall[g] != CLS) continue;  // uniform per block
-        const int64_t r0 = go[g], r1 = go[g + 1];
-        const int nrows = (int)(r1 - r0);  // <= kLdsRows (classification)
-        const int64_t w0 = woff[r0];
-        const int nwords = (int)(woff[r1 - 1] + ((row_len[r1 - 1] + 31) >> 5) - w0);  // <= kLdsWords
-        for (int i = tid; i < nrows; i += kBlock) {
-            m_len[i] = row_len[r0 + i];
-            m_nobs[i] = (int32_t)row_obs[r0 + i];
+    // the next group's class and descriptor are loaded while the current one is
+    // processed (one exposed round trip per group: its rows' lengths, offsets, words)
+    int64_t g_next = blockIdx.x;
+    uint8_t cls_next = g_next < G ? gsmall[g_next] : 0;
+    GroupDesc d_next = g_next < G ? gdesc[g_next] : GroupDesc{0, 0, 0, 0};
+    while (g_next < G) {
+        const int64_t g = g_next;
+        const uint8_t cls = cls_next;
+        const GroupDesc d = d_next;
+        g_next += gridDim.x;
+        if (g_next < G) {
+            cls_next = gsmall[g_next];
+            d_next = gdesc[g_next];
+        }
+        if (cls != CLS) continue;  // uniform per block
+        const int64_t r0 = d.r0, w0 = d.w0;
+        const int nrows = d.nrows, nwords = d.nwords;  // within LdsCfg<CLS> (classification)
+        for (int i = tid; i < nrows; i += TB) {
+            const int32_t len = row_len[r0 + i];
+            m_len[i] = len;
+            m_nobs[i] = len ? len - K + 1 : 0;
             m_w[i] = (int32_t)(woff[r0 + i] - w0);
         }
-        for (int i = tid; i < nwords; i += kBlock) words[i] = packed[w0 + i];
+        for (int i = tid; i < nwords; i += TB) words[i] = packed[w0 + i];
         if (tid == 0) {
             words[nwords] = 0;
             s_term = 0;
@@ -430,7 +451,7 @@ __global__ __launch_bounds__(kBlock) void k_kmer_lds(const int64_t* __restrict__
         }
         __syncthreads();
         // every k-mer observation of the group, straight from the packed words in LDS
-        for (int ri = wave; ri < nrows; ri += kWavesPerBlock) {
+        for (int ri = wave; ri < nrows; ri += kWaves) {
             const int nobs = m_nobs[ri];
             if (nobs == 0) continue;
             const int len = m_len[ri];
@@ -462,7 +483,7 @@ __global__ __launch_bounds__(kBlock) void k_kmer_lds(const int64_t* __restrict__
         // CountFilter + compaction over the claimed slots: wave-shuffle scan, one
         // barrier for the per-wave totals
         const uint32_t ncl = s_claimed;
-        const uint32_t per = (ncl + kBlock - 1) / kBlock;
+        const uint32_t per = (ncl + TB - 1) / TB;
         const uint32_t c0 = min(ncl, tid * per), c1 = min(ncl, c0 + per);
         uint32_t mine = 0;
         for (uint32_t i = c0; i < c1; ++i) {
@@ -479,7 +500,7 @@ __global__ __launch_bounds__(kBlock) void k_kmer_lds(const int64_t* __restrict__
         __syncthreads();
         uint32_t wbase = 0, nv = 0;
 #pragma unroll
-        for (int w2 = 0; w2 < kWavesPerBlock; ++w2) {
+        for (int w2 = 0; w2 < kWaves; ++w2) {
             if (w2 < wave) wbase += scan[w2];
             nv += scan[w2];
         }
@@ -496,7 +517,7 @@ __global__ __launch_bounds__(kBlock) void k_kmer_lds(const int64_t* __restrict__
         }
         __syncthreads();
         // reset the touched slots for the next group (the table is not read again here)
-        for (uint32_t i = tid; i < ncl; i += kBlock) {
+        for (uint32_t i = tid; i < ncl; i += TB) {
             const uint32_t sl = claimed[i];
             tkey[sl] = kEmpty;
             tinfo[sl] = 0;
@@ -565,14 +586,14 @@ __global__ __launch_bounds__(kBlock) void k_kmer_lds(const int64_t* __restrict__
         }
         uint32_t P = 2;
         while (P < nv) P <<= 1;
-        for (uint32_t i = nv + tid; i < P; i += kBlock) {
+        for (uint32_t i = nv + tid; i < P; i += TB) {
             vkey[i] = kEmpty;
             vinfo[i] = 1u << 31;
         }
         __syncthreads();
         for (uint32_t k2 = 2; k2 <= P; k2 <<= 1) {  // bitonic sort, ascending
             for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
-                for (uint32_t i = tid; i < P; i += kBlock) {
+                for (uint32_t i = tid; i < P; i += TB) {
                     const uint32_t ij = i ^ j;
                     if (ij > i) {
                         const uint64_t ka = vkey[i], kb = vkey[ij];
@@ -590,7 +611,7 @@ __global__ __launch_bounds__(kBlock) void k_kmer_lds(const int64_t* __restrict__
             }
         }
         // remove_censored_exts + output at the group's capacity offset
-        for (uint32_t i = tid; i < nv; i += kBlock) {
+        for (uint32_t i = tid; i < nv; i += TB) {
             const uint64_t key = vkey[i];
             const uint32_t info = vinfo[i];
             const uint32_t e = (info >> 16) & 0xFFu;
@@ -632,7 +653,8 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
                                                            const uint8_t* __restrict__ gk, int K,
                                                            const int64_t* __restrict__ row_obs,
                                                            const int64_t* __restrict__ row_words,
-                                                           uint8_t* __restrict__ gsmall) {
+                                                           const int64_t* __restrict__ woff,
+                                                           uint8_t* __restrict__ gsmall, GroupDesc* __restrict__ gdesc) {
     const int lane = threadIdx.x & 63;
     const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
     for (int64_t g = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); g < G; g += waves) {
@@ -657,6 +679,7 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
                 else if (obs <= LdsCfg<2>::kObs && nrows <= LdsCfg<2>::kRows && words <= LdsCfg<2>::kWords) cls = 2;
             }
             gsmall[g] = cls;
+            if (cls) gdesc[g] = GroupDesc{go[g], woff[go[g]], (int32_t)nrows, (int32_t)words};
         }
     }
 }
@@ -755,7 +778,7 @@ struct KmerCtx {
     int device = -1;
     hipStream_t stream = nullptr;
     DevBuf offsets, values, validity, go, gk, cap_off, gstat, gstart, gcount, out_off;
-    DevBuf row_group, row_obs, obs_off, row_len, row_words, woff, packed, row_st, raw_len;
+    DevBuf row_group, row_obs, obs_off, row_len, row_words, woff, packed, row_st, raw_len, gdesc;
     DevBuf key_lo, key_hi, ext, grp, idx, perm_a, perm_b, tmp_u64, tmp_u32;
     DevBuf s_lo, s_hi, s_ext, s_grp, head, rid, r_valid, r_first, r_ext, r_cnt, vpos;
     DevBuf v_lo, v_hi, v_grp, v_ext, v_cnt, t_kmer, t_ext, t_cnt, o_kmer, o_ext, o_cnt, cub, gsmall, caps, scal;
@@ -865,14 +888,18 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
     if (c->lds_path && K <= 32) {
         // one workgroup per small group, straight from the packed rows
         if (int rc = c->gsmall.ensure((size_t)G)) return rc;
+        if (int rc = c->gdesc.ensure((size_t)G * sizeof(GroupDesc))) return rc;
         hipLaunchKernelGGL(k_group_classify, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, go, G, in.gk, K,
-                           c->row_obs.as<int64_t>(), c->row_words.as<int64_t>(), c->gsmall.as<uint8_t>());
-        hipLaunchKernelGGL(k_kmer_lds<1>, dim3((unsigned)std::min<int64_t>(G, 65536)), dim3(kBlock), 0, s, go, G,
-                           c->gsmall.as<uint8_t>(), K, min_cov, c->row_obs.as<int64_t>(), c->row_len.as<int32_t>(),
+                           c->row_obs.as<int64_t>(), c->row_words.as<int64_t>(), c->woff.as<int64_t>(),
+                           c->gsmall.as<uint8_t>(), c->gdesc.as<GroupDesc>());
+        hipLaunchKernelGGL((k_kmer_lds<1, kLdsBlock>), dim3((unsigned)std::min<int64_t>(G, 65536)), dim3(kLdsBlock), 0, s,
+                           c->gdesc.as<GroupDesc>(), G,
+                           c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
                            c->woff.as<int64_t>(), c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
                            c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
-        hipLaunchKernelGGL(k_kmer_lds<2>, dim3((unsigned)std::min<int64_t>(G, 8192)), dim3(kBlock), 0, s, go, G,
-                           c->gsmall.as<uint8_t>(), K, min_cov, c->row_obs.as<int64_t>(), c->row_len.as<int32_t>(),
+        hipLaunchKernelGGL((k_kmer_lds<2, kLdsBlock>), dim3((unsigned)std::min<int64_t>(G, 8192)), dim3(kLdsBlock), 0, s,
+                           c->gdesc.as<GroupDesc>(), G,
+                           c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
                            c->woff.as<int64_t>(), c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
                            c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
         hipLaunchKernelGGL(k_drop_small_rows, dim3(grid_for(n_rows)), dim3(kBlock), 0, s, c->row_group.as<uint32_t>(),
