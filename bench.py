@@ -66,8 +66,14 @@ def setup_dist(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # ROGTK_DIST_BACKEND=gloo (tests only): several ranks may then share one GPU
+        backend = os.environ.get("ROGTK_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     return world, rank
@@ -156,7 +162,7 @@ def main():
             if launches:
                 kernels[k] = {"avg_us": 1000.0 * ms / launches, "launches": launches}
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     stats = pipe.slots[0].eng.stats()

@@ -31,6 +31,10 @@ def gather_bitmaps(local: torch.Tensor, group=None):
     out = torch.empty(n * local.numel(), dtype=local.dtype, device=local.device)
     if dist.get_backend(group) == "nccl":
         dist.all_gather_into_tensor(out, local, group=group)
+    elif local.is_cuda:  # gloo with device tensors (multi-rank rehearsal on one GPU): stage via host
+        host = torch.empty(n * local.numel(), dtype=local.dtype)
+        dist.all_gather(list(host.chunk(n)), local.cpu(), group=group)
+        out.copy_(host)
     else:
         dist.all_gather(list(out.chunk(n)), local, group=group)
     return out, n
