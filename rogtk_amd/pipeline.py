@@ -41,7 +41,7 @@ class UmiPipeline:
     def __init__(self, umi_len: int, max_distinct: int, n_max: int, device=None, depth: int = 3,
                  target: Optional[bytes] = b"ACGTACGTACGT", max_hamming: int = 1, max_distance: int = 1,
                  group=None, with_scores: bool = True, priorities=(0, 0, 0), mark: str = "xcd",
-                 on_assigned=None):
+                 on_assigned=None, score_alone: bool = False):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
@@ -62,6 +62,10 @@ class UmiPipeline:
         # on_assigned(slot, batch): called with the assign stream current, after the
         # batch's assign and before its slot may be reused (e.g. to copy outputs out)
         self.on_assigned = on_assigned
+        # score_alone: assign of the previous batch waits for this batch's score kernel,
+        # so the HBM-bound score overlaps only the latency-bound resolve kernels
+        self.score_alone = score_alone
+        self.last_scored: Optional[torch.cuda.Event] = None
         self.k = 0
         self.last_assigned: Optional[torch.cuda.Event] = None
 
@@ -73,6 +77,9 @@ class UmiPipeline:
             self.main.wait_event(slot.assigned)
         D.score_packed(batch, slot.scores, self.target, self.max_hamming, None, slot.within,
                        cluster=slot.eng if self.fused_mark else None, stream=self.main)
+        if self.score_alone:
+            self.last_scored = torch.cuda.Event()
+            self.last_scored.record(self.main)
         if not self.fused_mark:
             slot.eng.mark(batch, stream=self.main)
         slot.eng.build_local_bitmap(stream=self.main)
@@ -93,6 +100,8 @@ class UmiPipeline:
     def _assign_oldest(self):
         slot, batch, resolved = self.queue.popleft()
         self.s_assign.wait_event(resolved)
+        if self.score_alone and self.last_scored is not None:
+            self.s_assign.wait_event(self.last_scored)
         slot.eng.assign(batch, slot.cid, stream=self.s_assign)
         if self.on_assigned is not None:
             with torch.cuda.stream(self.s_assign):

@@ -337,9 +337,10 @@ def test_full_size_c2_properties(rg):
                           scores["combined_score"][:n].cpu().numpy().view(np.uint64))
 
 
-@pytest.mark.parametrize("depth,nb", [(4, 4), (2, 5), (1, 3), (3, 7)])
+@pytest.mark.parametrize("depth,nb,alone", [(4, 4, False), (2, 5, False), (1, 3, False), (3, 7, False),
+                                             (2, 6, True), (3, 5, True)])
 @pytest.mark.parametrize("mark", ["xcd", "fused"])
-def test_streaming_pipeline_matches_sequential(rg, depth, nb, mark):
+def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark):
     """rogtk_amd.pipeline (3 streams, `depth` batches in flight) == the sequential device
     path for EVERY batch (outputs copied out by the on_assigned hook before slot reuse)."""
     import torch
@@ -357,7 +358,7 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb, mark):
                      slot.scores["longest_homopolymer_run"][:n].clone()))
 
     pipe = UmiPipeline(L, n, n, "cuda", depth=depth, target=b"ACGTACGTACGT", max_distance=1, mark=mark,
-                       on_assigned=grab)
+                       on_assigned=grab, score_alone=alone)
     keep = []
     for s in seeds:
         codes = torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda()
