@@ -211,8 +211,9 @@ __device__ __forceinline__ uint64_t multi_of4(uint64_t a, uint64_t b, uint64_t c
 // ---------------------------------------------------------------- local CC
 // One workgroup owns 4^7 consecutive codes (256 bitmap words): every Hamming-1
 // edge at positions 0..6 stays inside it, so the whole union-find for those
-// positions runs in LDS: one pass of CAS unions over the local cliques (an
-// atomic-free link pre-pass was measured slower than it saved). Output: D (sorted distinct
+// positions runs in LDS. Positions 0..2 live inside one 64-bit word: their
+// components come from a bit-parallel BFS on the word mask (no atomics); positions
+// 3..6 unite whole word components that intersect (CAS union-find). Output: D (sorted distinct
 // codes), f (global index of the local root: stars), and UR[w] = the shared root
 // of word w when all its codes are in one local component (the common case when
 // the code space is dense).
@@ -257,6 +258,37 @@ __device__ __forceinline__ void lunite(uint32_t* lf, uint32_t a, uint32_t b) {
 }
 
 
+// Hamming-1 neighbours inside a 64-code word (positions 0..dims-1 of the code =
+// bit strides 1, 4, 16 in groups of 4): any bit set in a group of 4 spreads to all 4.
+__device__ __forceinline__ uint64_t word_spread(uint64_t x, int dims) {
+    uint64_t s = x;
+    const uint64_t g0 = (x | (x >> 1) | (x >> 2) | (x >> 3)) & 0x1111111111111111ull;
+    s |= g0 * 0xFull;
+    if (dims > 1) {
+        const uint64_t g1 = (x | (x >> 4) | (x >> 8) | (x >> 12)) & 0x000F000F000F000Full;
+        s |= g1 * 0x1111ull;
+    }
+    if (dims > 2) {
+        const uint64_t g2 = (x | (x >> 16) | (x >> 32) | (x >> 48)) & 0xFFFFull;
+        s |= g2 * 0x0001000100010001ull;
+    }
+    return s;
+}
+
+// the union of the components of word mask m that contain a bit of seed
+__device__ __forceinline__ uint64_t word_component_any(uint64_t m, uint64_t seed, int dims) {
+    uint64_t c = seed & m;
+    for (;;) {  // <= 4 rounds: the 4x4x4 rook graph has diameter 3
+        const uint64_t n = word_spread(c, dims) & m;
+        if (n == c) return c;
+        c = n;
+    }
+}
+
+__device__ __forceinline__ uint64_t word_component(uint64_t m, uint64_t seed_bit, int dims) {
+    return word_component_any(m, seed_bit, dims);
+}
+
 __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ RT, int64_t words, int L,
                                                      uint32_t* __restrict__ D, uint32_t* __restrict__ f,
                                                      uint32_t* __restrict__ UR, int64_t max_distinct,
@@ -276,45 +308,61 @@ __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ R
     const uint32_t ex = block_excl_scan((uint32_t)__popcll(m), s_wave, nloc);
     lpre[t] = ex;
     const uint32_t gbase = RT[base].z;
-    for (uint32_t i = t; i < nloc; i += kBlock) lf[i] = i;
-    __syncthreads();
-    // one pass over the local cliques: unite every member with the clique's first
+    const int indims = lpos < 3 ? lpos : 3;  // positions inside one 64-code word
+    // 1. components inside each word (positions 0..2): bit-parallel BFS on the word's
+    //    mask; every code's parent is its component's first code (stars, no atomics)
     {
-        uint32_t r[4];
-        const int inword = lpos < 3 ? lpos : 3;
-        for (int p = 0; m && p < inword; ++p) {
-            const int sh = 2 * p;
-            const uint64_t keep = p == 0 ? 0x1111111111111111ull : p == 1 ? 0x000F000F000F000Full
-                                                                            : 0x000000000000FFFFull;
-            uint64_t multi = multi_of4(m, m >> (1 << sh), m >> (2 << sh), m >> (3 << sh)) & keep;
-            while (multi) {
-                const int b = __ffsll((long long)multi) - 1;
-                multi &= multi - 1;
-                int k = 0;
-                for (int v = 0; v < 4; ++v) {
-                    const int bit = b + (v << sh);
-                    if ((m >> bit) & 1ull) r[k++] = ex + (uint32_t)__popcll(m & ((1ull << bit) - 1ull));
-                }
-                for (int v = 1; v < k; ++v) lunite(lf, r[0], r[v]);
+        uint64_t rem = m;
+        while (rem) {
+            const int b0 = __ffsll((long long)rem) - 1;
+            const uint64_t comp = word_component(m, 1ull << b0, indims);
+            rem &= ~comp;
+            const uint32_t root = ex + (uint32_t)__popcll(m & ((1ull << b0) - 1ull));
+            uint64_t cc = comp;
+            while (cc) {
+                const int b = __ffsll((long long)cc) - 1;
+                cc &= cc - 1;
+                lf[ex + (uint32_t)__popcll(m & ((1ull << b) - 1ull))] = root;
             }
         }
+    }
+    __syncthreads();
+    // 2. positions 3..lpos-1 join words 4^(p-3) apart: codes at the same bit of the 4
+    //    words of a group differ only at p, so two word components that share a bit
+    //    are adjacent; unite every intersecting pair of components (root = first code)
+    {
         const int per = nw >> 2;
         if (per > 0 && t < (lpos - 3) * per) {
             const int p = 3 + t / per, g = t % per, s2 = 2 * p - 6, stride = 1 << s2;
             const int w0 = ((g >> s2) << (s2 + 2)) | (g & (stride - 1));
             uint64_t mv[4];
+            uint32_t pv[4];
 #pragma unroll
-            for (int v = 0; v < 4; ++v) mv[v] = wb[w0 + v * stride];
-            uint64_t multi = multi_of4(mv[0], mv[1], mv[2], mv[3]);
-            while (multi) {
-                const int b = __ffsll((long long)multi) - 1;
-                multi &= multi - 1;
-                const uint64_t below = (1ull << b) - 1ull;
-                int k = 0;
-#pragma unroll
-                for (int v = 0; v < 4; ++v)
-                    if ((mv[v] >> b) & 1ull) r[k++] = lpre[w0 + v * stride] + (uint32_t)__popcll(mv[v] & below);
-                for (int v = 1; v < k; ++v) lunite(lf, r[0], r[v]);
+            for (int v = 0; v < 4; ++v) {
+                mv[v] = wb[w0 + v * stride];
+                pv[v] = lpre[w0 + v * stride];
+            }
+            for (int a = 0; a < 3; ++a) {
+                uint64_t rem = mv[a];
+                // only components that meet a later word matter
+                uint64_t later = 0;
+                for (int b = a + 1; b < 4; ++b) later |= mv[b];
+                rem &= word_component_any(mv[a], rem & later, indims);
+                while (rem) {
+                    const int ba = __ffsll((long long)rem) - 1;
+                    const uint64_t ca = word_component(mv[a], 1ull << ba, indims);
+                    rem &= ~ca;
+                    const uint32_t ra = pv[a] + (uint32_t)__popcll(mv[a] & ((1ull << ba) - 1ull));
+                    for (int b = a + 1; b < 4; ++b) {
+                        uint64_t x = ca & mv[b];
+                        while (x) {
+                            const uint64_t cb = word_component(mv[b], x & (~x + 1ull), indims);
+                            x &= ~cb;
+                            const int bb = __ffsll((long long)cb) - 1;
+                            lunite(lf, ra, pv[b] + (uint32_t)__popcll(mv[b] & ((1ull << bb) - 1ull)));
+                        }
+                    }
+                }
             }
         }
     }
