@@ -236,6 +236,47 @@ int rogtk_kmer_spectrum_host(const void* offsets, int offset_width, const uint8_
                              uint8_t* exts, uint16_t* counts, int64_t* entry_offsets,
                              int64_t* group_stats);
 
+/* ======= H4.4 + H5: de Bruijn assembly of one read group (host C++ + GPU spectra) =======
+ * One call = one polars group. The group's k-mer spectrum is computed on the GPU
+ * (rogtk_kmer_spectrum_host at min_coverage 0, once per effective k per call);
+ * CountFilter, censoring, graph build, compression (compress_graph, stranded,
+ * summed counts) and path finding (djfind.rs: petgraph Dijkstra over -ln(mean
+ * coverage) edge weights) run natively on the host. Methods: "compression",
+ * "shortest_path" (start_anchor and end_anchor required), "shortest_path_auto".
+ * Node order is ascending k-mer order (the reference's MPHF order is not
+ * reproducible): which of several equally long contigs is "largest", and Dijkstra
+ * ties, follow that order. Graph export (DOT / CSV files) is not performed. */
+
+/* assemble_sequences_expr (expressions.rs:695-762) / assemble_sequences
+ * (fracture.rs:188-280): contigs joined by '\n' into out (out_cap bytes; *out_len =
+ * the full length, ROGTK_E_OVERFLOW if larger than out_cap). min_length < 0 = none.
+ * Invalid method / anchor combinations fail with the reference's messages. */
+int rogtk_assemble_host(const void* offsets, int offset_width, const uint8_t* values, int64_t values_len,
+                        const uint8_t* validity, int64_t validity_offset, int64_t n_rows, int k,
+                        int64_t min_coverage, const char* method, const char* start_anchor,
+                        const char* end_anchor, int only_largest, int64_t min_length, int auto_k,
+                        char* out, int64_t out_cap, int64_t* out_len, int64_t* n_contigs);
+
+/* sweep_assembly_params_expr (expressions.rs:880-955): for k in k_start..=k_end by
+ * k_step, for min_coverage in cov_start..=cov_end by cov_step: the largest contig's
+ * length (0 when none). Rows in that order; *n_out rows (ROGTK_E_OVERFLOW > cap). */
+int rogtk_assembly_sweep_host(const void* offsets, int offset_width, const uint8_t* values,
+                              int64_t values_len, const uint8_t* validity, int64_t validity_offset,
+                              int64_t n_rows, int64_t k_start, int64_t k_end, int64_t k_step,
+                              int64_t cov_start, int64_t cov_end, int64_t cov_step, const char* method,
+                              const char* start_anchor, const char* end_anchor, int64_t cap,
+                              int64_t* out_k, int64_t* out_cov, int64_t* out_len, int64_t* n_out);
+
+/* optimize_assembly_expr (fracture_opt.rs:120-356): greedy beam (4 paths) over
+ * (k, min_coverage); out4 = {k, min_coverage, length, input_sequences} (all 0 but
+ * input_sequences when no contig qualifies); the contig goes to contig. */
+int rogtk_assembly_optimize_host(const void* offsets, int offset_width, const uint8_t* values,
+                                 int64_t values_len, const uint8_t* validity, int64_t validity_offset,
+                                 int64_t n_rows, const char* method, const char* start_anchor,
+                                 const char* end_anchor, int64_t start_k, int64_t start_min_coverage,
+                                 int64_t max_iterations, int explore_k, int prioritize_length, char* contig,
+                                 int64_t contig_cap, int64_t* contig_len, uint32_t* out4);
+
 /* ============================== profiling ================================ */
 /* When enabled, every kernel launch is bracketed by HIP events on its stream. */
 int rogtk_profile_enable(int on);

@@ -10,6 +10,7 @@ Drop-in surface (mirrors rogtk/__init__.py's `umi` / `hamming` namespaces):
     rg.umi_complexity_scores(umis)
     rg.umi_cluster(umis, max_distance=1)         # H3 (caller-side group_by('umi'))
     rg.kmer_spectrum(reads, k=17, min_coverage=20, group_offsets=...)  # H4 (fracture.rs)
+    rg.assemble_sequences(group_reads, k=13, min_coverage=1, method="compression")  # H5
 
 Device-resident pipeline (packed SoA in HBM, torch tensors as plumbing):
     rogtk_amd.device (PackedBatch, score_packed, ClusterEngine, cluster_batch)
@@ -17,6 +18,12 @@ Multi-GPU exchange: rogtk_amd.dist. Synthetic data: rogtk_amd.synth.
 C ABI: include/rogtk_hip.h (librogtk_hip.so, in-tree).
 """
 from ._lib import RogtkError, device_count, version  # noqa: F401
+from .assembly import (  # noqa: F401
+    assemble_sequences,
+    assemble_sequences_with_anchors,
+    optimize_assembly,
+    sweep_assembly_params,
+)
 from .api import (  # noqa: F401
     FIELDS,
     KMER_STATS,
@@ -36,5 +43,6 @@ from .api import (  # noqa: F401
 __all__ = [
     "RogtkError", "device_count", "version", "FIELDS", "STRUCT_TYPE", "Col", "HammingExpr",
     "UmiNamespace", "col", "hamming_distance", "hamming_within", "umi_cluster", "umi_complexity",
-    "umi_complexity_scores", "kmer_spectrum", "KMER_STATS",
+    "umi_complexity_scores", "kmer_spectrum", "KMER_STATS", "assemble_sequences",
+    "assemble_sequences_with_anchors", "sweep_assembly_params", "optimize_assembly",
 ]

@@ -80,6 +80,12 @@ SIGNATURES = {
     "rogtk_kmer_path_stats": [_P_I64],
     "rogtk_kmer_spectrum_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i32, _i32, _i64, _i64, _vp,
                                  _vp, _vp, _vp, _vp],
+    "rogtk_assemble_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _i32, _i64, ctypes.c_char_p, ctypes.c_char_p,
+                            ctypes.c_char_p, _i32, _i64, _i32, _vp, _i64, _P_I64, _P_I64],
+    "rogtk_assembly_sweep_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
+                                  ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, _i64, _vp, _vp, _vp, _P_I64],
+    "rogtk_assembly_optimize_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, ctypes.c_char_p, ctypes.c_char_p,
+                                     ctypes.c_char_p, _i64, _i64, _i64, _i32, _i32, _vp, _i64, _P_I64, _vp],
     "rogtk_profile_enable": [_i32],
     "rogtk_profile_reset": [],
     "rogtk_profile_read": [ctypes.c_char_p, _P_F64, _P_I64],

@@ -194,3 +194,24 @@ def test_kmer_oracle_reference_fixture():
     # k=4 (fracture.rs:685 test_compare_assembly_methods): non-empty spectrum
     r4 = P.kmer_spectrum(P.StrCol.from_list(seqs), 4, 1)
     assert r4["stats"][0][0] == 4 and r4["stats"][0][2] > 0
+
+
+# ---------------------------------------------------------------- H5 assembly restatement
+def test_assembly_restatement_reference_tests():
+    """oracle/pyassembly.py against the reference's own assembly tests (fracture.rs:593-761)."""
+    from oracle import pyassembly as A
+
+    seqs = [b"GAGACTGCATGGGCTGGTGGGCGTCCGTCTGC", b"GGGCTGGTGGGCGTCCGTCTGCTTTAGTGAGGGT"]
+    # :630-681 + the expected contig in the comment at :611
+    assert A.assemble(seqs, 13, 1, "shortest_path", "GAGACTGCATGG", "TTTAGTGAGGGT") == [
+        "GAGACTGCATGGGCTGGTGGGCGTCCGTCTGCTTTAGTGAGGGT"]
+    # :684-707 anchors absent -> no contig
+    assert A.assemble([b"AAAACCCCCAAAAA", b"TTTTTGGGGGTTTT"], 4, 1, "shortest_path", "NONEXISTENT",
+                      "ALSONOTHERE") == []
+    # :710-761 compression at k=4 yields a contig
+    assert A.assemble(seqs, 4, 1, "compression") != []
+    # Rust std BinaryHeap order (sift_up / sift_down_to_bottom) of the restated heap
+    h = A.RustHeap()
+    for s in (3.0, 1.0, 2.0, 1.0, 5.0, 0.5):
+        h.push((s, int(s * 10)))
+    assert [h.pop()[0] for _ in range(6)] == [0.5, 1.0, 1.0, 2.0, 3.0, 5.0]
