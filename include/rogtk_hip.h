@@ -277,6 +277,22 @@ int rogtk_assembly_optimize_host(const void* offsets, int offset_width, const ui
                                  int64_t max_iterations, int explore_k, int prioritize_length, char* contig,
                                  int64_t contig_cap, int64_t* contig_len, uint32_t* out4);
 
+/* ============ paired FASTQ ingest (host C++, zlib) ============
+ * parse_paired_fastqs (src/lib.rs:232-428) as a streaming reader of Arrow string
+ * columns: read_id, start ("0"), end ("1"), cbc, umi, cbc_qual, umi_qual, seq, qual
+ * (the reference's schema, lib.rs:258-268). limit_lines < 0 = no limit (the
+ * reference's `limit` counts LINES); do_rev_comp reverse-complements R2's sequence
+ * and reverses its qualities. A short read (cbc_len + umi_len beyond the line) or a
+ * truncated record is ROGTK_E_INVALID (a panic in the reference). */
+int rogtk_fastq_pair_open(const char* r1_path, const char* r2_path, int64_t cbc_len, int64_t umi_len,
+                          int64_t limit_lines, int do_rev_comp, void** reader);
+/* Next batch of <= max_records records: offsets9[c] (n + 1 int64) / values9[c] for
+ * the 9 columns, owned by the reader until the next call / close; *n_records = 0 at
+ * the end. */
+int rogtk_fastq_pair_next(void* reader, int64_t max_records, int64_t* n_records,
+                          const int64_t** offsets9, const uint8_t** values9);
+int rogtk_fastq_pair_close(void* reader);
+
 /* ============================== profiling ================================ */
 /* When enabled, every kernel launch is bracketed by HIP events on its stream. */
 int rogtk_profile_enable(int on);

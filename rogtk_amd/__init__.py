@@ -18,6 +18,7 @@ Multi-GPU exchange: rogtk_amd.dist. Synthetic data: rogtk_amd.synth.
 C ABI: include/rogtk_hip.h (librogtk_hip.so, in-tree).
 """
 from ._lib import RogtkError, device_count, version  # noqa: F401
+from .fastq import iter_paired_fastqs, parse_paired_fastqs  # noqa: F401
 from .assembly import (  # noqa: F401
     assemble_sequences,
     assemble_sequences_with_anchors,
@@ -44,5 +45,6 @@ __all__ = [
     "RogtkError", "device_count", "version", "FIELDS", "STRUCT_TYPE", "Col", "HammingExpr",
     "UmiNamespace", "col", "hamming_distance", "hamming_within", "umi_cluster", "umi_complexity",
     "umi_complexity_scores", "kmer_spectrum", "KMER_STATS", "assemble_sequences",
-    "assemble_sequences_with_anchors", "sweep_assembly_params", "optimize_assembly",
+    "assemble_sequences_with_anchors", "sweep_assembly_params", "optimize_assembly", "iter_paired_fastqs",
+    "parse_paired_fastqs",
 ]

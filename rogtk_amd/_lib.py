@@ -86,6 +86,9 @@ SIGNATURES = {
                                   ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, _i64, _vp, _vp, _vp, _P_I64],
     "rogtk_assembly_optimize_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, ctypes.c_char_p, ctypes.c_char_p,
                                      ctypes.c_char_p, _i64, _i64, _i64, _i32, _i32, _vp, _i64, _P_I64, _vp],
+    "rogtk_fastq_pair_open": [ctypes.c_char_p, ctypes.c_char_p, _i64, _i64, _i64, _i32, _vp],
+    "rogtk_fastq_pair_next": [_vp, _i64, _P_I64, _vp, _vp],
+    "rogtk_fastq_pair_close": [_vp],
     "rogtk_profile_enable": [_i32],
     "rogtk_profile_reset": [],
     "rogtk_profile_read": [ctypes.c_char_p, _P_F64, _P_I64],
