@@ -62,6 +62,10 @@ def parse():
     ap.add_argument("--overlap-score", action="store_true",
                     help="let assign of the previous batch overlap the score kernel (default: score overlaps "
                          "only the latency-bound resolve kernels)")
+    ap.add_argument("--emulate-ranks", type=int, default=1,
+                    help="(tools) on ONE GPU, act as rank 0 of W: the other W-1 shards' bitmaps are built once "
+                         "before timing and the all-gather is replaced by a device copy; predicts per-rank "
+                         "step time at N=W minus RCCL time. Never used by the driver.")
     ap.add_argument("--prio", type=str, default="0,0,0", help="stream priorities main,resolve,assign (-1 = high)")
     return ap.parse_args()
 
@@ -135,9 +139,34 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     codes = torch.from_numpy(codes_h.view(np.int32)).to(dev)
     batch = D.PackedBatch(codes, L)
+    exchange = None
+    if args.emulate_ranks > 1:
+        if world > 1:
+            raise SystemExit("--emulate-ranks is a single-process tool")
+        W = args.emulate_ranks
+        n_total = n * W
+        others = []
+        tmp = D.ClusterEngine(L, min(n_total, 4 ** L), dev)
+        for r in range(1, W):
+            s0, c0 = RD.shard_range(n_total, r, W)
+            cr = torch.from_numpy(synth.umi_codes(n_total, L, start=s0, count=c0).view(np.int32)).to(dev)
+            tmp.mark(D.PackedBatch(cr, L))
+            others.append(tmp.build_local_bitmap().clone())
+            del cr
+        del tmp
+        codes_h = synth.umi_codes(n_total, L, start=0, count=n)  # rank 0's shard of the W-rank dataset
+        codes = torch.from_numpy(codes_h.view(np.int32)).to(dev)
+        batch = D.PackedBatch(codes, L)
+        gathered = torch.cat([torch.zeros_like(others[0])] + others)
+
+        def exchange(bm):
+            gathered[: bm.numel()].copy_(bm)
+            return gathered, W
+
     pipe = UmiPipeline(L, min(n_total, 4 ** L), count, dev, depth=args.depth, target=TARGET,
                        max_distance=md, group=None,
-                       priorities=tuple(int(x) for x in args.prio.split(",")), mark=args.mark, score_alone=not args.overlap_score)
+                       priorities=tuple(int(x) for x in args.prio.split(",")), mark=args.mark,
+                       score_alone=not args.overlap_score, exchange=exchange)
 
     def step():
         pipe.submit(batch)
@@ -193,7 +222,7 @@ def main():
             dist.destroy_process_group()
         return
     ms_per_step = 1000.0 * el / args.steps
-    value = n_total * args.steps / el
+    value = n_total * args.steps / el if args.emulate_ranks == 1 else n * args.emulate_ranks * args.steps / el
     # roofline of the dominant kernel: algorithmic bytes per read of k_score_packed
     #   in: 4 B packed code; out: 6 x 8 B f64 fields + 4 B longest run + 1/8 B within bit
     bpr = 4 + 48 + 4 + 0.125
@@ -234,7 +263,9 @@ def main():
                                "H3 Hamming<=1 cluster ids",
                    "reads_per_gpu": count, "umi_len": L, "max_distance": md,
                    "n_distinct": stats["n_distinct"], "n_clusters": stats["n_clusters"],
-                   "parallelism": f"dp{world} shard-by-record + presence-bitmap all-gather"},
+                   "parallelism": f"dp{world} shard-by-record + presence-bitmap all-gather"
+                                  + (f" (rank 0 of {args.emulate_ranks} EMULATED on one GPU, no RCCL)"
+                                     if args.emulate_ranks > 1 else "")},
         "roofline": roof,
         "cpu_baseline": cpu,
         "kernels_us": {k: round(v["avg_us"], 2) for k, v in kernels.items()},

@@ -41,7 +41,7 @@ class UmiPipeline:
     def __init__(self, umi_len: int, max_distinct: int, n_max: int, device=None, depth: int = 3,
                  target: Optional[bytes] = b"ACGTACGTACGT", max_hamming: int = 1, max_distance: int = 1,
                  group=None, with_scores: bool = True, priorities=(0, 0, 0), mark: str = "xcd",
-                 on_assigned=None, score_alone: bool = False):
+                 on_assigned=None, score_alone: bool = False, exchange=None):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
@@ -65,6 +65,9 @@ class UmiPipeline:
         # score_alone: assign of the previous batch waits for this batch's score kernel,
         # so the HBM-bound score overlaps only the latency-bound resolve kernels
         self.score_alone = score_alone
+        # exchange(local_bitmap) -> (bitmaps, n): the cross-rank step (default: the
+        # all-gather of rogtk_amd.dist); tools may substitute an emulation
+        self.exchange = exchange if exchange is not None else (lambda bm: gather_bitmaps(bm, self.group))
         self.last_scored: Optional[torch.cuda.Event] = None
         self.k = 0
         self.last_assigned: Optional[torch.cuda.Event] = None
@@ -87,7 +90,7 @@ class UmiPipeline:
         marked.record(self.main)
         with torch.cuda.stream(self.s_resolve):
             self.s_resolve.wait_event(marked)
-            bitmaps, nb = gather_bitmaps(slot.eng.local_bitmap, self.group)
+            bitmaps, nb = self.exchange(slot.eng.local_bitmap)
             slot.eng.resolve(bitmaps, nb, self.max_distance, stream=self.s_resolve)
             resolved = torch.cuda.Event()
             resolved.record(self.s_resolve)
