@@ -159,6 +159,9 @@ int rogtk_cluster_assign(const void* ws, int umi_len, int64_t max_distinct,
 /* Copies {n_distinct, n_clusters, overflow, error} (int64 each) to host; syncs the stream. */
 int rogtk_cluster_stats(const void* ws, int umi_len, int64_t max_distinct, int64_t* out4,
                         void* stream);
+/* Diagnostics: the global hook rounds the last resolve of ws needed (completes it
+ * first, like rogtk_cluster_stats); 0 when it needed none (exact mode, umi_len <= 7). */
+int rogtk_cluster_rounds(const void* ws, void* stream, int* rounds);
 /* Releases the host-side resolve state kept for ws (call before freeing ws). */
 int rogtk_cluster_release(const void* ws);
 

@@ -479,6 +479,11 @@ int rogtk_cluster_stats(const void* ws, int umi_len, int64_t max_distinct, int64
     return ROGTK_OK;
 }
 
+int rogtk_cluster_rounds(const void* ws, void* stream, int* rounds) {
+    ROGTK_REQUIRE(ws && rounds, ROGTK_E_INVALID, "rounds: NULL buffer");
+    return cluster_rounds(ws, as_stream(stream), rounds);
+}
+
 int rogtk_cluster_release(const void* ws) {
     if (ws) cluster_release(ws);
     return ROGTK_OK;

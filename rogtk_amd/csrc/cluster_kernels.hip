@@ -31,7 +31,7 @@
 //           reads (1.08M distinct) converges in 3 productive rounds, at 80M reads
 //           (6.9M distinct, 41% of 4^12) in 2.
 //   roots   ballot root flags into an index-space bitmap; scan = dense cluster ids
-//   label   labelcode[D[i]] (L <= 13) or f[i] := dense id (index space)
+//   label   labelcode[code] (L <= 13) or ilab[i] := dense id (index space)
 //   assign  cluster_id[row] = label(code[row])
 #include <algorithm>
 #include <map>
@@ -60,9 +60,6 @@ __device__ __forceinline__ uint32_t rt_rank(const uint4 e, uint32_t code) {
     return e.z + (uint32_t)__popcll(rt_word(e) & ((1ull << (code & 63)) - 1ull));
 }
 
-__device__ __forceinline__ int64_t live_distinct(const unsigned long long* stats, int64_t max_distinct) {
-    return min<int64_t>((int64_t)stats[S_NDISTINCT], max_distinct);
-}
 
 // presence bytes -> bitmap words; one lane loads 16 contiguous bytes, 4 lanes make a word.
 __global__ __launch_bounds__(kBlock) void k_bitmap_wide(uint8_t* __restrict__ pres, int64_t words,
@@ -155,12 +152,14 @@ __global__ __launch_bounds__(kBlock) void k_scan_words(const uint64_t* __restric
     if (threadIdx.x == 0) blksum[blockIdx.x] = total;
 }
 
-// Single-block exclusive scan of block sums -> blkoff[0..nblocks], total -> stats.
+// Single-block exclusive scan of block sums -> blkoff[0..nblocks], total -> stats
+// (zero_stats: the stats block and round flags are cleared first).
 __global__ __launch_bounds__(kBlock) void k_scan_blocks(const uint32_t* __restrict__ blksum,
                                                         int64_t nblocks, uint32_t* __restrict__ blkoff,
                                                         unsigned long long* __restrict__ stats,
-                                                        int slot, int copy_slot) {
+                                                        int slot, int copy_slot, int zero_stats) {
     __shared__ uint32_t s_wave[kBlock / 64];
+    if (zero_stats && threadIdx.x < kStatsBytes / 8) stats[threadIdx.x] = 0;  // stats + round flags
     uint32_t carry = 0;
     for (int64_t base = 0; base < nblocks; base += kBlock) {
         const int64_t b = base + threadIdx.x;
@@ -177,11 +176,15 @@ __global__ __launch_bounds__(kBlock) void k_scan_blocks(const uint32_t* __restri
     }
 }
 
+// RT[w] = {word, rank of its first code}; also zeroes the index-space live bits
+// (zero_words <= words) for local_cc.
 __global__ __launch_bounds__(kBlock) void k_rt(const uint64_t* __restrict__ G, int64_t words,
                                                const uint32_t* __restrict__ wpref,
-                                               const uint32_t* __restrict__ blkoff, uint4* __restrict__ RT) {
+                                               const uint32_t* __restrict__ blkoff, uint4* __restrict__ RT,
+                                               uint64_t* __restrict__ zero, int64_t zero_words) {
     const int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (w >= words) return;
+    if (w < zero_words) zero[w] = 0;
     const uint64_t m = G[w];
     RT[w] = make_uint4((uint32_t)m, (uint32_t)(m >> 32), blkoff[w / kScanWords] + wpref[w], 0u);
 }
@@ -190,7 +193,8 @@ __global__ __launch_bounds__(kBlock) void k_rt(const uint64_t* __restrict__ G, i
 // 64 lanes of a wave share one RT entry (one load), present lanes store coalesced.
 __global__ __launch_bounds__(kBlock) void k_build_d(const uint4* __restrict__ RT, uint64_t nbits,
                                                     uint32_t* __restrict__ D, uint32_t* __restrict__ f,
-                                                    uint32_t* __restrict__ labelcode, int64_t max_distinct,
+                                                    uint32_t* __restrict__ labelcode, uint32_t* __restrict__ ilab,
+                                                    int64_t max_distinct,
                                                     unsigned long long* __restrict__ stats) {
     if ((int64_t)stats[S_NDISTINCT] > max_distinct && blockIdx.x == 0 && threadIdx.x == 0) stats[S_OVERFLOW] = 1;
     for (uint64_t c = (uint64_t)blockIdx.x * kBlock + threadIdx.x; c < nbits; c += (uint64_t)gridDim.x * kBlock) {
@@ -198,9 +202,10 @@ __global__ __launch_bounds__(kBlock) void k_build_d(const uint4* __restrict__ RT
         if (!((rt_word(e) >> (c & 63)) & 1ull)) continue;
         const uint32_t i = rt_rank(e, (uint32_t)c);
         if ((int64_t)i >= max_distinct) continue;
-        D[i] = (uint32_t)c;
         f[i] = i;
+        D[i] = (uint32_t)c;
         if (labelcode) labelcode[c] = i;  // exact mode: label = rank
+        else ilab[i] = i;
     }
 }
 
@@ -213,10 +218,18 @@ __device__ __forceinline__ uint64_t multi_of4(uint64_t a, uint64_t b, uint64_t c
 // edge at positions 0..6 stays inside it, so the whole union-find for those
 // positions runs in LDS. Positions 0..2 live inside one 64-bit word: their
 // components come from a bit-parallel BFS on the word mask (no atomics); positions
-// 3..6 unite whole word components that intersect (CAS union-find). Output: D (sorted distinct
-// codes), f (global index of the local root: stars), and UR[w] = the shared root
-// of word w when all its codes are in one local component (the common case when
-// the code space is dense).
+// 3..6 unite whole word components that intersect (CAS union-find). Outputs are per
+// word (UR[w] = the shared local root of word w when all its codes are in one local
+// component, the common case once the code space is dense), the live vertices as bits
+// of index space (lroot, zeroed before: the local roots and the codes of the other
+// words), and f over index space for the live vertices.
+#ifdef ROGTK_LCC_TIMING  // tools/local_cc_exp: per-phase clocks of k_local_cc
+__device__ unsigned long long g_lcc_clk[8];
+#define LCC_T(k) do { __syncthreads(); if (threadIdx.x == 0) { const unsigned long long now_ = wall_clock64(); \
+    atomicAdd(&g_lcc_clk[k], now_ - t_last_); t_last_ = now_; } } while (0)
+#else
+#define LCC_T(k) do { } while (0)
+#endif
 constexpr int kLocalWords = 256;
 constexpr int kLocalCodes = kLocalWords * 64;  // 16384
 constexpr int kLocalPos = 7;
@@ -240,6 +253,10 @@ __device__ __forceinline__ uint32_t lfind(uint32_t* lf, uint32_t x) {
 }
 
 __device__ __forceinline__ void lunite(uint32_t* lf, uint32_t a, uint32_t b) {
+#ifdef ROGTK_LCC_NOUNITE
+    if (a == b + 100000u) lf[0] = 0;  // keeps the call sites alive
+    return;
+#endif
     for (;;) {
         a = lfind(lf, a);
         b = lfind(lf, b);
@@ -289,15 +306,68 @@ __device__ __forceinline__ uint64_t word_component(uint64_t m, uint64_t seed_bit
     return word_component_any(m, seed_bit, dims);
 }
 
+// In-word components of one word, as phase 1 of k_local_cc leaves them: up to
+// kWordComps components of two or more codes (masks); every other code is a
+// singleton unless the word overflowed the list (then components come from BFS).
+constexpr int kWordComps = 4;
+struct WordComps {
+    uint64_t m;
+    uint64_t c[kWordComps];
+    int n;       // listed components; -1: overflow
+    bool one;    // the whole word is one component
+};
+
+__device__ __forceinline__ uint64_t comp_of(const WordComps& w, uint64_t seed_bit, int dims) {
+    if (w.one) return w.m;
+    if (w.n < 0) return word_component(w.m, seed_bit, dims);
+    uint64_t r = seed_bit;
+#pragma unroll
+    for (int k = 0; k < kWordComps; ++k)
+        if (k < w.n && (w.c[k] & seed_bit)) r = w.c[k];
+    return r;
+}
+
+// the union of the components of w that contain a bit of seed
+__device__ __forceinline__ uint64_t comps_any(const WordComps& w, uint64_t seed, int dims) {
+    if (!seed) return 0;
+    if (w.one) return w.m;
+    if (w.n < 0) return word_component_any(w.m, seed, dims);
+    uint64_t covered = 0, r = 0;
+#pragma unroll
+    for (int k = 0; k < kWordComps; ++k)
+        if (k < w.n) {
+            covered |= w.c[k];
+            if (w.c[k] & seed) r |= w.c[k];
+        }
+    return r | (seed & ~covered);
+}
+
+// Sparse code space: under 1/8 of the codes present. Then local_cc also writes D
+// (index -> code) and labels are assigned per index; dense spaces label per code.
+__device__ __forceinline__ bool is_sparse(const unsigned long long* stats, int64_t words) {
+    return stats[S_NDISTINCT] * 8 < (unsigned long long)words * 64;
+}
+
 __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ RT, int64_t words, int L,
-                                                     uint32_t* __restrict__ D, uint32_t* __restrict__ f,
-                                                     uint32_t* __restrict__ UR, int64_t max_distinct,
+                                                     uint32_t* __restrict__ f, uint32_t* __restrict__ D,
+                                                     uint32_t* __restrict__ UR, uint64_t* __restrict__ lroot,
+                                                     int64_t rwords,
+                                                     int64_t max_distinct,
                                                      unsigned long long* __restrict__ stats) {
     __shared__ uint64_t wb[kLocalWords];
+    __shared__ uint64_t wcm[kWordComps][kLocalWords];  // listed component masks per word
     __shared__ uint32_t lpre[kLocalWords];
-    __shared__ uint32_t lf[kLocalCodes];
+    __shared__ uint32_t lf[kLocalCodes];  // by local code (word * 64 + bit); valid at component roots
+    __shared__ int8_t wcn[kLocalWords];    // listed components (-1 overflow)
+    __shared__ uint8_t wone[kLocalWords];  // the word's codes form one in-word component
+    __shared__ uint64_t lrb[kLocalWords + 2];  // local-root bits of the block's index range
     __shared__ uint32_t s_wave[kBlock / 64];
     const int t = threadIdx.x;
+    lrb[t] = 0;
+    if (t < 2) lrb[kLocalWords + t] = 0;
+#ifdef ROGTK_LCC_TIMING
+    unsigned long long t_last_ = wall_clock64();
+#endif
     const int64_t base = (int64_t)blockIdx.x * kLocalWords;
     const int nw = (int)min<int64_t>(kLocalWords, words - base);
     const int lpos = L < kLocalPos ? L : kLocalPos;
@@ -310,56 +380,87 @@ __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ R
     const uint32_t gbase = RT[base].z;
     const int indims = lpos < 3 ? lpos : 3;  // positions inside one 64-code word
     // 1. components inside each word (positions 0..2): bit-parallel BFS on the word's
-    //    mask; every code's parent is its component's first code (stars, no atomics)
+    //    mask, once; each component is represented by its first code (lf[root] = root)
+    WordComps mine;
+    mine.m = m;
     {
         uint64_t rem = m;
+        int ncomp = 0, nl = 0;
+#pragma unroll
+        for (int k = 0; k < kWordComps; ++k) mine.c[k] = 0;
         while (rem) {
             const int b0 = __ffsll((long long)rem) - 1;
-            const uint64_t comp = word_component(m, 1ull << b0, indims);
-            rem &= ~comp;
-            const uint32_t root = ex + (uint32_t)__popcll(m & ((1ull << b0) - 1ull));
-            uint64_t cc = comp;
-            while (cc) {
-                const int b = __ffsll((long long)cc) - 1;
-                cc &= cc - 1;
-                lf[ex + (uint32_t)__popcll(m & ((1ull << b) - 1ull))] = root;
+            const uint64_t c = word_component(m, 1ull << b0, indims);
+            rem &= ~c;
+            lf[t * 64 + b0] = (uint32_t)(t * 64 + b0);
+            ++ncomp;
+            if (c & (c - 1)) {  // two or more codes
+                if (nl < kWordComps) {
+#pragma unroll
+                    for (int k = 0; k < kWordComps; ++k)
+                        if (k == nl) mine.c[k] = c;
+                }
+                ++nl;
             }
         }
+        mine.n = nl > kWordComps ? -1 : nl;
+        mine.one = ncomp == 1;
+#pragma unroll
+        for (int k = 0; k < kWordComps; ++k) wcm[k][t] = mine.c[k];
+        wcn[t] = (int8_t)mine.n;
+        wone[t] = mine.one;
     }
     __syncthreads();
+    LCC_T(0);
     // 2. positions 3..lpos-1 join words 4^(p-3) apart: codes at the same bit of the 4
     //    words of a group differ only at p, so two word components that share a bit
-    //    are adjacent; unite every intersecting pair of components (root = first code)
+    //    are adjacent; unite every intersecting pair of components
     {
         const int per = nw >> 2;
         if (per > 0 && t < (lpos - 3) * per) {
             const int p = 3 + t / per, g = t % per, s2 = 2 * p - 6, stride = 1 << s2;
             const int w0 = ((g >> s2) << (s2 + 2)) | (g & (stride - 1));
-            uint64_t mv[4];
-            uint32_t pv[4];
+            WordComps wv[4];
+            bool all_one = true;
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
-                mv[v] = wb[w0 + v * stride];
-                pv[v] = lpre[w0 + v * stride];
+                const int w = w0 + v * stride;
+                wv[v].m = wb[w];
+                wv[v].one = wone[w];
+                wv[v].n = wcn[w];
+#pragma unroll
+                for (int k = 0; k < kWordComps; ++k) wv[v].c[k] = wcm[k][w];
+                all_one &= wv[v].one || wv[v].m == 0;
             }
-            for (int a = 0; a < 3; ++a) {
-                uint64_t rem = mv[a];
-                // only components that meet a later word matter
-                uint64_t later = 0;
-                for (int b = a + 1; b < 4; ++b) later |= mv[b];
-                rem &= word_component_any(mv[a], rem & later, indims);
-                while (rem) {
-                    const int ba = __ffsll((long long)rem) - 1;
-                    const uint64_t ca = word_component(mv[a], 1ull << ba, indims);
-                    rem &= ~ca;
-                    const uint32_t ra = pv[a] + (uint32_t)__popcll(mv[a] & ((1ull << ba) - 1ull));
-                    for (int b = a + 1; b < 4; ++b) {
-                        uint64_t x = ca & mv[b];
-                        while (x) {
-                            const uint64_t cb = word_component(mv[b], x & (~x + 1ull), indims);
-                            x &= ~cb;
-                            const int bb = __ffsll((long long)cb) - 1;
-                            lunite(lf, ra, pv[b] + (uint32_t)__popcll(mv[b] & ((1ull << bb) - 1ull)));
+            if (all_one) {
+#pragma unroll
+                for (int x = 0; x < 3; ++x)
+#pragma unroll
+                    for (int y = x + 1; y < 4; ++y)
+                        if (wv[x].m & wv[y].m)
+                            lunite(lf, (uint32_t)((w0 + x * stride) * 64 + __ffsll((long long)wv[x].m) - 1),
+                                   (uint32_t)((w0 + y * stride) * 64 + __ffsll((long long)wv[y].m) - 1));
+            } else {
+#pragma unroll
+                for (int x = 0; x < 3; ++x) {
+                    uint64_t later = 0;
+#pragma unroll
+                    for (int y = x + 1; y < 4; ++y) later |= wv[y].m;
+                    // only components that meet a later word matter
+                    uint64_t rem = comps_any(wv[x], wv[x].m & later, indims);
+                    while (rem) {
+                        const int ba = __ffsll((long long)rem) - 1;
+                        const uint64_t ca = comp_of(wv[x], 1ull << ba, indims);
+                        rem &= ~ca;
+                        const uint32_t ra = (uint32_t)((w0 + x * stride) * 64 + ba);
+#pragma unroll
+                        for (int y = x + 1; y < 4; ++y) {
+                            uint64_t z = ca & wv[y].m;
+                            while (z) {
+                                const uint64_t cb = comp_of(wv[y], z & (~z + 1ull), indims);
+                                z &= ~cb;
+                                lunite(lf, ra, (uint32_t)((w0 + y * stride) * 64 + __ffsll((long long)cb) - 1));
+                            }
                         }
                     }
                 }
@@ -367,28 +468,104 @@ __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ R
         }
     }
     __syncthreads();
-    // outputs
-    if (t == 0 && (int64_t)gbase + nloc > max_distinct) stats[S_OVERFLOW] = 1;
-    if (t < nw) {
-        uint64_t mm = m;
-        uint32_t i = ex, first = kNone;
-        bool uniform = true;
-        while (mm) {
-            const int b = __ffsll((long long)mm) - 1;
-            mm &= mm - 1;
-            uint32_t root = i;
-            for (uint32_t q = lf[root]; q != root; q = lf[root]) root = q;  // read-only after the barrier
-            if (first == kNone) first = root;
-            uniform &= root == first;
-            const int64_t gi = (int64_t)gbase + i;
-            if (gi < max_distinct) {
-                f[gi] = gbase + root;
-                D[gi] = (uint32_t)((base + t) * 64 + b);
-            }
-            ++i;
+    LCC_T(1);
+    // 3a. compress: every component root of word t points at its final root (a
+    //     concurrent reader sees the old parent or the final root: both ancestors)
+    {
+        uint64_t rem = m;
+        while (rem) {
+            const int b0 = __ffsll((long long)rem) - 1;
+            rem &= ~comp_of(mine, 1ull << b0, indims);
+            const uint32_t c0 = (uint32_t)(t * 64 + b0);
+            uint32_t root = c0;
+            for (uint32_t q = lds_ld(lf + root); q != root; q = lds_ld(lf + root)) root = q;
+            if (root != c0) __hip_atomic_store(lf + c0, root, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        UR[base + t] = (m && uniform) ? gbase + first : kNone;
     }
+    __syncthreads();
+    LCC_T(2);
+    // 3b. outputs of word t, per in-word component (lf[c0] is now the final root):
+    //     UR = the word's shared local root (global index) or kNone, the live bits,
+    //     f[local root] = itself, f[i] = its local root for the codes of words without
+    //     a shared root (the only ones the rounds read by code), and in a sparse code
+    //     space (kSparse) D[i] = code for every code, so that labels run over indices
+    if (t == 0 && (int64_t)gbase + nloc > max_distinct) stats[S_OVERFLOW] = 1;
+    const bool sparse = is_sparse(stats, words);
+    if (t < nw) {
+        uint32_t first = kNone;
+        bool uniform = true;
+        uint64_t rem = m;
+        while (rem) {
+            const int b0 = __ffsll((long long)rem) - 1;
+            rem &= ~comp_of(mine, 1ull << b0, indims);
+            const uint32_t root = lf[t * 64 + b0];
+            const uint32_t rw = root >> 6;
+            const uint32_t rr = gbase + lpre[rw] + (uint32_t)__popcll(wb[rw] & ((1ull << (root & 63)) - 1ull));
+            if (first == kNone) first = rr;
+            uniform &= rr == first;
+            if (root == (uint32_t)(t * 64 + b0)) {
+                if ((int64_t)rr < max_distinct) f[rr] = rr;
+                const uint32_t k = (gbase & 63u) + (rr - gbase);  // bit of the block's staging
+                atomicOr((unsigned long long*)&lrb[k >> 6], 1ull << (k & 63));
+            }
+        }
+        if (m && !uniform) {
+            // codes of a word whose components keep different roots: f[i] = root index,
+            // and all of them are live (the rounds read them by code, so jumps keep them
+            // pointing at their root)
+            {
+                const uint32_t k0 = (gbase & 63u) + ex, cnt = (uint32_t)__popcll(m);
+                const uint32_t off = k0 & 63u;
+                const uint64_t range = cnt == 64 ? ~0ull : ((1ull << cnt) - 1ull);
+                atomicOr((unsigned long long*)&lrb[k0 >> 6], range << off);
+                if (off + cnt > 64) atomicOr((unsigned long long*)&lrb[(k0 >> 6) + 1], range >> (64 - off));
+            }
+            uint64_t r2 = m;
+            while (r2) {
+                const int b0 = __ffsll((long long)r2) - 1;
+                uint64_t cc = comp_of(mine, 1ull << b0, indims);
+                r2 &= ~cc;
+                const uint32_t root = lf[t * 64 + b0];
+                const uint32_t rw = root >> 6;
+                const uint32_t rr = gbase + lpre[rw] + (uint32_t)__popcll(wb[rw] & ((1ull << (root & 63)) - 1ull));
+                while (cc) {
+                    const int b = __ffsll((long long)cc) - 1;
+                    cc &= cc - 1;
+                    const int64_t gi = (int64_t)gbase + ex + (uint32_t)__popcll(m & ((1ull << b) - 1ull));
+                    if (gi < max_distinct) f[gi] = rr;
+                }
+            }
+        }
+        UR[base + t] = (m && uniform) ? first : kNone;
+        if (sparse) {
+            uint64_t mm = m;
+            uint32_t i = gbase + ex;
+            while (mm) {
+                const int b = __ffsll((long long)mm) - 1;
+                mm &= mm - 1;
+                if ((int64_t)i < max_distinct) D[i] = (uint32_t)((base + t) * 64 + b);
+                ++i;
+            }
+        }
+    }
+    __syncthreads();
+    // index-space live words: the block owns the interior words of its range; the
+    // first and last are shared with the neighbouring blocks (atomic OR, zeroed before)
+    {
+        const uint32_t nlw = nloc ? ((gbase & 63u) + nloc + 63u) / 64u : 0u;
+        const int64_t w0 = (int64_t)(gbase >> 6);
+        for (uint32_t k = t; k < nlw; k += kBlock) {
+            const int64_t w = w0 + k;
+            if (w >= rwords) break;
+            const uint64_t v = lrb[k];
+            if (k == 0 || k == nlw - 1) {
+                if (v) atomicOr((unsigned long long*)(lroot + w), (unsigned long long)v);
+            } else {
+                lroot[w] = v;
+            }
+        }
+    }
+    LCC_T(3);
 }
 
 // --------------------------------------------------------------- global CC
@@ -510,14 +687,26 @@ __global__ __launch_bounds__(kBlock) void k_hook_g(const uint4* __restrict__ RT,
     }
 }
 
-// Stars again: every vertex chases its parent to the root. Only f[i] is written by
-// lane i, and only with an ancestor, so concurrent chasers always see ancestors.
-__global__ __launch_bounds__(kBlock) void k_jump(uint32_t* f, int64_t max_distinct,
+__device__ __forceinline__ int64_t live_distinct(const unsigned long long* stats, int64_t max_distinct) {
+    return min<int64_t>((int64_t)stats[S_NDISTINCT], max_distinct);
+}
+
+// Stars again, over the live vertices only (bits of lroot: the local roots and the
+// codes of words without a shared root); every other vertex keeps pointing at its
+// local root. Only f[i] is written by lane i, and only with an ancestor, so
+// concurrent chasers always see ancestors.
+__global__ __launch_bounds__(kBlock) void k_jump(uint32_t* f, const uint64_t* __restrict__ lroot,
+                                                 int64_t max_distinct,
                                                  const unsigned long long* __restrict__ stats,
                                                  const unsigned int* __restrict__ flags, int round) {
     if (flags[round] == 0) return;
     const int64_t nd = live_distinct(stats, max_distinct);
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nd; i += (int64_t)gridDim.x * kBlock) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
+    for (int64_t w = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; w * 64 < nd; w += nwaves) {
+        const uint64_t lr = lroot[w];
+        const int64_t i = w * 64 + lane;
+        if (!((lr >> lane) & 1ull) || i >= nd) continue;
         uint32_t r = f[i];
         if (r == (uint32_t)i) continue;
         for (uint32_t p = f[r]; p != r; p = f[r]) r = p;
@@ -525,17 +714,19 @@ __global__ __launch_bounds__(kBlock) void k_jump(uint32_t* f, int64_t max_distin
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_roots(const uint32_t* __restrict__ f, int64_t max_distinct,
-                                                  uint64_t* __restrict__ rbits,
+// Global roots (live vertices i with f[i] == i: only local roots can be) -> rbits over
+// index space; their dense order is the label order.
+__global__ __launch_bounds__(kBlock) void k_roots(const uint32_t* __restrict__ f, const uint64_t* __restrict__ lroot,
+                                                  int64_t max_distinct, uint64_t* __restrict__ rbits,
                                                   const unsigned long long* __restrict__ stats) {
     const int64_t nd = live_distinct(stats, max_distinct);
     const int lane = threadIdx.x & 63;
-    const int64_t wave_g = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
     const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
-    for (int64_t base = wave_g * 64; base < nd; base += nwaves * 64) {
-        const int64_t i = base + lane;
-        const uint64_t m = __ballot(i < nd && f[i] == (uint32_t)i);
-        if (lane == 0) rbits[base >> 6] = m;
+    for (int64_t w = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; w * 64 < nd; w += nwaves) {
+        const int64_t i = w * 64 + lane;
+        const bool root = i < nd && ((lroot[w] >> lane) & 1ull) && f[i] == (uint32_t)i;
+        const uint64_t m = __ballot(root);
+        if (lane == 0) rbits[w] = m;
     }
 }
 
@@ -546,22 +737,62 @@ __device__ __forceinline__ uint32_t root_label(uint32_t r, const uint64_t* __res
     return rblkoff[w / kScanWords] + rpref[w] + (uint32_t)__popcll(rbits[w] & ((1ull << (r & 63)) - 1ull));
 }
 
-// Dense labels (max_distance 1): labelcode[D[i]] (L <= 13) or f[i] := label (index space).
-__global__ __launch_bounds__(kBlock) void k_label(uint32_t* __restrict__ f, const uint32_t* __restrict__ D,
-                                                  const uint64_t* __restrict__ rbits,
-                                                  const uint32_t* __restrict__ rpref,
-                                                  const uint32_t* __restrict__ rblkoff,
-                                                  uint32_t* __restrict__ labelcode, int64_t max_distinct,
-                                                  const unsigned long long* __restrict__ stats) {
-    const int64_t nd = live_distinct(stats, max_distinct);
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nd; i += (int64_t)gridDim.x * kBlock) {
-        const uint32_t lab = root_label(f[i], rbits, rpref, rblkoff);
-        if (labelcode) labelcode[D[i]] = lab;
-        f[i] = lab;  // in place: lane i only ever reads its own f[i]
+// Label of every word with a shared local root (kNone for the others), so that the
+// per-code pass below needs no dependent loads for them.
+__global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restrict__ f,
+                                                       const uint32_t* __restrict__ UR, int64_t words,
+                                                       const uint64_t* __restrict__ rbits,
+                                                       const uint32_t* __restrict__ rpref,
+                                                       const uint32_t* __restrict__ rblkoff,
+                                                       uint32_t* __restrict__ wlab) {
+    for (int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x; w < words; w += (int64_t)gridDim.x * kBlock) {
+        const uint32_t ur = UR[w];
+        wlab[w] = ur != kNone ? root_label(f[ur], rbits, rpref, rblkoff) : kNone;
     }
 }
 
-// MODE 0: labelcode[code]; MODE 1: f[rank(code)] (labels by index).
+// Dense labels (max_distance 1): words with a shared root take wlab, the other codes
+// are live (their f is their root). labelcode[code] (L <= 13) or ilab[index] (index
+// space). Dense code spaces run one lane per code (a wave per word: stores contiguous
+// per word); sparse ones one lane per index (D holds the codes; no idle lanes).
+__device__ __forceinline__ void put_label(uint64_t c, uint32_t i, uint32_t lab, uint32_t* __restrict__ labelcode,
+                                          uint32_t* __restrict__ ilab) {
+    if (labelcode) labelcode[c] = lab;
+    else ilab[i] = lab;
+}
+
+__global__ __launch_bounds__(kBlock) void k_label(const uint32_t* __restrict__ f, const uint4* __restrict__ RT,
+                                                  const uint32_t* __restrict__ wlab, uint64_t nbits,
+                                                  const uint64_t* __restrict__ rbits,
+                                                  const uint32_t* __restrict__ rpref,
+                                                  const uint32_t* __restrict__ rblkoff,
+                                                  uint32_t* __restrict__ labelcode, uint32_t* __restrict__ ilab,
+                                                  const uint32_t* __restrict__ D, int64_t max_distinct,
+                                                  const unsigned long long* __restrict__ stats) {
+    const uint64_t lanes = (uint64_t)gridDim.x * kBlock;
+    const uint64_t lane0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (is_sparse(stats, (int64_t)((nbits + 63) / 64))) {
+        const int64_t nd = live_distinct(stats, max_distinct);
+        for (int64_t i = (int64_t)lane0; i < nd; i += (int64_t)lanes) {
+            const uint32_t c = D[i];
+            const uint32_t wl = wlab[c >> 6];
+            const uint32_t lab = wl != kNone ? wl : root_label(f[i], rbits, rpref, rblkoff);
+            put_label(c, (uint32_t)i, lab, labelcode, ilab);
+        }
+        return;
+    }
+    for (uint64_t c = lane0; c < nbits; c += lanes) {
+        const uint4 e = RT[c >> 6];
+        const uint32_t wl = wlab[c >> 6];
+        const uint64_t m = rt_word(e);
+        if (!((m >> (c & 63)) & 1ull)) continue;
+        const uint32_t i = e.z + (uint32_t)__popcll(m & ((1ull << (c & 63)) - 1ull));
+        if ((int64_t)i >= max_distinct) continue;
+        put_label(c, i, wl != kNone ? wl : root_label(f[i], rbits, rpref, rblkoff), labelcode, ilab);
+    }
+}
+
+// MODE 0: labelcode[code]; MODE 1: flab[rank(code)] (labels by index, ilab).
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ codes,
                                                    const uint64_t* __restrict__ regbits, int64_t n,
@@ -608,8 +839,8 @@ struct WsPtrs {
     uint64_t* G;
     uint4* RT;
     uint32_t *wpref, *blksum, *blkoff, *D, *f, *UR;
-    uint64_t* rbits;
-    uint32_t *rpref, *rblksum, *rblkoff, *labelcode;
+    uint64_t *rbits, *lroot;
+    uint32_t *rpref, *rblksum, *rblkoff, *labelcode, *ilab;
 };
 
 inline WsPtrs ws_ptrs(const ClusterLayout& cl, uint8_t* ws) {
@@ -626,10 +857,12 @@ inline WsPtrs ws_ptrs(const ClusterLayout& cl, uint8_t* ws) {
     p.f = (uint32_t*)(ws + cl.off_f);
     p.UR = (uint32_t*)(ws + cl.off_ur);
     p.rbits = (uint64_t*)(ws + cl.off_rbits);
+    p.lroot = (uint64_t*)(ws + cl.off_lroot);
     p.rpref = (uint32_t*)(ws + cl.off_rpref);
     p.rblksum = (uint32_t*)(ws + cl.off_rblksum);
     p.rblkoff = (uint32_t*)(ws + cl.off_rblkoff);
     p.labelcode = cl.label_by_code ? (uint32_t*)(ws + cl.off_labelcode) : nullptr;
+    p.ilab = cl.label_by_code ? nullptr : (uint32_t*)(ws + cl.off_ilab);
     return p;
 }
 
@@ -669,10 +902,12 @@ int cluster_layout(int L, int64_t max_distinct, ClusterLayout* o) {
     c.off_f = take(max_distinct * 4);
     c.off_ur = take(c.words * 4);
     c.off_rbits = take(c.rwords * 8);
+    c.off_lroot = take(c.rwords * 8);
     c.off_rpref = take(c.rwords * 4);
     c.off_rblksum = take(c.rblocks * 4);
     c.off_rblkoff = take((c.rblocks + 1) * 4);
     c.off_labelcode = c.label_by_code ? take((int64_t)c.nbits * 4) : off;
+    c.off_ilab = c.label_by_code ? off : take(max_distinct * 4);
     c.total = off;
     *o = c;
     return ROGTK_OK;
@@ -750,6 +985,7 @@ struct ResolveState {
     unsigned int* hflags = nullptr;  // pinned, kMaxRounds entries
     int launched = 0;
     bool pending = false;
+    int rounds = 0;  // hook rounds the last resolve needed (the converged round included)
     ClusterLayout cl{};
 };
 std::mutex g_rs_mu;
@@ -761,36 +997,41 @@ int enqueue_rounds(const ClusterLayout& cl, const WsPtrs& p, int from, int to, h
     for (int k = from; k < to; ++k) {
         hipLaunchKernelGGL(k_hook_g, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words, cl.L,
                            kLocalPos, p.f, p.flags, k);
-        hipLaunchKernelGGL(k_jump, dim3(pg), dim3(kBlock), 0, s, p.f, cl.max_distinct, p.stats, p.flags, k);
+        hipLaunchKernelGGL(k_jump, dim3(pg), dim3(kBlock), 0, s, p.f, p.lroot, cl.max_distinct, p.stats, p.flags, k);
     }
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
 }
 
 int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s) {
-    const int pg = grid_for(cl.max_distinct, kPersistentGrid);
     {
         ProfScope prof(K_FLATTEN, s);
-        hipLaunchKernelGGL(k_roots, dim3(pg), dim3(kBlock), 0, s, p.f, cl.max_distinct, p.rbits, p.stats);
+        hipLaunchKernelGGL(k_roots, dim3(grid_for(cl.max_distinct, kPersistentGrid)), dim3(kBlock), 0, s, p.f,
+                           p.lroot, cl.max_distinct, p.rbits, p.stats);
         hipLaunchKernelGGL(k_scan_words, dim3((unsigned)cl.rblocks), dim3(kBlock), 0, s, p.rbits, 1,
                            cl.rwords, p.stats + S_NDISTINCT, (uint64_t*)nullptr, p.rpref, p.rblksum);
         hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, p.rblksum, cl.rblocks, p.rblkoff,
-                           p.stats, (int)S_NCLUSTERS, -1);
+                           p.stats, (int)S_NCLUSTERS, -1, 0);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     {
         ProfScope prof(K_LABEL, s);
-        hipLaunchKernelGGL(k_label, dim3(pg), dim3(kBlock), 0, s, p.f, p.D, p.rbits, p.rpref, p.rblkoff,
-                           p.labelcode, cl.max_distinct, p.stats);
+        const int lg = grid_for((int64_t)std::min<uint64_t>(cl.nbits, 1ull << 30), 16384);
+        // wpref (consumed into RT by k_rt) holds the word labels
+        hipLaunchKernelGGL(k_word_label, dim3(grid_for(cl.words, kPersistentGrid)), dim3(kBlock), 0, s, p.f, p.UR,
+                           cl.words, p.rbits, p.rpref, p.rblkoff, p.wpref);
+        hipLaunchKernelGGL(k_label, dim3(lg), dim3(kBlock), 0, s, p.f, p.RT, p.wpref, cl.nbits, p.rbits, p.rpref,
+                           p.rblkoff, p.labelcode, p.ilab, p.D, cl.max_distinct, p.stats);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     return ROGTK_OK;
 }
 
-bool any_zero(const unsigned int* f, int from, int to) {
+// index of the first round that found nothing to hook, or -1
+int first_zero(const unsigned int* f, int from, int to) {
     for (int k = from; k < to; ++k)
-        if (f[k] == 0) return true;
-    return false;
+        if (f[k] == 0) return k;
+    return -1;
 }
 
 }  // namespace
@@ -801,34 +1042,34 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
     std::lock_guard<std::mutex> lk(g_rs_mu);
     ResolveState& st = g_rs[ws];
     st.pending = false;
+    st.rounds = 0;
     st.cl = cl;
-    ROGTK_HIP_CHECK(hipMemsetAsync(p.stats, 0, kStatsBytes, s));
     {
         ProfScope prof(K_SCAN, s);
         hipLaunchKernelGGL(k_scan_words, dim3((unsigned)cl.blocks), dim3(kBlock), 0, s, bitmaps,
                            n_bitmaps, cl.words, (const unsigned long long*)nullptr, p.G, p.wpref,
                            p.blksum);
         hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, p.blksum, cl.blocks, p.blkoff,
-                           p.stats, (int)S_NDISTINCT, max_distance == 0 ? (int)S_NCLUSTERS : -1);
+                           p.stats, (int)S_NDISTINCT, max_distance == 0 ? (int)S_NCLUSTERS : -1, 1);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     {
         ProfScope prof(K_COMPACT, s);
         hipLaunchKernelGGL(k_rt, dim3(grid_for(cl.words)), dim3(kBlock), 0, s, p.G, cl.words, p.wpref,
-                           p.blkoff, p.RT);
+                           p.blkoff, p.RT, p.lroot, max_distance == 0 ? 0 : cl.rwords);
         if (max_distance == 0) {
             const int cgrid = grid_for((int64_t)std::min<uint64_t>(cl.nbits, 1ull << 30), 16384);
-            hipLaunchKernelGGL(k_build_d, dim3(cgrid), dim3(kBlock), 0, s, p.RT, cl.nbits, p.D, p.f, p.labelcode,
+            hipLaunchKernelGGL(k_build_d, dim3(cgrid), dim3(kBlock), 0, s, p.RT, cl.nbits, p.D, p.f, p.labelcode, p.ilab,
                                cl.max_distinct, p.stats);
             ROGTK_HIP_CHECK(hipGetLastError());
-            return ROGTK_OK;  // labels = ranks (labelcode / f[i] == i)
+            return ROGTK_OK;  // labels = ranks (labelcode / ilab)
         }
     }
     {
         ProfScope prof(K_UNION, s);
         const int64_t lblocks = (cl.words + kLocalWords - 1) / kLocalWords;
-        hipLaunchKernelGGL(k_local_cc, dim3((unsigned)lblocks), dim3(kBlock), 0, s, p.RT, cl.words, cl.L, p.D,
-                           p.f, p.UR, cl.max_distinct, p.stats);
+        hipLaunchKernelGGL(k_local_cc, dim3((unsigned)lblocks), dim3(kBlock), 0, s, p.RT, cl.words, cl.L,
+                           p.f, p.D, p.UR, p.lroot, cl.rwords, cl.max_distinct, p.stats);
         ROGTK_HIP_CHECK(hipGetLastError());
         if (cl.L > kLocalPos) {
             if (int rc = enqueue_rounds(cl, p, 0, kSpecRounds, s)) return rc;
@@ -853,8 +1094,9 @@ int cluster_finish(const void* ws, hipStream_t s) {
     if (it == g_rs.end() || !it->second.pending) return ROGTK_OK;
     ResolveState& st = it->second;
     ROGTK_HIP_CHECK(hipEventSynchronize(st.ev));
-    if (any_zero(st.hflags, 0, st.launched)) {
+    if (int z = first_zero(st.hflags, 0, st.launched); z >= 0) {
         st.pending = false;
+        st.rounds = z + 1;
         return ROGTK_OK;
     }
     // the speculative rounds were not enough: continue synchronously, then relabel
@@ -869,12 +1111,22 @@ int cluster_finish(const void* ws, hipStream_t s) {
         ROGTK_HIP_CHECK(hipMemcpyAsync(st.hflags + st.launched, p.flags + st.launched,
                                        (to - st.launched) * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
         ROGTK_HIP_CHECK(hipStreamSynchronize(s));
-        converged = any_zero(st.hflags, st.launched, to);
+        const int z = first_zero(st.hflags, st.launched, to);
+        converged = z >= 0;
+        if (converged) st.rounds = z + 1;
         st.launched = to;
     }
     st.pending = false;
     ROGTK_REQUIRE(converged, ROGTK_E_HIP, "cluster: union rounds did not converge in %d rounds", kMaxRounds);
     return enqueue_labels(st.cl, p, s);
+}
+
+int cluster_rounds(const void* ws, hipStream_t s, int* rounds) {
+    if (int rc = cluster_finish(ws, s)) return rc;
+    std::lock_guard<std::mutex> lk(g_rs_mu);
+    auto it = g_rs.find(ws);
+    *rounds = it == g_rs.end() ? 0 : it->second.rounds;
+    return ROGTK_OK;
 }
 
 void cluster_release(const void* ws) {
@@ -898,10 +1150,10 @@ int launch_cluster_assign(const ClusterLayout& cl, const uint8_t* ws, const uint
     ProfScope prof(K_ASSIGN, s);
     const int g = grid_for((n + 3) / 4);
     if (cl.label_by_code)
-        hipLaunchKernelGGL(k_assign<0>, dim3(g), dim3(kBlock), 0, s, codes, regular_bits, n, p.labelcode, p.f,
+        hipLaunchKernelGGL(k_assign<0>, dim3(g), dim3(kBlock), 0, s, codes, regular_bits, n, p.labelcode, p.D,
                            p.RT, cluster_id);
     else
-        hipLaunchKernelGGL(k_assign<1>, dim3(g), dim3(kBlock), 0, s, codes, regular_bits, n, p.labelcode, p.f,
+        hipLaunchKernelGGL(k_assign<1>, dim3(g), dim3(kBlock), 0, s, codes, regular_bits, n, p.labelcode, p.ilab,
                            p.RT, cluster_id);
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;

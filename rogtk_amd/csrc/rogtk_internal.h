@@ -135,7 +135,7 @@ struct ClusterLayout {
     bool label_by_code;  // dense label table indexed by code (L <= 13)
     // byte offsets into the workspace
     int64_t off_stats, off_presence, off_bitmap, off_rt, off_wpref, off_blksum, off_blkoff, off_D, off_f, off_ur,
-        off_rbits, off_rpref, off_rblksum, off_rblkoff, off_labelcode, total;
+        off_rbits, off_lroot, off_rpref, off_rblksum, off_rblkoff, off_labelcode, off_ilab, total;
 };
 int cluster_layout(int L, int64_t max_distinct, ClusterLayout* out);
 
@@ -174,6 +174,7 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
 // Waits for an asynchronous resolve's round flags and completes it if needed.
 int cluster_finish(const void* ws, hipStream_t s);
 void cluster_release(const void* ws);
+int cluster_rounds(const void* ws, hipStream_t s, int* rounds);
 int launch_cluster_assign(const ClusterLayout& cl, const uint8_t* ws, const uint32_t* codes,
                           const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id,
                           hipStream_t s);

@@ -161,6 +161,12 @@ class ClusterEngine:
         _lib.call("rogtk_cluster_stats", _p(self.ws), self.umi_len, self.max_distinct, out, _s(stream))
         return {"n_distinct": out[0], "n_clusters": out[1], "overflow": out[2], "error": out[3]}
 
+    def rounds(self, stream=None) -> int:
+        """Global hook rounds the last resolve needed (diagnostics)."""
+        r = ctypes.c_int(0)
+        _lib.call("rogtk_cluster_rounds", _p(self.ws), _s(stream), ctypes.byref(r))
+        return r.value
+
 
 def cluster_batch(engine: ClusterEngine, batch: PackedBatch, cluster_id: torch.Tensor,
                   max_distance: int = 1, group=None, marked: bool = False, stream=None) -> None:

@@ -418,6 +418,9 @@ def test_long_chains_need_extra_rounds(rg, L):
     cid = torch.empty(n, dtype=torch.int32, device="cuda")
     D.cluster_batch(eng, batch, cid, 1)
     stats = eng.stats()
+    rounds = eng.rounds()
+    print(f"L={L} n={n} rounds={rounds}")
     rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L)), L, 1)
     assert stats["n_clusters"] == rk
     assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc)
+    assert rounds >= 1
