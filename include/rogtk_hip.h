@@ -162,6 +162,10 @@ int rogtk_cluster_stats(const void* ws, int umi_len, int64_t max_distinct, int64
 /* Diagnostics: the global hook rounds the last resolve of ws needed (completes it
  * first, like rogtk_cluster_stats); 0 when it needed none (exact mode, umi_len <= 7). */
 int rogtk_cluster_rounds(const void* ws, void* stream, int* rounds);
+/* Tuning / tests: hook rounds launched speculatively by rogtk_cluster_resolve
+ * (1..64; 0 restores the default of 4). Process-wide. Fewer rounds never change
+ * results: the rest run when assign / stats find the flags not yet converged. */
+int rogtk_cluster_set_spec_rounds(int n);
 /* Releases the host-side resolve state kept for ws (call before freeing ws). */
 int rogtk_cluster_release(const void* ws);
 

@@ -69,6 +69,7 @@ SIGNATURES = {
     "rogtk_cluster_stats": [_vp, _i32, _i64, _P_I64, _vp],
     "rogtk_cluster_release": [_vp],
     "rogtk_cluster_rounds": [_vp, _vp, ctypes.POINTER(ctypes.c_int)],
+    "rogtk_cluster_set_spec_rounds": [_i32],
     "rogtk_umi_complexity_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _P_SCORES],
     "rogtk_hamming_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _u32, _vp, _vp],
     "rogtk_umi_cluster_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _P_I64,

@@ -484,6 +484,8 @@ int rogtk_cluster_rounds(const void* ws, void* stream, int* rounds) {
     return cluster_rounds(ws, as_stream(stream), rounds);
 }
 
+int rogtk_cluster_set_spec_rounds(int n) { return cluster_set_spec_rounds(n); }
+
 int rogtk_cluster_release(const void* ws) {
     if (ws) cluster_release(ws);
     return ROGTK_OK;

@@ -37,6 +37,8 @@
 #include <map>
 #include <mutex>
 
+#include <atomic>
+
 #include "rogtk_internal.h"
 
 namespace rogtk {
@@ -975,6 +977,7 @@ int launch_cluster_local_bitmap(const ClusterLayout& cl, uint8_t* ws, uint64_t* 
 namespace {
 
 constexpr int kSpecRounds = 4;  // speculative global rounds (synth-v1 needs 3-4)
+std::atomic<int> g_spec_rounds{kSpecRounds};
 
 // Host-side state of an in-flight resolve, keyed by workspace: the round flags are
 // copied asynchronously to pinned host memory so resolve never blocks the host;
@@ -1072,16 +1075,17 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
                            p.f, p.D, p.UR, p.lroot, cl.rwords, cl.max_distinct, p.stats);
         ROGTK_HIP_CHECK(hipGetLastError());
         if (cl.L > kLocalPos) {
-            if (int rc = enqueue_rounds(cl, p, 0, kSpecRounds, s)) return rc;
+            const int spec = g_spec_rounds.load();
+            if (int rc = enqueue_rounds(cl, p, 0, spec, s)) return rc;
             if (!st.ev) {
                 ROGTK_HIP_CHECK(hipEventCreateWithFlags(&st.ev, hipEventDisableTiming));
                 ROGTK_HIP_CHECK(hipHostMalloc((void**)&st.hflags, kMaxRounds * sizeof(unsigned int),
                                               hipHostMallocDefault));
             }
-            ROGTK_HIP_CHECK(hipMemcpyAsync(st.hflags, p.flags, kSpecRounds * sizeof(unsigned int),
+            ROGTK_HIP_CHECK(hipMemcpyAsync(st.hflags, p.flags, spec * sizeof(unsigned int),
                                            hipMemcpyDeviceToHost, s));
             ROGTK_HIP_CHECK(hipEventRecord(st.ev, s));
-            st.launched = kSpecRounds;
+            st.launched = spec;
             st.pending = true;
         }
     }
@@ -1119,6 +1123,12 @@ int cluster_finish(const void* ws, hipStream_t s) {
     st.pending = false;
     ROGTK_REQUIRE(converged, ROGTK_E_HIP, "cluster: union rounds did not converge in %d rounds", kMaxRounds);
     return enqueue_labels(st.cl, p, s);
+}
+
+int cluster_set_spec_rounds(int n) {
+    ROGTK_REQUIRE(n >= 0 && n <= kMaxRounds, ROGTK_E_INVALID, "spec rounds %d outside 0..%d", n, kMaxRounds);
+    g_spec_rounds.store(n == 0 ? kSpecRounds : n);
+    return ROGTK_OK;
 }
 
 int cluster_rounds(const void* ws, hipStream_t s, int* rounds) {

@@ -168,6 +168,11 @@ class ClusterEngine:
         return r.value
 
 
+def set_spec_rounds(n: int) -> None:
+    """Hook rounds launched speculatively per resolve (0 = default 4); results never change."""
+    _lib.call("rogtk_cluster_set_spec_rounds", int(n))
+
+
 def cluster_batch(engine: ClusterEngine, batch: PackedBatch, cluster_id: torch.Tensor,
                   max_distance: int = 1, group=None, marked: bool = False, stream=None) -> None:
     """mark -> local bitmap -> (all-gather over ranks) -> resolve -> assign."""

@@ -398,6 +398,36 @@ def _chain_codes(rng, L, length, high_bases):
     return np.array([(c << shift0) | low for c in path], dtype=np.uint32)
 
 
+@pytest.mark.parametrize("spec", [1, 2])
+@pytest.mark.parametrize("L", [12, 16])
+def test_deferred_rounds_match(rg, L, spec):
+    """With fewer speculative rounds than the data needs, the rounds that assign runs
+    after the (speculative) labels must give the same clusters: labels never clobber
+    the forest."""
+    import torch
+
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+
+    n = 200_000
+    codes_h = synth.umi_codes(n, L, seed=11)
+    codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
+    batch = D.PackedBatch(codes, L)
+    eng = D.ClusterEngine(L, n, "cuda")
+    cid = torch.empty(n, dtype=torch.int32, device="cuda")
+    try:
+        D.set_spec_rounds(spec)
+        D.cluster_batch(eng, batch, cid, 1)
+        rounds = eng.rounds()
+    finally:
+        D.set_spec_rounds(0)
+    if spec == 1:
+        assert rounds > spec  # the deferred path ran
+    rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L)), L, 1)
+    assert eng.stats()["n_clusters"] == rk
+    assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc)
+
+
 @pytest.mark.parametrize("L", [12, 16])
 def test_long_chains_need_extra_rounds(rg, L):
     """Long Hamming-1 paths (diameter >> speculative rounds) resolve exactly: the deferred
