@@ -302,6 +302,26 @@ int rogtk_fastq_pair_close(void* reader);
 
 /* ============================== profiling ================================ */
 /* When enabled, every kernel launch is bracketed by HIP events on its stream. */
+/* ============ polars plugin ABI (rogtk_amd/csrc/polars_plugin.cpp) ============
+ * librogtk_hip.so also exports the symbols polars resolves for the reference's
+ * register_plugin_function calls (pyo3-polars 0.17 #[polars_expr], Cargo.toml:39):
+ *   void _polars_plugin_<name>(SeriesExport*, size_t, const uint8_t* kwargs, size_t,
+ *                              SeriesExport* out, CallerContext*);
+ *   void _polars_plugin_field_<name>(ArrowSchema*, size_t, ArrowSchema* out,
+ *                                    const uint8_t* kwargs, size_t);
+ *   uint32_t _polars_plugin_get_version(void);
+ *   const char* _polars_plugin_get_last_error_message(void);
+ * for <name> in umi_complexity_all_expr, umi_{shannon_entropy, linguistic_complexity,
+ * homopolymer_fraction, dinucleotide_entropy, combined_score, longest_homopolymer,
+ * dust_score}_expr (expressions.rs:1234-1410), hamming_{distance,within}_expr
+ * (:1048-1101), assemble_sequences_expr (:695), assemble_sequences_with_anchors_expr
+ * (:770), sweep_assembly_params_expr (:880), optimize_assembly_expr
+ * (fracture_opt.rs:283). The structs are the Arrow C Data Interface and polars-ffi
+ * version_0's SeriesExport {ArrowSchema* field; ArrowArray** arrays; size_t len;
+ * void (*release)(SeriesExport*); void* private_data;}; see INTEGRATION.md.
+ * Diagnostics: the kwargs pickle as the plugin parses it, "key=value" lines. */
+int rogtk_plugin_kwargs_debug(const uint8_t* kwargs, int64_t len, char* out, int64_t cap, int64_t* out_len);
+
 int rogtk_profile_enable(int on);
 int rogtk_profile_reset(void);
 /* Total device milliseconds and launch count recorded for `kernel` (synchronises

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 HIP_LIB_PATH = os.path.join(_HERE, "librogtk_hip.so")
-SYNTH_LIB_PATH = os.path.join(_HERE, "librogtk_synth.so")
+SYNTH_LIB_PATH = os.path.join(_HERE, "_synth", "librogtk_synth.so")
 
 ROGTK_OK = 0
 ROGTK_E_INVALID = 1
@@ -70,6 +70,7 @@ SIGNATURES = {
     "rogtk_cluster_release": [_vp],
     "rogtk_cluster_rounds": [_vp, _vp, ctypes.POINTER(ctypes.c_int)],
     "rogtk_cluster_set_spec_rounds": [_i32],
+    "rogtk_plugin_kwargs_debug": [ctypes.c_char_p, _i64, ctypes.c_char_p, _i64, ctypes.POINTER(_i64)],
     "rogtk_umi_complexity_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _P_SCORES],
     "rogtk_hamming_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _u32, _vp, _vp],
     "rogtk_umi_cluster_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _P_I64,
@@ -130,6 +131,8 @@ def hip() -> ctypes.CDLL:
                                  "(make -C rogtk_amd/csrc). There is no CPU fallback.")
             lib = ctypes.CDLL(HIP_LIB_PATH)
             for name, argtypes in SIGNATURES.items():
+                if not hasattr(lib, name):  # a missing export fails loudly at its first call
+                    continue
                 fn = getattr(lib, name)
                 fn.argtypes = argtypes
                 fn.restype = ctypes.c_int

@@ -94,10 +94,9 @@ def umi_complexity_scores(column: ColumnLike) -> Union[pa.StructArray, pa.Chunke
         res = _complexity_chunk(ch, _FIELD_NAMES)
         vbuf = validity_buffer(ch)
         children = [_field_array(name, typ, res[name], vbuf, ch.n) for name, typ in FIELDS]
-        mask = None
-        if vbuf is not None:
-            mask = pa.array(~np.unpackbits(np.frombuffer(vbuf, np.uint8), bitorder="little")[: ch.n].astype(bool))
-        arrays.append(pa.StructArray.from_arrays(children, fields=list(STRUCT_TYPE), mask=mask))
+        # df.into_struct (expressions.rs:1283): struct rows stay valid, a null UMI gives
+        # a row whose seven fields are null (:1258-1266)
+        arrays.append(pa.StructArray.from_arrays(children, fields=list(STRUCT_TYPE)))
     return concat(arrays, STRUCT_TYPE)
 
 

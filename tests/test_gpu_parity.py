@@ -70,7 +70,9 @@ def test_golden_complexity(rg, fixture):
     col = _col_from_npz(z)
     got = rg.umi_complexity_scores(col)
     valid = z["valid"]
-    assert got.null_count == (~valid).sum()
+    assert got.null_count == 0  # df.into_struct: rows valid, fields null (expressions.rs:1258-1283)
+    for f in P().FIELDS:
+        assert got.field(f).null_count == (~valid).sum()
     ref = {f: (z["f_" + f].view(np.float64) if z["f_" + f].dtype == np.uint64 else z["f_" + f])
            for f in P().FIELDS}
     _assert_scores_equal(got, ref, valid)
@@ -160,7 +162,7 @@ def test_nulls_and_chunks(rg):
     umis = ["ACGTACGTACGT", None, "AAAAAAAAAAAA", None, "ACGTNACGTACG", ""]
     ch = pa.chunked_array([pa.array(umis[:3]), pa.array(umis[3:])])
     got = rg.umi_complexity_scores(ch)
-    assert got.null_count == 2
+    assert got.null_count == 0 and sum(c.field(0).null_count for c in got.chunks) == 2
     ref = P().umi_complexity(P().StrCol.from_list(umis))
     flat = pa.concat_arrays(got.chunks)
     _assert_scores_equal(flat, ref, ref["valid"])
