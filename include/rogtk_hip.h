@@ -302,6 +302,44 @@ int rogtk_fastq_pair_close(void* reader);
 
 /* ============================== profiling ================================ */
 /* When enabled, every kernel launch is bracketed by HIP events on its stream. */
+/* ============ BAM -> Arrow columns, decoded on the GPU ============
+ * Host: BGZF inflate (zlib, blocks in parallel on n_threads threads, <= 0: min(16, cores))
+ * and record framing. GPU: every per-record field (rogtk_amd/csrc/bam.hip). Columns
+ * follow create_bam_schema (src/bam.rs:3203-3221): name, chrom, start, end, flags,
+ * sequence, quality_scores; the record semantics per mode:
+ *   ROGTK_BAM_NOODLES       extract_record_data_enhanced (bam.rs:170-262): "*" name ->
+ *                           "unknown", 1-based start, end = start + CIGAR reference length - 1
+ *   ROGTK_BAM_HTSLIB        process_htslib_records_to_batch (bam.rs:3028-3148): 1-based
+ *                           start, end = start + seq_len - 1, 0xFF qualities -> null
+ *   ROGTK_BAM_HTSLIB_BLOCKS process_htslib_records_to_batch (bam_htslib.rs:154-241):
+ *                           0-based start, end = bam_endpos if > pos else start, IUPAC bases */
+#define ROGTK_BAM_NOODLES 0
+#define ROGTK_BAM_HTSLIB 1
+#define ROGTK_BAM_HTSLIB_BLOCKS 2
+typedef struct rogtk_bam_batch {
+    /* string columns [0] name [1] chrom [2] sequence [3] quality_scores: int64 offsets
+     * (n + 1, from 0), values, validity bitmap (Arrow LSB order; NULL = all valid) */
+    const int64_t* offsets[4];
+    const uint8_t* values[4];
+    const uint8_t* validity[4];
+    /* u32 columns [0] start [1] end [2] flags and their validity (NULL = all valid) */
+    const uint32_t* u32[3];
+    const uint8_t* u32_validity[3];
+} rogtk_bam_batch;
+int rogtk_bam_open(const char* path, int n_threads, void** reader);
+/* Binary header: reference names (lossy UTF-8) as offsets / values, and the SAM text. */
+int rogtk_bam_header(void* reader, int64_t* n_ref, const int64_t** name_offsets, const uint8_t** name_values,
+                     const char** text, int64_t* text_len);
+/* Next <= max_records records (host buffers owned by the reader until the next call;
+ * *n_records = 0 at the end). Sequence / quality columns are skipped (NULL) unless asked. */
+int rogtk_bam_next(void* reader, int64_t max_records, int mode, int include_sequence, int include_quality,
+                   int64_t* n_records, rogtk_bam_batch* out);
+/* Same, but the batch stays in DEVICE memory (valid until the next call); the work is
+ * enqueued on the reader's stream, returned in *stream (callers order after it). */
+int rogtk_bam_next_dev(void* reader, int64_t max_records, int mode, int include_sequence, int include_quality,
+                       int64_t* n_records, rogtk_bam_batch* out, void** stream);
+int rogtk_bam_close(void* reader);
+
 /* ============ polars plugin ABI (rogtk_amd/csrc/polars_plugin.cpp) ============
  * librogtk_hip.so also exports the symbols polars resolves for the reference's
  * register_plugin_function calls (pyo3-polars 0.17 #[polars_expr], Cargo.toml:39):

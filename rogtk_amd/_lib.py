@@ -45,6 +45,19 @@ class UmiScores(ctypes.Structure):
     ]
 
 
+class BamBatch(ctypes.Structure):
+    """rogtk_bam_batch (include/rogtk_hip.h): string columns name / chrom / sequence /
+    quality_scores, u32 columns start / end / flags (create_bam_schema, bam.rs:3203-3221)."""
+
+    _fields_ = [
+        ("offsets", ctypes.c_void_p * 4),
+        ("values", ctypes.c_void_p * 4),
+        ("validity", ctypes.c_void_p * 4),
+        ("u32", ctypes.c_void_p * 3),
+        ("u32_validity", ctypes.c_void_p * 3),
+    ]
+
+
 _vp, _i64, _i32, _u32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_uint32
 _P_SCORES = ctypes.POINTER(UmiScores)
 _P_I64 = ctypes.POINTER(ctypes.c_int64)
@@ -70,6 +83,13 @@ SIGNATURES = {
     "rogtk_cluster_release": [_vp],
     "rogtk_cluster_rounds": [_vp, _vp, ctypes.POINTER(ctypes.c_int)],
     "rogtk_cluster_set_spec_rounds": [_i32],
+    "rogtk_bam_open": [ctypes.c_char_p, _i32, ctypes.POINTER(_vp)],
+    "rogtk_bam_header": [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp),
+                         ctypes.POINTER(_i64)],
+    "rogtk_bam_next": [_vp, _i64, _i32, _i32, _i32, ctypes.POINTER(_i64), ctypes.POINTER(BamBatch)],
+    "rogtk_bam_next_dev": [_vp, _i64, _i32, _i32, _i32, ctypes.POINTER(_i64), ctypes.POINTER(BamBatch),
+                           ctypes.POINTER(_vp)],
+    "rogtk_bam_close": [_vp],
     "rogtk_plugin_kwargs_debug": [ctypes.c_char_p, _i64, ctypes.c_char_p, _i64, ctypes.POINTER(_i64)],
     "rogtk_umi_complexity_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _P_SCORES],
     "rogtk_hamming_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _u32, _vp, _vp],

@@ -1,0 +1,305 @@
+"""BAM -> Arrow conversion with per-record decoding on the GPU.
+
+Host-side mirror of rogtk's BAM converters (src/bam.rs, src/bam_htslib.rs; registered in
+src/lib.rs:489-505, re-exported by rogtk/__init__.py:17-56). Every converter writes the
+reference's schema (create_bam_schema, bam.rs:3203-3221; + source_file for bams_*,
+bam.rs:609-632):
+
+    name Utf8 (non-null), chrom Utf8, start UInt32, end UInt32, flags UInt32 (non-null),
+    [sequence Utf8], [quality_scores Utf8], [source_file Utf8 (non-null)]
+
+The per-record semantics come in three flavours, selected by which reference function is
+mirrored (include/rogtk_hip.h, ROGTK_BAM_*):
+
+* "noodles" — extract_record_data_enhanced (bam.rs:170-262): bam_to_parquet,
+  bams_to_parquet, bam_to_arrow_ipc, bams_to_arrow_ipc, bam_to_arrow_ipc_parallel,
+  bam_to_arrow_ipc_gzp_parallel.
+* "htslib" — process_htslib_records_to_batch (bam.rs:3028-3148):
+  bam_to_arrow_ipc_htslib_{parallel,optimized,mmap_parallel,multi_reader_parallel},
+  bams_to_arrow_ipc_htslib_optimized.
+* "htslib_blocks" — process_htslib_records_to_batch (bam_htslib.rs:154-241):
+  bam_to_arrow_ipc_htslib_bgzf_blocks.
+
+BGZF blocks are inflated on host threads (zlib); framing is one u32 per record; every
+field of every record is decoded by GPU kernels (rogtk_amd/csrc/bam.hip). Rows come out
+in file order. The reference's threaded writers may emit batches in any order ("no order
+preservation", bam.rs:1979-1981); file order is one of its possible outputs. Thread,
+buffer and worker knobs of the reference signatures are accepted and do not change
+results.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Iterator, List, Optional, Sequence
+
+import numpy as np
+import pyarrow as pa
+
+from . import _lib
+
+MODES = {"noodles": 0, "htslib": 1, "htslib_blocks": 2}
+# records decoded per GPU batch (independent of the output batch_size, which only
+# slices the Arrow record batches the way the reference batches its writes)
+DECODE_RECORDS = 1 << 20
+
+
+def bam_schema(include_sequence: bool = True, include_quality: bool = True,
+               include_source_file: bool = False) -> pa.Schema:
+    """create_bam_schema (bam.rs:3203-3221) / create_bam_schema_with_source (:609-632)."""
+    fields = [pa.field("name", pa.string(), nullable=False), pa.field("chrom", pa.string()),
+              pa.field("start", pa.uint32()), pa.field("end", pa.uint32()),
+              pa.field("flags", pa.uint32(), nullable=False)]
+    if include_sequence:
+        fields.append(pa.field("sequence", pa.string()))
+    if include_quality:
+        fields.append(pa.field("quality_scores", pa.string()))
+    if include_source_file:
+        fields.append(pa.field("source_file", pa.string(), nullable=False))
+    return pa.schema(fields)
+
+
+def _np_from(ptr: int, dtype, count: int) -> np.ndarray:
+    if count <= 0 or not ptr:
+        return np.zeros(0, dtype=dtype)
+    buf = (ctypes.c_char * (count * np.dtype(dtype).itemsize)).from_address(ptr)
+    return np.frombuffer(buf, dtype=dtype, count=count).copy()
+
+
+def _validity(ptr: int, n: int):
+    if not ptr or n == 0:
+        return None, 0
+    bits = _np_from(ptr, np.uint8, (n + 7) // 8)
+    nulls = n - int(np.unpackbits(bits, bitorder="little")[:n].sum())
+    return (pa.py_buffer(bits), nulls) if nulls else (None, 0)
+
+
+class BamReader:
+    """A BAM file open for GPU decoding (rogtk_bam_open / _next / _close)."""
+
+    def __init__(self, path: str, n_threads: int = 0):
+        self._h = ctypes.c_void_p()
+        _lib.call("rogtk_bam_open", os.fsencode(path), int(n_threads), ctypes.byref(self._h))
+
+    def close(self) -> None:
+        if self._h:
+            _lib.call("rogtk_bam_close", self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reference_names(self) -> List[str]:
+        n = ctypes.c_int64()
+        off, val, txt = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        tl = ctypes.c_int64()
+        _lib.call("rogtk_bam_header", self._h, ctypes.byref(n), ctypes.byref(off), ctypes.byref(val),
+                  ctypes.byref(txt), ctypes.byref(tl))
+        o = _np_from(off.value, np.int64, n.value + 1)
+        v = _np_from(val.value, np.uint8, int(o[-1]) if len(o) else 0).tobytes()
+        return [v[o[i]:o[i + 1]].decode() for i in range(n.value)]
+
+    def next_batch(self, max_records: int, mode: str = "noodles", include_sequence: bool = True,
+                   include_quality: bool = True) -> Optional[pa.RecordBatch]:
+        """Up to max_records records as a RecordBatch of the reference schema; None at the end."""
+        b = _lib.BamBatch()
+        n = ctypes.c_int64()
+        _lib.call("rogtk_bam_next", self._h, int(max_records), MODES[mode], int(bool(include_sequence)),
+                  int(bool(include_quality)), ctypes.byref(n), ctypes.byref(b))
+        n = int(n.value)
+        if n == 0:
+            return None
+        cols = []
+
+        def string_col(c):
+            off = _np_from(b.offsets[c], np.int64, n + 1)
+            vals = _np_from(b.values[c], np.uint8, int(off[-1]))
+            vbuf, nulls = _validity(b.validity[c], n)
+            if off[-1] < 2 ** 31:
+                return pa.Array.from_buffers(pa.string(), n, [vbuf, pa.py_buffer(off.astype(np.int32)),
+                                                              pa.py_buffer(vals)], null_count=nulls)
+            arr = pa.Array.from_buffers(pa.large_string(), n, [vbuf, pa.py_buffer(off), pa.py_buffer(vals)],
+                                        null_count=nulls)
+            return arr.cast(pa.string())
+
+        def u32_col(c):
+            vals = _np_from(b.u32[c], np.uint32, n)
+            vbuf, nulls = _validity(b.u32_validity[c], n)
+            return pa.Array.from_buffers(pa.uint32(), n, [vbuf, pa.py_buffer(vals)], null_count=nulls)
+
+        cols = [string_col(0), string_col(1), u32_col(0), u32_col(1), u32_col(2)]
+        if include_sequence:
+            cols.append(string_col(2))
+        if include_quality:
+            cols.append(string_col(3))
+        return pa.RecordBatch.from_arrays(cols, schema=bam_schema(include_sequence, include_quality))
+
+
+def iter_bam_batches(bam_path: str, batch_size: int = 50000, include_sequence: bool = True,
+                     include_quality: bool = True, mode: str = "noodles", limit: Optional[int] = None,
+                     n_threads: int = 0) -> Iterator[pa.RecordBatch]:
+    """Record batches of <= batch_size rows (the last one shorter), at most `limit` rows."""
+    if not os.path.exists(bam_path):
+        raise _lib.RogtkError(_lib.ROGTK_E_INVALID, f"BAM file does not exist: {bam_path}")
+    if batch_size <= 0:
+        raise _lib.RogtkError(_lib.ROGTK_E_INVALID, "batch_size must be greater than 0")
+    bs = min(int(batch_size), 1_000_000)  # effective_batch_size (bam.rs:306)
+    left = None if limit is None else int(limit)
+    with BamReader(bam_path, n_threads) as r:
+        while left is None or left > 0:
+            want = DECODE_RECORDS if left is None else min(DECODE_RECORDS, left)
+            rb = r.next_batch(want, mode, include_sequence, include_quality)
+            if rb is None:
+                break
+            if left is not None:
+                left -= rb.num_rows
+            for a in range(0, rb.num_rows, bs):
+                yield rb.slice(a, bs)
+
+
+def _with_source(rb: pa.RecordBatch, source: str, schema: pa.Schema) -> pa.RecordBatch:
+    """add_source_file_column (bam.rs:634-643)."""
+    col = pa.array([source] * rb.num_rows, type=pa.string())
+    return pa.RecordBatch.from_arrays(list(rb.columns) + [col], schema=schema)
+
+
+def _convert(paths: Sequence[str], out_path: str, fmt: str, batch_size: int, include_sequence: bool,
+             include_quality: bool, limit: Optional[int], mode: str, include_source_file: bool = False,
+             compression: str = "snappy") -> None:
+    if not paths:
+        raise _lib.RogtkError(_lib.ROGTK_E_INVALID, "No BAM files provided")
+    if batch_size <= 0:
+        raise _lib.RogtkError(_lib.ROGTK_E_INVALID, "batch_size must be greater than 0")
+    for p in paths:
+        if not os.path.exists(p):
+            raise _lib.RogtkError(_lib.ROGTK_E_INVALID, f"BAM file does not exist: {p}")
+    parent = os.path.dirname(out_path)
+    if parent:
+        os.makedirs(parent, exist_ok=True)
+    schema = bam_schema(include_sequence, include_quality, include_source_file)
+    if fmt == "ipc":
+        writer = pa.ipc.new_file(out_path, schema)
+    else:
+        import pyarrow.parquet as pq
+        writer = pq.ParquetWriter(out_path, schema, compression=_parquet_codec(compression))
+    left = None if limit is None else int(limit)
+    try:
+        for p in paths:
+            if left is not None and left <= 0:
+                break
+            source = os.path.basename(p) or p
+            for rb in iter_bam_batches(p, batch_size, include_sequence, include_quality, mode, left):
+                if left is not None:
+                    left -= rb.num_rows
+                if include_source_file:
+                    rb = _with_source(rb, source, schema)
+                if fmt == "ipc":
+                    writer.write_batch(rb)
+                else:
+                    writer.write_table(pa.Table.from_batches([rb], schema=schema))
+    finally:
+        writer.close()
+
+
+def _parquet_codec(compression: str) -> str:
+    """parse_compression (bam.rs:3287-3300): unknown names fall back to snappy."""
+    c = compression.lower()
+    return {"snappy": "snappy", "gzip": "gzip", "lz4": "lz4", "zstd": "zstd", "brotli": "brotli",
+            "uncompressed": "none", "none": "none"}.get(c, "snappy")
+
+
+# ------------------------------------------------- the reference's converters
+def bam_to_parquet(bam_path, parquet_path, batch_size=50000, include_sequence=True, include_quality=True,
+                   compression="snappy", limit=None):
+    """bam.rs:264-416 (noodles record semantics)."""
+    _convert([bam_path], parquet_path, "parquet", batch_size, include_sequence, include_quality, limit, "noodles",
+             compression=compression)
+
+
+def bams_to_parquet(bam_paths, parquet_path, batch_size=50000, include_sequence=True, include_quality=True,
+                    compression="snappy", limit=None, include_source_file=False):
+    """bam.rs:418-607."""
+    _convert(list(bam_paths), parquet_path, "parquet", batch_size, include_sequence, include_quality, limit,
+             "noodles", include_source_file, compression)
+
+
+def bam_to_arrow_ipc(bam_path, arrow_ipc_path, batch_size=50000, include_sequence=True, include_quality=True,
+                     limit=None):
+    """bam.rs:645-787."""
+    _convert([bam_path], arrow_ipc_path, "ipc", batch_size, include_sequence, include_quality, limit, "noodles")
+
+
+def bams_to_arrow_ipc(bam_paths, arrow_ipc_path, batch_size=50000, include_sequence=True, include_quality=True,
+                      limit=None, include_source_file=False):
+    """bam.rs:789-970."""
+    _convert(list(bam_paths), arrow_ipc_path, "ipc", batch_size, include_sequence, include_quality, limit,
+             "noodles", include_source_file)
+
+
+def bam_to_arrow_ipc_parallel(bam_path, arrow_ipc_path, batch_size=50000, include_sequence=True,
+                              include_quality=True, num_threads=4, preserve_order=False, limit=None):
+    """bam.rs:972-1264."""
+    _convert([bam_path], arrow_ipc_path, "ipc", batch_size, include_sequence, include_quality, limit, "noodles")
+
+
+def bam_to_arrow_ipc_gzp_parallel(bam_path, arrow_ipc_path, batch_size=50000, include_sequence=True,
+                                  include_quality=True, decompression_threads=4, processing_threads=2,
+                                  preserve_order=False, limit=None):
+    """bam.rs:1266-1582."""
+    _convert([bam_path], arrow_ipc_path, "ipc", batch_size, include_sequence, include_quality, limit, "noodles")
+
+
+def bam_to_arrow_ipc_htslib_parallel(bam_path, arrow_ipc_path, batch_size=15000, include_sequence=True,
+                                     include_quality=True, bgzf_threads=8, writing_threads=8, read_buffer_mb=1024,
+                                     write_buffer_mb=256, limit=None):
+    """bam.rs:1584-1843 (htslib record semantics)."""
+    _convert([bam_path], arrow_ipc_path, "ipc", batch_size, include_sequence, include_quality, limit, "htslib")
+
+
+def bam_to_arrow_ipc_htslib_optimized(bam_path, arrow_ipc_path, batch_size=15000, include_sequence=True,
+                                      include_quality=True, max_bgzf_threads=16, writing_threads=6,
+                                      read_buffer_mb=2048, write_buffer_mb=512, limit=None):
+    """bam.rs:1845-2116."""
+    _convert([bam_path], arrow_ipc_path, "ipc", batch_size, include_sequence, include_quality, limit, "htslib")
+
+
+def bams_to_arrow_ipc_htslib_optimized(bam_paths, arrow_ipc_path, batch_size=15000, include_sequence=True,
+                                       include_quality=True, max_bgzf_threads=4, writing_threads=6,
+                                       read_buffer_mb=2048, write_buffer_mb=128, limit=None,
+                                       include_source_file=False):
+    """bam.rs:2118-2344."""
+    _convert(list(bam_paths), arrow_ipc_path, "ipc", batch_size, include_sequence, include_quality, limit,
+             "htslib", include_source_file)
+
+
+def bam_to_arrow_ipc_htslib_mmap_parallel(bam_path, arrow_ipc_path, batch_size=15000, include_sequence=True,
+                                          include_quality=True, num_workers=4, chunk_size_mb=64,
+                                          bgzf_threads_per_worker=2, limit=None):
+    """bam.rs:2346-2609."""
+    _convert([bam_path], arrow_ipc_path, "ipc", batch_size, include_sequence, include_quality, limit, "htslib")
+
+
+def bam_to_arrow_ipc_htslib_multi_reader_parallel(bam_path, arrow_ipc_path, batch_size=15000,
+                                                  include_sequence=True, include_quality=True, num_readers=2,
+                                                  bgzf_threads=4, writing_threads=10, read_buffer_mb=1024,
+                                                  write_buffer_mb=256, limit=None):
+    """bam.rs:2825-3026."""
+    _convert([bam_path], arrow_ipc_path, "ipc", batch_size, include_sequence, include_quality, limit, "htslib")
+
+
+def bam_to_arrow_ipc_htslib_bgzf_blocks(bam_path, arrow_ipc_path, batch_size=20000, include_sequence=True,
+                                        include_quality=True, bgzf_threads=4, writing_threads=8,
+                                        read_buffer_mb=None, write_buffer_mb=None, limit=None,
+                                        num_block_workers=None):
+    """bam_htslib.rs:507-... (0-based start, bam_endpos end, IUPAC bases)."""
+    _convert([bam_path], arrow_ipc_path, "ipc", batch_size, include_sequence, include_quality, limit,
+             "htslib_blocks")

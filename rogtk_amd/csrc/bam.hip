@@ -1,0 +1,765 @@
+// bam.hip — BAM records -> Arrow columns, decoded on the GPU.
+//
+// Replaces the record loops of the reference's BAM converters:
+//   mode ROGTK_BAM_NOODLES       extract_record_data_enhanced   src/bam.rs:170-262 (noodles 0.82;
+//                                bam_to_parquet / bam_to_arrow_ipc / bams_* / *_parallel / *_gzp_parallel)
+//   mode ROGTK_BAM_HTSLIB        process_htslib_records_to_batch src/bam.rs:3028-3148 (rust-htslib 0.47;
+//                                bam_to_arrow_ipc_htslib_{parallel,optimized,mmap_parallel,multi_reader_parallel},
+//                                bams_to_arrow_ipc_htslib_optimized)
+//   mode ROGTK_BAM_HTSLIB_BLOCKS process_htslib_records_to_batch src/bam_htslib.rs:154-241
+//                                (bam_to_arrow_ipc_htslib_bgzf_blocks: 0-based start, bam_endpos end)
+// Schema (create_bam_schema, bam.rs:3203-3221): name, chrom, start, end, flags, [sequence], [quality_scores].
+//
+// Work split (MI355X-first):
+//   host  : BGZF inflate (zlib, one block per task, all blocks of a chunk in parallel on
+//           the reader's threads) into a pinned stream buffer; record framing (one u32 per
+//           record); the header (binary reference list, names lossy-UTF-8 as
+//           String::from_utf8_lossy, bam.rs:2611-2618).
+//   device: every per-record field: k_bam_fields (thread per record: fixed fields, CIGAR
+//           reference length, output lengths, validity via wave ballots), an exclusive scan
+//           of the lengths, k_bam_fill (one wave per record: read name with UTF-8 lossy
+//           repair, chromosome name, 4-bit -> ASCII bases, PHRED+33 qualities).
+// The raw record bytes cross PCIe once; columns are produced in HBM and copied back
+// (host API) or left there for the UMI engine (rogtk_bam_next_dev).
+#include <hipcub/hipcub.hpp>
+#include <zlib.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "rogtk_internal.h"
+
+namespace rogtk {
+namespace {
+
+// ------------------------------------------------------------------ device
+// Rust String::from_utf8_lossy: every maximal invalid subsequence -> U+FFFD (EF BF BD).
+// Returns the output length; writes when out != nullptr.
+__device__ __host__ inline int utf8_lossy(const uint8_t* p, int n, uint8_t* out) {
+    int i = 0, o = 0;
+    while (i < n) {
+        const uint8_t b = p[i];
+        int need = 0;
+        uint8_t lo = 0x80, hi = 0xBF;
+        if (b < 0x80) {
+            if (out) out[o] = b;
+            ++o;
+            ++i;
+            continue;
+        } else if (b >= 0xC2 && b <= 0xDF) {
+            need = 1;
+        } else if (b == 0xE0) {
+            need = 2, lo = 0xA0;
+        } else if ((b >= 0xE1 && b <= 0xEC) || b == 0xEE || b == 0xEF) {
+            need = 2;
+        } else if (b == 0xED) {
+            need = 2, hi = 0x9F;
+        } else if (b == 0xF0) {
+            need = 3, lo = 0x90;
+        } else if (b >= 0xF1 && b <= 0xF3) {
+            need = 3;
+        } else if (b == 0xF4) {
+            need = 3, hi = 0x8F;
+        }
+        int j = i + 1, got = 0;
+        if (need) {
+            for (; got < need && j < n; ++got, ++j) {
+                const uint8_t c = p[j];
+                const uint8_t l = got == 0 ? lo : 0x80, h = got == 0 ? hi : 0xBF;
+                if (c < l || c > h) break;
+            }
+        }
+        if (need && got == need) {
+            for (int k = i; k < j; ++k)
+                if (out) out[o + (k - i)] = p[k];
+            o += j - i;
+        } else {
+            if (out) out[o] = 0xEF, out[o + 1] = 0xBF, out[o + 2] = 0xBD;
+            o += 3;
+        }
+        i = j;
+    }
+    return o;
+}
+
+__device__ inline uint32_t ld_u32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+__device__ inline uint16_t ld_u16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+
+// Per-record layout (SAMv1 §4.2): after block_size: refID@0 pos@4 l_read_name@8 mapq@9
+// bin@10 n_cigar_op@12 flag@14 l_seq@16 next_refID@20 next_pos@24 tlen@28 read_name@32,
+// cigar, seq ((l_seq+1)/2), qual (l_seq), tags.
+struct RecView {
+    const uint8_t* b;  // first byte after block_size
+    uint32_t bsize;
+    int32_t ref_id, pos;
+    uint32_t l_name, n_cigar, flag, l_seq;
+    __device__ void load(const uint8_t* raw, int64_t off) {
+        bsize = ld_u32(raw + off);
+        b = raw + off + 4;
+        ref_id = (int32_t)ld_u32(b);
+        pos = (int32_t)ld_u32(b + 4);
+        l_name = b[8];
+        n_cigar = ld_u16(b + 12);
+        flag = ld_u16(b + 14);
+        l_seq = ld_u32(b + 16);
+    }
+    __device__ const uint8_t* name() const { return b + 32; }
+    __device__ const uint8_t* cigar() const { return b + 32 + l_name; }
+    __device__ const uint8_t* seq() const { return cigar() + 4u * n_cigar; }
+    __device__ const uint8_t* qual() const { return seq() + (l_seq + 1) / 2; }
+    // bytes the fixed fields + variable fields need (sanity against block_size)
+    __device__ bool fits() const {
+        return bsize >= 32 && (uint64_t)32 + l_name + 4ull * n_cigar + (l_seq + 1ull) / 2 + l_seq <= bsize;
+    }
+};
+
+// name length without the NUL terminator
+__device__ inline uint32_t qname_len(const RecView& r) { return r.l_name ? r.l_name - 1 : 0; }
+
+// noodles: a read name of "*" is a missing name (-> "unknown", bam.rs:178-180)
+__device__ inline bool noodles_missing_name(const RecView& r) {
+    return r.l_name == 0 || (r.l_name == 2 && r.name()[0] == '*');
+}
+
+struct FieldsOut {
+    int64_t* len[4];      // name, chrom, sequence, quality_scores (output bytes per row)
+    uint64_t* valid[7];   // chrom, start, end, sequence, quality_scores (bitmap words); [0..4]
+    uint32_t* start;
+    uint32_t* end;
+    uint32_t* flags;
+    int32_t* chrom_id;    // resolved reference index or -1
+    unsigned long long* bad;  // records whose fields overrun block_size
+};
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_bam_fields(const uint8_t* __restrict__ raw, const int64_t* __restrict__ roff,
+                                                    int64_t n, const int64_t* __restrict__ ref_off, int32_t n_ref,
+                                                    FieldsOut o) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool v_chrom = false, v_start = false, v_end = false, v_seq = false, v_qual = false;
+    if (r < n) {
+        RecView rv;
+        rv.load(raw, roff[r]);
+        if (!rv.fits()) {
+            atomicAdd(o.bad, 1ull);
+            rv.l_name = 0, rv.n_cigar = 0, rv.l_seq = 0;
+        }
+        // --- name
+        int64_t name_len;
+        const uint32_t ql = qname_len(rv);
+        if (MODE == ROGTK_BAM_NOODLES && noodles_missing_name(rv)) {
+            name_len = 7;  // "unknown"
+        } else {
+            bool ascii = true;
+            for (uint32_t i = 0; i < ql; ++i) ascii &= rv.name()[i] < 0x80;
+            name_len = ascii ? ql : utf8_lossy(rv.name(), (int)ql, nullptr);
+        }
+        // --- chrom: tid in [0, n_ref) (bam.rs:186-197, 3052-3062; bam_htslib.rs:178-183)
+        int32_t cid = (rv.ref_id >= 0 && rv.ref_id < n_ref) ? rv.ref_id : -1;
+        v_chrom = cid >= 0;
+        // --- positions
+        uint32_t start = 0, end = 0;
+        if (MODE == ROGTK_BAM_HTSLIB) {  // bam.rs:3064-3073: 1-based start, end = start + seq_len - 1
+            v_start = v_end = rv.pos >= 0;
+            start = (uint32_t)rv.pos + 1u;
+            end = start + rv.l_seq - 1u;
+        } else {
+            // reference length of the CIGAR: M D N = X (noodles calculate_bam_alignment_length
+            // bam.rs:3238-3256; htslib bam_cigar2rlen)
+            uint32_t rlen = 0;
+            const uint8_t* cg = rv.cigar();
+            for (uint32_t k = 0; k < rv.n_cigar; ++k) {
+                const uint32_t op = ld_u32(cg + 4 * k);
+                const uint32_t kind = op & 15u;
+                if (kind == 0 || kind == 2 || kind == 3 || kind == 7 || kind == 8) rlen += op >> 4;
+            }
+            if (MODE == ROGTK_BAM_NOODLES) {  // bam.rs:199-211: 1-based, end = start + ref_len - 1
+                v_start = v_end = rv.pos >= 0;
+                start = (uint32_t)rv.pos + 1u;
+                end = start + rlen - 1u;
+            } else {  // bam_htslib.rs:186-193: 0-based start, end = bam_endpos if > pos else start
+                v_start = rv.pos >= 0;
+                start = (uint32_t)rv.pos;
+                const int64_t ref_end = ((rv.flag & 4u) == 0 && rv.n_cigar > 0) ? (int64_t)rv.pos + rlen
+                                                                                : (int64_t)rv.pos + 1;
+                if (ref_end > (int64_t)rv.pos) {
+                    v_end = true;
+                    end = (uint32_t)ref_end;
+                } else {
+                    v_end = v_start;
+                    end = start;
+                }
+            }
+        }
+        // --- sequence / qualities
+        v_seq = rv.l_seq > 0;
+        if (MODE == ROGTK_BAM_HTSLIB)  // bam.rs:3095-3101: missing qualities (0xFF) -> null
+            v_qual = rv.l_seq > 0 && rv.qual()[0] != 0xFF;
+        else
+            v_qual = rv.l_seq > 0;
+        o.len[0][r] = name_len;
+        o.len[1][r] = v_chrom ? ref_off[cid + 1] - ref_off[cid] : 0;
+        o.len[2][r] = v_seq ? rv.l_seq : 0;
+        o.len[3][r] = v_qual ? rv.l_seq : 0;
+        o.start[r] = v_start ? start : 0;
+        o.end[r] = v_end ? end : 0;
+        o.flags[r] = rv.flag;
+        o.chrom_id[r] = cid;
+    }
+    // validity bitmaps: one 64-bit word per wave (lane order = Arrow LSB order)
+    const bool vs[5] = {v_chrom, v_start, v_end, v_seq, v_qual};
+    const int64_t w = r >> 6;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+        const uint64_t bits = __ballot(vs[c]);
+        if ((threadIdx.x & 63) == 0 && w * 64 < n) o.valid[c][w] = bits;
+    }
+}
+
+struct FillIn {
+    const int64_t* off[4];  // output offsets (exclusive scan of len, n + 1)
+    uint8_t* val[4];
+    const int64_t* len[4];
+    const int32_t* chrom_id;
+    const int64_t* ref_off;
+    const uint8_t* ref_val;
+    int include_seq, include_qual;
+};
+
+__device__ inline uint8_t base_ascii(uint32_t nib, int mode) {
+    // decode_base (bam.rs:3227-3236, 3083-3091): 1 A, 2 C, 4 G, 8 T, else N;
+    // htslib seq_nt16_str for ROGTK_BAM_HTSLIB_BLOCKS (`seq().as_bytes()`, bam_htslib.rs:199)
+    if (mode == ROGTK_BAM_HTSLIB_BLOCKS) {
+        const char* t = "=ACMGRSVTWYHKDBN";
+        return (uint8_t)t[nib & 15];
+    }
+    switch (nib) {
+        case 1: return 'A';
+        case 2: return 'C';
+        case 4: return 'G';
+        case 8: return 'T';
+        default: return 'N';
+    }
+}
+
+// One wave per record.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_bam_fill(const uint8_t* __restrict__ raw, const int64_t* __restrict__ roff,
+                                                  int64_t n, FillIn f) {
+    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (r >= n) return;
+    RecView rv;
+    rv.load(raw, roff[r]);
+    if (!rv.fits()) rv.l_name = 0, rv.n_cigar = 0, rv.l_seq = 0;
+    // name
+    {
+        uint8_t* out = f.val[0] + f.off[0][r];
+        const uint32_t ql = qname_len(rv);
+        if (MODE == ROGTK_BAM_NOODLES && noodles_missing_name(rv)) {
+            if (lane < 7) out[lane] = (uint8_t)"unknown"[lane];
+        } else if (f.len[0][r] == (int64_t)ql) {
+            for (uint32_t i = lane; i < ql; i += 64) out[i] = rv.name()[i];
+        } else if (lane == 0) {
+            utf8_lossy(rv.name(), (int)ql, out);
+        }
+    }
+    // chrom
+    if (f.chrom_id[r] >= 0) {
+        const int32_t c = f.chrom_id[r];
+        const int64_t a = f.ref_off[c], len = f.ref_off[c + 1] - a;
+        uint8_t* out = f.val[1] + f.off[1][r];
+        for (int64_t i = lane; i < len; i += 64) out[i] = f.ref_val[a + i];
+    }
+    // sequence: 4-bit codes, high nibble first
+    if (f.include_seq && f.len[2][r] > 0) {
+        const uint8_t* s = rv.seq();
+        uint8_t* out = f.val[2] + f.off[2][r];
+        for (uint32_t i = lane; i < rv.l_seq; i += 64) {
+            const uint8_t byte = s[i >> 1];
+            out[i] = base_ascii((i & 1) ? (byte & 15u) : (byte >> 4), MODE);
+        }
+    }
+    // qualities: PHRED + 33, wrapping u8 add (quality_to_string_zero_copy, bam.rs:2622-2636)
+    if (f.include_qual && f.len[3][r] > 0) {
+        const uint8_t* q = rv.qual();
+        uint8_t* out = f.val[3] + f.off[3][r];
+        for (uint32_t i = lane; i < rv.l_seq; i += 64) out[i] = (uint8_t)(q[i] + 33u);
+    }
+}
+
+// ------------------------------------------------------------------ host
+struct PinnedBuf {
+    uint8_t* p = nullptr;
+    size_t cap = 0;
+    ~PinnedBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    int ensure(size_t bytes, size_t keep = 0) {
+        if (bytes <= cap && p) return ROGTK_OK;
+        size_t want = std::max<size_t>(bytes + bytes / 2, 1 << 20);
+        uint8_t* q = nullptr;
+        ROGTK_HIP_CHECK(hipHostMalloc((void**)&q, want, hipHostMallocDefault));
+        if (p && keep) memcpy(q, p, keep);
+        if (p) (void)hipHostFree(p);
+        p = q;
+        cap = want;
+        return ROGTK_OK;
+    }
+};
+
+struct Bgzf {
+    FILE* f = nullptr;
+    int threads = 1;
+    bool file_eof = false;
+    std::vector<uint8_t> comp;  // compressed bytes not yet inflated
+    size_t comp_len = 0;
+    PinnedBuf buf;              // uncompressed stream: [pos, end)
+    size_t pos = 0, end = 0;
+    std::string err;
+
+    // Inflate the next chunk of whole blocks and append it after `end`. Keeps the bytes
+    // from `keep_from` on (they move to the front). Returns false at end of input.
+    bool more(size_t keep_from, size_t chunk = 32u << 20) {
+        if (!err.empty()) return false;
+        // read compressed bytes
+        if (!file_eof) {
+            if (comp.size() < comp_len + chunk) comp.resize(comp_len + chunk);
+            const size_t got = fread(comp.data() + comp_len, 1, chunk, f);
+            comp_len += got;
+            if (got < chunk) file_eof = true;
+        }
+        // frame whole BGZF blocks
+        struct Blk {
+            size_t c0, clen, out;
+            uint32_t isize;
+        };
+        std::vector<Blk> blks;
+        size_t o = 0, total = 0;
+        while (o + 18 <= comp_len) {
+            const uint8_t* h = comp.data() + o;
+            if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) {
+                err = "not a BGZF file (bad gzip block header)";
+                return false;
+            }
+            const size_t xlen = h[10] | (h[11] << 8);
+            if (o + 12 + xlen > comp_len) break;
+            size_t bsize = 0;
+            for (size_t x = 0; x + 4 <= xlen;) {
+                const uint8_t* sf = h + 12 + x;
+                const size_t slen = sf[2] | (sf[3] << 8);
+                if (sf[0] == 'B' && sf[1] == 'C' && slen == 2) bsize = (size_t)(sf[4] | (sf[5] << 8)) + 1;
+                x += 4 + slen;
+            }
+            if (bsize == 0) {
+                err = "BGZF block without a BC (BSIZE) subfield";
+                return false;
+            }
+            if (o + bsize > comp_len) break;
+            const uint8_t* t = h + bsize - 4;
+            const uint32_t isize = t[0] | (t[1] << 8) | (t[2] << 16) | ((uint32_t)t[3] << 24);
+            const size_t c0 = o + 12 + xlen;
+            if (bsize < 12 + xlen + 8) {
+                err = "corrupt BGZF block (BSIZE too small)";
+                return false;
+            }
+            blks.push_back({c0, bsize - 12 - xlen - 8, total, isize});
+            total += isize;
+            o += bsize;
+        }
+        if (blks.empty()) {
+            if (file_eof && comp_len > 0) err = "truncated BGZF block at end of file";
+            return false;
+        }
+        // make room: move [keep_from, end) to the front
+        const size_t keep = end - keep_from;
+        PinnedBuf nb;
+        const size_t need = keep + total;
+        if (need > buf.cap || keep_from > 0) {
+            if (need > buf.cap) {
+                if (nb.ensure(need) != ROGTK_OK) {
+                    err = "pinned host allocation failed";
+                    return false;
+                }
+                if (keep) memcpy(nb.p, buf.p + keep_from, keep);
+                std::swap(buf.p, nb.p);
+                std::swap(buf.cap, nb.cap);
+            } else if (keep) {
+                memmove(buf.p, buf.p + keep_from, keep);
+            }
+            pos -= keep_from;
+            end = keep;
+        }
+        // inflate blocks in parallel
+        std::atomic<size_t> next{0};
+        std::atomic<bool> bad{false};
+        uint8_t* dst = buf.p + end;
+        auto work = [&] {
+            z_stream zs;
+            memset(&zs, 0, sizeof zs);
+            if (inflateInit2(&zs, -15) != Z_OK) {
+                bad = true;
+                return;
+            }
+            for (size_t b; (b = next.fetch_add(1)) < blks.size();) {
+                const Blk& k = blks[b];
+                inflateReset(&zs);
+                zs.next_in = comp.data() + k.c0;
+                zs.avail_in = (uInt)k.clen;
+                zs.next_out = dst + k.out;
+                zs.avail_out = k.isize;
+                const int rc = inflate(&zs, Z_FINISH);
+                if (rc != Z_STREAM_END || zs.avail_out != 0) bad = true;
+            }
+            inflateEnd(&zs);
+        };
+        const int nt = (int)std::min<size_t>((size_t)std::max(threads, 1), blks.size());
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(work);
+        work();
+        for (auto& t : th) t.join();
+        if (bad) {
+            err = "BGZF inflate failed (corrupt deflate stream)";
+            return false;
+        }
+        end += total;
+        // keep the partial trailing block
+        memmove(comp.data(), comp.data() + o, comp_len - o);
+        comp_len -= o;
+        return true;
+    }
+    // at least n bytes available from pos + rel (compacting [pos, end) to the front)
+    bool ensure_rel(size_t rel, size_t n) {
+        while (end - pos < rel + n)
+            if (!more(pos)) return false;
+        return true;
+    }
+};
+
+struct BamReader {
+    Bgzf z;
+    std::string text;
+    std::vector<int64_t> ref_off{0};
+    std::vector<uint8_t> ref_val;
+    int device = -1;
+    hipStream_t stream = nullptr;
+    // batch state
+    int64_t n = 0;
+    std::vector<int64_t> roff;  // record offsets relative to batch start (n + 1)
+    DevBuf d_raw, d_roff, d_len[4], d_off[4], d_val[4], d_valid[5], d_start, d_end, d_flags, d_cid, d_ref_off,
+        d_ref_val, d_bad, d_cub;
+    // host outputs (pinned)
+    PinnedBuf h_off[4], h_val[4], h_valid[5], h_u32[3];
+    ~BamReader() {
+        if (z.f) fclose(z.f);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+// lossy UTF-8 (String::from_utf8_lossy) on the host, for header reference names
+std::string lossy_host(const uint8_t* p, int n) {
+    std::string s((size_t)utf8_lossy(p, n, nullptr), '\0');
+    utf8_lossy(p, n, (uint8_t*)&s[0]);
+    return s;
+}
+
+int read_header(BamReader* R) {
+    auto need = [&](size_t n) -> int {
+        ROGTK_REQUIRE(R->z.ensure_rel(0, n), ROGTK_E_INVALID, "BAM header: %s",
+                      R->z.err.empty() ? "unexpected end of file" : R->z.err.c_str());
+        return ROGTK_OK;
+    };
+    auto rd32 = [&]() {
+        const uint8_t* p = R->z.buf.p + R->z.pos;
+        R->z.pos += 4;
+        return (int32_t)((uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24));
+    };
+    int rc;
+    if ((rc = need(8)) != ROGTK_OK) return rc;
+    ROGTK_REQUIRE(memcmp(R->z.buf.p + R->z.pos, "BAM\1", 4) == 0, ROGTK_E_INVALID, "not a BAM file (bad magic)");
+    R->z.pos += 4;
+    const int32_t l_text = rd32();
+    ROGTK_REQUIRE(l_text >= 0, ROGTK_E_INVALID, "BAM header: negative l_text");
+    if ((rc = need((size_t)l_text + 4)) != ROGTK_OK) return rc;
+    R->text.assign((const char*)R->z.buf.p + R->z.pos, (size_t)l_text);
+    R->z.pos += l_text;
+    const int32_t n_ref = rd32();
+    ROGTK_REQUIRE(n_ref >= 0, ROGTK_E_INVALID, "BAM header: negative n_ref");
+    for (int32_t i = 0; i < n_ref; ++i) {
+        if ((rc = need(4)) != ROGTK_OK) return rc;
+        const int32_t l_name = rd32();
+        ROGTK_REQUIRE(l_name >= 1, ROGTK_E_INVALID, "BAM header: bad reference name length");
+        if ((rc = need((size_t)l_name + 4)) != ROGTK_OK) return rc;
+        const std::string nm = lossy_host(R->z.buf.p + R->z.pos, l_name - 1);
+        R->z.pos += l_name;
+        (void)rd32();  // l_ref
+        R->ref_val.insert(R->ref_val.end(), nm.begin(), nm.end());
+        R->ref_off.push_back((int64_t)R->ref_val.size());
+    }
+    return ROGTK_OK;
+}
+
+constexpr size_t kMaxBatchBytes = size_t(1) << 30;
+
+// Frame up to max_records records from the stream; leaves them at [pos, pos + roff[n]).
+int frame_batch(BamReader* R, int64_t max_records) {
+    Bgzf& z = R->z;
+    R->roff.assign(1, 0);
+    size_t rel = 0;  // bytes of the batch framed so far (from z.pos)
+    int64_t n = 0;
+    while (n < max_records && rel < kMaxBatchBytes) {
+        if (!z.ensure_rel(rel, 4)) {
+            ROGTK_REQUIRE(z.err.empty(), ROGTK_E_INVALID, "BAM: %s", z.err.c_str());
+            ROGTK_REQUIRE(z.end - z.pos == rel, ROGTK_E_INVALID,
+                          "BAM: truncated record at end of file (%zu stray bytes)", z.end - z.pos - rel);
+            break;  // clean end of file
+        }
+        const uint8_t* p = z.buf.p + z.pos + rel;
+        const uint32_t bs = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+        ROGTK_REQUIRE(bs >= 32 && bs < (1u << 30), ROGTK_E_INVALID, "BAM: invalid record block_size %u", bs);
+        ROGTK_REQUIRE(z.ensure_rel(rel, 4 + (size_t)bs), ROGTK_E_INVALID, "BAM: %s",
+                      z.err.empty() ? "truncated record at end of file" : z.err.c_str());
+        rel += 4 + bs;
+        ++n;
+        R->roff.push_back((int64_t)rel);
+    }
+    R->n = n;
+    return ROGTK_OK;
+}
+
+int decode_batch(BamReader* R, int mode, int include_seq, int include_qual) {
+    const int64_t n = R->n;
+    hipStream_t s = R->stream;
+    const int64_t bytes = R->roff[n];
+    if (R->d_raw.ensure((size_t)std::max<int64_t>(bytes, 4)) != ROGTK_OK ||
+        R->d_roff.ensure((size_t)(n + 1) * 8) != ROGTK_OK)
+        return ROGTK_E_HIP;
+    if (bytes) ROGTK_HIP_CHECK(hipMemcpyAsync(R->d_raw.p, R->z.buf.p + R->z.pos, bytes, hipMemcpyHostToDevice, s));
+    ROGTK_HIP_CHECK(hipMemcpyAsync(R->d_roff.p, R->roff.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, s));
+    const int64_t words = (n + 63) / 64;
+    for (int c = 0; c < 4; ++c) {
+        if (R->d_len[c].ensure((size_t)(n + 1) * 8) != ROGTK_OK || R->d_off[c].ensure((size_t)(n + 1) * 8) != ROGTK_OK)
+            return ROGTK_E_HIP;
+    }
+    for (int c = 0; c < 5; ++c)
+        if (R->d_valid[c].ensure((size_t)std::max<int64_t>(words, 1) * 8) != ROGTK_OK) return ROGTK_E_HIP;
+    if (R->d_start.ensure((size_t)std::max<int64_t>(n, 1) * 4) != ROGTK_OK ||
+        R->d_end.ensure((size_t)std::max<int64_t>(n, 1) * 4) != ROGTK_OK ||
+        R->d_flags.ensure((size_t)std::max<int64_t>(n, 1) * 4) != ROGTK_OK ||
+        R->d_cid.ensure((size_t)std::max<int64_t>(n, 1) * 4) != ROGTK_OK || R->d_bad.ensure(8) != ROGTK_OK)
+        return ROGTK_E_HIP;
+    ROGTK_HIP_CHECK(hipMemsetAsync(R->d_bad.p, 0, 8, s));
+    FieldsOut fo;
+    for (int c = 0; c < 4; ++c) fo.len[c] = R->d_len[c].as<int64_t>();
+    for (int c = 0; c < 5; ++c) fo.valid[c] = R->d_valid[c].as<uint64_t>();
+    fo.start = R->d_start.as<uint32_t>();
+    fo.end = R->d_end.as<uint32_t>();
+    fo.flags = R->d_flags.as<uint32_t>();
+    fo.chrom_id = R->d_cid.as<int32_t>();
+    fo.bad = R->d_bad.as<unsigned long long>();
+    const int32_t n_ref = (int32_t)R->ref_off.size() - 1;
+    if (n > 0) {
+        const dim3 g((unsigned)((n + 255) / 256));
+        if (mode == ROGTK_BAM_NOODLES)
+            hipLaunchKernelGGL(k_bam_fields<ROGTK_BAM_NOODLES>, g, dim3(256), 0, s, R->d_raw.as<uint8_t>(),
+                               R->d_roff.as<int64_t>(), n, R->d_ref_off.as<int64_t>(), n_ref, fo);
+        else if (mode == ROGTK_BAM_HTSLIB)
+            hipLaunchKernelGGL(k_bam_fields<ROGTK_BAM_HTSLIB>, g, dim3(256), 0, s, R->d_raw.as<uint8_t>(),
+                               R->d_roff.as<int64_t>(), n, R->d_ref_off.as<int64_t>(), n_ref, fo);
+        else
+            hipLaunchKernelGGL(k_bam_fields<ROGTK_BAM_HTSLIB_BLOCKS>, g, dim3(256), 0, s, R->d_raw.as<uint8_t>(),
+                               R->d_roff.as<int64_t>(), n, R->d_ref_off.as<int64_t>(), n_ref, fo);
+        ROGTK_HIP_CHECK(hipGetLastError());
+    }
+    // exclusive scans of the four length columns (n + 1 entries: the last is the total)
+    for (int c = 0; c < 4; ++c) {
+        ROGTK_HIP_CHECK(hipMemsetAsync(R->d_len[c].as<int64_t>() + n, 0, 8, s));
+        size_t tb = 0;
+        ROGTK_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, R->d_len[c].as<int64_t>(),
+                                                         R->d_off[c].as<int64_t>(), (int)(n + 1), s));
+        if (R->d_cub.ensure(tb) != ROGTK_OK) return ROGTK_E_HIP;
+        ROGTK_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(R->d_cub.p, tb, R->d_len[c].as<int64_t>(),
+                                                         R->d_off[c].as<int64_t>(), (int)(n + 1), s));
+    }
+    int64_t tot[4];
+    unsigned long long bad = 0;
+    for (int c = 0; c < 4; ++c)
+        ROGTK_HIP_CHECK(hipMemcpyAsync(&tot[c], R->d_off[c].as<int64_t>() + n, 8, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&bad, R->d_bad.p, 8, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    ROGTK_REQUIRE(bad == 0, ROGTK_E_INVALID, "BAM: %llu record(s) whose fields overrun their block_size", bad);
+    for (int c = 0; c < 4; ++c)
+        if (R->d_val[c].ensure((size_t)std::max<int64_t>(tot[c], 1)) != ROGTK_OK) return ROGTK_E_HIP;
+    FillIn fi;
+    for (int c = 0; c < 4; ++c) {
+        fi.off[c] = R->d_off[c].as<int64_t>();
+        fi.val[c] = R->d_val[c].as<uint8_t>();
+        fi.len[c] = R->d_len[c].as<int64_t>();
+    }
+    fi.chrom_id = R->d_cid.as<int32_t>();
+    fi.ref_off = R->d_ref_off.as<int64_t>();
+    fi.ref_val = R->d_ref_val.as<uint8_t>();
+    fi.include_seq = include_seq;
+    fi.include_qual = include_qual;
+    if (n > 0) {
+        const dim3 g((unsigned)((n * 64 + 255) / 256));
+        if (mode == ROGTK_BAM_NOODLES)
+            hipLaunchKernelGGL(k_bam_fill<ROGTK_BAM_NOODLES>, g, dim3(256), 0, s, R->d_raw.as<uint8_t>(),
+                               R->d_roff.as<int64_t>(), n, fi);
+        else if (mode == ROGTK_BAM_HTSLIB)
+            hipLaunchKernelGGL(k_bam_fill<ROGTK_BAM_HTSLIB>, g, dim3(256), 0, s, R->d_raw.as<uint8_t>(),
+                               R->d_roff.as<int64_t>(), n, fi);
+        else
+            hipLaunchKernelGGL(k_bam_fill<ROGTK_BAM_HTSLIB_BLOCKS>, g, dim3(256), 0, s, R->d_raw.as<uint8_t>(),
+                               R->d_roff.as<int64_t>(), n, fi);
+        ROGTK_HIP_CHECK(hipGetLastError());
+    }
+    return ROGTK_OK;
+}
+
+}  // namespace
+}  // namespace rogtk
+
+using namespace rogtk;
+
+extern "C" {
+
+int rogtk_bam_open(const char* path, int n_threads, void** reader) {
+    ROGTK_REQUIRE(path && reader, ROGTK_E_INVALID, "bam: NULL argument");
+    *reader = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        set_error("no HIP device available (librogtk_hip needs an MI355X / gfx950 GPU)");
+        return ROGTK_E_NODEVICE;
+    }
+    std::unique_ptr<BamReader> R(new BamReader());
+    R->z.f = fopen(path, "rb");
+    ROGTK_REQUIRE(R->z.f, ROGTK_E_INVALID, "Failed to open BAM file '%s'", path);
+    R->z.threads = n_threads > 0 ? n_threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    ROGTK_HIP_CHECK(hipGetDevice(&R->device));
+    ROGTK_HIP_CHECK(hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking));
+    int rc = read_header(R.get());
+    if (rc != ROGTK_OK) return rc;
+    const size_t rb = R->ref_off.size() * 8, vb = std::max<size_t>(R->ref_val.size(), 1);
+    if (R->d_ref_off.ensure(rb) != ROGTK_OK || R->d_ref_val.ensure(vb) != ROGTK_OK) return ROGTK_E_HIP;
+    ROGTK_HIP_CHECK(hipMemcpy(R->d_ref_off.p, R->ref_off.data(), rb, hipMemcpyHostToDevice));
+    if (!R->ref_val.empty())
+        ROGTK_HIP_CHECK(hipMemcpy(R->d_ref_val.p, R->ref_val.data(), R->ref_val.size(), hipMemcpyHostToDevice));
+    *reader = R.release();
+    return ROGTK_OK;
+}
+
+int rogtk_bam_header(void* reader, int64_t* n_ref, const int64_t** name_offsets, const uint8_t** name_values,
+                     const char** text, int64_t* text_len) {
+    ROGTK_REQUIRE(reader, ROGTK_E_INVALID, "bam: NULL reader");
+    auto* R = static_cast<BamReader*>(reader);
+    if (n_ref) *n_ref = (int64_t)R->ref_off.size() - 1;
+    if (name_offsets) *name_offsets = R->ref_off.data();
+    if (name_values) *name_values = R->ref_val.data();
+    if (text) *text = R->text.c_str();
+    if (text_len) *text_len = (int64_t)R->text.size();
+    return ROGTK_OK;
+}
+
+static int bam_next_common(BamReader* R, int64_t max_records, int mode, int include_sequence, int include_quality) {
+    ROGTK_REQUIRE(max_records > 0, ROGTK_E_INVALID, "bam: max_records must be > 0");
+    ROGTK_REQUIRE(mode == ROGTK_BAM_NOODLES || mode == ROGTK_BAM_HTSLIB || mode == ROGTK_BAM_HTSLIB_BLOCKS,
+                  ROGTK_E_INVALID, "bam: unknown mode %d", mode);
+    ROGTK_HIP_CHECK(hipSetDevice(R->device));
+    // release the previous batch's bytes
+    R->z.pos += R->n ? (size_t)R->roff[R->n] : 0;
+    R->n = 0;
+    int rc = frame_batch(R, max_records);
+    if (rc != ROGTK_OK) return rc;
+    return decode_batch(R, mode, include_sequence, include_quality);
+}
+
+int rogtk_bam_next(void* reader, int64_t max_records, int mode, int include_sequence, int include_quality,
+                   int64_t* n_records, rogtk_bam_batch* out) {
+    ROGTK_REQUIRE(reader && n_records && out, ROGTK_E_INVALID, "bam: NULL argument");
+    auto* R = static_cast<BamReader*>(reader);
+    *n_records = 0;
+    int rc = bam_next_common(R, max_records, mode, include_sequence, include_quality);
+    if (rc != ROGTK_OK) return rc;
+    const int64_t n = R->n;
+    hipStream_t s = R->stream;
+    memset(out, 0, sizeof *out);
+    const int64_t words = (n + 63) / 64;
+    for (int c = 0; c < 4; ++c) {
+        if ((c == 2 && !include_sequence) || (c == 3 && !include_quality)) continue;
+        int64_t tot = 0;
+        ROGTK_HIP_CHECK(hipMemcpyAsync(&tot, R->d_off[c].as<int64_t>() + n, 8, hipMemcpyDeviceToHost, s));
+        ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+        if (R->h_off[c].ensure((size_t)(n + 1) * 8) != ROGTK_OK ||
+            R->h_val[c].ensure((size_t)std::max<int64_t>(tot, 1)) != ROGTK_OK)
+            return ROGTK_E_HIP;
+        ROGTK_HIP_CHECK(hipMemcpyAsync(R->h_off[c].p, R->d_off[c].p, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, s));
+        if (tot) ROGTK_HIP_CHECK(hipMemcpyAsync(R->h_val[c].p, R->d_val[c].p, (size_t)tot, hipMemcpyDeviceToHost, s));
+        out->offsets[c] = (const int64_t*)R->h_off[c].p;
+        out->values[c] = R->h_val[c].p;
+    }
+    // validity: chrom, start, end, sequence, quality_scores
+    for (int c = 0; c < 5; ++c) {
+        if ((c == 3 && !include_sequence) || (c == 4 && !include_quality)) continue;
+        if (R->h_valid[c].ensure((size_t)std::max<int64_t>(words, 1) * 8) != ROGTK_OK) return ROGTK_E_HIP;
+        if (words)
+            ROGTK_HIP_CHECK(hipMemcpyAsync(R->h_valid[c].p, R->d_valid[c].p, (size_t)words * 8, hipMemcpyDeviceToHost, s));
+    }
+    out->validity[1] = R->h_valid[0].p;
+    out->validity[2] = include_sequence ? R->h_valid[3].p : nullptr;
+    out->validity[3] = include_quality ? R->h_valid[4].p : nullptr;
+    DevBuf* u[3] = {&R->d_start, &R->d_end, &R->d_flags};
+    for (int c = 0; c < 3; ++c) {
+        if (R->h_u32[c].ensure((size_t)std::max<int64_t>(n, 1) * 4) != ROGTK_OK) return ROGTK_E_HIP;
+        if (n) ROGTK_HIP_CHECK(hipMemcpyAsync(R->h_u32[c].p, u[c]->p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+        out->u32[c] = (const uint32_t*)R->h_u32[c].p;
+    }
+    out->u32_validity[0] = R->h_valid[1].p;
+    out->u32_validity[1] = R->h_valid[2].p;
+    out->u32_validity[2] = nullptr;
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    *n_records = n;
+    return ROGTK_OK;
+}
+
+int rogtk_bam_next_dev(void* reader, int64_t max_records, int mode, int include_sequence, int include_quality,
+                       int64_t* n_records, rogtk_bam_batch* out, void** stream) {
+    ROGTK_REQUIRE(reader && n_records && out, ROGTK_E_INVALID, "bam: NULL argument");
+    auto* R = static_cast<BamReader*>(reader);
+    *n_records = 0;
+    int rc = bam_next_common(R, max_records, mode, include_sequence, include_quality);
+    if (rc != ROGTK_OK) return rc;
+    memset(out, 0, sizeof *out);
+    for (int c = 0; c < 4; ++c) {
+        out->offsets[c] = R->d_off[c].as<int64_t>();
+        out->values[c] = R->d_val[c].as<uint8_t>();
+    }
+    out->validity[1] = R->d_valid[0].as<uint8_t>();
+    out->validity[2] = R->d_valid[3].as<uint8_t>();
+    out->validity[3] = R->d_valid[4].as<uint8_t>();
+    out->u32[0] = R->d_start.as<uint32_t>();
+    out->u32[1] = R->d_end.as<uint32_t>();
+    out->u32[2] = R->d_flags.as<uint32_t>();
+    out->u32_validity[0] = R->d_valid[1].as<uint8_t>();
+    out->u32_validity[1] = R->d_valid[2].as<uint8_t>();
+    if (stream) *stream = R->stream;
+    *n_records = R->n;
+    return ROGTK_OK;
+}
+
+int rogtk_bam_close(void* reader) {
+    if (!reader) return ROGTK_OK;
+    auto* R = static_cast<BamReader*>(reader);
+    if (R->stream) (void)hipStreamSynchronize(R->stream);
+    delete R;
+    return ROGTK_OK;
+}
+
+}  // extern "C"

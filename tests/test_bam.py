@@ -1,0 +1,222 @@
+"""BAM -> Arrow: GPU record decoding (rogtk_amd/csrc/bam.hip) vs
+the pure-Python restatement (oracle/pybam.py) of the reference's three record semantics.
+
+The reference ships no BAM fixtures; files are written here (rogtk_amd/synth_bam.py,
+SAMv1 layout) with the edge cases its code distinguishes: unmapped / out-of-range refIDs,
+pos -1 and < -1, '*' names, non-UTF-8 names, CIGARs with every op (and invalid op codes),
+empty and odd-length sequences, IUPAC bases, missing (0xFF) and > 93 qualities, records
+spanning BGZF blocks and decode batches.
+"""
+import os
+
+import numpy as np
+import pyarrow as pa
+import pytest
+
+from oracle import pybam
+from rogtk_amd import synth_bam
+
+MODES = ("noodles", "htslib", "htslib_blocks")
+REFS = [(b"chr1", 1000), (b"chrX", 500), (b"contig_\xff\xfe", 10)]
+
+
+def _random_records(seed, n):
+    rng = np.random.default_rng(seed)
+    iupac = "=ACMGRSVTWYHKDBN"
+    recs = []
+    for i in range(n):
+        kind = int(rng.integers(0, 12))
+        name = f"read{i}".encode()
+        if kind == 0:
+            name = b"*"
+        elif kind == 1:
+            name = b"bad\xff\xc3(x\xe2\x82" + bytes([int(rng.integers(128, 256))])
+        elif kind == 2:
+            name = bytes(rng.integers(33, 127, size=int(rng.integers(100, 250)), dtype=np.uint8))
+        ref_id = int(rng.choice([-1, 0, 1, 2, 3, -5]))
+        pos = int(rng.choice([-1, -2, 0, int(rng.integers(0, 10**6))]))
+        flag = int(rng.integers(0, 1 << 16))
+        l_seq = int(rng.choice([0, 1, 7, 12, 150, int(rng.integers(0, 300))]))
+        alphabet = iupac if kind in (3, 4) else "ACGTN"
+        seq = "".join(rng.choice(list(alphabet), l_seq)) if l_seq else ""
+        if kind == 5 and l_seq:
+            qual = None
+        elif kind == 6 and l_seq:
+            qual = bytes([0]) + b"\xff" * (l_seq - 1)
+        elif kind == 7 and l_seq:
+            qual = bytes(rng.integers(90, 255, size=l_seq, dtype=np.uint8))
+        else:
+            qual = bytes(rng.integers(0, 42, size=l_seq, dtype=np.uint8))
+        n_cig = int(rng.integers(0, 6))
+        raw_cigar = [int(rng.integers(0, 200)) << 4 | int(rng.integers(0, 16 if kind == 8 else 9)) for _ in range(n_cig)]
+        tags = b"NMi\x01\x00\x00\x00" if kind % 2 else b""
+        recs.append(synth_bam.record_bytes(name=name, ref_id=ref_id, pos=pos, flag=flag, seq=seq, qual=qual,
+                                           raw_cigar=raw_cigar, tags=tags))
+    return recs
+
+
+@pytest.fixture(scope="module")
+def edge_bam(tmp_path_factory):
+    p = str(tmp_path_factory.mktemp("bam") / "edge.bam")
+    # small BGZF blocks so records straddle block boundaries
+    synth_bam.write_bam(p, REFS, _random_records(7, 3000), text="@HD\tVN:1.6\n", block=997)
+    return p
+
+
+# ------------------------------------------------------------------ CPU
+def test_oracle_known_answers(tmp_path):
+    p = str(tmp_path / "kat.bam")
+    recs = [
+        # mapped, 5S10M2D3I4M (ref length 16), pos 99 (0-based)
+        synth_bam.record_bytes(name=b"q1", ref_id=1, pos=99, flag=0, cigar=[(5, "S"), (10, "M"), (2, "D"),
+                                                                          (3, "I"), (4, "M")],
+                               seq="ACGTNACGTAACGTAACGTAC", qual=bytes(range(21))),
+        # unmapped, no CIGAR, missing qualities, name "*"
+        synth_bam.record_bytes(name=b"*", ref_id=-1, pos=-1, flag=4, seq="ACGR", qual=None),
+        # empty sequence
+        synth_bam.record_bytes(name=b"e", ref_id=0, pos=0, flag=0, cigar=[(3, "N")], seq="", qual=b""),
+    ]
+    synth_bam.write_bam(p, REFS, recs)
+    n, h, b = (pybam.bam_rows(p, m) for m in MODES)
+    assert n[0] == {"name": "q1", "chrom": "chrX", "start": 100, "end": 115, "flags": 0,
+                    "sequence": "ACGTNACGTAACGTAACGTAC", "quality_scores": bytes(range(33, 54))}
+    assert h[0]["start"] == 100 and h[0]["end"] == 120  # start + seq_len - 1
+    assert b[0]["start"] == 99 and b[0]["end"] == 115  # 0-based, bam_endpos
+    assert n[1]["name"] == "unknown" and h[1]["name"] == "*" and b[1]["name"] == "*"
+    assert n[1]["chrom"] is None and n[1]["start"] is None and n[1]["end"] is None
+    assert b[1]["start"] is None and b[1]["end"] == 0  # bam_endpos(pos -1) = 0 > -1
+    assert h[1]["quality_scores"] is None and n[1]["quality_scores"] == b"\x20" * 4
+    assert n[1]["sequence"] == "ACGN" and b[1]["sequence"] == "ACGR"
+    assert n[2]["sequence"] is None and n[2]["quality_scores"] is None
+    assert n[2]["start"] == 1 and n[2]["end"] == 3 and h[2]["end"] == 0
+    assert pybam.read_bam(p)[0] == ["chr1", "chrX", "contig_��"]
+
+
+def test_bgzf_writer_round_trip(tmp_path):
+    import gzip
+    p = str(tmp_path / "rt.bam")
+    recs = _random_records(1, 200)
+    synth_bam.write_bam(p, REFS, recs, block=333)
+    refs, got = pybam.read_bam(p)
+    assert [r[4:] for r in recs] == got
+    raw = open(p, "rb").read()
+    assert raw.endswith(synth_bam.BGZF_EOF)
+    assert gzip.decompress(raw)[:4] == b"BAM\x01"
+
+
+# ------------------------------------------------------------------ GPU
+def _rows_of(batches, mode):
+    out = []
+    for rb in batches:
+        cols = {n: rb.column(n) for n in rb.schema.names}
+        for n in ("sequence", "quality_scores"):
+            if n in cols:
+                cols[n] = cols[n].view(pa.binary())
+        d = {k: v.to_pylist() for k, v in cols.items()}
+        for i in range(rb.num_rows):
+            out.append({k: d[k][i] for k in d})
+    return out
+
+
+def _expect(rows, include_sequence, include_quality):
+    out = []
+    for r in rows:
+        r = dict(r)
+        if r["sequence"] is not None:
+            r["sequence"] = r["sequence"].encode()
+        if not include_sequence:
+            del r["sequence"]
+        if not include_quality:
+            del r["quality_scores"]
+        out.append(r)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("max_records", [1, 97, 1 << 20])
+def test_gpu_decode_matches_oracle(edge_bam, mode, max_records):
+    from rogtk_amd.bam import BamReader
+    ref = _expect(pybam.bam_rows(edge_bam, mode), True, True)
+    got = []
+    with BamReader(edge_bam, n_threads=4) as r:
+        assert r.reference_names() == ["chr1", "chrX", "contig_��"]
+        while True:
+            rb = r.next_batch(max_records if max_records != 1 else 13 if got else 1, mode)
+            if rb is None:
+                break
+            got += _rows_of([rb], mode)
+    assert len(got) == len(ref)
+    bad = [i for i in range(len(ref)) if got[i] != ref[i]]
+    assert not bad, (bad[:3], got[bad[0]], ref[bad[0]])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inc", [(False, False), (True, False), (False, True)])
+def test_gpu_decode_column_selection(edge_bam, inc):
+    from rogtk_amd.bam import iter_bam_batches
+    ref = _expect(pybam.bam_rows(edge_bam, "htslib"), *inc)
+    got = _rows_of(iter_bam_batches(edge_bam, 500, inc[0], inc[1], mode="htslib"), "htslib")
+    assert got == ref
+
+
+@pytest.mark.gpu
+def test_synth_bam_umis_and_large_batches(tmp_path):
+    from rogtk_amd.bam import iter_bam_batches
+    p = str(tmp_path / "s.bam")
+    codes = synth_bam.synth_bam(p, 60_000, level=1)
+    ref = _expect(pybam.bam_rows(p, "noodles"), True, True)
+    got = _rows_of(iter_bam_batches(p, 50_000, mode="noodles"), "noodles")
+    assert got == ref
+    acgt = "ACGT"
+    umi0 = "".join(acgt[(int(codes[0]) >> (2 * (11 - j))) & 3] for j in range(12))
+    assert got[0]["sequence"][:12].decode() == umi0 and got[0]["name"].endswith("_" + umi0)
+
+
+@pytest.mark.gpu
+def test_converters_write_the_reference_schema(edge_bam, tmp_path):
+    import pyarrow.parquet as pq
+    from rogtk_amd import bam as B
+    ipc = str(tmp_path / "out" / "a.arrow")
+    B.bam_to_arrow_ipc_htslib_optimized(edge_bam, ipc, batch_size=700, limit=2500)
+    with pa.ipc.open_file(ipc) as f:
+        t = f.read_all()
+    assert t.schema == B.bam_schema(True, True)
+    assert t.num_rows == 2500 and max(b.num_rows for b in t.to_batches()) == 700
+    ref = _expect(pybam.bam_rows(edge_bam, "htslib"), True, True)[:2500]
+    assert _rows_of(t.to_batches(), "htslib") == ref
+    pqp = str(tmp_path / "b.parquet")
+    B.bams_to_parquet([edge_bam, edge_bam], pqp, batch_size=1000, include_quality=False, limit=4000,
+                      include_source_file=True)
+    t = pq.read_table(pqp)
+    assert t.schema.names == ["name", "chrom", "start", "end", "flags", "sequence", "source_file"]
+    assert t.num_rows == 4000 and set(t.column("source_file").to_pylist()) == {os.path.basename(edge_bam)}
+    nref = _expect(pybam.bam_rows(edge_bam, "noodles"), True, False)
+    got = _rows_of(t.drop_columns(["source_file"]).to_batches(), "noodles")
+    assert got == (nref + nref)[:4000]
+    B.bam_to_arrow_ipc_htslib_bgzf_blocks(edge_bam, ipc, include_sequence=False)
+    with pa.ipc.open_file(ipc) as f:
+        t = f.read_all()
+    assert _rows_of(t.to_batches(), "htslib_blocks") == _expect(pybam.bam_rows(edge_bam, "htslib_blocks"), False,
+                                                                True)
+
+
+@pytest.mark.gpu
+def test_errors(edge_bam, tmp_path):
+    from rogtk_amd import RogtkError
+    from rogtk_amd import bam as B
+    with pytest.raises(RogtkError, match="BAM file does not exist"):
+        B.bam_to_arrow_ipc(str(tmp_path / "nope.bam"), str(tmp_path / "x.arrow"))
+    with pytest.raises(RogtkError, match="batch_size must be greater than 0"):
+        B.bam_to_parquet(edge_bam, str(tmp_path / "x.parquet"), batch_size=0)
+    raw = open(edge_bam, "rb").read()
+    cut = str(tmp_path / "cut.bam")
+    with open(cut, "wb") as f:
+        f.write(raw[: len(raw) // 2])
+    with pytest.raises(RogtkError, match="truncated"):
+        list(B.iter_bam_batches(cut))
+    notbam = str(tmp_path / "plain.bam")
+    with open(notbam, "wb") as f:
+        f.write(synth_bam.bgzf_compress(b"SAM\x01" + b"\x00" * 64))
+    with pytest.raises(RogtkError, match="bad magic"):
+        list(B.iter_bam_batches(notbam))
