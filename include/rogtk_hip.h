@@ -192,6 +192,12 @@ int rogtk_umi_cluster_host(const void* offsets, int offset_width, const uint8_t*
                            int64_t n, int umi_len, int max_distance, uint32_t* cluster_id,
                            int64_t* n_clusters, int* resolved_umi_len);
 
+/* H3 over a DEVICE column (int64 offsets from 0, values, optional validity bitmap at bit
+ * offset 0), same semantics and ids as rogtk_umi_cluster_host; umi_len >= 1 required.
+ * cluster_id is a device buffer. Enqueued on `stream`; synchronises it once (sizes). */
+int rogtk_umi_cluster_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* validity, int64_t n,
+                          int umi_len, int max_distance, uint32_t* cluster_id, int64_t* n_clusters, void* stream);
+
 /* ================ H4: k-mer spectra of read groups (host buffers) ================
  * Replaces, per polars group (group_by(...).agg), the k-mer front end of fracture
  * assembly: expressions.rs:739-744 (nulls skipped), fracture.rs:200-256 (auto_k via
@@ -334,11 +340,20 @@ int rogtk_bam_header(void* reader, int64_t* n_ref, const int64_t** name_offsets,
  * *n_records = 0 at the end). Sequence / quality columns are skipped (NULL) unless asked. */
 int rogtk_bam_next(void* reader, int64_t max_records, int mode, int include_sequence, int include_quality,
                    int64_t* n_records, rogtk_bam_batch* out);
-/* Same, but the batch stays in DEVICE memory (valid until the next call); the work is
- * enqueued on the reader's stream, returned in *stream (callers order after it). */
+/* Same, but the batch stays in DEVICE memory (valid until the next call). The decode is
+ * enqueued on `stream` (NULL: the reader's own stream, synchronised before return). */
 int rogtk_bam_next_dev(void* reader, int64_t max_records, int mode, int include_sequence, int include_quality,
-                       int64_t* n_records, rogtk_bam_batch* out, void** stream);
+                       int64_t* n_records, rogtk_bam_batch* out, void* stream);
+/* The UMI column of a device batch for the H1-H3 engine (config C5): source 0 = the first
+ * umi_len bases of the sequence, 1 = the read name after its last `sep` byte (UMI-tools
+ * READNAME_<UMI>). Device outputs: int64 offsets (n + 1), values (values_cap bytes;
+ * ROGTK_E_OVERFLOW beyond), validity bitmap (ceil(n/64) u64 words). Synchronises `stream`. */
+int rogtk_bam_umi_dev(const rogtk_bam_batch* batch, int64_t n, int source, int umi_len, int sep, int64_t* offsets,
+                      uint8_t* values, int64_t values_cap, uint8_t* validity, void* stream);
 int rogtk_bam_close(void* reader);
+/* Copies bytes between any two buffers (device or host; hipMemcpyDefault) on `stream`
+ * and synchronises it: lets bindings move device batch columns into their own buffers. */
+int rogtk_copy(void* dst, const void* src, int64_t bytes, void* stream);
 
 /* ============ polars plugin ABI (rogtk_amd/csrc/polars_plugin.cpp) ============
  * librogtk_hip.so also exports the symbols polars resolves for the reference's

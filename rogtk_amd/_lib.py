@@ -83,13 +83,15 @@ SIGNATURES = {
     "rogtk_cluster_release": [_vp],
     "rogtk_cluster_rounds": [_vp, _vp, ctypes.POINTER(ctypes.c_int)],
     "rogtk_cluster_set_spec_rounds": [_i32],
+    "rogtk_umi_cluster_dev": [_vp, _vp, _vp, _i64, _i32, _i32, _vp, ctypes.POINTER(_i64), _vp],
     "rogtk_bam_open": [ctypes.c_char_p, _i32, ctypes.POINTER(_vp)],
     "rogtk_bam_header": [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp),
                          ctypes.POINTER(_i64)],
     "rogtk_bam_next": [_vp, _i64, _i32, _i32, _i32, ctypes.POINTER(_i64), ctypes.POINTER(BamBatch)],
-    "rogtk_bam_next_dev": [_vp, _i64, _i32, _i32, _i32, ctypes.POINTER(_i64), ctypes.POINTER(BamBatch),
-                           ctypes.POINTER(_vp)],
+    "rogtk_bam_next_dev": [_vp, _i64, _i32, _i32, _i32, ctypes.POINTER(_i64), ctypes.POINTER(BamBatch), _vp],
+    "rogtk_bam_umi_dev": [ctypes.POINTER(BamBatch), _i64, _i32, _i32, _i32, _vp, _vp, _i64, _vp, _vp],
     "rogtk_bam_close": [_vp],
+    "rogtk_copy": [_vp, _vp, _i64, _vp],
     "rogtk_plugin_kwargs_debug": [ctypes.c_char_p, _i64, ctypes.c_char_p, _i64, ctypes.POINTER(_i64)],
     "rogtk_umi_complexity_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _P_SCORES],
     "rogtk_hamming_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _u32, _vp, _vp],

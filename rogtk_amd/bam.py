@@ -303,3 +303,127 @@ def bam_to_arrow_ipc_htslib_bgzf_blocks(bam_path, arrow_ipc_path, batch_size=200
     """bam_htslib.rs:507-... (0-based start, bam_endpos end, IUPAC bases)."""
     _convert([bam_path], arrow_ipc_path, "ipc", batch_size, include_sequence, include_quality, limit,
              "htslib_blocks")
+
+
+# ------------------------------------------------- config C5: BAM -> UMI clusters
+UMI_SOURCES = {"sequence": 0, "name": 1}
+
+
+def _next_dev(reader: BamReader, max_records: int, mode: str, include_sequence: bool, stream):
+    b = _lib.BamBatch()
+    n = ctypes.c_int64()
+    _lib.call("rogtk_bam_next_dev", reader._h, int(max_records), MODES[mode], int(bool(include_sequence)), 0,
+              ctypes.byref(n), ctypes.byref(b), ctypes.c_void_p(stream.cuda_stream))
+    return int(n.value), b
+
+
+def bam_umis_dev(bam_path: str, umi_len: int = 12, source: str = "sequence", sep: str = "_",
+                 mode: str = "htslib", n_threads: int = 0, with_names: bool = False):
+    """Decode a BAM file on the GPU and return its UMI column in HBM (torch tensors:
+    int64 offsets [n + 1], uint8 values, int64 validity words), plus the read names
+    (host pyarrow array) when asked. UMI = the first umi_len bases of SEQ ("sequence")
+    or the read name after its last `sep` byte ("name", UMI-tools READNAME_<UMI>)."""
+    import torch
+
+    stream = torch.cuda.current_stream()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    src = UMI_SOURCES[source]
+    offs, vals, valids, counts, names = [], [], [], [], []
+    with BamReader(bam_path, n_threads) as r:
+        while True:
+            n, b = _next_dev(r, DECODE_RECORDS, mode, src == 0, stream)
+            if n == 0:
+                break
+            cap = n * umi_len if src == 0 else max(int(_dev_total(b, 0, n, stream)), 1)
+            off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+            val = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+            vw = torch.empty((n + 63) // 64, dtype=torch.int64, device=dev)
+            _lib.call("rogtk_bam_umi_dev", ctypes.byref(b), n, src, int(umi_len), ord(sep), ctypes.c_void_p(off.data_ptr()),
+                      ctypes.c_void_p(val.data_ptr()), cap, ctypes.c_void_p(vw.data_ptr()),
+                      ctypes.c_void_p(stream.cuda_stream))
+            offs.append(off)
+            vals.append(val[: int(off[-1].item())])
+            valids.append(vw)
+            counts.append(n)
+            if with_names:
+                names.append(_dev_string_to_host(b, 0, n, stream))
+    return _concat_dev(offs, vals, valids, counts, dev), (pa.concat_arrays(names) if with_names and names else None)
+
+
+def _dev_total(b, c, n, stream) -> int:
+    import torch
+    t = torch.empty(1, dtype=torch.int64, device="cuda")
+    _memcpy_dtod(t.data_ptr(), b.offsets[c] + 8 * n, 8, stream)
+    return int(t.item())
+
+
+def _memcpy_dtod(dst: int, src: int, nbytes: int, stream) -> None:
+    _lib.call("rogtk_copy", ctypes.c_void_p(dst), ctypes.c_void_p(src), int(nbytes),
+              ctypes.c_void_p(stream.cuda_stream))
+
+
+def _dev_string_to_host(b, c, n, stream) -> pa.Array:
+    import torch
+    off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    _memcpy_dtod(off.data_ptr(), b.offsets[c], 8 * (n + 1), stream)
+    tot = int(off[-1].item())
+    val = torch.empty(max(tot, 1), dtype=torch.uint8, device="cuda")
+    if tot:
+        _memcpy_dtod(val.data_ptr(), b.values[c], tot, stream)
+    o = off.cpu().numpy()
+    v = val[:tot].cpu().numpy()
+    return pa.Array.from_buffers(pa.large_string(), n, [None, pa.py_buffer(o), pa.py_buffer(v)]).cast(pa.string())
+
+
+def _concat_dev(offs, vals, valids, counts, dev):
+    import torch
+    n = sum(counts)
+    if n == 0:
+        z = torch.zeros(1, dtype=torch.int64, device=dev)
+        return z, torch.zeros(1, dtype=torch.uint8, device=dev), torch.zeros(1, dtype=torch.int64, device=dev), 0
+    if len(offs) == 1:
+        return offs[0], vals[0], valids[0], n
+    base = 0
+    parts = []
+    for o, v in zip(offs, vals):
+        parts.append(o[:-1] + base)
+        base += v.numel()
+    off = torch.cat(parts + [torch.tensor([base], dtype=torch.int64, device=dev)])
+    val = torch.cat(vals)
+    # validity: unpack to bools, concatenate, repack into little-endian words
+    bools = []
+    for w, c in zip(valids, counts):
+        bits = ((w.view(torch.uint8).unsqueeze(1) >> torch.arange(8, device=dev, dtype=torch.uint8)) & 1)
+        bools.append(bits.reshape(-1)[:c])
+    allb = torch.cat(bools)
+    pad = (-allb.numel()) % 64
+    allb = torch.cat([allb, torch.zeros(pad, dtype=torch.uint8, device=dev)]).view(-1, 8)
+    packed = (allb << torch.arange(8, device=dev, dtype=torch.uint8)).sum(1, dtype=torch.uint8)
+    return off, val, packed.view(torch.int64), n
+
+
+def bam_umi_cluster(bam_path: str, umi_len: int = 12, max_distance: int = 1, source: str = "sequence",
+                    sep: str = "_", mode: str = "htslib", n_threads: int = 0) -> pa.Table:
+    """Config C5: BAM -> GPU decode -> UMI column -> H3 cluster ids (and the UMI).
+    Returns a Table {name, umi, cluster_id} with the H3 semantics of umi_cluster
+    (DESIGN.md §4): dense ids, regular UMIs first, irregular ones after, null -> null."""
+    import torch
+
+    (off, val, vw, n), names = bam_umis_dev(bam_path, umi_len, source, sep, mode, n_threads, with_names=True)
+    stream = torch.cuda.current_stream()
+    cid = torch.empty(max(n, 1), dtype=torch.int32, device=off.device)
+    ncl = ctypes.c_int64(0)
+    _lib.call("rogtk_umi_cluster_dev", ctypes.c_void_p(off.data_ptr()), ctypes.c_void_p(val.data_ptr()),
+              ctypes.c_void_p(vw.data_ptr()), n, int(umi_len), int(max_distance), ctypes.c_void_p(cid.data_ptr()),
+              ctypes.byref(ncl), ctypes.c_void_p(stream.cuda_stream))
+    o = off.cpu().numpy()
+    v = val.cpu().numpy()
+    bits = vw.cpu().numpy().view(np.uint8)[: (n + 7) // 8] if n else np.zeros(1, np.uint8)
+    valid = np.unpackbits(bits, bitorder="little")[:n].astype(bool)
+    vbuf = None if valid.all() else pa.py_buffer(np.packbits(valid, bitorder="little"))
+    umi = pa.Array.from_buffers(pa.large_string(), n, [vbuf, pa.py_buffer(o), pa.py_buffer(v)]).cast(pa.string())
+    ids = cid[:n].cpu().numpy().view(np.uint32)
+    cl = pa.Array.from_buffers(pa.uint32(), n, [vbuf, pa.py_buffer(ids.copy())])
+    t = pa.table({"name": names if names is not None else pa.array([], pa.string()), "umi": umi, "cluster_id": cl})
+    t = t.replace_schema_metadata({"n_clusters": str(int(ncl.value))})
+    return t

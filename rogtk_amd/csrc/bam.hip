@@ -295,6 +295,44 @@ __global__ __launch_bounds__(256) void k_bam_fill(const uint8_t* __restrict__ ra
     }
 }
 
+// UMI of each record for the H1-H3 engine: source 0 = the first umi_len bases of the
+// decoded sequence, 1 = the read name after its last `sep` byte (UMI-tools
+// READNAME_<UMI> convention). Null when the sequence is null / the name has no sep.
+__global__ __launch_bounds__(256) void k_umi_len(const int64_t* __restrict__ seq_off, const uint64_t* __restrict__ seq_valid,
+                                                 const int64_t* __restrict__ name_off, const uint8_t* __restrict__ name_val,
+                                                 int64_t n, int source, int umi_len, int sep, int64_t* len,
+                                                 int64_t* start, uint64_t* valid) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool v = false;
+    if (r < n) {
+        int64_t a = 0, l = 0;
+        if (source == 0) {
+            v = !seq_valid || ((seq_valid[r >> 6] >> (r & 63)) & 1);
+            a = seq_off[r];
+            l = v ? min<int64_t>(umi_len, seq_off[r + 1] - a) : 0;
+        } else {
+            const int64_t b = name_off[r], e = name_off[r + 1];
+            int64_t k = e - 1;
+            while (k >= b && name_val[k] != (uint8_t)sep) --k;
+            v = k >= b;
+            a = k + 1;
+            l = v ? e - a : 0;
+        }
+        len[r] = l;
+        start[r] = a;
+    }
+    const uint64_t bits = __ballot(v);
+    if ((threadIdx.x & 63) == 0 && (r >> 6) * 64 < n) valid[r >> 6] = bits;
+}
+
+__global__ __launch_bounds__(256) void k_umi_fill(const uint8_t* __restrict__ src, const int64_t* __restrict__ start,
+                                                  const int64_t* __restrict__ off, int64_t n, uint8_t* __restrict__ out) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const int64_t a = start[r], o = off[r], l = off[r + 1] - o;
+    for (int64_t i = 0; i < l; ++i) out[o + i] = src[a + i];
+}
+
 // ------------------------------------------------------------------ host
 struct PinnedBuf {
     uint8_t* p = nullptr;
@@ -730,11 +768,15 @@ int rogtk_bam_next(void* reader, int64_t max_records, int mode, int include_sequ
 }
 
 int rogtk_bam_next_dev(void* reader, int64_t max_records, int mode, int include_sequence, int include_quality,
-                       int64_t* n_records, rogtk_bam_batch* out, void** stream) {
+                       int64_t* n_records, rogtk_bam_batch* out, void* stream) {
     ROGTK_REQUIRE(reader && n_records && out, ROGTK_E_INVALID, "bam: NULL argument");
     auto* R = static_cast<BamReader*>(reader);
     *n_records = 0;
+    // the batch is decoded on the caller's stream (ordered with what the caller does next)
+    hipStream_t own = R->stream;
+    if (stream) R->stream = reinterpret_cast<hipStream_t>(stream);
     int rc = bam_next_common(R, max_records, mode, include_sequence, include_quality);
+    R->stream = own;
     if (rc != ROGTK_OK) return rc;
     memset(out, 0, sizeof *out);
     for (int c = 0; c < 4; ++c) {
@@ -749,8 +791,52 @@ int rogtk_bam_next_dev(void* reader, int64_t max_records, int mode, int include_
     out->u32[2] = R->d_flags.as<uint32_t>();
     out->u32_validity[0] = R->d_valid[1].as<uint8_t>();
     out->u32_validity[1] = R->d_valid[2].as<uint8_t>();
-    if (stream) *stream = R->stream;
     *n_records = R->n;
+    return ROGTK_OK;
+}
+
+int rogtk_bam_umi_dev(const rogtk_bam_batch* batch, int64_t n, int source, int umi_len, int sep, int64_t* offsets,
+                      uint8_t* values, int64_t values_cap, uint8_t* validity, void* stream) {
+    ROGTK_REQUIRE(batch && offsets && values && validity, ROGTK_E_INVALID, "bam umi: NULL argument");
+    ROGTK_REQUIRE(source == 0 || source == 1, ROGTK_E_INVALID, "bam umi: source must be 0 (sequence) or 1 (name)");
+    ROGTK_REQUIRE(source == 1 || umi_len > 0, ROGTK_E_INVALID, "bam umi: umi_len must be > 0");
+    ROGTK_REQUIRE(source == 1 || batch->offsets[2], ROGTK_E_INVALID, "bam umi: the batch has no sequence column");
+    ROGTK_REQUIRE(n >= 0, ROGTK_E_INVALID, "bam umi: n must be >= 0");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    thread_local DevBuf len, start, cub;
+    if (len.ensure((size_t)(n + 1) * 8) != ROGTK_OK || start.ensure((size_t)(n + 1) * 8) != ROGTK_OK)
+        return ROGTK_E_HIP;
+    if (n > 0) {
+        hipLaunchKernelGGL(k_umi_len, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, batch->offsets[2],
+                           (const uint64_t*)batch->validity[2], batch->offsets[0], batch->values[0], n, source,
+                           umi_len, sep, len.as<int64_t>(), start.as<int64_t>(), (uint64_t*)validity);
+        ROGTK_HIP_CHECK(hipGetLastError());
+    }
+    ROGTK_HIP_CHECK(hipMemsetAsync(len.as<int64_t>() + n, 0, 8, s));
+    size_t tb = 0;
+    ROGTK_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, len.as<int64_t>(), offsets, (int)(n + 1), s));
+    if (cub.ensure(tb) != ROGTK_OK) return ROGTK_E_HIP;
+    ROGTK_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(cub.p, tb, len.as<int64_t>(), offsets, (int)(n + 1), s));
+    int64_t total = 0;
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&total, offsets + n, 8, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    ROGTK_REQUIRE(total <= values_cap, ROGTK_E_OVERFLOW, "bam umi: %lld bytes exceed values_cap %lld",
+                  (long long)total, (long long)values_cap);
+    if (n > 0) {
+        const uint8_t* src = source == 0 ? batch->values[2] : batch->values[0];
+        hipLaunchKernelGGL(k_umi_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, start.as<int64_t>(),
+                           offsets, n, values);
+        ROGTK_HIP_CHECK(hipGetLastError());
+    }
+    return ROGTK_OK;
+}
+
+int rogtk_copy(void* dst, const void* src, int64_t bytes, void* stream) {
+    ROGTK_REQUIRE(bytes >= 0 && (bytes == 0 || (dst && src)), ROGTK_E_INVALID, "copy: bad arguments");
+    if (bytes == 0) return ROGTK_OK;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    ROGTK_HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDefault, s));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
     return ROGTK_OK;
 }
 

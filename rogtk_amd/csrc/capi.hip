@@ -591,6 +591,70 @@ int rogtk_hamming_host(const void* offsets, int offset_width, const uint8_t* val
     return ROGTK_OK;
 }
 
+namespace {
+
+// Longest row of a device column (irregular rows' radix-sort width).
+__global__ void k_max_len(const int64_t* __restrict__ off, int64_t n, unsigned long long* out) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long m = 0;
+    if (r < n) m = (unsigned long long)(off[r + 1] - off[r]);
+    for (int d = 32; d; d >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, d));
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
+}
+
+// H3 over a column already staged into c->codes / regbits / irr (n_irr irregular rows):
+// regular rows through the cluster engine, irregular rows grouped by exact bytes after
+// them; ids into did (device), on stream s.
+int cluster_staged(HostCtx* c, const void* d_offsets, int ow, const uint8_t* d_values, int64_t n, int L,
+                   int64_t n_irr, int64_t max_len, int max_distance, uint32_t* did, int64_t* n_clusters,
+                   hipStream_t s) {
+    int64_t n_reg_clusters = 0;
+    const int64_t* stats_dev = nullptr;
+    if (L >= 1 && L <= kMaxPackedLen) {
+        const int64_t space = (int64_t)1 << std::min(2 * L, 40);
+        const int64_t maxd = std::max<int64_t>(1, std::min<int64_t>(space, n));
+        ClusterLayout cl;
+        if (int rc = cluster_layout(L, maxd, &cl)) return rc;
+        if (c->ws_L != L || c->ws_maxd < cl.max_distinct) {
+            if (int rc = c->ws.ensure((size_t)cl.total)) return rc;
+            if (int rc = rogtk_cluster_init(c->ws.p, L, cl.max_distinct, s)) return rc;
+            c->ws_L = L;
+            c->ws_maxd = cl.max_distinct;
+        }
+        ClusterLayout use;
+        cluster_layout(L, c->ws_maxd, &use);
+        if (int rc = c->bitmap.ensure((size_t)use.words * 8)) return rc;
+        int rc = rogtk_cluster_mark(c->codes.as<uint32_t>(), c->regbits.as<uint64_t>(), n, L, c->ws.p,
+                                    use.max_distinct, s);
+        if (!rc) rc = rogtk_cluster_local_bitmap(c->ws.p, L, use.max_distinct, c->bitmap.as<uint64_t>(), s);
+        if (!rc) rc = rogtk_cluster_resolve(c->ws.p, L, use.max_distinct, c->bitmap.as<uint64_t>(), 1,
+                                            max_distance, s);
+        if (!rc) rc = rogtk_cluster_assign(c->ws.p, L, use.max_distinct, c->codes.as<uint32_t>(),
+                                           c->regbits.as<uint64_t>(), n, did, s);
+        if (rc) {
+            c->ws_L = -1;  // presence may be dirty: re-initialise on the next call
+            return rc;
+        }
+        int64_t st[4];
+        if (int rc2 = rogtk_cluster_stats(c->ws.p, L, use.max_distinct, st, s)) return rc2;
+        ROGTK_REQUIRE(st[2] == 0, ROGTK_E_OVERFLOW, "cluster: distinct UMIs exceeded max_distinct");
+        n_reg_clusters = st[1];
+        stats_dev = (const int64_t*)((uint8_t*)c->ws.p + use.off_stats);
+    } else {
+        ROGTK_HIP_CHECK(hipMemsetAsync(did, 0xFF, (size_t)n * 4, s));
+    }
+    int64_t n_irr_clusters = 0;
+    if (n_irr > 0) {
+        int rc = irregular_cluster(d_offsets, ow, d_values, c->irr.as<int64_t>(), n_irr, max_len, stats_dev, did,
+                                   &n_irr_clusters, s);
+        if (rc) return rc;
+    }
+    if (n_clusters) *n_clusters = n_reg_clusters + n_irr_clusters;
+    return ROGTK_OK;
+}
+
+}  // namespace
+
 int rogtk_umi_cluster_host(const void* offsets, int offset_width, const uint8_t* values,
                            int64_t values_len, const uint8_t* validity, int64_t validity_offset,
                            int64_t n, int umi_len, int max_distance, uint32_t* cluster_id,
@@ -610,52 +674,42 @@ int rogtk_umi_cluster_host(const void* offsets, int offset_width, const uint8_t*
     if (int rc = upload_and_stage(c, h, L, &L, &n_irr)) return rc;
     if (int rc = c->out[0].ensure((size_t)std::max<int64_t>(n, 4) * 4)) return rc;
     uint32_t* did = c->out[0].as<uint32_t>();
-    int64_t n_reg_clusters = 0;
-    const int64_t* stats_dev = nullptr;
-    if (L >= 1 && L <= kMaxPackedLen) {
-        const int64_t space = (int64_t)1 << std::min(2 * L, 40);
-        const int64_t maxd = std::max<int64_t>(1, std::min<int64_t>(space, n));
-        ClusterLayout cl;
-        if (int rc = cluster_layout(L, maxd, &cl)) return rc;
-        if (c->ws_L != L || c->ws_maxd < cl.max_distinct) {
-            if (int rc = c->ws.ensure((size_t)cl.total)) return rc;
-            if (int rc = rogtk_cluster_init(c->ws.p, L, cl.max_distinct, c->stream)) return rc;
-            c->ws_L = L;
-            c->ws_maxd = cl.max_distinct;
-        }
-        ClusterLayout use;
-        cluster_layout(L, c->ws_maxd, &use);
-        if (int rc = c->bitmap.ensure((size_t)use.words * 8)) return rc;
-        int rc = rogtk_cluster_mark(c->codes.as<uint32_t>(), c->regbits.as<uint64_t>(), n, L, c->ws.p,
-                                    use.max_distinct, c->stream);
-        if (!rc) rc = rogtk_cluster_local_bitmap(c->ws.p, L, use.max_distinct, c->bitmap.as<uint64_t>(), c->stream);
-        if (!rc) rc = rogtk_cluster_resolve(c->ws.p, L, use.max_distinct, c->bitmap.as<uint64_t>(), 1,
-                                            max_distance, c->stream);
-        if (!rc) rc = rogtk_cluster_assign(c->ws.p, L, use.max_distinct, c->codes.as<uint32_t>(),
-                                           c->regbits.as<uint64_t>(), n, did, c->stream);
-        if (rc) {
-            c->ws_L = -1;  // presence may be dirty: re-initialise on the next call
-            return rc;
-        }
-        int64_t st[4];
-        if (int rc2 = rogtk_cluster_stats(c->ws.p, L, use.max_distinct, st, c->stream)) return rc2;
-        ROGTK_REQUIRE(st[2] == 0, ROGTK_E_OVERFLOW, "cluster: distinct UMIs exceeded max_distinct");
-        n_reg_clusters = st[1];
-        stats_dev = (const int64_t*)((uint8_t*)c->ws.p + use.off_stats);
-    } else {
-        ROGTK_HIP_CHECK(hipMemsetAsync(did, 0xFF, (size_t)n * 4, c->stream));
-    }
-    int64_t n_irr_clusters = 0;
-    if (n_irr > 0) {
-        int rc = irregular_cluster(c->offsets.p, offset_width, c->values.as<uint8_t>(),
-                                   c->irr.as<int64_t>(), n_irr, h.max_len(), stats_dev, did,
-                                   &n_irr_clusters, c->stream);
-        if (rc) return rc;
-    }
+    if (int rc = cluster_staged(c, c->offsets.p, offset_width, c->values.as<uint8_t>(), n, L, n_irr,
+                                n_irr ? h.max_len() : 0, max_distance, did, n_clusters, c->stream))
+        return rc;
     ROGTK_HIP_CHECK(hipMemcpyAsync(cluster_id, did, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
     ROGTK_HIP_CHECK(hipStreamSynchronize(c->stream));
-    if (n_clusters) *n_clusters = n_reg_clusters + n_irr_clusters;
     return ROGTK_OK;
+}
+
+int rogtk_umi_cluster_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* validity, int64_t n,
+                          int umi_len, int max_distance, uint32_t* cluster_id, int64_t* n_clusters, void* stream) {
+    ROGTK_REQUIRE(n >= 0 && (n == 0 || (offsets && values && cluster_id)), ROGTK_E_INVALID,
+                  "umi_cluster_dev: NULL argument");
+    ROGTK_REQUIRE(umi_len >= 1, ROGTK_E_INVALID, "umi_cluster_dev: umi_len must be >= 1");
+    ROGTK_REQUIRE(max_distance == 0 || max_distance == 1, ROGTK_E_UNSUPPORTED,
+                  "max_distance %d: only 0 and 1 are supported", max_distance);
+    if (n_clusters) *n_clusters = 0;
+    if (n == 0) return ROGTK_OK;
+    hipStream_t s = as_stream(stream);
+    HostCtx* c;
+    if (int rc = host_ctx(&c)) return rc;
+    const int64_t words = (n + 63) / 64;
+    if (c->codes.ensure((size_t)std::max<int64_t>(n, 4) * 4) != ROGTK_OK ||
+        c->regbits.ensure((size_t)std::max<int64_t>(words, 1) * 8) != ROGTK_OK ||
+        c->irr.ensure((size_t)std::max<int64_t>(n, 1) * 8) != ROGTK_OK || c->nirr.ensure(16) != ROGTK_OK)
+        return ROGTK_E_HIP;
+    ROGTK_HIP_CHECK(hipMemsetAsync(c->nirr.p, 0, 16, s));
+    if (int rc = launch_stage(offsets, 8, values, validity, 0, n, umi_len, c->codes.as<uint32_t>(),
+                              c->regbits.as<uint64_t>(), c->irr.as<int64_t>(), c->nirr.as<unsigned long long>(), s))
+        return rc;
+    hipLaunchKernelGGL(k_max_len, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, offsets, n,
+                       c->nirr.as<unsigned long long>() + 1);
+    ROGTK_HIP_CHECK(hipGetLastError());
+    int64_t hv[2];
+    ROGTK_HIP_CHECK(hipMemcpyAsync(hv, c->nirr.p, 16, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    return cluster_staged(c, offsets, 8, values, n, umi_len, hv[0], hv[1], max_distance, cluster_id, n_clusters, s);
 }
 
 // --------------------------------------------------------------- profiling

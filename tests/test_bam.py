@@ -220,3 +220,47 @@ def test_errors(edge_bam, tmp_path):
         f.write(synth_bam.bgzf_compress(b"SAM\x01" + b"\x00" * 64))
     with pytest.raises(RogtkError, match="bad magic"):
         list(B.iter_bam_batches(notbam))
+
+
+def _oracle_umis(rows, source, umi_len, sep="_"):
+    out = []
+    for r in rows:
+        if source == "sequence":
+            s = r["sequence"]
+            out.append(None if s is None else s[:umi_len].encode())
+        else:
+            nm = r["name"].encode()
+            k = nm.rfind(sep.encode())
+            out.append(None if k < 0 else nm[k + 1:])
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("source", ["sequence", "name"])
+@pytest.mark.parametrize("md", [0, 1])
+def test_bam_umi_cluster_matches_oracle(tmp_path, monkeypatch, source, md):
+    from oracle import pyoracle as P
+    from rogtk_amd import bam as B
+    p = str(tmp_path / "c5.bam")
+    synth_bam.synth_bam(p, 30_000, level=1)
+    # a few irregular UMIs (N in the UMI, short reads, names without the separator)
+    extra = [synth_bam.record_bytes(name=b"x_ACGNACGTACGT", seq="ACGNACGTACGTAAAA", qual=None),
+             synth_bam.record_bytes(name=b"noumi", seq="ACG", qual=b"\x01\x02\x03"),
+             synth_bam.record_bytes(name=b"y_ACGTACGTAC", seq="", qual=b"")]
+    raw = open(p, "rb").read()
+    import gzip
+    body = gzip.decompress(raw)
+    with open(p, "wb") as f:
+        f.write(synth_bam.bgzf_compress(body + b"".join(extra), level=1))
+    monkeypatch.setattr(B, "DECODE_RECORDS", 7_000)  # several device batches
+    t = B.bam_umi_cluster(p, umi_len=12, max_distance=md, source=source, mode="htslib")
+    rows = pybam.bam_rows(p, "htslib")
+    umis = _oracle_umis(rows, source, 12)
+    assert t.column("umi").to_pylist() == [None if u is None else u.decode() for u in umis]
+    rc, rv, rk, _ = P.umi_cluster(P.StrCol.from_list(umis), 12, md)
+    got = t.column("cluster_id").to_numpy(zero_copy_only=False)
+    valid = np.array([u is not None for u in umis])
+    assert int(t.schema.metadata[b"n_clusters"]) == rk
+    assert np.array_equal(np.asarray(t.column("cluster_id").is_valid()), valid)
+    assert np.array_equal(got[rv].astype(np.uint32), rc[rv])
+    assert t.column("name").to_pylist() == [r["name"] for r in rows]
