@@ -351,6 +351,9 @@ int rogtk_bam_next_dev(void* reader, int64_t max_records, int mode, int include_
 int rogtk_bam_umi_dev(const rogtk_bam_batch* batch, int64_t n, int source, int umi_len, int sep, int64_t* offsets,
                       uint8_t* values, int64_t values_cap, uint8_t* validity, void* stream);
 int rogtk_bam_close(void* reader);
+/* Diagnostics: seconds spent so far in {file read, buffer moves + block framing, BGZF
+ * inflate, record framing, H2D + GPU decode, D2H of host batches}. */
+int rogtk_bam_timers(void* reader, double* out6);
 /* Copies bytes between any two buffers (device or host; hipMemcpyDefault) on `stream`
  * and synchronises it: lets bindings move device batch columns into their own buffers. */
 int rogtk_copy(void* dst, const void* src, int64_t bytes, void* stream);

@@ -111,3 +111,44 @@ def record_row(b: bytes, refs: List[str], mode: str) -> Dict[str, Optional[objec
 def bam_rows(path: str, mode: str) -> List[dict]:
     refs, recs = read_bam(path)
     return [record_row(r, refs, mode) for r in recs]
+
+
+_FNV0, _FNVP = 1469598103934665603, 1099511628211
+_COLS = ("name", "chrom", "start", "end", "flags", "sequence", "quality_scores")
+
+
+def _fnv(h: int, data: bytes) -> int:
+    for x in data:
+        h = ((h ^ x) * _FNVP) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def rows_digest(rows) -> list:
+    """The per-column FNV-1a digests oracle_bam_digest (oracle/bam_oracle.cpp) computes."""
+    d = [_FNV0] * 7
+    for r in rows:
+        for c, k in enumerate(_COLS):
+            v = r[k]
+            if k == "flags":
+                d[c] = _fnv(d[c], struct.pack("<I", v))
+                continue
+            if v is None:
+                d[c] = _fnv(d[c], b"\xff")
+                continue
+            if isinstance(v, int):
+                v = struct.pack("<I", v)
+            elif isinstance(v, str):
+                v = v.encode()
+            d[c] = _fnv(_fnv(d[c], v), b"\x01")
+    return d
+
+
+def cpp_digest(path: str, mode: str):
+    """(record count, 7 column digests) from the C++ restatement (single core)."""
+    import ctypes
+    import numpy as np
+    from . import pyoracle
+    out = np.zeros(7, dtype=np.uint64)
+    n = pyoracle.lib().oracle_bam_digest(path.encode(), {"noodles": 0, "htslib": 1, "htslib_blocks": 2}[mode],
+                                         ctypes.c_void_p(out.ctypes.data))
+    return int(n), [int(x) for x in out]

@@ -60,6 +60,8 @@ def lib():
         L.oracle_kmer_spectrum.restype = i64
         L.oracle_kmer_observations.argtypes = [vp, i32, i64, i64, i32]
         L.oracle_kmer_observations.restype = i64
+        L.oracle_bam_digest.argtypes = [ctypes.c_char_p, i32, vp]
+        L.oracle_bam_digest.restype = i64
         _lib = L
     return _lib
 

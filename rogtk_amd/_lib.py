@@ -91,6 +91,7 @@ SIGNATURES = {
     "rogtk_bam_next_dev": [_vp, _i64, _i32, _i32, _i32, ctypes.POINTER(_i64), ctypes.POINTER(BamBatch), _vp],
     "rogtk_bam_umi_dev": [ctypes.POINTER(BamBatch), _i64, _i32, _i32, _i32, _vp, _vp, _i64, _vp, _vp],
     "rogtk_bam_close": [_vp],
+    "rogtk_bam_timers": [_vp, _vp],
     "rogtk_copy": [_vp, _vp, _i64, _vp],
     "rogtk_plugin_kwargs_debug": [ctypes.c_char_p, _i64, ctypes.c_char_p, _i64, ctypes.POINTER(_i64)],
     "rogtk_umi_complexity_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _P_SCORES],

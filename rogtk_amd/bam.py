@@ -98,6 +98,12 @@ class BamReader:
         except Exception:
             pass
 
+    def timers(self) -> dict:
+        """Seconds spent per stage so far (rogtk_bam_timers)."""
+        t = (ctypes.c_double * 6)()
+        _lib.call("rogtk_bam_timers", self._h, t)
+        return dict(zip(("read", "move_frame_blocks", "inflate", "frame_records", "h2d_decode", "d2h"), list(t)))
+
     def reference_names(self) -> List[str]:
         n = ctypes.c_int64()
         off, val, txt = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()

@@ -25,9 +25,11 @@
 #include <zlib.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -353,7 +355,17 @@ struct PinnedBuf {
     }
 };
 
+inline double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// One cached pinned stream buffer, handed from a closed reader to the next one opened
+// (page-locking hundreds of MB costs more than decoding them).
+std::mutex g_pin_mu;
+PinnedBuf g_pin_cache;
+
 struct Bgzf {
+    double t_read = 0, t_inflate = 0, t_move = 0;  // diagnostics (rogtk_bam_timers)
     FILE* f = nullptr;
     int threads = 1;
     bool file_eof = false;
@@ -368,12 +380,14 @@ struct Bgzf {
     bool more(size_t keep_from, size_t chunk = 32u << 20) {
         if (!err.empty()) return false;
         // read compressed bytes
+        double t0 = now_s();
         if (!file_eof) {
             if (comp.size() < comp_len + chunk) comp.resize(comp_len + chunk);
             const size_t got = fread(comp.data() + comp_len, 1, chunk, f);
             comp_len += got;
             if (got < chunk) file_eof = true;
         }
+        t_read += now_s() - t0;
         // frame whole BGZF blocks
         struct Blk {
             size_t c0, clen, out;
@@ -416,26 +430,30 @@ struct Bgzf {
             if (file_eof && comp_len > 0) err = "truncated BGZF block at end of file";
             return false;
         }
-        // make room: move [keep_from, end) to the front
-        const size_t keep = end - keep_from;
-        PinnedBuf nb;
-        const size_t need = keep + total;
-        if (need > buf.cap || keep_from > 0) {
+        // make room. Append in place while the buffer has space; otherwise move the
+        // bytes still needed ([keep_from, end)) to the front, growing the buffer
+        // geometrically if they do not fit (one move per batch in steady state).
+        if (end + total > buf.cap) {
+            const size_t keep = end - keep_from;
+            const size_t need = keep + total;
             if (need > buf.cap) {
-                if (nb.ensure(need) != ROGTK_OK) {
+                PinnedBuf nb;
+                if (nb.ensure(std::max(need, 2 * buf.cap)) != ROGTK_OK) {
                     err = "pinned host allocation failed";
                     return false;
                 }
                 if (keep) memcpy(nb.p, buf.p + keep_from, keep);
                 std::swap(buf.p, nb.p);
                 std::swap(buf.cap, nb.cap);
-            } else if (keep) {
+            } else if (keep && keep_from) {
                 memmove(buf.p, buf.p + keep_from, keep);
             }
             pos -= keep_from;
             end = keep;
         }
         // inflate blocks in parallel
+        const double t1 = now_s();
+        t_move += t1 - t0;
         std::atomic<size_t> next{0};
         std::atomic<bool> bad{false};
         uint8_t* dst = buf.p + end;
@@ -467,6 +485,7 @@ struct Bgzf {
             err = "BGZF inflate failed (corrupt deflate stream)";
             return false;
         }
+        t_inflate += now_s() - t1;
         end += total;
         // keep the partial trailing block
         memmove(comp.data(), comp.data() + o, comp_len - o);
@@ -483,6 +502,7 @@ struct Bgzf {
 
 struct BamReader {
     Bgzf z;
+    double t_frame = 0, t_decode = 0, t_d2h = 0;
     std::string text;
     std::vector<int64_t> ref_off{0};
     std::vector<uint8_t> ref_val;
@@ -497,6 +517,13 @@ struct BamReader {
     PinnedBuf h_off[4], h_val[4], h_valid[5], h_u32[3];
     ~BamReader() {
         if (z.f) fclose(z.f);
+        {
+            std::lock_guard<std::mutex> lk(g_pin_mu);
+            if (z.buf.cap > g_pin_cache.cap) {
+                std::swap(z.buf.p, g_pin_cache.p);
+                std::swap(z.buf.cap, g_pin_cache.cap);
+            }
+        }
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -604,6 +631,7 @@ int decode_batch(BamReader* R, int mode, int include_seq, int include_qual) {
     fo.bad = R->d_bad.as<unsigned long long>();
     const int32_t n_ref = (int32_t)R->ref_off.size() - 1;
     if (n > 0) {
+        ProfScope prof(K_BAM_FIELDS, s);
         const dim3 g((unsigned)((n + 255) / 256));
         if (mode == ROGTK_BAM_NOODLES)
             hipLaunchKernelGGL(k_bam_fields<ROGTK_BAM_NOODLES>, g, dim3(256), 0, s, R->d_raw.as<uint8_t>(),
@@ -618,6 +646,7 @@ int decode_batch(BamReader* R, int mode, int include_seq, int include_qual) {
     }
     // exclusive scans of the four length columns (n + 1 entries: the last is the total)
     for (int c = 0; c < 4; ++c) {
+        ProfScope prof_scan(K_BAM_SCAN, s);
         ROGTK_HIP_CHECK(hipMemsetAsync(R->d_len[c].as<int64_t>() + n, 0, 8, s));
         size_t tb = 0;
         ROGTK_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, R->d_len[c].as<int64_t>(),
@@ -647,6 +676,7 @@ int decode_batch(BamReader* R, int mode, int include_seq, int include_qual) {
     fi.include_seq = include_seq;
     fi.include_qual = include_qual;
     if (n > 0) {
+        ProfScope prof(K_BAM_FILL, s);
         const dim3 g((unsigned)((n * 64 + 255) / 256));
         if (mode == ROGTK_BAM_NOODLES)
             hipLaunchKernelGGL(k_bam_fill<ROGTK_BAM_NOODLES>, g, dim3(256), 0, s, R->d_raw.as<uint8_t>(),
@@ -680,6 +710,11 @@ int rogtk_bam_open(const char* path, int n_threads, void** reader) {
     std::unique_ptr<BamReader> R(new BamReader());
     R->z.f = fopen(path, "rb");
     ROGTK_REQUIRE(R->z.f, ROGTK_E_INVALID, "Failed to open BAM file '%s'", path);
+    {
+        std::lock_guard<std::mutex> lk(g_pin_mu);
+        std::swap(R->z.buf.p, g_pin_cache.p);
+        std::swap(R->z.buf.cap, g_pin_cache.cap);
+    }
     R->z.threads = n_threads > 0 ? n_threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     ROGTK_HIP_CHECK(hipGetDevice(&R->device));
     ROGTK_HIP_CHECK(hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking));
@@ -714,9 +749,15 @@ static int bam_next_common(BamReader* R, int64_t max_records, int mode, int incl
     // release the previous batch's bytes
     R->z.pos += R->n ? (size_t)R->roff[R->n] : 0;
     R->n = 0;
+    const double t0 = now_s();
+    const double in0 = R->z.t_read + R->z.t_inflate + R->z.t_move;
     int rc = frame_batch(R, max_records);
+    const double t1 = now_s();
+    R->t_frame += (t1 - t0) - (R->z.t_read + R->z.t_inflate + R->z.t_move - in0);
     if (rc != ROGTK_OK) return rc;
-    return decode_batch(R, mode, include_sequence, include_quality);
+    rc = decode_batch(R, mode, include_sequence, include_quality);
+    R->t_decode += now_s() - t1;
+    return rc;
 }
 
 int rogtk_bam_next(void* reader, int64_t max_records, int mode, int include_sequence, int include_quality,
@@ -730,6 +771,7 @@ int rogtk_bam_next(void* reader, int64_t max_records, int mode, int include_sequ
     hipStream_t s = R->stream;
     memset(out, 0, sizeof *out);
     const int64_t words = (n + 63) / 64;
+    const double td = now_s();
     for (int c = 0; c < 4; ++c) {
         if ((c == 2 && !include_sequence) || (c == 3 && !include_quality)) continue;
         int64_t tot = 0;
@@ -763,6 +805,7 @@ int rogtk_bam_next(void* reader, int64_t max_records, int mode, int include_sequ
     out->u32_validity[1] = R->h_valid[2].p;
     out->u32_validity[2] = nullptr;
     ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    R->t_d2h += now_s() - td;
     *n_records = n;
     return ROGTK_OK;
 }
@@ -837,6 +880,14 @@ int rogtk_copy(void* dst, const void* src, int64_t bytes, void* stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     ROGTK_HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDefault, s));
     ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    return ROGTK_OK;
+}
+
+int rogtk_bam_timers(void* reader, double* out6) {
+    ROGTK_REQUIRE(reader && out6, ROGTK_E_INVALID, "bam: NULL argument");
+    auto* R = static_cast<BamReader*>(reader);
+    const double t[6] = {R->z.t_read, R->z.t_move - R->z.t_read, R->z.t_inflate, R->t_frame, R->t_decode, R->t_d2h};
+    memcpy(out6, t, sizeof t);
     return ROGTK_OK;
 }
 

@@ -35,7 +35,8 @@ void set_error(const char* fmt, ...) {
 const char* const kKernelNames[K_COUNT_] = {
     "stage",          "score_packed",   "score_rows",    "cluster_mark",
     "cluster_bitmap", "cluster_scan",   "cluster_compact", "cluster_union",
-    "cluster_flatten", "cluster_label", "cluster_assign", "cluster_irregular"};
+    "cluster_flatten", "cluster_label", "cluster_assign", "cluster_irregular",
+    "bam_fields",     "bam_scan",       "bam_fill"};
 
 namespace {
 std::atomic<bool> g_prof{false};

@@ -46,6 +46,9 @@ enum KernelId {
     K_LABEL,
     K_ASSIGN,
     K_IRREGULAR,
+    K_BAM_FIELDS,
+    K_BAM_SCAN,
+    K_BAM_FILL,
     K_COUNT_
 };
 extern const char* const kKernelNames[K_COUNT_];

@@ -264,3 +264,12 @@ def test_bam_umi_cluster_matches_oracle(tmp_path, monkeypatch, source, md):
     assert np.array_equal(np.asarray(t.column("cluster_id").is_valid()), valid)
     assert np.array_equal(got[rv].astype(np.uint32), rc[rv])
     assert t.column("name").to_pylist() == [r["name"] for r in rows]
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_cpp_restatement_matches_python_oracle(edge_bam, mode):
+    """The single-core C++ restatement (CPU baseline of C5) = the Python oracle."""
+    rows = pybam.bam_rows(edge_bam, mode)
+    n, d = pybam.cpp_digest(edge_bam, mode)
+    assert n == len(rows)
+    assert d == pybam.rows_digest(rows)

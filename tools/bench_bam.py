@@ -1,0 +1,140 @@
+"""Config C5 measurement: BAM -> Arrow columns (GPU record decode) and BAM -> UMI clusters.
+
+  python tools/bench_bam.py [--reads N] [--threads T] [--mode htslib]
+
+Writes a synthetic BAM (rogtk_amd.synth_bam: 150-bp mapped reads, READNAME_<UMI> names,
+synth-v1 UMIs as the first 12 bases, zlib level 6 BGZF) to /tmp, then measures:
+
+* decode: rogtk_bam_next_dev over the file (host BGZF inflate on T threads + framing,
+  H2D of the raw records, k_bam_fields / scan / k_bam_fill) -> records/s, and the decode
+  kernels' HBM roofline from their algorithmic bytes (raw record bytes read + column
+  bytes written) over their HIP-event time;
+* convert: bam_to_arrow_ipc_htslib_optimized (the reference's production converter)
+  end to end, columns copied back to host and written as Arrow IPC;
+* C5: bam_umi_cluster (decode + UMI column + H3 Hamming<=1 ids) end to end;
+* CPU baseline: oracle/bam_oracle.cpp (single core, gzread + the reference's record
+  loop) over the same file.
+Prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=4_000_000)
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--mode", default="htslib")
+    ap.add_argument("--path", default="/tmp/rogtk_c5.bam")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--decode-only", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    import rogtk_amd  # noqa: F401
+    from rogtk_amd import bam as B
+    from rogtk_amd import device as D
+    from rogtk_amd import synth_bam
+
+    t0 = time.perf_counter()
+    synth_bam.synth_bam(args.path, args.reads, level=6, threads=args.threads)
+    gen_s = time.perf_counter() - t0
+    fsize = os.path.getsize(args.path)
+    n = args.reads
+    read_len, umi_len = 150, 12
+    name_len = 1 + 9 + 1 + umi_len
+    rec_bytes = 4 + 32 + (name_len + 1) + 4 + read_len // 2 + read_len
+    chrom_avg = 4.6  # "chr1".."chr24"
+    out_bytes = name_len + chrom_avg + 2 * read_len + 4 * 8 + 3 * 4 + 5 / 8  # values + offsets + u32 + validity
+    algo_per_rec = rec_bytes + out_bytes
+
+    torch.cuda.init()
+    stream = torch.cuda.current_stream()
+
+    def decode_pass(profile: bool):
+        D.profile_enable(profile)
+        D.profile_reset()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        got = 0
+        with B.BamReader(args.path, args.threads) as r:
+            while True:
+                k, _ = B._next_dev(r, B.DECODE_RECORDS, args.mode, True, stream)
+                if k == 0:
+                    break
+                got += k
+            stages = {k: round(v, 4) for k, v in r.timers().items()}
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t
+        ks = {}
+        for name in ("bam_fields", "bam_scan", "bam_fill"):
+            ms, launches = D.profile_read(name)
+            ks[name] = {"ms": round(ms, 3), "launches": launches}
+        D.profile_enable(False)
+        assert got == n, (got, n)
+        ks["host_stages_s"] = stages
+        return wall, ks
+
+    decode_pass(False)  # warm the page cache and the allocators
+    wall, ks = decode_pass(True)
+    kern_ms = sum(v["ms"] for k, v in ks.items() if k.startswith("bam_"))
+    achieved = n * algo_per_rec / (kern_ms / 1e3) / 1e9 if kern_ms else None
+    fill_ms = ks["bam_fill"]["ms"]
+
+    if args.decode_only:
+        print(json.dumps({"decode_wall_s": wall, "records_per_s": n / wall, "kernels": ks}))
+        return
+    t = time.perf_counter()
+    B.bam_to_arrow_ipc_htslib_optimized(args.path, "/tmp/rogtk_c5.arrow")
+    conv_s = time.perf_counter() - t
+
+    t = time.perf_counter()
+    tab = B.bam_umi_cluster(args.path, umi_len=umi_len, max_distance=1, source="sequence", mode=args.mode,
+                            n_threads=args.threads)
+    c5_s = time.perf_counter() - t
+    assert tab.num_rows == n
+
+    cpu = None
+    if not args.no_cpu_baseline:
+        from oracle import pybam
+        t = time.perf_counter()
+        m, _ = pybam.cpp_digest(args.path, args.mode)
+        cpu_s = time.perf_counter() - t
+        assert m == n
+        cpu = {"value": n / cpu_s, "unit": "records/s", "cores": 1, "kind": "port",
+               "sample": f"all {n} records: oracle/bam_oracle.cpp (gzread + the reference's record loop, "
+                         f"{args.mode} semantics), {cpu_s:.1f} s on 1 host core"}
+
+    out = {
+        "metric": "BAM records/s -> Arrow columns (GPU decode) and -> UMI clusters (config C5)",
+        "n_records": n, "file_bytes": fsize, "uncompressed_record_bytes": n * rec_bytes, "threads": args.threads,
+        "mode": args.mode, "gen_s": round(gen_s, 2),
+        "decode": {"records_per_s": n / wall, "wall_s": round(wall, 3),
+                   "uncompressed_GBps": n * rec_bytes / wall / 1e9, "kernels": ks},
+        "roofline": {"kernel": "k_bam_fields + scan + k_bam_fill", "bound": "hbm", "achieved": achieved,
+                     "peak": 8000.0, "unit": "GB/s",
+                     "frac": (achieved / 8000.0) if achieved else None,
+                     "bytes_per_record": round(algo_per_rec, 1),
+                     "fill_GBps": n * (name_len + 1 + 75 + 150 + name_len + chrom_avg + 300) / (fill_ms / 1e3) / 1e9
+                     if fill_ms else None},
+        "convert_ipc": {"records_per_s": n / conv_s, "wall_s": round(conv_s, 3),
+                        "function": "bam_to_arrow_ipc_htslib_optimized (columns D2H + Arrow IPC write)"},
+        "c5_umi_cluster": {"records_per_s": n / c5_s, "wall_s": round(c5_s, 3),
+                           "n_clusters": int(tab.schema.metadata[b"n_clusters"])},
+        "cpu_baseline": cpu,
+        "cores_available": os.cpu_count(),
+    }
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
