@@ -614,21 +614,34 @@ __device__ __forceinline__ bool hook_roots(HookTable& T, uint32_t* f, const uint
 // whose codes share one root (UR) need one f load instead of one per code; when
 // every word of a group is uniform, the <= 6 word pairs that share a bit are the
 // only hooks.
+//
+// Frontier: a group whose members already share one root never crosses again (roots
+// only merge), so round k > 0 visits only the groups that crossed in round k - 1.
+// active holds two generations of one bit per task (written whole by ballots).
 __global__ __launch_bounds__(kBlock) void k_hook_g(const uint4* __restrict__ RT, const uint32_t* __restrict__ UR,
                                                    int64_t words, int L, int p0, uint32_t* f,
-                                                   unsigned int* __restrict__ flags, int round) {
+                                                   unsigned int* __restrict__ flags, int round,
+                                                   uint64_t* __restrict__ active, int64_t active_words) {
     if (round > 0 && flags[round - 1] == 0) return;  // converged earlier
+    const int64_t per = words >> 2;
+    const int64_t tasks = (int64_t)(L - p0) * per;
+    const int64_t u = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t* prev = active + (int64_t)((round - 1) & 1) * active_words;
+    uint64_t* next = active + (int64_t)(round & 1) * active_words;
+    const bool act = per > 0 && u < tasks && (round == 0 || ((prev[u >> 6] >> (u & 63)) & 1ull));
+    if (!__syncthreads_or(act)) {
+        if ((threadIdx.x & 63) == 0 && (u >> 6) < active_words) next[u >> 6] = 0;
+        return;
+    }
     __shared__ HookTable T;
     for (int k = threadIdx.x; k < kHookSlots; k += kBlock) {
         T.key[k] = kNone;
         T.val[k] = kNone;
     }
     __syncthreads();
-    const int64_t per = words >> 2;
-    const int64_t u = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     uint32_t last_x = kNone, last_mn = kNone;
     bool crossed = false;
-    if (per > 0 && u < (int64_t)(L - p0) * per) {
+    if (act) {
         const int p = p0 + (int)(u / per);
         const int64_t g = u % per;
         const int s2 = 2 * p - 6;
@@ -681,7 +694,11 @@ __global__ __launch_bounds__(kBlock) void k_hook_g(const uint4* __restrict__ RT,
             }
         }
     }
-    if (__any(crossed) && (threadIdx.x & 63) == 0) flags[round] = 1u;
+    const uint64_t crossed_bits = __ballot(crossed);
+    if ((threadIdx.x & 63) == 0) {
+        if ((u >> 6) < active_words) next[u >> 6] = crossed_bits;
+        if (crossed_bits) flags[round] = 1u;
+    }
     __syncthreads();
     for (int k = threadIdx.x; k < kHookSlots; k += kBlock) {
         const uint32_t x = T.key[k];
@@ -843,6 +860,7 @@ struct WsPtrs {
     uint32_t *wpref, *blksum, *blkoff, *D, *f, *UR;
     uint64_t *rbits, *lroot;
     uint32_t *rpref, *rblksum, *rblkoff, *labelcode, *ilab;
+    uint64_t* active;
 };
 
 inline WsPtrs ws_ptrs(const ClusterLayout& cl, uint8_t* ws) {
@@ -865,6 +883,7 @@ inline WsPtrs ws_ptrs(const ClusterLayout& cl, uint8_t* ws) {
     p.rblkoff = (uint32_t*)(ws + cl.off_rblkoff);
     p.labelcode = cl.label_by_code ? (uint32_t*)(ws + cl.off_labelcode) : nullptr;
     p.ilab = cl.label_by_code ? nullptr : (uint32_t*)(ws + cl.off_ilab);
+    p.active = (uint64_t*)(ws + cl.off_active);
     return p;
 }
 
@@ -910,6 +929,10 @@ int cluster_layout(int L, int64_t max_distinct, ClusterLayout* o) {
     c.off_rblkoff = take((c.rblocks + 1) * 4);
     c.off_labelcode = c.label_by_code ? take((int64_t)c.nbits * 4) : off;
     c.off_ilab = c.label_by_code ? off : take(max_distinct * 4);
+    // hook-round frontier: one bit per (position, word group) task, two generations
+    const int64_t tasks = L > kLocalPos ? (int64_t)(L - kLocalPos) * (c.words >> 2) : 0;
+    c.active_words = (tasks + 63) / 64;
+    c.off_active = take(2 * std::max<int64_t>(c.active_words, 1) * 8);
     c.total = off;
     *o = c;
     return ROGTK_OK;
@@ -999,7 +1022,7 @@ int enqueue_rounds(const ClusterLayout& cl, const WsPtrs& p, int from, int to, h
     const int64_t tasks = (int64_t)(cl.L - kLocalPos) * (cl.words >> 2);
     for (int k = from; k < to; ++k) {
         hipLaunchKernelGGL(k_hook_g, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words, cl.L,
-                           kLocalPos, p.f, p.flags, k);
+                           kLocalPos, p.f, p.flags, k, p.active, cl.active_words);
         hipLaunchKernelGGL(k_jump, dim3(pg), dim3(kBlock), 0, s, p.f, p.lroot, cl.max_distinct, p.stats, p.flags, k);
     }
     ROGTK_HIP_CHECK(hipGetLastError());
