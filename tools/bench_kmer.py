@@ -40,6 +40,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--global-only", action="store_true", help="route every group through the radix-sort path")
+    ap.add_argument("--group-batch-rows", type=int, default=10_000_000,
+                    help="k-mer spectra run over consecutive groups of at most this many rows per call "
+                         "(bounds the output capacity: 19 B x (read_len - 3) per row)")
     args = ap.parse_args()
     n, RL, L = args.reads, args.read_len, 12
     dev = torch.device("cuda", 0)
@@ -55,11 +58,13 @@ def main():
     batch = D.PackedBatch(codes, L)
     eng = D.ClusterEngine(L, min(n, 4 ** L), dev)
     cid = torch.empty(n, dtype=torch.int32, device=dev)
-    cap = n * max(0, RL - 3)
+    br = min(n, args.group_batch_rows)
+    cap = br * max(0, RL - 3)
     _lib.call("rogtk_kmer_set_path", 0 if args.global_only else 1)
     ev = lambda: torch.cuda.Event(enable_timing=True)
     phases = {"cluster": 0.0, "group_by": 0.0, "kmer": 0.0}
     out = None
+    path_groups = [0, 0]
 
     def step(record):
         nonlocal out
@@ -69,7 +74,27 @@ def main():
         e1.record()
         rows, go, G = D.group_by_key(cid)
         e2.record()
-        out = D.kmer_spectrum_dev(offsets, reads, go, args.k, args.min_coverage, cap, rows=rows)
+        path_groups[:] = [0, 0]
+        # consecutive groups of <= br rows per spectrum call (a group is never split)
+        goh = go.cpu().numpy()
+        cuts = [0]
+        while cuts[-1] < G:
+            g0 = cuts[-1]
+            g1 = int(np.searchsorted(goh, goh[g0] + br, side="right")) - 1
+            cuts.append(min(G, max(g1, g0 + 1)))
+        valid, stats = 0, []
+        for g0, g1 in zip(cuts, cuts[1:]):
+            a, b = int(goh[g0]), int(goh[g1])
+            r = D.kmer_spectrum_dev(offsets, reads, go[g0:g1 + 1] - a, args.k, args.min_coverage, cap,
+                                    rows=rows[a:b])
+            valid += int(r["entry_offsets"][-1].item())
+            stats.append(r["stats"])
+            del r  # the next call reuses the output capacity (torch caching allocator)
+            ps = (ctypes.c_int64 * 2)()
+            _lib.call("rogtk_kmer_path_stats", ps)
+            path_groups[0] += ps[0]
+            path_groups[1] += ps[1]
+        out = {"n_calls": len(cuts) - 1, "valid": valid, "stats": torch.cat(stats)}
         e3.record()
         torch.cuda.synchronize()
         if record:
@@ -86,8 +111,7 @@ def main():
         G = step(True)
     torch.cuda.synchronize()
     el = time.perf_counter() - t
-    paths = (ctypes.c_int64 * 2)()
-    _lib.call("rogtk_kmer_path_stats", paths)
+    paths = path_groups
     st = out["stats"].cpu().numpy()
     line = {
         "metric": "reads/s UMI group_by + k-mer spectra (C3 front end), 150 bp reads, 12 bp UMI, 1 MI355X",
@@ -96,7 +120,7 @@ def main():
         "config": {"workload": "C3: H3 exact UMI ids -> group_by -> k-mer spectra per group",
                    "reads": n, "read_len": RL, "umi_len": L, "k": args.k, "k_eff": int(st[:, 0].max()),
                    "min_coverage": args.min_coverage, "groups": G, "lds_groups": paths[0],
-                   "global_groups": paths[1], "valid_kmers": int(out["entry_offsets"][-1].item()),
+                   "global_groups": paths[1], "valid_kmers": out["valid"], "spectrum_calls": out["n_calls"],
                    "sequences": int(st[:, 1].sum())},
         "phases_ms": {k: round(v / args.steps, 3) for k, v in phases.items()},
         "observations_per_s": round(n * (RL - int(st[:, 0].max()) + 1) * args.steps / el, 1),
