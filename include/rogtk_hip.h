@@ -308,6 +308,18 @@ int rogtk_fastq_pair_close(void* reader);
 
 /* ============================== profiling ================================ */
 /* When enabled, every kernel launch is bracketed by HIP events on its stream. */
+/* ======== multi-GPU exchange of read groups ========
+ * Packs the rows of a DEVICE string column (int64 offsets from 0, values) by
+ * destination rank dest[i] in [0, world) so that each destination's rows are one
+ * contiguous byte range for a single all-to-all (torch.distributed / RCCL does the
+ * exchange): perm[n] = rows ordered by destination (stable), packed_offsets[n + 1] /
+ * packed_values (values_cap bytes; ROGTK_E_OVERFLOW beyond) the column in perm order.
+ * counts[world] / byte_counts[world] are HOST arrays (rows / bytes per destination).
+ * Synchronises `stream` once (the counts). */
+int rogtk_route_pack(const int64_t* offsets, const uint8_t* values, const int32_t* dest, int64_t n, int world,
+                     int64_t* perm, int64_t* counts, int64_t* byte_counts, int64_t* packed_offsets,
+                     uint8_t* packed_values, int64_t values_cap, void* stream);
+
 /* ============ BAM -> Arrow columns, decoded on the GPU ============
  * Host: BGZF inflate (zlib, blocks in parallel on n_threads threads, <= 0: min(16, cores))
  * and record framing. GPU: every per-record field (rogtk_amd/csrc/bam.hip). Columns

@@ -86,3 +86,83 @@ def test_sharded_exchange_matches_single_process(world, md):
         assert k == rk
         got[start:start + len(ids)] = ids
     assert np.array_equal(got, ref)
+
+
+def _route_worker(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import pyoracle as P
+        from rogtk_amd import dist as RD
+        reads, keys = _route_data()
+        start, count = RD.shard_range(len(reads), rank, world)
+        mine = reads[start:start + count]
+        off = torch.tensor(np.concatenate([[0], np.cumsum([len(r) for r in mine])]), dtype=torch.int64)
+        vals = torch.tensor(np.frombuffer(b"".join(mine), np.uint8).copy())
+        k = torch.tensor(keys[start:start + count], dtype=torch.int32)
+        o, v, rk, srank, srow = RD.route_rows(off, vals, k)
+        o, v, rk = o.numpy(), v.numpy().tobytes(), rk.numpy()
+        got = [v[o[i]:o[i + 1]] for i in range(len(rk))]
+        # every key this rank received is owned here, with all of its rows, in source order
+        owned = {int(x) for x in rk}
+        dest = RD.route_destination(torch.tensor(keys, dtype=torch.int32), world).numpy()
+        assert owned == {int(x) for x in np.asarray(keys)[dest == rank]}
+        src_global = [RD.shard_range(len(reads), int(q), world)[0] + int(r) for q, r in zip(srank, srow)]
+        assert [reads[g] for g in src_global] == got
+        assert [keys[g] for g in src_global] == rk.tolist()
+        # per-group k-mer spectra of the owned groups (the work each rank then does alone)
+        order = np.argsort(rk, kind="stable")
+        gk, go = np.unique(rk[order], return_index=True)
+        go = np.concatenate([go, [len(rk)]]).astype(np.int64)
+        spec = P.kmer_spectrum(P.StrCol.from_list([got[i] for i in order]), 17, 2, False, go)
+        out_q.put((rank, gk.tolist(), {f: spec[f].tolist() for f in ("kmer_lo", "exts", "counts")},
+                   spec["group_offsets"].tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _route_data():
+    rng = np.random.default_rng(5)
+    reads, keys = [], []
+    for g in range(120):
+        tpl = bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), 120))
+        for _ in range(int(rng.integers(1, 12))):
+            a = int(rng.integers(0, 40))
+            reads.append(tpl[a:a + int(rng.integers(40, 80))])
+            keys.append(int(g * 7919 % 100003))
+    perm = rng.permutation(len(reads))
+    return [reads[i] for i in perm], [keys[i] for i in perm]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_route_rows_colocates_groups(world):
+    """H4 exchange: after one all-to-all every group lives on exactly one
+    rank, and the per-group spectra computed there equal the single-process spectra."""
+    from oracle import pyoracle as P
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_route_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    reads, keys = _route_data()
+    keys = np.asarray(keys)
+    order = np.argsort(keys, kind="stable")
+    gk, go = np.unique(keys[order], return_index=True)
+    go = np.concatenate([go, [len(keys)]]).astype(np.int64)
+    ref = P.kmer_spectrum(P.StrCol.from_list([reads[i] for i in order]), 17, 2, False, go)
+    eo = ref["group_offsets"]
+    seen = set()
+    for rank, rgk, spec, reo in results:
+        for j, key in enumerate(rgk):
+            assert key not in seen
+            seen.add(key)
+            g = int(np.searchsorted(gk, key))
+            for f in ("kmer_lo", "exts", "counts"):
+                assert spec[f][reo[j]:reo[j + 1]] == ref[f][eo[g]:eo[g + 1]].tolist(), (key, f)
+    assert seen == set(gk.tolist())
