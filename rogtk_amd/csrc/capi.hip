@@ -606,9 +606,11 @@ __global__ void k_max_len(const int64_t* __restrict__ off, int64_t n, unsigned l
 // H3 over a column already staged into c->codes / regbits / irr (n_irr irregular rows):
 // regular rows through the cluster engine, irregular rows grouped by exact bytes after
 // them; ids into did (device), on stream s.
-int cluster_staged(HostCtx* c, const void* d_offsets, int ow, const uint8_t* d_values, int64_t n, int L,
-                   int64_t n_irr, int64_t max_len, int max_distance, uint32_t* did, int64_t* n_clusters,
-                   hipStream_t s) {
+int cluster_staged(HostCtx* c, const void* d_offsets, int ow, const uint8_t* d_values, const uint8_t* d_validity,
+                   int64_t voff, int64_t n, int L, int64_t n_irr, int64_t max_len, int max_distance, uint32_t* did,
+                   int64_t* n_clusters, hipStream_t s) {
+    if (L > kMaxPackedLen && L <= 32)  // long UMIs: sort-based engine (regular + irregular rows)
+        return long_cluster(d_offsets, ow, d_values, d_validity, voff, n, L, max_distance, max_len, did, n_clusters, s);
     int64_t n_reg_clusters = 0;
     const int64_t* stats_dev = nullptr;
     if (L >= 1 && L <= kMaxPackedLen) {
@@ -675,8 +677,10 @@ int rogtk_umi_cluster_host(const void* offsets, int offset_width, const uint8_t*
     if (int rc = upload_and_stage(c, h, L, &L, &n_irr)) return rc;
     if (int rc = c->out[0].ensure((size_t)std::max<int64_t>(n, 4) * 4)) return rc;
     uint32_t* did = c->out[0].as<uint32_t>();
-    if (int rc = cluster_staged(c, c->offsets.p, offset_width, c->values.as<uint8_t>(), n, L, n_irr,
-                                n_irr ? h.max_len() : 0, max_distance, did, n_clusters, c->stream))
+    if (int rc = cluster_staged(c, c->offsets.p, offset_width, c->values.as<uint8_t>(),
+                                h.validity ? c->validity.as<uint8_t>() : nullptr, h.voff, n, L, n_irr,
+                                (n_irr || (L > kMaxPackedLen && L <= 32)) ? h.max_len() : 0, max_distance, did,
+                                n_clusters, c->stream))
         return rc;
     ROGTK_HIP_CHECK(hipMemcpyAsync(cluster_id, did, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
     ROGTK_HIP_CHECK(hipStreamSynchronize(c->stream));
@@ -710,7 +714,8 @@ int rogtk_umi_cluster_dev(const int64_t* offsets, const uint8_t* values, const u
     int64_t hv[2];
     ROGTK_HIP_CHECK(hipMemcpyAsync(hv, c->nirr.p, 16, hipMemcpyDeviceToHost, s));
     ROGTK_HIP_CHECK(hipStreamSynchronize(s));
-    return cluster_staged(c, offsets, 8, values, n, umi_len, hv[0], hv[1], max_distance, cluster_id, n_clusters, s);
+    return cluster_staged(c, offsets, 8, values, validity, 0, n, umi_len, hv[0], hv[1], max_distance, cluster_id,
+                          n_clusters, s);
 }
 
 // --------------------------------------------------------------- profiling

@@ -190,4 +190,10 @@ int irregular_cluster(const void* offsets, int offset_width, const uint8_t* valu
                       const int64_t* rows, int64_t n_rows, int64_t max_len, const int64_t* stats_dev,
                       uint32_t* cluster_id, int64_t* n_irregular_clusters, hipStream_t s);
 
+// H3 for 17 <= L <= 32 (sort-based, long_cluster.hip): regular + irregular rows of a
+// device column; ids into cid (device), *n_clusters on the host. Synchronises s.
+int long_cluster(const void* offsets, int ow, const uint8_t* values, const uint8_t* validity, int64_t voff,
+                 int64_t n, int L, int max_distance, int64_t max_len, uint32_t* cid, int64_t* n_clusters,
+                 hipStream_t s);
+
 }  // namespace rogtk

@@ -40,7 +40,7 @@ def edge_cases():
     e = [None, b"", b"A", b"AC", b"ACG", b"NNNN", b"acgt", b"ACGTN", "ACGTéACGTAC".encode(),
          "日本語ACGTAC".encode(), b"ACGTACGTACGTA", b"ACGTACGTACG"]
     for L in (63, 64, 65, 80, 150, 300):
-        e.append(bytes(rng.choice(list(b"ACGT"), size=L)))
+        e.append(rng.choice(list(b"ACGT"), size=L).astype(np.uint8).tobytes())
         e.append(b"ACGTTT" * (L // 6) + b"A" * (L % 6))
     e.append(b"A" * 150)
     e.append(b"AC" * 75)

@@ -131,7 +131,7 @@ def _random_strings(rng, n, lengths, alphabet=b"ACGT"):
     out = []
     for _ in range(n):
         L = int(rng.choice(lengths))
-        out.append(bytes(rng.choice(list(alphabet), size=L)))
+        out.append(rng.choice(list(alphabet), size=L).astype(np.uint8).tobytes())
     return out
 
 
@@ -190,10 +190,11 @@ def test_hamming_targets(rg, target, maxd):
     assert np.array_equal(gw[valid].astype(bool), rw[valid])
 
 
-@pytest.mark.parametrize("L", [1, 2, 3, 5, 8, 12, 13, 14, 16])
+@pytest.mark.parametrize("L", [1, 2, 3, 5, 8, 12, 13, 14, 16, 17, 20, 24, 31, 32])
 @pytest.mark.parametrize("md", [0, 1])
 def test_cluster_lengths(rg, L, md):
-    """Dense-table sizes from 4 codes up to 4^16 (label-by-code for L<=13, by index above)."""
+    """Dense-table sizes from 4 codes up to 4^16 (label-by-code for L<=13, by index above);
+    17..32: the sort-based long-UMI engine (long_cluster.hip)."""
     rng = np.random.default_rng(100 + L)
     n = 20000
     if L <= 6:
@@ -214,6 +215,48 @@ def test_cluster_lengths(rg, L, md):
     assert rl == L and k == rk
     g = _np(got)
     assert np.array_equal(g[rv].astype(np.uint32), rc[rv])
+
+
+@pytest.mark.parametrize("L", [18, 32])
+def test_long_cluster_bruteforce_and_chains(rg, L):
+    """Long UMIs vs the O(d^2) brute force, with Hamming-1 chains that cross every
+    position (many union rounds) and irregular / null rows mixed in."""
+    rng = np.random.default_rng(L)
+    umis = []
+    for c in range(30):  # chains: each step changes one random position
+        u = bytearray(_random_strings(rng, 1, [L])[0])
+        for _ in range(int(rng.integers(2, 40))):
+            j = int(rng.integers(L))
+            u[j] = b"ACGT"[(b"ACGT".index(u[j]) + int(rng.integers(1, 4))) % 4]
+            umis.append(bytes(u))
+    umis += _random_strings(rng, 800, [L])
+    umis += [None, b"N" * L, b"ACGT", b"acgt" * (L // 4), b"A" * (L + 1)]
+    order = rng.permutation(len(umis))
+    umis = [umis[i] for i in order]
+    ref, rk = P().py_cluster_bruteforce(umis, L, 1)
+    got, k, _ = rg.umi_cluster(pa.array(umis, type=pa.large_binary()), L, 1)
+    assert k == rk
+    assert got.to_pylist() == ref
+
+
+def test_cluster_dev_matches_host_long_and_short(rg):
+    """rogtk_umi_cluster_dev (device column) == rogtk_umi_cluster_host, both engines."""
+    import ctypes
+    import torch
+    from rogtk_amd import _lib
+    rng = np.random.default_rng(77)
+    for L in (12, 20):
+        umis = _random_strings(rng, 5000, [L]) + [b"N" * L, b"ACG", b""]
+        host, k, _ = rg.umi_cluster(pa.array(umis, type=pa.large_binary()), L, 1)
+        off = torch.tensor(np.concatenate([[0], np.cumsum([len(u) for u in umis])]), dtype=torch.int64).cuda()
+        val = torch.tensor(np.frombuffer(b"".join(umis), np.uint8).copy()).cuda()
+        cid = torch.empty(len(umis), dtype=torch.int32, device="cuda")
+        nk = ctypes.c_int64(0)
+        _lib.call("rogtk_umi_cluster_dev", ctypes.c_void_p(off.data_ptr()), ctypes.c_void_p(val.data_ptr()), None,
+                  len(umis), L, 1, ctypes.c_void_p(cid.data_ptr()), ctypes.byref(nk),
+                  ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        assert nk.value == k
+        assert np.array_equal(cid.cpu().numpy().view(np.uint32), _np(host).astype(np.uint32))
 
 
 def test_cluster_bruteforce_small(rg):
