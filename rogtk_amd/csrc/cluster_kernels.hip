@@ -812,12 +812,16 @@ __global__ __launch_bounds__(kBlock) void k_label(const uint32_t* __restrict__ f
 }
 
 // MODE 0: labelcode[code]; MODE 1: flab[rank(code)] (labels by index, ilab).
+// wlab (max_distance 1 only, else NULL): the label of every word whose codes share one
+// root, 4 B per 64 codes (1 MB at L = 12, L2-resident): most rows resolve there and only
+// the others gather from the 4^L-entry table.
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ codes,
                                                    const uint64_t* __restrict__ regbits, int64_t n,
                                                    const uint32_t* __restrict__ labelcode,
                                                    const uint32_t* __restrict__ flab,
-                                                   const uint4* __restrict__ RT, uint32_t* __restrict__ out) {
+                                                   const uint4* __restrict__ RT, const uint32_t* __restrict__ wlab,
+                                                   uint32_t* __restrict__ out) {
     const int64_t row0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
     if (row0 >= n) return;
     const bool full = row0 + 4 <= n;
@@ -834,7 +838,10 @@ __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ 
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         id[k] = 0xFFFFFFFFu;
-        if ((reg >> k) & 1u) id[k] = MODE == 0 ? labelcode[c[k]] : flab[rt_rank(RT[c[k] >> 6], c[k])];
+        if ((reg >> k) & 1u) {
+            const uint32_t wl = wlab ? wlab[c[k] >> 6] : kNone;
+            id[k] = wl != kNone ? wl : MODE == 0 ? labelcode[c[k]] : flab[rt_rank(RT[c[k] >> 6], c[k])];
+        }
     }
     if (full) {
         *reinterpret_cast<uint4*>(out + row0) = make_uint4(id[0], id[1], id[2], id[3]);
@@ -1012,6 +1019,7 @@ struct ResolveState {
     int launched = 0;
     bool pending = false;
     int rounds = 0;  // hook rounds the last resolve needed (the converged round included)
+    bool word_labels = false;  // wpref holds word labels (max_distance 1)
     ClusterLayout cl{};
 };
 std::mutex g_rs_mu;
@@ -1070,6 +1078,7 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
     st.pending = false;
     st.rounds = 0;
     st.cl = cl;
+    st.word_labels = max_distance == 1;
     {
         ProfScope prof(K_SCAN, s);
         hipLaunchKernelGGL(k_scan_words, dim3((unsigned)cl.blocks), dim3(kBlock), 0, s, bitmaps,
@@ -1180,14 +1189,21 @@ int launch_cluster_assign(const ClusterLayout& cl, const uint8_t* ws, const uint
     if (int rc = cluster_finish(ws, s)) return rc;
     if (n <= 0) return ROGTK_OK;
     WsPtrs p = ws_ptrs(cl, const_cast<uint8_t*>(ws));
+    bool wl = false;
+    {
+        std::lock_guard<std::mutex> lk(g_rs_mu);
+        auto it = g_rs.find(ws);
+        wl = it != g_rs.end() && it->second.word_labels;
+    }
+    const uint32_t* wlab = wl ? p.wpref : nullptr;
     ProfScope prof(K_ASSIGN, s);
     const int g = grid_for((n + 3) / 4);
     if (cl.label_by_code)
         hipLaunchKernelGGL(k_assign<0>, dim3(g), dim3(kBlock), 0, s, codes, regular_bits, n, p.labelcode, p.D,
-                           p.RT, cluster_id);
+                           p.RT, wlab, cluster_id);
     else
         hipLaunchKernelGGL(k_assign<1>, dim3(g), dim3(kBlock), 0, s, codes, regular_bits, n, p.labelcode, p.ilab,
-                           p.RT, cluster_id);
+                           p.RT, wlab, cluster_id);
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
 }

@@ -10,7 +10,7 @@ for n in [int(x) for x in os.environ.get("NS", "10000000,80000000").split(",")]:
     eng = D.ClusterEngine(L, min(n, 4**L), "cuda")
     eng.mark(batch); bm = eng.build_local_bitmap().clone()
     cid = torch.empty(n, dtype=torch.int32, device="cuda")
-    for md in (1, 0):
+    for md in [int(x) for x in os.environ.get("MDS", "1,0").split(",")]:
         eng.resolve(bm, 1, md); torch.cuda.synchronize()
         D.profile_reset(); D.profile_enable(True)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
