@@ -166,6 +166,10 @@ int rogtk_cluster_rounds(const void* ws, void* stream, int* rounds);
  * (1..64; 0 restores the default of 4). Process-wide. Fewer rounds never change
  * results: the rest run when assign / stats find the flags not yet converged. */
 int rogtk_cluster_set_spec_rounds(int n);
+/* Global phase of max_distance 1 (positions 7..L-1), process-wide: 2 = bulk-synchronous
+ * hook + jump rounds with speculative launch and deferred completion (default; 0
+ * restores it), 1 = one-pass lock-free CAS union-find. Identical results. */
+int rogtk_cluster_set_global_mode(int mode);
 /* Releases the host-side resolve state kept for ws (call before freeing ws). */
 int rogtk_cluster_release(const void* ws);
 

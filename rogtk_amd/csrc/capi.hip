@@ -486,6 +486,7 @@ int rogtk_cluster_rounds(const void* ws, void* stream, int* rounds) {
 }
 
 int rogtk_cluster_set_spec_rounds(int n) { return cluster_set_spec_rounds(n); }
+int rogtk_cluster_set_global_mode(int mode) { return cluster_set_global_mode(mode); }
 
 int rogtk_cluster_release(const void* ws) {
     if (ws) cluster_release(ws);

@@ -733,6 +733,132 @@ __global__ __launch_bounds__(kBlock) void k_jump(uint32_t* f, const uint64_t* __
     }
 }
 
+// ------------------------------------------------- global CC, one-pass union-find
+// The same word-group clique sweep as k_hook_g, but every clique is merged at once
+// with a lock-free union-find over f (CAS link of the larger root under the smaller,
+// intermediate pointer jumping in find). After one pass every cross-tile edge has
+// both ends in one tree, so no rounds, no convergence flags and no host check.
+// Invariant: f[x] <= x, f[x] == x only at roots; path jumping writes an ancestor,
+// links happen only by CAS on a root, so trees stay acyclic and a component's root
+// is its smallest vertex (the label the rounds variant converges to).
+// Loads of f bypass the non-coherent vector L1 (agent-scope atomics): a stale read
+// only ever yields an ancestor, and a failed CAS returns the current parent.
+__device__ __forceinline__ uint32_t uf_ld(const uint32_t* p) {
+#ifdef ROGTK_UF_COHERENT
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    return *p;  // may be stale in L1: only ever an ancestor
+#endif
+}
+
+__device__ __forceinline__ uint32_t uf_find(uint32_t* f, uint32_t x) {
+    uint32_t r = uf_ld(f + x);
+    if (r == x) return x;
+    uint32_t prev = x, next;
+    while (r != (next = uf_ld(f + r))) {
+        __hip_atomic_store(f + prev, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        prev = r;
+        r = next;
+    }
+    return r;
+}
+
+__device__ __forceinline__ void uf_union(uint32_t* f, uint32_t a, uint32_t b) {
+    a = uf_find(f, a);
+    b = uf_find(f, b);
+    while (a != b) {
+        if (a > b) {
+            const uint32_t t = a;
+            a = b;
+            b = t;
+        }
+        const uint32_t old = atomicCAS(f + b, b, a);  // link root b under a < b
+        if (old == b) return;
+        b = uf_find(f, old);  // b was linked meanwhile: continue from its new root
+        a = uf_find(f, a);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_union_g(const uint4* __restrict__ RT, const uint32_t* __restrict__ UR,
+                                                    int64_t words, int L, int p0, uint32_t* f) {
+    const int64_t per = words >> 2;
+    const int64_t tasks = (int64_t)(L - p0) * per;
+    const int64_t u = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (per == 0 || u >= tasks) return;
+    const int p = p0 + (int)(u / per);
+    const int64_t g = u % per;
+    const int s2 = 2 * p - 6;
+    const int64_t stride = 1ll << s2;
+    const int64_t w0 = ((g >> s2) << (s2 + 2)) | (g & (stride - 1));
+    uint4 e[4];
+    uint64_t m[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        e[v] = RT[w0 + v * stride];
+        m[v] = rt_word(e[v]);
+    }
+    const uint64_t multi = multi_of4(m[0], m[1], m[2], m[3]);
+    if (!multi) return;
+    uint32_t ur[4];
+    bool all_uniform = true;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        ur[v] = kNone;
+        if (m[v] & multi) {
+            ur[v] = UR[w0 + v * stride];
+            all_uniform &= ur[v] != kNone;
+        }
+    }
+    if (all_uniform) {
+        // whole words: the <= 6 word pairs that share a bit are the only links; find
+        // each member's root once and union only pairs whose roots differ
+        uint32_t r[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) r[v] = (m[v] & multi) ? uf_find(f, ur[v]) : kNone;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = a + 1; b < 4; ++b)
+                if ((m[a] & m[b]) && r[a] != r[b]) {
+                    uf_union(f, r[a], r[b]);
+                    r[a] = r[b] = uf_find(f, r[a] < r[b] ? r[a] : r[b]);
+                }
+        return;
+    }
+    uint64_t mm = multi;
+    while (mm) {
+        const int b = __ffsll((long long)mm) - 1;
+        mm &= mm - 1;
+        const uint64_t below = (1ull << b) - 1ull;
+        uint32_t x0 = kNone;
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+            if ((m[v] >> b) & 1ull) {
+                const uint32_t x = ur[v] != kNone ? ur[v] : e[v].z + (uint32_t)__popcll(m[v] & below);
+                if (x0 == kNone) x0 = x;
+                else uf_union(f, x0, x);
+            }
+    }
+}
+
+// Flatten after the union pass: every live vertex points at its root (stars).
+__global__ __launch_bounds__(kBlock) void k_flatten_live(uint32_t* f, const uint64_t* __restrict__ lroot,
+                                                         int64_t max_distinct,
+                                                         const unsigned long long* __restrict__ stats) {
+    const int64_t nd = live_distinct(stats, max_distinct);
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
+    for (int64_t w = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; w * 64 < nd; w += nwaves) {
+        const uint64_t lr = lroot[w];
+        const int64_t i = w * 64 + lane;
+        if (!((lr >> lane) & 1ull) || i >= nd) continue;
+        uint32_t r = f[i];
+        if (r == (uint32_t)i) continue;
+        for (uint32_t q = f[r]; q != r; q = f[r]) r = q;
+        f[i] = r;
+    }
+}
+
 // Global roots (live vertices i with f[i] == i: only local roots can be) -> rbits over
 // index space; their dense order is the label order.
 __global__ __launch_bounds__(kBlock) void k_roots(const uint32_t* __restrict__ f, const uint64_t* __restrict__ lroot,
@@ -1008,6 +1134,14 @@ namespace {
 
 constexpr int kSpecRounds = 4;  // speculative global rounds (synth-v1 needs 3-4)
 std::atomic<int> g_spec_rounds{kSpecRounds};
+// global phase of max_distance 1: bulk-synchronous hook + jump rounds (default) or a
+// one-pass lock-free union-find. Measured on MI355X at 10M synth-v1 reads (1.08M
+// distinct, a few giant components): rounds 115 us of kernels, union-find 194 us
+// (CAS retries and dependent find chains on the hot roots; the rounds' LDS hook
+// table deduplicates them). Both are exact and give identical ids.
+[[maybe_unused]] constexpr int kGlobalUnionFind = 1;
+constexpr int kGlobalRounds = 2;
+std::atomic<int> g_global_mode{kGlobalRounds};
 
 // Host-side state of an in-flight resolve, keyed by workspace: the round flags are
 // copied asynchronously to pinned host memory so resolve never blocks the host;
@@ -1106,7 +1240,16 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
         hipLaunchKernelGGL(k_local_cc, dim3((unsigned)lblocks), dim3(kBlock), 0, s, p.RT, cl.words, cl.L,
                            p.f, p.D, p.UR, p.lroot, cl.rwords, cl.max_distinct, p.stats);
         ROGTK_HIP_CHECK(hipGetLastError());
-        if (cl.L > kLocalPos) {
+        if (cl.L > kLocalPos && g_global_mode.load() != kGlobalRounds) {
+            // one-pass union-find: exact when the stream reaches the labels
+            const int64_t tasks = (int64_t)(cl.L - kLocalPos) * (cl.words >> 2);
+            hipLaunchKernelGGL(k_union_g, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words, cl.L,
+                               kLocalPos, p.f);
+            hipLaunchKernelGGL(k_flatten_live, dim3(grid_for(cl.max_distinct, kPersistentGrid)), dim3(kBlock), 0, s,
+                               p.f, p.lroot, cl.max_distinct, p.stats);
+            ROGTK_HIP_CHECK(hipGetLastError());
+            st.rounds = 1;
+        } else if (cl.L > kLocalPos) {
             const int spec = g_spec_rounds.load();
             if (int rc = enqueue_rounds(cl, p, 0, spec, s)) return rc;
             if (!st.ev) {
@@ -1160,6 +1303,13 @@ int cluster_finish(const void* ws, hipStream_t s) {
 int cluster_set_spec_rounds(int n) {
     ROGTK_REQUIRE(n >= 0 && n <= kMaxRounds, ROGTK_E_INVALID, "spec rounds %d outside 0..%d", n, kMaxRounds);
     g_spec_rounds.store(n == 0 ? kSpecRounds : n);
+    return ROGTK_OK;
+}
+
+int cluster_set_global_mode(int mode) {
+    ROGTK_REQUIRE(mode >= 0 && mode <= kGlobalRounds, ROGTK_E_INVALID, "global mode %d outside 0..%d", mode,
+                  kGlobalRounds);
+    g_global_mode.store(mode == 0 ? kGlobalRounds : mode);
     return ROGTK_OK;
 }
 

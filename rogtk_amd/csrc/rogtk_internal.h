@@ -180,6 +180,7 @@ int cluster_finish(const void* ws, hipStream_t s);
 void cluster_release(const void* ws);
 int cluster_rounds(const void* ws, hipStream_t s, int* rounds);
 int cluster_set_spec_rounds(int n);
+int cluster_set_global_mode(int mode);
 int launch_cluster_assign(const ClusterLayout& cl, const uint8_t* ws, const uint32_t* codes,
                           const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id,
                           hipStream_t s);

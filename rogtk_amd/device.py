@@ -173,6 +173,15 @@ def set_spec_rounds(n: int) -> None:
     _lib.call("rogtk_cluster_set_spec_rounds", int(n))
 
 
+GLOBAL_UNION_FIND, GLOBAL_ROUNDS = 1, 2
+
+
+def set_global_mode(mode: int) -> None:
+    """Global CC phase: 2 = hook + jump rounds, speculative + deferred (default, 0 restores
+    it), 1 = one-pass CAS union-find; both give identical ids."""
+    _lib.call("rogtk_cluster_set_global_mode", int(mode))
+
+
 def cluster_batch(engine: ClusterEngine, batch: PackedBatch, cluster_id: torch.Tensor,
                   max_distance: int = 1, group=None, marked: bool = False, stream=None) -> None:
     """mark -> local bitmap -> (all-gather over ranks) -> resolve -> assign."""

@@ -461,11 +461,13 @@ def test_deferred_rounds_match(rg, L, spec):
     eng = D.ClusterEngine(L, n, "cuda")
     cid = torch.empty(n, dtype=torch.int32, device="cuda")
     try:
+        D.set_global_mode(D.GLOBAL_ROUNDS)
         D.set_spec_rounds(spec)
         D.cluster_batch(eng, batch, cid, 1)
         rounds = eng.rounds()
     finally:
         D.set_spec_rounds(0)
+        D.set_global_mode(0)
     if spec == 1:
         assert rounds > spec  # the deferred path ran
     rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L)), L, 1)
@@ -473,10 +475,12 @@ def test_deferred_rounds_match(rg, L, spec):
     assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc)
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("L", [12, 16])
-def test_long_chains_need_extra_rounds(rg, L):
-    """Long Hamming-1 paths (diameter >> speculative rounds) resolve exactly: the deferred
-    completion in assign must finish them."""
+def test_long_chains_need_extra_rounds(rg, L, mode):
+    """Long Hamming-1 paths (diameter >> speculative rounds) resolve exactly: the one-pass
+    union-find (mode 1) links them at once; with rounds (mode 2) the deferred completion in
+    assign must finish them."""
     import torch
 
     from rogtk_amd import device as D
@@ -491,11 +495,46 @@ def test_long_chains_need_extra_rounds(rg, L):
     batch = D.PackedBatch(codes, L)
     eng = D.ClusterEngine(L, n, "cuda")
     cid = torch.empty(n, dtype=torch.int32, device="cuda")
-    D.cluster_batch(eng, batch, cid, 1)
-    stats = eng.stats()
-    rounds = eng.rounds()
-    print(f"L={L} n={n} rounds={rounds}")
+    try:
+        D.set_global_mode(mode)
+        D.cluster_batch(eng, batch, cid, 1)
+        stats = eng.stats()
+        rounds = eng.rounds()
+    finally:
+        D.set_global_mode(0)
+    print(f"L={L} n={n} mode={mode} rounds={rounds}")
     rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L)), L, 1)
     assert stats["n_clusters"] == rk
     assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc)
     assert rounds >= 1
+
+
+@pytest.mark.parametrize("n", [1_000_000, 6_000_000])
+@pytest.mark.parametrize("L", [10, 12, 14])
+def test_global_modes_identical(rg, L, n):
+    """Union-find (default) and hook + jump rounds give bit-identical ids on dense and
+    sparse code spaces (4^10 is saturated at these sizes, 4^14 is sparse)."""
+    import torch
+
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+
+    codes_h = synth.umi_codes(n, L, seed=L + n)
+    codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
+    batch = D.PackedBatch(codes, L)
+    out = {}
+    try:
+        for mode in (D.GLOBAL_ROUNDS, D.GLOBAL_UNION_FIND):
+            D.set_global_mode(mode)
+            eng = D.ClusterEngine(L, min(n, 4 ** L), "cuda")
+            cid = torch.empty(n, dtype=torch.int32, device="cuda")
+            D.cluster_batch(eng, batch, cid, 1)
+            out[mode] = (cid.cpu().numpy(), eng.stats()["n_clusters"])
+    finally:
+        D.set_global_mode(0)
+    assert out[1][1] == out[2][1]
+    assert np.array_equal(out[1][0], out[2][0])
+    if n <= 1_000_000:
+        rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L)), L, 1)
+        assert out[1][1] == rk
+        assert np.array_equal(out[1][0].view(np.uint32), rc)
