@@ -310,6 +310,56 @@ int rogtk_fastq_pair_next(void* reader, int64_t max_records, int64_t* n_records,
                           const int64_t** offsets9, const uint8_t** values9);
 int rogtk_fastq_pair_close(void* reader);
 
+/* ====== element-wise string transforms (strings.hip) ======
+ * One op per reference polars expression (src/expressions.rs); null in any input the
+ * reference matches on -> null out; Utf8 in, Utf8 out (PHRED_LIST: the u8 values of
+ * List[UInt8], rows of null inputs are dropped by the caller as the reference does).
+ * Inputs must be valid UTF-8 (Rust &str). A column of 1 row next to longer ones is
+ * broadcast (the scalar reference of cigar_aligned_*_expr, expressions.rs:344-349). */
+#define ROGTK_STR_REVCOMP 1          /* reverse_complement_series        :957-977           */
+#define ROGTK_STR_PARSE_CIGAR 2      /* parse_cigar_series (param block_dels) :450-505      */
+#define ROGTK_STR_ALIGNED_REF 3      /* cigar_aligned_ref_expr (ref, query, cigar) :257-394 */
+#define ROGTK_STR_ALIGNED_QUERY 4    /* cigar_aligned_query_expr (ref, query, cigar) :396-444 */
+#define ROGTK_STR_CIGAR_INSERTIONS 5 /* extract_cigar_insertions_expr (seq, cigar) :29-80,207-251 */
+#define ROGTK_STR_ENRICH_ALLELE 6    /* enrich_allele_insertions_expr (allele, seq, cigar) :84-205 */
+#define ROGTK_STR_PHRED_STR 7        /* phred_to_numeric_series_str (param base) :632-665   */
+#define ROGTK_STR_PHRED_LIST 8       /* phred_to_numeric_series values (param base) :598-630 */
+
+typedef struct rogtk_str_col {
+    const void* offsets; /* n + 1 entries, int32 or int64 */
+    int offset_width;
+    const uint8_t* values;
+    int64_t values_len; /* < 0: unchecked */
+    const uint8_t* validity;
+    int64_t validity_offset;
+    int64_t n;
+} rogtk_str_col;
+
+/* Level 1 (device columns, enqueue-only): measure writes out_offsets[n_rows + 1]
+ * (exclusive scan of the output byte lengths; out_offsets[n_rows] = total) and the
+ * output validity (bit per row, LSB order); the caller sizes out_values from the
+ * total and calls fill. temp: rogtk_str_temp_bytes(n_rows) bytes of device memory. */
+int rogtk_str_temp_bytes(int64_t n_rows, int64_t* bytes);
+int rogtk_str_measure(int op, const rogtk_str_col* cols, int n_cols, int64_t n_rows, int64_t param,
+                      int64_t* out_offsets, uint64_t* out_valid_bits, void* temp, int64_t temp_bytes,
+                      void* stream);
+int rogtk_str_fill(int op, const rogtk_str_col* cols, int n_cols, int64_t n_rows, int64_t param,
+                   const int64_t* offsets, uint8_t* out_values, void* stream);
+
+/* Level 2 (host columns): the library allocates the result (malloc); free it with
+ * rogtk_str_result_free. offsets are int64 (Arrow LargeUtf8), validity LSB bits. */
+typedef struct rogtk_str_result {
+    int64_t n;
+    int64_t* offsets;
+    uint8_t* values;
+    int64_t values_len;
+    uint8_t* validity;
+    int64_t null_count;
+} rogtk_str_result;
+int rogtk_str_transform_host(int op, const rogtk_str_col* cols, int n_cols, int64_t n_rows, int64_t param,
+                             rogtk_str_result* out);
+void rogtk_str_result_free(rogtk_str_result* r);
+
 /* ============================== profiling ================================ */
 /* When enabled, every kernel launch is bracketed by HIP events on its stream. */
 /* ======== multi-GPU exchange of read groups ========

@@ -11,6 +11,8 @@ Drop-in surface (mirrors rogtk/__init__.py's `umi` / `hamming` namespaces):
     rg.umi_cluster(umis, max_distance=1)         # H3 (caller-side group_by('umi'))
     rg.kmer_spectrum(reads, k=17, min_coverage=20, group_offsets=...)  # H4 (fracture.rs)
     rg.assemble_sequences(group_reads, k=13, min_coverage=1, method="compression")  # H5
+    rg.col(seqs).dna.reverse_complement(); rg.parse_cigar(cigars, block_dels=False)
+    rg.col(ref).cigar.align_to_ref(query, cigars); rg.extract_cigar_insertions(seq, cigars)
 
 Device-resident pipeline (packed SoA in HBM, torch tensors as plumbing):
     rogtk_amd.device (PackedBatch, score_packed, ClusterEngine, cluster_batch)
@@ -24,6 +26,15 @@ from .assembly import (  # noqa: F401
     assemble_sequences_with_anchors,
     optimize_assembly,
     sweep_assembly_params,
+)
+from .strings import (  # noqa: F401
+    CigarNamespace,
+    DnaNamespace,
+    extract_cigar_insertions,
+    parse_cigar,
+    phred_to_numeric,
+    phred_to_numeric_str,
+    reverse_complement,
 )
 from .api import (  # noqa: F401
     FIELDS,
@@ -46,5 +57,6 @@ __all__ = [
     "UmiNamespace", "col", "hamming_distance", "hamming_within", "umi_cluster", "umi_complexity",
     "umi_complexity_scores", "kmer_spectrum", "KMER_STATS", "assemble_sequences",
     "assemble_sequences_with_anchors", "sweep_assembly_params", "optimize_assembly", "iter_paired_fastqs",
-    "parse_paired_fastqs",
+    "parse_paired_fastqs", "DnaNamespace", "CigarNamespace", "reverse_complement", "parse_cigar",
+    "phred_to_numeric_str", "phred_to_numeric", "extract_cigar_insertions",
 ]

@@ -58,6 +58,33 @@ class BamBatch(ctypes.Structure):
     ]
 
 
+class StrCol(ctypes.Structure):
+    """rogtk_str_col (include/rogtk_hip.h): one Arrow string column."""
+
+    _fields_ = [
+        ("offsets", ctypes.c_void_p),
+        ("offset_width", ctypes.c_int),
+        ("values", ctypes.c_void_p),
+        ("values_len", ctypes.c_int64),
+        ("validity", ctypes.c_void_p),
+        ("validity_offset", ctypes.c_int64),
+        ("n", ctypes.c_int64),
+    ]
+
+
+class StrResult(ctypes.Structure):
+    """rogtk_str_result (include/rogtk_hip.h): library-allocated LargeUtf8 output."""
+
+    _fields_ = [
+        ("n", ctypes.c_int64),
+        ("offsets", ctypes.c_void_p),
+        ("values", ctypes.c_void_p),
+        ("values_len", ctypes.c_int64),
+        ("validity", ctypes.c_void_p),
+        ("null_count", ctypes.c_int64),
+    ]
+
+
 _vp, _i64, _i32, _u32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_uint32
 _P_SCORES = ctypes.POINTER(UmiScores)
 _P_I64 = ctypes.POINTER(ctypes.c_int64)
@@ -117,9 +144,18 @@ SIGNATURES = {
     "rogtk_fastq_pair_open": [ctypes.c_char_p, ctypes.c_char_p, _i64, _i64, _i64, _i32, _vp],
     "rogtk_fastq_pair_next": [_vp, _i64, _P_I64, _vp, _vp],
     "rogtk_fastq_pair_close": [_vp],
+    "rogtk_str_temp_bytes": [_i64, _P_I64],
+    "rogtk_str_measure": [_i32, ctypes.POINTER(StrCol), _i32, _i64, _i64, _vp, _vp, _vp, _i64, _vp],
+    "rogtk_str_fill": [_i32, ctypes.POINTER(StrCol), _i32, _i64, _i64, _vp, _vp, _vp],
+    "rogtk_str_transform_host": [_i32, ctypes.POINTER(StrCol), _i32, _i64, _i64, ctypes.POINTER(StrResult)],
     "rogtk_profile_enable": [_i32],
     "rogtk_profile_reset": [],
     "rogtk_profile_read": [ctypes.c_char_p, _P_F64, _P_I64],
+}
+
+# functions returning void
+VOID_SIGNATURES = {
+    "rogtk_str_result_free": [ctypes.POINTER(StrResult)],
 }
 
 _lock = threading.Lock()
@@ -161,6 +197,10 @@ def hip() -> ctypes.CDLL:
                 fn = getattr(lib, name)
                 fn.argtypes = argtypes
                 fn.restype = ctypes.c_int
+            for name, argtypes in VOID_SIGNATURES.items():
+                if hasattr(lib, name):
+                    getattr(lib, name).argtypes = argtypes
+                    getattr(lib, name).restype = None
             lib.rogtk_version.restype = ctypes.c_char_p
             lib.rogtk_version.argtypes = []
             lib.rogtk_last_error.restype = ctypes.c_char_p

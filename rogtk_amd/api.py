@@ -257,6 +257,10 @@ class Col:
         self.column = column
         self.umi = UmiNamespace(column)
         self.hamming = HammingExpr(column)
+        from .strings import CigarNamespace, DnaNamespace
+
+        self.dna = DnaNamespace(column)
+        self.cigar = CigarNamespace(column)
 
 
 def col(column: ColumnLike) -> Col:

@@ -863,6 +863,145 @@ void optimize(SeriesExport* in, size_t n_in, const Kwargs& kw, SeriesExport* out
     export_series(out, optimize_struct(s.name), std::move(chunks));
 }
 
+// ------------------------------------------- element-wise string transforms
+// A whole series as one host chunk, nulls kept (the row space the reference zips over).
+struct FlatCol {
+    std::vector<int64_t> off;
+    std::vector<uint8_t> val, valid;
+    int64_t n = 0, nulls = 0;
+};
+FlatCol flatten_all(const StrSeries& s) {
+    FlatCol f;
+    f.off.push_back(0);
+    for (const Chunk& c : s.chunks)
+        for (int64_t r = 0; r < c.n; ++r) {
+            const bool ok = c.valid(r);
+            if ((f.n & 7) == 0) f.valid.push_back(0);
+            if (ok) {
+                f.valid.back() |= (uint8_t)(1u << (f.n & 7));
+                f.val.insert(f.val.end(), c.values + c.off(r), c.values + c.off(r + 1));
+            } else {
+                ++f.nulls;
+            }
+            f.off.push_back((int64_t)f.val.size());
+            ++f.n;
+        }
+    if (f.val.empty()) f.val.push_back(0);
+    if (f.valid.empty()) f.valid.push_back(0);
+    return f;
+}
+
+rogtk_str_col str_desc(const FlatCol& f) {
+    return rogtk_str_col{f.off.data(), 8, f.val.data(), (int64_t)f.val.size(), f.nulls ? f.valid.data() : nullptr,
+                         0, f.n};
+}
+
+// Utf8View column of a rogtk_str_result (nulls kept).
+Col view_col_result(const rogtk_str_result& r) {
+    Col c;
+    c.length = r.n;
+    c.null_count = r.null_count;
+    std::vector<uint8_t> views(std::max<size_t>((size_t)r.n * 16, 16), 0), data;
+    for (int64_t i = 0; i < r.n; ++i) {
+        const int64_t a = r.offsets[i], b = r.offsets[i + 1];
+        if (b - a > (int64_t)std::numeric_limits<int32_t>::max()) fail("string too long for a Utf8View");
+        const int32_t L = (int32_t)(b - a);
+        uint8_t* v = views.data() + 16 * i;
+        memcpy(v, &L, 4);
+        if (L <= 12) {
+            if (L) memcpy(v + 4, r.values + a, L);
+        } else {
+            const int32_t bi = 0, bo = (int32_t)data.size();
+            if (data.size() + L > (size_t)std::numeric_limits<int32_t>::max()) fail("Utf8View buffer over 2 GiB");
+            memcpy(v + 4, r.values + a, 4);
+            memcpy(v + 8, &bi, 4);
+            memcpy(v + 12, &bo, 4);
+            data.insert(data.end(), r.values + a, r.values + b);
+        }
+    }
+    const int64_t dlen = (int64_t)data.size();
+    if (data.empty()) data.push_back(0);
+    std::vector<uint8_t> sizes(8);
+    memcpy(sizes.data(), &dlen, 8);
+    std::vector<uint8_t> vb;
+    if (r.null_count) vb.assign(r.validity, r.validity + (r.n + 7) / 8);
+    c.bufs.push_back(std::move(vb));
+    c.bufs.push_back(std::move(views));
+    c.bufs.push_back(std::move(data));
+    c.bufs.push_back(std::move(sizes));
+    return c;
+}
+
+// Run one op over the zipped inputs (the shortest input wins, as `.zip()`; the aligned
+// exprs broadcast a 1-row reference, expressions.rs:344-349).
+struct StrResultHolder {
+    rogtk_str_result r{};
+    ~StrResultHolder() { rogtk_str_result_free(&r); }
+};
+void str_transform(int op, SeriesExport* in, size_t n_in, size_t need, int64_t param, StrResultHolder* out,
+                   std::string* name) {
+    if (n_in < need) fail("expected %zu input series, got %zu", need, n_in);
+    std::vector<FlatCol> cols;
+    for (size_t k = 0; k < need; ++k) cols.push_back(flatten_all(str_series(in[k])));
+    *name = str_series(in[0]).name;
+    const bool aligned = op == ROGTK_STR_ALIGNED_REF || op == ROGTK_STR_ALIGNED_QUERY;
+    const bool scalar_ref = aligned && cols[0].n == 1 && cols[1].n > 1;
+    int64_t n = INT64_MAX;
+    for (size_t k = scalar_ref ? 1 : 0; k < need; ++k) n = std::min(n, cols[k].n);
+    std::vector<rogtk_str_col> d;
+    for (size_t k = 0; k < need; ++k) {
+        rogtk_str_col c = str_desc(cols[k]);
+        if (!(scalar_ref && k == 0)) c.n = n;  // zip: rows past the shortest input are dropped
+        d.push_back(c);
+    }
+    check(rogtk_str_transform_host(op, d.data(), (int)need, n, param, &out->r));
+}
+
+// reverse_complement_series, parse_cigar_series, cigar_aligned_*_expr,
+// extract_cigar_insertions_expr, enrich_allele_insertions_expr, phred_to_numeric_series_str
+void string_expr(SeriesExport* in, size_t n_in, SeriesExport* out, int op, size_t need, int64_t param) {
+    StrResultHolder h;
+    std::string name;
+    str_transform(op, in, n_in, need, param, &h, &name);
+    std::vector<Col> chunks;
+    chunks.push_back(view_col_result(h.r));
+    export_series(out, {name, "vu", {}}, std::move(chunks));
+}
+
+// phred_to_numeric_series (expressions.rs:598-630): List[UInt8] named "numeric_phred";
+// `ca.for_each` appends nothing for null rows, so they are dropped from the output.
+void phred_list_expr(SeriesExport* in, size_t n_in, SeriesExport* out, int64_t base) {
+    StrResultHolder h;
+    std::string name;
+    str_transform(ROGTK_STR_PHRED_LIST, in, n_in, 1, base, &h, &name);
+    const rogtk_str_result& r = h.r;
+    std::vector<int64_t> loff{0};
+    std::vector<uint8_t> vals;
+    for (int64_t i = 0; i < r.n; ++i) {
+        if (!((r.validity[i >> 3] >> (i & 7)) & 1)) continue;
+        vals.insert(vals.end(), r.values + r.offsets[i], r.values + r.offsets[i + 1]);
+        loff.push_back((int64_t)vals.size());
+    }
+    const int64_t m = (int64_t)loff.size() - 1;
+    Col child = prim_col<uint8_t>({}, 0, std::move(vals), (int64_t)loff.back());
+    Col list;
+    list.length = m;
+    list.bufs.push_back({});
+    std::vector<uint8_t> ob(loff.size() * 8);
+    memcpy(ob.data(), loff.data(), ob.size());
+    list.bufs.push_back(std::move(ob));
+    list.children.push_back(std::move(child));
+    std::vector<Col> chunks;
+    chunks.push_back(std::move(list));
+    export_series(out, {"numeric_phred", "+L", {{"item", "C", {}}}}, std::move(chunks));
+}
+
+int64_t phred_base(const Kwargs& kw) {
+    const int64_t b = kw.uint("base");  // Phred2NmKwargs.base: u8 (expressions.rs:493-496)
+    if (b > 255) fail("could not parse kwargs: base does not fit in u8");
+    return b;
+}
+
 // ----------------------------------------------------------- entry wrappers
 template <class F>
 void guarded(SeriesExport* in, size_t n_in, SeriesExport* out, F&& f) {
@@ -1016,5 +1155,30 @@ ROGTK_FIELD(sweep_assembly_params_expr,
             (FieldSpec{name, "+s", {{"k", "l", {}}, {"min_coverage", "l", {}}, {"contig_length", "l", {}}}}))
 ROGTK_EXPR(optimize_assembly_expr, optimize(inputs, n_inputs, parse_kwargs(kwargs_ptr, kwargs_len), return_value))
 ROGTK_FIELD(optimize_assembly_expr, optimize_struct(name))
+
+// element-wise string expressions (expressions.rs:29-665, 957-977)
+ROGTK_EXPR(reverse_complement_series, string_expr(inputs, n_inputs, return_value, ROGTK_STR_REVCOMP, 1, 0))
+ROGTK_FIELD(reverse_complement_series, (FieldSpec{name, "vu", {}}))
+ROGTK_EXPR(parse_cigar_series,
+           string_expr(inputs, n_inputs, return_value, ROGTK_STR_PARSE_CIGAR, 1,
+                       parse_kwargs(kwargs_ptr, kwargs_len).uint("block_dels") != 0))
+ROGTK_FIELD(parse_cigar_series, (FieldSpec{name, "vu", {}}))
+ROGTK_EXPR(cigar_aligned_ref_expr, string_expr(inputs, n_inputs, return_value, ROGTK_STR_ALIGNED_REF, 3, 0))
+ROGTK_FIELD(cigar_aligned_ref_expr, (FieldSpec{name, "vu", {}}))
+ROGTK_EXPR(cigar_aligned_query_expr, string_expr(inputs, n_inputs, return_value, ROGTK_STR_ALIGNED_QUERY, 3, 0))
+ROGTK_FIELD(cigar_aligned_query_expr, (FieldSpec{name, "vu", {}}))
+ROGTK_EXPR(extract_cigar_insertions_expr,
+           string_expr(inputs, n_inputs, return_value, ROGTK_STR_CIGAR_INSERTIONS, 2, 0))
+ROGTK_FIELD(extract_cigar_insertions_expr, (FieldSpec{name, "vu", {}}))
+ROGTK_EXPR(enrich_allele_insertions_expr,
+           string_expr(inputs, n_inputs, return_value, ROGTK_STR_ENRICH_ALLELE, 3, 0))
+ROGTK_FIELD(enrich_allele_insertions_expr, (FieldSpec{name, "vu", {}}))
+ROGTK_EXPR(phred_to_numeric_series_str,
+           string_expr(inputs, n_inputs, return_value, ROGTK_STR_PHRED_STR, 1,
+                       phred_base(parse_kwargs(kwargs_ptr, kwargs_len))))
+ROGTK_FIELD(phred_to_numeric_series_str, (FieldSpec{name, "vu", {}}))
+ROGTK_EXPR(phred_to_numeric_series,
+           phred_list_expr(inputs, n_inputs, return_value, phred_base(parse_kwargs(kwargs_ptr, kwargs_len))))
+ROGTK_FIELD(phred_to_numeric_series, (FieldSpec{name, "+L", {{"item", "C", {}}}}))
 
 }  // extern "C"
