@@ -34,6 +34,10 @@ EXPRESSIONS = (
     "umi_longest_homopolymer_expr", "umi_dust_score_expr", "hamming_distance_expr", "hamming_within_expr",
     "assemble_sequences_expr", "assemble_sequences_with_anchors_expr", "sweep_assembly_params_expr",
     "optimize_assembly_expr",
+    # element-wise string expressions (expressions.rs:29-665, 957-977)
+    "reverse_complement_series", "parse_cigar_series", "cigar_aligned_ref_expr", "cigar_aligned_query_expr",
+    "extract_cigar_insertions_expr", "enrich_allele_insertions_expr", "phred_to_numeric_series_str",
+    "phred_to_numeric_series",
 )
 
 

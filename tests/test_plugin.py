@@ -71,6 +71,14 @@ def test_plugin_version():
     ("optimize_assembly_expr", pa.struct([("contig", pa.string_view()), ("k", pa.uint32()),
                                           ("min_coverage", pa.uint32()), ("length", pa.uint32()),
                                           ("input_sequences", pa.uint32())])),
+    ("reverse_complement_series", pa.string_view()),
+    ("parse_cigar_series", pa.string_view()),
+    ("cigar_aligned_ref_expr", pa.string_view()),
+    ("cigar_aligned_query_expr", pa.string_view()),
+    ("extract_cigar_insertions_expr", pa.string_view()),
+    ("enrich_allele_insertions_expr", pa.string_view()),
+    ("phred_to_numeric_series_str", pa.string_view()),
+    ("phred_to_numeric_series", pa.large_list(pa.uint8())),
 ])
 def test_output_fields(name, typ):
     f = plugin.call_plugin_field(name, [pa.field("umi", pa.string_view())])
@@ -325,3 +333,54 @@ def test_empty_and_all_null_columns():
         assert len(got) == 0
         got = plugin.call_plugin("hamming_distance_expr", [pa.array([None, None], type=t)], {"target": "AC"})
         assert got.to_pylist() == [None, None]
+
+
+@pytest.mark.gpu
+def test_string_exprs_match_oracle():
+    """The element-wise string expressions through the plugin ABI (Utf8View / Utf8 /
+    LargeUtf8, chunked, sliced) equal the oracle restatement."""
+    from oracle import pystrings as O
+
+    rng = np.random.default_rng(9)
+    n = 600
+    al = np.frombuffer(b"ACGTNacgt", np.uint8)
+    seqs = [bytes(rng.choice(al, int(rng.integers(0, 60)))).decode() for _ in range(n)]
+    cig = []
+    for s in seqs:
+        parts, used = [], 0
+        while used < len(s):
+            op = "MIDNSHP=X"[int(rng.integers(9))]
+            k = int(rng.integers(0, 8))
+            parts.append(f"{k}{op}")
+            used += k if op in "MIS=X" else 0
+        cig.append("".join(parts))
+    seqs[3] = None
+    cig[4] = None
+    alleles = [f"AC[{int(rng.integers(0, 40))}:{int(rng.integers(1, 4))}I]GG[None]" for _ in range(n)]
+    quals = [bytes(rng.integers(33, 74, int(rng.integers(0, 30)), dtype=np.uint8)).decode() for _ in range(n)]
+    quals[7] = None
+    for lay in ("view", "utf8", "large", "chunked_view", "sliced_view", "sliced_utf8"):
+        S, C, A, Q = (_layouts(v)[lay] for v in (seqs, cig, alleles, quals))
+        got = plugin.call_plugin("reverse_complement_series", [S]).combine_chunks().to_pylist()
+        assert got == O.column("revcomp", [seqs]), lay
+        for bd in (False, True):
+            got = plugin.call_plugin("parse_cigar_series", [C], {"block_dels": bd}).combine_chunks().to_pylist()
+            assert got == O.column("parse_cigar", [cig], int(bd)), lay
+        for name, op in (("cigar_aligned_ref_expr", "aligned_ref"), ("cigar_aligned_query_expr", "aligned_query")):
+            got = plugin.call_plugin(name, [S, S, C]).combine_chunks().to_pylist()
+            assert got == O.column(op, [seqs, seqs, cig]), (lay, name)
+        got = plugin.call_plugin("extract_cigar_insertions_expr", [S, C]).combine_chunks().to_pylist()
+        assert got == O.column("cigar_insertions", [seqs, cig]), lay
+        got = plugin.call_plugin("enrich_allele_insertions_expr", [A, S, C]).combine_chunks().to_pylist()
+        assert got == O.column("enrich", [alleles, seqs, cig]), lay
+        got = plugin.call_plugin("phred_to_numeric_series_str", [Q], {"base": 33}).combine_chunks().to_pylist()
+        assert got == O.column("phred_str", [quals], 33), lay
+        got = plugin.call_plugin("phred_to_numeric_series", [Q], {"base": 33}).combine_chunks().to_pylist()
+        assert got == [v for v in O.column("phred_list", [quals], 33) if v is not None], lay
+    # scalar reference (pl.lit(ref)) broadcast over the query column
+    ref1 = pa.array(["ACGTACGTAAcc"], type=pa.string_view())
+    got = plugin.call_plugin("cigar_aligned_ref_expr", [ref1, _layouts(seqs)["view"], _layouts(cig)["view"]])
+    assert got.combine_chunks().to_pylist() == O.column("aligned_ref", [["ACGTACGTAAcc"], seqs, cig])
+    # serde errors: required kwargs
+    assert "missing field `block_dels`" in _err("parse_cigar_series", [_layouts(cig)["view"]], {})
+    assert "missing field `base`" in _err("phred_to_numeric_series_str", [_layouts(quals)["view"]], {})
