@@ -953,7 +953,7 @@ __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ 
     const bool full = row0 + 4 <= n;
     uint32_t c[4] = {0, 0, 0, 0};
     if (full) {
-        const uint4 v = *reinterpret_cast<const uint4*>(codes + row0);
+        const u32x4_t v = stream_load(reinterpret_cast<const u32x4_t*>(codes + row0));
         c[0] = v.x; c[1] = v.y; c[2] = v.z; c[3] = v.w;
     } else {
         for (int k = 0; k < 4; ++k)
@@ -970,7 +970,7 @@ __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ 
         }
     }
     if (full) {
-        *reinterpret_cast<uint4*>(out + row0) = make_uint4(id[0], id[1], id[2], id[3]);
+        stream_store(u32x4_t{id[0], id[1], id[2], id[3]}, reinterpret_cast<u32x4_t*>(out + row0));
     } else {
         for (int k = 0; k < 4; ++k)
             if (row0 + k < n) out[row0 + k] = id[k];
@@ -1090,7 +1090,7 @@ __global__ __launch_bounds__(kBlock) void k_mark_xcd(const uint32_t* __restrict_
         uint32_t c[4];
         uint32_t reg = regbits ? (uint32_t)(regbits[r >> 6] >> (r & 63)) & 0xFu : 0xFu;
         if (r + 4 <= n) {
-            const uint4 v = *reinterpret_cast<const uint4*>(codes + r);
+            const u32x4_t v = stream_load(reinterpret_cast<const u32x4_t*>(codes + r));
             c[0] = v.x; c[1] = v.y; c[2] = v.z; c[3] = v.w;
         } else {
             reg &= (1u << (uint32_t)(n - r)) - 1u;

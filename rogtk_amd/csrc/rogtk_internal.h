@@ -75,6 +75,44 @@ int lut_ensure(int64_t max_total, const double** dev, int64_t* covered);
 
 constexpr int kMaxPackedLen = 16;
 
+// Streaming (non-temporal) vector accesses for data touched once per kernel (the code
+// stream, the per-row outputs), so that the randomly accessed tables of the same
+// kernel keep their L2 lines. ROGTK_NT=0 builds plain accesses (A/B).
+#ifndef ROGTK_NT
+#define ROGTK_NT 1
+#endif
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+typedef double f64x2_t __attribute__((ext_vector_type(2)));
+template <class V>
+__device__ __forceinline__ V stream_load(const V* p) {
+#if ROGTK_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+template <class V>
+__device__ __forceinline__ void stream_store(V v, V* p) {
+#if ROGTK_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+// the score kernel's 52 B/row of outputs (ROGTK_NT_SCORE_STORE=0: plain stores)
+#ifndef ROGTK_NT_SCORE_STORE
+#define ROGTK_NT_SCORE_STORE 1
+#endif
+template <class V>
+__device__ __forceinline__ void score_store(V v, V* p) {
+#if ROGTK_NT_SCORE_STORE
+    stream_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 // Per-call constants of the packed kernel (passed by value as a kernel argument).
 struct PackedParams {
     double sh[kMaxPackedLen + 1];    // plogp(c, L)

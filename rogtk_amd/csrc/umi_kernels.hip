@@ -196,8 +196,8 @@ __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restr
     uint32_t c[kRowsPerLane] = {0, 0, 0, 0};
     uint32_t reg = 0;
     if (full) {
-        const uint2 va = *reinterpret_cast<const uint2*>(codes + rA);
-        const uint2 vb = *reinterpret_cast<const uint2*>(codes + rB);
+        const u32x2_t va = stream_load(reinterpret_cast<const u32x2_t*>(codes + rA));
+        const u32x2_t vb = stream_load(reinterpret_cast<const u32x2_t*>(codes + rB));
         c[0] = va.x; c[1] = va.y; c[2] = vb.x; c[3] = vb.y;
         reg = regbits ? ((uint32_t)(regbits[rA >> 6] >> (rA & 63)) & 3u) |
                             (((uint32_t)(regbits[rB >> 6] >> (rB & 63)) & 3u) << 2)
@@ -233,14 +233,14 @@ __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restr
             if (full) {
                 auto st2 = [&](double* p, const double* v) {
                     if (!p) return;
-                    *reinterpret_cast<double2*>(p + rA) = make_double2(v[0], v[1]);
-                    *reinterpret_cast<double2*>(p + rB) = make_double2(v[2], v[3]);
+                    score_store(f64x2_t{v[0], v[1]}, reinterpret_cast<f64x2_t*>(p + rA));
+                    score_store(f64x2_t{v[2], v[3]}, reinterpret_cast<f64x2_t*>(p + rB));
                 };
                 st2(O.sh, sh); st2(O.ling, li); st2(O.homo, ho); st2(O.di, di);
                 st2(O.dust, du); st2(O.comb, co);
                 if (O.longest) {
-                    *reinterpret_cast<uint2*>(O.longest + rA) = make_uint2(lg[0], lg[1]);
-                    *reinterpret_cast<uint2*>(O.longest + rB) = make_uint2(lg[2], lg[3]);
+                    score_store(u32x2_t{lg[0], lg[1]}, reinterpret_cast<u32x2_t*>(O.longest + rA));
+                    score_store(u32x2_t{lg[2], lg[3]}, reinterpret_cast<u32x2_t*>(O.longest + rB));
                 }
             } else {
                 const int64_t rr[4] = {rA, rA + 1, rB, rB + 1};
