@@ -34,6 +34,7 @@
 //   label   labelcode[code] (L <= 13) or ilab[i] := dense id (index space)
 //   assign  cluster_id[row] = label(code[row])
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 
@@ -1038,7 +1039,12 @@ int cluster_layout(int L, int64_t max_distinct, ClusterLayout* o) {
     c.blocks = (c.words + kScanWords - 1) / kScanWords;
     c.rwords = (max_distinct + 63) / 64;
     c.rblocks = (c.rwords + kScanWords - 1) / kScanWords;
-    c.label_by_code = L <= 13;
+    // ROGTK_LABEL_BY_INDEX=1: labels by rank even for L <= 13 (A/B of the assign gather)
+    static const bool by_index = [] {
+        const char* e = getenv("ROGTK_LABEL_BY_INDEX");
+        return e && e[0] == '1';
+    }();
+    c.label_by_code = L <= 13 && !by_index;
     int64_t off = 0;
     auto take = [&](int64_t bytes) {
         const int64_t at = off;
