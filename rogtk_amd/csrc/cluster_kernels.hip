@@ -885,15 +885,36 @@ __device__ __forceinline__ uint32_t root_label(uint32_t r, const uint64_t* __res
 
 // Label of every word with a shared local root (kNone for the others), so that the
 // per-code pass below needs no dependent loads for them.
+// A word without a shared LOCAL root still gets a word label when the global phase put
+// all of its codes in one component (their f are global roots then: they are live): in
+// the giant components of a 1-edit-saturated space most words end up uniform, and assign
+// then needs one L2-resident load per row instead of a gather from the 4^L table.
 __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restrict__ f,
                                                        const uint32_t* __restrict__ UR, int64_t words,
+                                                       const uint4* __restrict__ RT, int64_t max_distinct,
                                                        const uint64_t* __restrict__ rbits,
                                                        const uint32_t* __restrict__ rpref,
                                                        const uint32_t* __restrict__ rblkoff,
                                                        uint32_t* __restrict__ wlab) {
     for (int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x; w < words; w += (int64_t)gridDim.x * kBlock) {
         const uint32_t ur = UR[w];
-        wlab[w] = ur != kNone ? root_label(f[ur], rbits, rpref, rblkoff) : kNone;
+        uint32_t root = kNone;
+        if (ur != kNone) {
+            root = f[ur];
+        } else {
+            const uint4 e = RT[w];
+            uint64_t m = rt_word(e);
+            const int cnt = __popcll(m);
+            if (cnt > 0 && (int64_t)e.z + cnt <= max_distinct) {
+                root = f[e.z];
+                for (int k = 1; k < cnt; ++k)
+                    if (f[e.z + k] != root) {
+                        root = kNone;
+                        break;
+                    }
+            }
+        }
+        wlab[w] = root != kNone ? root_label(root, rbits, rpref, rblkoff) : kNone;
     }
 }
 
@@ -1193,7 +1214,7 @@ int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s) {
         const int lg = grid_for((int64_t)std::min<uint64_t>(cl.nbits, 1ull << 30), 16384);
         // wpref (consumed into RT by k_rt) holds the word labels
         hipLaunchKernelGGL(k_word_label, dim3(grid_for(cl.words, kPersistentGrid)), dim3(kBlock), 0, s, p.f, p.UR,
-                           cl.words, p.rbits, p.rpref, p.rblkoff, p.wpref);
+                           cl.words, p.RT, cl.max_distinct, p.rbits, p.rpref, p.rblkoff, p.wpref);
         hipLaunchKernelGGL(k_label, dim3(lg), dim3(kBlock), 0, s, p.f, p.RT, p.wpref, cl.nbits, p.rbits, p.rpref,
                            p.rblkoff, p.labelcode, p.ilab, p.D, cl.max_distinct, p.stats);
         ROGTK_HIP_CHECK(hipGetLastError());
