@@ -57,8 +57,9 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="skip in-run HIP-event kernel timing")
     ap.add_argument("--iso-launches", type=int, default=10, help="isolated score-kernel launches after timing")
     ap.add_argument("--depth", type=int, default=2, help="batches in flight (1 = no cross-batch overlap)")
-    ap.add_argument("--mark", choices=("xcd", "fused"), default="xcd",
-                    help="H3 presence mark: XCD-partitioned kernel or fused into k_score_packed")
+    ap.add_argument("--mark", choices=("auto", "xcd", "fused", "sort"), default="auto",
+                    help="H3 presence bitmap: partition sort + LDS bitmap (auto for umi_len 7..13), "
+                         "XCD-partitioned mark kernel, or mark fused into k_score_packed")
     ap.add_argument("--overlap-score", action="store_true",
                     help="let assign of the previous batch overlap the score kernel (default: score overlaps "
                          "only the latency-bound resolve kernels)")

@@ -166,6 +166,14 @@ int rogtk_cluster_rounds(const void* ws, void* stream, int* rounds);
  * (1..64; 0 restores the default of 4). Process-wide. Fewer rounds never change
  * results: the rest run when assign / stats find the flags not yet converged. */
 int rogtk_cluster_set_spec_rounds(int n);
+/* Local presence bitmap straight from the codes (7 <= umi_len <= 13), replacing
+ * rogtk_cluster_mark + rogtk_cluster_local_bitmap: an 8-bit radix pass groups the codes
+ * by code partition, then one workgroup per partition builds its slice of the bitmap in
+ * LDS. bitmap_out: rogtk_cluster_bitmap_words() words; temp: device scratch of
+ * rogtk_cluster_mark_bitmap_temp_bytes(n, umi_len) bytes. Enqueue-only. */
+int rogtk_cluster_mark_bitmap_temp_bytes(int64_t n, int umi_len, int64_t* bytes);
+int rogtk_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
+                              uint64_t* bitmap_out, void* temp, int64_t temp_bytes, void* stream);
 /* Global phase of max_distance 1 (positions 7..L-1), process-wide: 2 = bulk-synchronous
  * hook + jump rounds with speculative launch and deferred completion (default; 0
  * restores it), 1 = one-pass lock-free CAS union-find. Identical results. */

@@ -111,6 +111,8 @@ SIGNATURES = {
     "rogtk_cluster_rounds": [_vp, _vp, ctypes.POINTER(ctypes.c_int)],
     "rogtk_cluster_set_spec_rounds": [_i32],
     "rogtk_cluster_set_global_mode": [_i32],
+    "rogtk_cluster_mark_bitmap_temp_bytes": [_i64, _i32, _P_I64],
+    "rogtk_cluster_mark_bitmap": [_vp, _vp, _i64, _i32, _vp, _vp, _i64, _vp],
     "rogtk_umi_cluster_dev": [_vp, _vp, _vp, _i64, _i32, _i32, _vp, ctypes.POINTER(_i64), _vp],
     "rogtk_route_pack": [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp],
     "rogtk_bam_open": [ctypes.c_char_p, _i32, ctypes.POINTER(_vp)],

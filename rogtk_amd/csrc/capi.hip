@@ -487,6 +487,16 @@ int rogtk_cluster_rounds(const void* ws, void* stream, int* rounds) {
 
 int rogtk_cluster_set_spec_rounds(int n) { return cluster_set_spec_rounds(n); }
 int rogtk_cluster_set_global_mode(int mode) { return cluster_set_global_mode(mode); }
+int rogtk_cluster_mark_bitmap_temp_bytes(int64_t n, int umi_len, int64_t* bytes) {
+    ROGTK_REQUIRE(bytes, ROGTK_E_INVALID, "null bytes");
+    return cluster_mark_bitmap_temp(n, umi_len, bytes);
+}
+int rogtk_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
+                              uint64_t* bitmap_out, void* temp, int64_t temp_bytes, void* stream) {
+    ROGTK_REQUIRE((codes || n == 0) && bitmap_out, ROGTK_E_INVALID, "null codes / bitmap_out");
+    return launch_cluster_mark_bitmap(codes, regular_bits, n, umi_len, bitmap_out, temp, temp_bytes,
+                                      as_stream(stream));
+}
 
 int rogtk_cluster_release(const void* ws) {
     if (ws) cluster_release(ws);

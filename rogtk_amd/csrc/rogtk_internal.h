@@ -211,6 +211,10 @@ int launch_cluster_mark(const uint32_t* codes, const uint64_t* regular_bits, int
                         uint8_t* presence, hipStream_t s);
 int launch_cluster_local_bitmap(const ClusterLayout& cl, uint8_t* ws, uint64_t* bitmap_out,
                                 hipStream_t s);
+// presence bitmap straight from the codes by an 8-bit partition sort (7 <= L <= 13)
+int cluster_mark_bitmap_temp(int64_t n, int L, int64_t* bytes);
+int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int L,
+                               uint64_t* bitmap, void* temp, int64_t temp_bytes, hipStream_t s);
 int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t* bitmaps,
                            int n_bitmaps, int max_distance, hipStream_t s);
 // Waits for an asynchronous resolve's round flags and completes it if needed.

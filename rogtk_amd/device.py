@@ -141,6 +141,16 @@ class ClusterEngine:
         _lib.call("rogtk_cluster_mark", _p(batch.codes), _p(batch.regular_bits), batch.n, self.umi_len,
                   _p(self.ws), self.max_distinct, _s(stream))
 
+    def mark_bitmap(self, batch: PackedBatch, stream=None) -> torch.Tensor:
+        """mark + build_local_bitmap in one: partition sort + LDS bitmap (7 <= L <= 13)."""
+        need = ctypes.c_int64(0)
+        _lib.call("rogtk_cluster_mark_bitmap_temp_bytes", batch.n, self.umi_len, ctypes.byref(need))
+        if getattr(self, "_mark_temp", None) is None or self._mark_temp.numel() < need.value:
+            self._mark_temp = torch.empty(need.value, dtype=torch.uint8, device=self.local_bitmap.device)
+        _lib.call("rogtk_cluster_mark_bitmap", _p(batch.codes), _p(batch.regular_bits), batch.n, self.umi_len,
+                  _p(self.local_bitmap), _p(self._mark_temp), self._mark_temp.numel(), _s(stream))
+        return self.local_bitmap
+
     def build_local_bitmap(self, stream=None) -> torch.Tensor:
         _lib.call("rogtk_cluster_local_bitmap", _p(self.ws), self.umi_len, self.max_distinct,
                   _p(self.local_bitmap), _s(stream))

@@ -1,8 +1,10 @@
 """Streaming pipeline over packed batches: three HIP streams, `depth` batches in flight.
 
 The hot path has three phases with different limits on MI355X:
-  main stream     k_score_packed (H1 scores + H2 Hamming), the XCD-partitioned
-                  presence mark (or the mark fused into k_score_packed) and the
+  main stream     k_score_packed (H1 scores + H2 Hamming), then the local presence
+                  bitmap: by default an 8-bit partition sort of the codes + one LDS
+                  bitmap slice per partition (umi_len 7..13); else the XCD-partitioned
+                  presence mark (or the mark fused into k_score_packed) + the
                   presence->bitmap pass: HBM-bandwidth bound
   resolve stream  [RCCL all-gather of the bitmaps] + rank tables + LDS-local and
                   global connected components: latency bound (small tables, many
@@ -40,13 +42,17 @@ class _Slot:
 class UmiPipeline:
     def __init__(self, umi_len: int, max_distinct: int, n_max: int, device=None, depth: int = 3,
                  target: Optional[bytes] = b"ACGTACGTACGT", max_hamming: int = 1, max_distance: int = 1,
-                 group=None, with_scores: bool = True, priorities=(0, 0, 0), mark: str = "xcd",
+                 group=None, with_scores: bool = True, priorities=(0, 0, 0), mark: str = "auto",
                  on_assigned=None, score_alone: bool = False, exchange=None):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
-        if mark not in ("xcd", "fused"):
-            raise ValueError("mark must be 'xcd' (XCD-partitioned mark kernel) or 'fused' (inside k_score_packed)")
+        if mark == "auto":  # the partition-sort bitmap where it applies (measured fastest)
+            mark = "sort" if 7 <= umi_len <= 13 else "xcd"
+        if mark not in ("xcd", "fused", "sort"):
+            raise ValueError("mark must be 'xcd' (XCD-partitioned mark kernel), 'fused' (inside k_score_packed) "
+                             "or 'sort' (partition sort + LDS bitmap, umi_len 7..13)")
+        self.sort_mark = mark == "sort"
         self.fused_mark = mark == "fused"
         self.slots = [_Slot(umi_len, max_distinct, n_max, dev, with_scores) for _ in range(depth)]
         # priorities: (main, resolve, assign); lower = higher priority (torch convention)
@@ -83,9 +89,12 @@ class UmiPipeline:
         if self.score_alone:
             self.last_scored = torch.cuda.Event()
             self.last_scored.record(self.main)
-        if not self.fused_mark:
-            slot.eng.mark(batch, stream=self.main)
-        slot.eng.build_local_bitmap(stream=self.main)
+        if self.sort_mark:
+            slot.eng.mark_bitmap(batch, stream=self.main)
+        else:
+            if not self.fused_mark:
+                slot.eng.mark(batch, stream=self.main)
+            slot.eng.build_local_bitmap(stream=self.main)
         marked = torch.cuda.Event()
         marked.record(self.main)
         with torch.cuda.stream(self.s_resolve):

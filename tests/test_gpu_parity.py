@@ -384,7 +384,7 @@ def test_full_size_c2_properties(rg):
 
 @pytest.mark.parametrize("depth,nb,alone", [(4, 4, False), (2, 5, False), (1, 3, False), (3, 7, False),
                                              (2, 6, True), (3, 5, True)])
-@pytest.mark.parametrize("mark", ["xcd", "fused"])
+@pytest.mark.parametrize("mark", ["xcd", "fused", "sort"])
 def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark):
     """rogtk_amd.pipeline (3 streams, `depth` batches in flight) == the sequential device
     path for EVERY batch (outputs copied out by the on_assigned hook before slot reuse)."""
@@ -538,3 +538,36 @@ def test_global_modes_identical(rg, L, n):
         rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L)), L, 1)
         assert out[1][1] == rk
         assert np.array_equal(out[1][0].view(np.uint32), rc)
+
+
+@pytest.mark.parametrize("n", [0, 1, 5000, 300_000, 3_000_000])
+@pytest.mark.parametrize("L", [7, 8, 10, 12, 13])
+def test_mark_bitmap_sort_equals_presence_path(rg, L, n):
+    """The partition-sort bitmap equals mark + local_bitmap bit for bit, with irregular
+    rows (regular bit 0) mixed in, whose codes must not be marked."""
+    import torch
+
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+
+    codes_h = synth.umi_codes(max(n, 1), L, seed=L * 7 + n)[:n] if n else np.zeros(0, np.uint32)
+    codes = torch.from_numpy(codes_h.view(np.int32).copy()).cuda() if n else torch.zeros(4, dtype=torch.int32,
+                                                                                          device="cuda")[:0]
+    rng = np.random.default_rng(n)
+    reg = rng.random(n) > 0.01
+    if n:
+        reg[-1] = False  # an irregular row in the last partition's bucket
+        codes_h = codes_h.copy()
+        codes_h[-1] = 4 ** L - 1
+        codes = torch.from_numpy(codes_h.view(np.int32).copy()).cuda()
+    bits = np.packbits(np.concatenate([reg, np.zeros((-n) % 64, bool)]), bitorder="little").view(np.int64)
+    regbits = torch.from_numpy(bits.copy()).cuda() if n else torch.zeros(1, dtype=torch.int64, device="cuda")
+    for rb in (regbits, None):
+        batch = D.PackedBatch(codes, L, rb)
+        a = D.ClusterEngine(L, max(min(n, 4 ** L), 1), "cuda")
+        a.mark(batch)
+        ref = a.build_local_bitmap().clone()
+        b = D.ClusterEngine(L, max(min(n, 4 ** L), 1), "cuda")
+        got = b.mark_bitmap(batch).clone()
+        torch.cuda.synchronize()
+        assert torch.equal(ref, got), (L, n, rb is None)
