@@ -299,6 +299,8 @@ def main():
                    "reads_per_gpu": count, "umi_len": L, "max_distance": md,
                    "n_distinct": stats["n_distinct"], "n_clusters": stats["n_clusters"],
                    "h3_global": "one-pass union-find" if args.global_mode == "uf" else "hook+jump rounds",
+                   "h3_bitmap": "partition sort + LDS bitmap" if pipe.sort_mark else
+                                ("mark fused in score kernel" if pipe.fused_mark else "XCD-partitioned mark"),
                    "parallelism": f"dp{world} shard-by-record + presence-bitmap all-gather"
                                   + (f" (rank 0 of {args.emulate_ranks} EMULATED on one GPU, no RCCL)"
                                      if args.emulate_ranks > 1 else "")},
