@@ -1410,12 +1410,20 @@ __global__ __launch_bounds__(kBlock) void k_mark_keys(const uint32_t* __restrict
     keys[i] = reg ? codes[i] : 0xFFFFFFFFu;  // sentinel >= 4^L: skipped by k_part_bitmap
 }
 
-__device__ __forceinline__ int64_t lower_bound_u32(const uint32_t* __restrict__ a, int64_t n, uint64_t v) {
-    int64_t lo = 0, hi = n;
+// First index i with a[i] >= v (n if none), found by the whole workgroup: each round
+// probes kPartBlock evenly spaced positions of [lo, hi] at once, so 10M keys take ~4
+// dependent loads instead of ~24. a[0, n) must be ordered by the predicate a[i] < v.
+__device__ int64_t wg_lower_bound(const uint32_t* __restrict__ a, int64_t n, uint64_t v) {
+    int64_t lo = 0, hi = n;  // the answer lies in [lo, hi]
     while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if ((uint64_t)a[mid] < v) lo = mid + 1;
-        else hi = mid;
+        const int64_t step = (hi - lo + kPartBlock - 1) / kPartBlock;
+        const int64_t pos = lo + (int64_t)threadIdx.x * step;
+        const bool less = pos < hi && (uint64_t)a[pos] < v;
+        const int64_t cnt = __syncthreads_count(less);
+        const int64_t nlo = cnt ? lo + (cnt - 1) * step + 1 : lo;
+        const int64_t nhi = min(hi, lo + cnt * step);
+        lo = nlo;
+        hi = nhi;
     }
     return lo;
 }
@@ -1428,11 +1436,13 @@ __global__ __launch_bounds__(kPartBlock) void k_part_bitmap(const uint32_t* __re
     const uint32_t pwords32 = (1u << shift) >> 5;  // >= 1 for two_l >= 13
     for (uint32_t k = threadIdx.x; k < pwords32; k += kPartBlock) lbits[k] = 0;
     __shared__ int64_t range[2];
+    const int64_t r0 = wg_lower_bound(sorted, n, (uint64_t)p << shift);
+    // the sort orders the partition bits only: sentinels share the last bucket with real
+    // codes, so that bucket runs to the end and skips them one by one
+    const int64_t r1 = p + 1 == (1 << kPartBits) ? n : wg_lower_bound(sorted, n, (uint64_t)(p + 1) << shift);
     if (threadIdx.x == 0) {
-        range[0] = lower_bound_u32(sorted, n, (uint64_t)p << shift);
-        // the sort orders the partition bits only: sentinels share the last bucket with
-        // real codes, so that bucket runs to the end and skips them one by one
-        range[1] = p + 1 == (1 << kPartBits) ? n : lower_bound_u32(sorted, n, (uint64_t)(p + 1) << shift);
+        range[0] = r0;
+        range[1] = r1;
     }
     __syncthreads();
     const uint32_t mask = (1u << shift) - 1u;
