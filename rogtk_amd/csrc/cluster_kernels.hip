@@ -1446,11 +1446,22 @@ __global__ __launch_bounds__(kPartBlock) void k_part_bitmap(const uint32_t* __re
     }
     __syncthreads();
     const uint32_t mask = (1u << shift) - 1u;
-    for (int64_t i = range[0] + threadIdx.x; i < range[1]; i += kPartBlock) {
-        const uint32_t key = __builtin_nontemporal_load(sorted + i);
-        if ((uint64_t)key >> two_l) continue;  // irregular-row sentinel
-        const uint32_t c = key & mask;
-        atomicOr(&lbits[c >> 5], 1u << (c & 31));
+    // 8 independent loads in flight per lane before the LDS atomics that consume them
+    constexpr int kUnroll = 8;
+    const int64_t rend = range[1];
+    for (int64_t i0 = range[0] + threadIdx.x; i0 < rend; i0 += (int64_t)kPartBlock * kUnroll) {
+        uint32_t key[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t i = i0 + (int64_t)u * kPartBlock;
+            key[u] = i < rend ? __builtin_nontemporal_load(sorted + i) : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            if ((uint64_t)key[u] >> two_l) continue;  // irregular-row sentinel / past the range
+            const uint32_t c = key[u] & mask;
+            atomicOr(&lbits[c >> 5], 1u << (c & 31));
+        }
     }
     __syncthreads();
     uint64_t* out = bitmap + ((uint64_t)p << shift >> 6);
