@@ -67,7 +67,7 @@ def parse():
                     help="(tools) on ONE GPU, act as rank 0 of W: the other W-1 shards' bitmaps are built once "
                          "before timing and the all-gather is replaced by a device copy; predicts per-rank "
                          "step time at N=W minus RCCL time. Never used by the driver.")
-    ap.add_argument("--global-mode", choices=("uf", "rounds"), default="rounds",
+    ap.add_argument("--global-mode", choices=("uf", "rounds", "rounds1f"), default="rounds",
                     help="H3 global CC phase: one-pass union-find or hook + jump rounds")
     ap.add_argument("--prio", type=str, default="0,0,0", help="stream priorities main,resolve,assign (-1 = high)")
     return ap.parse_args()
@@ -197,7 +197,8 @@ def main():
             gathered[: bm.numel()].copy_(bm)
             return gathered, W
 
-    D.set_global_mode(D.GLOBAL_UNION_FIND if args.global_mode == "uf" else D.GLOBAL_ROUNDS)
+    D.set_global_mode({"uf": D.GLOBAL_UNION_FIND, "rounds": D.GLOBAL_ROUNDS,
+                       "rounds1f": D.GLOBAL_ROUNDS_ONE_FLATTEN}[args.global_mode])
     pipe = UmiPipeline(L, min(n_total, 4 ** L), count, dev, depth=args.depth, target=TARGET,
                        max_distance=md, group=None,
                        priorities=tuple(int(x) for x in args.prio.split(",")), mark=args.mark,
@@ -298,7 +299,8 @@ def main():
                                "H3 Hamming<=1 cluster ids",
                    "reads_per_gpu": count, "umi_len": L, "max_distance": md,
                    "n_distinct": stats["n_distinct"], "n_clusters": stats["n_clusters"],
-                   "h3_global": "one-pass union-find" if args.global_mode == "uf" else "hook+jump rounds",
+                   "h3_global": {"uf": "one-pass union-find", "rounds": "hook+jump rounds",
+                                 "rounds1f": "root-chasing hook rounds + one flatten"}[args.global_mode],
                    "h3_bitmap": "partition sort + LDS bitmap" if pipe.sort_mark else
                                 ("mark fused in score kernel" if pipe.fused_mark else "XCD-partitioned mark"),
                    "parallelism": f"dp{world} shard-by-record + presence-bitmap all-gather"

@@ -176,7 +176,8 @@ int rogtk_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bit
                               uint64_t* bitmap_out, void* temp, int64_t temp_bytes, void* stream);
 /* Global phase of max_distance 1 (positions 7..L-1), process-wide: 2 = bulk-synchronous
  * hook + jump rounds with speculative launch and deferred completion (default; 0
- * restores it), 1 = one-pass lock-free CAS union-find. Identical results. */
+ * restores it), 1 = one-pass lock-free CAS union-find, 3 = hook rounds that chase
+ * roots with one flatten per batch of rounds. Identical results (A/B knob). */
 int rogtk_cluster_set_global_mode(int mode);
 /* Releases the host-side resolve state kept for ws (call before freeing ws). */
 int rogtk_cluster_release(const void* ws);

@@ -621,6 +621,17 @@ __device__ __forceinline__ bool hook_roots(HookTable& T, uint32_t* f, const uint
 // Frontier: a group whose members already share one root never crosses again (roots
 // only merge), so round k > 0 visits only the groups that crossed in round k - 1.
 // active holds two generations of one bit per task (written whole by ballots).
+// CHASE: the forest need not be stars (no jump between rounds): follow f to the root
+// (f only ever points at smaller ancestors, so the walk ends).
+template <bool CHASE>
+__device__ __forceinline__ uint32_t root_of(const uint32_t* f, uint32_t x) {
+    uint32_t r = f[x];
+    if (CHASE)
+        for (uint32_t q = f[r]; q != r; q = f[r]) r = q;
+    return r;
+}
+
+template <bool CHASE>
 __global__ __launch_bounds__(kBlock) void k_hook_g(const uint4* __restrict__ RT, const uint32_t* __restrict__ UR,
                                                    int64_t words, int L, int p0, uint32_t* f,
                                                    unsigned int* __restrict__ flags, int round,
@@ -666,7 +677,7 @@ __global__ __launch_bounds__(kBlock) void k_hook_g(const uint4* __restrict__ RT,
                 root[v] = kNone;
                 if (m[v] & multi) {
                     const uint32_t ur = UR[w0 + v * stride];
-                    if (ur != kNone) root[v] = f[ur];
+                    if (ur != kNone) root[v] = root_of<CHASE>(f, ur);
                     else all_uniform = false;
                 }
             }
@@ -691,7 +702,8 @@ __global__ __launch_bounds__(kBlock) void k_hook_g(const uint4* __restrict__ RT,
 #pragma unroll
                     for (int v = 0; v < 4; ++v)
                         if ((m[v] >> b) & 1ull)
-                            x[k++] = root[v] != kNone ? root[v] : f[e[v].z + (uint32_t)__popcll(m[v] & below)];
+                            x[k++] = root[v] != kNone ? root[v]
+                                                      : root_of<CHASE>(f, e[v].z + (uint32_t)__popcll(m[v] & below));
                     crossed |= hook_roots(T, f, x, k, last_x, last_mn);
                 }
             }
@@ -1168,8 +1180,9 @@ std::atomic<int> g_spec_rounds{kSpecRounds};
 // distinct, a few giant components): rounds 115 us of kernels, union-find 194 us
 // (CAS retries and dependent find chains on the hot roots; the rounds' LDS hook
 // table deduplicates them). Both are exact and give identical ids.
-[[maybe_unused]] constexpr int kGlobalUnionFind = 1;
+constexpr int kGlobalUnionFind = 1;
 constexpr int kGlobalRounds = 2;
+constexpr int kGlobalRoundsOneFlatten = 3;  // hook rounds that chase roots, one flatten per batch
 std::atomic<int> g_global_mode{kGlobalRounds};
 
 // Host-side state of an in-flight resolve, keyed by workspace: the round flags are
@@ -1191,10 +1204,19 @@ std::map<const void*, ResolveState> g_rs;
 int enqueue_rounds(const ClusterLayout& cl, const WsPtrs& p, int from, int to, hipStream_t s) {
     const int pg = grid_for(cl.max_distinct, kPersistentGrid);
     const int64_t tasks = (int64_t)(cl.L - kLocalPos) * (cl.words >> 2);
-    for (int k = from; k < to; ++k) {
-        hipLaunchKernelGGL(k_hook_g, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words, cl.L,
-                           kLocalPos, p.f, p.flags, k, p.active, cl.active_words);
-        hipLaunchKernelGGL(k_jump, dim3(pg), dim3(kBlock), 0, s, p.f, p.lroot, cl.max_distinct, p.stats, p.flags, k);
+    if (g_global_mode.load() == kGlobalRoundsOneFlatten) {
+        // hooks chase to the roots themselves; one flatten after the batch of rounds
+        for (int k = from; k < to; ++k)
+            hipLaunchKernelGGL(k_hook_g<true>, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words, cl.L,
+                               kLocalPos, p.f, p.flags, k, p.active, cl.active_words);
+        hipLaunchKernelGGL(k_flatten_live, dim3(pg), dim3(kBlock), 0, s, p.f, p.lroot, cl.max_distinct, p.stats);
+    } else {
+        for (int k = from; k < to; ++k) {
+            hipLaunchKernelGGL(k_hook_g<false>, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words,
+                               cl.L, kLocalPos, p.f, p.flags, k, p.active, cl.active_words);
+            hipLaunchKernelGGL(k_jump, dim3(pg), dim3(kBlock), 0, s, p.f, p.lroot, cl.max_distinct, p.stats, p.flags,
+                               k);
+        }
     }
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
@@ -1269,7 +1291,7 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
         hipLaunchKernelGGL(k_local_cc, dim3((unsigned)lblocks), dim3(kBlock), 0, s, p.RT, cl.words, cl.L,
                            p.f, p.D, p.UR, p.lroot, cl.rwords, cl.max_distinct, p.stats);
         ROGTK_HIP_CHECK(hipGetLastError());
-        if (cl.L > kLocalPos && g_global_mode.load() != kGlobalRounds) {
+        if (cl.L > kLocalPos && g_global_mode.load() == kGlobalUnionFind) {
             // one-pass union-find: exact when the stream reaches the labels
             const int64_t tasks = (int64_t)(cl.L - kLocalPos) * (cl.words >> 2);
             hipLaunchKernelGGL(k_union_g, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words, cl.L,
@@ -1336,8 +1358,8 @@ int cluster_set_spec_rounds(int n) {
 }
 
 int cluster_set_global_mode(int mode) {
-    ROGTK_REQUIRE(mode >= 0 && mode <= kGlobalRounds, ROGTK_E_INVALID, "global mode %d outside 0..%d", mode,
-                  kGlobalRounds);
+    ROGTK_REQUIRE(mode >= 0 && mode <= kGlobalRoundsOneFlatten, ROGTK_E_INVALID, "global mode %d outside 0..%d",
+                  mode, kGlobalRoundsOneFlatten);
     g_global_mode.store(mode == 0 ? kGlobalRounds : mode);
     return ROGTK_OK;
 }

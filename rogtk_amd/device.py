@@ -183,7 +183,7 @@ def set_spec_rounds(n: int) -> None:
     _lib.call("rogtk_cluster_set_spec_rounds", int(n))
 
 
-GLOBAL_UNION_FIND, GLOBAL_ROUNDS = 1, 2
+GLOBAL_UNION_FIND, GLOBAL_ROUNDS, GLOBAL_ROUNDS_ONE_FLATTEN = 1, 2, 3
 
 
 def set_global_mode(mode: int) -> None:

@@ -443,9 +443,10 @@ def _chain_codes(rng, L, length, high_bases):
     return np.array([(c << shift0) | low for c in path], dtype=np.uint32)
 
 
+@pytest.mark.parametrize("gm", [2, 3])
 @pytest.mark.parametrize("spec", [1, 2])
 @pytest.mark.parametrize("L", [12, 16])
-def test_deferred_rounds_match(rg, L, spec):
+def test_deferred_rounds_match(rg, L, spec, gm):
     """With fewer speculative rounds than the data needs, the rounds that assign runs
     after the (speculative) labels must give the same clusters: labels never clobber
     the forest."""
@@ -461,7 +462,7 @@ def test_deferred_rounds_match(rg, L, spec):
     eng = D.ClusterEngine(L, n, "cuda")
     cid = torch.empty(n, dtype=torch.int32, device="cuda")
     try:
-        D.set_global_mode(D.GLOBAL_ROUNDS)
+        D.set_global_mode(gm)
         D.set_spec_rounds(spec)
         D.cluster_batch(eng, batch, cid, 1)
         rounds = eng.rounds()
@@ -475,7 +476,7 @@ def test_deferred_rounds_match(rg, L, spec):
     assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc)
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 @pytest.mark.parametrize("L", [12, 16])
 def test_long_chains_need_extra_rounds(rg, L, mode):
     """Long Hamming-1 paths (diameter >> speculative rounds) resolve exactly: the one-pass
@@ -524,7 +525,7 @@ def test_global_modes_identical(rg, L, n):
     batch = D.PackedBatch(codes, L)
     out = {}
     try:
-        for mode in (D.GLOBAL_ROUNDS, D.GLOBAL_UNION_FIND):
+        for mode in (D.GLOBAL_ROUNDS, D.GLOBAL_UNION_FIND, D.GLOBAL_ROUNDS_ONE_FLATTEN):
             D.set_global_mode(mode)
             eng = D.ClusterEngine(L, min(n, 4 ** L), "cuda")
             cid = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -532,8 +533,8 @@ def test_global_modes_identical(rg, L, n):
             out[mode] = (cid.cpu().numpy(), eng.stats()["n_clusters"])
     finally:
         D.set_global_mode(0)
-    assert out[1][1] == out[2][1]
-    assert np.array_equal(out[1][0], out[2][0])
+    assert out[1][1] == out[2][1] == out[3][1]
+    assert np.array_equal(out[1][0], out[2][0]) and np.array_equal(out[3][0], out[2][0])
     if n <= 1_000_000:
         rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L)), L, 1)
         assert out[1][1] == rk
