@@ -453,7 +453,12 @@ int rogtk_copy(void* dst, const void* src, int64_t bytes, void* stream);
  * Diagnostics: the kwargs pickle as the plugin parses it, "key=value" lines. */
 int rogtk_plugin_kwargs_debug(const uint8_t* kwargs, int64_t len, char* out, int64_t cap, int64_t* out_len);
 
+/* Launch-bracketing HIP events (on the launch stream) around the library's kernels. */
 int rogtk_profile_enable(int on);
+/* Restricts the bracketing to one kernel name (below); NULL or "" = every kernel. Each
+ * bracketed launch adds two event records to its stream, so a timed region should
+ * select only the kernel it reports. */
+int rogtk_profile_select(const char* kernel);
 int rogtk_profile_reset(void);
 /* Total device milliseconds and launch count recorded for `kernel` (synchronises
  * the recorded events). Kernel names: "stage", "score_packed", "score_rows",

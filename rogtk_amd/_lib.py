@@ -151,6 +151,7 @@ SIGNATURES = {
     "rogtk_str_fill": [_i32, ctypes.POINTER(StrCol), _i32, _i64, _i64, _vp, _vp, _vp],
     "rogtk_str_transform_host": [_i32, ctypes.POINTER(StrCol), _i32, _i64, _i64, ctypes.POINTER(StrResult)],
     "rogtk_profile_enable": [_i32],
+    "rogtk_profile_select": [ctypes.c_char_p],
     "rogtk_profile_reset": [],
     "rogtk_profile_read": [ctypes.c_char_p, _P_F64, _P_I64],
 }

@@ -40,6 +40,7 @@ const char* const kKernelNames[K_COUNT_] = {
 
 namespace {
 std::atomic<bool> g_prof{false};
+std::atomic<uint32_t> g_prof_mask{~0u};  // kernels bracketed while g_prof is on (bit per KernelId)
 std::mutex g_prof_mu;
 struct ProfRec {
     KernelId id;
@@ -64,7 +65,7 @@ void prof_drain_locked() {
 }  // namespace
 
 ProfScope::ProfScope(KernelId id, hipStream_t stream) : id_(id), stream_(stream) {
-    if (!g_prof.load(std::memory_order_relaxed)) return;
+    if (!g_prof.load(std::memory_order_relaxed) || !((g_prof_mask.load(std::memory_order_relaxed) >> id) & 1u)) return;
     if (hipEventCreate(&start_) != hipSuccess) {
         start_ = nullptr;
         return;
@@ -733,6 +734,20 @@ int rogtk_umi_cluster_dev(const int64_t* offsets, const uint8_t* values, const u
 int rogtk_profile_enable(int on) {
     g_prof.store(on != 0);
     return ROGTK_OK;
+}
+
+int rogtk_profile_select(const char* kernel) {
+    if (!kernel || !kernel[0]) {
+        g_prof_mask.store(~0u);
+        return ROGTK_OK;
+    }
+    for (int k = 0; k < K_COUNT_; ++k)
+        if (std::strcmp(kernel, kKernelNames[k]) == 0) {
+            g_prof_mask.store(1u << k);
+            return ROGTK_OK;
+        }
+    set_error("profile_select: unknown kernel '%s'", kernel);
+    return ROGTK_E_INVALID;
 }
 
 int rogtk_profile_reset(void) {

@@ -244,6 +244,11 @@ def profile_enable(on: bool = True) -> None:
     _lib.call("rogtk_profile_enable", 1 if on else 0)
 
 
+def profile_select(kernel: str | None = None) -> None:
+    """Bracket only `kernel`'s launches with events (None: every kernel)."""
+    _lib.call("rogtk_profile_select", (kernel or "").encode())
+
+
 def profile_reset() -> None:
     _lib.call("rogtk_profile_reset")
 
