@@ -57,9 +57,10 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="skip in-run HIP-event kernel timing")
     ap.add_argument("--iso-launches", type=int, default=10, help="isolated score-kernel launches after timing")
     ap.add_argument("--depth", type=int, default=2, help="batches in flight (1 = no cross-batch overlap)")
-    ap.add_argument("--mark", choices=("auto", "xcd", "fused", "sort"), default="auto",
-                    help="H3 presence bitmap: partition sort + LDS bitmap (auto for umi_len 7..13), "
-                         "XCD-partitioned mark kernel, or mark fused into k_score_packed")
+    ap.add_argument("--mark", choices=("auto", "xcd", "fused", "sort", "slices"), default="auto",
+                    help="H3 presence bitmap: auto (LDS code slices for umi_len 7..12, partition sort for 13), "
+                         "partition sort + LDS bitmap, LDS code slices, XCD-partitioned mark kernel, or mark "
+                         "fused into k_score_packed")
     ap.add_argument("--overlap-score", action="store_true",
                     help="let assign of the previous batch overlap the score kernel (default: score overlaps "
                          "only the latency-bound resolve kernels)")
@@ -67,8 +68,13 @@ def parse():
                     help="(tools) on ONE GPU, act as rank 0 of W: the other W-1 shards' bitmaps are built once "
                          "before timing and the all-gather is replaced by a device copy; predicts per-rank "
                          "step time at N=W minus RCCL time. Never used by the driver.")
-    ap.add_argument("--global-mode", choices=("uf", "rounds", "rounds1f"), default="rounds",
+    ap.add_argument("--global-mode", choices=("uf", "rounds", "rounds1f", "edges"), default="rounds",
                     help="H3 global CC phase: one-pass union-find or hook + jump rounds")
+    ap.add_argument("--assign-on", choices=("resolve", "separate"), default="separate",
+                    help="assign of batch k on its own stream one batch later (default) or behind its "
+                         "resolve on the resolve stream (deferred assign)")
+    ap.add_argument("--resolve-streams", type=int, default=1,
+                    help="resolve streams: consecutive batches resolve concurrently (needs depth > streams)")
     ap.add_argument("--prio", type=str, default="0,0,0", help="stream priorities main,resolve,assign (-1 = high)")
     return ap.parse_args()
 
@@ -197,12 +203,14 @@ def main():
             gathered[: bm.numel()].copy_(bm)
             return gathered, W
 
+    D.set_mark_method({"sort": D.MARK_SORT, "slices": D.MARK_SLICES}.get(args.mark, D.MARK_AUTO))
     D.set_global_mode({"uf": D.GLOBAL_UNION_FIND, "rounds": D.GLOBAL_ROUNDS,
-                       "rounds1f": D.GLOBAL_ROUNDS_ONE_FLATTEN}[args.global_mode])
+                       "rounds1f": D.GLOBAL_ROUNDS_ONE_FLATTEN, "edges": D.GLOBAL_EDGES}[args.global_mode])
     pipe = UmiPipeline(L, min(n_total, 4 ** L), count, dev, depth=args.depth, target=TARGET,
                        max_distance=md, group=None,
                        priorities=tuple(int(x) for x in args.prio.split(",")), mark=args.mark,
-                       score_alone=not args.overlap_score, exchange=exchange)
+                       score_alone=not args.overlap_score, exchange=exchange,
+                       resolve_streams=args.resolve_streams, assign_on=args.assign_on)
 
     def step():
         pipe.submit(batch)
@@ -320,8 +328,10 @@ def main():
                    "reads_per_gpu": count, "umi_len": L, "max_distance": md,
                    "n_distinct": stats["n_distinct"], "n_clusters": stats["n_clusters"],
                    "h3_global": {"uf": "one-pass union-find", "rounds": "hook+jump rounds",
-                                 "rounds1f": "root-chasing hook rounds + one flatten"}[args.global_mode],
-                   "h3_bitmap": "partition sort + LDS bitmap" if pipe.sort_mark else
+                                 "rounds1f": "root-chasing hook rounds + one flatten",
+                                 "edges": "one clique sweep + rounds over the crossing edges"}[args.global_mode],
+                   "h3_bitmap": ("LDS code slices" if args.mark in ("auto", "slices") and 7 <= L <= 12 else
+                                 "partition sort + LDS bitmap") if pipe.sort_mark else
                                 ("mark fused in score kernel" if pipe.fused_mark else "XCD-partitioned mark"),
                    "parallelism": f"dp{world} shard-by-record + presence-bitmap all-gather"
                                   + (f" (rank 0 of {args.emulate_ranks} EMULATED on one GPU, no RCCL)"

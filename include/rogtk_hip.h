@@ -156,6 +156,18 @@ int rogtk_cluster_resolve(void* ws, int umi_len, int64_t max_distinct,
 int rogtk_cluster_assign(const void* ws, int umi_len, int64_t max_distinct,
                          const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
                          uint32_t* cluster_id, void* stream);
+/* The same without the host wait: enqueues the assign right behind the resolve on
+ * `stream` (the speculative rounds converge for almost every input), and remembers it.
+ * rogtk_cluster_sync (or stats / rounds / the next resolve of ws) then checks the round
+ * flags and, if the speculative rounds were not enough, finishes the rounds, relabels
+ * and re-runs this assign on its stream. Read cluster_id only after that check. */
+int rogtk_cluster_assign_deferred(const void* ws, int umi_len, int64_t max_distinct,
+                                  const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
+                                  uint32_t* cluster_id, void* stream);
+/* Completes the pending resolve of ws (and its deferred assign) on `stream`; the host
+ * waits only for the resolve's flag copy. *redone (nullable) = 1 when it had to enqueue
+ * more rounds + labels (+ the deferred assign) on `stream`, else 0. */
+int rogtk_cluster_sync(const void* ws, void* stream, int* redone);
 /* Copies {n_distinct, n_clusters, overflow, error} (int64 each) to host; syncs the stream. */
 int rogtk_cluster_stats(const void* ws, int umi_len, int64_t max_distinct, int64_t* out4,
                         void* stream);
@@ -172,13 +184,22 @@ int rogtk_cluster_set_spec_rounds(int n);
  * LDS. bitmap_out: rogtk_cluster_bitmap_words() words; temp: device scratch of
  * rogtk_cluster_mark_bitmap_temp_bytes(n, umi_len) bytes. Enqueue-only. */
 int rogtk_cluster_mark_bitmap_temp_bytes(int64_t n, int umi_len, int64_t* bytes);
+/* Method of rogtk_cluster_mark_bitmap, process-wide (A/B knob, identical bitmaps):
+ * 0 = auto (code slices in LDS for umi_len <= 12, partition sort for 13), 1 = partition
+ * sort, 2 = code slices (umi_len <= 12). */
+int rogtk_cluster_set_mark_method(int method);
 int rogtk_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
                               uint64_t* bitmap_out, void* temp, int64_t temp_bytes, void* stream);
 /* Global phase of max_distance 1 (positions 7..L-1), process-wide: 2 = bulk-synchronous
  * hook + jump rounds with speculative launch and deferred completion (default; 0
  * restores it), 1 = one-pass lock-free CAS union-find, 3 = hook rounds that chase
- * roots with one flatten per batch of rounds. Identical results (A/B knob). */
+ * roots with one flatten per batch of rounds, 4 = one sweep of the bitmap cliques that
+ * lists the crossing local-root pairs, then rounds over that shrinking edge list (an
+ * overflowing list falls back to mode 2). Identical results (A/B knob). */
 int rogtk_cluster_set_global_mode(int mode);
+/* Tests: edge-list capacity (pairs) of workspaces laid out from now on (mode 4);
+ * 0 restores the default (max_distinct / 2, clamped to 2^16..2^25). Process-wide. */
+int rogtk_cluster_set_edge_cap(int64_t pairs);
 /* Releases the host-side resolve state kept for ws (call before freeing ws). */
 int rogtk_cluster_release(const void* ws);
 

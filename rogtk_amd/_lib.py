@@ -106,11 +106,15 @@ SIGNATURES = {
     "rogtk_cluster_local_bitmap": [_vp, _i32, _i64, _vp, _vp],
     "rogtk_cluster_resolve": [_vp, _i32, _i64, _vp, _i32, _i32, _vp],
     "rogtk_cluster_assign": [_vp, _i32, _i64, _vp, _vp, _i64, _vp, _vp],
+    "rogtk_cluster_assign_deferred": [_vp, _i32, _i64, _vp, _vp, _i64, _vp, _vp],
+    "rogtk_cluster_sync": [_vp, _vp, ctypes.POINTER(ctypes.c_int)],
     "rogtk_cluster_stats": [_vp, _i32, _i64, _P_I64, _vp],
     "rogtk_cluster_release": [_vp],
     "rogtk_cluster_rounds": [_vp, _vp, ctypes.POINTER(ctypes.c_int)],
     "rogtk_cluster_set_spec_rounds": [_i32],
     "rogtk_cluster_set_global_mode": [_i32],
+    "rogtk_cluster_set_edge_cap": [ctypes.c_int64],
+    "rogtk_cluster_set_mark_method": [_i32],
     "rogtk_cluster_mark_bitmap_temp_bytes": [_i64, _i32, _P_I64],
     "rogtk_cluster_mark_bitmap": [_vp, _vp, _i64, _i32, _vp, _vp, _i64, _vp],
     "rogtk_umi_cluster_dev": [_vp, _vp, _vp, _i64, _i32, _i32, _vp, ctypes.POINTER(_i64), _vp],

@@ -469,6 +469,22 @@ int rogtk_cluster_assign(const void* ws, int umi_len, int64_t max_distinct, cons
                                  as_stream(stream));
 }
 
+int rogtk_cluster_assign_deferred(const void* ws, int umi_len, int64_t max_distinct, const uint32_t* codes,
+                                  const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id, void* stream) {
+    ClusterLayout cl;
+    if (int rc = cluster_layout(umi_len, max_distinct, &cl)) return rc;
+    ROGTK_REQUIRE(ws && (n == 0 || (codes && cluster_id)), ROGTK_E_INVALID, "assign: NULL buffer");
+    ROGTK_REQUIRE(aligned16(codes) && aligned16(cluster_id), ROGTK_E_INVALID,
+                  "assign: codes/cluster_id must be 16-byte aligned");
+    return launch_cluster_assign(cl, (const uint8_t*)ws, codes, regular_bits, n, cluster_id, as_stream(stream),
+                                 true);
+}
+
+int rogtk_cluster_sync(const void* ws, void* stream, int* redone) {
+    ROGTK_REQUIRE(ws, ROGTK_E_INVALID, "ws is NULL");
+    return cluster_finish(ws, as_stream(stream), redone);
+}
+
 int rogtk_cluster_stats(const void* ws, int umi_len, int64_t max_distinct, int64_t* out4,
                         void* stream) {
     ClusterLayout cl;
@@ -488,6 +504,8 @@ int rogtk_cluster_rounds(const void* ws, void* stream, int* rounds) {
 
 int rogtk_cluster_set_spec_rounds(int n) { return cluster_set_spec_rounds(n); }
 int rogtk_cluster_set_global_mode(int mode) { return cluster_set_global_mode(mode); }
+int rogtk_cluster_set_edge_cap(int64_t pairs) { return cluster_set_edge_cap(pairs); }
+int rogtk_cluster_set_mark_method(int method) { return cluster_set_mark_method(method); }
 int rogtk_cluster_mark_bitmap_temp_bytes(int64_t n, int umi_len, int64_t* bytes) {
     ROGTK_REQUIRE(bytes, ROGTK_E_INVALID, "null bytes");
     return cluster_mark_bitmap_temp(n, umi_len, bytes);

@@ -41,6 +41,7 @@
 #include <mutex>
 
 #include <atomic>
+#include <thread>
 
 #include "rogtk_internal.h"
 
@@ -56,8 +57,13 @@ constexpr int kRoundBatch = 4;
 
 // stats block (int64 slots): 0 n_distinct, 1 n_clusters, 2 overflow, 3 error,
 // 4 rounds run; round flags (u32 per round) follow at byte 64.
-enum StatSlot { S_NDISTINCT = 0, S_NCLUSTERS = 1, S_OVERFLOW = 2, S_ERROR = 3, S_ROUNDS = 4 };
-constexpr int kStatsBytes = 64 + 4 * kMaxRounds;
+// S_EDGE_OVF: the edge list of the global phase (mode 4) overflowed its capacity.
+enum StatSlot { S_NDISTINCT = 0, S_NCLUSTERS = 1, S_OVERFLOW = 2, S_ERROR = 3, S_ROUNDS = 4, S_EDGE_OVF = 5 };
+// stats (8 x int64), round flags (u32 per round) at byte 64, edge-list counts (u32 per
+// round, +1) after them
+constexpr int kFlagsOff = 64;
+constexpr int kEcntOff = kFlagsOff + 4 * kMaxRounds;
+constexpr int kStatsBytes = kEcntOff + 4 * (kMaxRounds + 2);
 
 __device__ __forceinline__ uint64_t rt_word(const uint4 e) { return (uint64_t)e.x | ((uint64_t)e.y << 32); }
 
@@ -577,6 +583,10 @@ __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ R
 // Per-workgroup hook table in LDS: (root -> smallest proposed parent). Cliques that
 // cross stars insert here; the block flushes one global atomicMin per distinct root.
 constexpr int kHookSlots = 1024;
+// ROGTK_EDGE_ATOMIC_HOOK=1: hooks by memory-side atomicMin instead of plain stores (A/B)
+#ifndef ROGTK_EDGE_ATOMIC_HOOK
+#define ROGTK_EDGE_ATOMIC_HOOK 0
+#endif
 
 struct HookTable {
     uint32_t key[kHookSlots];
@@ -717,7 +727,10 @@ __global__ __launch_bounds__(kBlock) void k_hook_g(const uint4* __restrict__ RT,
     __syncthreads();
     for (int k = threadIdx.x; k < kHookSlots; k += kBlock) {
         const uint32_t x = T.key[k];
-        if (x != kNone && T.val[k] < f[x]) atomicMin(f + x, T.val[k]);
+        if (x == kNone) continue;
+        // atomicMin, not a plain store: with "smallest proposal wins" synth-v1 converges
+        // in 3 productive rounds, with "any proposal wins" in 4 (measured)
+        if (T.val[k] < f[x]) atomicMin(f + x, T.val[k]);
     }
 }
 
@@ -871,6 +884,228 @@ __global__ __launch_bounds__(kBlock) void k_flatten_live(uint32_t* f, const uint
         if (r == (uint32_t)i) continue;
         for (uint32_t q = f[r]; q != r; q = f[r]) r = q;
         f[i] = r;
+    }
+}
+
+// ------------------------------------------- global CC over an edge list (mode 4)
+// Round 0 (k_sweep_edges) walks the same word-group cliques as k_hook_g once: it finds
+// the local roots of each clique's members (UR or f after k_local_cc), keeps the pairs
+// of different roots in a per-workgroup LDS set (many cliques of a block share a pair),
+// hooks the larger root of every distinct pair under the smaller and appends
+// the pair to an edge list. Every later round (k_edge_hook) walks only the edges that
+// crossed in the round before: an edge whose ends share a root stays internal for good.
+// k_edge_jump compresses the surviving edges' ends to their roots between rounds, so
+// that a hook reads one f per end; one k_flatten_live after the last round makes every
+// live vertex point at its root for the labels. The set of hooks of a round is the one
+// of the bulk-synchronous rounds (roots only merge under the smallest proposal), so the
+// components - rooted at their smallest vertex - and the ids are the same.
+constexpr int kPairSlots = 2048;  // 16 KB of LDS per workgroup
+constexpr unsigned long long kNoPair = ~0ull;
+
+struct EdgeSink {
+    uint2* E;                  // output list {lo, hi}
+    unsigned int* cnt;         // its device count (may run past cap: then ovf is set)
+    unsigned int cap;
+    unsigned long long* ovf;   // stats[S_EDGE_OVF]
+};
+
+// Hook root hi under lo with a PLAIN store (no memory-side atomic): when several pairs
+// of one round hook the same root, any one of them may win (each written lo is a root
+// of this round and smaller than hi, so the forest stays acyclic and no tree splits),
+// and every losing pair is in the list of crossing edges the next round re-checks.
+__device__ __forceinline__ void hook_store(uint32_t* f, uint32_t lo, uint32_t hi) {
+#if ROGTK_EDGE_ATOMIC_HOOK
+    if (lo < f[hi]) atomicMin(f + hi, lo);
+#else
+    if (lo < f[hi]) f[hi] = lo;
+#endif
+}
+
+__device__ __forceinline__ void edge_append(const EdgeSink& o, uint32_t lo, uint32_t hi) {
+    const unsigned int at = atomicAdd(o.cnt, 1u);
+    if (at < o.cap) o.E[at] = make_uint2(lo, hi);
+    else *o.ovf = 1ull;
+}
+
+// LDS pair set: open addressing on the 64-bit key (lo << 32 | hi); a crowded table
+// sends the pair straight to the list (and to the hook), so nothing is dropped.
+__device__ __forceinline__ void pair_put(unsigned long long* T, const EdgeSink& o, uint32_t* f, uint32_t lo,
+                                         uint32_t hi) {
+    const unsigned long long k = ((unsigned long long)lo << 32) | hi;
+    uint32_t h = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 53);  // 11 bits
+    for (int probe = 0; probe < 32; ++probe, h = (h + 1) & (kPairSlots - 1)) {
+        unsigned long long cur = T[h];
+        if (cur == k) return;
+        if (cur == kNoPair) {
+            cur = atomicCAS(&T[h], kNoPair, k);
+            if (cur == kNoPair || cur == k) return;
+        }
+    }
+    hook_store(f, lo, hi);
+    edge_append(o, lo, hi);
+}
+
+__device__ __forceinline__ void pairs_init(unsigned long long* T) {
+    for (int k = threadIdx.x; k < kPairSlots; k += kBlock) T[k] = kNoPair;
+}
+
+// Hook every distinct pair of the block (larger root under the smaller) and append it
+// to the list with one atomicAdd per block.
+__device__ __forceinline__ void pairs_flush(unsigned long long* T, const EdgeSink& o, uint32_t* f,
+                                            uint32_t* s_wave, unsigned int* s_base) {
+    __syncthreads();
+    constexpr int kPer = kPairSlots / kBlock;  // contiguous slots per thread
+    unsigned long long mine[kPer];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        mine[k] = T[threadIdx.x * kPer + k];
+        cnt += mine[k] != kNoPair;
+    }
+    uint32_t total;
+    uint32_t ex = block_excl_scan(cnt, s_wave, total);
+    if (threadIdx.x == 0) *s_base = total ? atomicAdd(o.cnt, total) : 0u;
+    __syncthreads();
+    if (!total) return;
+    const unsigned int base = *s_base;
+    if (threadIdx.x == 0 && (uint64_t)base + total > o.cap) *o.ovf = 1ull;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        if (mine[k] == kNoPair) continue;
+        const uint32_t lo = (uint32_t)(mine[k] >> 32), hi = (uint32_t)mine[k];
+        hook_store(f, lo, hi);
+        const uint64_t at = (uint64_t)base + ex++;
+        if (at < o.cap) o.E[at] = make_uint2(lo, hi);
+    }
+}
+
+__device__ __forceinline__ void put_clique(unsigned long long* T, const EdgeSink& o, uint32_t* f, const uint32_t* x,
+                                           int k, bool& crossed) {
+    uint32_t mn = kNone;
+    for (int v = 0; v < k; ++v) mn = x[v] < mn ? x[v] : mn;
+    for (int v = 0; v < k; ++v)
+        if (x[v] != mn) {
+            crossed = true;
+            pair_put(T, o, f, mn, x[v]);
+        }
+}
+
+// Round 0: positions p0..L-1 as word-group cliques (the tasks of k_hook_g).
+__global__ __launch_bounds__(kBlock) void k_sweep_edges(const uint4* __restrict__ RT, const uint32_t* __restrict__ UR,
+                                                        int64_t words, int L, int p0, uint32_t* f, EdgeSink o,
+                                                        unsigned int* __restrict__ flags) {
+    __shared__ unsigned long long T[kPairSlots];
+    __shared__ uint32_t s_wave[kBlock / 64];
+    __shared__ unsigned int s_base;
+    pairs_init(T);
+    __syncthreads();
+    const int64_t per = words >> 2;
+    const int64_t tasks = (int64_t)(L - p0) * per;
+    const int64_t u = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    bool crossed = false;
+    if (per > 0 && u < tasks) {
+        const int p = p0 + (int)(u / per);
+        const int64_t g = u % per;
+        const int s2 = 2 * p - 6;
+        const int64_t stride = 1ll << s2;
+        const int64_t w0 = ((g >> s2) << (s2 + 2)) | (g & (stride - 1));
+        uint4 e[4];
+        uint64_t m[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            e[v] = RT[w0 + v * stride];
+            m[v] = rt_word(e[v]);
+        }
+        const uint64_t multi = multi_of4(m[0], m[1], m[2], m[3]);
+        if (multi) {
+            uint32_t root[4];
+            bool all_uniform = true;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                root[v] = kNone;
+                if (m[v] & multi) {
+                    root[v] = UR[w0 + v * stride];
+                    all_uniform &= root[v] != kNone;
+                }
+            }
+            uint32_t x[4];
+            if (all_uniform) {
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+#pragma unroll
+                    for (int b = a + 1; b < 4; ++b)
+                        if ((m[a] & m[b]) && root[a] != root[b]) {
+                            x[0] = root[a];
+                            x[1] = root[b];
+                            put_clique(T, o, f, x, 2, crossed);
+                        }
+            } else {
+                uint64_t mm = multi;
+                while (mm) {
+                    const int b = __ffsll((long long)mm) - 1;
+                    mm &= mm - 1;
+                    const uint64_t below = (1ull << b) - 1ull;
+                    int k = 0;
+#pragma unroll
+                    for (int v = 0; v < 4; ++v)
+                        if ((m[v] >> b) & 1ull)
+                            x[k++] = root[v] != kNone ? root[v] : f[e[v].z + (uint32_t)__popcll(m[v] & below)];
+                    put_clique(T, o, f, x, k, crossed);
+                }
+            }
+        }
+    }
+    if (__syncthreads_or(crossed) && threadIdx.x == 0) flags[0] = 1u;
+    pairs_flush(T, o, f, s_wave, &s_base);
+}
+
+// Round r >= 1 over the edges that crossed in round r - 1 (their ends are roots after
+// k_edge_jump); survivors go to the next list.
+__global__ __launch_bounds__(kBlock) void k_edge_hook(const uint2* __restrict__ Ein, const unsigned int* __restrict__ nin,
+                                                      EdgeSink o, uint32_t* f, unsigned int* __restrict__ flags,
+                                                      int round, const unsigned long long* __restrict__ stats) {
+    if (flags[round - 1] == 0) return;  // converged earlier
+    if (stats[S_EDGE_OVF]) {            // the host falls back to the rounds; never "converged" here
+        if (blockIdx.x == 0 && threadIdx.x == 0) flags[round] = 1u;
+        return;
+    }
+    const uint32_t n = min(*nin, o.cap);
+    if ((uint64_t)blockIdx.x * kBlock >= n) return;
+    __shared__ unsigned long long T[kPairSlots];
+    __shared__ uint32_t s_wave[kBlock / 64];
+    __shared__ unsigned int s_base;
+    pairs_init(T);
+    __syncthreads();
+    bool crossed = false;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const uint2 ed = Ein[i];
+        const uint32_t ra = f[ed.x], rb = f[ed.y];
+        if (ra != rb) {
+            crossed = true;
+            pair_put(T, o, f, min(ra, rb), max(ra, rb));
+        }
+    }
+    if (__syncthreads_or(crossed) && threadIdx.x == 0) flags[round] = 1u;
+    pairs_flush(T, o, f, s_wave, &s_base);
+}
+
+// Compress both ends of every edge that crossed in `round` to their roots.
+__global__ __launch_bounds__(kBlock) void k_edge_jump(const uint2* __restrict__ E, const unsigned int* __restrict__ n_p,
+                                                      unsigned int cap, uint32_t* f,
+                                                      const unsigned int* __restrict__ flags, int round,
+                                                      const unsigned long long* __restrict__ stats) {
+    if (flags[round] == 0 || stats[S_EDGE_OVF]) return;
+    const uint32_t n = min(*n_p, cap);
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const uint2 ed = E[i];
+        const uint32_t xs[2] = {ed.x, ed.y};
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            uint32_t r = f[xs[k]];
+            if (r == xs[k]) continue;
+            for (uint32_t q = f[r]; q != r; q = f[r]) r = q;
+            f[xs[k]] = r;
+        }
     }
 }
 
@@ -1030,12 +1265,14 @@ struct WsPtrs {
     uint64_t *rbits, *lroot;
     uint32_t *rpref, *rblksum, *rblkoff, *labelcode, *ilab;
     uint64_t* active;
+    uint2* edges;             // two lists of ecap pairs
+    unsigned int* ecnt;       // per-round list counts (stats block)
 };
 
 inline WsPtrs ws_ptrs(const ClusterLayout& cl, uint8_t* ws) {
     WsPtrs p;
     p.stats = (unsigned long long*)(ws + cl.off_stats);
-    p.flags = (unsigned int*)(ws + cl.off_stats + 64);
+    p.flags = (unsigned int*)(ws + cl.off_stats + kFlagsOff);
     p.presence = ws + cl.off_presence;
     p.G = (uint64_t*)(ws + cl.off_bitmap);
     p.RT = (uint4*)(ws + cl.off_rt);
@@ -1053,12 +1290,25 @@ inline WsPtrs ws_ptrs(const ClusterLayout& cl, uint8_t* ws) {
     p.labelcode = cl.label_by_code ? (uint32_t*)(ws + cl.off_labelcode) : nullptr;
     p.ilab = cl.label_by_code ? nullptr : (uint32_t*)(ws + cl.off_ilab);
     p.active = (uint64_t*)(ws + cl.off_active);
+    p.edges = (uint2*)(ws + cl.off_edges);
+    p.ecnt = (unsigned int*)(ws + cl.off_stats + kEcntOff);
     return p;
 }
 
 constexpr int64_t kPersistentGrid = 2048;  // 256 CUs x 8 blocks
 
 }  // namespace
+
+namespace {
+std::atomic<int64_t> g_edge_cap{0};  // 0: derived from max_distinct (rogtk_cluster_set_edge_cap)
+}  // namespace
+
+int cluster_set_edge_cap(int64_t pairs) {
+    ROGTK_REQUIRE(pairs >= 0 && pairs <= (1ll << 30), ROGTK_E_INVALID, "edge cap %lld outside 0..2^30",
+                  (long long)pairs);
+    g_edge_cap.store(pairs);
+    return ROGTK_OK;
+}
 
 int cluster_layout(int L, int64_t max_distinct, ClusterLayout* o) {
     ROGTK_REQUIRE(L >= 1 && L <= kMaxPackedLen, ROGTK_E_UNSUPPORTED,
@@ -1107,6 +1357,14 @@ int cluster_layout(int L, int64_t max_distinct, ClusterLayout* o) {
     const int64_t tasks = L > kLocalPos ? (int64_t)(L - kLocalPos) * (c.words >> 2) : 0;
     c.active_words = (tasks + 63) / 64;
     c.off_active = take(2 * std::max<int64_t>(c.active_words, 1) * 8);
+    // global phase over an edge list (mode 4): two lists of {lo, hi} root pairs. The
+    // capacity is a generous multiple of what synth-v1 needs (0.05 pairs per distinct
+    // UMI at 10M reads); an overflow falls back to the bitmap rounds.
+    const int64_t ecap_set = g_edge_cap.load();
+    c.ecap = L <= kLocalPos ? 0
+             : ecap_set   ? ecap_set
+                          : std::min<int64_t>(std::max<int64_t>(max_distinct / 2, 65536), 1ll << 25);
+    c.off_edges = take(2 * std::max<int64_t>(c.ecap, 1) * 8);
     c.total = off;
     *o = c;
     return ROGTK_OK;
@@ -1183,6 +1441,7 @@ std::atomic<int> g_spec_rounds{kSpecRounds};
 constexpr int kGlobalUnionFind = 1;
 constexpr int kGlobalRounds = 2;
 constexpr int kGlobalRoundsOneFlatten = 3;  // hook rounds that chase roots, one flatten per batch
+constexpr int kGlobalEdges = 4;             // one clique sweep, then rounds over the crossing edges
 std::atomic<int> g_global_mode{kGlobalRounds};
 
 // Host-side state of an in-flight resolve, keyed by workspace: the round flags are
@@ -1191,20 +1450,54 @@ std::atomic<int> g_global_mode{kGlobalRounds};
 // rounds were not enough, runs more rounds and relabels.
 struct ResolveState {
     hipEvent_t ev = nullptr;
-    unsigned int* hflags = nullptr;  // pinned, kMaxRounds entries
+    uint8_t* hstats = nullptr;  // pinned copy of the stats block (round flags, edge overflow)
     int launched = 0;
+    int mode = 0;  // global mode of the pending resolve
     bool pending = false;
     int rounds = 0;  // hook rounds the last resolve needed (the converged round included)
     bool word_labels = false;  // wpref holds word labels (max_distance 1)
     ClusterLayout cl{};
+    // an assign enqueued before the flags were checked (rogtk_cluster_assign_deferred)
+    struct {
+        bool on = false;
+        const uint32_t* codes;
+        const uint64_t* regbits;
+        int64_t n;
+        uint32_t* cid;
+    } deferred;
 };
 std::mutex g_rs_mu;
 std::map<const void*, ResolveState> g_rs;
 
-int enqueue_rounds(const ClusterLayout& cl, const WsPtrs& p, int from, int to, hipStream_t s) {
+EdgeSink edge_sink(const ClusterLayout& cl, const WsPtrs& p, int round) {
+    // the list produced by round r (the input of round r + 1) lives in buffer (r + 1) & 1
+    EdgeSink o;
+    o.E = p.edges + (int64_t)((round + 1) & 1) * cl.ecap;
+    o.cnt = p.ecnt + round + 1;
+    o.cap = (unsigned int)cl.ecap;
+    o.ovf = p.stats + S_EDGE_OVF;
+    return o;
+}
+
+int enqueue_rounds(const ClusterLayout& cl, const WsPtrs& p, int from, int to, hipStream_t s, int mode) {
     const int pg = grid_for(cl.max_distinct, kPersistentGrid);
     const int64_t tasks = (int64_t)(cl.L - kLocalPos) * (cl.words >> 2);
-    if (g_global_mode.load() == kGlobalRoundsOneFlatten) {
+    if (mode == kGlobalEdges) {
+        const int eg = grid_for(cl.ecap, kPersistentGrid);
+        for (int k = from; k < to; ++k) {
+            const EdgeSink o = edge_sink(cl, p, k);
+            if (k == 0) {
+                hipLaunchKernelGGL(k_sweep_edges, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words,
+                                   cl.L, kLocalPos, p.f, o, p.flags);
+            } else {
+                const uint2* ein = p.edges + (int64_t)(k & 1) * cl.ecap;
+                hipLaunchKernelGGL(k_edge_hook, dim3(eg), dim3(kBlock), 0, s, ein, p.ecnt + k, o, p.f, p.flags, k,
+                                   (const unsigned long long*)p.stats);
+            }
+            hipLaunchKernelGGL(k_edge_jump, dim3(eg), dim3(kBlock), 0, s, o.E, o.cnt, o.cap, p.f, p.flags, k,
+                               (const unsigned long long*)p.stats);
+        }
+    } else if (mode == kGlobalRoundsOneFlatten) {
         // hooks chase to the roots themselves; one flatten after the batch of rounds
         for (int k = from; k < to; ++k)
             hipLaunchKernelGGL(k_hook_g<true>, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words, cl.L,
@@ -1218,6 +1511,15 @@ int enqueue_rounds(const ClusterLayout& cl, const WsPtrs& p, int from, int to, h
                                k);
         }
     }
+    ROGTK_HIP_CHECK(hipGetLastError());
+    return ROGTK_OK;
+}
+
+// After the last round of the edge mode: every live vertex points at its root.
+int enqueue_post_rounds(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s, int mode) {
+    if (mode != kGlobalEdges) return ROGTK_OK;
+    hipLaunchKernelGGL(k_flatten_live, dim3(grid_for(cl.max_distinct, kPersistentGrid)), dim3(kBlock), 0, s, p.f,
+                       p.lroot, cl.max_distinct, p.stats);
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
 }
@@ -1255,12 +1557,22 @@ int first_zero(const unsigned int* f, int from, int to) {
 
 }  // namespace
 
+namespace {
+int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, bool word_labels, const uint32_t* codes,
+                   const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id, hipStream_t s);
+int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone = nullptr);
+}  // namespace
+
 int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t* bitmaps,
                            int n_bitmaps, int max_distance, hipStream_t s) {
     WsPtrs p = ws_ptrs(cl, ws);
     std::lock_guard<std::mutex> lk(g_rs_mu);
     ResolveState& st = g_rs[ws];
+    if (st.pending && st.deferred.on) {  // a deferred assign must see its resolve complete first
+        if (int rc = finish_locked(ws, st, s)) return rc;
+    }
     st.pending = false;
+    st.deferred.on = false;
     st.rounds = 0;
     st.cl = cl;
     st.word_labels = max_distance == 1;
@@ -1302,54 +1614,91 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
             st.rounds = 1;
         } else if (cl.L > kLocalPos) {
             const int spec = g_spec_rounds.load();
-            if (int rc = enqueue_rounds(cl, p, 0, spec, s)) return rc;
+            st.mode = g_global_mode.load();
+            if (int rc = enqueue_rounds(cl, p, 0, spec, s, st.mode)) return rc;
             if (!st.ev) {
                 ROGTK_HIP_CHECK(hipEventCreateWithFlags(&st.ev, hipEventDisableTiming));
-                ROGTK_HIP_CHECK(hipHostMalloc((void**)&st.hflags, kMaxRounds * sizeof(unsigned int),
-                                              hipHostMallocDefault));
+                ROGTK_HIP_CHECK(hipHostMalloc((void**)&st.hstats, kStatsBytes, hipHostMallocDefault));
             }
-            ROGTK_HIP_CHECK(hipMemcpyAsync(st.hflags, p.flags, spec * sizeof(unsigned int),
-                                           hipMemcpyDeviceToHost, s));
+            ROGTK_HIP_CHECK(hipMemcpyAsync(st.hstats, p.stats, kStatsBytes, hipMemcpyDeviceToHost, s));
             ROGTK_HIP_CHECK(hipEventRecord(st.ev, s));
             st.launched = spec;
             st.pending = true;
+            if (int rc = enqueue_post_rounds(cl, p, s, st.mode)) return rc;
         }
     }
     return enqueue_labels(cl, p, s);
 }
 
-int cluster_finish(const void* ws, hipStream_t s) {
+int cluster_finish(const void* ws, hipStream_t s, int* redone) {
+    if (redone) *redone = 0;
     std::lock_guard<std::mutex> lk(g_rs_mu);
     auto it = g_rs.find(ws);
     if (it == g_rs.end() || !it->second.pending) return ROGTK_OK;
-    ResolveState& st = it->second;
-    ROGTK_HIP_CHECK(hipEventSynchronize(st.ev));
-    if (int z = first_zero(st.hflags, 0, st.launched); z >= 0) {
-        st.pending = false;
-        st.rounds = z + 1;
-        return ROGTK_OK;
+    return finish_locked(ws, it->second, s, redone);
+}
+
+namespace {
+int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone) {
+    // Spin on the event: a blocking hipEventSynchronize woke up ~0.2 ms after the flags
+    // copy completed in the pipelined bench, which delayed the assign launch behind it.
+    for (;;) {
+        const hipError_t q = hipEventQuery(st.ev);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) ROGTK_HIP_CHECK(q);
+        std::this_thread::yield();
+    }
+    unsigned int* hflags = (unsigned int*)(st.hstats + kFlagsOff);
+    const bool edge_ovf = st.mode == kGlobalEdges && ((const unsigned long long*)st.hstats)[S_EDGE_OVF] != 0;
+    if (!edge_ovf) {
+        if (int z = first_zero(hflags, 0, st.launched); z >= 0) {
+            st.pending = false;
+            st.deferred.on = false;
+            st.rounds = z + 1;
+            return ROGTK_OK;
+        }
     }
     // the speculative rounds were not enough: continue synchronously, then relabel
+    if (redone) *redone = 1;
     WsPtrs p = ws_ptrs(st.cl, const_cast<uint8_t*>((const uint8_t*)ws));
+    if (edge_ovf) {
+        // the edge list overflowed (the round-0 hooks stand): stars again, then the
+        // bitmap rounds from round 0
+        ProfScope prof(K_UNION, s);
+        hipLaunchKernelGGL(k_flatten_live, dim3(grid_for(st.cl.max_distinct, kPersistentGrid)), dim3(kBlock), 0, s,
+                           p.f, p.lroot, st.cl.max_distinct, p.stats);
+        ROGTK_HIP_CHECK(hipGetLastError());
+        ROGTK_HIP_CHECK(hipMemsetAsync(p.flags, 0, kMaxRounds * sizeof(unsigned int), s));
+        st.mode = kGlobalRounds;
+        st.launched = 0;
+    }
     bool converged = false;
     while (!converged && st.launched < kMaxRounds) {
         const int to = std::min(st.launched + kRoundBatch, kMaxRounds);
         {
             ProfScope prof(K_UNION, s);
-            if (int rc = enqueue_rounds(st.cl, p, st.launched, to, s)) return rc;
+            if (int rc = enqueue_rounds(st.cl, p, st.launched, to, s, st.mode)) return rc;
         }
-        ROGTK_HIP_CHECK(hipMemcpyAsync(st.hflags + st.launched, p.flags + st.launched,
+        ROGTK_HIP_CHECK(hipMemcpyAsync(hflags + st.launched, p.flags + st.launched,
                                        (to - st.launched) * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
         ROGTK_HIP_CHECK(hipStreamSynchronize(s));
-        const int z = first_zero(st.hflags, st.launched, to);
+        const int z = first_zero(hflags, st.launched, to);
         converged = z >= 0;
         if (converged) st.rounds = z + 1;
         st.launched = to;
     }
     st.pending = false;
     ROGTK_REQUIRE(converged, ROGTK_E_HIP, "cluster: union rounds did not converge in %d rounds", kMaxRounds);
-    return enqueue_labels(st.cl, p, s);
+    if (int rc = enqueue_post_rounds(st.cl, p, s, st.mode)) return rc;
+    if (int rc = enqueue_labels(st.cl, p, s)) return rc;
+    if (st.deferred.on) {  // the assign that ran on the speculative labels, again
+        st.deferred.on = false;
+        return enqueue_assign(st.cl, p, st.word_labels, st.deferred.codes, st.deferred.regbits, st.deferred.n,
+                              st.deferred.cid, s);
+    }
+    return ROGTK_OK;
 }
+}  // namespace
 
 int cluster_set_spec_rounds(int n) {
     ROGTK_REQUIRE(n >= 0 && n <= kMaxRounds, ROGTK_E_INVALID, "spec rounds %d outside 0..%d", n, kMaxRounds);
@@ -1358,8 +1707,8 @@ int cluster_set_spec_rounds(int n) {
 }
 
 int cluster_set_global_mode(int mode) {
-    ROGTK_REQUIRE(mode >= 0 && mode <= kGlobalRoundsOneFlatten, ROGTK_E_INVALID, "global mode %d outside 0..%d",
-                  mode, kGlobalRoundsOneFlatten);
+    ROGTK_REQUIRE(mode >= 0 && mode <= kGlobalEdges, ROGTK_E_INVALID, "global mode %d outside 0..%d", mode,
+                  kGlobalEdges);
     g_global_mode.store(mode == 0 ? kGlobalRounds : mode);
     return ROGTK_OK;
 }
@@ -1380,23 +1729,40 @@ void cluster_release(const void* ws) {
         hipEventSynchronize(it->second.ev);
         hipEventDestroy(it->second.ev);
     }
-    if (it->second.hflags) hipHostFree(it->second.hflags);
+    if (it->second.hstats) hipHostFree(it->second.hstats);
     g_rs.erase(it);
 }
 
 int launch_cluster_assign(const ClusterLayout& cl, const uint8_t* ws, const uint32_t* codes,
                           const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id,
-                          hipStream_t s) {
-    if (int rc = cluster_finish(ws, s)) return rc;
-    if (n <= 0) return ROGTK_OK;
+                          hipStream_t s, bool deferred) {
+    if (!deferred)
+        if (int rc = cluster_finish(ws, s)) return rc;
     WsPtrs p = ws_ptrs(cl, const_cast<uint8_t*>(ws));
     bool wl = false;
     {
         std::lock_guard<std::mutex> lk(g_rs_mu);
         auto it = g_rs.find(ws);
-        wl = it != g_rs.end() && it->second.word_labels;
+        if (it != g_rs.end()) {
+            wl = it->second.word_labels;
+            if (deferred && it->second.pending) {
+                auto& d = it->second.deferred;
+                d.on = true;
+                d.codes = codes;
+                d.regbits = regular_bits;
+                d.n = n;
+                d.cid = cluster_id;
+            }
+        }
     }
-    const uint32_t* wlab = wl ? p.wpref : nullptr;
+    return enqueue_assign(cl, p, wl, codes, regular_bits, n, cluster_id, s);
+}
+
+namespace {
+int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, bool word_labels, const uint32_t* codes,
+                   const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id, hipStream_t s) {
+    if (n <= 0) return ROGTK_OK;
+    const uint32_t* wlab = word_labels ? p.wpref : nullptr;
     ProfScope prof(K_ASSIGN, s);
     const int g = grid_for((n + 3) / 4);
     if (cl.label_by_code)
@@ -1408,6 +1774,7 @@ int launch_cluster_assign(const ClusterLayout& cl, const uint8_t* ws, const uint
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
 }
+}  // namespace
 
 
 
@@ -1491,6 +1858,81 @@ __global__ __launch_bounds__(kPartBlock) void k_part_bitmap(const uint32_t* __re
         out[k] = (uint64_t)lbits[2 * k] | ((uint64_t)lbits[2 * k + 1] << 32);
 }
 
+// ---- mark by code slices in LDS (umi_len 7..12, default)
+// The code space is cut into slices of 2^20 codes (128 KB of LDS as a bitmap) and the
+// rows into kSliceChunks chunks; workgroup (slice s, chunk c) reads chunk c's codes and
+// sets the bits of the codes that fall in slice s, then stores its slice of chunk c's
+// partial bitmap; one pass ORs the chunks' partials. Every code is read once from HBM:
+// the slices of one chunk are the workgroups b = s * chunks + c, which share the XCD
+// c % 8 under the round-robin placement (measured exact; speed only), so their repeated
+// reads of the chunk hit that XCD's L2. No sort, no scattered global stores.
+constexpr int kSliceBlock = 1024;
+constexpr int kSliceChunks = 16;   // a multiple of the 8 XCDs
+constexpr int kSliceLog2 = 20;     // codes per slice (LDS bits)
+
+__global__ __launch_bounds__(kSliceBlock) void k_slice_mark(const uint32_t* __restrict__ codes,
+                                                            const uint64_t* __restrict__ regbits, int64_t n,
+                                                            int slice_log2, int chunks, int64_t chunk_rows,
+                                                            uint64_t* __restrict__ out, int64_t words) {
+    __shared__ uint32_t sbits[(1u << kSliceLog2) / 32];  // 128 KB: the slice's bits (2^slice_log2 used)
+    const int c = blockIdx.x % chunks, sl = blockIdx.x / chunks;
+    const uint32_t sw32 = (1u << slice_log2) >> 5;
+    for (uint32_t k = threadIdx.x; k < sw32; k += kSliceBlock) sbits[k] = 0;
+    __syncthreads();
+    const uint32_t smask = (1u << slice_log2) - 1u;
+    const int64_t r0 = (int64_t)c * chunk_rows, r1 = min(n, r0 + chunk_rows);
+    // kSliceUnroll independent 16-B loads in flight per lane before the LDS atomics that
+    // consume them (one load per iteration left the kernel latency-bound: 125 us)
+    constexpr int kSliceUnroll = 8;
+    constexpr int64_t kStep = 4 * (int64_t)kSliceBlock;
+    for (int64_t rb = r0 + 4 * (int64_t)threadIdx.x; rb < r1; rb += kStep * kSliceUnroll) {
+        uint4 v[kSliceUnroll];
+        uint32_t reg[kSliceUnroll];
+#pragma unroll
+        for (int u = 0; u < kSliceUnroll; ++u) {
+            const int64_t r = rb + u * kStep;
+            reg[u] = 0;
+            v[u] = make_uint4(0, 0, 0, 0);
+            if (r + 4 <= r1) {
+                v[u] = *reinterpret_cast<const uint4*>(codes + r);
+                reg[u] = regbits ? (uint32_t)(regbits[r >> 6] >> (r & 63)) & 0xFu : 0xFu;  // r % 4 == 0
+            } else if (r < r1) {
+                v[u].x = codes[r];
+                if (r + 1 < r1) v[u].y = codes[r + 1];
+                if (r + 2 < r1) v[u].z = codes[r + 2];
+                reg[u] = (regbits ? (uint32_t)(regbits[r >> 6] >> (r & 63)) & 0xFu : 0xFu) &
+                         ((1u << (uint32_t)(r1 - r)) - 1u);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kSliceUnroll; ++u) {
+            const uint32_t cc[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (((reg[u] >> k) & 1u) && (cc[k] >> slice_log2) == (uint32_t)sl) {  // codes >= 4^L never match
+                    const uint32_t b = cc[k] & smask;
+                    atomicOr(&sbits[b >> 5], 1u << (b & 31));
+                }
+        }
+    }
+    __syncthreads();
+    uint64_t* o = out + (int64_t)c * words + (((int64_t)sl << slice_log2) >> 6);
+    for (uint32_t k = threadIdx.x; k < sw32 / 2; k += kSliceBlock)
+        o[k] = (uint64_t)sbits[2 * k] | ((uint64_t)sbits[2 * k + 1] << 32);
+}
+
+__global__ __launch_bounds__(kBlock) void k_or_partials(const uint64_t* __restrict__ partials, int chunks,
+                                                        int64_t words, uint64_t* __restrict__ out) {
+    for (int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x; w < words; w += (int64_t)gridDim.x * kBlock) {
+        uint64_t v = 0;
+        for (int c = 0; c < chunks; ++c) v |= __builtin_nontemporal_load(partials + (int64_t)c * words + w);
+        out[w] = v;
+    }
+}
+
+// chunks of the slice mark for n rows (1 = the slices write the bitmap directly)
+inline int slice_chunks(int64_t n) { return n >= (1 << 20) ? kSliceChunks : 1; }
+
 size_t part_sort_temp(int64_t n) {
     size_t tb = 0;
     hipcub::DeviceRadixSort::SortKeys(nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 8);
@@ -1499,11 +1941,30 @@ size_t part_sort_temp(int64_t n) {
 
 }  // namespace
 
+namespace {
+// mark_bitmap method: 0 auto (slices for umi_len <= 12, partition sort for 13), 1 sort, 2 slices
+std::atomic<int> g_mark_method{0};
+bool use_slices(int L) {
+    const int m = g_mark_method.load();
+    return L <= 12 && m != 1;
+}
+}  // namespace
+
+int cluster_set_mark_method(int m) {
+    ROGTK_REQUIRE(m >= 0 && m <= 2, ROGTK_E_INVALID, "mark method %d outside 0..2", m);
+    g_mark_method.store(m);
+    return ROGTK_OK;
+}
+
 int cluster_mark_bitmap_temp(int64_t n, int L, int64_t* bytes) {
-    ROGTK_REQUIRE(L >= 7 && L <= 13, ROGTK_E_UNSUPPORTED, "mark by partition sort needs umi_len 7..13, got %d", L);
+    ROGTK_REQUIRE(L >= 7 && L <= 13, ROGTK_E_UNSUPPORTED, "mark_bitmap needs umi_len 7..13, got %d", L);
     ROGTK_REQUIRE(n >= 0 && n < ((int64_t)1 << 31), ROGTK_E_INVALID, "n outside 0..2^31-1");
     const int64_t nn = std::max<int64_t>(n, 1);
-    *bytes = 2 * ((nn * 4 + 255) / 256 * 256) + (int64_t)part_sort_temp(nn) + 256;
+    // both methods' scratch, so that the method can be switched on a live buffer
+    const int64_t sort_bytes = 2 * ((nn * 4 + 255) / 256 * 256) + (int64_t)part_sort_temp(nn) + 256;
+    const int64_t words = ((int64_t)1 << (2 * L)) / 64;
+    const int64_t slice_bytes = L <= 12 && slice_chunks(nn) > 1 ? (int64_t)slice_chunks(nn) * words * 8 : 0;
+    *bytes = std::max(sort_bytes, slice_bytes);
     return ROGTK_OK;
 }
 
@@ -1517,6 +1978,22 @@ int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bi
     const int two_l = 2 * L;
     if (n == 0) {
         ROGTK_HIP_CHECK(hipMemsetAsync(bitmap, 0, ((size_t)1 << two_l) / 8, s));
+        return ROGTK_OK;
+    }
+    ROGTK_REQUIRE(((uintptr_t)codes & 15u) == 0, ROGTK_E_INVALID, "mark_bitmap: codes must be 16-byte aligned");
+    if (use_slices(L)) {
+        const int slog = std::min(two_l, kSliceLog2);
+        const int slices = 1 << (two_l - slog);
+        const int chunks = slice_chunks(n);
+        int64_t chunk_rows = (n + chunks - 1) / chunks;
+        chunk_rows = (chunk_rows + 3) / 4 * 4;  // rows of a chunk start 4-aligned (uint4 loads)
+        const int64_t words = ((int64_t)1 << two_l) / 64;
+        uint64_t* dst = chunks > 1 ? (uint64_t*)temp : bitmap;
+        hipLaunchKernelGGL(k_slice_mark, dim3((unsigned)(slices * chunks)), dim3(kSliceBlock), 0, s, codes, regular_bits, n, slog, chunks, chunk_rows, dst, words);
+        if (chunks > 1)
+            hipLaunchKernelGGL(k_or_partials, dim3(grid_for(words, 4096)), dim3(kBlock), 0, s, dst, chunks, words,
+                               bitmap);
+        ROGTK_HIP_CHECK(hipGetLastError());
         return ROGTK_OK;
     }
     const int64_t slab = (n * 4 + 255) / 256 * 256;

@@ -177,7 +177,7 @@ struct ClusterLayout {
     // byte offsets into the workspace
     int64_t off_stats, off_presence, off_bitmap, off_rt, off_wpref, off_blksum, off_blkoff, off_D, off_f, off_ur,
         off_rbits, off_lroot, off_rpref, off_rblksum, off_rblkoff, off_labelcode, off_ilab, off_active,
-        active_words, total;
+        active_words, off_edges, ecap, total;
 };
 int cluster_layout(int L, int64_t max_distinct, ClusterLayout* out);
 
@@ -218,14 +218,19 @@ int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bi
 int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t* bitmaps,
                            int n_bitmaps, int max_distance, hipStream_t s);
 // Waits for an asynchronous resolve's round flags and completes it if needed.
-int cluster_finish(const void* ws, hipStream_t s);
+// *redone (nullable): 1 when more rounds (+ labels, + a deferred assign) were enqueued.
+int cluster_finish(const void* ws, hipStream_t s, int* redone = nullptr);
 void cluster_release(const void* ws);
 int cluster_rounds(const void* ws, hipStream_t s, int* rounds);
 int cluster_set_spec_rounds(int n);
 int cluster_set_global_mode(int mode);
+int cluster_set_edge_cap(int64_t pairs);
+int cluster_set_mark_method(int m);
+// deferred: enqueue without waiting for the resolve's flags (cluster_finish re-runs it
+// if the speculative rounds were not enough)
 int launch_cluster_assign(const ClusterLayout& cl, const uint8_t* ws, const uint32_t* codes,
                           const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id,
-                          hipStream_t s);
+                          hipStream_t s, bool deferred = false);
 
 // Irregular rows grouped by exact bytes (any length <= max_len); ids continue after
 // stats_dev[1] (the regular cluster count) or from 0 when stats_dev is NULL.

@@ -162,9 +162,19 @@ class ClusterEngine:
         _lib.call("rogtk_cluster_resolve", _p(self.ws), self.umi_len, self.max_distinct, _p(bitmaps),
                   int(n_bitmaps), int(max_distance), _s(stream))
 
-    def assign(self, batch: PackedBatch, cluster_id: torch.Tensor, stream=None) -> None:
-        _lib.call("rogtk_cluster_assign", _p(self.ws), self.umi_len, self.max_distinct, _p(batch.codes),
-                  _p(batch.regular_bits), batch.n, _p(cluster_id), _s(stream))
+    def assign(self, batch: PackedBatch, cluster_id: torch.Tensor, stream=None, deferred: bool = False) -> None:
+        """cluster ids of the batch's rows. deferred=True: no host wait for the resolve's
+        convergence flags; sync() before reading cluster_id re-runs it if needed."""
+        fn = "rogtk_cluster_assign_deferred" if deferred else "rogtk_cluster_assign"
+        _lib.call(fn, _p(self.ws), self.umi_len, self.max_distinct, _p(batch.codes), _p(batch.regular_bits),
+                  batch.n, _p(cluster_id), _s(stream))
+
+    def sync(self, stream=None) -> bool:
+        """Completes the pending resolve (+ deferred assign) on `stream`; True when that
+        enqueued more work (the speculative rounds were not enough)."""
+        redone = ctypes.c_int(0)
+        _lib.call("rogtk_cluster_sync", _p(self.ws), _s(stream), ctypes.byref(redone))
+        return bool(redone.value)
 
     def stats(self, stream=None) -> Dict[str, int]:
         out = (ctypes.c_int64 * 4)()
@@ -183,13 +193,29 @@ def set_spec_rounds(n: int) -> None:
     _lib.call("rogtk_cluster_set_spec_rounds", int(n))
 
 
-GLOBAL_UNION_FIND, GLOBAL_ROUNDS, GLOBAL_ROUNDS_ONE_FLATTEN = 1, 2, 3
+GLOBAL_UNION_FIND, GLOBAL_ROUNDS, GLOBAL_ROUNDS_ONE_FLATTEN, GLOBAL_EDGES = 1, 2, 3, 4
 
 
 def set_global_mode(mode: int) -> None:
-    """Global CC phase: 2 = hook + jump rounds, speculative + deferred (default, 0 restores
-    it), 1 = one-pass CAS union-find; both give identical ids."""
+    """Global CC phase: 2 = hook + jump rounds over the bitmap cliques, speculative +
+    deferred (default, 0 restores it), 1 = one-pass CAS union-find, 3 = root-chasing
+    rounds + one flatten, 4 = one clique sweep + rounds over the crossing edges; all give
+    identical ids."""
     _lib.call("rogtk_cluster_set_global_mode", int(mode))
+
+
+MARK_AUTO, MARK_SORT, MARK_SLICES = 0, 1, 2
+
+
+def set_mark_method(method: int) -> None:
+    """mark_bitmap method: 0 auto (LDS code slices for umi_len <= 12, partition sort for 13),
+    1 partition sort, 2 code slices; identical bitmaps."""
+    _lib.call("rogtk_cluster_set_mark_method", int(method))
+
+
+def set_edge_cap(pairs: int) -> None:
+    """(tests) Edge-list capacity of workspaces created from now on (mode 4); 0 = default."""
+    _lib.call("rogtk_cluster_set_edge_cap", int(pairs))
 
 
 def cluster_batch(engine: ClusterEngine, batch: PackedBatch, cluster_id: torch.Tensor,

@@ -18,6 +18,14 @@ workspace and outputs; events order every cross-stream hand-off:
   assign(k)  waits resolved(k)                      -> records assigned(k)
 Resolve is enqueue-only (rogtk_cluster_resolve); assign completes a resolve whose
 speculative rounds were not enough, so results never depend on timing.
+
+assign_on="resolve" (option; "separate" is the default): the assign of batch k runs right behind its resolve on
+the resolve stream, as a deferred assign (no host wait); the slot's convergence flags
+are checked when the slot is reused or at drain(), which re-runs the rounds, labels and
+assign on the resolve stream in the rare case the speculative rounds were not enough.
+The assign's random gathers then never run beside the next batch's latency-bound
+resolve kernels (hook round 0 took 111 us beside assign, 31 us alone), but the host's
+wait for batch k-1's flags moves onto the critical cycle: 0.487 vs 0.430 ms/step at 10M.
 """
 from __future__ import annotations
 
@@ -43,12 +51,15 @@ class UmiPipeline:
     def __init__(self, umi_len: int, max_distinct: int, n_max: int, device=None, depth: int = 3,
                  target: Optional[bytes] = b"ACGTACGTACGT", max_hamming: int = 1, max_distance: int = 1,
                  group=None, with_scores: bool = True, priorities=(0, 0, 0), mark: str = "auto",
-                 on_assigned=None, score_alone: bool = False, exchange=None):
+                 on_assigned=None, score_alone: bool = False, exchange=None, resolve_streams: int = 1,
+                 assign_on: str = "separate"):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
-        if mark == "auto":  # the partition-sort bitmap where it applies (measured fastest)
+        if mark == "auto":  # rogtk_cluster_mark_bitmap where it applies (measured fastest)
             mark = "sort" if 7 <= umi_len <= 13 else "xcd"
+        if mark == "slices":  # the method of rogtk_cluster_mark_bitmap is a process-wide knob
+            mark = "sort"
         if mark not in ("xcd", "fused", "sort"):
             raise ValueError("mark must be 'xcd' (XCD-partitioned mark kernel), 'fused' (inside k_score_packed) "
                              "or 'sort' (partition sort + LDS bitmap, umi_len 7..13)")
@@ -59,12 +70,17 @@ class UmiPipeline:
         self.caller = torch.cuda.current_stream(dev)
         self.main = torch.cuda.Stream(dev, priority=priorities[0])
         self.main.wait_stream(self.caller)
-        self.s_resolve = torch.cuda.Stream(dev, priority=priorities[1])
+        # resolve_streams > 1: consecutive batches resolve on different streams, so two
+        # latency-bound resolve chains overlap (needs depth >= resolve_streams + 1)
+        if resolve_streams < 1 or (resolve_streams > 1 and depth < resolve_streams + 1):
+            raise ValueError("resolve_streams must be >= 1 and < depth")
+        self.s_resolves = [torch.cuda.Stream(dev, priority=priorities[1]) for _ in range(resolve_streams)]
+        self.s_resolve = self.s_resolves[0]
         self.s_assign = torch.cuda.Stream(dev, priority=priorities[2])
         self.queue = deque()
         # assign lags resolve by one batch only when a second slot exists: with one
         # slot the next batch's resolve would overwrite the tables assign reads
-        self.lag = 1 if depth > 1 else 0
+        self.lag = resolve_streams if depth > 1 else 0
         # on_assigned(slot, batch): called with the assign stream current, after the
         # batch's assign and before its slot may be reused (e.g. to copy outputs out)
         self.on_assigned = on_assigned
@@ -77,11 +93,22 @@ class UmiPipeline:
         self.last_scored: Optional[torch.cuda.Event] = None
         self.k = 0
         self.last_assigned: Optional[torch.cuda.Event] = None
+        # assign_on "resolve": assign(k) is enqueued right behind resolve(k) on the same
+        # stream as a deferred assign (no host wait for the resolve's flags), so it never
+        # competes with the latency-bound resolve kernels of the next batch; the flags
+        # are checked when the slot comes round again (or at drain)
+        if assign_on not in ("resolve", "separate"):
+            raise ValueError("assign_on must be 'resolve' or 'separate'")
+        self.assign_on = assign_on
+        if assign_on == "resolve" and resolve_streams != 1:
+            raise ValueError("assign_on='resolve' uses one resolve stream")
 
     def submit(self, batch: D.PackedBatch):
         """Enqueue one batch; returns its slot (outputs valid after drain() or a later event)."""
         slot = self.slots[self.k % len(self.slots)]
         self.main.wait_stream(torch.cuda.current_stream(self.main.device))  # batch producer -> main
+        if self.assign_on == "resolve":
+            return self._submit_assign_on_resolve(slot, batch)
         if slot.assigned is not None:
             self.main.wait_event(slot.assigned)
         D.score_packed(batch, slot.scores, self.target, self.max_hamming, None, slot.within,
@@ -97,15 +124,54 @@ class UmiPipeline:
             slot.eng.build_local_bitmap(stream=self.main)
         marked = torch.cuda.Event()
         marked.record(self.main)
-        with torch.cuda.stream(self.s_resolve):
-            self.s_resolve.wait_event(marked)
+        sr = self.s_resolves[self.k % len(self.s_resolves)]
+        with torch.cuda.stream(sr):
+            sr.wait_event(marked)
             bitmaps, nb = self.exchange(slot.eng.local_bitmap)
-            slot.eng.resolve(bitmaps, nb, self.max_distance, stream=self.s_resolve)
+            slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr)
             resolved = torch.cuda.Event()
-            resolved.record(self.s_resolve)
+            resolved.record(sr)
         self.queue.append((slot, batch, resolved))
         while len(self.queue) > self.lag:
             self._assign_oldest()
+        self.k += 1
+        return slot
+
+    def _settle(self, slot: _Slot):
+        """The slot's previous batch is final: its resolve converged (or is completed now,
+        with its assign re-run, on the resolve stream)."""
+        if slot.assigned is None:
+            return
+        if slot.eng.sync(stream=self.s_resolve):
+            slot.assigned = torch.cuda.Event()
+            slot.assigned.record(self.s_resolve)
+            self.last_assigned = slot.assigned
+
+    def _submit_assign_on_resolve(self, slot: _Slot, batch: D.PackedBatch):
+        self._settle(slot)
+        if slot.assigned is not None:
+            self.main.wait_event(slot.assigned)
+        D.score_packed(batch, slot.scores, self.target, self.max_hamming, None, slot.within,
+                       cluster=slot.eng if self.fused_mark else None, stream=self.main)
+        if self.sort_mark:
+            slot.eng.mark_bitmap(batch, stream=self.main)
+        else:
+            if not self.fused_mark:
+                slot.eng.mark(batch, stream=self.main)
+            slot.eng.build_local_bitmap(stream=self.main)
+        marked = torch.cuda.Event()
+        marked.record(self.main)
+        sr = self.s_resolve
+        with torch.cuda.stream(sr):
+            sr.wait_event(marked)
+            bitmaps, nb = self.exchange(slot.eng.local_bitmap)
+            slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr)
+            slot.eng.assign(batch, slot.cid, stream=sr, deferred=self.on_assigned is None)
+            if self.on_assigned is not None:
+                self.on_assigned(slot, batch)
+            slot.assigned = torch.cuda.Event()
+            slot.assigned.record(sr)
+        self.last_assigned = slot.assigned
         self.k += 1
         return slot
 
@@ -124,6 +190,9 @@ class UmiPipeline:
 
     def drain(self):
         """Finish every submitted batch; the main stream waits for the last assign."""
+        if self.assign_on == "resolve":
+            for slot in self.slots:
+                self._settle(slot)
         while self.queue:
             self._assign_oldest()
         if self.last_assigned is not None:

@@ -385,7 +385,8 @@ def test_full_size_c2_properties(rg):
 @pytest.mark.parametrize("depth,nb,alone", [(4, 4, False), (2, 5, False), (1, 3, False), (3, 7, False),
                                              (2, 6, True), (3, 5, True)])
 @pytest.mark.parametrize("mark", ["xcd", "fused", "sort"])
-def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark):
+@pytest.mark.parametrize("assign_on", ["resolve", "separate"])
+def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assign_on):
     """rogtk_amd.pipeline (3 streams, `depth` batches in flight) == the sequential device
     path for EVERY batch (outputs copied out by the on_assigned hook before slot reuse)."""
     import torch
@@ -403,7 +404,7 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark):
                      slot.scores["longest_homopolymer_run"][:n].clone()))
 
     pipe = UmiPipeline(L, n, n, "cuda", depth=depth, target=b"ACGTACGTACGT", max_distance=1, mark=mark,
-                       on_assigned=grab, score_alone=alone)
+                       on_assigned=grab, score_alone=alone, assign_on=assign_on)
     keep = []
     for s in seeds:
         codes = torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda()
@@ -419,6 +420,42 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark):
         assert np.array_equal(g_w, hw.cpu().numpy()), k
         assert np.array_equal(g_comb.view(np.uint64), scores["combined_score"][:n].cpu().numpy().view(np.uint64)), k
         assert np.array_equal(g_long, scores["longest_homopolymer_run"][:n].cpu().numpy()), k
+
+
+@pytest.mark.parametrize("spec", [1, 4])
+@pytest.mark.parametrize("depth,nb", [(2, 5), (3, 3), (1, 2)])
+def test_pipeline_deferred_assign(rg, depth, nb, spec):
+    """assign_on="resolve" without an on_assigned hook: assigns are enqueued before their
+    resolve's flags are checked; with 1 speculative round every batch needs the deferred
+    completion (rounds + labels + the assign again) when its slot comes round or at drain.
+    The slots' final outputs equal the sequential device path."""
+    import torch
+
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+    from rogtk_amd.pipeline import UmiPipeline
+
+    n, L = 200_003, 12
+    seeds = [synth.DEFAULT_SEED + 29 * k for k in range(nb)]
+    try:
+        D.set_spec_rounds(spec)
+        pipe = UmiPipeline(L, n, n, "cuda", depth=depth, target=b"ACGTACGTACGT", max_distance=1)
+        keep, last = [], {}
+        for k, s in enumerate(seeds):
+            codes = torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda()
+            keep.append(D.PackedBatch(codes, L))
+            last[id(pipe.submit(keep[-1]))] = k
+        pipe.drain()
+        torch.cuda.synchronize()
+    finally:
+        D.set_spec_rounds(0)
+    for slot in pipe.slots:
+        if id(slot) not in last:
+            continue
+        k = last[id(slot)]
+        _, scores, _, hw, cid, _ = _device_run(n, seed=seeds[k])
+        assert np.array_equal(slot.cid[:n].cpu().numpy(), cid.cpu().numpy()), k
+        assert np.array_equal(slot.within.cpu().numpy()[:len(hw)], hw.cpu().numpy()), k
 
 
 def _chain_codes(rng, L, length, high_bases):
@@ -443,7 +480,7 @@ def _chain_codes(rng, L, length, high_bases):
     return np.array([(c << shift0) | low for c in path], dtype=np.uint32)
 
 
-@pytest.mark.parametrize("gm", [2, 3])
+@pytest.mark.parametrize("gm", [2, 3, 4])
 @pytest.mark.parametrize("spec", [1, 2])
 @pytest.mark.parametrize("L", [12, 16])
 def test_deferred_rounds_match(rg, L, spec, gm):
@@ -476,7 +513,7 @@ def test_deferred_rounds_match(rg, L, spec, gm):
     assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc)
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
 @pytest.mark.parametrize("L", [12, 16])
 def test_long_chains_need_extra_rounds(rg, L, mode):
     """Long Hamming-1 paths (diameter >> speculative rounds) resolve exactly: the one-pass
@@ -525,7 +562,7 @@ def test_global_modes_identical(rg, L, n):
     batch = D.PackedBatch(codes, L)
     out = {}
     try:
-        for mode in (D.GLOBAL_ROUNDS, D.GLOBAL_UNION_FIND, D.GLOBAL_ROUNDS_ONE_FLATTEN):
+        for mode in (D.GLOBAL_ROUNDS, D.GLOBAL_UNION_FIND, D.GLOBAL_ROUNDS_ONE_FLATTEN, D.GLOBAL_EDGES):
             D.set_global_mode(mode)
             eng = D.ClusterEngine(L, min(n, 4 ** L), "cuda")
             cid = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -533,16 +570,46 @@ def test_global_modes_identical(rg, L, n):
             out[mode] = (cid.cpu().numpy(), eng.stats()["n_clusters"])
     finally:
         D.set_global_mode(0)
-    assert out[1][1] == out[2][1] == out[3][1]
-    assert np.array_equal(out[1][0], out[2][0]) and np.array_equal(out[3][0], out[2][0])
+    assert out[1][1] == out[2][1] == out[3][1] == out[4][1]
+    for m in (1, 3, 4):
+        assert np.array_equal(out[m][0], out[2][0]), m
     if n <= 1_000_000:
         rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L)), L, 1)
         assert out[1][1] == rk
         assert np.array_equal(out[1][0].view(np.uint32), rc)
 
 
-@pytest.mark.parametrize("n", [0, 1, 5000, 300_000, 3_000_000])
-@pytest.mark.parametrize("L", [7, 8, 10, 12, 13])
+@pytest.mark.parametrize("cap", [1, 4096])
+@pytest.mark.parametrize("L", [10, 12, 16])
+def test_edge_list_overflow_falls_back(rg, L, cap):
+    """Mode 4 with an edge list far too small for the data: the overflow is detected and
+    the bitmap rounds finish from the round-0 hooks (flattened to stars), exactly."""
+    import torch
+
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+
+    n = 300_000
+    codes_h = synth.umi_codes(n, L, seed=5 + L)
+    codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
+    batch = D.PackedBatch(codes, L)
+    try:
+        D.set_global_mode(D.GLOBAL_EDGES)
+        D.set_edge_cap(cap)
+        eng = D.ClusterEngine(L, min(n, 4 ** L), "cuda")
+        cid = torch.empty(n, dtype=torch.int32, device="cuda")
+        D.cluster_batch(eng, batch, cid, 1)
+        stats = eng.stats()
+    finally:
+        D.set_edge_cap(0)
+        D.set_global_mode(0)
+    rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L)), L, 1)
+    assert stats["n_clusters"] == rk
+    assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc)
+
+
+@pytest.mark.parametrize("n", [0, 1, 5000, 300_000, 3_000_000, 1_048_579])
+@pytest.mark.parametrize("L", [7, 8, 10, 11, 12, 13])
 def test_mark_bitmap_sort_equals_presence_path(rg, L, n):
     """The partition-sort bitmap equals mark + local_bitmap bit for bit, with irregular
     rows (regular bit 0) mixed in, whose codes must not be marked."""
@@ -568,7 +635,14 @@ def test_mark_bitmap_sort_equals_presence_path(rg, L, n):
         a = D.ClusterEngine(L, max(min(n, 4 ** L), 1), "cuda")
         a.mark(batch)
         ref = a.build_local_bitmap().clone()
-        b = D.ClusterEngine(L, max(min(n, 4 ** L), 1), "cuda")
-        got = b.mark_bitmap(batch).clone()
-        torch.cuda.synchronize()
-        assert torch.equal(ref, got), (L, n, rb is None)
+        for method in (D.MARK_SORT, D.MARK_SLICES):
+            if method == D.MARK_SLICES and L > 12:
+                continue
+            try:
+                D.set_mark_method(method)
+                b = D.ClusterEngine(L, max(min(n, 4 ** L), 1), "cuda")
+                got = b.mark_bitmap(batch).clone()
+                torch.cuda.synchronize()
+            finally:
+                D.set_mark_method(D.MARK_AUTO)
+            assert torch.equal(ref, got), (L, n, rb is None, method)

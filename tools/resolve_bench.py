@@ -24,6 +24,8 @@ for n in [int(x) for x in os.environ.get("NS", "10000000,80000000").split(",")]:
             if c: r[k] = round(1000 * ms / c, 1)
         st = eng.ws[:64].view(torch.int64).cpu().numpy()
         flags = eng.ws[64:64 + 4 * 16].view(torch.int32).cpu().numpy()
+        ecnt = eng.ws[320:320 + 4 * 8].view(torch.int32).cpu().numpy()
+        r["edge_counts"] = ecnt.tolist()
         print(f"n={n} md={md} distinct={st[0]} clusters={st[1]} rounds_flags={flags.tolist()}", r, flush=True)
     eng.assign(batch, cid); torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
