@@ -15,6 +15,8 @@
 // for Shannon; ascending byte pair for dinucleotides = the oracle's canonical
 // order); the file is compiled with -ffp-contract=off so `e -= t` and the combined
 // score are never fused into FMAs; f64 division is IEEE (correctly rounded).
+#include <cstdlib>
+
 #include "rogtk_internal.h"
 
 namespace rogtk {
@@ -98,10 +100,14 @@ struct RowScore {
     uint32_t longest;
 };
 
-__device__ __forceinline__ RowScore score_code(uint32_t code, int L, const double* __restrict__ t_sh,
+// LT > 0: the UMI length as a compile-time constant (the loops over bases unroll into
+// straight-line code); LT == 0: the runtime length L.
+template <int LT>
+__device__ __forceinline__ RowScore score_code(uint32_t code, int L_rt, const double* __restrict__ t_sh,
                                                const double* __restrict__ t_di,
                                                const double* __restrict__ t_ling,
                                                const double* __restrict__ t_frac) {
+    const int L = LT > 0 ? LT : L_rt;
     RowScore r;
     // shannon_entropy (umi_score.rs:45-73): base counts from the 2-bit planes,
     // terms subtracted in A,C,G,T order; t_sh[0] == 0.0 stands for a skipped term.
@@ -169,7 +175,7 @@ __device__ __forceinline__ uint32_t hamming_code(uint32_t code, const PackedPara
     return (uint32_t)__popc((x | (x >> 1)) & P.cmplo) + P.always_mismatch;
 }
 
-template <bool SCORE, bool HAMD, bool HAMW, bool MARK>
+template <bool SCORE, bool HAMD, bool HAMW, bool MARK, int LT = 0>
 __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restrict__ codes,
                                                           const uint64_t* __restrict__ regbits,
                                                           int64_t n, const PackedParams P,
@@ -221,7 +227,7 @@ __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restr
 #pragma unroll
             for (int k = 0; k < kRowsPerLane; ++k) {
                 if ((reg >> k) & 1u) {
-                    const RowScore r = score_code(c[k], L, s_tab[0], s_tab[1], s_tab[2], s_tab[3]);
+                    const RowScore r = score_code<LT>(c[k], L, s_tab[0], s_tab[1], s_tab[2], s_tab[3]);
                     sh[k] = r.sh; li[k] = r.ling; ho[k] = r.homo; di[k] = r.di; co[k] = r.comb;
                     lg[k] = r.longest;
                 } else {
@@ -499,6 +505,18 @@ int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int
         hipLaunchKernelGGL((k_score_packed<S, D, W, M>), dim3(g), dim3(kBlock), 0, s, codes, \
                            regular_bits, n, p, o, hd, hw, presence);                          \
         break;
+    // the bench / C2 configuration (12-bp UMIs, all fields + within bits) has a
+    // length-specialised instance (ROGTK_SCORE_GENERIC=1: runtime-length kernel, A/B)
+    static const bool generic = [] {
+        const char* e = getenv("ROGTK_SCORE_GENERIC");
+        return e && e[0] == '1';
+    }();
+    if (!generic && p.L == 12 && sel == 8 + 2) {
+        hipLaunchKernelGGL((k_score_packed<true, false, true, false, 12>), dim3(g), dim3(kBlock), 0, s, codes,
+                           regular_bits, n, p, o, hd, hw, presence);
+        ROGTK_HIP_CHECK(hipGetLastError());
+        return ROGTK_OK;
+    }
     switch (sel) {
         ROGTK_SP(0, 0, 0, 1) ROGTK_SP(0, 0, 1, 0) ROGTK_SP(0, 0, 1, 1) ROGTK_SP(0, 1, 0, 0)
         ROGTK_SP(0, 1, 0, 1) ROGTK_SP(0, 1, 1, 0) ROGTK_SP(0, 1, 1, 1) ROGTK_SP(1, 0, 0, 0)
