@@ -203,6 +203,45 @@ int rogtk_cluster_set_edge_cap(int64_t pairs);
 /* Releases the host-side resolve state kept for ws (call before freeing ws). */
 int rogtk_cluster_release(const void* ws);
 
+/* ===================== sharded H3 (any umi_len 1..32) =====================
+ * Device steps of rogtk_amd/dist.py umi_cluster_sharded (rogtk_amd/csrc/dist_cluster.hip):
+ * the clusters of rows spread over ranks, merged with RCCL all-to-alls of distinct codes
+ * and of masked-key records instead of the 4^L bitmap (the north_star's
+ * "RCCL all-to-all merge"); ids identical to the single-GPU engines. Device pointers;
+ * the entry points that report sizes (host int64 outputs) synchronise `stream`.
+ * codes: u64 2-bit codes (first base most significant); kind: 0 null, 1 regular,
+ * 2 irregular (valid, not umi_len pure ACGT). */
+int rogtk_long_codes(const void* offsets, int offset_width, const uint8_t* values, const uint8_t* validity,
+                     int64_t validity_offset, int64_t n, int umi_len, uint64_t* codes, uint8_t* kind,
+                     void* stream);
+/* Sorted distinct codes of the rows with kind 1 (kind NULL: all rows); *n_out on the host. */
+int rogtk_unique_codes(const uint64_t* codes, const uint8_t* kind, int64_t n, int umi_len, uint64_t* out,
+                       int64_t* n_out, void* stream);
+/* Owner rank of a code = floor(code * world / 4^umi_len); counts[world] (host) of a
+ * sorted array (already grouped by owner). */
+int rogtk_owner_counts(const uint64_t* sorted, int64_t n, int umi_len, int world, int64_t* counts, void* stream);
+/* n * umi_len records (code with digit p zeroed, p, code) of the distinct codes D, packed
+ * by destination rank hash(masked code, p) % world; counts[world] (host). */
+int rogtk_masked_records(const uint64_t* D, int64_t n, int umi_len, int world, uint64_t* masked, uint32_t* pos,
+                         uint64_t* code, int64_t* counts, void* stream);
+/* Groups received records by (p, masked code); consecutive members -> an edge between
+ * their codes' indices in the global sorted distinct set G. edges: 2 x u32 per edge,
+ * capacity n; *n_edges (host). */
+int rogtk_clique_edges(const uint64_t* masked, const uint32_t* pos, const uint64_t* code, int64_t n, int umi_len,
+                       const uint64_t* G, int64_t ng, uint32_t* edges, int64_t* n_edges, void* stream);
+/* Connected components of nv vertices under m edges (2 x u32 each): labels[v] dense, in
+ * order of each component's smallest vertex; *n_clusters (host). */
+int rogtk_cc_labels(int64_t nv, const uint32_t* edges, int64_t m, uint32_t* labels, int64_t* n_clusters,
+                    void* stream);
+/* cluster_id[i] = labels[index of codes[i] in G] for kind 1, 0xFFFFFFFF for kind 0;
+ * kind 2 rows untouched. Fails when a regular code is absent from G. */
+int rogtk_assign_codes(const uint64_t* codes, const uint8_t* kind, int64_t n, const uint64_t* G, int64_t ng,
+                       const uint32_t* labels, uint32_t* cluster_id, void* stream);
+/* Exact-bytes groups of n strings (int64 offsets from 0): ids[i] = id_base + rank of the
+ * string among the distinct strings in byte-lexicographic order; *n_groups (host). */
+int rogtk_group_strings(const int64_t* offsets, const uint8_t* values, int64_t n, int64_t max_len, uint32_t id_base,
+                        uint32_t* ids, int64_t* n_groups, void* stream);
+
 /* ========================= Level 2: host buffers ========================= */
 
 /* umi_complexity_all_expr + the 7 single-field exprs (expressions.rs:1234-1410). */

@@ -136,3 +136,220 @@ def route_rows(offsets: torch.Tensor, values: torch.Tensor, keys: torch.Tensor, 
     src_rank = torch.repeat_interleave(torch.arange(W, dtype=torch.int32, device=dev),
                                        torch.tensor(rrows, dtype=torch.int64, device=dev))
     return out_off, out_vals[:sum(rbytes)], out_keys, src_rank, out_src
+
+
+# ---------------------------------------------------------------------------------------
+# Sharded H3 for any UMI length (1..32): clusters of rows spread over ranks, merged with
+# all-to-alls (SURVEY.md §8e variant for long UMIs; the north_star's "RCCL all-to-all
+# merge"). The device steps are the C-ABI entry points of rogtk_amd/csrc/dist_cluster.hip;
+# this function is the exchange plan between them:
+#   codes/kind (rows)  -> local distinct codes
+#   -> all-to-all by owner = code range -> owned distinct codes -> all-gather: G (sorted)
+#   -> masked-key records of the owned codes -> all-to-all by hash(masked key, position)
+#   -> clique edges (indices into G) -> all-gather -> connected components on every rank
+#   -> rows: cluster id = label of the code's index in G
+#   irregular rows: all-gather their strings, exact-bytes ids after the regular clusters.
+# Every rank computes the same G, edges and labels, so ids equal the single-GPU ids.
+# ---------------------------------------------------------------------------------------
+
+class _HipOps:
+    """Device steps through librogtk_hip (the product path; no fallback)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+
+    def _stream(self):
+        import ctypes
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    @staticmethod
+    def _p(t):
+        import ctypes
+        return ctypes.c_void_p(t.data_ptr() if t is not None and t.numel() else 0)
+
+    def long_codes(self, offsets, values, validity, voff, n, L):
+        from . import _lib
+        codes = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+        kind = torch.empty(max(n, 1), dtype=torch.uint8, device=self.device)
+        _lib.call("rogtk_long_codes", self._p(offsets), offsets.element_size(), self._p(values),
+                  self._p(validity), int(voff), int(n), int(L), self._p(codes), self._p(kind), self._stream())
+        return codes[:n], kind[:n]
+
+    def unique(self, codes, kind, L):
+        import ctypes
+        from . import _lib
+        n = codes.numel()
+        out = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+        m = ctypes.c_int64(0)
+        _lib.call("rogtk_unique_codes", self._p(codes), self._p(kind), int(n), int(L), self._p(out),
+                  ctypes.byref(m), self._stream())
+        return out[:m.value]
+
+    def owner_counts(self, sorted_codes, L, W):
+        import ctypes
+        from . import _lib
+        c = (ctypes.c_int64 * W)()
+        _lib.call("rogtk_owner_counts", self._p(sorted_codes), int(sorted_codes.numel()), int(L), int(W), c,
+                  self._stream())
+        return list(c)
+
+    def masked_records(self, D, L, W):
+        import ctypes
+        from . import _lib
+        total = D.numel() * L
+        mk = torch.empty(max(total, 1), dtype=torch.int64, device=self.device)
+        pos = torch.empty(max(total, 1), dtype=torch.int32, device=self.device)
+        code = torch.empty(max(total, 1), dtype=torch.int64, device=self.device)
+        c = (ctypes.c_int64 * W)()
+        _lib.call("rogtk_masked_records", self._p(D), int(D.numel()), int(L), int(W), self._p(mk), self._p(pos),
+                  self._p(code), c, self._stream())
+        return mk[:total], pos[:total], code[:total], list(c)
+
+    def clique_edges(self, mk, pos, code, L, G):
+        import ctypes
+        from . import _lib
+        n = mk.numel()
+        E = torch.empty((max(n, 1), 2), dtype=torch.int32, device=self.device)
+        m = ctypes.c_int64(0)
+        _lib.call("rogtk_clique_edges", self._p(mk), self._p(pos), self._p(code), int(n), int(L), self._p(G),
+                  int(G.numel()), self._p(E), ctypes.byref(m), self._stream())
+        return E[:m.value]
+
+    def cc_labels(self, nv, E):
+        import ctypes
+        from . import _lib
+        lab = torch.empty(max(nv, 1), dtype=torch.int32, device=self.device)
+        k = ctypes.c_int64(0)
+        _lib.call("rogtk_cc_labels", int(nv), self._p(E), int(E.shape[0]), self._p(lab), ctypes.byref(k),
+                  self._stream())
+        return lab[:nv], k.value
+
+    def assign(self, codes, kind, G, labels, cid):
+        from . import _lib
+        _lib.call("rogtk_assign_codes", self._p(codes), self._p(kind), int(codes.numel()), self._p(G),
+                  int(G.numel()), self._p(labels), self._p(cid), self._stream())
+
+    def group_strings(self, offsets, values, n, max_len, base):
+        import ctypes
+        from . import _lib
+        ids = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+        g = ctypes.c_int64(0)
+        _lib.call("rogtk_group_strings", self._p(offsets), self._p(values), int(n), int(max_len), int(base),
+                  self._p(ids), ctypes.byref(g), self._stream())
+        return ids[:n], g.value
+
+
+def _exchange_device(t: torch.Tensor, group) -> torch.device:
+    """Where collective buffers live: the tensor's device with nccl (RCCL), the host with gloo."""
+    return t.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+
+
+def _a2a_var(t: torch.Tensor, send_counts, group=None):
+    """Variable all-to-all of the rows of t (grouped by destination rank, send_counts[r]
+    rows for rank r); returns the received rows, grouped by source rank."""
+    W = world(group)
+    if W == 1:
+        return t, [int(send_counts[0])]
+    xd = _exchange_device(t, group)
+    sc = torch.tensor([int(c) for c in send_counts], dtype=torch.int64, device=xd)
+    rc = torch.empty(W, dtype=torch.int64, device=xd)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv = [int(v) for v in rc.cpu().tolist()]
+    out = torch.empty((sum(recv),) + tuple(t.shape[1:]), dtype=t.dtype, device=xd)
+    inp = t.to(xd) if t.device != xd else t
+    dist.all_to_all_single(out, inp.contiguous(), recv, [int(c) for c in send_counts], group=group)
+    return out.to(t.device), recv
+
+
+def _allgather_var(t: torch.Tensor, group=None):
+    """All-gather of variable-length row blocks: the concatenation in rank order, and each
+    rank's row count."""
+    W = world(group)
+    if W == 1:
+        return t, [t.shape[0]]
+    xd = _exchange_device(t, group)
+    nccl = dist.get_backend(group) == "nccl"
+
+    def gather(out, inp):
+        if nccl:
+            dist.all_gather_into_tensor(out, inp, group=group)
+        else:
+            dist.all_gather(list(out.chunk(W)), inp, group=group)
+
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=xd)
+    ns = torch.empty(W, dtype=torch.int64, device=xd)
+    gather(ns, n)
+    sizes = [int(v) for v in ns.cpu().tolist()]
+    mx = max(max(sizes), 1)
+    pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=xd)
+    pad[: t.shape[0]] = t.to(xd)
+    full = torch.empty((W * mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=xd)
+    gather(full, pad)
+    parts = [full[r * mx: r * mx + sizes[r]] for r in range(W)]
+    return torch.cat(parts).to(t.device), sizes
+
+
+def _irregular_strings(offsets: torch.Tensor, values: torch.Tensor, rows: torch.Tensor):
+    """(int64 offsets from 0, bytes) of the listed rows (plumbing: gathers bytes)."""
+    off = offsets.to(torch.int64)
+    starts, lens = off[rows], off[rows + 1] - off[rows]
+    poff = torch.zeros(rows.numel() + 1, dtype=torch.int64, device=offsets.device)
+    if rows.numel():
+        poff[1:] = torch.cumsum(lens, 0)
+    total = int(poff[-1].item()) if rows.numel() else 0
+    if total == 0:
+        return poff, values[:0]
+    idx = torch.repeat_interleave(starts - poff[:-1], lens) + torch.arange(total, dtype=torch.int64,
+                                                                          device=offsets.device)
+    return poff, values[idx]
+
+
+def umi_cluster_sharded(offsets: torch.Tensor, values: torch.Tensor, n: int, umi_len: int, max_distance: int = 1,
+                        validity: torch.Tensor = None, validity_offset: int = 0, group=None, ops=None):
+    """H3 cluster ids of this rank's rows of a UMI column sharded over the ranks of
+    `group` (int32/int64 Arrow offsets, uint8 values, optional validity bitmap; device
+    tensors). Returns (cluster_id int32 [n] (0xFFFFFFFF = null), n_clusters). Spec and
+    ids as the single-GPU umi_cluster, for any umi_len 1..32, through
+    all-to-alls instead of the 4^L bitmap."""
+    if not 1 <= umi_len <= 32:
+        raise ValueError("umi_len must be 1..32")
+    if max_distance not in (0, 1):
+        raise ValueError("max_distance must be 0 or 1")
+    ops = ops if ops is not None else _HipOps(offsets.device)
+    W = world(group)
+    rank = dist.get_rank(group) if W > 1 else 0
+    L = umi_len
+    codes, kind = ops.long_codes(offsets, values, validity, validity_offset, n, L)
+    D = ops.unique(codes, kind, L)
+    # owners: contiguous code ranges, so the received runs and G stay sorted by rank
+    recv, _ = _a2a_var(D, ops.owner_counts(D, L, W), group)
+    O = ops.unique(recv, None, L) if W > 1 else D
+    G, _ = _allgather_var(O, group)
+    if max_distance == 1 and G.numel() > 1:
+        mk, pos, code, cnt = ops.masked_records(O, L, W)
+        rmk, _ = _a2a_var(mk, cnt, group)
+        rpos, _ = _a2a_var(pos, cnt, group)
+        rcode, _ = _a2a_var(code, cnt, group)
+        E_local = ops.clique_edges(rmk, rpos, rcode, L, G)
+        E, _ = _allgather_var(E_local, group)
+        labels, n_reg = ops.cc_labels(G.numel(), E)
+    else:
+        labels = torch.arange(G.numel(), dtype=torch.int32, device=G.device)
+        n_reg = G.numel()
+    cid = torch.full((max(n, 1),), -1, dtype=torch.int32, device=offsets.device)[:n]
+    ops.assign(codes, kind, G, labels, cid)
+    # irregular rows (N, lowercase, other lengths): exact bytes, ids after the regular ones
+    irr = torch.nonzero(kind == 2).flatten()
+    poff, pval = _irregular_strings(offsets, values, irr)
+    lens = poff[1:] - poff[:-1]
+    all_lens, counts = _allgather_var(lens, group)
+    all_vals, _ = _allgather_var(pval, group)
+    n_irr_groups = 0
+    if all_lens.numel():
+        aoff = torch.zeros(all_lens.numel() + 1, dtype=torch.int64, device=all_lens.device)
+        aoff[1:] = torch.cumsum(all_lens, 0)
+        ids, n_irr_groups = ops.group_strings(aoff, all_vals, all_lens.numel(), int(all_lens.max().item()), n_reg)
+        start = sum(counts[:rank])
+        if irr.numel():
+            cid[irr] = ids[start: start + irr.numel()].to(cid.device)
+    return cid, int(n_reg + n_irr_groups)

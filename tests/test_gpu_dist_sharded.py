@@ -1,0 +1,104 @@
+"""GPU: rogtk_amd.dist.umi_cluster_sharded with the HIP steps (rogtk_amd/csrc/dist_cluster.hip).
+
+world 1 in-process, and world 2 as two gloo ranks sharing cuda:0 (collective buffers
+staged on the host; the same exchange plan the driver runs over RCCL). Ids must equal
+the oracle on the whole column and the single-GPU engines (umi_cluster).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from test_dist_sharded import _arrow, _free_port, make_column
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rg():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    import rogtk_amd
+
+    assert rogtk_amd.device_count() >= 1
+    return rogtk_amd
+
+
+@pytest.mark.parametrize("L,md,n", [(12, 1, 30_000), (12, 0, 30_000), (20, 1, 30_000), (32, 1, 20_000),
+                                    (7, 1, 5_000), (1, 1, 300), (16, 1, 40_000)])
+def test_sharded_world1_matches_oracle_and_engine(rg, L, md, n):
+    import pyarrow as pa
+
+    from oracle import pyoracle as P
+    from rogtk_amd import dist as RD
+
+    col = make_column(n, L, seed=L * 3 + md)
+    off, vals, vbits = (t.cuda() for t in _arrow(col))
+    cid, k = RD.umi_cluster_sharded(off, vals, n, L, md, validity=vbits)
+    torch.cuda.synchronize()
+    got = cid.cpu().numpy().view(np.uint32)
+    ref, valid, rk, _ = P.umi_cluster(P.StrCol.from_list(col), L, md)
+    assert k == rk
+    assert np.array_equal(got[valid], ref[valid])
+    assert (got[~valid] == 0xFFFFFFFF).all()
+    eng, ek, _ = rg.umi_cluster(pa.array(col, type=pa.large_binary()), L, md)
+    assert ek == k
+    assert np.array_equal(np.asarray(eng.fill_null(0).to_numpy(zero_copy_only=False)).astype(np.uint32)[valid],
+                          got[valid])
+
+
+def test_sharded_empty_and_all_irregular(rg):
+    from rogtk_amd import dist as RD
+
+    for col in ([], [None, None], [b"NNNN", b"acgt", b"ACG", None, b"NNNN"]):
+        off, vals, vbits = (t.cuda() for t in _arrow(col))
+        cid, k = RD.umi_cluster_sharded(off, vals, len(col), 4, 1, validity=vbits)
+        got = cid.cpu().numpy().view(np.uint32).tolist()
+        if len(col) == 5:
+            assert k == 3 and got == [1, 2, 0, 0xFFFFFFFF, 1]  # b"ACG" < b"NNNN" < b"acgt"
+        else:
+            assert k == 0 and all(g == 0xFFFFFFFF for g in got)
+
+
+def _worker(rank, world, port, L, md, n, seed, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rogtk_amd import dist as RD
+        col = make_column(n, L, seed)
+        start, count = RD.shard_range(n, rank, world)
+        off, vals, vbits = (t.cuda() for t in _arrow(col[start:start + count]))
+        cid, k = RD.umi_cluster_sharded(off, vals, count, L, md, validity=vbits)
+        out_q.put((rank, start, cid.cpu().numpy().view(np.uint32).copy(), k))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("L,md", [(12, 1), (24, 1), (32, 0)])
+def test_sharded_world2_matches_oracle(rg, L, md):
+    from oracle import pyoracle as P
+
+    world, n, seed = 2, 20_000, 11 + L
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, L, md, n, seed, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=100) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    col = make_column(n, L, seed)
+    ref, valid, rk, _ = P.umi_cluster(P.StrCol.from_list(col), L, md)
+    got = np.zeros(n, dtype=np.uint32)
+    for rank, start, ids, k in results:
+        assert k == rk
+        got[start:start + len(ids)] = ids
+    assert np.array_equal(got[valid], ref[valid])
