@@ -367,6 +367,16 @@ int rogtk_masked_records(const uint64_t* D, int64_t n, int umi_len, int world, u
     if (n == 0) return ROGTK_OK;
     ROGTK_REQUIRE(D && mk && pos && code, ROGTK_E_INVALID, "masked_records: NULL buffer");
     hipStream_t s = (hipStream_t)stream;
+    if (world == 1) {  // one destination: records in (code, position) order, no packing sort
+        Scratch S1;
+        if (int rc = S1.get((size_t)total * 4, s)) return rc;
+        hipLaunchKernelGGL(k_iota, grid(total, 16384), dim3(kB), 0, s, (uint32_t*)S1.p, total);
+        hipLaunchKernelGGL(k_record_fill, grid(total, 16384), dim3(kB), 0, s, D, (const uint32_t*)S1.p, total,
+                           umi_len, mk, pos, code);
+        ROGTK_HIP_CHECK(hipGetLastError());
+        counts[0] = total;
+        return ROGTK_OK;
+    }
     size_t sort_b = 0;
     ROGTK_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_b, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                                        (uint32_t*)nullptr, (uint32_t*)nullptr, (int)total, 0, 32, s));
