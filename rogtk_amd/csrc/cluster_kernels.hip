@@ -42,6 +42,8 @@
 
 #include <atomic>
 #include <thread>
+#include <chrono>
+#include <cstring>
 
 #include "rogtk_internal.h"
 
@@ -1144,30 +1146,54 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
                                                        const uint64_t* __restrict__ rbits,
                                                        const uint32_t* __restrict__ rpref,
                                                        const uint32_t* __restrict__ rblkoff,
-                                                       uint32_t* __restrict__ wlab) {
+                                                       uint32_t* __restrict__ wlab, uint64_t* __restrict__ wexc,
+                                                       int use_exc) {
     for (int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x; w < words; w += (int64_t)gridDim.x * kBlock) {
         const uint32_t ur = UR[w];
         uint32_t root = kNone;
+        uint64_t exc = 0;
         if (ur != kNone) {
             root = f[ur];
         } else {
             const uint4 e = RT[w];
-            uint64_t m = rt_word(e);
+            const uint64_t m = rt_word(e);
             const int cnt = __popcll(m);
             if (cnt > 0 && (int64_t)e.z + cnt <= max_distinct) {
-                root = f[e.z];
-                for (int k = 1; k < cnt; ++k)
-                    if (f[e.z + k] != root) {
-                        root = kNone;
-                        break;
+                // the word's label is its most frequent root (Boyer-Moore vote; any choice
+                // is exact): the codes of other components are the exceptions, labelled
+                // per code
+                uint32_t cand = f[e.z], votes = 1;
+                for (int k = 1; k < cnt; ++k) {
+                    const uint32_t r = f[e.z + k];
+                    if (r == cand) ++votes;
+                    else if (votes == 0) {
+                        cand = r;
+                        votes = 1;
+                    } else {
+                        --votes;
                     }
+                }
+                root = cand;
+                uint64_t mm = m;
+                for (int k = 0; mm; ++k) {
+                    const int b = __ffsll((long long)mm) - 1;
+                    mm &= mm - 1;
+                    if (f[e.z + k] != cand) exc |= 1ull << b;
+                }
             }
         }
-        wlab[w] = root != kNone ? root_label(root, rbits, rpref, rblkoff) : kNone;
+        // bit 31 flags a word with exceptions (labels < 2^31: umi_len <= 15; at 16 a word
+        // with exceptions stays unlabelled and all its codes are labelled per code)
+        if (exc && !use_exc) root = kNone;  // A/B: only uniform words labelled by word
+        uint32_t lab = root != kNone ? root_label(root, rbits, rpref, rblkoff) : kNone;
+        if (exc && lab != kNone) lab = lab < 0x80000000u ? (lab | 0x80000000u) : kNone;
+        wlab[w] = lab;
+        wexc[w] = exc;
     }
 }
 
-// Dense labels (max_distance 1): words with a shared root take wlab, the other codes
+// Dense labels (max_distance 1) of the exception codes only (wexc: codes outside their
+// word's labelled component; every other code is labelled by its word). Exception codes
 // are live (their f is their root). labelcode[code] (L <= 13) or ilab[index] (index
 // space). Dense code spaces run one lane per code (a wave per word: stores contiguous
 // per word); sparse ones one lane per index (D holds the codes; no idle lanes).
@@ -1177,8 +1203,19 @@ __device__ __forceinline__ void put_label(uint64_t c, uint32_t i, uint32_t lab, 
     else ilab[i] = lab;
 }
 
+// The label of code c from its word (kNone: label it per code): wlab[w] = the label of
+// the word's most frequent component, bit 31 set when some of its codes (wexc[w]) belong
+// to other components. Only flagged words cost a second (2 MB-table) load.
+__device__ __forceinline__ uint32_t word_label_of(const uint32_t* __restrict__ wlab,
+                                                  const uint64_t* __restrict__ wexc, uint64_t c) {
+    const uint32_t wl = wlab[c >> 6];
+    if (wl == kNone || !(wl >> 31)) return wl;
+    return ((wexc[c >> 6] >> (c & 63)) & 1ull) ? kNone : (wl & 0x7FFFFFFFu);
+}
+
 __global__ __launch_bounds__(kBlock) void k_label(const uint32_t* __restrict__ f, const uint4* __restrict__ RT,
-                                                  const uint32_t* __restrict__ wlab, uint64_t nbits,
+                                                  const uint32_t* __restrict__ wlab,
+                                                  const uint64_t* __restrict__ wexc, uint64_t nbits,
                                                   const uint64_t* __restrict__ rbits,
                                                   const uint32_t* __restrict__ rpref,
                                                   const uint32_t* __restrict__ rblkoff,
@@ -1191,34 +1228,34 @@ __global__ __launch_bounds__(kBlock) void k_label(const uint32_t* __restrict__ f
         const int64_t nd = live_distinct(stats, max_distinct);
         for (int64_t i = (int64_t)lane0; i < nd; i += (int64_t)lanes) {
             const uint32_t c = D[i];
-            const uint32_t wl = wlab[c >> 6];
-            const uint32_t lab = wl != kNone ? wl : root_label(f[i], rbits, rpref, rblkoff);
-            put_label(c, (uint32_t)i, lab, labelcode, ilab);
+            if (word_label_of(wlab, wexc, c) != kNone) continue;  // labelled by its word
+            put_label(c, (uint32_t)i, root_label(f[i], rbits, rpref, rblkoff), labelcode, ilab);
         }
         return;
     }
     for (uint64_t c = lane0; c < nbits; c += lanes) {
-        const uint4 e = RT[c >> 6];
-        const uint32_t wl = wlab[c >> 6];
+        const uint64_t w = c >> 6;
+        if (word_label_of(wlab, wexc, c) != kNone) continue;  // labelled by its word (absent codes: below)
+        const uint4 e = RT[w];
         const uint64_t m = rt_word(e);
         if (!((m >> (c & 63)) & 1ull)) continue;
         const uint32_t i = e.z + (uint32_t)__popcll(m & ((1ull << (c & 63)) - 1ull));
         if ((int64_t)i >= max_distinct) continue;
-        put_label(c, i, wl != kNone ? wl : root_label(f[i], rbits, rpref, rblkoff), labelcode, ilab);
+        put_label(c, i, root_label(f[i], rbits, rpref, rblkoff), labelcode, ilab);
     }
 }
 
 // MODE 0: labelcode[code]; MODE 1: flab[rank(code)] (labels by index, ilab).
-// wlab (max_distance 1 only, else NULL): the label of every word whose codes share one
-// root, 4 B per 64 codes (1 MB at L = 12, L2-resident): most rows resolve there and only
-// the others gather from the 4^L-entry table.
+// wlab / wexc (max_distance 1 only, else NULL): per 64 codes the label of the word's most
+// frequent component (1 MB at L = 12, L2-resident) and, for flagged words only, the mask
+// of its other codes (2 MB): only exception codes gather from the 4^L-entry table.
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ codes,
                                                    const uint64_t* __restrict__ regbits, int64_t n,
                                                    const uint32_t* __restrict__ labelcode,
                                                    const uint32_t* __restrict__ flab,
                                                    const uint4* __restrict__ RT, const uint32_t* __restrict__ wlab,
-                                                   uint32_t* __restrict__ out) {
+                                                   const uint64_t* __restrict__ wexc, uint32_t* __restrict__ out) {
     const int64_t row0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
     if (row0 >= n) return;
     const bool full = row0 + 4 <= n;
@@ -1236,7 +1273,7 @@ __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ 
     for (int k = 0; k < 4; ++k) {
         id[k] = 0xFFFFFFFFu;
         if ((reg >> k) & 1u) {
-            const uint32_t wl = wlab ? wlab[c[k] >> 6] : kNone;
+            const uint32_t wl = wlab ? word_label_of(wlab, wexc, c[k]) : kNone;
             id[k] = wl != kNone ? wl : MODE == 0 ? labelcode[c[k]] : flab[rt_rank(RT[c[k] >> 6], c[k])];
         }
     }
@@ -1449,8 +1486,11 @@ std::atomic<int> g_global_mode{kGlobalRounds};
 // assign (or rogtk_cluster_stats) checks them and only then, if the speculative
 // rounds were not enough, runs more rounds and relabels.
 struct ResolveState {
-    hipEvent_t ev = nullptr;
-    uint8_t* hstats = nullptr;  // pinned copy of the stats block (round flags, edge overflow)
+    // the stats block (round flags, edge overflow) published by k_publish_stats into
+    // mapped, coherent host memory, followed by a sequence word = the resolve's epoch
+    uint8_t* hstats = nullptr;
+    uint8_t* hstats_dev = nullptr;  // its device address
+    uint64_t epoch = 0;
     int launched = 0;
     int mode = 0;  // global mode of the pending resolve
     bool pending = false;
@@ -1477,6 +1517,29 @@ EdgeSink edge_sink(const ClusterLayout& cl, const WsPtrs& p, int round) {
     o.cap = (unsigned int)cl.ecap;
     o.ovf = p.stats + S_EDGE_OVF;
     return o;
+}
+
+// k_publish_stats: the stats block into mapped host memory, then the sequence word
+__global__ __launch_bounds__(128) void k_publish_stats(const unsigned long long* __restrict__ stats,
+                                                       unsigned long long* host, unsigned long long epoch) {
+    for (int k = threadIdx.x; k < kStatsBytes / 8; k += 128)
+        __hip_atomic_store(host + k, stats[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(host + kStatsBytes / 8, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Host side: spin until this resolve's stats are published (normally long done).
+int wait_published(const ResolveState& st) {
+    const volatile unsigned long long* seq = (const volatile unsigned long long*)(st.hstats + kStatsBytes);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (*seq != st.epoch) {
+        std::this_thread::yield();
+        ROGTK_REQUIRE(std::chrono::steady_clock::now() - t0 < std::chrono::seconds(120), ROGTK_E_HIP,
+                      "cluster: resolve flags not published within 120 s (stream stalled?)");
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return ROGTK_OK;
 }
 
 int enqueue_rounds(const ClusterLayout& cl, const WsPtrs& p, int from, int to, hipStream_t s, int mode) {
@@ -1538,11 +1601,15 @@ int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s) {
     {
         ProfScope prof(K_LABEL, s);
         const int lg = grid_for((int64_t)std::min<uint64_t>(cl.nbits, 1ull << 30), 16384);
-        // wpref (consumed into RT by k_rt) holds the word labels
+        // wpref and G (consumed into RT by k_rt) hold the word labels and exception masks
+        static const int use_exc = [] {  // ROGTK_WORD_EXC=0: words with exceptions stay unlabelled (A/B)
+            const char* e = getenv("ROGTK_WORD_EXC");
+            return e && e[0] == '0' ? 0 : 1;
+        }();
         hipLaunchKernelGGL(k_word_label, dim3(grid_for(cl.words, kPersistentGrid)), dim3(kBlock), 0, s, p.f, p.UR,
-                           cl.words, p.RT, cl.max_distinct, p.rbits, p.rpref, p.rblkoff, p.wpref);
-        hipLaunchKernelGGL(k_label, dim3(lg), dim3(kBlock), 0, s, p.f, p.RT, p.wpref, cl.nbits, p.rbits, p.rpref,
-                           p.rblkoff, p.labelcode, p.ilab, p.D, cl.max_distinct, p.stats);
+                           cl.words, p.RT, cl.max_distinct, p.rbits, p.rpref, p.rblkoff, p.wpref, p.G, use_exc);
+        hipLaunchKernelGGL(k_label, dim3(lg), dim3(kBlock), 0, s, p.f, p.RT, p.wpref, p.G, cl.nbits, p.rbits,
+                           p.rpref, p.rblkoff, p.labelcode, p.ilab, p.D, cl.max_distinct, p.stats);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     return ROGTK_OK;
@@ -1616,12 +1683,19 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
             const int spec = g_spec_rounds.load();
             st.mode = g_global_mode.load();
             if (int rc = enqueue_rounds(cl, p, 0, spec, s, st.mode)) return rc;
-            if (!st.ev) {
-                ROGTK_HIP_CHECK(hipEventCreateWithFlags(&st.ev, hipEventDisableTiming));
-                ROGTK_HIP_CHECK(hipHostMalloc((void**)&st.hstats, kStatsBytes, hipHostMallocDefault));
+            if (!st.hstats) {
+                ROGTK_HIP_CHECK(hipHostMalloc((void**)&st.hstats, kStatsBytes + 64,
+                                              hipHostMallocMapped | hipHostMallocCoherent));
+                std::memset(st.hstats, 0, kStatsBytes + 64);
+                ROGTK_HIP_CHECK(hipHostGetDevicePointer((void**)&st.hstats_dev, st.hstats, 0));
             }
-            ROGTK_HIP_CHECK(hipMemcpyAsync(st.hstats, p.stats, kStatsBytes, hipMemcpyDeviceToHost, s));
-            ROGTK_HIP_CHECK(hipEventRecord(st.ev, s));
+            // a one-block kernel stores the flags into host memory and then the epoch: no
+            // copy-engine transfer and no event (a D2H copy + event record cost ~15 us of
+            // the resolve chain)
+            ++st.epoch;
+            hipLaunchKernelGGL(k_publish_stats, dim3(1), dim3(128), 0, s, p.stats,
+                               (unsigned long long*)st.hstats_dev, (unsigned long long)st.epoch);
+            ROGTK_HIP_CHECK(hipGetLastError());
             st.launched = spec;
             st.pending = true;
             if (int rc = enqueue_post_rounds(cl, p, s, st.mode)) return rc;
@@ -1640,14 +1714,7 @@ int cluster_finish(const void* ws, hipStream_t s, int* redone) {
 
 namespace {
 int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone) {
-    // Spin on the event: a blocking hipEventSynchronize woke up ~0.2 ms after the flags
-    // copy completed in the pipelined bench, which delayed the assign launch behind it.
-    for (;;) {
-        const hipError_t q = hipEventQuery(st.ev);
-        if (q == hipSuccess) break;
-        if (q != hipErrorNotReady) ROGTK_HIP_CHECK(q);
-        std::this_thread::yield();
-    }
+    if (int rc = wait_published(st)) return rc;
     unsigned int* hflags = (unsigned int*)(st.hstats + kFlagsOff);
     const bool edge_ovf = st.mode == kGlobalEdges && ((const unsigned long long*)st.hstats)[S_EDGE_OVF] != 0;
     if (!edge_ovf) {
@@ -1725,11 +1792,10 @@ void cluster_release(const void* ws) {
     std::lock_guard<std::mutex> lk(g_rs_mu);
     auto it = g_rs.find(ws);
     if (it == g_rs.end()) return;
-    if (it->second.ev) {
-        hipEventSynchronize(it->second.ev);
-        hipEventDestroy(it->second.ev);
+    if (it->second.hstats) {
+        if (it->second.pending) (void)wait_published(it->second);  // the kernel writes into it
+        hipHostFree(it->second.hstats);
     }
-    if (it->second.hstats) hipHostFree(it->second.hstats);
     g_rs.erase(it);
 }
 
@@ -1763,14 +1829,15 @@ int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, bool word_labels, c
                    const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id, hipStream_t s) {
     if (n <= 0) return ROGTK_OK;
     const uint32_t* wlab = word_labels ? p.wpref : nullptr;
+    const uint64_t* wexc = word_labels ? p.G : nullptr;
     ProfScope prof(K_ASSIGN, s);
     const int g = grid_for((n + 3) / 4);
     if (cl.label_by_code)
         hipLaunchKernelGGL(k_assign<0>, dim3(g), dim3(kBlock), 0, s, codes, regular_bits, n, p.labelcode, p.D,
-                           p.RT, wlab, cluster_id);
+                           p.RT, wlab, wexc, cluster_id);
     else
         hipLaunchKernelGGL(k_assign<1>, dim3(g), dim3(kBlock), 0, s, codes, regular_bits, n, p.labelcode, p.ilab,
-                           p.RT, wlab, cluster_id);
+                           p.RT, wlab, wexc, cluster_id);
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
 }

@@ -1,11 +1,4 @@
-# A/B of an environment knob on bench.py: ENVA vs ENVB (e.g. ENVB="ROGTK_LABEL_BY_INDEX=1")
-set -e
-mkdir -p gpurun_out; : > gpurun_out/ab_env.log
-for round in 1 2; do
-  for v in A B; do
-    if [ $v = A ]; then E="${ENVA:-}"; else E="${ENVB:-}"; fi
-    r=$(env $E timeout -k 10 300 python bench.py --steps 30 --warmup 3 --no-cpu-baseline 2>>gpurun_out/ab.err | tail -1)
-    echo "$v $r" >> gpurun_out/ab_env.log
-    echo "$v $(echo "$r" | python -c "import json,sys; j=json.loads(sys.stdin.read()); k=j['kernels_us']; print(j['ms_per_step'], j['roofline']['frac'], k['score_packed'], k['cluster_mark'], k['cluster_label'], k['cluster_assign'], j['config']['n_clusters'])")"
-  done
-done
+#!/bin/bash
+# A/B of bench.py under environment settings: each argument is "VAR=VAL ..." (or "" for none).
+set -u
+for a in "$@"; do env $a timeout -k 10 120 python bench.py --no-cpu-baseline --steps 30 > gpurun_out/b.log 2>&1 || { tail -5 gpurun_out/b.log; exit 1; }; python -c "import json,sys; j=json.loads(open('gpurun_out/b.log').read().strip().splitlines()[-1]); print(sys.argv[1:], j['ms_per_step'], (j.get('roofline') or {}).get('frac'), j['kernels_us'].get('cluster_assign'), j['kernels_us'].get('cluster_label'))" "$a"; done
