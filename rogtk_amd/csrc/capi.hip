@@ -64,6 +64,8 @@ void prof_drain_locked() {
 }
 }  // namespace
 
+bool profiling_on() { return g_prof.load(std::memory_order_relaxed); }
+
 ProfScope::ProfScope(KernelId id, hipStream_t stream) : id_(id), stream_(stream) {
     if (!g_prof.load(std::memory_order_relaxed) || !((g_prof_mask.load(std::memory_order_relaxed) >> id) & 1u)) return;
     if (hipEventCreate(&start_) != hipSuccess) {

@@ -1302,6 +1302,7 @@ struct WsPtrs {
     uint64_t *rbits, *lroot;
     uint32_t *rpref, *rblksum, *rblkoff, *labelcode, *ilab;
     uint64_t* active;
+    unsigned long long* epoch;  // resolves published (k_publish_stats)
     uint2* edges;             // two lists of ecap pairs
     unsigned int* ecnt;       // per-round list counts (stats block)
 };
@@ -1328,6 +1329,7 @@ inline WsPtrs ws_ptrs(const ClusterLayout& cl, uint8_t* ws) {
     p.ilab = cl.label_by_code ? nullptr : (uint32_t*)(ws + cl.off_ilab);
     p.active = (uint64_t*)(ws + cl.off_active);
     p.edges = (uint2*)(ws + cl.off_edges);
+    p.epoch = (unsigned long long*)(ws + cl.off_epoch);
     p.ecnt = (unsigned int*)(ws + cl.off_stats + kEcntOff);
     return p;
 }
@@ -1402,6 +1404,7 @@ int cluster_layout(int L, int64_t max_distinct, ClusterLayout* o) {
              : ecap_set   ? ecap_set
                           : std::min<int64_t>(std::max<int64_t>(max_distinct / 2, 65536), 1ll << 25);
     c.off_edges = take(2 * std::max<int64_t>(c.ecap, 1) * 8);
+    c.off_epoch = take(8);
     c.total = off;
     *o = c;
     return ROGTK_OK;
@@ -1485,12 +1488,27 @@ std::atomic<int> g_global_mode{kGlobalRounds};
 // copied asynchronously to pinned host memory so resolve never blocks the host;
 // assign (or rogtk_cluster_stats) checks them and only then, if the speculative
 // rounds were not enough, runs more rounds and relabels.
+struct GraphKey {
+    const uint64_t* bitmaps = nullptr;
+    int n_bitmaps = 0, max_distance = -1, mode = 0, spec = 0, L = 0;
+    int64_t max_distinct = 0, ecap = 0;
+    bool operator==(const GraphKey& o) const {
+        return bitmaps == o.bitmaps && n_bitmaps == o.n_bitmaps && max_distance == o.max_distance && mode == o.mode &&
+               spec == o.spec && L == o.L && max_distinct == o.max_distinct && ecap == o.ecap;
+    }
+};
+
 struct ResolveState {
     // the stats block (round flags, edge overflow) published by k_publish_stats into
     // mapped, coherent host memory, followed by a sequence word = the resolve's epoch
     uint8_t* hstats = nullptr;
     uint8_t* hstats_dev = nullptr;  // its device address
-    uint64_t epoch = 0;
+    uint64_t epoch = 0;             // resolves with rounds published so far (device: p.epoch)
+    // the resolve as a replayable graph (launch_cluster_resolve)
+    GraphKey gkey{};
+    hipGraphExec_t gexec = nullptr;
+    hipStream_t cap = nullptr;
+    int glaunched = 0;
     int launched = 0;
     int mode = 0;  // global mode of the pending resolve
     bool pending = false;
@@ -1521,12 +1539,15 @@ EdgeSink edge_sink(const ClusterLayout& cl, const WsPtrs& p, int round) {
 
 // k_publish_stats: the stats block into mapped host memory, then the sequence word
 __global__ __launch_bounds__(128) void k_publish_stats(const unsigned long long* __restrict__ stats,
-                                                       unsigned long long* host, unsigned long long epoch) {
+                                                       unsigned long long* host, unsigned long long* epoch) {
     for (int k = threadIdx.x; k < kStatsBytes / 8; k += 128)
         __hip_atomic_store(host + k, stats[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __syncthreads();
-    if (threadIdx.x == 0)
-        __hip_atomic_store(host + kStatsBytes / 8, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) {
+        const unsigned long long e = *epoch + 1;  // one publish per resolve: no race
+        *epoch = e;
+        __hip_atomic_store(host + kStatsBytes / 8, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // Host side: spin until this resolve's stats are published (normally long done).
@@ -1630,6 +1651,70 @@ int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, bool word_labels, c
 int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone = nullptr);
 }  // namespace
 
+namespace {
+// The kernels of one resolve, enqueued on s (direct, or into a graph under capture).
+// Returns the number of speculative rounds launched (0: no global rounds), -1 on error.
+int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bitmaps, int n_bitmaps,
+                    int max_distance, int mode, int spec, unsigned long long* host_stats, hipStream_t s) {
+    {
+        ProfScope prof(K_SCAN, s);
+        hipLaunchKernelGGL(k_scan_words, dim3((unsigned)cl.blocks), dim3(kBlock), 0, s, bitmaps,
+                           n_bitmaps, cl.words, (const unsigned long long*)nullptr, p.G, p.wpref,
+                           p.blksum);
+        hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, p.blksum, cl.blocks, p.blkoff,
+                           p.stats, (int)S_NDISTINCT, max_distance == 0 ? (int)S_NCLUSTERS : -1, 1);
+    }
+    {
+        ProfScope prof(K_COMPACT, s);
+        hipLaunchKernelGGL(k_rt, dim3(grid_for(cl.words)), dim3(kBlock), 0, s, p.G, cl.words, p.wpref,
+                           p.blkoff, p.RT, p.lroot, max_distance == 0 ? 0 : cl.rwords);
+        if (max_distance == 0) {
+            const int cgrid = grid_for((int64_t)std::min<uint64_t>(cl.nbits, 1ull << 30), 16384);
+            hipLaunchKernelGGL(k_build_d, dim3(cgrid), dim3(kBlock), 0, s, p.RT, cl.nbits, p.D, p.f, p.labelcode, p.ilab,
+                               cl.max_distinct, p.stats);
+            return hipGetLastError() == hipSuccess ? 0 : -1;  // labels = ranks (labelcode / ilab)
+        }
+    }
+    int launched = 0;
+    {
+        ProfScope prof(K_UNION, s);
+        const int64_t lblocks = (cl.words + kLocalWords - 1) / kLocalWords;
+        hipLaunchKernelGGL(k_local_cc, dim3((unsigned)lblocks), dim3(kBlock), 0, s, p.RT, cl.words, cl.L,
+                           p.f, p.D, p.UR, p.lroot, cl.rwords, cl.max_distinct, p.stats);
+        if (cl.L > kLocalPos && mode == kGlobalUnionFind) {
+            // one-pass union-find: exact when the stream reaches the labels
+            const int64_t tasks = (int64_t)(cl.L - kLocalPos) * (cl.words >> 2);
+            hipLaunchKernelGGL(k_union_g, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words, cl.L,
+                               kLocalPos, p.f);
+            hipLaunchKernelGGL(k_flatten_live, dim3(grid_for(cl.max_distinct, kPersistentGrid)), dim3(kBlock), 0, s,
+                               p.f, p.lroot, cl.max_distinct, p.stats);
+        } else if (cl.L > kLocalPos) {
+            if (enqueue_rounds(cl, p, 0, spec, s, mode)) return -1;
+            // a one-block kernel stores the flags into mapped host memory and then the
+            // resolve's epoch (counted on the device): no copy-engine transfer and no event
+            // (a D2H copy + event record cost ~15 us of the resolve chain)
+            hipLaunchKernelGGL(k_publish_stats, dim3(1), dim3(128), 0, s, (const unsigned long long*)p.stats,
+                               host_stats, p.epoch);
+            if (enqueue_post_rounds(cl, p, s, mode)) return -1;
+            launched = spec;
+        }
+    }
+    if (enqueue_labels(cl, p, s)) return -1;
+    return hipGetLastError() == hipSuccess ? launched : -1;
+}
+
+// ROGTK_RESOLVE_GRAPH=1: replay the resolve as a hipGraph (A/B knob, off by default:
+// measured 0.536 vs 0.411 ms/step at 10M - the graph replays ran without overlapping the
+// other streams' kernels, serialising the pipeline)
+bool graphs_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("ROGTK_RESOLVE_GRAPH");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+}  // namespace
+
 int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t* bitmaps,
                            int n_bitmaps, int max_distance, hipStream_t s) {
     WsPtrs p = ws_ptrs(cl, ws);
@@ -1643,65 +1728,58 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
     st.rounds = 0;
     st.cl = cl;
     st.word_labels = max_distance == 1;
-    {
-        ProfScope prof(K_SCAN, s);
-        hipLaunchKernelGGL(k_scan_words, dim3((unsigned)cl.blocks), dim3(kBlock), 0, s, bitmaps,
-                           n_bitmaps, cl.words, (const unsigned long long*)nullptr, p.G, p.wpref,
-                           p.blksum);
-        hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, p.blksum, cl.blocks, p.blkoff,
-                           p.stats, (int)S_NDISTINCT, max_distance == 0 ? (int)S_NCLUSTERS : -1, 1);
-        ROGTK_HIP_CHECK(hipGetLastError());
+    const int mode = g_global_mode.load();
+    const int spec = g_spec_rounds.load();
+    const bool rounds = max_distance == 1 && cl.L > kLocalPos && mode != kGlobalUnionFind;
+    if (rounds && !st.hstats) {
+        ROGTK_HIP_CHECK(hipHostMalloc((void**)&st.hstats, kStatsBytes + 64, hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(st.hstats, 0, kStatsBytes + 64);
+        ROGTK_HIP_CHECK(hipHostGetDevicePointer((void**)&st.hstats_dev, st.hstats, 0));
     }
-    {
-        ProfScope prof(K_COMPACT, s);
-        hipLaunchKernelGGL(k_rt, dim3(grid_for(cl.words)), dim3(kBlock), 0, s, p.G, cl.words, p.wpref,
-                           p.blkoff, p.RT, p.lroot, max_distance == 0 ? 0 : cl.rwords);
-        if (max_distance == 0) {
-            const int cgrid = grid_for((int64_t)std::min<uint64_t>(cl.nbits, 1ull << 30), 16384);
-            hipLaunchKernelGGL(k_build_d, dim3(cgrid), dim3(kBlock), 0, s, p.RT, cl.nbits, p.D, p.f, p.labelcode, p.ilab,
-                               cl.max_distinct, p.stats);
-            ROGTK_HIP_CHECK(hipGetLastError());
-            return ROGTK_OK;  // labels = ranks (labelcode / ilab)
-        }
-    }
-    {
-        ProfScope prof(K_UNION, s);
-        const int64_t lblocks = (cl.words + kLocalWords - 1) / kLocalWords;
-        hipLaunchKernelGGL(k_local_cc, dim3((unsigned)lblocks), dim3(kBlock), 0, s, p.RT, cl.words, cl.L,
-                           p.f, p.D, p.UR, p.lroot, cl.rwords, cl.max_distinct, p.stats);
-        ROGTK_HIP_CHECK(hipGetLastError());
-        if (cl.L > kLocalPos && g_global_mode.load() == kGlobalUnionFind) {
-            // one-pass union-find: exact when the stream reaches the labels
-            const int64_t tasks = (int64_t)(cl.L - kLocalPos) * (cl.words >> 2);
-            hipLaunchKernelGGL(k_union_g, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words, cl.L,
-                               kLocalPos, p.f);
-            hipLaunchKernelGGL(k_flatten_live, dim3(grid_for(cl.max_distinct, kPersistentGrid)), dim3(kBlock), 0, s,
-                               p.f, p.lroot, cl.max_distinct, p.stats);
-            ROGTK_HIP_CHECK(hipGetLastError());
-            st.rounds = 1;
-        } else if (cl.L > kLocalPos) {
-            const int spec = g_spec_rounds.load();
-            st.mode = g_global_mode.load();
-            if (int rc = enqueue_rounds(cl, p, 0, spec, s, st.mode)) return rc;
-            if (!st.hstats) {
-                ROGTK_HIP_CHECK(hipHostMalloc((void**)&st.hstats, kStatsBytes + 64,
-                                              hipHostMallocMapped | hipHostMallocCoherent));
-                std::memset(st.hstats, 0, kStatsBytes + 64);
-                ROGTK_HIP_CHECK(hipHostGetDevicePointer((void**)&st.hstats_dev, st.hstats, 0));
+    unsigned long long* hs = (unsigned long long*)st.hstats_dev;
+    // The resolve is ~17 small kernels. With ROGTK_RESOLVE_GRAPH=1 the sequence (a
+    // function of the workspace, the bitmaps pointer / count and the knobs) is captured
+    // once into a hipGraph per such key and replayed with one launch (never while
+    // profiling: the per-phase events need the direct launches).
+    const GraphKey key{bitmaps, n_bitmaps, max_distance, mode, spec, cl.L, cl.max_distinct, cl.ecap};
+    const bool graph = graphs_enabled() && !profiling_on();
+    int launched = 0;
+    if (graph) {
+        if (!st.gexec || !(st.gkey == key)) {
+            if (st.gexec) {
+                ROGTK_HIP_CHECK(hipStreamSynchronize(s));  // a replay may still be in flight
+                hipGraphExecDestroy(st.gexec);
+                st.gexec = nullptr;
             }
-            // a one-block kernel stores the flags into host memory and then the epoch: no
-            // copy-engine transfer and no event (a D2H copy + event record cost ~15 us of
-            // the resolve chain)
-            ++st.epoch;
-            hipLaunchKernelGGL(k_publish_stats, dim3(1), dim3(128), 0, s, p.stats,
-                               (unsigned long long*)st.hstats_dev, (unsigned long long)st.epoch);
-            ROGTK_HIP_CHECK(hipGetLastError());
-            st.launched = spec;
-            st.pending = true;
-            if (int rc = enqueue_post_rounds(cl, p, s, st.mode)) return rc;
+            if (!st.cap) ROGTK_HIP_CHECK(hipStreamCreateWithFlags(&st.cap, hipStreamNonBlocking));
+            hipGraph_t g = nullptr;
+            ROGTK_HIP_CHECK(hipStreamBeginCapture(st.cap, hipStreamCaptureModeThreadLocal));
+            const int r = enqueue_resolve(cl, p, bitmaps, n_bitmaps, max_distance, mode, spec, hs, st.cap);
+            const hipError_t ec = hipStreamEndCapture(st.cap, &g);
+            ROGTK_REQUIRE(r >= 0 && ec == hipSuccess && g, ROGTK_E_HIP, "cluster: resolve graph capture failed (%s)",
+                          hipGetErrorString(ec));
+            const hipError_t ei = hipGraphInstantiate(&st.gexec, g, nullptr, nullptr, 0);
+            hipGraphDestroy(g);
+            ROGTK_REQUIRE(ei == hipSuccess, ROGTK_E_HIP, "cluster: resolve graph instantiate failed (%s)",
+                          hipGetErrorString(ei));
+            st.gkey = key;
+            st.glaunched = r;
         }
+        ROGTK_HIP_CHECK(hipGraphLaunch(st.gexec, s));
+        launched = st.glaunched;
+    } else {
+        launched = enqueue_resolve(cl, p, bitmaps, n_bitmaps, max_distance, mode, spec, hs, s);
+        ROGTK_REQUIRE(launched >= 0, ROGTK_E_HIP, "cluster: resolve launch failed (%s)",
+                      hipGetErrorString(hipGetLastError()));
     }
-    return enqueue_labels(cl, p, s);
+    if (max_distance == 1 && cl.L > kLocalPos && mode == kGlobalUnionFind) st.rounds = 1;
+    if (rounds) {
+        ++st.epoch;  // k_publish_stats publishes the device count of resolves, which matches
+        st.mode = mode;
+        st.launched = launched;
+        st.pending = true;
+    }
+    return ROGTK_OK;
 }
 
 int cluster_finish(const void* ws, hipStream_t s, int* redone) {
@@ -1796,6 +1874,8 @@ void cluster_release(const void* ws) {
         if (it->second.pending) (void)wait_published(it->second);  // the kernel writes into it
         hipHostFree(it->second.hstats);
     }
+    if (it->second.gexec) hipGraphExecDestroy(it->second.gexec);
+    if (it->second.cap) hipStreamDestroy(it->second.cap);
     g_rs.erase(it);
 }
 

@@ -53,6 +53,7 @@ enum KernelId {
 };
 extern const char* const kKernelNames[K_COUNT_];
 
+bool profiling_on();
 // Brackets one launch with HIP events on `stream` when profiling is enabled.
 class ProfScope {
    public:
@@ -177,7 +178,7 @@ struct ClusterLayout {
     // byte offsets into the workspace
     int64_t off_stats, off_presence, off_bitmap, off_rt, off_wpref, off_blksum, off_blkoff, off_D, off_f, off_ur,
         off_rbits, off_lroot, off_rpref, off_rblksum, off_rblkoff, off_labelcode, off_ilab, off_active,
-        active_words, off_edges, ecap, total;
+        active_words, off_edges, ecap, off_epoch, total;
 };
 int cluster_layout(int L, int64_t max_distinct, ClusterLayout* out);
 
