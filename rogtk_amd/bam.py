@@ -408,6 +408,50 @@ def _concat_dev(offs, vals, valids, counts, dev):
     return off, val, packed.view(torch.int64), n
 
 
+def _umi_table(off, val, vw, n, names, cid, n_clusters, extra=None) -> pa.Table:
+    o = off.cpu().numpy()
+    v = val.cpu().numpy()
+    bits = vw.cpu().numpy().view(np.uint8)[: (n + 7) // 8] if n else np.zeros(1, np.uint8)
+    valid = np.unpackbits(bits, bitorder="little")[:n].astype(bool)
+    vbuf = None if valid.all() else pa.py_buffer(np.packbits(valid, bitorder="little"))
+    umi = pa.Array.from_buffers(pa.large_string(), n, [vbuf, pa.py_buffer(o), pa.py_buffer(v)]).cast(pa.string())
+    ids = cid[:n].cpu().numpy().view(np.uint32)
+    cl = pa.Array.from_buffers(pa.uint32(), n, [vbuf, pa.py_buffer(ids.copy())])
+    cols = {"name": names if names is not None else pa.array([], pa.string()), "umi": umi, "cluster_id": cl}
+    cols.update(extra or {})
+    t = pa.table(cols)
+    return t.replace_schema_metadata({"n_clusters": str(int(n_clusters))})
+
+
+def bams_umi_cluster(bam_paths: Sequence[str], umi_len: int = 12, max_distance: int = 1, source: str = "sequence",
+                     sep: str = "_", mode: str = "htslib", n_threads: int = 0, group=None) -> pa.Table:
+    """Config C5 across ranks (one process per GPU): rank r decodes bam_paths[r::world] on
+    its GPU, and the ranks merge their UMI clusters with the all-to-all H3
+    (rogtk_amd.dist.umi_cluster_sharded). Returns this rank's rows {name, umi, cluster_id,
+    source}: ids are those of umi_cluster over all files' UMIs together (DESIGN.md §4:
+    they depend only on the set of distinct UMIs), identical on every rank."""
+    import torch
+
+    from . import dist as RD
+
+    W = RD.world(group)
+    r = torch.distributed.get_rank(group) if W > 1 else 0
+    mine = list(bam_paths)[r::W]
+    dev = torch.device("cuda", torch.cuda.current_device())
+    parts, names, srcs = [], [], []
+    for path in mine:
+        (off, val, vw, n), nm = bam_umis_dev(path, umi_len, source, sep, mode, n_threads, with_names=True)
+        parts.append((off, val, vw, n))
+        names.append(nm if nm is not None else pa.array([], pa.string()))
+        srcs.append(pa.array([path] * n, pa.string()))
+    off, val, vw, n = _concat_dev([p[0] for p in parts], [p[1] for p in parts], [p[2] for p in parts],
+                                  [p[3] for p in parts], dev) if parts else _concat_dev([], [], [], [], dev)
+    cid, k = RD.umi_cluster_sharded(off, val, n, umi_len, max_distance, validity=vw.view(torch.uint8), group=group)
+    nm = pa.concat_arrays(names) if names else pa.array([], pa.string())
+    src = pa.concat_arrays(srcs) if srcs else pa.array([], pa.string())
+    return _umi_table(off, val, vw, n, nm, cid, k, {"source": src})
+
+
 def bam_umi_cluster(bam_path: str, umi_len: int = 12, max_distance: int = 1, source: str = "sequence",
                     sep: str = "_", mode: str = "htslib", n_threads: int = 0) -> pa.Table:
     """Config C5: BAM -> GPU decode -> UMI column -> H3 cluster ids (and the UMI).
@@ -422,14 +466,4 @@ def bam_umi_cluster(bam_path: str, umi_len: int = 12, max_distance: int = 1, sou
     _lib.call("rogtk_umi_cluster_dev", ctypes.c_void_p(off.data_ptr()), ctypes.c_void_p(val.data_ptr()),
               ctypes.c_void_p(vw.data_ptr()), n, int(umi_len), int(max_distance), ctypes.c_void_p(cid.data_ptr()),
               ctypes.byref(ncl), ctypes.c_void_p(stream.cuda_stream))
-    o = off.cpu().numpy()
-    v = val.cpu().numpy()
-    bits = vw.cpu().numpy().view(np.uint8)[: (n + 7) // 8] if n else np.zeros(1, np.uint8)
-    valid = np.unpackbits(bits, bitorder="little")[:n].astype(bool)
-    vbuf = None if valid.all() else pa.py_buffer(np.packbits(valid, bitorder="little"))
-    umi = pa.Array.from_buffers(pa.large_string(), n, [vbuf, pa.py_buffer(o), pa.py_buffer(v)]).cast(pa.string())
-    ids = cid[:n].cpu().numpy().view(np.uint32)
-    cl = pa.Array.from_buffers(pa.uint32(), n, [vbuf, pa.py_buffer(ids.copy())])
-    t = pa.table({"name": names if names is not None else pa.array([], pa.string()), "umi": umi, "cluster_id": cl})
-    t = t.replace_schema_metadata({"n_clusters": str(int(ncl.value))})
-    return t
+    return _umi_table(off, val, vw, n, names, cid, ncl.value)

@@ -102,3 +102,77 @@ def test_sharded_world2_matches_oracle(rg, L, md):
         assert k == rk
         got[start:start + len(ids)] = ids
     assert np.array_equal(got[valid], ref[valid])
+
+
+# ---- config C5 across ranks: BAM files sharded over ranks, clusters merged by all-to-all
+
+def _bam_files(tmp, k):
+    from rogtk_amd import synth_bam
+    paths = []
+    for i in range(k):
+        p = os.path.join(tmp, f"part{i}.bam")
+        synth_bam.synth_bam(p, 4000 + 997 * i, seed=0x524F47544B + i, level=1)
+        paths.append(p)
+    return paths
+
+
+def _bam_oracle(paths, md):
+    from oracle import pybam
+    from oracle import pyoracle as P
+    umis, names = [], []
+    for p in paths:
+        for r in pybam.bam_rows(p, "htslib"):
+            s = r["sequence"]
+            umis.append(None if s is None else s[:12].encode())
+            names.append((p, r["name"]))
+    rc, rv, rk, _ = P.umi_cluster(P.StrCol.from_list(umis), 12, md)
+    return {key: (int(c), bool(v)) for key, c, v in zip(names, rc, rv)}, rk
+
+
+def _bam_worker(rank, world, port, paths, md, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rogtk_amd import bam as B
+        t = B.bams_umi_cluster(paths, umi_len=12, max_distance=md)
+        out_q.put((rank, t.column("source").to_pylist(), t.column("name").to_pylist(),
+                   t.column("cluster_id").to_pylist(), int(t.schema.metadata[b"n_clusters"])))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+@pytest.mark.parametrize("md", [0, 1])
+def test_bams_umi_cluster_sharded_matches_oracle(rg, tmp_path, world, md):
+    """Every record of 3 BAM files, decoded on the rank that owns its file, gets the id the
+    oracle gives it over all files' UMIs together."""
+    paths = _bam_files(str(tmp_path), 3)
+    want, rk = _bam_oracle(paths, md)
+    if world == 1:
+        from rogtk_amd import bam as B
+        t = B.bams_umi_cluster(paths, umi_len=12, max_distance=md)
+        results = [(0, t.column("source").to_pylist(), t.column("name").to_pylist(),
+                    t.column("cluster_id").to_pylist(), int(t.schema.metadata[b"n_clusters"]))]
+    else:
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_bam_worker, args=(r, world, port, paths, md, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        results = [q.get(timeout=100) for _ in range(world)]
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    seen = 0
+    for rank, src, names, ids, k in results:
+        assert k == rk
+        for s, nm, c in zip(src, names, ids):
+            wc, wv = want[(s, nm)]
+            assert (c is None) == (not wv)
+            if wv:
+                assert c == wc
+            seen += 1
+    assert seen == len(want)
