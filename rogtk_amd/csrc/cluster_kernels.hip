@@ -1256,32 +1256,33 @@ __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ flab,
                                                    const uint4* __restrict__ RT, const uint32_t* __restrict__ wlab,
                                                    const uint64_t* __restrict__ wexc, uint32_t* __restrict__ out) {
-    const int64_t row0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
-    if (row0 >= n) return;
-    const bool full = row0 + 4 <= n;
-    uint32_t c[4] = {0, 0, 0, 0};
-    if (full) {
-        const u32x4_t v = stream_load(reinterpret_cast<const u32x4_t*>(codes + row0));
-        c[0] = v.x; c[1] = v.y; c[2] = v.z; c[3] = v.w;
-    } else {
-        for (int k = 0; k < 4; ++k)
-            if (row0 + k < n) c[k] = codes[row0 + k];
-    }
-    uint32_t reg = regbits ? (uint32_t)(regbits[row0 >> 6] >> (row0 & 63)) & 0xFu : 0xFu;
-    uint32_t id[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        id[k] = 0xFFFFFFFFu;
-        if ((reg >> k) & 1u) {
-            const uint32_t wl = wlab ? word_label_of(wlab, wexc, c[k]) : kNone;
-            id[k] = wl != kNone ? wl : MODE == 0 ? labelcode[c[k]] : flab[rt_rank(RT[c[k] >> 6], c[k])];
+    for (int64_t row0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4; row0 < n;
+         row0 += (int64_t)gridDim.x * kBlock * 4) {
+        const bool full = row0 + 4 <= n;
+        uint32_t c[4] = {0, 0, 0, 0};
+        if (full) {
+            const u32x4_t v = stream_load(reinterpret_cast<const u32x4_t*>(codes + row0));
+            c[0] = v.x; c[1] = v.y; c[2] = v.z; c[3] = v.w;
+        } else {
+            for (int k = 0; k < 4; ++k)
+                if (row0 + k < n) c[k] = codes[row0 + k];
         }
-    }
-    if (full) {
-        stream_store(u32x4_t{id[0], id[1], id[2], id[3]}, reinterpret_cast<u32x4_t*>(out + row0));
-    } else {
-        for (int k = 0; k < 4; ++k)
-            if (row0 + k < n) out[row0 + k] = id[k];
+        uint32_t reg = regbits ? (uint32_t)(regbits[row0 >> 6] >> (row0 & 63)) & 0xFu : 0xFu;
+        uint32_t id[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            id[k] = 0xFFFFFFFFu;
+            if ((reg >> k) & 1u) {
+                const uint32_t wl = wlab ? word_label_of(wlab, wexc, c[k]) : kNone;
+                id[k] = wl != kNone ? wl : MODE == 0 ? labelcode[c[k]] : flab[rt_rank(RT[c[k] >> 6], c[k])];
+            }
+        }
+        if (full) {
+            stream_store(u32x4_t{id[0], id[1], id[2], id[3]}, reinterpret_cast<u32x4_t*>(out + row0));
+        } else {
+            for (int k = 0; k < 4; ++k)
+                if (row0 + k < n) out[row0 + k] = id[k];
+        }
     }
 }
 
@@ -1911,7 +1912,21 @@ int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, bool word_labels, c
     const uint32_t* wlab = word_labels ? p.wpref : nullptr;
     const uint64_t* wexc = word_labels ? p.G : nullptr;
     ProfScope prof(K_ASSIGN, s);
-    const int g = grid_for((n + 3) / 4);
+    // Two workgroups per CU, grid-stride: assign runs beside the next batch's resolve,
+    // whose hook rounds are latency-bound; a full grid of gathers (40k waves at 10M rows)
+    // slowed the concurrent hook round 0 from 31 to 94 us. Measured at 10M rows, 2-deep
+    // pipeline: 0.425 ms/step full grid, 0.382-0.385 at 512 workgroups (256 CUs).
+    // ROGTK_ASSIGN_BLOCKS=k overrides (0: full grid; A/B).
+    static const int64_t cap = [] {
+        const char* e = getenv("ROGTK_ASSIGN_BLOCKS");
+        if (e) return std::max<int64_t>(0, atoll(e));
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return (int64_t)2 * cus;
+    }();
+    const int g = grid_for((n + 3) / 4, cap);
     if (cl.label_by_code)
         hipLaunchKernelGGL(k_assign<0>, dim3(g), dim3(kBlock), 0, s, codes, regular_bits, n, p.labelcode, p.D,
                            p.RT, wlab, wexc, cluster_id);

@@ -194,117 +194,120 @@ __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restr
     const int L = P.L;
     // Wave tile of 256 rows; lane l owns rows {2l, 2l+1, 128+2l, 129+2l} so that every
     // 16-B (double2) store instruction of the wave writes 1 KB of contiguous output.
-    const int lane = threadIdx.x & 63;
-    const int64_t base = ((int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63)) * kRowsPerLane;
-    const int64_t rA = base + 2 * lane, rB = rA + 128;
-    const bool full = base + 64 * kRowsPerLane <= n;
+    // grid-stride over 1024-row block tiles (a capped grid keeps fewer waves in flight)
+    for (int64_t tile = blockIdx.x; tile * kBlock * kRowsPerLane < n; tile += gridDim.x) {
+        const int lane = threadIdx.x & 63;
+        const int64_t base = ((int64_t)tile * kBlock + (threadIdx.x & ~63)) * kRowsPerLane;
+        const int64_t rA = base + 2 * lane, rB = rA + 128;
+        const bool full = base + 64 * kRowsPerLane <= n;
 
-    uint32_t c[kRowsPerLane] = {0, 0, 0, 0};
-    uint32_t reg = 0;
-    if (full) {
-        const u32x2_t va = stream_load(reinterpret_cast<const u32x2_t*>(codes + rA));
-        const u32x2_t vb = stream_load(reinterpret_cast<const u32x2_t*>(codes + rB));
-        c[0] = va.x; c[1] = va.y; c[2] = vb.x; c[3] = vb.y;
-        reg = regbits ? ((uint32_t)(regbits[rA >> 6] >> (rA & 63)) & 3u) |
-                            (((uint32_t)(regbits[rB >> 6] >> (rB & 63)) & 3u) << 2)
-                      : 0xFu;
-    } else {
-        const int64_t rr[4] = {rA, rA + 1, rB, rB + 1};
-#pragma unroll
-        for (int k = 0; k < kRowsPerLane; ++k) {
-            if (rr[k] < n) {
-                c[k] = codes[rr[k]];
-                if (!regbits || ((regbits[rr[k] >> 6] >> (rr[k] & 63)) & 1u)) reg |= 1u << k;
-            }
-        }
-    }
-
-    uint32_t wnib = 0;
-    if (rA < n) {
-        if (SCORE) {
-            double sh[4], li[4], ho[4], di[4], du[4], co[4];
-            uint32_t lg[4];
+        uint32_t c[kRowsPerLane] = {0, 0, 0, 0};
+        uint32_t reg = 0;
+        if (full) {
+            const u32x2_t va = stream_load(reinterpret_cast<const u32x2_t*>(codes + rA));
+            const u32x2_t vb = stream_load(reinterpret_cast<const u32x2_t*>(codes + rB));
+            c[0] = va.x; c[1] = va.y; c[2] = vb.x; c[3] = vb.y;
+            reg = regbits ? ((uint32_t)(regbits[rA >> 6] >> (rA & 63)) & 3u) |
+                                (((uint32_t)(regbits[rB >> 6] >> (rB & 63)) & 3u) << 2)
+                          : 0xFu;
+        } else {
+            const int64_t rr[4] = {rA, rA + 1, rB, rB + 1};
 #pragma unroll
             for (int k = 0; k < kRowsPerLane; ++k) {
-                if ((reg >> k) & 1u) {
-                    const RowScore r = score_code<LT>(c[k], L, s_tab[0], s_tab[1], s_tab[2], s_tab[3]);
-                    sh[k] = r.sh; li[k] = r.ling; ho[k] = r.homo; di[k] = r.di; co[k] = r.comb;
-                    lg[k] = r.longest;
-                } else {
-                    sh[k] = li[k] = ho[k] = di[k] = co[k] = 0.0;
-                    lg[k] = 0;
+                if (rr[k] < n) {
+                    c[k] = codes[rr[k]];
+                    if (!regbits || ((regbits[rr[k] >> 6] >> (rr[k] & 63)) & 1u)) reg |= 1u << k;
                 }
-                du[k] = 0.0;
             }
-            if (full) {
-                auto st2 = [&](double* p, const double* v) {
-                    if (!p) return;
-                    score_store(f64x2_t{v[0], v[1]}, reinterpret_cast<f64x2_t*>(p + rA));
-                    score_store(f64x2_t{v[2], v[3]}, reinterpret_cast<f64x2_t*>(p + rB));
-                };
-                st2(O.sh, sh); st2(O.ling, li); st2(O.homo, ho); st2(O.di, di);
-                st2(O.dust, du); st2(O.comb, co);
-                if (O.longest) {
-                    score_store(u32x2_t{lg[0], lg[1]}, reinterpret_cast<u32x2_t*>(O.longest + rA));
-                    score_store(u32x2_t{lg[2], lg[3]}, reinterpret_cast<u32x2_t*>(O.longest + rB));
-                }
-            } else {
-                const int64_t rr[4] = {rA, rA + 1, rB, rB + 1};
+        }
+
+        uint32_t wnib = 0;
+        if (rA < n) {
+            if (SCORE) {
+                double sh[4], li[4], ho[4], di[4], du[4], co[4];
+                uint32_t lg[4];
+#pragma unroll
                 for (int k = 0; k < kRowsPerLane; ++k) {
-                    const int64_t r = rr[k];
-                    if (r >= n) continue;
-                    if (O.sh) O.sh[r] = sh[k];
-                    if (O.ling) O.ling[r] = li[k];
-                    if (O.homo) O.homo[r] = ho[k];
-                    if (O.di) O.di[r] = di[k];
-                    if (O.dust) O.dust[r] = du[k];
-                    if (O.comb) O.comb[r] = co[k];
-                    if (O.longest) O.longest[r] = lg[k];
+                    if ((reg >> k) & 1u) {
+                        const RowScore r = score_code<LT>(c[k], L, s_tab[0], s_tab[1], s_tab[2], s_tab[3]);
+                        sh[k] = r.sh; li[k] = r.ling; ho[k] = r.homo; di[k] = r.di; co[k] = r.comb;
+                        lg[k] = r.longest;
+                    } else {
+                        sh[k] = li[k] = ho[k] = di[k] = co[k] = 0.0;
+                        lg[k] = 0;
+                    }
+                    du[k] = 0.0;
                 }
-            }
-        }
-        if (HAMD || HAMW) {
-            uint32_t d[4];
-#pragma unroll
-            for (int k = 0; k < kRowsPerLane; ++k) {
-                d[k] = 0;
-                if ((reg >> k) & 1u) {
-                    d[k] = P.ham_mode == 1 ? hamming_code(c[k], P) : 0xFFFFFFFFu;
-                    if (P.ham_mode == 1 && d[k] <= P.max_distance) wnib |= 1u << k;
-                }
-            }
-            if (HAMD) {
                 if (full) {
-                    *reinterpret_cast<uint2*>(hd + rA) = make_uint2(d[0], d[1]);
-                    *reinterpret_cast<uint2*>(hd + rB) = make_uint2(d[2], d[3]);
+                    auto st2 = [&](double* p, const double* v) {
+                        if (!p) return;
+                        score_store(f64x2_t{v[0], v[1]}, reinterpret_cast<f64x2_t*>(p + rA));
+                        score_store(f64x2_t{v[2], v[3]}, reinterpret_cast<f64x2_t*>(p + rB));
+                    };
+                    st2(O.sh, sh); st2(O.ling, li); st2(O.homo, ho); st2(O.di, di);
+                    st2(O.dust, du); st2(O.comb, co);
+                    if (O.longest) {
+                        score_store(u32x2_t{lg[0], lg[1]}, reinterpret_cast<u32x2_t*>(O.longest + rA));
+                        score_store(u32x2_t{lg[2], lg[3]}, reinterpret_cast<u32x2_t*>(O.longest + rB));
+                    }
                 } else {
                     const int64_t rr[4] = {rA, rA + 1, rB, rB + 1};
-                    for (int k = 0; k < kRowsPerLane; ++k)
-                        if (rr[k] < n) hd[rr[k]] = d[k];
+                    for (int k = 0; k < kRowsPerLane; ++k) {
+                        const int64_t r = rr[k];
+                        if (r >= n) continue;
+                        if (O.sh) O.sh[r] = sh[k];
+                        if (O.ling) O.ling[r] = li[k];
+                        if (O.homo) O.homo[r] = ho[k];
+                        if (O.di) O.di[r] = di[k];
+                        if (O.dust) O.dust[r] = du[k];
+                        if (O.comb) O.comb[r] = co[k];
+                        if (O.longest) O.longest[r] = lg[k];
+                    }
                 }
             }
-        }
-        if (MARK) {
+            if (HAMD || HAMW) {
+                uint32_t d[4];
 #pragma unroll
-            for (int k = 0; k < kRowsPerLane; ++k)
-                if ((reg >> k) & 1u) pres[c[k]] = 1;  // benign same-value race
-        }
-    }
-    if (HAMW) {
-        // 32 lanes x 2 rows = one 64-row word (LSB = first row): OR-reduce per half-wave.
-        // Lanes 0..31 hold words 0 (rows 0..63) and 2 (rows 128..191) of the tile,
-        // lanes 32..63 words 1 and 3.
-        uint64_t w01 = (uint64_t)(wnib & 3u) << (2 * (lane & 31));
-        uint64_t w23 = (uint64_t)((wnib >> 2) & 3u) << (2 * (lane & 31));
+                for (int k = 0; k < kRowsPerLane; ++k) {
+                    d[k] = 0;
+                    if ((reg >> k) & 1u) {
+                        d[k] = P.ham_mode == 1 ? hamming_code(c[k], P) : 0xFFFFFFFFu;
+                        if (P.ham_mode == 1 && d[k] <= P.max_distance) wnib |= 1u << k;
+                    }
+                }
+                if (HAMD) {
+                    if (full) {
+                        *reinterpret_cast<uint2*>(hd + rA) = make_uint2(d[0], d[1]);
+                        *reinterpret_cast<uint2*>(hd + rB) = make_uint2(d[2], d[3]);
+                    } else {
+                        const int64_t rr[4] = {rA, rA + 1, rB, rB + 1};
+                        for (int k = 0; k < kRowsPerLane; ++k)
+                            if (rr[k] < n) hd[rr[k]] = d[k];
+                    }
+                }
+            }
+            if (MARK) {
 #pragma unroll
-        for (int m = 1; m < 32; m <<= 1) {
-            w01 |= __shfl_xor(w01, m);
-            w23 |= __shfl_xor(w23, m);
+                for (int k = 0; k < kRowsPerLane; ++k)
+                    if ((reg >> k) & 1u) pres[c[k]] = 1;  // benign same-value race
+            }
         }
-        if ((lane & 31) == 0) {
-            const int64_t wa = (base >> 6) + (lane >> 5), wb = wa + 2;
-            if (wa * 64 < n) hw[wa] = w01;
-            if (wb * 64 < n) hw[wb] = w23;
+        if (HAMW) {
+            // 32 lanes x 2 rows = one 64-row word (LSB = first row): OR-reduce per half-wave.
+            // Lanes 0..31 hold words 0 (rows 0..63) and 2 (rows 128..191) of the tile,
+            // lanes 32..63 words 1 and 3.
+            uint64_t w01 = (uint64_t)(wnib & 3u) << (2 * (lane & 31));
+            uint64_t w23 = (uint64_t)((wnib >> 2) & 3u) << (2 * (lane & 31));
+#pragma unroll
+            for (int m = 1; m < 32; m <<= 1) {
+                w01 |= __shfl_xor(w01, m);
+                w23 |= __shfl_xor(w23, m);
+            }
+            if ((lane & 31) == 0) {
+                const int64_t wa = (base >> 6) + (lane >> 5), wb = wa + 2;
+                if (wa * 64 < n) hw[wa] = w01;
+                if (wb * 64 < n) hw[wb] = w23;
+            }
         }
     }
 }
@@ -498,7 +501,13 @@ int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int
                mark = presence != nullptr;
     if (!score && !hamd && !hamw && !mark) return ROGTK_OK;
     ProfScope prof(score || hamd || hamw ? K_SCORE_PACKED : K_MARK, s);
-    const int g = grid_for((n + kRowsPerLane - 1) / kRowsPerLane);
+    // ROGTK_SCORE_BLOCKS=k: at most k workgroups, grid-stride (A/B; default full grid)
+    static const int64_t cap = [] {
+        const char* e = getenv("ROGTK_SCORE_BLOCKS");
+        return e ? std::max<int64_t>(0, atoll(e)) : 0;
+    }();
+    int g = grid_for((n + kRowsPerLane - 1) / kRowsPerLane);
+    if (cap && g > cap) g = (int)cap;
     const int sel = (score ? 8 : 0) | (hamd ? 4 : 0) | (hamw ? 2 : 0) | (mark ? 1 : 0);
 #define ROGTK_SP(S, D, W, M)                                                                    \
     case (S * 8 + D * 4 + W * 2 + M):                                                          \
