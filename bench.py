@@ -73,6 +73,8 @@ def parse():
     ap.add_argument("--assign-on", choices=("resolve", "separate"), default="separate",
                     help="assign of batch k on its own stream one batch later (default) or behind its "
                          "resolve on the resolve stream (deferred assign)")
+    ap.add_argument("--split-resolve", action="store_true",
+                    help="local phase of the resolve on the main stream, global phase on the resolve stream")
     ap.add_argument("--resolve-streams", type=int, default=1,
                     help="resolve streams: consecutive batches resolve concurrently (needs depth > streams)")
     ap.add_argument("--prio", type=str, default="0,0,0", help="stream priorities main,resolve,assign (-1 = high)")
@@ -210,7 +212,8 @@ def main():
                        max_distance=md, group=None,
                        priorities=tuple(int(x) for x in args.prio.split(",")), mark=args.mark,
                        score_alone=not args.overlap_score, exchange=exchange,
-                       resolve_streams=args.resolve_streams, assign_on=args.assign_on)
+                       resolve_streams=args.resolve_streams, assign_on=args.assign_on,
+                       split_resolve=args.split_resolve)
 
     def step():
         pipe.submit(batch)

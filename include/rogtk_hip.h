@@ -151,6 +151,12 @@ int rogtk_cluster_local_bitmap(void* ws, int umi_len, int64_t max_distinct,
 int rogtk_cluster_resolve(void* ws, int umi_len, int64_t max_distinct,
                           const uint64_t* bitmaps, int n_bitmaps, int max_distance,
                           void* stream);
+/* rogtk_cluster_resolve in two halves, for callers that pipeline batches across
+ * streams: phase 1 = rank tables + LDS-local components (needs only the bitmaps), phase 2
+ * = global rounds + labels; phase 2 must follow phase 1 of the same workspace and bitmaps
+ * (stream order or an event). Enqueue-only. */
+int rogtk_cluster_resolve_phase(void* ws, int umi_len, int64_t max_distinct, const uint64_t* bitmaps,
+                                int n_bitmaps, int max_distance, int phase, void* stream);
 /* cluster_id[i] for regular rows; 0xFFFFFFFF for the others. Completes a pending
  * resolve of this workspace first (host waits on that resolve's event). */
 int rogtk_cluster_assign(const void* ws, int umi_len, int64_t max_distinct,

@@ -105,6 +105,7 @@ SIGNATURES = {
     "rogtk_cluster_mark": [_vp, _vp, _i64, _i32, _vp, _i64, _vp],
     "rogtk_cluster_local_bitmap": [_vp, _i32, _i64, _vp, _vp],
     "rogtk_cluster_resolve": [_vp, _i32, _i64, _vp, _i32, _i32, _vp],
+    "rogtk_cluster_resolve_phase": [_vp, _i32, _i64, _vp, _i32, _i32, _i32, _vp],
     "rogtk_cluster_assign": [_vp, _i32, _i64, _vp, _vp, _i64, _vp, _vp],
     "rogtk_cluster_assign_deferred": [_vp, _i32, _i64, _vp, _vp, _i64, _vp, _vp],
     "rogtk_cluster_sync": [_vp, _vp, ctypes.POINTER(ctypes.c_int)],

@@ -459,6 +459,18 @@ int rogtk_cluster_resolve(void* ws, int umi_len, int64_t max_distinct, const uin
     return launch_cluster_resolve(cl, (uint8_t*)ws, bitmaps, n_bitmaps, max_distance, as_stream(stream));
 }
 
+int rogtk_cluster_resolve_phase(void* ws, int umi_len, int64_t max_distinct, const uint64_t* bitmaps,
+                                int n_bitmaps, int max_distance, int phase, void* stream) {
+    ClusterLayout cl;
+    if (int rc = cluster_layout(umi_len, max_distinct, &cl)) return rc;
+    ROGTK_REQUIRE(ws && bitmaps, ROGTK_E_INVALID, "ws/bitmaps is NULL");
+    ROGTK_REQUIRE(n_bitmaps >= 1, ROGTK_E_INVALID, "n_bitmaps must be >= 1");
+    ROGTK_REQUIRE(max_distance == 0 || max_distance == 1, ROGTK_E_UNSUPPORTED,
+                  "max_distance %d: only 0 (exact) and 1 (Hamming<=1 components) are supported", max_distance);
+    ROGTK_REQUIRE(phase == 1 || phase == 2, ROGTK_E_INVALID, "phase must be 1 or 2, got %d", phase);
+    return launch_cluster_resolve(cl, (uint8_t*)ws, bitmaps, n_bitmaps, max_distance, as_stream(stream), phase);
+}
+
 int rogtk_cluster_assign(const void* ws, int umi_len, int64_t max_distinct, const uint32_t* codes,
                          const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id,
                          void* stream) {

@@ -1655,9 +1655,12 @@ int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone =
 namespace {
 // The kernels of one resolve, enqueued on s (direct, or into a graph under capture).
 // Returns the number of speculative rounds launched (0: no global rounds), -1 on error.
+// phases: bit 0 = the rank tables and the local CC (a function of the bitmaps only),
+// bit 1 = the global rounds, the flags publish and the labels.
 int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bitmaps, int n_bitmaps,
-                    int max_distance, int mode, int spec, unsigned long long* host_stats, hipStream_t s) {
-    {
+                    int max_distance, int mode, int spec, unsigned long long* host_stats, hipStream_t s,
+                    int phases = 3) {
+    if (phases & 1) {
         ProfScope prof(K_SCAN, s);
         hipLaunchKernelGGL(k_scan_words, dim3((unsigned)cl.blocks), dim3(kBlock), 0, s, bitmaps,
                            n_bitmaps, cl.words, (const unsigned long long*)nullptr, p.G, p.wpref,
@@ -1665,7 +1668,7 @@ int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bi
         hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, p.blksum, cl.blocks, p.blkoff,
                            p.stats, (int)S_NDISTINCT, max_distance == 0 ? (int)S_NCLUSTERS : -1, 1);
     }
-    {
+    if (phases & 1) {
         ProfScope prof(K_COMPACT, s);
         hipLaunchKernelGGL(k_rt, dim3(grid_for(cl.words)), dim3(kBlock), 0, s, p.G, cl.words, p.wpref,
                            p.blkoff, p.RT, p.lroot, max_distance == 0 ? 0 : cl.rwords);
@@ -1676,12 +1679,17 @@ int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bi
             return hipGetLastError() == hipSuccess ? 0 : -1;  // labels = ranks (labelcode / ilab)
         }
     }
+    if (max_distance == 0) return 0;  // phase 2 of an exact resolve: nothing
     int launched = 0;
-    {
+    if (phases & 1) {
         ProfScope prof(K_UNION, s);
         const int64_t lblocks = (cl.words + kLocalWords - 1) / kLocalWords;
         hipLaunchKernelGGL(k_local_cc, dim3((unsigned)lblocks), dim3(kBlock), 0, s, p.RT, cl.words, cl.L,
                            p.f, p.D, p.UR, p.lroot, cl.rwords, cl.max_distinct, p.stats);
+        if (!(phases & 2)) return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+    {
+        ProfScope prof(K_UNION, s);
         if (cl.L > kLocalPos && mode == kGlobalUnionFind) {
             // one-pass union-find: exact when the stream reaches the labels
             const int64_t tasks = (int64_t)(cl.L - kLocalPos) * (cl.words >> 2);
@@ -1717,12 +1725,20 @@ bool graphs_enabled() {
 }  // namespace
 
 int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t* bitmaps,
-                           int n_bitmaps, int max_distance, hipStream_t s) {
+                           int n_bitmaps, int max_distance, hipStream_t s, int phases) {
     WsPtrs p = ws_ptrs(cl, ws);
     std::lock_guard<std::mutex> lk(g_rs_mu);
     ResolveState& st = g_rs[ws];
     if (st.pending && st.deferred.on) {  // a deferred assign must see its resolve complete first
         if (int rc = finish_locked(ws, st, s)) return rc;
+    }
+    if (phases == 1) {  // the local phase alone; the global phase follows on another stream
+        const int r = enqueue_resolve(cl, p, bitmaps, n_bitmaps, max_distance, g_global_mode.load(),
+                                      g_spec_rounds.load(), nullptr, s, 1);
+        ROGTK_REQUIRE(r >= 0, ROGTK_E_HIP, "cluster: resolve launch failed (%s)", hipGetErrorString(hipGetLastError()));
+        st.pending = false;
+        st.deferred.on = false;
+        return ROGTK_OK;
     }
     st.pending = false;
     st.deferred.on = false;
@@ -1743,7 +1759,7 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
     // once into a hipGraph per such key and replayed with one launch (never while
     // profiling: the per-phase events need the direct launches).
     const GraphKey key{bitmaps, n_bitmaps, max_distance, mode, spec, cl.L, cl.max_distinct, cl.ecap};
-    const bool graph = graphs_enabled() && !profiling_on();
+    const bool graph = graphs_enabled() && !profiling_on() && phases == 3;
     int launched = 0;
     if (graph) {
         if (!st.gexec || !(st.gkey == key)) {
@@ -1769,7 +1785,7 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
         ROGTK_HIP_CHECK(hipGraphLaunch(st.gexec, s));
         launched = st.glaunched;
     } else {
-        launched = enqueue_resolve(cl, p, bitmaps, n_bitmaps, max_distance, mode, spec, hs, s);
+        launched = enqueue_resolve(cl, p, bitmaps, n_bitmaps, max_distance, mode, spec, hs, s, phases);
         ROGTK_REQUIRE(launched >= 0, ROGTK_E_HIP, "cluster: resolve launch failed (%s)",
                       hipGetErrorString(hipGetLastError()));
     }

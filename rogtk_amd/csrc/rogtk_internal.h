@@ -216,8 +216,10 @@ int launch_cluster_local_bitmap(const ClusterLayout& cl, uint8_t* ws, uint64_t* 
 int cluster_mark_bitmap_temp(int64_t n, int L, int64_t* bytes);
 int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int L,
                                uint64_t* bitmap, void* temp, int64_t temp_bytes, hipStream_t s);
+// phases: 1 = rank tables + local CC, 2 = global rounds + labels (after phase 1 of the
+// same bitmaps), 3 = both
 int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t* bitmaps,
-                           int n_bitmaps, int max_distance, hipStream_t s);
+                           int n_bitmaps, int max_distance, hipStream_t s, int phases = 3);
 // Waits for an asynchronous resolve's round flags and completes it if needed.
 // *redone (nullable): 1 when more rounds (+ labels, + a deferred assign) were enqueued.
 int cluster_finish(const void* ws, hipStream_t s, int* redone = nullptr);

@@ -156,11 +156,18 @@ class ClusterEngine:
                   _p(self.local_bitmap), _s(stream))
         return self.local_bitmap
 
-    def resolve(self, bitmaps: torch.Tensor, n_bitmaps: int, max_distance: int, stream=None) -> None:
+    def resolve(self, bitmaps: torch.Tensor, n_bitmaps: int, max_distance: int, stream=None,
+                phase: int = 0) -> None:
+        """phase 0: the whole resolve; 1: rank tables + local components; 2: the global
+        rounds + labels (after phase 1 of the same bitmaps)."""
         if bitmaps.numel() != n_bitmaps * self.words:
             raise ValueError("bitmaps must hold n_bitmaps * words int64 words")
-        _lib.call("rogtk_cluster_resolve", _p(self.ws), self.umi_len, self.max_distinct, _p(bitmaps),
-                  int(n_bitmaps), int(max_distance), _s(stream))
+        if phase:
+            _lib.call("rogtk_cluster_resolve_phase", _p(self.ws), self.umi_len, self.max_distinct, _p(bitmaps),
+                      int(n_bitmaps), int(max_distance), int(phase), _s(stream))
+        else:
+            _lib.call("rogtk_cluster_resolve", _p(self.ws), self.umi_len, self.max_distinct, _p(bitmaps),
+                      int(n_bitmaps), int(max_distance), _s(stream))
 
     def assign(self, batch: PackedBatch, cluster_id: torch.Tensor, stream=None, deferred: bool = False) -> None:
         """cluster ids of the batch's rows. deferred=True: no host wait for the resolve's

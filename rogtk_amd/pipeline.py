@@ -52,7 +52,7 @@ class UmiPipeline:
                  target: Optional[bytes] = b"ACGTACGTACGT", max_hamming: int = 1, max_distance: int = 1,
                  group=None, with_scores: bool = True, priorities=(0, 0, 0), mark: str = "auto",
                  on_assigned=None, score_alone: bool = False, exchange=None, resolve_streams: int = 1,
-                 assign_on: str = "separate"):
+                 assign_on: str = "separate", split_resolve: bool = False):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
@@ -100,6 +100,10 @@ class UmiPipeline:
         if assign_on not in ("resolve", "separate"):
             raise ValueError("assign_on must be 'resolve' or 'separate'")
         self.assign_on = assign_on
+        # split_resolve: the local phase of batch k's resolve (rank tables + LDS-local
+        # components, a function of its bitmaps only) runs on the main stream behind its
+        # mark, so it overlaps the global rounds of batch k-1 on the resolve stream
+        self.split_resolve = split_resolve
         if assign_on == "resolve" and resolve_streams != 1:
             raise ValueError("assign_on='resolve' uses one resolve stream")
 
@@ -109,6 +113,8 @@ class UmiPipeline:
         self.main.wait_stream(torch.cuda.current_stream(self.main.device))  # batch producer -> main
         if self.assign_on == "resolve":
             return self._submit_assign_on_resolve(slot, batch)
+        if self.on_assigned is None:
+            self._settle(slot, self.s_assign)
         if slot.assigned is not None:
             self.main.wait_event(slot.assigned)
         D.score_packed(batch, slot.scores, self.target, self.max_hamming, None, slot.within,
@@ -122,13 +128,20 @@ class UmiPipeline:
             if not self.fused_mark:
                 slot.eng.mark(batch, stream=self.main)
             slot.eng.build_local_bitmap(stream=self.main)
+        sr = self.s_resolves[self.k % len(self.s_resolves)]
+        if self.split_resolve:
+            with torch.cuda.stream(self.main):
+                bitmaps, nb = self.exchange(slot.eng.local_bitmap)
+                slot.eng.resolve(bitmaps, nb, self.max_distance, stream=self.main, phase=1)
         marked = torch.cuda.Event()
         marked.record(self.main)
-        sr = self.s_resolves[self.k % len(self.s_resolves)]
         with torch.cuda.stream(sr):
             sr.wait_event(marked)
-            bitmaps, nb = self.exchange(slot.eng.local_bitmap)
-            slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr)
+            if self.split_resolve:
+                slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr, phase=2)
+            else:
+                bitmaps, nb = self.exchange(slot.eng.local_bitmap)
+                slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr)
             resolved = torch.cuda.Event()
             resolved.record(sr)
         self.queue.append((slot, batch, resolved))
@@ -137,14 +150,15 @@ class UmiPipeline:
         self.k += 1
         return slot
 
-    def _settle(self, slot: _Slot):
+    def _settle(self, slot: _Slot, stream=None):
         """The slot's previous batch is final: its resolve converged (or is completed now,
-        with its assign re-run, on the resolve stream)."""
+        with its assign re-run, on `stream`, the stream its assign ran on)."""
+        stream = self.s_resolve if stream is None else stream
         if slot.assigned is None:
             return
-        if slot.eng.sync(stream=self.s_resolve):
+        if slot.eng.sync(stream=stream):
             slot.assigned = torch.cuda.Event()
-            slot.assigned.record(self.s_resolve)
+            slot.assigned.record(stream)
             self.last_assigned = slot.assigned
 
     def _submit_assign_on_resolve(self, slot: _Slot, batch: D.PackedBatch):
@@ -180,7 +194,10 @@ class UmiPipeline:
         self.s_assign.wait_event(resolved)
         if self.score_alone and self.last_scored is not None:
             self.s_assign.wait_event(self.last_scored)
-        slot.eng.assign(batch, slot.cid, stream=self.s_assign)
+        # without a consumer hook the assign is deferred (no host wait for the resolve's
+        # flags: the host would otherwise stall behind the resolve stream's queue and
+        # enqueue the next batch late); the slot is settled before its reuse / at drain
+        slot.eng.assign(batch, slot.cid, stream=self.s_assign, deferred=self.on_assigned is None)
         if self.on_assigned is not None:
             with torch.cuda.stream(self.s_assign):
                 self.on_assigned(slot, batch)
@@ -195,6 +212,9 @@ class UmiPipeline:
                 self._settle(slot)
         while self.queue:
             self._assign_oldest()
+        if self.assign_on == "separate" and self.on_assigned is None:
+            for slot in self.slots:
+                self._settle(slot, self.s_assign)
         if self.last_assigned is not None:
             self.main.wait_event(self.last_assigned)
         torch.cuda.current_stream(self.main.device).wait_stream(self.main)
