@@ -77,6 +77,8 @@ def parse():
                     help="local phase of the resolve on the main stream, global phase on the resolve stream")
     ap.add_argument("--resolve-streams", type=int, default=1,
                     help="resolve streams: consecutive batches resolve concurrently (needs depth > streams)")
+    ap.add_argument("--reuse-gate", choices=("auto", "score", "resolve"), default="auto",
+                    help="slot reuse: the main stream (score) or only the resolve waits for the slot's last assign")
     ap.add_argument("--prio", type=str, default="0,0,0", help="stream priorities main,resolve,assign (-1 = high)")
     return ap.parse_args()
 
@@ -213,7 +215,7 @@ def main():
                        priorities=tuple(int(x) for x in args.prio.split(",")), mark=args.mark,
                        score_alone=not args.overlap_score, exchange=exchange,
                        resolve_streams=args.resolve_streams, assign_on=args.assign_on,
-                       split_resolve=args.split_resolve)
+                       split_resolve=args.split_resolve, reuse_gate=args.reuse_gate)
 
     def step():
         pipe.submit(batch)

@@ -13,9 +13,12 @@ The hot path has three phases with different limits on MI355X:
 Batch k's resolve overlaps batch k+1's scoring and batch k-1's assign, so a
 steady-state step costs max(phase) instead of the sum. Each slot owns its
 workspace and outputs; events order every cross-stream hand-off:
-  main(k)   waits assign(k - depth) (slot reuse)   -> records marked(k)
-  resolve(k) waits marked(k)                        -> records resolved(k)
-  assign(k)  waits resolved(k)                      -> records assigned(k)
+  main(k)    waits assign(k - depth) (slot reuse)   -> records marked(k)
+  resolve(k) waits marked(k)                         -> records resolved(k)
+  assign(k)  waits resolved(k)                       -> records assigned(k)
+(reuse_gate="resolve", an A/B option: only resolve(k) waits assign(k - depth) and the
+mark waits resolve(k - depth); score, mark, resolve and assign then all overlap, and at
+10M reads the step slowed 0.375 -> 0.401 ms: score 119 -> 195 us, assign 125 -> 200 us.)
 Resolve is enqueue-only (rogtk_cluster_resolve); assign completes a resolve whose
 speculative rounds were not enough, so results never depend on timing.
 
@@ -45,6 +48,7 @@ class _Slot:
         self.within = torch.empty(max((n_max + 63) // 64, 1), dtype=torch.int64, device=dev)
         self.cid = torch.empty(max(n_max, 4), dtype=torch.int32, device=dev)
         self.assigned: Optional[torch.cuda.Event] = None
+        self.resolved: Optional[torch.cuda.Event] = None
 
 
 class UmiPipeline:
@@ -52,7 +56,7 @@ class UmiPipeline:
                  target: Optional[bytes] = b"ACGTACGTACGT", max_hamming: int = 1, max_distance: int = 1,
                  group=None, with_scores: bool = True, priorities=(0, 0, 0), mark: str = "auto",
                  on_assigned=None, score_alone: bool = False, exchange=None, resolve_streams: int = 1,
-                 assign_on: str = "separate", split_resolve: bool = False):
+                 assign_on: str = "separate", split_resolve: bool = False, reuse_gate: str = "auto"):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
@@ -106,6 +110,21 @@ class UmiPipeline:
         self.split_resolve = split_resolve
         if assign_on == "resolve" and resolve_streams != 1:
             raise ValueError("assign_on='resolve' uses one resolve stream")
+        # reuse_gate: what waits for the assign of the slot's previous batch.
+        #   "score":   the main stream (score + mark of batch k wait for assign(k - depth))
+        #   "resolve": only the resolve of batch k (its rank / label tables are the ones
+        #              assign(k - depth) reads); the mark waits for resolve(k - depth), the
+        #              reader of the presence bitmap it overwrites. Score and mark then run
+        #              ahead of the assign, off the critical cycle resolve -> assign -> resolve.
+        #   "auto":    "score" (measured faster: every kernel here is memory-system bound,
+        #              so overlapping all four phases slows each of them more than it hides)
+        if reuse_gate not in ("auto", "score", "resolve"):
+            raise ValueError("reuse_gate must be 'auto', 'score' or 'resolve'")
+        if reuse_gate == "auto":
+            reuse_gate = "score"
+        if reuse_gate == "resolve" and (on_assigned is not None or split_resolve):
+            raise ValueError("reuse_gate='resolve' needs on_assigned=None and split_resolve=False")
+        self.reuse_gate = reuse_gate
 
     def submit(self, batch: D.PackedBatch):
         """Enqueue one batch; returns its slot (outputs valid after drain() or a later event)."""
@@ -115,13 +134,16 @@ class UmiPipeline:
             return self._submit_assign_on_resolve(slot, batch)
         if self.on_assigned is None:
             self._settle(slot, self.s_assign)
-        if slot.assigned is not None:
+        gate_resolve = self.reuse_gate == "resolve"
+        if slot.assigned is not None and not gate_resolve:
             self.main.wait_event(slot.assigned)
         D.score_packed(batch, slot.scores, self.target, self.max_hamming, None, slot.within,
                        cluster=slot.eng if self.fused_mark else None, stream=self.main)
         if self.score_alone:
             self.last_scored = torch.cuda.Event()
             self.last_scored.record(self.main)
+        if gate_resolve and slot.resolved is not None:
+            self.main.wait_event(slot.resolved)  # the previous resolve read the bitmap
         if self.sort_mark:
             slot.eng.mark_bitmap(batch, stream=self.main)
         else:
@@ -137,6 +159,8 @@ class UmiPipeline:
         marked.record(self.main)
         with torch.cuda.stream(sr):
             sr.wait_event(marked)
+            if gate_resolve and slot.assigned is not None:
+                sr.wait_event(slot.assigned)  # assign(k - depth) reads the tables rewritten here
             if self.split_resolve:
                 slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr, phase=2)
             else:
@@ -144,6 +168,7 @@ class UmiPipeline:
                 slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr)
             resolved = torch.cuda.Event()
             resolved.record(sr)
+        slot.resolved = resolved
         self.queue.append((slot, batch, resolved))
         while len(self.queue) > self.lag:
             self._assign_oldest()

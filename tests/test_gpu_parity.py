@@ -424,11 +424,13 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assig
 
 @pytest.mark.parametrize("spec", [1, 4])
 @pytest.mark.parametrize("depth,nb", [(2, 5), (3, 3), (1, 2)])
-def test_pipeline_deferred_assign(rg, depth, nb, spec):
-    """assign_on="resolve" without an on_assigned hook: assigns are enqueued before their
-    resolve's flags are checked; with 1 speculative round every batch needs the deferred
-    completion (rounds + labels + the assign again) when its slot comes round or at drain.
-    The slots' final outputs equal the sequential device path."""
+@pytest.mark.parametrize("assign_on,gate", [("separate", "auto"), ("separate", "resolve"), ("resolve", "auto")])
+def test_pipeline_deferred_assign(rg, depth, nb, spec, assign_on, gate):
+    """No on_assigned hook: assigns are enqueued before their resolve's flags are checked;
+    with 1 speculative round every batch needs the deferred completion (rounds + labels +
+    the assign again) when its slot comes round or at drain. With reuse_gate "resolve",
+    score and mark of a slot's next batch do not wait for its assign.
+    The slots' final outputs (ids, scores, Hamming bits) equal the sequential device path."""
     import torch
 
     from rogtk_amd import device as D
@@ -439,7 +441,8 @@ def test_pipeline_deferred_assign(rg, depth, nb, spec):
     seeds = [synth.DEFAULT_SEED + 29 * k for k in range(nb)]
     try:
         D.set_spec_rounds(spec)
-        pipe = UmiPipeline(L, n, n, "cuda", depth=depth, target=b"ACGTACGTACGT", max_distance=1)
+        pipe = UmiPipeline(L, n, n, "cuda", depth=depth, target=b"ACGTACGTACGT", max_distance=1,
+                           assign_on=assign_on, reuse_gate=gate, score_alone=depth == 2)
         keep, last = [], {}
         for k, s in enumerate(seeds):
             codes = torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda()
@@ -455,6 +458,8 @@ def test_pipeline_deferred_assign(rg, depth, nb, spec):
         k = last[id(slot)]
         _, scores, _, hw, cid, _ = _device_run(n, seed=seeds[k])
         assert np.array_equal(slot.cid[:n].cpu().numpy(), cid.cpu().numpy()), k
+        assert np.array_equal(slot.scores["combined_score"][:n].cpu().numpy().view(np.uint64),
+                              scores["combined_score"][:n].cpu().numpy().view(np.uint64)), k
         assert np.array_equal(slot.within.cpu().numpy()[:len(hw)], hw.cpu().numpy()), k
 
 
