@@ -77,6 +77,8 @@ def parse():
                     help="local phase of the resolve on the main stream, global phase on the resolve stream")
     ap.add_argument("--resolve-streams", type=int, default=1,
                     help="resolve streams: consecutive batches resolve concurrently (needs depth > streams)")
+    ap.add_argument("--spec-rounds", type=int, default=0,
+                    help="H3 speculative global rounds per resolve (0 = the library default)")
     ap.add_argument("--reuse-gate", choices=("auto", "score", "resolve"), default="auto",
                     help="slot reuse: the main stream (score) or only the resolve waits for the slot's last assign")
     ap.add_argument("--prio", type=str, default="0,0,0", help="stream priorities main,resolve,assign (-1 = high)")
@@ -210,6 +212,7 @@ def main():
     D.set_mark_method({"sort": D.MARK_SORT, "slices": D.MARK_SLICES}.get(args.mark, D.MARK_AUTO))
     D.set_global_mode({"uf": D.GLOBAL_UNION_FIND, "rounds": D.GLOBAL_ROUNDS,
                        "rounds1f": D.GLOBAL_ROUNDS_ONE_FLATTEN, "edges": D.GLOBAL_EDGES}[args.global_mode])
+    D.set_spec_rounds(args.spec_rounds)
     pipe = UmiPipeline(L, min(n_total, 4 ** L), count, dev, depth=args.depth, target=TARGET,
                        max_distance=md, group=None,
                        priorities=tuple(int(x) for x in args.prio.split(",")), mark=args.mark,

@@ -585,10 +585,6 @@ __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ R
 // Per-workgroup hook table in LDS: (root -> smallest proposed parent). Cliques that
 // cross stars insert here; the block flushes one global atomicMin per distinct root.
 constexpr int kHookSlots = 1024;
-// ROGTK_EDGE_ATOMIC_HOOK=1: hooks by memory-side atomicMin instead of plain stores (A/B)
-#ifndef ROGTK_EDGE_ATOMIC_HOOK
-#define ROGTK_EDGE_ATOMIC_HOOK 0
-#endif
 
 struct HookTable {
     uint32_t key[kHookSlots];
@@ -909,18 +905,20 @@ struct EdgeSink {
     unsigned int* cnt;         // its device count (may run past cap: then ovf is set)
     unsigned int cap;
     unsigned long long* ovf;   // stats[S_EDGE_OVF]
+    int plain_hooks;           // 1: hook by plain store (ROGTK_EDGE_PLAIN_HOOK=1, A/B)
 };
 
-// Hook root hi under lo with a PLAIN store (no memory-side atomic): when several pairs
-// of one round hook the same root, any one of them may win (each written lo is a root
-// of this round and smaller than hi, so the forest stays acyclic and no tree splits),
-// and every losing pair is in the list of crossing edges the next round re-checks.
-__device__ __forceinline__ void hook_store(uint32_t* f, uint32_t lo, uint32_t hi) {
-#if ROGTK_EDGE_ATOMIC_HOOK
-    if (lo < f[hi]) atomicMin(f + hi, lo);
-#else
-    if (lo < f[hi]) f[hi] = lo;
-#endif
+// Hook root hi under lo. Default: memory-side atomicMin, so that the smallest proposal
+// wins (synth-v1 converges in the same 3 productive rounds as k_hook_g). With plain
+// stores any proposal may win (each written lo is a root of this round and smaller than
+// hi, so the forest stays acyclic and no tree splits; every losing pair is in the list of
+// crossing edges the next round re-checks): measured 1-2 more rounds, past the
+// speculative ones.
+__device__ __forceinline__ void hook_store(const EdgeSink& o, uint32_t* f, uint32_t lo, uint32_t hi) {
+    if (lo < f[hi]) {
+        if (o.plain_hooks) f[hi] = lo;
+        else atomicMin(f + hi, lo);
+    }
 }
 
 __device__ __forceinline__ void edge_append(const EdgeSink& o, uint32_t lo, uint32_t hi) {
@@ -943,7 +941,7 @@ __device__ __forceinline__ void pair_put(unsigned long long* T, const EdgeSink& 
             if (cur == kNoPair || cur == k) return;
         }
     }
-    hook_store(f, lo, hi);
+    hook_store(o, f, lo, hi);
     edge_append(o, lo, hi);
 }
 
@@ -975,7 +973,7 @@ __device__ __forceinline__ void pairs_flush(unsigned long long* T, const EdgeSin
     for (int k = 0; k < kPer; ++k) {
         if (mine[k] == kNoPair) continue;
         const uint32_t lo = (uint32_t)(mine[k] >> 32), hi = (uint32_t)mine[k];
-        hook_store(f, lo, hi);
+        hook_store(o, f, lo, hi);
         const uint64_t at = (uint64_t)base + ex++;
         if (at < o.cap) o.E[at] = make_uint2(lo, hi);
     }
@@ -1535,6 +1533,11 @@ EdgeSink edge_sink(const ClusterLayout& cl, const WsPtrs& p, int round) {
     o.cnt = p.ecnt + round + 1;
     o.cap = (unsigned int)cl.ecap;
     o.ovf = p.stats + S_EDGE_OVF;
+    static const int plain = [] {
+        const char* e = getenv("ROGTK_EDGE_PLAIN_HOOK");
+        return e && e[0] == '1' ? 1 : 0;
+    }();
+    o.plain_hooks = plain;
     return o;
 }
 
