@@ -361,39 +361,54 @@ __device__ __forceinline__ bool is_sparse(const unsigned long long* stats, int64
     return stats[S_NDISTINCT] * 8 < (unsigned long long)words * 64;
 }
 
+// The union-find runs over LOCAL RANKS (index - gbase) of the present codes, not over
+// local codes: a tile of nloc present codes needs nloc LDS slots. Two instances share
+// the tiles: in a sparse code space (under 1/8 of the codes present, e.g. one 10M-read
+// batch at L = 12) CAP = kLocalCapSmall (16 KB of LDS: 5 workgroups per CU instead of 2)
+// takes the tiles of at most 4096 codes and CAP = kLocalCodes (64 KB) the rest; in a
+// dense one (e.g. the merged bitmap of 8 ranks) the 64 KB instance takes every tile.
+// Measured (tools/local_cc_exp, uniform bitmaps): 6.5% dense 68 -> 51 us; splitting the
+// tiles of a 25%-dense space between both instances was slower (146 -> 219 us).
+constexpr int kLocalCapSmall = 4096;
+
+template <int CAP>
 __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ RT, int64_t words, int L,
                                                      uint32_t* __restrict__ f, uint32_t* __restrict__ D,
                                                      uint32_t* __restrict__ UR, uint64_t* __restrict__ lroot,
                                                      int64_t rwords,
                                                      int64_t max_distinct,
                                                      unsigned long long* __restrict__ stats) {
+    constexpr bool kSmall = CAP < kLocalCodes;
+    const bool sparse = is_sparse(stats, words);
+    if (kSmall && !sparse) return;  // dense space: all tiles in the 64 KB instance
     __shared__ uint64_t wb[kLocalWords];
     __shared__ uint64_t wcm[kWordComps][kLocalWords];  // listed component masks per word
     __shared__ uint32_t lpre[kLocalWords];
-    __shared__ uint32_t lf[kLocalCodes];  // by local code (word * 64 + bit); valid at component roots
+    __shared__ uint32_t lf[CAP];  // by local rank; valid at the first code of each in-word component
     __shared__ int8_t wcn[kLocalWords];    // listed components (-1 overflow)
     __shared__ uint8_t wone[kLocalWords];  // the word's codes form one in-word component
     __shared__ uint64_t lrb[kLocalWords + 2];  // local-root bits of the block's index range
     __shared__ uint32_t s_wave[kBlock / 64];
     const int t = threadIdx.x;
+    const int64_t base = (int64_t)blockIdx.x * kLocalWords;
+    const int nw = (int)min<int64_t>(kLocalWords, words - base);
+    const uint4 e = t < nw ? RT[base + t] : make_uint4(0, 0, 0, 0);
+    const uint64_t m = rt_word(e);
+    uint32_t nloc;
+    const uint32_t ex = block_excl_scan((uint32_t)__popcll(m), s_wave, nloc);
+    if (kSmall ? nloc > (uint32_t)CAP : (sparse && nloc <= (uint32_t)kLocalCapSmall)) return;  // the other's
     lrb[t] = 0;
     if (t < 2) lrb[kLocalWords + t] = 0;
 #ifdef ROGTK_LCC_TIMING
     unsigned long long t_last_ = wall_clock64();
 #endif
-    const int64_t base = (int64_t)blockIdx.x * kLocalWords;
-    const int nw = (int)min<int64_t>(kLocalWords, words - base);
     const int lpos = L < kLocalPos ? L : kLocalPos;
-    const uint4 e = t < nw ? RT[base + t] : make_uint4(0, 0, 0, 0);
-    const uint64_t m = rt_word(e);
     wb[t] = m;
-    uint32_t nloc;
-    const uint32_t ex = block_excl_scan((uint32_t)__popcll(m), s_wave, nloc);
     lpre[t] = ex;
     const uint32_t gbase = RT[base].z;
     const int indims = lpos < 3 ? lpos : 3;  // positions inside one 64-code word
     // 1. components inside each word (positions 0..2): bit-parallel BFS on the word's
-    //    mask, once; each component is represented by its first code (lf[root] = root)
+    //    mask, once; each component is represented by its first code (lf[rank] = rank)
     WordComps mine;
     mine.m = m;
     {
@@ -405,7 +420,8 @@ __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ R
             const int b0 = __ffsll((long long)rem) - 1;
             const uint64_t c = word_component(m, 1ull << b0, indims);
             rem &= ~c;
-            lf[t * 64 + b0] = (uint32_t)(t * 64 + b0);
+            const uint32_t r0 = ex + (uint32_t)__popcll(m & ((1ull << b0) - 1ull));
+            lf[r0] = r0;
             ++ncomp;
             if (c & (c - 1)) {  // two or more codes
                 if (nl < kWordComps) {
@@ -427,13 +443,15 @@ __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ R
     LCC_T(0);
     // 2. positions 3..lpos-1 join words 4^(p-3) apart: codes at the same bit of the 4
     //    words of a group differ only at p, so two word components that share a bit
-    //    are adjacent; unite every intersecting pair of components
+    //    are adjacent; unite every intersecting pair of components (by the local rank
+    //    of each component's first code)
     {
         const int per = nw >> 2;
         if (per > 0 && t < (lpos - 3) * per) {
             const int p = 3 + t / per, g = t % per, s2 = 2 * p - 6, stride = 1 << s2;
             const int w0 = ((g >> s2) << (s2 + 2)) | (g & (stride - 1));
             WordComps wv[4];
+            uint32_t lp[4];
             bool all_one = true;
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
@@ -441,6 +459,7 @@ __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ R
                 wv[v].m = wb[w];
                 wv[v].one = wone[w];
                 wv[v].n = wcn[w];
+                lp[v] = lpre[w];
 #pragma unroll
                 for (int k = 0; k < kWordComps; ++k) wv[v].c[k] = wcm[k][w];
                 all_one &= wv[v].one || wv[v].m == 0;
@@ -450,9 +469,7 @@ __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ R
                 for (int x = 0; x < 3; ++x)
 #pragma unroll
                     for (int y = x + 1; y < 4; ++y)
-                        if (wv[x].m & wv[y].m)
-                            lunite(lf, (uint32_t)((w0 + x * stride) * 64 + __ffsll((long long)wv[x].m) - 1),
-                                   (uint32_t)((w0 + y * stride) * 64 + __ffsll((long long)wv[y].m) - 1));
+                        if (wv[x].m & wv[y].m) lunite(lf, lp[x], lp[y]);  // first code = rank lp
             } else {
 #pragma unroll
                 for (int x = 0; x < 3; ++x) {
@@ -465,14 +482,15 @@ __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ R
                         const int ba = __ffsll((long long)rem) - 1;
                         const uint64_t ca = comp_of(wv[x], 1ull << ba, indims);
                         rem &= ~ca;
-                        const uint32_t ra = (uint32_t)((w0 + x * stride) * 64 + ba);
+                        const uint32_t ra = lp[x] + (uint32_t)__popcll(wv[x].m & ((1ull << ba) - 1ull));
 #pragma unroll
                         for (int y = x + 1; y < 4; ++y) {
                             uint64_t z = ca & wv[y].m;
                             while (z) {
                                 const uint64_t cb = comp_of(wv[y], z & (~z + 1ull), indims);
                                 z &= ~cb;
-                                lunite(lf, ra, (uint32_t)((w0 + y * stride) * 64 + __ffsll((long long)cb) - 1));
+                                const int bb = __ffsll((long long)cb) - 1;
+                                lunite(lf, ra, lp[y] + (uint32_t)__popcll(wv[y].m & ((1ull << bb) - 1ull)));
                             }
                         }
                     }
@@ -489,21 +507,20 @@ __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ R
         while (rem) {
             const int b0 = __ffsll((long long)rem) - 1;
             rem &= ~comp_of(mine, 1ull << b0, indims);
-            const uint32_t c0 = (uint32_t)(t * 64 + b0);
-            uint32_t root = c0;
+            const uint32_t r0 = ex + (uint32_t)__popcll(m & ((1ull << b0) - 1ull));
+            uint32_t root = r0;
             for (uint32_t q = lds_ld(lf + root); q != root; q = lds_ld(lf + root)) root = q;
-            if (root != c0) __hip_atomic_store(lf + c0, root, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (root != r0) __hip_atomic_store(lf + r0, root, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
     __syncthreads();
     LCC_T(2);
-    // 3b. outputs of word t, per in-word component (lf[c0] is now the final root):
+    // 3b. outputs of word t, per in-word component (lf[first] is now the final root):
     //     UR = the word's shared local root (global index) or kNone, the live bits,
     //     f[local root] = itself, f[i] = its local root for the codes of words without
     //     a shared root (the only ones the rounds read by code), and in a sparse code
     //     space (kSparse) D[i] = code for every code, so that labels run over indices
     if (t == 0 && (int64_t)gbase + nloc > max_distinct) stats[S_OVERFLOW] = 1;
-    const bool sparse = is_sparse(stats, words);
     if (t < nw) {
         uint32_t first = kNone;
         bool uniform = true;
@@ -511,14 +528,14 @@ __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ R
         while (rem) {
             const int b0 = __ffsll((long long)rem) - 1;
             rem &= ~comp_of(mine, 1ull << b0, indims);
-            const uint32_t root = lf[t * 64 + b0];
-            const uint32_t rw = root >> 6;
-            const uint32_t rr = gbase + lpre[rw] + (uint32_t)__popcll(wb[rw] & ((1ull << (root & 63)) - 1ull));
+            const uint32_t r0 = ex + (uint32_t)__popcll(m & ((1ull << b0) - 1ull));
+            const uint32_t root = lf[r0];
+            const uint32_t rr = gbase + root;
             if (first == kNone) first = rr;
             uniform &= rr == first;
-            if (root == (uint32_t)(t * 64 + b0)) {
+            if (root == r0) {
                 if ((int64_t)rr < max_distinct) f[rr] = rr;
-                const uint32_t k = (gbase & 63u) + (rr - gbase);  // bit of the block's staging
+                const uint32_t k = (gbase & 63u) + root;  // bit of the block's staging
                 atomicOr((unsigned long long*)&lrb[k >> 6], 1ull << (k & 63));
             }
         }
@@ -538,9 +555,7 @@ __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ R
                 const int b0 = __ffsll((long long)r2) - 1;
                 uint64_t cc = comp_of(mine, 1ull << b0, indims);
                 r2 &= ~cc;
-                const uint32_t root = lf[t * 64 + b0];
-                const uint32_t rw = root >> 6;
-                const uint32_t rr = gbase + lpre[rw] + (uint32_t)__popcll(wb[rw] & ((1ull << (root & 63)) - 1ull));
+                const uint32_t rr = gbase + lf[ex + (uint32_t)__popcll(m & ((1ull << b0) - 1ull))];
                 while (cc) {
                     const int b = __ffsll((long long)cc) - 1;
                     cc &= cc - 1;
@@ -579,6 +594,17 @@ __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ R
         }
     }
     LCC_T(3);
+}
+
+// Both instances of k_local_cc (each exits early for the tiles of the other).
+inline void launch_local_cc(const uint4* RT, int64_t words, int L, uint32_t* f, uint32_t* D, uint32_t* UR,
+                            uint64_t* lroot, int64_t rwords, int64_t max_distinct, unsigned long long* stats,
+                            hipStream_t s) {
+    const int64_t lblocks = (words + kLocalWords - 1) / kLocalWords;
+    hipLaunchKernelGGL(k_local_cc<kLocalCapSmall>, dim3((unsigned)lblocks), dim3(kBlock), 0, s, RT, words, L, f, D,
+                       UR, lroot, rwords, max_distinct, stats);
+    hipLaunchKernelGGL(k_local_cc<kLocalCodes>, dim3((unsigned)lblocks), dim3(kBlock), 0, s, RT, words, L, f, D, UR,
+                       lroot, rwords, max_distinct, stats);
 }
 
 // --------------------------------------------------------------- global CC
@@ -1686,9 +1712,7 @@ int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bi
     int launched = 0;
     if (phases & 1) {
         ProfScope prof(K_UNION, s);
-        const int64_t lblocks = (cl.words + kLocalWords - 1) / kLocalWords;
-        hipLaunchKernelGGL(k_local_cc, dim3((unsigned)lblocks), dim3(kBlock), 0, s, p.RT, cl.words, cl.L,
-                           p.f, p.D, p.UR, p.lroot, cl.rwords, cl.max_distinct, p.stats);
+        launch_local_cc(p.RT, cl.words, cl.L, p.f, p.D, p.UR, p.lroot, cl.rwords, cl.max_distinct, p.stats, s);
         if (!(phases & 2)) return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     {

@@ -44,8 +44,7 @@ int main() {
         for (int it = 0; it < 8; ++it) {
             CK(hipDeviceSynchronize());
             hipEventRecord(a);
-            hipLaunchKernelGGL(k_local_cc, dim3((unsigned)lblocks), dim3(kBlock), 0, 0, p.RT, cl.words, L, p.f, p.D, p.UR,
-                               p.lroot, cl.rwords, cl.max_distinct, p.stats);
+            launch_local_cc(p.RT, cl.words, L, p.f, p.D, p.UR, p.lroot, cl.rwords, cl.max_distinct, p.stats, 0);
             hipEventRecord(b);
             CK(hipEventSynchronize(b));
             float ms;
@@ -54,8 +53,7 @@ int main() {
         }
         unsigned long long clk[8] = {0};
         CK(hipMemcpyToSymbol(HIP_SYMBOL(g_lcc_clk), clk, sizeof(clk)));
-        hipLaunchKernelGGL(k_local_cc, dim3((unsigned)lblocks), dim3(kBlock), 0, 0, p.RT, cl.words, L, p.f, p.D, p.UR,
-                           p.lroot, cl.rwords, cl.max_distinct, p.stats);
+        launch_local_cc(p.RT, cl.words, L, p.f, p.D, p.UR, p.lroot, cl.rwords, cl.max_distinct, p.stats, 0);
         CK(hipMemcpyFromSymbol(clk, HIP_SYMBOL(g_lcc_clk), sizeof(clk)));
         printf("  per-block us: phase1 %.2f union %.2f compress %.2f out %.2f\n", clk[0] / 100.0 / lblocks,
                clk[1] / 100.0 / lblocks, clk[2] / 100.0 / lblocks, clk[3] / 100.0 / lblocks);
