@@ -165,14 +165,13 @@ __global__ __launch_bounds__(kBlock) void k_scan_words(const uint64_t* __restric
     if (threadIdx.x == 0) blksum[blockIdx.x] = total;
 }
 
-// Single-block exclusive scan of block sums -> blkoff[0..nblocks], total -> stats
+// One workgroup: exclusive scan of block sums -> blkoff[0..nblocks], total -> stats
 // (zero_stats: the stats block and round flags are cleared first).
-__global__ __launch_bounds__(kBlock) void k_scan_blocks(const uint32_t* __restrict__ blksum,
-                                                        int64_t nblocks, uint32_t* __restrict__ blkoff,
-                                                        unsigned long long* __restrict__ stats,
-                                                        int slot, int copy_slot, int zero_stats) {
-    __shared__ uint32_t s_wave[kBlock / 64];
+__device__ __forceinline__ void scan_block_sums(const uint32_t* blksum, int64_t nblocks, uint32_t* blkoff,
+                                                unsigned long long* stats, int slot, int copy_slot, int zero_stats,
+                                                uint32_t* s_wave) {
     if (zero_stats && threadIdx.x < kStatsBytes / 8) stats[threadIdx.x] = 0;  // stats + round flags
+    __syncthreads();
     uint32_t carry = 0;
     for (int64_t base = 0; base < nblocks; base += kBlock) {
         const int64_t b = base + threadIdx.x;
@@ -187,6 +186,18 @@ __global__ __launch_bounds__(kBlock) void k_scan_blocks(const uint32_t* __restri
         stats[slot] = carry;
         if (copy_slot >= 0) stats[copy_slot] = carry;
     }
+}
+
+// per_live > 0: only the blocks that hold live indices (ceil(stats[S_NDISTINCT] /
+// per_live)) are scanned; later offsets are never read
+__global__ __launch_bounds__(kBlock) void k_scan_blocks(const uint32_t* __restrict__ blksum,
+                                                        int64_t nblocks, uint32_t* __restrict__ blkoff,
+                                                        unsigned long long* __restrict__ stats,
+                                                        int slot, int copy_slot, int zero_stats,
+                                                        int64_t per_live = 0) {
+    __shared__ uint32_t s_wave[kBlock / 64];
+    if (per_live > 0) nblocks = min<int64_t>(nblocks, ((int64_t)stats[S_NDISTINCT] + per_live - 1) / per_live);
+    scan_block_sums(blksum, nblocks, blkoff, stats, slot, copy_slot, zero_stats, s_wave);
 }
 
 // RT[w] = {word, rank of its first code}; also zeroes the index-space live bits
@@ -1136,18 +1147,69 @@ __global__ __launch_bounds__(kBlock) void k_edge_jump(const uint2* __restrict__ 
 }
 
 // Global roots (live vertices i with f[i] == i: only local roots can be) -> rbits over
-// index space; their dense order is the label order.
-__global__ __launch_bounds__(kBlock) void k_roots(const uint32_t* __restrict__ f, const uint64_t* __restrict__ lroot,
-                                                  int64_t max_distinct, uint64_t* __restrict__ rbits,
-                                                  const unsigned long long* __restrict__ stats) {
+// index space; their dense order is the label order. One pass: each workgroup owns
+// kRootWords root words (16 per wave, 16 loads of f in flight per lane), stores their
+// in-block prefix (rpref) and its sum; the last workgroup to finish scans the sums into
+// rblksum (k_scan_blocks then makes rblkoff and the cluster count). Workgroup 0 first
+// publishes the stats block (the round flags, final once the rounds' kernels are done)
+// into mapped host memory and then the resolve's epoch (host != nullptr), so the host
+// needs no copy or event. (Measured: letting the last workgroup to arrive scan the sums
+// instead - a device-scope fence + atomic per workgroup - made this kernel 64-137 us.)
+constexpr int kRootWords = 64;
+__global__ __launch_bounds__(kBlock) void k_roots_scan(const uint32_t* __restrict__ f,
+                                                       const uint64_t* __restrict__ lroot, int64_t max_distinct,
+                                                       int64_t rwords, uint64_t* __restrict__ rbits,
+                                                       uint32_t* __restrict__ rpref, uint32_t* rblksum,
+                                                       const unsigned long long* stats, unsigned long long* host,
+                                                       unsigned long long* epoch) {
+    __shared__ uint32_t s_cnt[kRootWords];
+    if (host && blockIdx.x == 0) {
+        for (int k = threadIdx.x; k < kStatsBytes / 8; k += kBlock)
+            __hip_atomic_store(host + k, stats[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned long long e = *epoch + 1;  // one publish per resolve: no race
+            *epoch = e;
+            __hip_atomic_store(host + kStatsBytes / 8, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
     const int64_t nd = live_distinct(stats, max_distinct);
-    const int lane = threadIdx.x & 63;
-    const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
-    for (int64_t w = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; w * 64 < nd; w += nwaves) {
-        const int64_t i = w * 64 + lane;
-        const bool root = i < nd && ((lroot[w] >> lane) & 1ull) && f[i] == (uint32_t)i;
-        const uint64_t m = __ballot(root);
-        if (lane == 0) rbits[w] = m;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int kPerWave = kRootWords / (kBlock / 64);  // 16
+    const int64_t w0 = (int64_t)blockIdx.x * kRootWords + wave * kPerWave;
+    uint32_t fv[kPerWave];
+    uint64_t lr[kPerWave];
+#pragma unroll
+    for (int k = 0; k < kPerWave; ++k) {
+        const int64_t i = (w0 + k) * 64 + lane;
+        lr[k] = (w0 + k) * 64 < nd ? lroot[w0 + k] : 0ull;
+        fv[k] = i < nd ? f[i] : 0u;
+    }
+    uint64_t mine = 0;
+#pragma unroll
+    for (int k = 0; k < kPerWave; ++k) {
+        const int64_t i = (w0 + k) * 64 + lane;
+        const uint64_t m = __ballot(i < nd && ((lr[k] >> lane) & 1ull) && fv[k] == (uint32_t)i);
+        if (lane == k) mine = m;
+    }
+    if (lane < kPerWave) {
+        const int64_t w = w0 + lane;
+        if (w < rwords) rbits[w] = mine;
+        s_cnt[wave * kPerWave + lane] = (uint32_t)__popcll(mine);
+    }
+    __syncthreads();
+        // in-block prefix of the kRootWords counts (one wave), block sum
+    if (wave == 0) {
+        const uint32_t v = lane < kRootWords ? s_cnt[lane] : 0u;
+        uint32_t incl = v;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t t = __shfl_up(incl, off);
+            if (lane >= off) incl += t;
+        }
+        const int64_t w = (int64_t)blockIdx.x * kRootWords + lane;
+        if (lane < kRootWords && w < rwords) rpref[w] = incl - v;
+        if (lane == kRootWords - 1) rblksum[blockIdx.x] = incl;
     }
 }
 
@@ -1155,11 +1217,19 @@ __device__ __forceinline__ uint32_t root_label(uint32_t r, const uint64_t* __res
                                                const uint32_t* __restrict__ rpref,
                                                const uint32_t* __restrict__ rblkoff) {
     const uint32_t w = r >> 6;
-    return rblkoff[w / kScanWords] + rpref[w] + (uint32_t)__popcll(rbits[w] & ((1ull << (r & 63)) - 1ull));
+    return rblkoff[w / kRootWords] + rpref[w] + (uint32_t)__popcll(rbits[w] & ((1ull << (r & 63)) - 1ull));
 }
 
-// Label of every word with a shared local root (kNone for the others), so that the
-// per-code pass below needs no dependent loads for them.
+// Dense label of one code: labelcode[code] (L <= 13) or ilab[index] (index space).
+__device__ __forceinline__ void put_label(uint64_t c, uint32_t i, uint32_t lab, uint32_t* __restrict__ labelcode,
+                                          uint32_t* __restrict__ ilab) {
+    if (labelcode) labelcode[c] = lab;
+    else ilab[i] = lab;
+}
+
+// Label of every word with a shared local root, and per code of the codes no word
+// label covers (one pass: a word's exception codes are labelled by the lane that
+// labels the word).
 // A word without a shared LOCAL root still gets a word label when the global phase put
 // all of its codes in one component (their f are global roots then: they are live): in
 // the giant components of a 1-edit-saturated space most words end up uniform, and assign
@@ -1171,16 +1241,19 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
                                                        const uint32_t* __restrict__ rpref,
                                                        const uint32_t* __restrict__ rblkoff,
                                                        uint32_t* __restrict__ wlab, uint64_t* __restrict__ wexc,
+                                                       uint32_t* __restrict__ labelcode, uint32_t* __restrict__ ilab,
                                                        int use_exc) {
     for (int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x; w < words; w += (int64_t)gridDim.x * kBlock) {
         const uint32_t ur = UR[w];
         uint32_t root = kNone;
         uint64_t exc = 0;
+        uint4 e = make_uint4(0, 0, 0, 0);
+        uint64_t m = 0;
         if (ur != kNone) {
             root = f[ur];
         } else {
-            const uint4 e = RT[w];
-            const uint64_t m = rt_word(e);
+            e = RT[w];
+            m = rt_word(e);
             const int cnt = __popcll(m);
             if (cnt > 0 && (int64_t)e.z + cnt <= max_distinct) {
                 // the word's label is its most frequent root (Boyer-Moore vote; any choice
@@ -1213,18 +1286,18 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
         if (exc && lab != kNone) lab = lab < 0x80000000u ? (lab | 0x80000000u) : kNone;
         wlab[w] = lab;
         wexc[w] = exc;
+        // the codes the word label does not cover (its exceptions, or all of them when
+        // the word stays unlabelled) get their own label (f[i] is their root: they are
+        // live); a uniform word (ur != kNone) always has a label
+        uint64_t per_code = lab == kNone ? m : exc;
+        while (per_code) {
+            const int b = __ffsll((long long)per_code) - 1;
+            per_code &= per_code - 1;
+            const uint32_t i = e.z + (uint32_t)__popcll(m & ((1ull << b) - 1ull));
+            if ((int64_t)i >= max_distinct) continue;
+            put_label((uint64_t)w * 64 + b, i, root_label(f[i], rbits, rpref, rblkoff), labelcode, ilab);
+        }
     }
-}
-
-// Dense labels (max_distance 1) of the exception codes only (wexc: codes outside their
-// word's labelled component; every other code is labelled by its word). Exception codes
-// are live (their f is their root). labelcode[code] (L <= 13) or ilab[index] (index
-// space). Dense code spaces run one lane per code (a wave per word: stores contiguous
-// per word); sparse ones one lane per index (D holds the codes; no idle lanes).
-__device__ __forceinline__ void put_label(uint64_t c, uint32_t i, uint32_t lab, uint32_t* __restrict__ labelcode,
-                                          uint32_t* __restrict__ ilab) {
-    if (labelcode) labelcode[c] = lab;
-    else ilab[i] = lab;
 }
 
 // The label of code c from its word (kNone: label it per code): wlab[w] = the label of
@@ -1235,38 +1308,6 @@ __device__ __forceinline__ uint32_t word_label_of(const uint32_t* __restrict__ w
     const uint32_t wl = wlab[c >> 6];
     if (wl == kNone || !(wl >> 31)) return wl;
     return ((wexc[c >> 6] >> (c & 63)) & 1ull) ? kNone : (wl & 0x7FFFFFFFu);
-}
-
-__global__ __launch_bounds__(kBlock) void k_label(const uint32_t* __restrict__ f, const uint4* __restrict__ RT,
-                                                  const uint32_t* __restrict__ wlab,
-                                                  const uint64_t* __restrict__ wexc, uint64_t nbits,
-                                                  const uint64_t* __restrict__ rbits,
-                                                  const uint32_t* __restrict__ rpref,
-                                                  const uint32_t* __restrict__ rblkoff,
-                                                  uint32_t* __restrict__ labelcode, uint32_t* __restrict__ ilab,
-                                                  const uint32_t* __restrict__ D, int64_t max_distinct,
-                                                  const unsigned long long* __restrict__ stats) {
-    const uint64_t lanes = (uint64_t)gridDim.x * kBlock;
-    const uint64_t lane0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (is_sparse(stats, (int64_t)((nbits + 63) / 64))) {
-        const int64_t nd = live_distinct(stats, max_distinct);
-        for (int64_t i = (int64_t)lane0; i < nd; i += (int64_t)lanes) {
-            const uint32_t c = D[i];
-            if (word_label_of(wlab, wexc, c) != kNone) continue;  // labelled by its word
-            put_label(c, (uint32_t)i, root_label(f[i], rbits, rpref, rblkoff), labelcode, ilab);
-        }
-        return;
-    }
-    for (uint64_t c = lane0; c < nbits; c += lanes) {
-        const uint64_t w = c >> 6;
-        if (word_label_of(wlab, wexc, c) != kNone) continue;  // labelled by its word (absent codes: below)
-        const uint4 e = RT[w];
-        const uint64_t m = rt_word(e);
-        if (!((m >> (c & 63)) & 1ull)) continue;
-        const uint32_t i = e.z + (uint32_t)__popcll(m & ((1ull << (c & 63)) - 1ull));
-        if ((int64_t)i >= max_distinct) continue;
-        put_label(c, i, root_label(f[i], rbits, rpref, rblkoff), labelcode, ilab);
-    }
 }
 
 // MODE 0: labelcode[code]; MODE 1: flab[rank(code)] (labels by index, ilab).
@@ -1327,7 +1368,7 @@ struct WsPtrs {
     uint64_t *rbits, *lroot;
     uint32_t *rpref, *rblksum, *rblkoff, *labelcode, *ilab;
     uint64_t* active;
-    unsigned long long* epoch;  // resolves published (k_publish_stats)
+    unsigned long long* epoch;  // resolves published (k_roots_scan)
     uint2* edges;             // two lists of ecap pairs
     unsigned int* ecnt;       // per-round list counts (stats block)
 };
@@ -1387,7 +1428,7 @@ int cluster_layout(int L, int64_t max_distinct, ClusterLayout* o) {
     c.words = (int64_t)((c.nbits + 63) / 64);
     c.blocks = (c.words + kScanWords - 1) / kScanWords;
     c.rwords = (max_distinct + 63) / 64;
-    c.rblocks = (c.rwords + kScanWords - 1) / kScanWords;
+    c.rblocks = (c.rwords + kRootWords - 1) / kRootWords;
     // ROGTK_LABEL_BY_INDEX=1: labels by rank even for L <= 13 (A/B of the assign gather)
     static const bool by_index = [] {
         const char* e = getenv("ROGTK_LABEL_BY_INDEX");
@@ -1524,7 +1565,7 @@ struct GraphKey {
 };
 
 struct ResolveState {
-    // the stats block (round flags, edge overflow) published by k_publish_stats into
+    // the stats block (round flags, edge overflow) published by k_roots_scan into
     // mapped, coherent host memory, followed by a sequence word = the resolve's epoch
     uint8_t* hstats = nullptr;
     uint8_t* hstats_dev = nullptr;  // its device address
@@ -1565,19 +1606,6 @@ EdgeSink edge_sink(const ClusterLayout& cl, const WsPtrs& p, int round) {
     }();
     o.plain_hooks = plain;
     return o;
-}
-
-// k_publish_stats: the stats block into mapped host memory, then the sequence word
-__global__ __launch_bounds__(128) void k_publish_stats(const unsigned long long* __restrict__ stats,
-                                                       unsigned long long* host, unsigned long long* epoch) {
-    for (int k = threadIdx.x; k < kStatsBytes / 8; k += 128)
-        __hip_atomic_store(host + k, stats[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned long long e = *epoch + 1;  // one publish per resolve: no race
-        *epoch = e;
-        __hip_atomic_store(host + kStatsBytes / 8, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
 }
 
 // Host side: spin until this resolve's stats are published (normally long done).
@@ -1638,29 +1666,29 @@ int enqueue_post_rounds(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
     return ROGTK_OK;
 }
 
-int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s) {
+// host_stats != nullptr: k_roots_scan also publishes the stats block (the resolve's
+// first labels pass; never the re-run after extra rounds, which the host waits for)
+int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
+                   unsigned long long* host_stats = nullptr) {
     {
         ProfScope prof(K_FLATTEN, s);
-        hipLaunchKernelGGL(k_roots, dim3(grid_for(cl.max_distinct, kPersistentGrid)), dim3(kBlock), 0, s, p.f,
-                           p.lroot, cl.max_distinct, p.rbits, p.stats);
-        hipLaunchKernelGGL(k_scan_words, dim3((unsigned)cl.rblocks), dim3(kBlock), 0, s, p.rbits, 1,
-                           cl.rwords, p.stats + S_NDISTINCT, (uint64_t*)nullptr, p.rpref, p.rblksum);
-        hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, p.rblksum, cl.rblocks, p.rblkoff,
-                           p.stats, (int)S_NCLUSTERS, -1, 0);
+        hipLaunchKernelGGL(k_roots_scan, dim3((unsigned)cl.rblocks), dim3(kBlock), 0, s, p.f, p.lroot,
+                           cl.max_distinct, cl.rwords, p.rbits, p.rpref, p.rblksum,
+                           (const unsigned long long*)p.stats, host_stats, p.epoch);
+        hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, p.rblksum, cl.rblocks, p.rblkoff, p.stats,
+                           (int)S_NCLUSTERS, -1, 0, (int64_t)kRootWords * 64);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     {
         ProfScope prof(K_LABEL, s);
-        const int lg = grid_for((int64_t)std::min<uint64_t>(cl.nbits, 1ull << 30), 16384);
         // wpref and G (consumed into RT by k_rt) hold the word labels and exception masks
         static const int use_exc = [] {  // ROGTK_WORD_EXC=0: words with exceptions stay unlabelled (A/B)
             const char* e = getenv("ROGTK_WORD_EXC");
             return e && e[0] == '0' ? 0 : 1;
         }();
         hipLaunchKernelGGL(k_word_label, dim3(grid_for(cl.words, kPersistentGrid)), dim3(kBlock), 0, s, p.f, p.UR,
-                           cl.words, p.RT, cl.max_distinct, p.rbits, p.rpref, p.rblkoff, p.wpref, p.G, use_exc);
-        hipLaunchKernelGGL(k_label, dim3(lg), dim3(kBlock), 0, s, p.f, p.RT, p.wpref, p.G, cl.nbits, p.rbits,
-                           p.rpref, p.rblkoff, p.labelcode, p.ilab, p.D, cl.max_distinct, p.stats);
+                           cl.words, p.RT, cl.max_distinct, p.rbits, p.rpref, p.rblkoff, p.wpref, p.G, p.labelcode,
+                           p.ilab, use_exc);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     return ROGTK_OK;
@@ -1726,13 +1754,13 @@ int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bi
                                p.f, p.lroot, cl.max_distinct, p.stats);
         } else if (cl.L > kLocalPos) {
             if (enqueue_rounds(cl, p, 0, spec, s, mode)) return -1;
-            // a one-block kernel stores the flags into mapped host memory and then the
-            // resolve's epoch (counted on the device): no copy-engine transfer and no event
-            // (a D2H copy + event record cost ~15 us of the resolve chain)
-            hipLaunchKernelGGL(k_publish_stats, dim3(1), dim3(128), 0, s, (const unsigned long long*)p.stats,
-                               host_stats, p.epoch);
             if (enqueue_post_rounds(cl, p, s, mode)) return -1;
             launched = spec;
+            // k_roots_scan stores the flags into mapped host memory and then the resolve's
+            // epoch (counted on the device): no copy-engine transfer, no event, no kernel
+            // of its own (a D2H copy + event record cost ~15 us of the resolve chain)
+            if (enqueue_labels(cl, p, s, host_stats)) return -1;
+            return hipGetLastError() == hipSuccess ? launched : -1;
         }
     }
     if (enqueue_labels(cl, p, s)) return -1;

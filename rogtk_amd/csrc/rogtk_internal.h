@@ -173,7 +173,7 @@ struct ClusterLayout {
     int64_t words;       // bitmap words over code space
     int64_t blocks;      // scan blocks over code-space words (1024 words each)
     int64_t rwords;      // root-bitmap words over index space
-    int64_t rblocks;     // scan blocks over index-space words
+    int64_t rblocks;     // root-scan workgroups over index-space words (kRootWords each)
     bool label_by_code;  // dense label table indexed by code (L <= 13)
     // byte offsets into the workspace
     int64_t off_stats, off_presence, off_bitmap, off_rt, off_wpref, off_blksum, off_blkoff, off_D, off_f, off_ur,
