@@ -1314,39 +1314,58 @@ __device__ __forceinline__ uint32_t word_label_of(const uint32_t* __restrict__ w
 // wlab / wexc (max_distance 1 only, else NULL): per 64 codes the label of the word's most
 // frequent component (1 MB at L = 12, L2-resident) and, for flagged words only, the mask
 // of its other codes (2 MB): only exception codes gather from the 4^L-entry table.
-template <int MODE>
+// G groups of 4 rows per lane and loop trip (all loads of a trip in flight at once):
+// lane l of a wave owns rows {tile + 256 g + 4 l .. + 3}, so each 16-B load / store
+// instruction of a wave covers 1 KB contiguous.
+template <int MODE, int G>
 __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ codes,
                                                    const uint64_t* __restrict__ regbits, int64_t n,
                                                    const uint32_t* __restrict__ labelcode,
                                                    const uint32_t* __restrict__ flab,
                                                    const uint4* __restrict__ RT, const uint32_t* __restrict__ wlab,
                                                    const uint64_t* __restrict__ wexc, uint32_t* __restrict__ out) {
-    for (int64_t row0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4; row0 < n;
-         row0 += (int64_t)gridDim.x * kBlock * 4) {
-        const bool full = row0 + 4 <= n;
-        uint32_t c[4] = {0, 0, 0, 0};
-        if (full) {
-            const u32x4_t v = stream_load(reinterpret_cast<const u32x4_t*>(codes + row0));
-            c[0] = v.x; c[1] = v.y; c[2] = v.z; c[3] = v.w;
-        } else {
-            for (int k = 0; k < 4; ++k)
-                if (row0 + k < n) c[k] = codes[row0 + k];
-        }
-        uint32_t reg = regbits ? (uint32_t)(regbits[row0 >> 6] >> (row0 & 63)) & 0xFu : 0xFu;
-        uint32_t id[4];
+    constexpr int64_t kTile = 256 * G;  // rows per wave and trip
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
+    for (int64_t tile = (((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6) * kTile; tile < n;
+         tile += nwaves * kTile) {
+        uint32_t c[G][4];
+        uint32_t reg[G];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            id[k] = 0xFFFFFFFFu;
-            if ((reg >> k) & 1u) {
-                const uint32_t wl = wlab ? word_label_of(wlab, wexc, c[k]) : kNone;
-                id[k] = wl != kNone ? wl : MODE == 0 ? labelcode[c[k]] : flab[rt_rank(RT[c[k] >> 6], c[k])];
+        for (int g = 0; g < G; ++g) {
+            const int64_t row0 = tile + 256 * g + 4 * lane;
+            c[g][0] = c[g][1] = c[g][2] = c[g][3] = 0;
+            if (row0 + 4 <= n) {
+                const u32x4_t v = stream_load(reinterpret_cast<const u32x4_t*>(codes + row0));
+                c[g][0] = v.x; c[g][1] = v.y; c[g][2] = v.z; c[g][3] = v.w;
+            } else {
+                for (int k = 0; k < 4; ++k)
+                    if (row0 + k < n) c[g][k] = codes[row0 + k];
             }
+            reg[g] = row0 >= n ? 0u : regbits ? (uint32_t)(regbits[row0 >> 6] >> (row0 & 63)) & 0xFu : 0xFu;
         }
-        if (full) {
-            stream_store(u32x4_t{id[0], id[1], id[2], id[3]}, reinterpret_cast<u32x4_t*>(out + row0));
-        } else {
-            for (int k = 0; k < 4; ++k)
-                if (row0 + k < n) out[row0 + k] = id[k];
+        uint32_t id[G][4];
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                id[g][k] = 0xFFFFFFFFu;
+                if ((reg[g] >> k) & 1u) {
+                    const uint32_t wl = wlab ? word_label_of(wlab, wexc, c[g][k]) : kNone;
+                    id[g][k] = wl != kNone ? wl
+                               : MODE == 0 ? labelcode[c[g][k]]
+                                           : flab[rt_rank(RT[c[g][k] >> 6], c[g][k])];
+                }
+            }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int64_t row0 = tile + 256 * g + 4 * lane;
+            if (row0 + 4 <= n) {
+                stream_store(u32x4_t{id[g][0], id[g][1], id[g][2], id[g][3]}, reinterpret_cast<u32x4_t*>(out + row0));
+            } else {
+                for (int k = 0; k < 4; ++k)
+                    if (row0 + k < n) out[row0 + k] = id[g][k];
+            }
         }
     }
 }
@@ -1997,13 +2016,26 @@ int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, bool word_labels, c
             cus = 256;
         return (int64_t)2 * cus;
     }();
-    const int g = grid_for((n + 3) / 4, cap);
-    if (cl.label_by_code)
-        hipLaunchKernelGGL(k_assign<0>, dim3(g), dim3(kBlock), 0, s, codes, regular_bits, n, p.labelcode, p.D,
-                           p.RT, wlab, wexc, cluster_id);
-    else
-        hipLaunchKernelGGL(k_assign<1>, dim3(g), dim3(kBlock), 0, s, codes, regular_bits, n, p.labelcode, p.ilab,
-                           p.RT, wlab, wexc, cluster_id);
+    // ROGTK_ASSIGN_GROUPS=1|2|4: 4-row groups per lane and trip (A/B; default 2)
+    static const int groups = [] {
+        const char* e = getenv("ROGTK_ASSIGN_GROUPS");
+        const int v = e ? atoi(e) : 2;
+        return v == 1 || v == 4 ? v : 2;
+    }();
+    const int g = grid_for((n + 4 * groups - 1) / (4 * groups), cap);
+#define ROGTK_ASSIGN_LAUNCH(M, G)                                                                                 \
+    hipLaunchKernelGGL((k_assign<M, G>), dim3(g), dim3(kBlock), 0, s, codes, regular_bits, n, p.labelcode,       \
+                       M == 0 ? p.D : p.ilab, p.RT, wlab, wexc, cluster_id)
+    if (cl.label_by_code) {
+        if (groups == 1) ROGTK_ASSIGN_LAUNCH(0, 1);
+        else if (groups == 4) ROGTK_ASSIGN_LAUNCH(0, 4);
+        else ROGTK_ASSIGN_LAUNCH(0, 2);
+    } else {
+        if (groups == 1) ROGTK_ASSIGN_LAUNCH(1, 1);
+        else if (groups == 4) ROGTK_ASSIGN_LAUNCH(1, 4);
+        else ROGTK_ASSIGN_LAUNCH(1, 2);
+    }
+#undef ROGTK_ASSIGN_LAUNCH
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
 }
