@@ -39,6 +39,7 @@ import torch
 
 from . import device as D
 from .dist import gather_bitmaps
+from .dist import world as dist_world
 
 
 class _Slot:
@@ -94,6 +95,11 @@ class UmiPipeline:
         # exchange(local_bitmap) -> (bitmaps, n): the cross-rank step (default: the
         # all-gather of rogtk_amd.dist); tools may substitute an emulation
         self.exchange = exchange if exchange is not None else (lambda bm: gather_bitmaps(bm, self.group))
+        # across ranks the bitmap all-gather runs on its own stream, right behind the mark,
+        # so it overlaps the previous batch's resolve instead of lengthening the resolve
+        # stream's chain (a substituted exchange may reuse one buffer: it stays in line)
+        self.s_comm = (torch.cuda.Stream(dev) if exchange is None and not split_resolve and dist_world(group) > 1
+                       else None)
         self.last_scored: Optional[torch.cuda.Event] = None
         self.k = 0
         self.last_assigned: Optional[torch.cuda.Event] = None
@@ -157,6 +163,12 @@ class UmiPipeline:
                 slot.eng.resolve(bitmaps, nb, self.max_distance, stream=self.main, phase=1)
         marked = torch.cuda.Event()
         marked.record(self.main)
+        if self.s_comm is not None:
+            with torch.cuda.stream(self.s_comm):
+                self.s_comm.wait_event(marked)
+                bitmaps, nb = self.exchange(slot.eng.local_bitmap)
+                gathered = torch.cuda.Event()
+                gathered.record(self.s_comm)
         with torch.cuda.stream(sr):
             sr.wait_event(marked)
             if gate_resolve and slot.assigned is not None:
@@ -164,7 +176,11 @@ class UmiPipeline:
             if self.split_resolve:
                 slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr, phase=2)
             else:
-                bitmaps, nb = self.exchange(slot.eng.local_bitmap)
+                if self.s_comm is not None:
+                    sr.wait_event(gathered)
+                    bitmaps.record_stream(sr)  # allocated on the comm stream
+                else:
+                    bitmaps, nb = self.exchange(slot.eng.local_bitmap)
                 slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr)
             resolved = torch.cuda.Event()
             resolved.record(sr)

@@ -176,3 +176,61 @@ def test_bams_umi_cluster_sharded_matches_oracle(rg, tmp_path, world, md):
                 assert c == wc
             seen += 1
     assert seen == len(want)
+
+
+# ---- the streaming pipeline across ranks (the bench path at N > 1): bitmap all-gather on
+# its own stream, resolve of the merged bitmaps, labels of each rank's own reads
+
+def _pipe_worker(rank, world, port, n_total, seeds, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rogtk_amd import device as D
+        from rogtk_amd import dist as RD
+        from rogtk_amd import synth
+        from rogtk_amd.pipeline import UmiPipeline
+        start, count = RD.shard_range(n_total, rank, world)
+        outs = []
+        pipe = UmiPipeline(12, n_total, count, "cuda", depth=2, target=b"ACGTACGTACGT", max_distance=1,
+                           score_alone=True, on_assigned=lambda slot, b: outs.append(slot.cid[:count].clone()))
+        assert pipe.s_comm is not None
+        keep = []
+        for s in seeds:
+            codes = synth.umi_codes(n_total, 12, seed=s, start=start, count=count)
+            keep.append(D.PackedBatch(torch.from_numpy(codes.view(np.int32)).cuda(), 12))
+            pipe.submit(keep[-1])
+        pipe.drain()
+        torch.cuda.synchronize()
+        out_q.put((rank, start, [o.cpu().numpy().view(np.uint32).copy() for o in outs]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pipeline_world2_matches_oracle(rg):
+    """Two gloo ranks on cuda:0, 4 batches each through UmiPipeline: every batch's ids on
+    every rank equal the oracle over the union of both ranks' reads of that batch."""
+    from oracle import pyoracle as P
+    from rogtk_amd import synth
+
+    world, n_total = 2, 120_000
+    seeds = [synth.DEFAULT_SEED + 101 * k for k in range(4)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, n_total, seeds, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=100) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for k, s in enumerate(seeds):
+        codes = synth.umi_codes(n_total, 12, seed=s)
+        ref, _, _, _ = P.umi_cluster(P.StrCol.from_fixed(synth.codes_to_ascii(codes, 12)), 12, 1)
+        got = np.zeros(n_total, dtype=np.uint32)
+        for rank, start, outs in results:
+            assert len(outs) == len(seeds)
+            got[start:start + len(outs[k])] = outs[k]
+        assert np.array_equal(got, ref), k
