@@ -54,13 +54,17 @@ constexpr int kBlock = 256;
 constexpr int kMarkParts = 8;     // XCD partitions of the code space (mark)
 constexpr int kMarkChunks = 256;  // row chunks of the XCD-partitioned kernels; grid = 8 * chunks
 constexpr int kScanWords = 1024;  // words per scan block (4 per thread)
+constexpr int kLocal8Words = 1024;  // words per 8-position local tile (= one scan block)
+constexpr int kLocal8Cap = 8192;    // present codes an 8-position tile may hold
 constexpr int kMaxRounds = 64;
 constexpr int kRoundBatch = 4;
 
 // stats block (int64 slots): 0 n_distinct, 1 n_clusters, 2 overflow, 3 error,
 // 4 rounds run; round flags (u32 per round) follow at byte 64.
 // S_EDGE_OVF: the edge list of the global phase (mode 4) overflowed its capacity.
-enum StatSlot { S_NDISTINCT = 0, S_NCLUSTERS = 1, S_OVERFLOW = 2, S_ERROR = 3, S_ROUNDS = 4, S_EDGE_OVF = 5 };
+// S_P0: the first code position of the global phase (7, or 8 when every 4^8-code tile
+// fits the 8-position local CC), chosen on the device by the first scan
+enum StatSlot { S_NDISTINCT = 0, S_NCLUSTERS = 1, S_OVERFLOW = 2, S_ERROR = 3, S_ROUNDS = 4, S_EDGE_OVF = 5, S_P0 = 6 };
 // stats (8 x int64), round flags (u32 per round) at byte 64, edge-list counts (u32 per
 // round, +1) after them
 constexpr int kFlagsOff = 64;
@@ -107,7 +111,8 @@ __global__ void k_bitmap_small(uint8_t* __restrict__ pres, uint64_t nbits, uint6
     out[0] = m;
 }
 
-// Block-wide exclusive scan of one value per thread (256 threads = 4 waves).
+// Block-wide exclusive scan of one value per thread (NT threads, NT / 64 waves).
+template <int NT = kBlock>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave, uint32_t& total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t incl = v;
@@ -121,7 +126,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave
     uint32_t before = 0;
     total = 0;
 #pragma unroll
-    for (int k = 0; k < kBlock / 64; ++k) {
+    for (int k = 0; k < NT / 64; ++k) {
         const uint32_t s = s_wave[k];
         if (k < wave) before += s;
         total += s;
@@ -190,14 +195,27 @@ __device__ __forceinline__ void scan_block_sums(const uint32_t* blksum, int64_t 
 
 // per_live > 0: only the blocks that hold live indices (ceil(stats[S_NDISTINCT] /
 // per_live)) are scanned; later offsets are never read
+// p0_L > 0 (the first scan of a resolve, umi_len p0_L): also choose the local tiling.
+// A scan block (kScanWords = 1024 words) is exactly one 4^8-code tile, so the largest
+// block sum says whether every such tile fits the 8-position local CC (stats[S_P0]).
 __global__ __launch_bounds__(kBlock) void k_scan_blocks(const uint32_t* __restrict__ blksum,
                                                         int64_t nblocks, uint32_t* __restrict__ blkoff,
                                                         unsigned long long* __restrict__ stats,
                                                         int slot, int copy_slot, int zero_stats,
-                                                        int64_t per_live = 0) {
+                                                        int64_t per_live = 0, int p0_L = 0) {
     __shared__ uint32_t s_wave[kBlock / 64];
+    __shared__ unsigned int s_max;
     if (per_live > 0) nblocks = min<int64_t>(nblocks, ((int64_t)stats[S_NDISTINCT] + per_live - 1) / per_live);
     scan_block_sums(blksum, nblocks, blkoff, stats, slot, copy_slot, zero_stats, s_wave);
+    if (p0_L > 0) {
+        if (threadIdx.x == 0) s_max = 0;
+        __syncthreads();
+        unsigned int mx = 0;
+        for (int64_t b = threadIdx.x; b < nblocks; b += kBlock) mx = max(mx, blksum[b]);
+        atomicMax(&s_max, mx);
+        __syncthreads();
+        if (threadIdx.x == 0) stats[S_P0] = (p0_L >= 8 && s_max <= (unsigned int)kLocal8Cap) ? 8 : 7;
+    }
 }
 
 // RT[w] = {word, rank of its first code}; also zeroes the index-space live bits
@@ -373,47 +391,53 @@ __device__ __forceinline__ bool is_sparse(const unsigned long long* stats, int64
 }
 
 // The union-find runs over LOCAL RANKS (index - gbase) of the present codes, not over
-// local codes: a tile of nloc present codes needs nloc LDS slots. Two instances share
-// the tiles: in a sparse code space (under 1/8 of the codes present, e.g. one 10M-read
-// batch at L = 12) CAP = kLocalCapSmall (16 KB of LDS: 5 workgroups per CU instead of 2)
-// takes the tiles of at most 4096 codes and CAP = kLocalCodes (64 KB) the rest; in a
-// dense one (e.g. the merged bitmap of 8 ranks) the 64 KB instance takes every tile.
-// Measured (tools/local_cc_exp, uniform bitmaps): 6.5% dense 68 -> 51 us; splitting the
-// tiles of a 25%-dense space between both instances was slower (146 -> 219 us).
+// local codes: a tile of nloc present codes needs nloc LDS slots. Instances:
+//  * LP = 8 (tiles of 4^8 codes = 1024 words, one thread per word, CAP 8192 ranks): when
+//    every such tile holds at most 8192 codes (a sparse space, e.g. one 10M-read batch
+//    at L = 12; decided on the device by the first scan, stats[S_P0] = 8). Position 7 is
+//    then local too: 24% fewer local components and 41% fewer crossing pairs for the
+//    global rounds, which start at position 8.
+//  * LP = 7 (tiles of 4^7 codes = 256 words) otherwise: in a sparse code space (under 1/8
+//    of the codes present) CAP = kLocalCapSmall (16 KB of LDS: 5 workgroups per CU) takes
+//    the tiles of at most 4096 codes and CAP = kLocalCodes (64 KB) the rest; in a dense
+//    one (e.g. the merged bitmap of 8 ranks) the 64 KB instance takes every tile.
+// Measured (tools/local_cc_exp, uniform bitmaps, LP = 7): 6.5% dense 68 -> 51 us with the
+// small instance; splitting the tiles of a 25%-dense space between both was slower.
 constexpr int kLocalCapSmall = 4096;
 
-template <int CAP>
-__global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ RT, int64_t words, int L,
-                                                     uint32_t* __restrict__ f, uint32_t* __restrict__ D,
-                                                     uint32_t* __restrict__ UR, uint64_t* __restrict__ lroot,
-                                                     int64_t rwords,
-                                                     int64_t max_distinct,
-                                                     unsigned long long* __restrict__ stats) {
-    constexpr bool kSmall = CAP < kLocalCodes;
+template <int CAP, int TW, int LP>
+__global__ __launch_bounds__(TW) void k_local_cc(const uint4* __restrict__ RT, int64_t words, int L,
+                                                 uint32_t* __restrict__ f, uint32_t* __restrict__ D,
+                                                 uint32_t* __restrict__ UR, uint64_t* __restrict__ lroot,
+                                                 int64_t rwords,
+                                                 int64_t max_distinct,
+                                                 unsigned long long* __restrict__ stats) {
+    constexpr bool kSmall = LP == 7 && CAP < kLocalCodes;
+    constexpr int kLrb = CAP / 64 + 2;
+    if (((int)stats[S_P0] == 8 ? 8 : 7) != LP) return;  // the other tiling
     const bool sparse = is_sparse(stats, words);
     if (kSmall && !sparse) return;  // dense space: all tiles in the 64 KB instance
-    __shared__ uint64_t wb[kLocalWords];
-    __shared__ uint64_t wcm[kWordComps][kLocalWords];  // listed component masks per word
-    __shared__ uint32_t lpre[kLocalWords];
+    __shared__ uint64_t wb[TW];
+    __shared__ uint64_t wcm[kWordComps][TW];  // listed component masks per word
+    __shared__ uint32_t lpre[TW];
     __shared__ uint32_t lf[CAP];  // by local rank; valid at the first code of each in-word component
-    __shared__ int8_t wcn[kLocalWords];    // listed components (-1 overflow)
-    __shared__ uint8_t wone[kLocalWords];  // the word's codes form one in-word component
-    __shared__ uint64_t lrb[kLocalWords + 2];  // local-root bits of the block's index range
-    __shared__ uint32_t s_wave[kBlock / 64];
+    __shared__ int8_t wcn[TW];    // listed components (-1 overflow)
+    __shared__ uint8_t wone[TW];  // the word's codes form one in-word component
+    __shared__ uint64_t lrb[kLrb];  // local-root bits of the block's index range
+    __shared__ uint32_t s_wave[TW / 64];
     const int t = threadIdx.x;
-    const int64_t base = (int64_t)blockIdx.x * kLocalWords;
-    const int nw = (int)min<int64_t>(kLocalWords, words - base);
+    const int64_t base = (int64_t)blockIdx.x * TW;
+    const int nw = (int)min<int64_t>(TW, words - base);
     const uint4 e = t < nw ? RT[base + t] : make_uint4(0, 0, 0, 0);
     const uint64_t m = rt_word(e);
     uint32_t nloc;
-    const uint32_t ex = block_excl_scan((uint32_t)__popcll(m), s_wave, nloc);
-    if (kSmall ? nloc > (uint32_t)CAP : (sparse && nloc <= (uint32_t)kLocalCapSmall)) return;  // the other's
-    lrb[t] = 0;
-    if (t < 2) lrb[kLocalWords + t] = 0;
+    const uint32_t ex = block_excl_scan<TW>((uint32_t)__popcll(m), s_wave, nloc);
+    if (LP == 7 && (kSmall ? nloc > (uint32_t)CAP : (sparse && nloc <= (uint32_t)kLocalCapSmall))) return;
+    for (int k = t; k < kLrb; k += TW) lrb[k] = 0;
 #ifdef ROGTK_LCC_TIMING
     unsigned long long t_last_ = wall_clock64();
 #endif
-    const int lpos = L < kLocalPos ? L : kLocalPos;
+    const int lpos = L < LP ? L : LP;
     wb[t] = m;
     lpre[t] = ex;
     const uint32_t gbase = RT[base].z;
@@ -456,10 +480,9 @@ __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ R
     //    words of a group differ only at p, so two word components that share a bit
     //    are adjacent; unite every intersecting pair of components (by the local rank
     //    of each component's first code)
-    {
-        const int per = nw >> 2;
-        if (per > 0 && t < (lpos - 3) * per) {
-            const int p = 3 + t / per, g = t % per, s2 = 2 * p - 6, stride = 1 << s2;
+    for (int task = t, per = nw >> 2; per > 0 && task < (lpos - 3) * per; task += TW) {
+        {
+            const int p = 3 + task / per, g = task % per, s2 = 2 * p - 6, stride = 1 << s2;
             const int w0 = ((g >> s2) << (s2 + 2)) | (g & (stride - 1));
             WordComps wv[4];
             uint32_t lp[4];
@@ -593,7 +616,7 @@ __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ R
     {
         const uint32_t nlw = nloc ? ((gbase & 63u) + nloc + 63u) / 64u : 0u;
         const int64_t w0 = (int64_t)(gbase >> 6);
-        for (uint32_t k = t; k < nlw; k += kBlock) {
+        for (uint32_t k = t; k < nlw; k += TW) {
             const int64_t w = w0 + k;
             if (w >= rwords) break;
             const uint64_t v = lrb[k];
@@ -607,15 +630,28 @@ __global__ __launch_bounds__(kBlock) void k_local_cc(const uint4* __restrict__ R
     LCC_T(3);
 }
 
-// Both instances of k_local_cc (each exits early for the tiles of the other).
+// ROGTK_LOCAL8=0: never the 8-position local tiling (A/B)
+inline bool local8_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("ROGTK_LOCAL8");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// Every instance of k_local_cc (each exits early for the tiles of the others).
 inline void launch_local_cc(const uint4* RT, int64_t words, int L, uint32_t* f, uint32_t* D, uint32_t* UR,
                             uint64_t* lroot, int64_t rwords, int64_t max_distinct, unsigned long long* stats,
                             hipStream_t s) {
+    if (L >= 8 && local8_enabled())
+        hipLaunchKernelGGL((k_local_cc<kLocal8Cap, kLocal8Words, 8>),
+                           dim3((unsigned)((words + kLocal8Words - 1) / kLocal8Words)), dim3(kLocal8Words), 0, s, RT,
+                           words, L, f, D, UR, lroot, rwords, max_distinct, stats);
     const int64_t lblocks = (words + kLocalWords - 1) / kLocalWords;
-    hipLaunchKernelGGL(k_local_cc<kLocalCapSmall>, dim3((unsigned)lblocks), dim3(kBlock), 0, s, RT, words, L, f, D,
-                       UR, lroot, rwords, max_distinct, stats);
-    hipLaunchKernelGGL(k_local_cc<kLocalCodes>, dim3((unsigned)lblocks), dim3(kBlock), 0, s, RT, words, L, f, D, UR,
-                       lroot, rwords, max_distinct, stats);
+    hipLaunchKernelGGL((k_local_cc<kLocalCapSmall, kLocalWords, 7>), dim3((unsigned)lblocks), dim3(kBlock), 0, s, RT,
+                       words, L, f, D, UR, lroot, rwords, max_distinct, stats);
+    hipLaunchKernelGGL((k_local_cc<kLocalCodes, kLocalWords, 7>), dim3((unsigned)lblocks), dim3(kBlock), 0, s, RT,
+                       words, L, f, D, UR, lroot, rwords, max_distinct, stats);
 }
 
 // --------------------------------------------------------------- global CC
@@ -680,8 +716,10 @@ template <bool CHASE>
 __global__ __launch_bounds__(kBlock) void k_hook_g(const uint4* __restrict__ RT, const uint32_t* __restrict__ UR,
                                                    int64_t words, int L, int p0, uint32_t* f,
                                                    unsigned int* __restrict__ flags, int round,
-                                                   uint64_t* __restrict__ active, int64_t active_words) {
+                                                   uint64_t* __restrict__ active, int64_t active_words,
+                                                   const unsigned long long* __restrict__ stats) {
     if (round > 0 && flags[round - 1] == 0) return;  // converged earlier
+    p0 = max(p0, (int)stats[S_P0]);  // the local phase's last position + 1 (7 or 8)
     const int64_t per = words >> 2;
     const int64_t tasks = (int64_t)(L - p0) * per;
     const int64_t u = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -843,7 +881,9 @@ __device__ __forceinline__ void uf_union(uint32_t* f, uint32_t a, uint32_t b) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_union_g(const uint4* __restrict__ RT, const uint32_t* __restrict__ UR,
-                                                    int64_t words, int L, int p0, uint32_t* f) {
+                                                    int64_t words, int L, int p0, uint32_t* f,
+                                                    const unsigned long long* __restrict__ stats) {
+    p0 = max(p0, (int)stats[S_P0]);
     const int64_t per = words >> 2;
     const int64_t tasks = (int64_t)(L - p0) * per;
     const int64_t u = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -1030,7 +1070,9 @@ __device__ __forceinline__ void put_clique(unsigned long long* T, const EdgeSink
 // Round 0: positions p0..L-1 as word-group cliques (the tasks of k_hook_g).
 __global__ __launch_bounds__(kBlock) void k_sweep_edges(const uint4* __restrict__ RT, const uint32_t* __restrict__ UR,
                                                         int64_t words, int L, int p0, uint32_t* f, EdgeSink o,
-                                                        unsigned int* __restrict__ flags) {
+                                                        unsigned int* __restrict__ flags,
+                                                        const unsigned long long* __restrict__ stats) {
+    p0 = max(p0, (int)stats[S_P0]);
     __shared__ unsigned long long T[kPairSlots];
     __shared__ uint32_t s_wave[kBlock / 64];
     __shared__ unsigned int s_base;
@@ -1649,7 +1691,7 @@ int enqueue_rounds(const ClusterLayout& cl, const WsPtrs& p, int from, int to, h
             const EdgeSink o = edge_sink(cl, p, k);
             if (k == 0) {
                 hipLaunchKernelGGL(k_sweep_edges, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words,
-                                   cl.L, kLocalPos, p.f, o, p.flags);
+                                   cl.L, kLocalPos, p.f, o, p.flags, (const unsigned long long*)p.stats);
             } else {
                 const uint2* ein = p.edges + (int64_t)(k & 1) * cl.ecap;
                 hipLaunchKernelGGL(k_edge_hook, dim3(eg), dim3(kBlock), 0, s, ein, p.ecnt + k, o, p.f, p.flags, k,
@@ -1662,12 +1704,14 @@ int enqueue_rounds(const ClusterLayout& cl, const WsPtrs& p, int from, int to, h
         // hooks chase to the roots themselves; one flatten after the batch of rounds
         for (int k = from; k < to; ++k)
             hipLaunchKernelGGL(k_hook_g<true>, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words, cl.L,
-                               kLocalPos, p.f, p.flags, k, p.active, cl.active_words);
+                               kLocalPos, p.f, p.flags, k, p.active, cl.active_words,
+                               (const unsigned long long*)p.stats);
         hipLaunchKernelGGL(k_flatten_live, dim3(pg), dim3(kBlock), 0, s, p.f, p.lroot, cl.max_distinct, p.stats);
     } else {
         for (int k = from; k < to; ++k) {
             hipLaunchKernelGGL(k_hook_g<false>, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words,
-                               cl.L, kLocalPos, p.f, p.flags, k, p.active, cl.active_words);
+                               cl.L, kLocalPos, p.f, p.flags, k, p.active, cl.active_words,
+                               (const unsigned long long*)p.stats);
             hipLaunchKernelGGL(k_jump, dim3(pg), dim3(kBlock), 0, s, p.f, p.lroot, cl.max_distinct, p.stats, p.flags,
                                k);
         }
@@ -1742,7 +1786,8 @@ int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bi
                            n_bitmaps, cl.words, (const unsigned long long*)nullptr, p.G, p.wpref,
                            p.blksum);
         hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, p.blksum, cl.blocks, p.blkoff,
-                           p.stats, (int)S_NDISTINCT, max_distance == 0 ? (int)S_NCLUSTERS : -1, 1);
+                           p.stats, (int)S_NDISTINCT, max_distance == 0 ? (int)S_NCLUSTERS : -1, 1, (int64_t)0,
+                           local8_enabled() ? cl.L : 0);
     }
     if (phases & 1) {
         ProfScope prof(K_COMPACT, s);
@@ -1768,7 +1813,7 @@ int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bi
             // one-pass union-find: exact when the stream reaches the labels
             const int64_t tasks = (int64_t)(cl.L - kLocalPos) * (cl.words >> 2);
             hipLaunchKernelGGL(k_union_g, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words, cl.L,
-                               kLocalPos, p.f);
+                               kLocalPos, p.f, (const unsigned long long*)p.stats);
             hipLaunchKernelGGL(k_flatten_live, dim3(grid_for(cl.max_distinct, kPersistentGrid)), dim3(kBlock), 0, s,
                                p.f, p.lroot, cl.max_distinct, p.stats);
         } else if (cl.L > kLocalPos) {

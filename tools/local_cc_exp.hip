@@ -37,7 +37,8 @@ int main() {
         CK(hipMemset(p.stats, 0, 64));
         hipLaunchKernelGGL(k_scan_words, dim3((unsigned)cl.blocks), dim3(kBlock), 0, 0, bm, 1, cl.words,
                            (const unsigned long long*)nullptr, p.G, p.wpref, p.blksum);
-        hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, 0, p.blksum, cl.blocks, p.blkoff, p.stats, 0, -1, 1);
+        hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, 0, p.blksum, cl.blocks, p.blkoff, p.stats, 0, -1, 1,
+                           (int64_t)0, getenv("LCC_P0_7") ? 0 : L);
         hipLaunchKernelGGL(k_rt, dim3(grid_for(cl.words)), dim3(kBlock), 0, 0, p.G, cl.words, p.wpref, p.blkoff, p.RT, p.lroot, cl.rwords);
         const int64_t lblocks = (cl.words + kLocalWords - 1) / kLocalWords;
         float best = 1e9;
