@@ -217,6 +217,37 @@ def test_cluster_lengths(rg, L, md):
     assert np.array_equal(g[rv].astype(np.uint32), rc[rv])
 
 
+@pytest.mark.parametrize("L,n,want_p0", [(9, 20_000, 8), (9, 120_000, 7), (8, 6_000, 8), (8, 30_000, 7),
+                                          (10, 150_000, 8), (12, 200_000, 8)])
+def test_local_tiling_both_paths(rg, L, n, want_p0):
+    """The local phase covers positions 0..7 (4^8-code tiles) when every tile holds at most
+    8192 distinct codes and 0..6 otherwise (decided on the device, stats[S_P0]): uniformly
+    random codes of a few densities take each path, and the ids equal the oracle."""
+    import torch
+
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+
+    rng = np.random.default_rng(L * 1000 + n)
+    parents = rng.integers(0, 4 ** L, size=max(n // 4, 1), dtype=np.uint64)
+    codes_h = parents[rng.integers(0, len(parents), size=n)]
+    flip = rng.random(n) < 0.3
+    pos = rng.integers(0, L, size=n).astype(np.uint64)
+    codes_h = np.where(flip, codes_h ^ (rng.integers(1, 4, size=n).astype(np.uint64) << (2 * pos)), codes_h)
+    codes_h = codes_h.astype(np.uint32)
+    codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
+    batch = D.PackedBatch(codes, L)
+    eng = D.ClusterEngine(L, min(n, 4 ** L), "cuda")
+    cid = torch.empty(n, dtype=torch.int32, device="cuda")
+    D.cluster_batch(eng, batch, cid, 1)
+    torch.cuda.synchronize()
+    p0 = int(eng.ws[:64].view(torch.int64)[6].item())
+    assert p0 == want_p0
+    rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L)), L, 1)
+    assert eng.stats()["n_clusters"] == rk
+    assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc)
+
+
 @pytest.mark.parametrize("L", [18, 32])
 def test_long_cluster_bruteforce_and_chains(rg, L):
     """Long UMIs vs the O(d^2) brute force, with Hamming-1 chains that cross every
