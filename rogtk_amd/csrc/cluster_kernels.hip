@@ -397,13 +397,11 @@ __device__ __forceinline__ bool is_sparse(const unsigned long long* stats, int64
 //    at L = 12; decided on the device by the first scan, stats[S_P0] = 8). Position 7 is
 //    then local too: 24% fewer local components and 41% fewer crossing pairs for the
 //    global rounds, which start at position 8.
-//  * LP = 7 (tiles of 4^7 codes = 256 words) otherwise: in a sparse code space (under 1/8
-//    of the codes present) CAP = kLocalCapSmall (16 KB of LDS: 5 workgroups per CU) takes
-//    the tiles of at most 4096 codes and CAP = kLocalCodes (64 KB) the rest; in a dense
-//    one (e.g. the merged bitmap of 8 ranks) the 64 KB instance takes every tile.
-// Measured (tools/local_cc_exp, uniform bitmaps, LP = 7): 6.5% dense 68 -> 51 us with the
-// small instance; splitting the tiles of a 25%-dense space between both was slower.
-constexpr int kLocalCapSmall = 4096;
+//  * LP = 7 (tiles of 4^7 codes = 256 words, CAP = kLocalCodes: 64 KB) otherwise, e.g. the
+//    merged bitmap of 8 ranks, or a skewed sparse space with a crowded 4^8 tile.
+// (Round 2 also had a 16 KB LP = 7 instance for the small tiles of a sparse space: 6.5%
+// dense 68 -> 51 us; the LP = 8 tiling now takes those spaces, so it was dropped - its
+// empty launch cost ~5 us of every resolve.)
 
 template <int CAP, int TW, int LP>
 __global__ __launch_bounds__(TW) void k_local_cc(const uint4* __restrict__ RT, int64_t words, int L,
@@ -412,11 +410,9 @@ __global__ __launch_bounds__(TW) void k_local_cc(const uint4* __restrict__ RT, i
                                                  int64_t rwords,
                                                  int64_t max_distinct,
                                                  unsigned long long* __restrict__ stats) {
-    constexpr bool kSmall = LP == 7 && CAP < kLocalCodes;
     constexpr int kLrb = CAP / 64 + 2;
     if (((int)stats[S_P0] == 8 ? 8 : 7) != LP) return;  // the other tiling
     const bool sparse = is_sparse(stats, words);
-    if (kSmall && !sparse) return;  // dense space: all tiles in the 64 KB instance
     __shared__ uint64_t wb[TW];
     __shared__ uint64_t wcm[kWordComps][TW];  // listed component masks per word
     __shared__ uint32_t lpre[TW];
@@ -432,7 +428,6 @@ __global__ __launch_bounds__(TW) void k_local_cc(const uint4* __restrict__ RT, i
     const uint64_t m = rt_word(e);
     uint32_t nloc;
     const uint32_t ex = block_excl_scan<TW>((uint32_t)__popcll(m), s_wave, nloc);
-    if (LP == 7 && (kSmall ? nloc > (uint32_t)CAP : (sparse && nloc <= (uint32_t)kLocalCapSmall))) return;
     for (int k = t; k < kLrb; k += TW) lrb[k] = 0;
 #ifdef ROGTK_LCC_TIMING
     unsigned long long t_last_ = wall_clock64();
@@ -648,8 +643,6 @@ inline void launch_local_cc(const uint4* RT, int64_t words, int L, uint32_t* f, 
                            dim3((unsigned)((words + kLocal8Words - 1) / kLocal8Words)), dim3(kLocal8Words), 0, s, RT,
                            words, L, f, D, UR, lroot, rwords, max_distinct, stats);
     const int64_t lblocks = (words + kLocalWords - 1) / kLocalWords;
-    hipLaunchKernelGGL((k_local_cc<kLocalCapSmall, kLocalWords, 7>), dim3((unsigned)lblocks), dim3(kBlock), 0, s, RT,
-                       words, L, f, D, UR, lroot, rwords, max_distinct, stats);
     hipLaunchKernelGGL((k_local_cc<kLocalCodes, kLocalWords, 7>), dim3((unsigned)lblocks), dim3(kBlock), 0, s, RT,
                        words, L, f, D, UR, lroot, rwords, max_distinct, stats);
 }
