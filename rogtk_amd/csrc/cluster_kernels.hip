@@ -2172,18 +2172,55 @@ __global__ __launch_bounds__(kPartBlock) void k_part_bitmap(const uint32_t* __re
 constexpr int kSliceBlock = 1024;
 constexpr int kSliceChunks = 16;   // a multiple of the 8 XCDs
 constexpr int kSliceLog2 = 20;     // codes per slice (LDS bits)
+constexpr int kMaxSlices = 16;     // 4^12 / 2^20
+constexpr int kBucketRows = 8192;  // rows per segment workgroup (32 per lane)
+constexpr int kSegCap = 2048;      // codes per (slice, workgroup) segment: 4x the mean share at 16 slices
 
+// Segment mode (segs != nullptr, written by k_slice_bucket): workgroup (s, c) reads only
+// slice s's segments of the bucket workgroups of chunk c (every code is read once in
+// all); if one of them overflowed, it reads those workgroups' rows instead.
 __global__ __launch_bounds__(kSliceBlock) void k_slice_mark(const uint32_t* __restrict__ codes,
                                                             const uint64_t* __restrict__ regbits, int64_t n,
                                                             int slice_log2, int chunks, int64_t chunk_rows,
-                                                            uint64_t* __restrict__ out, int64_t words) {
+                                                            uint64_t* __restrict__ out, int64_t words,
+                                                            const uint32_t* __restrict__ segs = nullptr,
+                                                            const uint32_t* __restrict__ seglen = nullptr,
+                                                            int nbuckets = 0) {
     __shared__ uint32_t sbits[(1u << kSliceLog2) / 32];  // 128 KB: the slice's bits (2^slice_log2 used)
     const int c = blockIdx.x % chunks, sl = blockIdx.x / chunks;
     const uint32_t sw32 = (1u << slice_log2) >> 5;
     for (uint32_t k = threadIdx.x; k < sw32; k += kSliceBlock) sbits[k] = 0;
     __syncthreads();
     const uint32_t smask = (1u << slice_log2) - 1u;
-    const int64_t r0 = (int64_t)c * chunk_rows, r1 = min(n, r0 + chunk_rows);
+    int64_t r0 = (int64_t)c * chunk_rows, r1 = min(n, r0 + chunk_rows);
+    if (segs) {
+        // the bucket workgroups of this chunk; a segment longer than kSegCap was not stored
+        // (its workgroup overflowed): then this chunk's rows are read instead
+        const int b0 = (int)((int64_t)c * nbuckets / chunks), b1 = (int)((int64_t)(c + 1) * nbuckets / chunks);
+        bool over = false;
+        for (int b = b0 + (int)threadIdx.x; b < b1; b += kSliceBlock) over |= seglen[(int64_t)sl * nbuckets + b] > kSegCap;
+        r0 = (int64_t)b0 * kBucketRows;
+        r1 = min(n, (int64_t)b1 * kBucketRows);
+        if (!__syncthreads_or(over)) {
+            // one wave per segment: 256 codes per pass of 16-B loads
+            const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+            for (int b = b0 + wave; b < b1; b += kSliceBlock / 64) {
+                const uint32_t len = seglen[(int64_t)sl * nbuckets + b];
+                const uint32_t* seg = segs + ((int64_t)sl * nbuckets + b) * kSegCap;
+                for (uint32_t i = 4 * lane; i < len; i += 256) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(seg + i);
+                    const uint32_t cc[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (i + k < len) {
+                            const uint32_t bb = cc[k] & smask;
+                            atomicOr(&sbits[bb >> 5], 1u << (bb & 31));
+                        }
+                }
+            }
+            r1 = r0;  // no row pass
+        }
+    }
     // kSliceUnroll independent 16-B loads in flight per lane before the LDS atomics that
     // consume them (one load per iteration left the kernel latency-bound: 125 us)
     constexpr int kSliceUnroll = 8;
@@ -2224,6 +2261,93 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_mark(const uint32_t* __re
         o[k] = (uint64_t)sbits[2 * k] | ((uint64_t)sbits[2 * k + 1] << 32);
 }
 
+// Pass 1 of the segment mode: one workgroup per kBucketRows rows ranks its valid codes
+// by slice (lanes of a wave with one slice found by 4 ballots, one LDS atomic per slice
+// and wave) and stores them into its own segment of each slice (kSegCap codes, 4x the
+// mean share at 16 slices), with the segment lengths: no global atomics (a global
+// cursor per slice, hit by every workgroup, serialised the pass to 236 us). A segment
+// that would overflow is not stored (its length says so), and the slice pass reads the
+// rows of that chunk instead.
+__global__ __launch_bounds__(kBlock) void k_slice_bucket(const uint32_t* __restrict__ codes,
+                                                         const uint64_t* __restrict__ regbits, int64_t n,
+                                                         int slice_log2, int nslices, uint32_t* __restrict__ segs,
+                                                         uint32_t* __restrict__ seglen, int nbuckets) {
+    __shared__ unsigned int cnt[kMaxSlices], lbase[kMaxSlices + 1];
+    __shared__ uint32_t stage[kBucketRows];
+    const int t = threadIdx.x, lane = t & 63;
+    if (t < kMaxSlices) cnt[t] = 0;
+    __syncthreads();
+    const int64_t row0 = (int64_t)blockIdx.x * kBucketRows;
+    constexpr int kPer = kBucketRows / kBlock / 4;  // uint4 loads per lane
+    uint32_t key[kPer * 4];  // slice << 16 | index within the slice's segment, or kNone
+    uint32_t val[kPer * 4];
+    uint32_t regs[kPer];
+    // all kPer 16-B loads in flight before the ranking that consumes them
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+        const int64_t r = row0 + 4 * ((int64_t)u * kBlock + t);
+        uint4 v = make_uint4(0, 0, 0, 0);
+        uint32_t reg = 0;
+        if (r + 4 <= n) {
+            v = *reinterpret_cast<const uint4*>(codes + r);
+            reg = regbits ? (uint32_t)(regbits[r >> 6] >> (r & 63)) & 0xFu : 0xFu;
+        } else if (r < n) {
+            v.x = codes[r];
+            if (r + 1 < n) v.y = codes[r + 1];
+            if (r + 2 < n) v.z = codes[r + 2];
+            reg = (regbits ? (uint32_t)(regbits[r >> 6] >> (r & 63)) & 0xFu : 0xFu) & ((1u << (uint32_t)(n - r)) - 1u);
+        }
+        val[4 * u] = v.x;
+        val[4 * u + 1] = v.y;
+        val[4 * u + 2] = v.z;
+        val[4 * u + 3] = v.w;
+        regs[u] = reg;
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t sl = val[4 * u + k] >> slice_log2;
+            const bool ok = ((regs[u] >> k) & 1u) && sl < (uint32_t)nslices;
+            uint64_t peers = __ballot(ok);
+#pragma unroll
+            for (int bit = 0; bit < 4; ++bit) {
+                const uint64_t b = __ballot((sl >> bit) & 1u);
+                peers &= ((sl >> bit) & 1u) ? b : ~b;
+            }
+            const int leader = peers ? __ffsll((long long)peers) - 1 : 0;
+            unsigned int base = 0;
+            if (ok && lane == leader) base = atomicAdd(&cnt[sl], (unsigned int)__popcll(peers));
+            base = __shfl(base, leader);
+            key[4 * u + k] = ok ? (sl << 16) | (base + (uint32_t)__popcll(peers & ((1ull << lane) - 1ull))) : kNone;
+        }
+    }
+    __syncthreads();
+    if (t < nslices) seglen[(int64_t)t * nbuckets + blockIdx.x] = cnt[t];  // > kSegCap: not stored
+    if (t == 0) {
+        unsigned int acc = 0;
+        for (int k = 0; k < nslices; ++k) {
+            lbase[k] = acc;
+            acc += cnt[k];
+        }
+        lbase[nslices] = acc;
+    }
+    __syncthreads();
+    // stage sorted by slice in LDS, then store each slice's run contiguously
+#pragma unroll
+    for (int u = 0; u < kPer * 4; ++u) {
+        const uint32_t kk = key[u];
+        if (kk != kNone) stage[lbase[kk >> 16] + (kk & 0xFFFFu)] = val[u];
+    }
+    __syncthreads();
+    const unsigned int total = lbase[nslices];
+    for (unsigned int i = t; i < total; i += kBlock) {
+        const uint32_t c = stage[i];
+        const uint32_t sl = c >> slice_log2;
+        if (cnt[sl] <= (unsigned int)kSegCap) segs[((int64_t)sl * nbuckets + blockIdx.x) * kSegCap + (i - lbase[sl])] = c;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_or_partials(const uint64_t* __restrict__ partials, int chunks,
                                                         int64_t words, uint64_t* __restrict__ out) {
     for (int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x; w < words; w += (int64_t)gridDim.x * kBlock) {
@@ -2235,6 +2359,20 @@ __global__ __launch_bounds__(kBlock) void k_or_partials(const uint64_t* __restri
 
 // chunks of the slice mark for n rows (1 = the slices write the bitmap directly)
 inline int slice_chunks(int64_t n) { return n >= (1 << 20) ? kSliceChunks : 1; }
+inline int slices_of(int L) { return 1 << (2 * L - std::min(2 * L, kSliceLog2)); }
+inline int64_t seg_buckets(int64_t n) { return (n + kBucketRows - 1) / kBucketRows; }
+// segments + their lengths of the segment mode
+inline int64_t seg_bytes(int64_t n) {
+    return ((int64_t)kMaxSlices * seg_buckets(n) * kSegCap * 4) + ((int64_t)kMaxSlices * seg_buckets(n) * 4 + 255) / 256 * 256;
+}
+// ROGTK_SLICE_BUCKETS=0: slices read all rows (A/B)
+inline bool slice_buckets_on() {
+    static const bool on = [] {
+        const char* e = getenv("ROGTK_SLICE_BUCKETS");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 
 size_t part_sort_temp(int64_t n) {
     size_t tb = 0;
@@ -2266,7 +2404,11 @@ int cluster_mark_bitmap_temp(int64_t n, int L, int64_t* bytes) {
     // both methods' scratch, so that the method can be switched on a live buffer
     const int64_t sort_bytes = 2 * ((nn * 4 + 255) / 256 * 256) + (int64_t)part_sort_temp(nn) + 256;
     const int64_t words = ((int64_t)1 << (2 * L)) / 64;
-    const int64_t slice_bytes = L <= 12 && slice_chunks(nn) > 1 ? (int64_t)slice_chunks(nn) * words * 8 : 0;
+    int64_t slice_bytes = 0;
+    if (L <= 12 && slice_chunks(nn) > 1) {
+        slice_bytes = (int64_t)slice_chunks(nn) * words * 8;
+        if (slices_of(L) > 1) slice_bytes += seg_bytes(nn);
+    }
     *bytes = std::max(sort_bytes, slice_bytes);
     return ROGTK_OK;
 }
@@ -2292,7 +2434,19 @@ int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bi
         chunk_rows = (chunk_rows + 3) / 4 * 4;  // rows of a chunk start 4-aligned (uint4 loads)
         const int64_t words = ((int64_t)1 << two_l) / 64;
         uint64_t* dst = chunks > 1 ? (uint64_t*)temp : bitmap;
-        hipLaunchKernelGGL(k_slice_mark, dim3((unsigned)(slices * chunks)), dim3(kSliceBlock), 0, s, codes, regular_bits, n, slog, chunks, chunk_rows, dst, words);
+        const uint32_t* segs = nullptr;
+        uint32_t* seglen = nullptr;
+        const int nb = (int)seg_buckets(n);
+        if (chunks > 1 && slices > 1 && slices <= kMaxSlices && slice_buckets_on()) {
+            // segment pass: every slice workgroup then reads only its slice's codes (the
+            // chunks of all rows were read once per slice: 16x at L = 12, from L2)
+            segs = (const uint32_t*)((uint8_t*)temp + (int64_t)chunks * words * 8);
+            seglen = (uint32_t*)((uint8_t*)segs + (int64_t)kMaxSlices * nb * kSegCap * 4);
+            hipLaunchKernelGGL(k_slice_bucket, dim3((unsigned)nb), dim3(kBlock), 0, s, codes, regular_bits, n, slog,
+                               slices, (uint32_t*)segs, seglen, nb);
+        }
+        hipLaunchKernelGGL(k_slice_mark, dim3((unsigned)(slices * chunks)), dim3(kSliceBlock), 0, s, codes, regular_bits,
+                           n, slog, chunks, chunk_rows, dst, words, segs, (const uint32_t*)seglen, nb);
         if (chunks > 1)
             hipLaunchKernelGGL(k_or_partials, dim3(grid_for(words, 4096)), dim3(kBlock), 0, s, dst, chunks, words,
                                bitmap);

@@ -682,3 +682,42 @@ def test_mark_bitmap_sort_equals_presence_path(rg, L, n):
             finally:
                 D.set_mark_method(D.MARK_AUTO)
             assert torch.equal(ref, got), (L, n, rb is None, method)
+
+
+@pytest.mark.parametrize("L,skew", [(12, "one_slice"), (12, "two_slices"), (11, "one_slice"), (12, "uniform"),
+                                    (12, "half")])
+def test_slice_bucket_overflow_falls_back(rg, L, skew):
+    """Slice mark with per-workgroup segments: rows concentrated in one or two code slices
+    overflow their segments (4x the mean share), and the slice pass reads those rows
+    instead, per chunk; every bitmap equals the presence path bit for bit."""
+    import torch
+
+    from rogtk_amd import device as D
+
+    rng = np.random.default_rng(hash(skew) % 1000 + L)
+    n = 2_100_000
+    space = 4 ** L
+    if skew == "one_slice":
+        codes_h = rng.integers(0, 1 << 20, size=n, dtype=np.uint64).astype(np.uint32)
+    elif skew == "two_slices":
+        codes_h = (rng.integers(0, 1 << 20, size=n, dtype=np.uint64) + (rng.integers(0, 2, size=n) << 22).astype(np.uint64)).astype(np.uint32)
+    else:
+        codes_h = rng.integers(0, space, size=n, dtype=np.uint64).astype(np.uint32)
+        if skew == "half":  # the second half in one slice: some chunks overflow, others not
+            codes_h[n // 2:] = rng.integers(0, 1 << 20, size=n - n // 2, dtype=np.uint64).astype(np.uint32)
+    codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
+    reg = rng.random(n) > 0.02
+    bits = np.packbits(np.concatenate([reg, np.zeros((-n) % 64, bool)]), bitorder="little").view(np.int64)
+    batch = D.PackedBatch(codes, L, torch.from_numpy(bits.copy()).cuda())
+    a = D.ClusterEngine(L, min(n, space), "cuda")
+    a.mark(batch)
+    ref = a.build_local_bitmap().clone()
+    try:
+        D.set_mark_method(D.MARK_SLICES)
+        b = D.ClusterEngine(L, min(n, space), "cuda")
+        for _ in range(2):  # the bucket cursors are reset per call
+            got = b.mark_bitmap(batch).clone()
+            torch.cuda.synchronize()
+            assert torch.equal(ref, got), skew
+    finally:
+        D.set_mark_method(D.MARK_AUTO)
