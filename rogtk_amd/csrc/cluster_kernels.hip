@@ -2268,7 +2268,8 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_mark(const uint32_t* __re
 // cursor per slice, hit by every workgroup, serialised the pass to 236 us). A segment
 // that would overflow is not stored (its length says so), and the slice pass reads the
 // rows of that chunk instead.
-__global__ __launch_bounds__(kBlock) void k_slice_bucket(const uint32_t* __restrict__ codes,
+constexpr int kBucketThreads = 1024;  // 8 rows per lane: short rank chains per wave
+__global__ __launch_bounds__(kBucketThreads) void k_slice_bucket(const uint32_t* __restrict__ codes,
                                                          const uint64_t* __restrict__ regbits, int64_t n,
                                                          int slice_log2, int nslices, uint32_t* __restrict__ segs,
                                                          uint32_t* __restrict__ seglen, int nbuckets) {
@@ -2278,14 +2279,14 @@ __global__ __launch_bounds__(kBlock) void k_slice_bucket(const uint32_t* __restr
     if (t < kMaxSlices) cnt[t] = 0;
     __syncthreads();
     const int64_t row0 = (int64_t)blockIdx.x * kBucketRows;
-    constexpr int kPer = kBucketRows / kBlock / 4;  // uint4 loads per lane
+    constexpr int kPer = kBucketRows / kBucketThreads / 4;  // uint4 loads per lane
     uint32_t key[kPer * 4];  // slice << 16 | index within the slice's segment, or kNone
     uint32_t val[kPer * 4];
     uint32_t regs[kPer];
     // all kPer 16-B loads in flight before the ranking that consumes them
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
-        const int64_t r = row0 + 4 * ((int64_t)u * kBlock + t);
+        const int64_t r = row0 + 4 * ((int64_t)u * kBucketThreads + t);
         uint4 v = make_uint4(0, 0, 0, 0);
         uint32_t reg = 0;
         if (r + 4 <= n) {
@@ -2341,7 +2342,7 @@ __global__ __launch_bounds__(kBlock) void k_slice_bucket(const uint32_t* __restr
     }
     __syncthreads();
     const unsigned int total = lbase[nslices];
-    for (unsigned int i = t; i < total; i += kBlock) {
+    for (unsigned int i = t; i < total; i += kBucketThreads) {
         const uint32_t c = stage[i];
         const uint32_t sl = c >> slice_log2;
         if (cnt[sl] <= (unsigned int)kSegCap) segs[((int64_t)sl * nbuckets + blockIdx.x) * kSegCap + (i - lbase[sl])] = c;
@@ -2442,7 +2443,7 @@ int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bi
             // chunks of all rows were read once per slice: 16x at L = 12, from L2)
             segs = (const uint32_t*)((uint8_t*)temp + (int64_t)chunks * words * 8);
             seglen = (uint32_t*)((uint8_t*)segs + (int64_t)kMaxSlices * nb * kSegCap * 4);
-            hipLaunchKernelGGL(k_slice_bucket, dim3((unsigned)nb), dim3(kBlock), 0, s, codes, regular_bits, n, slog,
+            hipLaunchKernelGGL(k_slice_bucket, dim3((unsigned)nb), dim3(kBucketThreads), 0, s, codes, regular_bits, n, slog,
                                slices, (uint32_t*)segs, seglen, nb);
         }
         hipLaunchKernelGGL(k_slice_mark, dim3((unsigned)(slices * chunks)), dim3(kSliceBlock), 0, s, codes, regular_bits,
