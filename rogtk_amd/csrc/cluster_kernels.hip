@@ -2173,7 +2173,7 @@ constexpr int kSliceBlock = 1024;
 constexpr int kSliceChunks = 16;   // a multiple of the 8 XCDs
 constexpr int kSliceLog2 = 20;     // codes per slice (LDS bits)
 constexpr int kMaxSlices = 16;     // 4^12 / 2^20
-constexpr int kBucketRows = 8192;  // rows per segment workgroup (32 per lane)
+constexpr int kBucketRows = 8192;  // rows per segment workgroup (8 per lane)
 constexpr int kSegCap = 2048;      // codes per (slice, workgroup) segment: 4x the mean share at 16 slices
 
 // Segment mode (segs != nullptr, written by k_slice_bucket): workgroup (s, c) reads only
