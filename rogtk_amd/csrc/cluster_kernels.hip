@@ -759,15 +759,38 @@ __global__ __launch_bounds__(kBlock) void k_hook_g(const uint4* __restrict__ RT,
             }
             uint32_t x[4];
             if (all_uniform) {
+                // whole words: the word pairs that share a bit link them; hook every root
+                // to the smallest root of its connected group of words (<= 3 hooks instead
+                // of one per linked pair: dense spaces link all 6 pairs of most groups)
+                uint32_t adj[4];
 #pragma unroll
-                for (int a = 0; a < 4; ++a)
+                for (int a = 0; a < 4; ++a) {
+                    adj[a] = 1u << a;
 #pragma unroll
-                    for (int b = a + 1; b < 4; ++b)
-                        if (m[a] & m[b]) {
-                            x[0] = root[a];
-                            x[1] = root[b];
-                            crossed |= hook_roots(T, f, x, 2, last_x, last_mn);
-                        }
+                    for (int b = 0; b < 4; ++b)
+                        if (b != a && (m[a] & m[b])) adj[a] |= 1u << b;
+                }
+#pragma unroll
+                for (int it = 0; it < 2; ++it)  // closure: 4 nodes, diameter <= 3
+#pragma unroll
+                    for (int a = 0; a < 4; ++a) {
+                        uint32_t r = adj[a];
+#pragma unroll
+                        for (int b = 0; b < 4; ++b)
+                            if ((adj[a] >> b) & 1u) r |= adj[b];
+                        adj[a] = r;
+                    }
+#pragma unroll
+                for (int a = 0; a < 4; ++a) {
+                    if (adj[a] == (1u << a)) continue;  // shares no bit with another word
+                    uint32_t mn = root[a];
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        if ((adj[a] >> b) & 1u) mn = root[b] < mn ? root[b] : mn;
+                    x[0] = root[a];
+                    x[1] = mn;
+                    crossed |= hook_roots(T, f, x, 2, last_x, last_mn);
+                }
             } else {
                 uint64_t mm = multi;
                 while (mm) {
