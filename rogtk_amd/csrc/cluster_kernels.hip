@@ -494,11 +494,32 @@ __global__ __launch_bounds__(TW) void k_local_cc(const uint4* __restrict__ RT, i
                 all_one &= wv[v].one || wv[v].m == 0;
             }
             if (all_one) {
+                // each word is one component: unite every word with the first word of its
+                // linked group (<= 3 unites instead of one per linked pair; a dense tile
+                // links all 6 pairs of most groups)
+                uint32_t adj[4];
 #pragma unroll
-                for (int x = 0; x < 3; ++x)
+                for (int a = 0; a < 4; ++a) {
+                    adj[a] = 1u << a;
 #pragma unroll
-                    for (int y = x + 1; y < 4; ++y)
-                        if (wv[x].m & wv[y].m) lunite(lf, lp[x], lp[y]);  // first code = rank lp
+                    for (int b = 0; b < 4; ++b)
+                        if (b != a && (wv[a].m & wv[b].m)) adj[a] |= 1u << b;
+                }
+#pragma unroll
+                for (int it = 0; it < 2; ++it)  // closure: 4 nodes, diameter <= 3
+#pragma unroll
+                    for (int a = 0; a < 4; ++a) {
+                        uint32_t r = adj[a];
+#pragma unroll
+                        for (int b = 0; b < 4; ++b)
+                            if ((adj[a] >> b) & 1u) r |= adj[b];
+                        adj[a] = r;
+                    }
+#pragma unroll
+                for (int a = 1; a < 4; ++a) {
+                    const int lead = __ffs((int)adj[a]) - 1;
+                    if (lead != a) lunite(lf, lp[lead], lp[a]);  // first code = rank lp
+                }
             } else {
 #pragma unroll
                 for (int x = 0; x < 3; ++x) {
