@@ -384,11 +384,6 @@ __device__ __forceinline__ uint64_t comps_any(const WordComps& w, uint64_t seed,
     return r | (seed & ~covered);
 }
 
-// Sparse code space: under 1/8 of the codes present. Then local_cc also writes D
-// (index -> code) and labels are assigned per index; dense spaces label per code.
-__device__ __forceinline__ bool is_sparse(const unsigned long long* stats, int64_t words) {
-    return stats[S_NDISTINCT] * 8 < (unsigned long long)words * 64;
-}
 
 // The union-find runs over LOCAL RANKS (index - gbase) of the present codes, not over
 // local codes: a tile of nloc present codes needs nloc LDS slots. Instances:
@@ -412,7 +407,6 @@ __global__ __launch_bounds__(TW) void k_local_cc(const uint4* __restrict__ RT, i
                                                  unsigned long long* __restrict__ stats) {
     constexpr int kLrb = CAP / 64 + 2;
     if (((int)stats[S_P0] == 8 ? 8 : 7) != LP) return;  // the other tiling
-    const bool sparse = is_sparse(stats, words);
     __shared__ uint64_t wb[TW];
     __shared__ uint64_t wcm[kWordComps][TW];  // listed component masks per word
     __shared__ uint32_t lpre[TW];
@@ -568,8 +562,8 @@ __global__ __launch_bounds__(TW) void k_local_cc(const uint4* __restrict__ RT, i
     // 3b. outputs of word t, per in-word component (lf[first] is now the final root):
     //     UR = the word's shared local root (global index) or kNone, the live bits,
     //     f[local root] = itself, f[i] = its local root for the codes of words without
-    //     a shared root (the only ones the rounds read by code), and in a sparse code
-    //     space (kSparse) D[i] = code for every code, so that labels run over indices
+    //     a shared root (the only ones the rounds read by code). (No index -> code table:
+    //     the labels run per word, k_word_label.)
     if (t == 0 && (int64_t)gbase + nloc > max_distinct) stats[S_OVERFLOW] = 1;
     if (t < nw) {
         uint32_t first = kNone;
@@ -615,16 +609,6 @@ __global__ __launch_bounds__(TW) void k_local_cc(const uint4* __restrict__ RT, i
             }
         }
         UR[base + t] = (m && uniform) ? first : kNone;
-        if (sparse) {
-            uint64_t mm = m;
-            uint32_t i = gbase + ex;
-            while (mm) {
-                const int b = __ffsll((long long)mm) - 1;
-                mm &= mm - 1;
-                if ((int64_t)i < max_distinct) D[i] = (uint32_t)((base + t) * 64 + b);
-                ++i;
-            }
-        }
     }
     __syncthreads();
     // index-space live words: the block owns the interior words of its range; the
