@@ -360,12 +360,14 @@ constexpr int kLdsBlock = 512;  // 8 waves per group workgroup (16 per CU for cl
 // Two size classes: class 1 (<= 2048 observations, ~78 KB LDS, 2 workgroups per CU)
 // and class 2 (<= 4096 observations, ~155 KB, 1 per CU). Larger groups take the
 // global radix-sort path.
+// Class 3 (<= 1536 observations, 2048 slots, load factor <= 0.75, ~46 KB: 3 workgroups
+// per CU) takes the typical C3 group (~10 reads of 119 k-mers) first.
 template <int CLS>
 struct LdsCfg {
-    static constexpr int kObs = CLS == 1 ? 2048 : 4096;
-    static constexpr int kSlots = 2 * kObs;                  // power of two, load factor <= 0.5
-    static constexpr int kRows = CLS == 1 ? 256 : 512;       // rows of one group
-    static constexpr int kWords = CLS == 1 ? 768 : 1536;     // packed words of one group
+    static constexpr int kObs = CLS == 3 ? 1536 : CLS == 1 ? 2048 : 4096;
+    static constexpr int kSlots = CLS == 3 ? 2048 : 2 * kObs;  // power of two
+    static constexpr int kRows = CLS == 3 ? 192 : CLS == 1 ? 256 : 512;    // rows of one group
+    static constexpr int kWords = CLS == 3 ? 576 : CLS == 1 ? 768 : 1536;  // packed words of one group
     // insert phase (packed words + row metadata) and sort phase (valid entries) share LDS
     static constexpr int kUnionWords = (kObs * 12 + 7) / 8;
     static_assert((kWords + 1) * 8 + kRows * 12 <= kUnionWords * 8, "LDS union too small");
@@ -675,7 +677,8 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
         if (lane == 0) {
             uint8_t cls = 0;
             if (K <= 32 && obs > 0) {
-                if (obs <= LdsCfg<1>::kObs && nrows <= LdsCfg<1>::kRows && words <= LdsCfg<1>::kWords) cls = 1;
+                if (obs <= LdsCfg<3>::kObs && nrows <= LdsCfg<3>::kRows && words <= LdsCfg<3>::kWords) cls = 3;
+                else if (obs <= LdsCfg<1>::kObs && nrows <= LdsCfg<1>::kRows && words <= LdsCfg<1>::kWords) cls = 1;
                 else if (obs <= LdsCfg<2>::kObs && nrows <= LdsCfg<2>::kRows && words <= LdsCfg<2>::kWords) cls = 2;
             }
             gsmall[g] = cls;
@@ -892,6 +895,11 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
         hipLaunchKernelGGL(k_group_classify, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, go, G, in.gk, K,
                            c->row_obs.as<int64_t>(), c->row_words.as<int64_t>(), c->woff.as<int64_t>(),
                            c->gsmall.as<uint8_t>(), c->gdesc.as<GroupDesc>());
+        hipLaunchKernelGGL((k_kmer_lds<3, kLdsBlock>), dim3((unsigned)std::min<int64_t>(G, 65536)), dim3(kLdsBlock), 0, s,
+                           c->gdesc.as<GroupDesc>(), G,
+                           c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
+                           c->woff.as<int64_t>(), c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
+                           c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
         hipLaunchKernelGGL((k_kmer_lds<1, kLdsBlock>), dim3((unsigned)std::min<int64_t>(G, 65536)), dim3(kLdsBlock), 0, s,
                            c->gdesc.as<GroupDesc>(), G,
                            c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
