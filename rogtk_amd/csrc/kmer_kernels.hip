@@ -374,6 +374,13 @@ struct LdsCfg {
 };
 constexpr unsigned long long kEmpty = ~0ull;
 
+#ifdef ROGTK_KMER_TIMING  // experiment builds only: per-phase clocks of k_kmer_lds (thread 0)
+__device__ unsigned long long g_kmer_clk[8];
+#define KT(k) do { if (tid == 0) { const unsigned long long now_ = wall_clock64(); kt_acc[k] += now_ - kt_last; kt_last = now_; } } while (0)
+#else
+#define KT(k) do { } while (0)
+#endif
+
 __device__ __forceinline__ uint32_t pk_base(const uint64_t* pk, int64_t p) {
     return (uint32_t)(pk[p >> 5] >> (62 - 2 * (p & 31))) & 3u;
 }
@@ -422,6 +429,9 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
         tinfo[i] = 0;
     }
     if (tid == 0) s_claimed = 0;
+#ifdef ROGTK_KMER_TIMING
+    unsigned long long kt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, kt_last = wall_clock64();
+#endif
     // the next group's class and descriptor are loaded while the current one is
     // processed (one exposed round trip per group: its rows' lengths, offsets, words)
     int64_t g_next = blockIdx.x;
@@ -437,6 +447,7 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
             d_next = gdesc[g_next];
         }
         if (cls != CLS) continue;  // uniform per block
+        KT(0);
         const int64_t r0 = d.r0, w0 = d.w0;
         const int nrows = d.nrows, nwords = d.nwords;  // within LdsCfg<CLS> (classification)
         for (int i = tid; i < nrows; i += TB) {
@@ -452,6 +463,7 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
             s_iso = 0;
         }
         __syncthreads();
+        KT(1);
         // every k-mer observation of the group, straight from the packed words in LDS
         for (int ri = wave; ri < nrows; ri += kWaves) {
             const int nobs = m_nobs[ri];
@@ -482,6 +494,7 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
             }
         }
         __syncthreads();
+        KT(2);
         // CountFilter + compaction over the claimed slots: wave-shuffle scan, one
         // barrier for the per-wave totals
         const uint32_t ncl = s_claimed;
@@ -492,19 +505,41 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
             const uint32_t c = tinfo[claimed[i]] & 0xFFFFFFu;
             if ((int64_t)min(c, 0xFFFFu) >= min_cov) ++mine;
         }
-        uint32_t incl = mine;
+        uint32_t incl = 0;
+        if (__ballot(mine != 0)) {  // most waves (and most groups, at the usual coverage floors) pass nothing
+            incl = mine;
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t v = __shfl_up(incl, off);
-            if (lane >= off) incl += v;
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t v = __shfl_up(incl, off);
+                if (lane >= off) incl += v;
+            }
         }
         if (lane == 63) scan[wave] = incl;
         __syncthreads();
+        KT(3);
         uint32_t wbase = 0, nv = 0;
 #pragma unroll
         for (int w2 = 0; w2 < kWaves; ++w2) {
             if (w2 < wave) wbase += scan[w2];
             nv += scan[w2];
+        }
+        if (nv == 0) {
+            // nothing passed CountFilter: reset the touched slots and record the empty
+            // group, no compaction, sort or further barrier (the next group's first
+            // barrier orders these resets before its inserts)
+            for (uint32_t i = tid; i < ncl; i += TB) {
+                const uint32_t sl = claimed[i];
+                tkey[sl] = kEmpty;
+                tinfo[sl] = 0;
+            }
+            if (tid == 0) {
+                gcount[g] = 0;
+                gstat[5 * g + 3] = 0;
+                gstat[5 * g + 4] = 0;
+                s_claimed = 0;
+            }
+            KT(5);
+            continue;
         }
         uint32_t w = wbase + incl - mine;
         for (uint32_t i = c0; i < c1; ++i) {
@@ -518,6 +553,7 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
             }
         }
         __syncthreads();
+        KT(4);
         // reset the touched slots for the next group (the table is not read again here)
         for (uint32_t i = tid; i < ncl; i += TB) {
             const uint32_t sl = claimed[i];
@@ -531,8 +567,11 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
             if (wave == 0) {
                 uint64_t key = lane < (int)nv ? vkey[lane] : kEmpty;
                 uint32_t info = lane < (int)nv ? vinfo[lane] : (1u << 31);
+                // bitonic over the first P lanes only (P = nv rounded up to a power of
+                // two): the last merge leaves lanes 0..P-1 ascending, pads last
 #pragma unroll
                 for (int k2 = 2; k2 <= 64; k2 <<= 1) {
+                    if (k2 >= 2 * (int)nv && k2 > 2) break;
 #pragma unroll
                     for (int j = k2 >> 1; j > 0; j >>= 1) {
                         const uint64_t ok = __shfl_xor(key, j);
@@ -584,6 +623,7 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
                 }
             }
             __syncthreads();
+            KT(5);
             continue;
         }
         uint32_t P = 2;
@@ -647,7 +687,13 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
             s_claimed = 0;
         }
         __syncthreads();
+        KT(6);
     }
+#ifdef ROGTK_KMER_TIMING
+    KT(7);
+    if (tid == 0)
+        for (int k = 0; k < 8; ++k) atomicAdd(&g_kmer_clk[k], kt_acc[k]);
+#endif
 }
 
 // Per group of effective k K: observation, row and packed-word totals decide the path.
@@ -1044,6 +1090,16 @@ int rogtk_kmer_set_path(int lds_small_groups) {
     c->lds_path = lds_small_groups != 0;
     return ROGTK_OK;
 }
+
+#ifdef ROGTK_KMER_TIMING
+// experiment builds only: reads and clears the per-phase clocks (100 MHz ticks summed over workgroups)
+extern "C" int rogtk_kmer_timing(unsigned long long* out8) {
+    hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_kmer_clk), 8 * sizeof(unsigned long long));
+    unsigned long long z[8] = {0};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_kmer_clk), z, sizeof(z));
+    return ROGTK_OK;
+}
+#endif
 
 int rogtk_kmer_path_stats(int64_t* out2) {
     ROGTK_REQUIRE(out2, ROGTK_E_INVALID, "kmer_path_stats: NULL");

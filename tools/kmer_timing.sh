@@ -1,0 +1,6 @@
+#!/bin/bash
+# GPU box: swap in the ROGTK_KMER_TIMING library (box copy only) and print k_kmer_lds's phase split.
+set -eu
+cd "$GRAFT_REPO_ROOT"
+cp tools/kt/librogtk_hip.so rogtk_amd/librogtk_hip.so
+timeout -k 10 180 python3 tools/kmer_timing.py
