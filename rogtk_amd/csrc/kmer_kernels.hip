@@ -432,21 +432,20 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
 #ifdef ROGTK_KMER_TIMING
     unsigned long long kt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, kt_last = wall_clock64();
 #endif
-    // the next group's class and descriptor are loaded while the current one is
-    // processed (one exposed round trip per group: its rows' lengths, offsets, words)
-    int64_t g_next = blockIdx.x;
-    uint8_t cls_next = g_next < G ? gsmall[g_next] : 0;
-    GroupDesc d_next = g_next < G ? gdesc[g_next] : GroupDesc{0, 0, 0, 0};
-    while (g_next < G) {
-        const int64_t g = g_next;
-        const uint8_t cls = cls_next;
-        const GroupDesc d = d_next;
-        g_next += gridDim.x;
-        if (g_next < G) {
-            cls_next = gsmall[g_next];
-            d_next = gdesc[g_next];
-        }
-        if (cls != CLS) continue;  // uniform per block
+    // Groups are taken in chunks of 64 consecutive ids: one coalesced load of their
+    // classes and a ballot give this class's groups of the chunk, so the instances of
+    // the rarer classes skip 64 groups per load. Within a chunk the next group's
+    // descriptor is loaded while the current group is processed (one exposed round
+    // trip per group: its rows' lengths, offsets, words).
+    const int64_t n_chunks = (G + 63) >> 6;
+    for (int64_t ch = blockIdx.x; ch < n_chunks; ch += gridDim.x) {
+    const int64_t g0 = ch << 6;
+    uint64_t own = __ballot(g0 + lane < G && gsmall[g0 + lane] == CLS);
+    GroupDesc d_next = own ? gdesc[g0 + __ffsll((unsigned long long)own) - 1] : GroupDesc{0, 0, 0, 0};
+    for (GroupDesc d = d_next; own; d = d_next) {
+        const int64_t g = g0 + __ffsll((unsigned long long)own) - 1;
+        own &= own - 1;
+        if (own) d_next = gdesc[g0 + __ffsll((unsigned long long)own) - 1];
         KT(0);
         const int64_t r0 = d.r0, w0 = d.w0;
         const int nrows = d.nrows, nwords = d.nwords;  // within LdsCfg<CLS> (classification)
@@ -688,6 +687,7 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
         }
         __syncthreads();
         KT(6);
+    }
     }
 #ifdef ROGTK_KMER_TIMING
     KT(7);
@@ -941,17 +941,17 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
         hipLaunchKernelGGL(k_group_classify, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, go, G, in.gk, K,
                            c->row_obs.as<int64_t>(), c->row_words.as<int64_t>(), c->woff.as<int64_t>(),
                            c->gsmall.as<uint8_t>(), c->gdesc.as<GroupDesc>());
-        hipLaunchKernelGGL((k_kmer_lds<3, kLdsBlock>), dim3((unsigned)std::min<int64_t>(G, 65536)), dim3(kLdsBlock), 0, s,
+        hipLaunchKernelGGL((k_kmer_lds<3, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)), dim3(kLdsBlock), 0, s,
                            c->gdesc.as<GroupDesc>(), G,
                            c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
                            c->woff.as<int64_t>(), c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
                            c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
-        hipLaunchKernelGGL((k_kmer_lds<1, kLdsBlock>), dim3((unsigned)std::min<int64_t>(G, 65536)), dim3(kLdsBlock), 0, s,
+        hipLaunchKernelGGL((k_kmer_lds<1, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)), dim3(kLdsBlock), 0, s,
                            c->gdesc.as<GroupDesc>(), G,
                            c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
                            c->woff.as<int64_t>(), c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
                            c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
-        hipLaunchKernelGGL((k_kmer_lds<2, kLdsBlock>), dim3((unsigned)std::min<int64_t>(G, 8192)), dim3(kLdsBlock), 0, s,
+        hipLaunchKernelGGL((k_kmer_lds<2, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 8192)), dim3(kLdsBlock), 0, s,
                            c->gdesc.as<GroupDesc>(), G,
                            c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
                            c->woff.as<int64_t>(), c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
