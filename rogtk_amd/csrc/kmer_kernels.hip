@@ -79,9 +79,39 @@ __global__ __launch_bounds__(kBlock) void k_row_meta(const void* offsets, const 
     }
 }
 
-// One wave per grouped row, bytes loaded once: the ACGT check of fracture.rs:217-229
-// (ballot), the observation count, n_sequences, and the packed 2-bit staging
-// (packed[woff[r] ..], base j in word j / 32 at bits 62 - 2 (j % 32)).
+// 32 bits -> 64: bit i of x moves to bit 2i
+__device__ __forceinline__ uint64_t spread2(uint32_t x) {
+    uint64_t v = x;
+    v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+    v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+    v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    v = (v | (v << 2)) & 0x3333333333333333ull;
+    v = (v | (v << 1)) & 0x5555555555555555ull;
+    return v;
+}
+
+// 64 bases of one row, one byte per lane (base j0 + lane): the ACGT check and the 2-bit
+// pack by two ballots (base j at bits 62 - 2 (j % 32) of word j / 32, first base most
+// significant; bytes past the row end pack as 0). Returns this lane's "bad byte".
+__device__ __forceinline__ bool stage_chunk(uint8_t c, int64_t j0, int64_t len, int lane, uint64_t* out) {
+    const bool in = j0 + lane < len;
+    const uint32_t b = in ? base2(c) : 0u;
+    const uint64_t lo = __ballot(b & 1u), hi = __ballot(b & 2u);
+    if (lane < 2) {
+        const int64_t w = (j0 >> 5) + lane;
+        const uint32_t l32 = (uint32_t)(lo >> (32 * lane)), h32 = (uint32_t)(hi >> (32 * lane));
+        if (w * 32 < len)
+            out[w] = (spread2(__builtin_bitreverse32(h32)) << 1) | spread2(__builtin_bitreverse32(l32));
+    }
+    return in && !acgt(c);
+}
+
+// One wave per 64 grouped rows: every row's metadata in one coalesced load (a lane per
+// row), then the rows' bytes kRowBatch rows at a time (their first 256 bytes in flight
+// together), loaded once: the ACGT check of fracture.rs:217-229 (ballot), the 2-bit
+// staging (packed[woff[r] ..], base j in word j / 32 at bits 62 - 2 (j % 32)), and, a
+// lane per row again, the observation counts and n_sequences (one atomic per run of
+// same-group rows).
 __global__ __launch_bounds__(kBlock) void k_row_stage(const uint8_t* __restrict__ values, int64_t n_rows, int K,
                                                       const uint32_t* __restrict__ row_group,
                                                       const int64_t* __restrict__ row_st,
@@ -90,45 +120,62 @@ __global__ __launch_bounds__(kBlock) void k_row_stage(const uint8_t* __restrict_
                                                       uint64_t* __restrict__ packed,
                                                       int64_t* __restrict__ row_obs, int32_t* __restrict__ row_len,
                                                       unsigned long long* __restrict__ gstat) {
+    constexpr int kRowBatch = 4;
     const int lane = threadIdx.x & 63;
     const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
-    for (int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); r < n_rows; r += waves) {
-        const int64_t len = raw_len[r];
-        if (len < 0) {
-            if (lane == 0) {
-                row_obs[r] = 0;
-                row_len[r] = 0;
+    for (int64_t rb = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 64; rb < n_rows;
+         rb += waves * 64) {
+        const int64_t r = rb + lane;
+        const bool live = r < n_rows;
+        const int32_t my_len = live ? raw_len[r] : -1;
+        const int64_t my_st = live ? row_st[r] : 0, my_wo = live ? woff[r] : 0;
+        const uint32_t my_g = live ? row_group[r] : 0u;
+        const int nq = (int)min<int64_t>(64, n_rows - rb);
+        uint64_t okbits = 0;  // rows of this trip that pass the ACGT check
+        for (int q0 = 0; q0 < nq; q0 += kRowBatch) {
+            int64_t L[kRowBatch], S[kRowBatch];
+            uint8_t cb[kRowBatch][4];
+#pragma unroll
+            for (int k = 0; k < kRowBatch; ++k) {
+                const int q = min(q0 + k, nq - 1);
+                L[k] = q0 + k < nq ? __shfl(my_len, q) : -1;
+                S[k] = __shfl(my_st, q);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int64_t j = (int64_t)u * 64 + lane;
+                    cb[k][u] = j < L[k] ? values[S[k] + j] : (uint8_t)'A';
+                }
             }
-            continue;
+#pragma unroll
+            for (int k = 0; k < kRowBatch; ++k) {
+                if (L[k] < 0) continue;  // past the trip, or no part in this call
+                uint64_t* out = packed + __shfl(my_wo, q0 + k);
+                bool bad = false;
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if ((int64_t)u * 64 < L[k]) bad |= stage_chunk(cb[k][u], (int64_t)u * 64, L[k], lane, out);
+                for (int64_t j0 = 256; j0 < L[k]; j0 += 64) {  // rows longer than 256 bases
+                    const uint8_t c = j0 + lane < L[k] ? values[S[k] + j0 + lane] : (uint8_t)'A';
+                    bad |= stage_chunk(c, j0, L[k], lane, out);
+                }
+                if (__ballot(bad) == 0) okbits |= 1ull << (q0 + k);
+            }
         }
-        const int64_t st = row_st[r];
-        const int iters = (int)((len + 63) >> 6);
-        uint64_t* out = packed + woff[r];
-        bool bad = false;
-        for (int it0 = 0; it0 < iters; it0 += 4) {
-            uint8_t cb[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int64_t j = (int64_t)(it0 + u) * 64 + lane;
-                cb[u] = j < len ? values[st + j] : (uint8_t)'A';
+        if (live) {
+            const bool ok = my_len >= 0 && ((okbits >> lane) & 1ull);
+            const bool use = ok && my_len >= K;
+            row_obs[r] = use ? my_len - K + 1 : 0;
+            row_len[r] = use ? my_len : 0;
+            // n_sequences: the first lane of each run of same-group rows adds the run's ok rows
+            const uint32_t g_prev = __shfl_up(my_g, 1);
+            const uint64_t heads = __ballot(lane == 0 || my_g != g_prev);
+            const uint64_t oks = __ballot(ok);
+            if ((heads >> lane) & 1ull) {
+                const uint64_t above = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
+                const uint64_t run = (above ? (above & (0ull - above)) - 1ull : ~0ull) & (~0ull << lane);
+                const int cnt = __popcll(oks & run);
+                if (cnt) atomicAdd(gstat + 5 * (int64_t)my_g + 1, (unsigned long long)cnt);
             }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                if (it0 + u >= iters) break;
-                bad |= !acgt(cb[u]);
-                uint64_t v = (uint64_t)base2(cb[u]) << (62 - 2 * (lane & 31));
-#pragma unroll
-                for (int m = 1; m < 32; m <<= 1) v |= __shfl_xor(v, m);
-                const int64_t w = 2 * (int64_t)(it0 + u) + (lane >> 5);
-                if ((lane & 31) == 0 && w * 32 < len) out[w] = v;
-            }
-        }
-        const bool ok = __ballot(bad) == 0;
-        if (lane == 0) {
-            const bool use = ok && len >= K;
-            row_obs[r] = use ? len - K + 1 : 0;
-            row_len[r] = use ? (int32_t)len : 0;
-            if (ok) atomicAdd(gstat + 5 * row_group[r] + 1, 1ull);  // n_sequences
         }
     }
 }
