@@ -484,31 +484,71 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
     // the rarer classes skip 64 groups per load. Within a chunk the next group's
     // descriptor is loaded while the current group is processed (one exposed round
     // trip per group: its rows' lengths, offsets, words).
+    // Within a chunk, the next group's rows (lengths, word offsets, packed words) are
+    // loaded into registers while the current group is processed, and the descriptor
+    // of the group after it as well, so a group's HBM round trips overlap the previous
+    // group's work; only a chunk's first group waits for its rows.
+    constexpr int kWPT = (kLdsWords + TB - 1) / TB;  // packed words per thread
+    static_assert(kLdsRows <= TB, "one row per thread");
+    int32_t p_len = 0, p_w = 0;
+    uint64_t p_words[kWPT];
+    auto load_rows = [&](const GroupDesc& dd) {
+        if (tid < dd.nrows) {
+            p_len = row_len[dd.r0 + tid];
+            p_w = (int32_t)(woff[dd.r0 + tid] - dd.w0);
+        }
+#pragma unroll
+        for (int j = 0; j < kWPT; ++j) {
+            const int i = tid + j * TB;
+            p_words[j] = i < dd.nwords ? packed[dd.w0 + i] : 0;
+        }
+    };
     const int64_t n_chunks = (G + 63) >> 6;
     for (int64_t ch = blockIdx.x; ch < n_chunks; ch += gridDim.x) {
     const int64_t g0 = ch << 6;
     uint64_t own = __ballot(g0 + lane < G && gsmall[g0 + lane] == CLS);
-    GroupDesc d_next = own ? gdesc[g0 + __ffsll((unsigned long long)own) - 1] : GroupDesc{0, 0, 0, 0};
-    for (GroupDesc d = d_next; own; d = d_next) {
-        const int64_t g = g0 + __ffsll((unsigned long long)own) - 1;
-        own &= own - 1;
-        if (own) d_next = gdesc[g0 + __ffsll((unsigned long long)own) - 1];
+    if (!own) continue;
+    int i0 = __ffsll((unsigned long long)own) - 1;
+    own &= own - 1;
+    GroupDesc d = gdesc[g0 + i0];
+    GroupDesc d1 = own ? gdesc[g0 + __ffsll((unsigned long long)own) - 1] : GroupDesc{0, 0, 0, 0};
+    GroupDesc d2{0, 0, 0, 0};
+    load_rows(d);
+    bool more = true;
+    int i1 = -1;
+    uint64_t own2 = 0;
+    auto advance = [&]() {
+        if (i1 < 0) return false;
+        i0 = i1;
+        own = own2;
+        d = d1;
+        d1 = d2;
+        return true;
+    };
+    for (; more; more = advance()) {
+        const int64_t g = g0 + i0;
         KT(0);
-        const int64_t r0 = d.r0, w0 = d.w0;
         const int nrows = d.nrows, nwords = d.nwords;  // within LdsCfg<CLS> (classification)
-        for (int i = tid; i < nrows; i += TB) {
-            const int32_t len = row_len[r0 + i];
-            m_len[i] = len;
-            m_nobs[i] = len ? len - K + 1 : 0;
-            m_w[i] = (int32_t)(woff[r0 + i] - w0);
+        if (tid < nrows) {
+            m_len[tid] = p_len;
+            m_nobs[tid] = p_len ? p_len - K + 1 : 0;
+            m_w[tid] = p_w;
         }
-        for (int i = tid; i < nwords; i += TB) words[i] = packed[w0 + i];
+#pragma unroll
+        for (int j = 0; j < kWPT; ++j) {
+            const int i = tid + j * TB;
+            if (i < nwords) words[i] = p_words[j];
+        }
         if (tid == 0) {
             words[nwords] = 0;
             s_term = 0;
             s_iso = 0;
         }
         __syncthreads();
+        i1 = own ? __ffsll((unsigned long long)own) - 1 : -1;
+        own2 = own & (own - 1);
+        if (i1 >= 0) load_rows(d1);  // in flight while this group is processed
+        if (own2) d2 = gdesc[g0 + __ffsll((unsigned long long)own2) - 1];
         KT(1);
         // every k-mer observation of the group, straight from the packed words in LDS
         for (int ri = wave; ri < nrows; ri += kWaves) {
