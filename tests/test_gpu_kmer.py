@@ -123,6 +123,28 @@ def test_many_groups_mixed(rg):
     _check(rg, items, 0, 2, auto_k=True, group_offsets=go)
 
 
+def test_long_rows_and_chunk_edges(rg):
+    """Rows of 193..700 bases (the staging kernel's 4th 64-base chunk and its tail loop
+    past 256 bases, with a bad byte past 256 dropping a row), and group counts around
+    the LDS path's 64-group chunks (63, 64, 65, 130 groups: partial last chunks, chunks
+    whose groups are all of one class or of none)."""
+    rng = np.random.default_rng(21)
+    for n_groups in (63, 64, 65, 130):
+        items, go = [], [0]
+        for g in range(n_groups):
+            tpl = _reads(rng, 1, 800, 800)[0]
+            m = int(rng.integers(0, 12)) if g % 7 else int(rng.integers(25, 40))
+            for _ in range(m):
+                a = int(rng.integers(0, 90))
+                r = bytearray(tpl[a:a + int(rng.integers(193, 701))])
+                if len(r) > 258 and rng.random() < 0.05:
+                    r[int(rng.integers(257, len(r)))] = ord("N")  # past the first 256 bases
+                items.append(bytes(r))
+            go.append(len(items))
+        for k, mc in ((17, 2), (31, 1)):
+            _check(rg, items, k, mc, group_offsets=go)
+
+
 def test_saturating_count(rg):
     """> 65535 observations of one k-mer: the count saturates at u16::MAX (CountFilter)."""
     items = [b"A" * 80] * 1200  # 77 observations of AAAA..(k=4) per row -> 92,400
