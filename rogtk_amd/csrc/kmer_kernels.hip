@@ -409,15 +409,23 @@ constexpr int kLdsBlock = 512;  // 8 waves per group workgroup (16 per CU for cl
 // global radix-sort path.
 // Class 3 (<= 1536 observations, 2048 slots, load factor <= 0.75, ~46 KB: 3 workgroups
 // per CU) takes the typical C3 group (~10 reads of 119 k-mers) first.
+// Class 4 (round 2): groups above class 2 with <= 512 rows and <= 4096 packed words,
+// any number of observations: the 8192-slot table takes up to kClaim distinct k-mers
+// and the sort buffer up to kObs valid ones (~150 KB, 1 workgroup per CU). A group
+// that exceeds either is handed to the global path (its class is reset to 0 before
+// k_drop_small_rows, which then keeps its rows), so the outputs never depend on it.
 template <int CLS>
 struct LdsCfg {
-    static constexpr int kObs = CLS == 3 ? 1536 : CLS == 1 ? 2048 : 4096;
-    static constexpr int kSlots = CLS == 3 ? 2048 : 2 * kObs;  // power of two
+    static constexpr int kObs = CLS == 3 ? 1536 : CLS == 1 ? 2048 : CLS == 2 ? 4096 : 3072;
+    static constexpr int kSlots = CLS == 3 ? 2048 : CLS == 4 ? 8192 : 2 * kObs;  // power of two
+    static constexpr int kClaim = CLS == 4 ? 6144 : kObs;  // distinct k-mers (claimed slots)
     static constexpr int kRows = CLS == 3 ? 192 : CLS == 1 ? 256 : 512;    // rows of one group
-    static constexpr int kWords = CLS == 3 ? 576 : CLS == 1 ? 768 : 1536;  // packed words of one group
+    static constexpr int kWords = CLS == 3 ? 576 : CLS == 1 ? 768 : CLS == 2 ? 1536 : 4096;  // packed words
     // insert phase (packed words + row metadata) and sort phase (valid entries) share LDS
-    static constexpr int kUnionWords = (kObs * 12 + 7) / 8;
-    static_assert((kWords + 1) * 8 + kRows * 12 <= kUnionWords * 8, "LDS union too small");
+    static constexpr int kInsertWords = kWords + 1 + (kRows * 12 + 7) / 8;
+    static constexpr int kUnionWords = (kObs * 12 + 7) / 8 > kInsertWords ? (kObs * 12 + 7) / 8 : kInsertWords;
+    static_assert(CLS == 4 || kInsertWords <= (kObs * 12 + 7) / 8, "LDS union too small");
+    static_assert(kSlots - kClaim >= 512, "class 4: one in-flight insert per thread past the claim cap");
 };
 constexpr unsigned long long kEmpty = ~0ull;
 
@@ -445,7 +453,7 @@ struct GroupDesc {
 
 template <int CLS, int TB>
 __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ gdesc, int64_t G,
-                                                     const uint8_t* __restrict__ gsmall, int K, int64_t min_cov,
+                                                     uint8_t* __restrict__ gsmall, int K, int64_t min_cov,
                                                      const int32_t* __restrict__ row_len,
                                                      const int64_t* __restrict__ woff,
                                                      const uint64_t* __restrict__ packed,
@@ -458,7 +466,7 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
     constexpr int kLdsObs = C::kObs, kLdsSlots = C::kSlots, kLdsRows = C::kRows, kLdsWords = C::kWords;
     __shared__ unsigned long long tkey[kLdsSlots + 1];
     __shared__ uint32_t tinfo[kLdsSlots + 1];  // count (bits 0..23) | exts << 24
-    __shared__ uint16_t claimed[kLdsObs + 1];  // slots first touched by this group
+    __shared__ uint16_t claimed[C::kClaim + 1];  // slots first touched by this group
     __shared__ uint64_t ubuf[C::kUnionWords];
     uint64_t* const words = ubuf;                                      // the group's packed rows
     int32_t* const m_len = reinterpret_cast<int32_t*>(ubuf + kLdsWords + 1);
@@ -467,7 +475,7 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
     uint64_t* const vkey = ubuf;                                       // after the inserts
     uint32_t* const vinfo = reinterpret_cast<uint32_t*>(ubuf + kLdsObs);  // count | exts << 16 | pad << 31
     __shared__ uint32_t scan[kWaves];
-    __shared__ uint32_t s_claimed, s_term, s_iso;
+    __shared__ uint32_t s_claimed, s_term, s_iso, s_over;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int hbits = 31 - __clz(kLdsSlots);
     const uint64_t kmask = K == 32 ? ~0ull : ((1ull << (2 * K)) - 1ull);
@@ -475,16 +483,16 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
         tkey[i] = kEmpty;
         tinfo[i] = 0;
     }
-    if (tid == 0) s_claimed = 0;
+    if (tid == 0) {
+        s_claimed = 0;
+        s_over = 0;
+    }
 #ifdef ROGTK_KMER_TIMING
     unsigned long long kt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, kt_last = wall_clock64();
 #endif
     // Groups are taken in chunks of 64 consecutive ids: one coalesced load of their
     // classes and a ballot give this class's groups of the chunk, so the instances of
-    // the rarer classes skip 64 groups per load. Within a chunk the next group's
-    // descriptor is loaded while the current group is processed (one exposed round
-    // trip per group: its rows' lengths, offsets, words).
-    // Within a chunk, the next group's rows (lengths, word offsets, packed words) are
+    // the rarer classes skip 64 groups per load. Within a chunk, the next group's rows (lengths, word offsets, packed words) are
     // loaded into registers while the current group is processed, and the descriptor
     // of the group after it as well, so a group's HBM round trips overlap the previous
     // group's work; only a chunk's first group waits for its rows.
@@ -564,6 +572,7 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
                 uint32_t e = 0;
                 if (p > 0) e |= 1u << pk_base(rw, p - 1);
                 if (p + K < len) e |= 1u << (4 + pk_base(rw, p + K));
+                if (CLS == 4 && __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
                 uint32_t slot;
                 if (key == kEmpty) {
                     slot = kLdsSlots;
@@ -575,12 +584,34 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
                         slot = (slot + 1) & (kLdsSlots - 1);
                     }
                 }
-                if ((atomicAdd(&tinfo[slot], 1u) & 0xFFFFFFu) == 0) claimed[atomicAdd(&s_claimed, 1u)] = (uint16_t)slot;
+                if ((atomicAdd(&tinfo[slot], 1u) & 0xFFFFFFu) == 0) {
+                    const uint32_t ci = atomicAdd(&s_claimed, 1u);
+                    if (CLS != 4 || ci < (uint32_t)C::kClaim) claimed[ci] = (uint16_t)slot;
+                    else s_over = 1;  // more distinct k-mers than the table takes
+                }
                 if (e) atomicOr(&tinfo[slot], e << 24);
             }
         }
         __syncthreads();
         KT(2);
+        if (CLS == 4) {
+            const bool over = s_over;
+            __syncthreads();  // every thread has read the flag before it is cleared
+            if (over) {
+                // the claimed list is incomplete: clear the whole table; the group goes
+                // to the global path (the next group's first barrier orders the resets)
+                for (int i = tid; i <= kLdsSlots; i += TB) {
+                    tkey[i] = kEmpty;
+                    tinfo[i] = 0;
+                }
+                if (tid == 0) {
+                    gsmall[g] = 0;
+                    s_claimed = 0;
+                    s_over = 0;
+                }
+                continue;
+            }
+        }
         // CountFilter + compaction over the claimed slots: wave-shuffle scan, one
         // barrier for the per-wave totals
         const uint32_t ncl = s_claimed;
@@ -625,6 +656,19 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
                 s_claimed = 0;
             }
             KT(5);
+            continue;
+        }
+        if (CLS == 4 && nv > (uint32_t)kLdsObs) {
+            // more valid k-mers than the sort buffer takes: global path
+            for (uint32_t i = tid; i < ncl; i += TB) {
+                const uint32_t sl = claimed[i];
+                tkey[sl] = kEmpty;
+                tinfo[sl] = 0;
+            }
+            if (tid == 0) {
+                gsmall[g] = 0;
+                s_claimed = 0;
+            }
             continue;
         }
         uint32_t w = wbase + incl - mine;
@@ -813,6 +857,7 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
                 if (obs <= LdsCfg<3>::kObs && nrows <= LdsCfg<3>::kRows && words <= LdsCfg<3>::kWords) cls = 3;
                 else if (obs <= LdsCfg<1>::kObs && nrows <= LdsCfg<1>::kRows && words <= LdsCfg<1>::kWords) cls = 1;
                 else if (obs <= LdsCfg<2>::kObs && nrows <= LdsCfg<2>::kRows && words <= LdsCfg<2>::kWords) cls = 2;
+                else if (nrows <= LdsCfg<4>::kRows && words <= LdsCfg<4>::kWords) cls = 4;
             }
             gsmall[g] = cls;
             if (cls) gdesc[g] = GroupDesc{go[g], woff[go[g]], (int32_t)nrows, (int32_t)words};
@@ -1039,6 +1084,11 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
                            c->woff.as<int64_t>(), c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
                            c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
         hipLaunchKernelGGL((k_kmer_lds<2, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 8192)), dim3(kLdsBlock), 0, s,
+                           c->gdesc.as<GroupDesc>(), G,
+                           c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
+                           c->woff.as<int64_t>(), c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
+                           c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
+        hipLaunchKernelGGL((k_kmer_lds<4, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 8192)), dim3(kLdsBlock), 0, s,
                            c->gdesc.as<GroupDesc>(), G,
                            c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
                            c->woff.as<int64_t>(), c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),

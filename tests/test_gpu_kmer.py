@@ -87,14 +87,14 @@ def test_auto_k(rg):
 
 
 def test_many_groups_mixed(rg):
-    """Many groups, each one polars group: sizes 0..200 rows (small and medium ones take
-    the two LDS size classes, the largest the global path, all in the same call), mixed
-    validity and bytes."""
+    """Many groups, each one polars group: sizes 0..600 rows (small and medium ones take
+    the LDS size classes 3, 1, 2 and 4, groups of more than 512 rows the global path, all
+    in the same call), mixed validity and bytes."""
     rng = np.random.default_rng(11)
     items, go = [], [0]
     for g in range(300):
-        u = rng.random()  # LDS class 1 (<= 2048 obs), class 2 (<= 4096) and global-path groups
-        m = int(rng.integers(0, 40)) if u < 0.8 else int(rng.integers(60, 100)) if u < 0.9 else int(rng.integers(120, 200))
+        u = rng.random()  # LDS classes (<= 512 rows) and global-path groups (> 512 rows)
+        m = int(rng.integers(0, 40)) if u < 0.8 else int(rng.integers(60, 200)) if u < 0.9 else int(rng.integers(513, 600))
         tpl = _reads(rng, 1, 150, 150)[0]
         for _ in range(m):
             r = rng.random()
@@ -143,6 +143,31 @@ def test_long_rows_and_chunk_edges(rg):
             go.append(len(items))
         for k, mc in ((17, 2), (31, 1)):
             _check(rg, items, k, mc, group_offsets=go)
+
+
+def test_lds_class4_overflow(rg):
+    """Groups above class 2 (> 4096 observations, <= 512 rows): within class 4's table
+    and sort buffer they stay on the LDS path; more than 6144 distinct k-mers, or more
+    than 3072 valid ones, hand the group to the global path. Every case == the oracle."""
+    import ctypes
+
+    from rogtk_amd import _lib
+
+    rng = np.random.default_rng(8)
+    tpl = _reads(rng, 1, 400, 400)[0]
+    fits = [tpl[int(a):int(a) + 150] for a in rng.integers(0, 250, 60)]  # ~7k obs, few distinct
+    many_distinct = _reads(rng, 100, 150, 150)  # 11.9k distinct k-mers
+    many_valid = _reads(rng, 40, 150, 150)  # 4.8k distinct, all valid at min_cov 1
+    groups = [fits, many_distinct, many_valid, fits[:5]]
+    items = [x for grp in groups for x in grp]
+    go = np.r_[0, np.cumsum([len(grp) for grp in groups])].tolist()
+    for k, mc in ((17, 1), (31, 2), (21, 1)):
+        _check(rg, items, k, mc, group_offsets=go)
+        paths = (ctypes.c_int64 * 2)()
+        _lib.call("rogtk_kmer_path_stats", paths)
+        if _LAST_MODE[0] == 1:
+            # the distinct-overflow group always leaves; the valid-overflow one at min_cov 1
+            assert paths[1] == (2 if mc == 1 else 1) and paths[0] == 4 - paths[1], tuple(paths)
 
 
 def test_saturating_count(rg):
