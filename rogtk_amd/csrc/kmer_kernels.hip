@@ -395,32 +395,33 @@ __global__ __launch_bounds__(kBlock) void k_pack(const uint64_t* __restrict__ t_
 }
 
 // ----------------------------------------------------------- LDS fast path
-// One workgroup per small group (size class CLS: observations, rows and packed
-// words within LdsCfg<CLS>, k_eff <= 32): the group's rows, already packed to 2-bit
-// words in HBM by k_kmer_pack, are loaded into LDS in one coalesced pass; every observation is
+// One workgroup per small group (size class CLS: rows and packed words, and for class
+// 3 observations, within LdsCfg<CLS>; k_eff <= 32): the group's rows, already packed
+// to 2-bit words in HBM by k_row_stage, are loaded into LDS in one pass; every observation is
 // inserted into an LDS hash table (64-bit CAS on the key; the count and the OR of
 // exts share one u32: count in bits 0..23, exts in 24..31), the valid entries are
 // compacted, bitonic-sorted and censored by binary search, all in LDS. The all-ones
 // key (TTT..T at k = 32) equals the empty marker and gets a dedicated slot.
 constexpr int kLdsBlock = 512;  // 8 waves per group workgroup (16 per CU for class 1; 1024 measured slower)
 
-// Two size classes: class 1 (<= 2048 observations, ~78 KB LDS, 2 workgroups per CU)
-// and class 2 (<= 4096 observations, ~155 KB, 1 per CU). Larger groups take the
-// global radix-sort path.
-// Class 3 (<= 1536 observations, 2048 slots, load factor <= 0.75, ~46 KB: 3 workgroups
-// per CU) takes the typical C3 group (~10 reads of 119 k-mers) first.
-// Class 4 (round 2): groups above class 2 with <= 512 rows and <= 4096 packed words,
-// any number of observations: the 8192-slot table takes up to kClaim distinct k-mers
-// and the sort buffer up to kObs valid ones (~150 KB, 1 workgroup per CU). A group
-// that exceeds either is handed to the global path (its class is reset to 0 before
-// k_drop_small_rows, which then keeps its rows), so the outputs never depend on it.
+// Size classes, tried in the order 3, 1, 4; larger groups take the global radix-sort
+// path. Class 3 (<= 1536 observations, 2048 slots, load factor <= 0.75, ~46 KB: 3
+// workgroups per CU) takes the typical C3 group (~10 reads of 119 k-mers).
+// Class 1 (<= 256 rows, <= 768 packed words, any number of observations): a 4096-slot
+// table takes up to 2048 distinct k-mers (~78 KB, 2 workgroups per CU). Class 4 (round
+// 2; <= 512 rows, <= 4096 words): an 8192-slot table for up to 6144 distinct and 3072
+// valid k-mers (~150 KB, 1 workgroup per CU). A class-1 group past its claim cap goes
+// on to class 4 (whose instance runs last), a class-4 group past either bound to the
+// global path: its class is rewritten before k_drop_small_rows, which then keeps its
+// rows, so the outputs never depend on where a group ends up.
 template <int CLS>
 struct LdsCfg {
-    static constexpr int kObs = CLS == 3 ? 1536 : CLS == 1 ? 2048 : CLS == 2 ? 4096 : 3072;
+    static_assert(CLS == 1 || CLS == 3 || CLS == 4, "LDS size classes 3, 1, 4");
+    static constexpr int kObs = CLS == 3 ? 1536 : CLS == 1 ? 2048 : 3072;
     static constexpr int kSlots = CLS == 3 ? 2048 : CLS == 4 ? 8192 : 2 * kObs;  // power of two
     static constexpr int kClaim = CLS == 4 ? 6144 : kObs;  // distinct k-mers (claimed slots)
     static constexpr int kRows = CLS == 3 ? 192 : CLS == 1 ? 256 : 512;    // rows of one group
-    static constexpr int kWords = CLS == 3 ? 576 : CLS == 1 ? 768 : CLS == 2 ? 1536 : 4096;  // packed words
+    static constexpr int kWords = CLS == 3 ? 576 : CLS == 1 ? 768 : 4096;  // packed words
     // insert phase (packed words + row metadata) and sort phase (valid entries) share LDS
     static constexpr int kInsertWords = kWords + 1 + (kRows * 12 + 7) / 8;
     static constexpr int kUnionWords = (kObs * 12 + 7) / 8 > kInsertWords ? (kObs * 12 + 7) / 8 : kInsertWords;
@@ -463,6 +464,9 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
                                                      unsigned long long* __restrict__ gstat) {
     using C = LdsCfg<CLS>;
     constexpr int kWaves = TB / 64;
+    // classes 1 and 4 take groups of any observation count: their distinct k-mers are
+    // bounded by the claim cap (and class 4's valid ones by its sort buffer) instead
+    constexpr bool kBounded = CLS == 1 || CLS == 4;
     constexpr int kLdsObs = C::kObs, kLdsSlots = C::kSlots, kLdsRows = C::kRows, kLdsWords = C::kWords;
     __shared__ unsigned long long tkey[kLdsSlots + 1];
     __shared__ uint32_t tinfo[kLdsSlots + 1];  // count (bits 0..23) | exts << 24
@@ -572,7 +576,7 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
                 uint32_t e = 0;
                 if (p > 0) e |= 1u << pk_base(rw, p - 1);
                 if (p + K < len) e |= 1u << (4 + pk_base(rw, p + K));
-                if (CLS == 4 && __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+                if (kBounded && __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
                 uint32_t slot;
                 if (key == kEmpty) {
                     slot = kLdsSlots;
@@ -586,7 +590,7 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
                 }
                 if ((atomicAdd(&tinfo[slot], 1u) & 0xFFFFFFu) == 0) {
                     const uint32_t ci = atomicAdd(&s_claimed, 1u);
-                    if (CLS != 4 || ci < (uint32_t)C::kClaim) claimed[ci] = (uint16_t)slot;
+                    if (!kBounded || ci < (uint32_t)C::kClaim) claimed[ci] = (uint16_t)slot;
                     else s_over = 1;  // more distinct k-mers than the table takes
                 }
                 if (e) atomicOr(&tinfo[slot], e << 24);
@@ -594,18 +598,19 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
         }
         __syncthreads();
         KT(2);
-        if (CLS == 4) {
+        if (kBounded) {
             const bool over = s_over;
             __syncthreads();  // every thread has read the flag before it is cleared
             if (over) {
                 // the claimed list is incomplete: clear the whole table; the group goes
-                // to the global path (the next group's first barrier orders the resets)
+                // to class 4 (from class 1) or the global path (the next group's first
+                // barrier orders the resets)
                 for (int i = tid; i <= kLdsSlots; i += TB) {
                     tkey[i] = kEmpty;
                     tinfo[i] = 0;
                 }
                 if (tid == 0) {
-                    gsmall[g] = 0;
+                    gsmall[g] = CLS == 1 ? 4 : 0;
                     s_claimed = 0;
                     s_over = 0;
                 }
@@ -855,8 +860,7 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
             uint8_t cls = 0;
             if (K <= 32 && obs > 0) {
                 if (obs <= LdsCfg<3>::kObs && nrows <= LdsCfg<3>::kRows && words <= LdsCfg<3>::kWords) cls = 3;
-                else if (obs <= LdsCfg<1>::kObs && nrows <= LdsCfg<1>::kRows && words <= LdsCfg<1>::kWords) cls = 1;
-                else if (obs <= LdsCfg<2>::kObs && nrows <= LdsCfg<2>::kRows && words <= LdsCfg<2>::kWords) cls = 2;
+                else if (nrows <= LdsCfg<1>::kRows && words <= LdsCfg<1>::kWords) cls = 1;
                 else if (nrows <= LdsCfg<4>::kRows && words <= LdsCfg<4>::kWords) cls = 4;
             }
             gsmall[g] = cls;
@@ -1079,11 +1083,6 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
                            c->woff.as<int64_t>(), c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
                            c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
         hipLaunchKernelGGL((k_kmer_lds<1, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)), dim3(kLdsBlock), 0, s,
-                           c->gdesc.as<GroupDesc>(), G,
-                           c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
-                           c->woff.as<int64_t>(), c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
-                           c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
-        hipLaunchKernelGGL((k_kmer_lds<2, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 8192)), dim3(kLdsBlock), 0, s,
                            c->gdesc.as<GroupDesc>(), G,
                            c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
                            c->woff.as<int64_t>(), c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),

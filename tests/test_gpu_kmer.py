@@ -88,8 +88,8 @@ def test_auto_k(rg):
 
 def test_many_groups_mixed(rg):
     """Many groups, each one polars group: sizes 0..600 rows (small and medium ones take
-    the LDS size classes 3, 1, 2 and 4, groups of more than 512 rows the global path, all
-    in the same call), mixed validity and bytes."""
+    the LDS size classes 3, 1 and 4, groups of more than 512 rows the global path, all in
+    the same call), mixed validity and bytes."""
     rng = np.random.default_rng(11)
     items, go = [], [0]
     for g in range(300):
@@ -146,9 +146,9 @@ def test_long_rows_and_chunk_edges(rg):
 
 
 def test_lds_class4_overflow(rg):
-    """Groups above class 2 (> 4096 observations, <= 512 rows): within class 4's table
-    and sort buffer they stay on the LDS path; more than 6144 distinct k-mers, or more
-    than 3072 valid ones, hand the group to the global path. Every case == the oracle."""
+    """Groups of > 1536 observations and <= 256 rows take class 1 whatever their
+    observation count; past 2048 distinct k-mers they move on to class 4, and past its
+    6144 distinct or 3072 valid k-mers to the global path. Every case == the oracle."""
     import ctypes
 
     from rogtk_amd import _lib
