@@ -419,14 +419,16 @@ struct LdsCfg {
     static_assert(CLS == 1 || CLS == 3 || CLS == 4, "LDS size classes 3, 1, 4");
     static constexpr int kObs = CLS == 3 ? 1536 : CLS == 1 ? 2048 : 3072;
     static constexpr int kSlots = CLS == 3 ? 2048 : CLS == 4 ? 8192 : 2 * kObs;  // power of two
-    static constexpr int kClaim = CLS == 4 ? 6144 : kObs;  // distinct k-mers (claimed slots)
+    // distinct k-mers (claimed slots): at most TB more can be claimed by the inserts in
+    // flight when the cap is passed, and the table keeps an empty slot after those
+    static constexpr int kClaim = CLS == 4 ? 6144 : CLS == 3 ? 1472 : kObs;
     static constexpr int kRows = CLS == 3 ? 192 : CLS == 1 ? 256 : 512;    // rows of one group
     static constexpr int kWords = CLS == 3 ? 576 : CLS == 1 ? 768 : 4096;  // packed words
     // insert phase (packed words + row metadata) and sort phase (valid entries) share LDS
     static constexpr int kInsertWords = kWords + 1 + (kRows * 12 + 7) / 8;
     static constexpr int kUnionWords = (kObs * 12 + 7) / 8 > kInsertWords ? (kObs * 12 + 7) / 8 : kInsertWords;
     static_assert(CLS == 4 || kInsertWords <= (kObs * 12 + 7) / 8, "LDS union too small");
-    static_assert(kSlots - kClaim >= 512, "class 4: one in-flight insert per thread past the claim cap");
+    static_assert(kSlots - kClaim > 512, "one in-flight insert per thread past the claim cap");
 };
 constexpr unsigned long long kEmpty = ~0ull;
 
@@ -464,9 +466,9 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
                                                      unsigned long long* __restrict__ gstat) {
     using C = LdsCfg<CLS>;
     constexpr int kWaves = TB / 64;
-    // classes 1 and 4 take groups of any observation count: their distinct k-mers are
+    // every class takes groups of any observation count: their distinct k-mers are
     // bounded by the claim cap (and class 4's valid ones by its sort buffer) instead
-    constexpr bool kBounded = CLS == 1 || CLS == 4;
+    constexpr bool kBounded = true;
     constexpr int kLdsObs = C::kObs, kLdsSlots = C::kSlots, kLdsRows = C::kRows, kLdsWords = C::kWords;
     __shared__ unsigned long long tkey[kLdsSlots + 1];
     __shared__ uint32_t tinfo[kLdsSlots + 1];  // count (bits 0..23) | exts << 24
@@ -610,7 +612,7 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
                     tinfo[i] = 0;
                 }
                 if (tid == 0) {
-                    gsmall[g] = CLS == 1 ? 4 : 0;
+                    gsmall[g] = CLS == 3 ? 1 : CLS == 1 ? 4 : 0;
                     s_claimed = 0;
                     s_over = 0;
                 }
@@ -859,7 +861,7 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
         if (lane == 0) {
             uint8_t cls = 0;
             if (K <= 32 && obs > 0) {
-                if (obs <= LdsCfg<3>::kObs && nrows <= LdsCfg<3>::kRows && words <= LdsCfg<3>::kWords) cls = 3;
+                if (nrows <= LdsCfg<3>::kRows && words <= LdsCfg<3>::kWords) cls = 3;
                 else if (nrows <= LdsCfg<1>::kRows && words <= LdsCfg<1>::kWords) cls = 1;
                 else if (nrows <= LdsCfg<4>::kRows && words <= LdsCfg<4>::kWords) cls = 4;
             }
