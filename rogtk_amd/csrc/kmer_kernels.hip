@@ -405,11 +405,12 @@ __global__ __launch_bounds__(kBlock) void k_pack(const uint64_t* __restrict__ t_
 constexpr int kLdsBlock = 512;  // 8 waves per group workgroup (16 per CU for class 1; 1024 measured slower)
 
 // Size classes, tried in the order 3, 1, 4; larger groups take the global radix-sort
-// path. Class 3 (<= 1536 observations, 2048 slots, load factor <= 0.75, ~46 KB: 3
-// workgroups per CU) takes the typical C3 group (~10 reads of 119 k-mers).
-// Class 1 (<= 256 rows, <= 768 packed words, any number of observations): a 4096-slot
+// path. Class 3 (<= 192 rows, <= 576 words, a 2048-slot table for up to 1472 distinct
+// and 1024 valid k-mers, ~37 KB and at most 64 VGPRs: 4 workgroups per CU) takes the
+// typical C3 group (~10 reads of 119 k-mers); past either bound a group moves on to
+// class 1. Class 1 (<= 256 rows, <= 768 packed words, any number of observations): a 4096-slot
 // table takes up to 2048 distinct k-mers (~78 KB, 2 workgroups per CU). Class 4 (round
-// 2; <= 512 rows, <= 4096 words): an 8192-slot table for up to 6144 distinct and 3072
+// 2; <= 512 rows, <= 4096 words): an 8192-slot table for up to 6144 distinct and 2048
 // valid k-mers (~150 KB, 1 workgroup per CU). A class-1 group past its claim cap goes
 // on to class 4 (whose instance runs last), a class-4 group past either bound to the
 // global path: its class is rewritten before k_drop_small_rows, which then keeps its
@@ -417,7 +418,9 @@ constexpr int kLdsBlock = 512;  // 8 waves per group workgroup (16 per CU for cl
 template <int CLS>
 struct LdsCfg {
     static_assert(CLS == 1 || CLS == 3 || CLS == 4, "LDS size classes 3, 1, 4");
-    static constexpr int kObs = CLS == 3 ? 1536 : CLS == 1 ? 2048 : 3072;
+    // valid k-mers (the sort buffer; a power of two: the bitonic sort pads to one)
+    static constexpr int kObs = CLS == 3 ? 1024 : 2048;
+    static_assert((kObs & (kObs - 1)) == 0, "sort buffer: a power of two");
     static constexpr int kSlots = CLS == 3 ? 2048 : CLS == 4 ? 8192 : 2 * kObs;  // power of two
     // distinct k-mers (claimed slots): at most TB more can be claimed by the inserts in
     // flight when the cap is passed, and the table keeps an empty slot after those
@@ -427,7 +430,6 @@ struct LdsCfg {
     // insert phase (packed words + row metadata) and sort phase (valid entries) share LDS
     static constexpr int kInsertWords = kWords + 1 + (kRows * 12 + 7) / 8;
     static constexpr int kUnionWords = (kObs * 12 + 7) / 8 > kInsertWords ? (kObs * 12 + 7) / 8 : kInsertWords;
-    static_assert(CLS == 4 || kInsertWords <= (kObs * 12 + 7) / 8, "LDS union too small");
     static_assert(kSlots - kClaim > 512, "one in-flight insert per thread past the claim cap");
 };
 constexpr unsigned long long kEmpty = ~0ull;
@@ -455,7 +457,7 @@ struct GroupDesc {
 };
 
 template <int CLS, int TB>
-__global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ gdesc, int64_t G,
+__global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDesc* __restrict__ gdesc, int64_t G,
                                                      uint8_t* __restrict__ gsmall, int K, int64_t min_cov,
                                                      const int32_t* __restrict__ row_len,
                                                      const int64_t* __restrict__ woff,
@@ -665,15 +667,15 @@ __global__ __launch_bounds__(TB) void k_kmer_lds(const GroupDesc* __restrict__ g
             KT(5);
             continue;
         }
-        if (CLS == 4 && nv > (uint32_t)kLdsObs) {
-            // more valid k-mers than the sort buffer takes: global path
+        if (nv > (uint32_t)kLdsObs) {
+            // more valid k-mers than the sort buffer takes: the next class or the global path
             for (uint32_t i = tid; i < ncl; i += TB) {
                 const uint32_t sl = claimed[i];
                 tkey[sl] = kEmpty;
                 tinfo[sl] = 0;
             }
             if (tid == 0) {
-                gsmall[g] = 0;
+                gsmall[g] = CLS == 3 ? 1 : CLS == 1 ? 4 : 0;
                 s_claimed = 0;
             }
             continue;

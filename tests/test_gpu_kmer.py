@@ -146,9 +146,11 @@ def test_long_rows_and_chunk_edges(rg):
 
 
 def test_lds_class4_overflow(rg):
-    """Groups of > 1536 observations and <= 256 rows take class 1 whatever their
-    observation count; past 2048 distinct k-mers they move on to class 4, and past its
-    6144 distinct or 3072 valid k-mers to the global path. Every case == the oracle."""
+    """Groups move along the LDS classes by their distinct and valid k-mers: class 3
+    (<= 1472 distinct, <= 1024 valid) -> class 1 (<= 2048 distinct) -> class 4 (<= 6144
+    distinct, <= 2048 valid) -> the global path. `mid_valid` (1190 valid k-mers at
+    min_cov 1) leaves class 3 for class 1 (its bitonic sort pads to 2048 entries, more
+    than class 3's buffer). Every case == the oracle."""
     import ctypes
 
     from rogtk_amd import _lib
@@ -158,7 +160,8 @@ def test_lds_class4_overflow(rg):
     fits = [tpl[int(a):int(a) + 150] for a in rng.integers(0, 250, 60)]  # ~7k obs, few distinct
     many_distinct = _reads(rng, 100, 150, 150)  # 11.9k distinct k-mers
     many_valid = _reads(rng, 40, 150, 150)  # 4.8k distinct, all valid at min_cov 1
-    groups = [fits, many_distinct, many_valid, fits[:5]]
+    mid_valid = _reads(rng, 10, 150, 150)  # 1190 distinct k-mers, all valid at min_cov 1
+    groups = [fits, many_distinct, many_valid, fits[:5], mid_valid]
     items = [x for grp in groups for x in grp]
     go = np.r_[0, np.cumsum([len(grp) for grp in groups])].tolist()
     for k, mc in ((17, 1), (31, 2), (21, 1)):
@@ -167,7 +170,7 @@ def test_lds_class4_overflow(rg):
         _lib.call("rogtk_kmer_path_stats", paths)
         if _LAST_MODE[0] == 1:
             # the distinct-overflow group always leaves; the valid-overflow one at min_cov 1
-            assert paths[1] == (2 if mc == 1 else 1) and paths[0] == 4 - paths[1], tuple(paths)
+            assert paths[1] == (2 if mc == 1 else 1) and paths[0] == 5 - paths[1], tuple(paths)
 
 
 def test_saturating_count(rg):
