@@ -247,6 +247,15 @@ int rogtk_assign_codes(const uint64_t* codes, const uint8_t* kind, int64_t n, co
  * string among the distinct strings in byte-lexicographic order; *n_groups (host). */
 int rogtk_group_strings(const int64_t* offsets, const uint8_t* values, int64_t n, int64_t max_len, uint32_t id_base,
                         uint32_t* ids, int64_t* n_groups, void* stream);
+/* Step 8 of the sharded H3 for max_distance 0 or 1: the n
+ * all-gathered irregular strings (int64 offsets from 0) -> ids[n]. max_distance 0: exact
+ * bytes, ids from n_reg. max_distance 1: Hamming-1 edges among the strings and to the
+ * sorted global codes G[ng] (umi_len <= 32), connected components with the n_reg regular
+ * clusters (labels[ng]: each G code's regular id, remapped IN PLACE when irregular strings
+ * bridge regular clusters). *n_clusters = all clusters. Same result on every rank. */
+int rogtk_irregular_merge(const int64_t* offsets, const uint8_t* values, int64_t n, int64_t max_len, int umi_len,
+                          int max_distance, const uint64_t* G, int64_t ng, uint32_t* labels, int64_t n_reg,
+                          uint32_t* ids, int64_t* n_clusters, void* stream);
 
 /* ========================= Level 2: host buffers ========================= */
 

@@ -275,14 +275,22 @@ def py_hamming(s: bytes, target: bytes) -> int:
 
 
 def py_cluster_bruteforce(items: Sequence[Optional[bytes]], umi_len: int = 0, max_distance: int = 1):
-    """H3 spec by brute force: O(d^2) pairwise H2 distances between distinct UMIs."""
+    """H3 spec by brute force: O(d^2) pairwise H2 distances
+    (expressions.rs:1054-1069: equal byte length, then mismatching bytes) between ALL
+    distinct non-null strings, regular or not. Ids: components holding a regular UMI
+    (byte length umi_len <= 32, pure ACGT) first, by smallest regular string; then the
+    rest by smallest string (byte-lexicographic)."""
     L = umi_len
     if L <= 0:
         L = next((len(x) for x in items if x is not None), 0)
-    regular = sorted({x for x in items if x is not None and len(x) == L and L >= 1
-                      and all(c in b"ACGT" for c in x)})
-    irregular = sorted({x for x in items if x is not None and x not in set(regular)})
-    parent = list(range(len(regular)))
+
+    def is_regular(x):
+        return 1 <= L <= 32 and len(x) == L and all(c in b"ACGT" for c in x)
+
+    distinct = {bytes(x) for x in items if x is not None}
+    # vertex order: regular strings (lexicographic = code order), then the others
+    verts = sorted(x for x in distinct if is_regular(x)) + sorted(x for x in distinct if not is_regular(x))
+    parent = list(range(len(verts)))
 
     def find(x):
         while parent[x] != x:
@@ -290,25 +298,18 @@ def py_cluster_bruteforce(items: Sequence[Optional[bytes]], umi_len: int = 0, ma
         return x
 
     if max_distance == 1:
-        for i in range(len(regular)):
+        for i in range(len(verts)):
             for j in range(i):
-                if sum(1 for a, b in zip(regular[i], regular[j]) if a != b) <= 1:
+                a, b = verts[i], verts[j]
+                if len(a) == len(b) and sum(1 for x, y in zip(a, b) if x != y) <= 1:
                     ri, rj = find(i), find(j)
                     if ri != rj:
                         parent[max(ri, rj)] = min(ri, rj)
-    roots = sorted({find(i) for i in range(len(regular))})
+    roots = sorted({find(i) for i in range(len(verts))})
     rank = {r: k for k, r in enumerate(roots)}
-    reg_id = {u: rank[find(i)] for i, u in enumerate(regular)}
-    irr_id = {u: len(roots) + k for k, u in enumerate(irregular)}
-    out = []
-    for x in items:
-        if x is None:
-            out.append(None)
-        elif x in reg_id:
-            out.append(reg_id[x])
-        else:
-            out.append(irr_id[x])
-    return out, len(roots) + len(irregular)
+    vid = {u: rank[find(i)] for i, u in enumerate(verts)}
+    out = [None if x is None else vid[bytes(x)] for x in items]
+    return out, len(roots)
 
 
 # --------------------------------------------------------------------------

@@ -276,15 +276,19 @@ void oracle_hamming_batch(const void* offsets, int offset_width, const uint8_t* 
     }
 }
 
-// ---- H3: UMI cluster assignment (spec owned by this build; DESIGN.md §H3) ----
-// Regular rows (byte length == L, all of A/C/G/T) are packed 2 bits/base, first
-// base most significant (A=0,C=1,G=2,T=3), so code order == lexicographic order.
-// max_distance 0: clusters = distinct regular UMIs. max_distance 1: connected
-// components of the graph with an edge between distinct UMIs at Hamming 1.
-// Representative = smallest code of the component. Irregular non-null rows are
-// grouped by exact byte equality. Cluster ids are dense: regular clusters in
-// representative-code order, then irregular clusters in byte-lexicographic
-// order. Null rows get no id (out_valid = 0).
+// ---- H3: UMI cluster assignment (spec owned by this build; DESIGN.md §4) ----
+// Regular rows (byte length == L <= 32, all of A/C/G/T) are packed 2 bits/base, first
+// base most significant (A=0,C=1,G=2,T=3), so code order == lexicographic order. Every
+// other non-null row is irregular (N, lowercase, other lengths, any bytes).
+// max_distance 0: clusters = distinct strings. max_distance 1: connected components of
+// the graph over ALL distinct non-null strings with an edge wherever the H2.1 distance
+// (expressions.rs:1054-1069: equal byte length, then mismatches) is 1, compared byte by
+// byte (N and lowercase are ordinary bytes, distinct from A/C/G/T).
+// An irregular string can thus join a regular cluster (ACGTNACGTACG ~ ACGTAACGTACG) and
+// bridge two of them.
+// Ids are dense: components holding a regular UMI first, in order of their smallest
+// regular code; then components of irregular strings only, in byte-lexicographic order of
+// their smallest string. Null rows get no id (out_valid = 0).
 // umi_len <= 0: L = byte length of the first non-null row.
 // Returns the number of clusters, or -1 on bad arguments.
 int64_t oracle_umi_cluster(const void* offsets, int offset_width, const uint8_t* values,
@@ -351,13 +355,7 @@ int64_t oracle_umi_cluster(const void* offsets, int offset_width, const uint8_t*
                 }
         }
     }
-    std::vector<uint32_t> label(D);
-    uint32_t n_regular = 0;
-    for (size_t i = 0; i < D; ++i) {  // roots in ascending code order
-        uint32_t r = find((uint32_t)i);
-        if (r == i) label[i] = n_regular++;
-        else label[i] = label[r];  // r < i already labelled
-    }
+    // irregular distinct strings, byte-lexicographic: vertices D + j
     std::map<std::string, uint32_t> irregular;
     for (int64_t i = 0; i < n; ++i)
         if (cls[i] == 2) {
@@ -365,8 +363,66 @@ int64_t oracle_umi_cluster(const void* offsets, int offset_width, const uint8_t*
             row_span(offsets, offset_width, i, &st, &len);
             irregular.emplace(std::string((const char*)values + st, (size_t)len), 0);
         }
-    uint32_t next = n_regular;
-    for (auto& kv : irregular) kv.second = next++;
+    std::vector<const std::string*> istr;
+    for (auto& kv : irregular) {
+        kv.second = (uint32_t)istr.size();
+        istr.push_back(&kv.first);
+    }
+    const size_t I = istr.size();
+    parent.resize(D + I);
+    for (size_t j = 0; j < I; ++j) parent[D + j] = (uint32_t)(D + j);
+    auto unite = [&](uint32_t x, uint32_t y) {
+        uint32_t a = find(x), b = find(y);
+        if (a == b) return;
+        if (a < b) std::swap(a, b);
+        parent[a] = b;  // root = smallest vertex: regular codes first, then strings
+    };
+    if (max_distance == 1) {
+        // irregular ~ irregular: equal length, equal except at one position p -> same
+        // (length, p, string without byte p) key; link each to the first string seen
+        std::map<std::pair<size_t, std::string>, uint32_t> first;
+        for (size_t j = 0; j < I; ++j) {
+            const std::string& s = *istr[j];
+            for (size_t p = 0; p < s.size(); ++p) {
+                std::string key = s.substr(0, p) + s.substr(p + 1);
+                auto it = first.emplace(std::make_pair(p, std::move(key)), (uint32_t)j);
+                if (!it.second) unite((uint32_t)(D + it.first->second), (uint32_t)(D + j));
+            }
+        }
+        // irregular ~ regular: length L with exactly one non-ACGT byte at p -> the codes
+        // with A/C/G/T at p
+        for (size_t j = 0; packable && j < I; ++j) {
+            const std::string& s = *istr[j];
+            if ((int)s.size() != L) continue;
+            int bad = -1, nbad = 0;
+            uint64_t c = 0;
+            for (int q = 0; q < L; ++q) {
+                const char ch = s[(size_t)q];
+                int b = ch == 'A' ? 0 : ch == 'C' ? 1 : ch == 'G' ? 2 : ch == 'T' ? 3 : -1;
+                if (b < 0) {
+                    ++nbad;
+                    bad = q;
+                    b = 0;
+                }
+                c = (c << 2) | (uint64_t)b;
+            }
+            if (nbad != 1) continue;
+            const int sh = 2 * (L - 1 - bad);
+            for (uint64_t x = 0; x < 4; ++x) {
+                const uint64_t nb = (c & ~(3ull << sh)) | (x << sh);
+                auto it = std::lower_bound(distinct.begin(), distinct.end(), nb);
+                if (it != distinct.end() && *it == nb)
+                    unite((uint32_t)(D + j), (uint32_t)(it - distinct.begin()));
+            }
+        }
+    }
+    std::vector<uint32_t> label(D + I);
+    uint32_t next = 0;
+    for (size_t i = 0; i < D + I; ++i) {  // roots in vertex order
+        uint32_t r = find((uint32_t)i);
+        if (r == i) label[i] = next++;
+        else label[i] = label[r];  // r < i already labelled
+    }
     for (int64_t i = 0; i < n; ++i) {
         if (out_valid) out_valid[i] = cls[i] != 0;
         if (cls[i] == 0) { cluster_id[i] = 0; continue; }
@@ -376,7 +432,7 @@ int64_t oracle_umi_cluster(const void* offsets, int offset_width, const uint8_t*
         } else {
             int64_t st, len;
             row_span(offsets, offset_width, i, &st, &len);
-            cluster_id[i] = irregular[std::string((const char*)values + st, (size_t)len)];
+            cluster_id[i] = label[D + irregular[std::string((const char*)values + st, (size_t)len)]];
         }
     }
     return (int64_t)next;

@@ -66,10 +66,17 @@ void prof_drain_locked() {
 
 bool profiling_on() { return g_prof.load(std::memory_order_relaxed); }
 
-ProfScope::ProfScope(KernelId id, hipStream_t stream) : id_(id), stream_(stream) {
+ProfScope::ProfScope(KernelId id, hipStream_t stream, bool exact) : id_(id), stream_(stream), exact_(exact) {
     if (!g_prof.load(std::memory_order_relaxed) || !((g_prof_mask.load(std::memory_order_relaxed) >> id) & 1u)) return;
     if (hipEventCreate(&start_) != hipSuccess) {
         start_ = nullptr;
+        return;
+    }
+    if (exact_) {  // both events ride on the dispatch packet (hipExtLaunchKernelGGL)
+        if (hipEventCreate(&stop_) != hipSuccess) {
+            hipEventDestroy(start_);
+            start_ = stop_ = nullptr;
+        }
         return;
     }
     hipEventRecord(start_, stream_);
@@ -77,12 +84,14 @@ ProfScope::ProfScope(KernelId id, hipStream_t stream) : id_(id), stream_(stream)
 
 ProfScope::~ProfScope() {
     if (!start_) return;
-    hipEvent_t stop = nullptr;
-    if (hipEventCreate(&stop) != hipSuccess) {
-        hipEventDestroy(start_);
-        return;
+    hipEvent_t stop = stop_;
+    if (!exact_) {
+        if (hipEventCreate(&stop) != hipSuccess) {
+            hipEventDestroy(start_);
+            return;
+        }
+        hipEventRecord(stop, stream_);
     }
-    hipEventRecord(stop, stream_);
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof_pending.push_back({id_, start_, stop});
 }
@@ -648,8 +657,9 @@ __global__ void k_max_len(const int64_t* __restrict__ off, int64_t n, unsigned l
 }
 
 // H3 over a column already staged into c->codes / regbits / irr (n_irr irregular rows):
-// regular rows through the cluster engine, irregular rows grouped by exact bytes after
-// them; ids into did (device), on stream s.
+// regular rows through the cluster engine, then the irregular rows (exact bytes, or for
+// max_distance 1 their Hamming-1 edges merged with the regular clusters, irregular.hip);
+// ids into did (device), on stream s.
 int cluster_staged(HostCtx* c, const void* d_offsets, int ow, const uint8_t* d_values, const uint8_t* d_validity,
                    int64_t voff, int64_t n, int L, int64_t n_irr, int64_t max_len, int max_distance, uint32_t* did,
                    int64_t* n_clusters, hipStream_t s) {
@@ -690,13 +700,27 @@ int cluster_staged(HostCtx* c, const void* d_offsets, int ow, const uint8_t* d_v
     } else {
         ROGTK_HIP_CHECK(hipMemsetAsync(did, 0xFF, (size_t)n * 4, s));
     }
-    int64_t n_irr_clusters = 0;
-    if (n_irr > 0) {
+    int64_t total = n_reg_clusters;
+    if (n_irr > 0 && max_distance == 1) {
+        // Hamming-1 edges of the irregular rows (to each other and to regular codes)
+        const bool packable = L >= 1 && L <= kMaxPackedLen;
+        ClusterLayout use{};
+        if (packable) cluster_layout(L, c->ws_maxd, &use);
+        const uint8_t* ws = (const uint8_t*)c->ws.p;
+        CodeLookup lk = [&](const uint64_t* q, int64_t nq, uint32_t* lab, hipStream_t st) {
+            return launch_cluster_lookup(use, ws, q, nq, lab, st);
+        };
+        int rc = irregular_merge(d_offsets, ow, d_values, c->irr.as<int64_t>(), n_irr, max_len, L, n_reg_clusters,
+                                 packable ? &lk : nullptr, did, n, did, &total, s);
+        if (rc) return rc;
+    } else if (n_irr > 0) {
+        int64_t n_irr_clusters = 0;
         int rc = irregular_cluster(d_offsets, ow, d_values, c->irr.as<int64_t>(), n_irr, max_len, stats_dev, did,
                                    &n_irr_clusters, s);
         if (rc) return rc;
+        total += n_irr_clusters;
     }
-    if (n_clusters) *n_clusters = n_reg_clusters + n_irr_clusters;
+    if (n_clusters) *n_clusters = total;
     return ROGTK_OK;
 }
 

@@ -1433,6 +1433,28 @@ __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ 
     }
 }
 
+// Label of arbitrary packed codes (the irregular merge's neighbour probes): kNone for
+// ~0 or a code that is not present, else the label k_assign would give it.
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_lookup(const uint64_t* __restrict__ q, int64_t nq, uint64_t nbits,
+                                                   const uint32_t* __restrict__ labelcode,
+                                                   const uint32_t* __restrict__ flab, const uint4* __restrict__ RT,
+                                                   const uint32_t* __restrict__ wlab,
+                                                   const uint64_t* __restrict__ wexc, uint32_t* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nq; i += (int64_t)gridDim.x * kBlock) {
+        const uint64_t c = q[i];
+        uint32_t lab = kNone;
+        if (c < nbits) {
+            const uint4 e = RT[c >> 6];
+            if ((rt_word(e) >> (c & 63)) & 1ull) {
+                const uint32_t wl = wlab ? word_label_of(wlab, wexc, c) : kNone;
+                lab = wl != kNone ? wl : MODE == 0 ? labelcode[c] : flab[rt_rank(e, (uint32_t)c)];
+            }
+        }
+        out[i] = lab;
+    }
+}
+
 inline int grid_for(int64_t lanes, int64_t cap = 0) {
     int64_t g = (lanes + kBlock - 1) / kBlock;
     if (g < 1) g = 1;
@@ -2059,6 +2081,30 @@ int launch_cluster_assign(const ClusterLayout& cl, const uint8_t* ws, const uint
         }
     }
     return enqueue_assign(cl, p, wl, codes, regular_bits, n, cluster_id, s);
+}
+
+int launch_cluster_lookup(const ClusterLayout& cl, const uint8_t* ws, const uint64_t* q, int64_t nq, uint32_t* lab,
+                          hipStream_t s) {
+    if (nq <= 0) return ROGTK_OK;
+    if (int rc = cluster_finish(ws, s)) return rc;
+    WsPtrs p = ws_ptrs(cl, const_cast<uint8_t*>(ws));
+    bool wl = false;
+    {
+        std::lock_guard<std::mutex> lk(g_rs_mu);
+        auto it = g_rs.find(ws);
+        if (it != g_rs.end()) wl = it->second.word_labels;
+    }
+    const uint32_t* wlab = wl ? p.wpref : nullptr;
+    const uint64_t* wexc = wl ? p.G : nullptr;
+    const int g = grid_for(nq, 4096);
+    if (cl.label_by_code)
+        hipLaunchKernelGGL(k_lookup<0>, dim3(g), dim3(kBlock), 0, s, q, nq, cl.nbits, p.labelcode, p.D, p.RT, wlab,
+                           wexc, lab);
+    else
+        hipLaunchKernelGGL(k_lookup<1>, dim3(g), dim3(kBlock), 0, s, q, nq, cl.nbits, p.labelcode, p.ilab, p.RT, wlab,
+                           wexc, lab);
+    ROGTK_HIP_CHECK(hipGetLastError());
+    return ROGTK_OK;
 }
 
 namespace {

@@ -20,8 +20,11 @@
 //                             (redundant on every rank, deterministic): dense labels in
 //                             order of each component's smallest code
 //   7. rogtk_assign_codes     row -> its code's index in G (binary search) -> label
-//   8. rogtk_group_strings    irregular rows: exact-bytes groups over the all-gathered
-//                             irregular strings, ids after the regular clusters
+//   8. rogtk_irregular_merge  irregular rows (all-gathered strings): exact-bytes groups, or
+//                             for max_distance 1 their Hamming-1 edges to each other and
+//                             to G's codes merged with the regular clusters (irregular.hip;
+//                             the G labels are remapped in place when clusters merge)
+//   (7 runs after 8, so rows see the final labels)
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -165,34 +168,56 @@ __global__ __launch_bounds__(kB) void k_iota(uint32_t* __restrict__ v, int64_t n
     for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kB) v[i] = (uint32_t)i;
 }
 
+__global__ __launch_bounds__(kB) void k_iota64(int64_t* __restrict__ v, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kB) v[i] = i;
+}
+
 __global__ __launch_bounds__(kB) void k_gather_pos(const uint32_t* __restrict__ pos, const uint32_t* __restrict__ perm,
                                                    int64_t n, uint32_t* __restrict__ out) {
     for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kB) out[i] = pos[perm[i]];
 }
 
-// consecutive records of one (p, masked key) group -> an edge between their codes' indices in G
+// consecutive records of one (p, masked key) group -> an edge between their codes' indices
+// in G. Grid-stride over whole workgroup tiles (the wave append needs every lane in step),
+// so any record count is covered by a capped grid.
 __global__ __launch_bounds__(kB) void k_group_edges(const uint64_t* __restrict__ mk, const uint32_t* __restrict__ pos,
                                                     const uint64_t* __restrict__ code, const uint32_t* __restrict__ perm,
                                                     int64_t n, const uint64_t* __restrict__ G, int64_t ng,
                                                     uint2* __restrict__ E, unsigned long long* __restrict__ ne) {
-    const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
-    bool e = false;
-    uint32_t a = 0, b = 0;
-    if (i > 0 && i < n) {
-        const uint32_t x = perm[i - 1], y = perm[i];
-        if (pos[x] == pos[y] && mk[x] == mk[y] && code[x] != code[y]) {
-            e = true;
-            a = (uint32_t)lower_bound_u64(G, ng, code[x]);
-            b = (uint32_t)lower_bound_u64(G, ng, code[y]);
-        }
-    }
-    const uint64_t m = __ballot(e);
-    if (!m) return;
     const int lane = threadIdx.x & 63;
-    unsigned long long base = 0;
-    if (lane == 0) base = atomicAdd(ne, (unsigned long long)__popcll(m));
-    base = __shfl(base, 0);
-    if (e) E[base + __popcll(m & ((1ull << lane) - 1ull))] = make_uint2(a, b);
+    for (int64_t i0 = (int64_t)blockIdx.x * kB; i0 < n; i0 += (int64_t)gridDim.x * kB) {
+        const int64_t i = i0 + threadIdx.x;
+        bool e = false;
+        uint32_t a = 0, b = 0;
+        if (i > 0 && i < n) {
+            const uint32_t x = perm[i - 1], y = perm[i];
+            if (pos[x] == pos[y] && mk[x] == mk[y] && code[x] != code[y]) {
+                e = true;
+                a = (uint32_t)lower_bound_u64(G, ng, code[x]);
+                b = (uint32_t)lower_bound_u64(G, ng, code[y]);
+            }
+        }
+        const uint64_t m = __ballot(e);
+        if (!m) continue;
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(ne, (unsigned long long)__popcll(m));
+        base = __shfl(base, 0);
+        if (e) E[base + __popcll(m & ((1ull << lane) - 1ull))] = make_uint2(a, b);
+    }
+}
+
+// records of positions p0 .. p0 + np - 1 of every distinct code (world 1, long engine)
+__global__ __launch_bounds__(kB) void k_record_range(const uint64_t* __restrict__ D, int64_t nd, int p0, int np,
+                                                     uint64_t* __restrict__ mk, uint32_t* __restrict__ pos,
+                                                     uint64_t* __restrict__ code) {
+    const int64_t total = nd * np;
+    for (int64_t k = (int64_t)blockIdx.x * kB + threadIdx.x; k < total; k += (int64_t)gridDim.x * kB) {
+        const int p = p0 + (int)(k % np);
+        const uint64_t c = D[k / np];
+        mk[k] = mask_digit(c, p);
+        pos[k] = (uint32_t)p;
+        code[k] = c;
+    }
 }
 
 __device__ __forceinline__ uint32_t find_root(const uint32_t* f, uint32_t x) {
@@ -267,6 +292,15 @@ int check_len(int L) {
 }
 
 }  // namespace
+
+int masked_records_range(const uint64_t* D, int64_t nd, int p0, int np, uint64_t* mk, uint32_t* pos, uint64_t* code,
+                         hipStream_t s) {
+    if (nd <= 0 || np <= 0) return ROGTK_OK;
+    hipLaunchKernelGGL(k_record_range, grid(nd * np, 16384), dim3(kB), 0, s, D, nd, p0, np, mk, pos, code);
+    ROGTK_HIP_CHECK(hipGetLastError());
+    return ROGTK_OK;
+}
+
 }  // namespace rogtk
 
 using namespace rogtk;
@@ -435,7 +469,7 @@ int rogtk_clique_edges(const uint64_t* mk, const uint32_t* pos, const uint64_t* 
     b = tb;
     ROGTK_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, b, p1, sp, perm1, perm, (int)n, 0, 8, s));
     ROGTK_HIP_CHECK(hipMemsetAsync(ne, 0, 8, s));
-    hipLaunchKernelGGL(k_group_edges, grid(n), dim3(kB), 0, s, mk, pos, code, perm, n, G, ng, (uint2*)edges, ne);
+    hipLaunchKernelGGL(k_group_edges, grid(n, 16384), dim3(kB), 0, s, mk, pos, code, perm, n, G, ng, (uint2*)edges, ne);
     ROGTK_HIP_CHECK(hipGetLastError());
     unsigned long long h = 0;
     ROGTK_HIP_CHECK(hipMemcpyAsync(&h, ne, 8, hipMemcpyDeviceToHost, s));
@@ -533,6 +567,35 @@ int rogtk_group_strings(const int64_t* offsets, const uint8_t* values, int64_t n
     ROGTK_HIP_CHECK(hipStreamSynchronize(s));
     *n_groups = groups;
     return ROGTK_OK;
+}
+
+int rogtk_irregular_merge(const int64_t* offsets, const uint8_t* values, int64_t n, int64_t max_len, int umi_len,
+                          int max_distance, const uint64_t* G, int64_t ng, uint32_t* labels, int64_t n_reg,
+                          uint32_t* ids, int64_t* n_clusters, void* stream) {
+    ROGTK_REQUIRE(n_clusters && n >= 0 && ng >= 0 && n_reg >= 0, ROGTK_E_INVALID, "irregular_merge: bad sizes");
+    ROGTK_REQUIRE(max_distance == 0 || max_distance == 1, ROGTK_E_UNSUPPORTED,
+                  "max_distance %d: only 0 and 1 are supported", max_distance);
+    *n_clusters = n_reg;
+    if (n == 0) return ROGTK_OK;
+    if (max_distance == 0) {
+        int64_t groups = 0;
+        if (int rc = rogtk_group_strings(offsets, values, n, max_len, (uint32_t)n_reg, ids, &groups, stream))
+            return rc;
+        *n_clusters = n_reg + groups;
+        return ROGTK_OK;
+    }
+    ROGTK_REQUIRE(offsets && ids && (ng == 0 || (G && labels)), ROGTK_E_INVALID, "irregular_merge: NULL buffer");
+    hipStream_t s = (hipStream_t)stream;
+    Scratch S;
+    if (int rc = S.get((size_t)n * 8, s)) return rc;
+    int64_t* rows = (int64_t*)S.p;
+    hipLaunchKernelGGL(k_iota64, grid(n, 16384), dim3(kB), 0, s, rows, n);
+    ROGTK_HIP_CHECK(hipGetLastError());
+    CodeLookup lk = [&](const uint64_t* q, int64_t nq, uint32_t* lab, hipStream_t st) {
+        return sorted_code_lookup(G, ng, labels, q, nq, lab, st);
+    };
+    return irregular_merge(offsets, 8, values, rows, n, std::max<int64_t>(max_len, 1), umi_len, n_reg,
+                           ng > 0 ? &lk : nullptr, labels, ng, ids, n_clusters, s);
 }
 
 }  // extern "C"

@@ -28,6 +28,13 @@ namespace rogtk {
 namespace {
 
 constexpr int kB = 256;
+// (code, position) records per edge-finding batch; ROGTK_LONG_REC_BATCH overrides (read
+// per call: tests lower it to cover the batching)
+inline int64_t rec_batch() {
+    const char* e = getenv("ROGTK_LONG_REC_BATCH");
+    const long long v = e ? atoll(e) : 0;
+    return v > 0 ? (int64_t)v : (int64_t)1 << 28;
+}
 
 inline dim3 grid(int64_t n) { return dim3((unsigned)std::max<int64_t>(1, (n + kB - 1) / kB)); }
 
@@ -155,6 +162,13 @@ __global__ __launch_bounds__(kB) void k_assign_long(const int64_t* __restrict__ 
 
 __global__ void k_put_count(int64_t* stats, int64_t v) { stats[1] = v; }
 
+// label of every distinct code (the irregular merge's lookup table)
+__global__ __launch_bounds__(kB) void k_dlab(const uint32_t* __restrict__ f, const uint32_t* __restrict__ rlab,
+                                             int64_t nd, uint32_t* __restrict__ dlab) {
+    const int64_t d = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (d < nd) dlab[d] = rlab[f[d]];
+}
+
 struct Arena {
     uint8_t* base = nullptr;
     size_t off = 0, cap = 0;
@@ -218,6 +232,7 @@ int long_cluster(const void* offsets, int ow, const uint8_t* values, const uint8
     ROGTK_HIP_CHECK(hipStreamSynchronize(s));
     const int64_t nreg = (int64_t)h[0], nirr = (int64_t)h[1];
     int64_t n_reg_clusters = 0;
+    int64_t nd_all = 0;  // distinct regular codes
     if (nreg > 0) {
         size_t tb = tmp_b;
         ROGTK_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, rkey, skey, rrow, srow, (int)nreg, 0, 2 * L, s));
@@ -231,25 +246,35 @@ int long_cluster(const void* offsets, int ow, const uint8_t* values, const uint8
         ROGTK_HIP_CHECK(hipMemcpyAsync(&hnd, cnt + 2, 8, hipMemcpyDeviceToHost, s));
         ROGTK_HIP_CHECK(hipStreamSynchronize(s));
         const int64_t nd = (int64_t)hnd;
+        nd_all = nd;
         if (max_distance == 1) {
             hipLaunchKernelGGL(k_iota32, grid(nd), dim3(kB), 0, s, f, nd);
             // edges: one record (code with digit p zeroed, p, code) per distinct code and
             // position, grouped by (p, masked code) with two sorts (dist_cluster.hip, the
             // steps of the sharded engine at world 1) instead of one sort per position:
             // 1.7x faster at L = 20 (10M reads)
+            // positions in batches of <= rec_batch() records (nd * L may pass 2^31, the
+            // sorts' limit; the batch also bounds the 20 B/record scratch)
             int64_t ne = 0;
             {
-                const int64_t nrec = nd * (int64_t)L;
+                const int64_t per = std::max<int64_t>(1, std::min<int64_t>(L, rec_batch() / std::max<int64_t>(nd, 1)));
+                ROGTK_REQUIRE(nd < (1ll << 31), ROGTK_E_UNSUPPORTED, "long_cluster: 2^31 distinct UMIs");
+                const int64_t nrec_max = nd * per;
                 Arena R;
                 R.s = s;
-                R.cap = (size_t)nrec * 20 + 3 * 256;
+                R.cap = (size_t)nrec_max * 20 + 3 * 256;
                 ROGTK_HIP_CHECK(hipMallocAsync((void**)&R.base, R.cap, s));
-                uint64_t* rmk = R.take<uint64_t>(nrec);
-                uint32_t* rpos = R.take<uint32_t>(nrec);
-                uint64_t* rcode = R.take<uint64_t>(nrec);
-                int64_t one = 0;
-                if (int rc = rogtk_masked_records(D, nd, L, 1, rmk, rpos, rcode, &one, s)) return rc;
-                if (int rc = rogtk_clique_edges(rmk, rpos, rcode, nrec, L, D, nd, (uint32_t*)E, &ne, s)) return rc;
+                uint64_t* rmk = R.take<uint64_t>(nrec_max);
+                uint32_t* rpos = R.take<uint32_t>(nrec_max);
+                uint64_t* rcode = R.take<uint64_t>(nrec_max);
+                for (int p0 = 0; p0 < L; p0 += (int)per) {
+                    const int np = (int)std::min<int64_t>(per, L - p0);
+                    if (int rc = masked_records_range(D, nd, p0, np, rmk, rpos, rcode, s)) return rc;
+                    int64_t got = 0;
+                    if (int rc = rogtk_clique_edges(rmk, rpos, rcode, nd * np, L, D, nd, (uint32_t*)(E + ne), &got, s))
+                        return rc;
+                    ne += got;
+                }
             }
             for (int round = 0; ne > 0; ++round) {
                 ROGTK_REQUIRE(round < 4096, ROGTK_E_HIP, "long_cluster: union rounds did not converge");
@@ -275,14 +300,31 @@ int long_cluster(const void* offsets, int ow, const uint8_t* values, const uint8
         hipLaunchKernelGGL(k_assign_long, grid(nreg), dim3(kB), 0, s, srow, ex, nreg, f, rlab, max_distance, cid);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
-    int64_t n_irr_clusters = 0;
-    if (nirr > 0) {
+    int64_t total = n_reg_clusters;
+    if (nirr > 0 && max_distance == 1) {
+        // Hamming-1 edges of the irregular rows, merged with the regular clusters
+        // (irregular.hip); the lookup binary-searches the sorted distinct codes
+        const int64_t nd = n_reg_clusters > 0 ? nd_all : 0;
+        uint32_t* dlab = flag;  // free after the labels: one label per distinct code
+        if (nd > 0) {
+            hipLaunchKernelGGL(k_dlab, grid(nd), dim3(kB), 0, s, f, rlab, nd, dlab);
+            ROGTK_HIP_CHECK(hipGetLastError());
+        }
+        CodeLookup lk = [&](const uint64_t* q, int64_t nq, uint32_t* lab, hipStream_t st) {
+            return sorted_code_lookup(D, nd, dlab, q, nq, lab, st);
+        };
+        if (int rc = irregular_merge(offsets, ow, values, irr, nirr, max_len, L, n_reg_clusters, nd > 0 ? &lk : nullptr,
+                                     cid, n, cid, &total, s))
+            return rc;
+    } else if (nirr > 0) {
+        int64_t n_irr_clusters = 0;
         hipLaunchKernelGGL(k_put_count, dim3(1), dim3(1), 0, s, stats, n_reg_clusters);
         if (int rc = irregular_cluster(offsets, ow, values, irr, nirr, max_len, stats, cid, &n_irr_clusters, s))
             return rc;
+        total += n_irr_clusters;
     }
     ROGTK_HIP_CHECK(hipStreamSynchronize(s));
-    if (n_clusters) *n_clusters = n_reg_clusters + n_irr_clusters;
+    if (n_clusters) *n_clusters = total;
     return ROGTK_OK;
 }
 

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 
 #include "../../include/rogtk_hip.h"
 
@@ -55,15 +56,22 @@ extern const char* const kKernelNames[K_COUNT_];
 
 bool profiling_on();
 // Brackets one launch with HIP events on `stream` when profiling is enabled.
+// exact = true: the events are not recorded on the stream; the launcher attaches them to
+// the kernel's dispatch packet (hipExtLaunchKernelGGL(..., start(), stop(), ...)), so the
+// elapsed time is the kernel's own execution, as in rocprofv3's kernel trace.
 class ProfScope {
    public:
-    ProfScope(KernelId id, hipStream_t stream);
+    ProfScope(KernelId id, hipStream_t stream, bool exact = false);
     ~ProfScope();
+    hipEvent_t start() const { return start_; }
+    hipEvent_t stop() const { return stop_; }
 
    private:
     KernelId id_;
     hipStream_t stream_;
+    bool exact_ = false;
     hipEvent_t start_ = nullptr;
+    hipEvent_t stop_ = nullptr;
 };
 
 // ------------------------------------------------- entropy / ratio tables
@@ -240,6 +248,29 @@ int launch_cluster_assign(const ClusterLayout& cl, const uint8_t* ws, const uint
 int irregular_cluster(const void* offsets, int offset_width, const uint8_t* values,
                       const int64_t* rows, int64_t n_rows, int64_t max_len, const int64_t* stats_dev,
                       uint32_t* cluster_id, int64_t* n_irregular_clusters, hipStream_t s);
+
+// Labels of packed regular codes: lab[i] = the regular cluster id of code q[i], or
+// 0xFFFFFFFF when q[i] is ~0 or not a present code. Enqueued on s.
+using CodeLookup = std::function<int(const uint64_t* q, int64_t nq, uint32_t* lab, hipStream_t s)>;
+// max_distance 1 over the irregular rows (irregular.hip): Hamming-1 edges among the
+// distinct irregular strings and to the regular clusters (lookup; NULL: no regular
+// codes), connected components with the n_reg regular clusters, ids into cluster_id
+// (irregular rows) and, when regular clusters merged, relabel[0..relabel_n) remapped in
+// place (entries < n_reg). *n_clusters = all clusters. Synchronises s.
+int irregular_merge(const void* offsets, int offset_width, const uint8_t* values, const int64_t* rows,
+                    int64_t n_rows, int64_t max_len, int L, int64_t n_reg, const CodeLookup* lookup,
+                    uint32_t* relabel, int64_t relabel_n, uint32_t* cluster_id, int64_t* n_clusters, hipStream_t s);
+// lookup over a sorted code array G[ng] with one label per entry
+int sorted_code_lookup(const uint64_t* G, int64_t ng, const uint32_t* labels, const uint64_t* q, int64_t nq,
+                       uint32_t* lab, hipStream_t s);
+// lookup through a resolved (and assigned) bitmap-engine workspace
+int launch_cluster_lookup(const ClusterLayout& cl, const uint8_t* ws, const uint64_t* q, int64_t nq, uint32_t* lab,
+                          hipStream_t s);
+
+// records (code with digit p zeroed, p, code) of positions p0 .. p0+np-1 of every code of
+// D[nd] (dist_cluster.hip; world 1)
+int masked_records_range(const uint64_t* D, int64_t nd, int p0, int np, uint64_t* mk, uint32_t* pos, uint64_t* code,
+                         hipStream_t s);
 
 // H3 for 17 <= L <= 32 (sort-based, long_cluster.hip): regular + irregular rows of a
 // device column; ids into cid (device), *n_clusters on the host. Synchronises s.

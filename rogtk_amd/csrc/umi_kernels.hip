@@ -17,6 +17,8 @@
 // score are never fused into FMAs; f64 division is IEEE (correctly rounded).
 #include <cstdlib>
 
+#include <hip/hip_ext.h>
+
 #include "rogtk_internal.h"
 
 namespace rogtk {
@@ -500,7 +502,9 @@ int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int
     const bool score = any_score(o), hamd = p.ham_mode && hd, hamw = p.ham_mode && hw,
                mark = presence != nullptr;
     if (!score && !hamd && !hamw && !mark) return ROGTK_OK;
-    ProfScope prof(score || hamd || hamw ? K_SCORE_PACKED : K_MARK, s);
+    // exact: the profiling events ride on the dispatch packet (kernel execution time only,
+    // comparable with rocprofv3's kernel trace; bench.py's roofline.frac)
+    ProfScope prof(score || hamd || hamw ? K_SCORE_PACKED : K_MARK, s, true);
     // ROGTK_SCORE_BLOCKS=k: at most k workgroups, grid-stride (A/B; default full grid)
     static const int64_t cap = [] {
         const char* e = getenv("ROGTK_SCORE_BLOCKS");
@@ -511,8 +515,9 @@ int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int
     const int sel = (score ? 8 : 0) | (hamd ? 4 : 0) | (hamw ? 2 : 0) | (mark ? 1 : 0);
 #define ROGTK_SP(S, D, W, M)                                                                    \
     case (S * 8 + D * 4 + W * 2 + M):                                                          \
-        hipLaunchKernelGGL((k_score_packed<S, D, W, M>), dim3(g), dim3(kBlock), 0, s, codes, \
-                           regular_bits, n, p, o, hd, hw, presence);                          \
+        hipExtLaunchKernelGGL((k_score_packed<S, D, W, M>), dim3(g), dim3(kBlock), 0, s,       \
+                              prof.start(), prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, \
+                              presence);                                                         \
         break;
     // the bench / C2 configuration (12-bp UMIs, all fields + within bits) has a
     // length-specialised instance (ROGTK_SCORE_GENERIC=1: runtime-length kernel, A/B)
@@ -521,8 +526,8 @@ int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int
         return e && e[0] == '1';
     }();
     if (!generic && p.L == 12 && sel == 8 + 2) {
-        hipLaunchKernelGGL((k_score_packed<true, false, true, false, 12>), dim3(g), dim3(kBlock), 0, s, codes,
-                           regular_bits, n, p, o, hd, hw, presence);
+        hipExtLaunchKernelGGL((k_score_packed<true, false, true, false, 12>), dim3(g), dim3(kBlock), 0, s,
+                              prof.start(), prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, presence);
         ROGTK_HIP_CHECK(hipGetLastError());
         return ROGTK_OK;
     }

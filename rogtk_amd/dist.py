@@ -148,7 +148,8 @@ def route_rows(offsets: torch.Tensor, values: torch.Tensor, keys: torch.Tensor, 
 #   -> masked-key records of the owned codes -> all-to-all by hash(masked key, position)
 #   -> clique edges (indices into G) -> all-gather -> connected components on every rank
 #   -> rows: cluster id = label of the code's index in G
-#   irregular rows: all-gather their strings, exact-bytes ids after the regular clusters.
+#   irregular rows: all-gather their strings; exact bytes, or (max_distance 1) Hamming-1
+#   edges to each other and to G's codes, merged with the regular clusters.
 # Every rank computes the same G, edges and labels, so ids equal the single-GPU ids.
 # ---------------------------------------------------------------------------------------
 
@@ -228,6 +229,17 @@ class _HipOps:
         from . import _lib
         _lib.call("rogtk_assign_codes", self._p(codes), self._p(kind), int(codes.numel()), self._p(G),
                   int(G.numel()), self._p(labels), self._p(cid), self._stream())
+
+    def irregular_merge(self, offsets, values, n, max_len, L, md, G, labels, n_reg):
+        """ids of the n gathered irregular strings; labels (per G code) remapped in place."""
+        import ctypes
+        from . import _lib
+        ids = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+        k = ctypes.c_int64(0)
+        _lib.call("rogtk_irregular_merge", self._p(offsets), self._p(values), int(n), int(max_len), int(L), int(md),
+                  self._p(G), int(G.numel()), self._p(labels), int(n_reg), self._p(ids), ctypes.byref(k),
+                  self._stream())
+        return ids[:n], k.value
 
     def group_strings(self, offsets, values, n, max_len, base):
         import ctypes
@@ -336,20 +348,25 @@ def umi_cluster_sharded(offsets: torch.Tensor, values: torch.Tensor, n: int, umi
     else:
         labels = torch.arange(G.numel(), dtype=torch.int32, device=G.device)
         n_reg = G.numel()
-    cid = torch.full((max(n, 1),), -1, dtype=torch.int32, device=offsets.device)[:n]
-    ops.assign(codes, kind, G, labels, cid)
-    # irregular rows (N, lowercase, other lengths): exact bytes, ids after the regular ones
+    # irregular rows (N, lowercase, other lengths): their strings are all-gathered; exact
+    # bytes (max_distance 0) or Hamming-1 edges to each other and to G's codes, merged with
+    # the regular clusters (max_distance 1; labels remapped in place when clusters merge)
     irr = torch.nonzero(kind == 2).flatten()
     poff, pval = _irregular_strings(offsets, values, irr)
     lens = poff[1:] - poff[:-1]
     all_lens, counts = _allgather_var(lens, group)
     all_vals, _ = _allgather_var(pval, group)
-    n_irr_groups = 0
+    n_total = n_reg
+    ids = None
     if all_lens.numel():
         aoff = torch.zeros(all_lens.numel() + 1, dtype=torch.int64, device=all_lens.device)
         aoff[1:] = torch.cumsum(all_lens, 0)
-        ids, n_irr_groups = ops.group_strings(aoff, all_vals, all_lens.numel(), int(all_lens.max().item()), n_reg)
+        labels = labels.contiguous()
+        ids, n_total = ops.irregular_merge(aoff, all_vals, all_lens.numel(), int(all_lens.max().item()), L,
+                                           max_distance, G, labels, n_reg)
+    cid = torch.full((max(n, 1),), -1, dtype=torch.int32, device=offsets.device)[:n]
+    ops.assign(codes, kind, G, labels, cid)
+    if ids is not None and irr.numel():
         start = sum(counts[:rank])
-        if irr.numel():
-            cid[irr] = ids[start: start + irr.numel()].to(cid.device)
-    return cid, int(n_reg + n_irr_groups)
+        cid[irr] = ids[start: start + irr.numel()].to(cid.device)
+    return cid, int(n_total)

@@ -133,7 +133,11 @@ class UmiPipeline:
         self.reuse_gate = reuse_gate
 
     def submit(self, batch: D.PackedBatch):
-        """Enqueue one batch; returns its slot (outputs valid after drain() or a later event)."""
+        """Enqueue one batch; returns its slot. Scores and Hamming outputs are valid once the
+        slot's events have fired. Cluster ids (slot.cid) are FINAL only after drain(), after
+        settle(slot), or inside on_assigned: without on_assigned the assign is deferred and
+        may be built from the speculative rounds (slot.assigned / last_assigned mark that
+        assign, not a settled one); the slot is settled before its reuse."""
         slot = self.slots[self.k % len(self.slots)]
         self.main.wait_stream(torch.cuda.current_stream(self.main.device))  # batch producer -> main
         if self.assign_on == "resolve":
@@ -245,6 +249,17 @@ class UmiPipeline:
         slot.assigned = torch.cuda.Event()
         slot.assigned.record(self.s_assign)
         self.last_assigned = slot.assigned
+
+    def settle(self, slot):
+        """Make slot.cid final now (enqueues the slot's assign if it is still queued, waits
+        for its resolve's flags, re-runs the rounds, labels and assign in the rare
+        non-converged case); the current stream then waits for it. Returns slot.cid."""
+        while any(q[0] is slot for q in self.queue):
+            self._assign_oldest()
+        self._settle(slot, self.s_assign if self.assign_on == "separate" else None)
+        if slot.assigned is not None:
+            torch.cuda.current_stream(self.main.device).wait_event(slot.assigned)
+        return slot.cid
 
     def drain(self):
         """Finish every submitted batch; the main stream waits for the last assign."""

@@ -22,3 +22,33 @@ def _built():
 
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def irregular_families(seed, n_parents, L, fam=6, p_sub=0.08, p_n=0.05, p_lower=0.03, p_len=0.05, alphabet=b"ACGT"):
+    """UMI families whose members carry substitutions, N, lowercase bytes and length
+    changes at high rates, so Hamming-1 edges join irregular strings to regular codes,
+    to each other, and bridge regular clusters (the H3.2 spec)."""
+    import numpy as np
+
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n_parents):
+        parent = bytearray(rng.choice(list(alphabet), size=L).astype(np.uint8).tobytes())
+        for _ in range(int(rng.integers(1, fam + 1))):
+            u = bytearray(parent)
+            for q in range(L):
+                r = rng.random()
+                if r < p_sub:
+                    u[q] = int(rng.choice(list(alphabet)))
+                elif r < p_sub + p_n:
+                    u[q] = ord("N")
+                elif r < p_sub + p_n + p_lower:
+                    u[q] = u[q] | 0x20
+            r = rng.random()
+            if r < p_len / 2:
+                u = u[:-1]
+            elif r < p_len:
+                u = u + b"A"
+            out.append(bytes(u))
+    out += [None, b"", b"N" * L, b"n" * L]
+    return out

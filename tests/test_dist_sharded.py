@@ -29,7 +29,12 @@ def _free_port():
 
 
 def make_column(n: int, L: int, seed: int):
-    """UMI strings with Hamming-1 families, irregular rows and nulls (list of bytes|None)."""
+    """UMI strings with Hamming-1 families, irregular rows and nulls (list of bytes|None).
+    A negative seed gives irregular_families (N / lowercase / length changes at high rates)."""
+    if seed < 0:
+        from conftest import irregular_families
+        out = irregular_families(-seed, n, L)  # >= n rows; keep the edge rows at the end
+        return out[:n - 4] + out[-4:]
     rng = np.random.default_rng(seed)
     parents = rng.integers(0, 4, size=(max(n // 6, 1), L))
     acgt = np.frombuffer(b"ACGT", np.uint8)
@@ -151,6 +156,54 @@ class NumpyOps:
                 assert j < len(g) and g[j] == c[i]
                 out[i] = labels[j]
 
+    def irregular_merge(self, offsets, values, n, max_len, L, md, G, labels, n_reg):
+        """rogtk_irregular_merge: exact bytes (md 0) or Hamming-1 edges among the strings
+        and to G's codes, components with the regular clusters (md 1)."""
+        off = offsets.numpy()
+        val = values.numpy().tobytes()
+        strs = [val[off[i]:off[i + 1]] for i in range(n)]
+        order = sorted(set(strs))
+        rank = {s: i for i, s in enumerate(order)}
+        if md == 0:
+            return torch.tensor([n_reg + rank[s] for s in strs], dtype=torch.int32), n_reg + len(order)
+        g = G.numpy().view(np.uint64)
+        lab = labels.numpy()
+        f = list(range(n_reg + len(order)))
+
+        def find(x):
+            while f[x] != x:
+                x = f[x]
+            return x
+
+        def unite(a, b):
+            ra, rb = find(a), find(b)
+            if ra != rb:
+                f[max(ra, rb)] = min(ra, rb)
+
+        first = {}
+        for j, s in enumerate(order):
+            for p in range(len(s)):
+                key = (p, s[:p] + s[p + 1:])
+                if key in first:
+                    unite(n_reg + first[key], n_reg + j)
+                else:
+                    first[key] = j
+            bad = [q for q in range(len(s)) if s[q] not in b"ACGT"]
+            if len(s) == L and len(bad) == 1:
+                for x in b"ACGT":
+                    t = s[:bad[0]] + bytes([x]) + s[bad[0] + 1:]
+                    c = 0
+                    for ch in t:
+                        c = (c << 2) | b"ACGT".index(ch)
+                    i = int(np.searchsorted(g, np.uint64(c)))
+                    if i < len(g) and g[i] == c:
+                        unite(int(lab[i]), n_reg + j)
+        roots = sorted({find(v) for v in range(len(f))})
+        dense = {r: i for i, r in enumerate(roots)}
+        for i in range(len(lab)):
+            lab[i] = dense[find(int(lab[i]))]
+        return torch.tensor([dense[find(n_reg + rank[s])] for s in strs], dtype=torch.int32), len(roots)
+
     def group_strings(self, offsets, values, n, max_len, base):
         off = offsets.numpy()
         val = values.numpy().tobytes()
@@ -187,11 +240,11 @@ def _worker(rank, world, port, L, md, n, seed, out_q):
 
 
 @pytest.mark.parametrize("world", [1, 2, 3])
-@pytest.mark.parametrize("L,md", [(8, 1), (20, 1), (32, 1), (20, 0)])
-def test_sharded_cluster_plan_matches_oracle(world, L, md):
+@pytest.mark.parametrize("L,md,irr", [(8, 1, 0), (20, 1, 0), (32, 1, 0), (20, 0, 0), (6, 1, 1), (12, 1, 1)])
+def test_sharded_cluster_plan_matches_oracle(world, L, md, irr):
     from oracle import pyoracle as P
 
-    n, seed = 900, 7 + L
+    n, seed = 900, (-(3 + L) if irr else 7 + L)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

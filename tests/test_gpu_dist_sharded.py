@@ -28,15 +28,17 @@ def rg():
     return rogtk_amd
 
 
-@pytest.mark.parametrize("L,md,n", [(12, 1, 30_000), (12, 0, 30_000), (20, 1, 30_000), (32, 1, 20_000),
-                                    (7, 1, 5_000), (1, 1, 300), (16, 1, 40_000)])
-def test_sharded_world1_matches_oracle_and_engine(rg, L, md, n):
+@pytest.mark.parametrize("L,md,n,irr", [(12, 1, 30_000, 0), (12, 0, 30_000, 0), (20, 1, 30_000, 0),
+                                        (32, 1, 20_000, 0), (7, 1, 5_000, 0), (1, 1, 300, 0), (16, 1, 40_000, 0),
+                                        (6, 1, 3_000, 1), (12, 1, 3_000, 1), (24, 1, 3_000, 1)])
+def test_sharded_world1_matches_oracle_and_engine(rg, L, md, n, irr):
+    """irr: N / lowercase / length-change families (Hamming-1 edges of irregular strings)."""
     import pyarrow as pa
 
     from oracle import pyoracle as P
     from rogtk_amd import dist as RD
 
-    col = make_column(n, L, seed=L * 3 + md)
+    col = make_column(n, L, seed=-(L * 3 + md) if irr else L * 3 + md)
     off, vals, vbits = (t.cuda() for t in _arrow(col))
     cid, k = RD.umi_cluster_sharded(off, vals, n, L, md, validity=vbits)
     torch.cuda.synchronize()
@@ -80,11 +82,11 @@ def _worker(rank, world, port, L, md, n, seed, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("L,md", [(12, 1), (24, 1), (32, 0)])
-def test_sharded_world2_matches_oracle(rg, L, md):
+@pytest.mark.parametrize("L,md,irr", [(12, 1, 0), (24, 1, 0), (32, 0, 0), (12, 1, 1), (24, 1, 1)])
+def test_sharded_world2_matches_oracle(rg, L, md, irr):
     from oracle import pyoracle as P
 
-    world, n, seed = 2, 20_000, 11 + L
+    world, n, seed = 2, (4_000 if irr else 20_000), (-(11 + L) if irr else 11 + L)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

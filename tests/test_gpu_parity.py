@@ -270,6 +270,28 @@ def test_long_cluster_bruteforce_and_chains(rg, L):
     assert got.to_pylist() == ref
 
 
+def test_long_cluster_position_batches(rg, monkeypatch):
+    """The long engine finds its edges in batches of positions when nd * L passes the
+    record budget (ROGTK_LONG_REC_BATCH lowered): ids equal the one-batch run."""
+    rng = np.random.default_rng(5)
+    L = 24
+    umis = []
+    for _ in range(3000):
+        u = bytearray(_random_strings(rng, 1, [L])[0])
+        for _ in range(int(rng.integers(1, 6))):
+            j = int(rng.integers(L))
+            u[j] = b"ACGT"[int(rng.integers(4))]
+            umis.append(bytes(u))
+    col = pa.array(umis, type=pa.large_binary())
+    ref, rk = rg.umi_cluster(col, L, 1)[:2]
+    for batch in ("1", "5000", "40000"):
+        monkeypatch.setenv("ROGTK_LONG_REC_BATCH", batch)
+        got, k, _ = rg.umi_cluster(col, L, 1)
+        assert k == rk and got.to_pylist() == ref.to_pylist(), batch
+    rc, _, ok, _ = P().umi_cluster(P().StrCol.from_list(umis), L, 1)
+    assert ok == rk and np.array_equal(_np(ref).astype(np.uint32), rc)
+
+
 def test_cluster_dev_matches_host_long_and_short(rg):
     """rogtk_umi_cluster_dev (device column) == rogtk_umi_cluster_host, both engines."""
     import ctypes
@@ -288,6 +310,56 @@ def test_cluster_dev_matches_host_long_and_short(rg):
                   ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
         assert nk.value == k
         assert np.array_equal(cid.cpu().numpy().view(np.uint32), _np(host).astype(np.uint32))
+
+
+@pytest.mark.parametrize("L", [4, 6, 8, 12, 13, 16, 20, 32, 33])
+def test_cluster_irregular_families(rg, L):
+    """SURVEY §8a H3.2 for every engine: strings with N, lowercase bytes and other lengths
+    get Hamming-1 edges to each other and to regular codes (and bridge regular clusters);
+    host and device-column paths vs the oracle and the O(d^2) brute force."""
+    import ctypes
+    import torch
+    from conftest import irregular_families
+    from rogtk_amd import _lib
+
+    umis = irregular_families(L, 400 if L <= 8 else 700, L)
+    col = P().StrCol.from_list(umis)
+    for md in (0, 1):
+        rc, rv, rk, _ = P().umi_cluster(col, L, md)
+        ref, bk = P().py_cluster_bruteforce(umis, L, md)
+        assert rk == bk
+        got, k, rl = rg.umi_cluster(pa.array(umis, type=pa.large_binary()), L, md)
+        assert rl == L and k == rk, (md, k, rk)
+        assert got.to_pylist() == ref
+        # device column (rogtk_umi_cluster_dev, nulls as empty strings -> compare valid rows)
+        dense = [u if u is not None else b"" for u in umis]
+        off = torch.tensor(np.concatenate([[0], np.cumsum([len(u) for u in dense])]), dtype=torch.int64).cuda()
+        val = torch.tensor(np.frombuffer(b"".join(dense) or b"\0", np.uint8).copy()).cuda()
+        vbits = torch.from_numpy(np.packbits(np.array([u is not None for u in umis] + [False] * 7),
+                                             bitorder="little")).cuda()
+        cid = torch.empty(len(umis), dtype=torch.int32, device="cuda")
+        nk = ctypes.c_int64(0)
+        _lib.call("rogtk_umi_cluster_dev", ctypes.c_void_p(off.data_ptr()), ctypes.c_void_p(val.data_ptr()),
+                  ctypes.c_void_p(vbits.data_ptr()), len(umis), L, md, ctypes.c_void_p(cid.data_ptr()),
+                  ctypes.byref(nk), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        assert nk.value == rk
+        assert np.array_equal(cid.cpu().numpy().view(np.uint32)[rv], rc[rv])
+
+
+@pytest.mark.parametrize("L", [12, 24])
+def test_cluster_n_stress_large(rg, L):
+    """200k synth reads with N at 1e-3/base and lowercase at 5e-4/base (SURVEY §8d's
+    N-stress variant): ids equal the oracle."""
+    from rogtk_amd import synth
+
+    umis = [bytes(r) for r in synth.umi_ascii(200_000, L, p_n=1e-3, p_lower=5e-4)]
+    col = P().StrCol.from_list(umis)
+    rc, rv, rk, _ = P().umi_cluster(col, L, 1)
+    got, k, _ = rg.umi_cluster(pa.array(umis, type=pa.large_binary()), L, 1)
+    assert k == rk
+    assert np.array_equal(_np(got).astype(np.uint32), rc)
+    n_irr = sum(1 for u in umis if any(c not in b"ACGT" for c in u))
+    assert n_irr > 1000
 
 
 def test_cluster_bruteforce_small(rg):
@@ -492,6 +564,35 @@ def test_pipeline_deferred_assign(rg, depth, nb, spec, assign_on, gate):
         assert np.array_equal(slot.scores["combined_score"][:n].cpu().numpy().view(np.uint64),
                               scores["combined_score"][:n].cpu().numpy().view(np.uint64)), k
         assert np.array_equal(slot.within.cpu().numpy()[:len(hw)], hw.cpu().numpy()), k
+
+
+def test_pipeline_settle_gives_final_ids(rg):
+    """settle(slot) right after submit (1 speculative round: every batch needs the deferred
+    completion) returns the final ids of that batch, mid-stream."""
+    import torch
+
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+    from rogtk_amd.pipeline import UmiPipeline
+
+    n, L = 150_001, 12
+    seeds = [synth.DEFAULT_SEED + 31 * k for k in range(4)]
+    try:
+        D.set_spec_rounds(1)
+        pipe = UmiPipeline(L, n, n, "cuda", depth=2, target=b"ACGTACGTACGT", max_distance=1, score_alone=True)
+        keep, got = [], []
+        for s in seeds:
+            codes = torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda()
+            keep.append(D.PackedBatch(codes, L))
+            slot = pipe.submit(keep[-1])
+            got.append(pipe.settle(slot)[:n].clone())
+        pipe.drain()
+        torch.cuda.synchronize()
+    finally:
+        D.set_spec_rounds(0)
+    for k, s in enumerate(seeds):
+        cid = _device_run(n, seed=s)[4]
+        assert np.array_equal(got[k].cpu().numpy(), cid.cpu().numpy()), k
 
 
 def _chain_codes(rng, L, length, high_bases):

@@ -144,16 +144,46 @@ def test_cluster_oracle_vs_bruteforce(md):
 
 
 def test_cluster_spec_properties():
-    """Ids are dense, ordered by each cluster's smallest UMI, transitive for d=1."""
-    umis = [b"AAAA", b"AAAC", b"AACC", b"TTTT", b"GGGG", b"GGGA", b"CCCC", b"AAAN", b"AAAN", None]
+    """Ids are dense, ordered by each cluster's smallest UMI, transitive for d=1; strings
+    with N join the regular clusters they are 1 byte away from."""
+    umis = [b"AAAA", b"AAAC", b"AACC", b"TTTT", b"GGGG", b"GGGA", b"CCCC", b"AAAN", b"AAAN", None, b"NNCN", b"NNNN"]
     cid, valid, k, _ = P.umi_cluster(P.StrCol.from_list(umis), 4, 1)
     ids = dict(zip(umis, cid))
-    assert ids[b"AAAA"] == ids[b"AAAC"] == ids[b"AACC"] == 0  # chain AAAA-AAAC-AACC
+    assert ids[b"AAAA"] == ids[b"AAAC"] == ids[b"AACC"] == ids[b"AAAN"] == 0  # AAAN ~ AAAA
     assert ids[b"CCCC"] == 1 and ids[b"GGGA"] == ids[b"GGGG"] == 2 and ids[b"TTTT"] == 3
-    assert ids[b"AAAN"] == 4  # irregular rows after the regular clusters
-    assert k == 5 and not valid[-1]
+    assert ids[b"NNCN"] == ids[b"NNNN"] == 4  # irregular-only cluster after the regular ones
+    assert k == 5 and not valid[-3]
     cid0, _, k0, _ = P.umi_cluster(P.StrCol.from_list(umis), 4, 0)
-    assert k0 == 8  # 7 distinct regular + 1 irregular
+    assert k0 == 10  # 7 distinct regular + 3 irregular
+
+
+def test_cluster_irregular_bridges_regular_clusters():
+    """AAGT ~ ANGT ~ ANNT ~ ACNT ~ ACAT: two regular clusters (2 bytes apart) merge
+    through strings with N; the merged id is the one of the smaller code."""
+    umis = [b"ACAT", b"AAGT", b"ANGT", b"ANNT", b"ACNT", b"TTTT"]
+    cid, valid, k, _ = P.umi_cluster(P.StrCol.from_list(umis), 4, 1)
+    assert list(cid) == [0, 0, 0, 0, 0, 1] and k == 2
+    cid, valid, k, _ = P.umi_cluster(P.StrCol.from_list(umis[:2] + umis[5:]), 4, 1)
+    assert list(cid) == [1, 0, 2] and k == 3
+    # lowercase and other lengths: ordinary bytes; other lengths cluster among themselves
+    umis = [b"acgt", b"acga", b"ACGTA", b"ACGTC", b"ACG", b"ACGT", b"aCGT"]
+    cid, valid, k, _ = P.umi_cluster(P.StrCol.from_list(umis), 4, 1)
+    ids = dict(zip(umis, cid))
+    assert ids[b"ACGT"] == ids[b"aCGT"] == 0
+    assert ids[b"acgt"] == ids[b"acga"] and ids[b"ACGTA"] == ids[b"ACGTC"]
+    assert len({ids[b"ACG"], ids[b"ACGTA"], ids[b"acgt"], 0}) == 4 and k == 4
+
+
+@pytest.mark.parametrize("seed,L", [(1, 4), (2, 6), (3, 12), (4, 20), (5, 33)])
+def test_cluster_oracle_vs_bruteforce_irregular_families(seed, L):
+    from conftest import irregular_families
+
+    umis = irregular_families(seed, 120 if L <= 6 else 250, L)
+    for md in (0, 1):
+        ref, rk = P.py_cluster_bruteforce(umis, L, md)
+        cid, valid, k, rl = P.umi_cluster(P.StrCol.from_list(umis), L, md)
+        assert rl == L and k == rk
+        assert [int(c) if v else None for c, v in zip(cid, valid)] == ref
 
 
 # ---------------------------------------------------------------- H4 k-mer oracle
