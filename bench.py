@@ -15,8 +15,13 @@ batches in flight; the timed region ends after every submitted batch is done):
 Weak scaling: every rank owns reads_per_gpu records of one global dataset
 (shard by record); value = all ranks' reads / max-over-ranks wall time.
 
-Usage: python bench.py [--gpus N --steps K --warmup W]
+Workloads (--workload): C2 (default; BASELINE configs[1]) = 10M reads per GPU, weak
+scaling; C4 (configs[3]) = 500M reads in all, 500M/N per GPU, strong scaling.
+
+Usage: python bench.py [--gpus N --steps K --warmup W] [--workload C2|C4]
        torchrun --nproc-per-node N bench.py --gpus N ...
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N ranks itself
+(rogtk_amd.launch: spawned processes, one per GPU, before anything touches the GPU).
 """
 from __future__ import annotations
 
@@ -49,12 +54,18 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--reads-per-gpu", type=int, default=10_000_000)
+    ap.add_argument("--workload", choices=("C2", "C4"), default="C2",
+                    help="C2: 10M reads per GPU (weak scaling); C4: 500M reads over all GPUs (strong scaling)")
+    ap.add_argument("--reads-per-gpu", type=int, default=None,
+                    help="override the workload's reads per GPU (C2 default 10M)")
+    ap.add_argument("--total-reads", type=int, default=500_000_000, help="C4: reads over all GPUs")
     ap.add_argument("--umi-len", type=int, default=12)
     ap.add_argument("--max-distance", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip in-run HIP-event kernel timing")
+    ap.add_argument("--no-end-to-end", action="store_true",
+                    help="skip the host Arrow in -> host Arrow out measurement (level-2 entry points)")
     ap.add_argument("--iso-launches", type=int, default=10, help="isolated score-kernel launches after timing")
     ap.add_argument("--depth", type=int, default=2, help="batches in flight (1 = no cross-batch overlap)")
     ap.add_argument("--mark", choices=("auto", "xcd", "fused", "sort", "slices"), default="auto",
@@ -89,6 +100,8 @@ def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     if world > 1:
         # ROGTK_DIST_BACKEND=gloo (tests only): several ranks may then share one GPU
         backend = os.environ.get("ROGTK_DIST_BACKEND", "nccl")
@@ -98,6 +111,8 @@ def setup_dist(args):
         else:
             torch.cuda.set_device(local % torch.cuda.device_count())
             dist.init_process_group(backend)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: the process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
     else:
         torch.cuda.set_device(0)
     return world, rank
@@ -133,15 +148,63 @@ def cpu_baseline(codes_h: np.ndarray, L: int, md: int, budget_s: float):
     return out
 
 
-def cpu_baseline_threads(codes_h: np.ndarray, L: int, md: int, threads: int = 16):
-    """The same sample with H1 + H2 split over `threads` host threads (the oracle's C loops
-    release the GIL; row-parallel like a rayon/polars thread pool) and H3 on one thread
-    (the oracle's union-find is serial)."""
+def end_to_end(codes_h: np.ndarray, L: int, md: int, iters: int = 3):
+    """The drop-in boundary path on the same column: host Arrow LargeUtf8 buffers in ->
+    rogtk_umi_complexity_host + rogtk_hamming_host + rogtk_umi_cluster_host (the three
+    plugin calls a polars pipeline makes, expressions.rs:1234-1284, 1075-1101, and the
+    caller's group_by) -> host Arrow arrays out. Every call uploads the column (the
+    plugin ABI hands each expression its input); results land in pinned buffers
+    (rogtk_host_alloc), so the D2H is direct DMA."""
+    import pyarrow as pa
+
+    import rogtk_amd as rg
+
+    n = len(codes_h)
+    asc = synth.codes_to_ascii(codes_h, L)
+    offs = np.arange(0, (n + 1) * L, L, dtype=np.int64)
+    col = pa.Array.from_buffers(pa.large_binary(), n, [None, pa.py_buffer(offs), pa.py_buffer(asc.reshape(-1))])
+    calls = {"umi_complexity_host": lambda: rg.umi_complexity_scores(col),
+             "hamming_host": lambda: rg.hamming_within(col, TARGET, 1),
+             "umi_cluster_host": lambda: rg.umi_cluster(col, L, md)}
+    for f in calls.values():  # warm: device buffers, pinned staging and result blocks
+        f()
+    ms = {k: [] for k in calls}
+    for _ in range(iters):
+        for k, f in calls.items():
+            t0 = time.perf_counter()
+            r = f()
+            ms[k].append(1000 * (time.perf_counter() - t0))
+            del r
+    best = {k: min(v) for k, v in ms.items()}
+    total = sum(best.values())
+    pcie = 3 * (8 + L) + (48 + 4) + 1 / 8 + 4  # 3 uploads of the column; H1 + H2 bits + H3 ids back
+    return {"value": round(n / (total / 1000), 1), "unit": "reads/s", "reads": n,
+            "ms": {k: round(v, 2) for k, v in best.items()},
+            "pcie_bytes_per_read": round(pcie, 3), "pcie_GBps": round(n * pcie / (total / 1000) / 1e9, 2),
+            "path": "host Arrow LargeUtf8 -> rogtk_umi_complexity_host + rogtk_hamming_host + "
+                    "rogtk_umi_cluster_host -> host Arrow (pinned result buffers); best of "
+                    f"{iters} after a warm-up call"}
+
+
+def host_threads() -> int:
+    """Host threads this job may use: OMP_NUM_THREADS (the GPU box sets the job's CPU
+    share there, 16 per GPU) or every core os.cpu_count() shows."""
+    n = os.cpu_count() or 1
+    try:
+        return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", n))))
+    except ValueError:
+        return n
+
+
+def cpu_baseline_threads(codes_h: np.ndarray, L: int, md: int, threads: int = 0):
+    """The same sample on `threads` host threads: H1 + H2 row-parallel (the oracle's C loops
+    release the GIL; like a polars thread pool over chunks) and H3 through the oracle's
+    threaded union-find (row passes + edge search split over the threads; identical ids)."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import pyoracle as P
 
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    threads = threads or host_threads()
     k = len(codes_h)
     asc = synth.codes_to_ascii(codes_h, L)
     cuts = np.linspace(0, k, threads + 1).astype(np.int64)
@@ -156,30 +219,37 @@ def cpu_baseline_threads(codes_h: np.ndarray, L: int, md: int, threads: int = 16
     with ThreadPoolExecutor(threads) as ex:
         list(ex.map(h12, parts))
     t1 = time.perf_counter()
-    P.umi_cluster(col, L, md)
+    P.umi_cluster(col, L, md, threads=threads)
     t2 = time.perf_counter()
     return {"value": k / (t2 - t0), "unit": "reads/s", "cores": threads, "kind": "port",
-            "sample": f"same {k} reads: H1+H2 on {threads} threads {t1 - t0:.2f} s, H3 serial {t2 - t1:.2f} s"}
+            "sample": f"same {k} reads, every stage on {threads} host threads (OMP_NUM_THREADS share of "
+                      f"{os.cpu_count()} cores): H1+H2 {t1 - t0:.2f} s, H3 (threaded union-find) {t2 - t1:.2f} s"}
 
 
-def load_traffic():
-    """Per-launch HBM bytes of k_score_packed from the latest committed PMC summary, if any."""
+def load_traffic(reads_per_launch: int):
+    """Per-launch HBM bytes of k_score_packed from the latest committed PMC summary made
+    at the same reads per launch, if any."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
-    if not files:
-        return None, None
-    try:
-        with open(files[-1]) as f:
-            j = json.load(f)
-        return j.get("score_packed_hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
-    except Exception:
-        return None, None
+    for path in reversed(files):
+        try:
+            with open(path) as f:
+                j = json.load(f)
+        except Exception:
+            continue
+        if j.get("reads_per_launch", 10_000_000) == reads_per_launch and j.get("score_packed_hbm_bytes_per_launch"):
+            return j["score_packed_hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
 
 
 def main():
     args = parse()
     world, rank = setup_dist(args)
-    L, md, n = args.umi_len, args.max_distance, args.reads_per_gpu
-    n_total = n * world
+    L, md = args.umi_len, args.max_distance
+    if args.workload == "C4":  # strong scaling: a fixed total split over the ranks
+        n_total = args.total_reads if args.reads_per_gpu is None else args.reads_per_gpu * world
+    else:  # C2, weak scaling: a fixed shard per rank
+        n_total = (args.reads_per_gpu or 10_000_000) * world
+    n = -(-n_total // world)
     start, count = RD.shard_range(n_total, rank, world)
     codes_h = synth.umi_codes(n_total, L, start=start, count=count)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -247,8 +317,13 @@ def main():
     if not args.no_profile:
         D.profile_enable(False)
         ms, launches = D.profile_read("score_packed")
-        if launches:
-            kernels["score_packed"] = {"avg_us": 1000.0 * ms / launches, "launches": launches}
+        sms, slaunches = D.profile_read_span("score_packed")
+        if slaunches:
+            # the kernel's own execution span (in-kernel device clock: first workgroup in ->
+            # last out, what rocprofv3's kernel trace reports); the bracketing stream events
+            # also time their own fences (~15 us more per launch)
+            kernels["score_packed"] = {"avg_us": 1000.0 * sms / slaunches, "launches": slaunches,
+                                       "event_avg_us": 1000.0 * ms / launches if launches else None}
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -285,7 +360,7 @@ def main():
             D.score_packed(batch, slot.scores, TARGET, 1, None, slot.within)
         torch.cuda.synchronize()
         D.profile_enable(False)
-        ms, launches = D.profile_read("score_packed")
+        ms, launches = D.profile_read_span("score_packed")
         if launches:
             iso = 1000.0 * ms / launches
 
@@ -302,11 +377,16 @@ def main():
     if "score_packed" in kernels:
         avg_s = kernels["score_packed"]["avg_us"] * 1e-6
         achieved = count * bpr / avg_s / 1e9
-        traffic, src = load_traffic()
+        traffic, src = load_traffic(count)
         roof = {"kernel": "k_score_packed", "bound": "hbm", "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "traffic_source": src,
                 "algorithmic_bytes_per_launch": int(count * bpr), "bytes_per_read": bpr,
+                "avg_us": round(kernels["score_packed"]["avg_us"], 2),
+                "timing": "in-kernel span (device wall clock, first workgroup entry to last exit) of every "
+                          "launch in the timed region",
+                "event_avg_us": (round(kernels["score_packed"]["event_avg_us"], 2)
+                                 if kernels["score_packed"]["event_avg_us"] else None),
                 "measured_over": f"timed region, {args.depth} batches in flight (kernel overlaps the resolve "
                                  f"of the previous batch" + (" and assign" if args.overlap_score else "") + ")"}
         if iso:
@@ -314,6 +394,9 @@ def main():
             roof["isolated"] = {"avg_us": round(iso, 2), "achieved": round(a_iso, 1),
                                 "frac": round(a_iso / HBM_PEAK_GBS, 4), "launches": args.iso_launches,
                                 "note": "same kernel, same batch, launched alone after the timed region"}
+    e2e = None
+    if not args.no_end_to_end and args.emulate_ranks == 1:
+        e2e = end_to_end(codes_h[: min(count, 10_000_000)], L, md)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(codes_h, L, md, args.cpu_seconds)
@@ -327,12 +410,15 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.workload == "C4" else "weak",
         "vs_baseline": None,
         "dtype": "u32/f64",
         "data": "synthetic (synth-v1: seeded 12-bp UMIs, N/10 molecules, 0.001/base UMI errors), packed 2-bit SoA resident in HBM",
-        "config": {"workload": "C2: 10M reads per GPU, 12-bp UMI, H1 complexity (7 fields) + H2 Hamming-within + "
-                               "H3 Hamming<=1 cluster ids",
+        "config": {"workload": (f"C4: {n_total // 1_000_000}M reads over {world} GPU(s), " if args.workload == "C4"
+                                else f"C2: {count // 1_000_000}M reads per GPU, ")
+                               + f"{L}-bp UMI, H1 complexity (7 fields) + H2 Hamming-within + H3 Hamming<=1 "
+                                 "cluster ids",
+                   "total_reads": n_total,
                    "reads_per_gpu": count, "umi_len": L, "max_distance": md,
                    "n_distinct": stats["n_distinct"], "n_clusters": stats["n_clusters"],
                    "h3_global": {"uf": "one-pass union-find", "rounds": "hook+jump rounds",
@@ -345,6 +431,7 @@ def main():
                                   + (f" (rank 0 of {args.emulate_ranks} EMULATED on one GPU, no RCCL)"
                                      if args.emulate_ranks > 1 else "")},
         "roofline": roof,
+        "end_to_end": e2e,
         "cpu_baseline": cpu,
         "kernels_us": breakdown,
     }
@@ -353,5 +440,20 @@ def main():
         dist.destroy_process_group()
 
 
+def _rank_main(argv):
+    sys.argv = [sys.argv[0]] + list(argv)
+    main()
+
+
 if __name__ == "__main__":
+    _args = parse()
+    if _args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU, started before anything touches the GPU (device_count()
+        # does not initialise HIP on this image)
+        from rogtk_amd.launch import run_local_ranks
+
+        # (ROGTK_DIST_BACKEND=gloo, tests only: ranks may share a GPU)
+        if os.environ.get("ROGTK_DIST_BACKEND", "nccl") == "nccl" and torch.cuda.device_count() < _args.gpus:
+            raise SystemExit(f"bench.py: --gpus {_args.gpus} but {torch.cuda.device_count()} GPU(s) visible")
+        sys.exit(run_local_ranks(_args.gpus, _rank_main, (sys.argv[1:],)))
     main()

@@ -53,6 +53,11 @@ const char* rogtk_version(void);
 const char* rogtk_last_error(void);
 /* Number of visible HIP devices (0 when none). */
 int rogtk_device_count(int* out_count);
+/* Pinned host memory for Arrow buffers the caller hands to the level-2 (host) entry
+ * points: copies to / from it are direct DMA (pageable memory is staged through the
+ * calling thread's pinned buffers). Blocks are cached for reuse after rogtk_host_free. */
+int rogtk_host_alloc(size_t bytes, void** out);
+int rogtk_host_free(void* p);
 
 /*
  * Output set of UMI complexity scoring: ComplexityScore (umi_score.rs:5-13)
@@ -322,6 +327,23 @@ int rogtk_kmer_spectrum_dev(const int64_t* offsets, const uint8_t* values, const
                             const int64_t* group_offsets, int64_t n_groups, int k, int64_t min_coverage,
                             int64_t capacity, uint64_t* kmers, uint8_t* exts, uint16_t* counts,
                             int64_t* entry_offsets, int64_t* group_stats, int64_t* n_entries, void* stream);
+/* A read column (int64 offsets, uint8 values, optional validity) packed once, in column
+ * order, into fixed-size 2-bit blocks of block_words u64 per row (blocks: n * block_words):
+ * word 0 = byte length | ACGT-clean << 32 (0xFFFFFFFF for a null row), then the bases, 32
+ * per word, first base most significant. block_words = rogtk_read_block_words(max_len):
+ * 8, 16 or 32 (rows up to 224 / 480 / 992 bases), 0 when the column is too long. */
+int rogtk_read_block_words(int64_t max_len);
+int rogtk_pack_reads(const int64_t* offsets, const uint8_t* values, const uint8_t* validity, int64_t validity_offset,
+                     int64_t n, int block_words, uint64_t* blocks, void* stream);
+/* rogtk_kmer_spectrum_dev over a column packed by rogtk_pack_reads (same outputs,
+ * bit-exact): each grouped row is staged from its block (whole 64-B lines) instead of
+ * its ASCII bytes. offsets / values stay needed (capacities, the radix path). */
+int rogtk_kmer_spectrum_blocks(const uint64_t* blocks, int block_words, int64_t max_len, const int64_t* offsets,
+                               const uint8_t* values, const uint8_t* validity, int64_t validity_offset,
+                               const int64_t* rows, int64_t n_rows, const int64_t* group_offsets, int64_t n_groups,
+                               int k, int64_t min_coverage, int64_t capacity, uint64_t* kmers, uint8_t* exts,
+                               uint16_t* counts, int64_t* entry_offsets, int64_t* group_stats, int64_t* n_entries,
+                               void* stream);
 /* polars group_by over u32 keys on the device (e.g. H3 cluster ids): rows_out[n] =
  * row indices ordered by key (stable), group_offsets_out[0 .. *n_groups] their
  * group boundaries (capacity n + 1). Synchronises the stream. */
@@ -540,6 +562,11 @@ int rogtk_profile_reset(void);
  * "cluster_mark", "cluster_bitmap", "cluster_scan", "cluster_compact",
  * "cluster_union", "cluster_flatten", "cluster_label", "cluster_assign". */
 int rogtk_profile_read(const char* kernel, double* total_ms, int64_t* launches);
+/* Kernels that support it (k_score_packed) also time their own execution span while
+ * profiled: max over workgroups of the exit clock - min of the entry clock (device
+ * wall clock), i.e. the duration rocprofv3's kernel trace reports, without the fences of
+ * the bracketing stream events. Totals since rogtk_profile_reset. */
+int rogtk_profile_read_span(const char* kernel, double* total_ms, int64_t* launches);
 
 #ifdef __cplusplus
 }

@@ -53,6 +53,8 @@ def lib():
         L.oracle_hamming_batch.restype = None
         L.oracle_umi_cluster.argtypes = [vp, i32, vp, vp, i64, i64, i32, i32, vp, vp, vp]
         L.oracle_umi_cluster.restype = i64
+        L.oracle_umi_cluster_mt.argtypes = [vp, i32, vp, vp, i64, i64, i32, i32, vp, vp, vp, i32]
+        L.oracle_umi_cluster_mt.restype = i64
         L.oracle_plogp.argtypes = [u32, u32]
         L.oracle_plogp.restype = ctypes.c_double
         L.oracle_version.restype = ctypes.c_char_p
@@ -156,16 +158,17 @@ def hamming(col: StrCol, target: str | bytes, max_distance: int = 1):
     return dist, within.astype(bool), col.valid_mask()
 
 
-def umi_cluster(col: StrCol, umi_len: int = 0, max_distance: int = 1):
-    """Oracle H3. Returns (cluster_id u32, valid bool, n_clusters, resolved L)."""
+def umi_cluster(col: StrCol, umi_len: int = 0, max_distance: int = 1, threads: int = 1):
+    """Oracle H3. Returns (cluster_id u32, valid bool, n_clusters, resolved L). threads > 1
+    splits the row passes and the edge search over host threads (identical result)."""
     L = lib()
     cid = np.zeros(col.n, dtype=np.uint32)
     valid = np.zeros(col.n, dtype=np.uint8)
     rl = ctypes.c_int(0)
     o, v, val = col._ptrs()
     vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)
-    k = L.oracle_umi_cluster(o, 8, v, val, 0, col.n, umi_len, max_distance, vp(cid), vp(valid),
-                             ctypes.byref(rl))
+    k = L.oracle_umi_cluster_mt(o, 8, v, val, 0, col.n, umi_len, max_distance, vp(cid), vp(valid),
+                                ctypes.byref(rl), int(threads))
     if k < 0:
         raise ValueError("oracle_umi_cluster: bad arguments")
     return cid, valid.astype(bool), int(k), rl.value
@@ -320,33 +323,52 @@ def effective_k(k: int) -> int:
     return 4 if k <= 4 else 8 if k <= 8 else 16 if k <= 16 else 32 if k <= 32 else 64
 
 
-def kmer_spectrum(col: StrCol, k: int, min_cov: int, auto_k: bool = False, group_offsets=None):
+def kmer_spectrum(col: StrCol, k: int, min_cov: int, auto_k: bool = False, group_offsets=None, threads: int = 1):
     """Per-group spectra, concatenated in group order. Returns a dict with
     kmer_hi, kmer_lo (u64), exts (u8), counts (u16), group_offsets (n_groups+1, int64)
-    and stats (n_groups x 5: k_eff, n_sequences, node_count, terminal_count, isolated_count)."""
+    and stats (n_groups x 5: k_eff, n_sequences, node_count, terminal_count, isolated_count).
+    threads > 1: groups split over host threads (the C calls release the GIL)."""
     L = lib()
     go = np.array([0, col.n], dtype=np.int64) if group_offsets is None else np.asarray(group_offsets, np.int64)
     G = len(go) - 1
     offs, vals, valid = col._ptrs()
-    his, los, exs, cns = [], [], [], []
     stats = np.zeros((G, 5), dtype=np.int64)
+    counts = np.zeros(G, dtype=np.int64)
+
+    def run(g0, g1):
+        his, los, exs, cns = [], [], [], []
+        for g in range(g0, g1):
+            cap = int(L.oracle_kmer_observations(offs, 8, int(go[g]), int(go[g + 1]), 4)) + 1
+            km = np.zeros(2 * cap, dtype=np.uint64)
+            ex = np.zeros(cap, dtype=np.uint8)
+            cn = np.zeros(cap, dtype=np.uint16)
+            st = np.zeros(5, dtype=np.int64)
+            m = L.oracle_kmer_spectrum(offs, 8, vals, valid, 0, int(go[g]), int(go[g + 1]), int(k),
+                                       int(bool(auto_k)), int(min_cov), km.ctypes.data_as(ctypes.c_void_p),
+                                       ex.ctypes.data_as(ctypes.c_void_p), cn.ctypes.data_as(ctypes.c_void_p), cap,
+                                       st.ctypes.data_as(ctypes.c_void_p))
+            assert m >= 0
+            his.append(km[0:2 * m:2])
+            los.append(km[1:2 * m:2])
+            exs.append(ex[:m])
+            cns.append(cn[:m])
+            stats[g] = st
+            counts[g] = m
+        return his, los, exs, cns
+
+    cuts = np.linspace(0, G, max(1, min(threads, G)) + 1).astype(np.int64)
+    if len(cuts) > 2:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(len(cuts) - 1) as ex:
+            parts = list(ex.map(lambda ab: run(int(ab[0]), int(ab[1])), zip(cuts, cuts[1:])))
+    else:
+        parts = [run(0, G)]
+    his = [a for p in parts for a in p[0]]
+    los = [a for p in parts for a in p[1]]
+    exs = [a for p in parts for a in p[2]]
+    cns = [a for p in parts for a in p[3]]
     out_off = np.zeros(G + 1, dtype=np.int64)
-    for g in range(G):
-        cap = int(L.oracle_kmer_observations(offs, 8, int(go[g]), int(go[g + 1]), 4)) + 1
-        km = np.zeros(2 * cap, dtype=np.uint64)
-        ex = np.zeros(cap, dtype=np.uint8)
-        cn = np.zeros(cap, dtype=np.uint16)
-        st = np.zeros(5, dtype=np.int64)
-        m = L.oracle_kmer_spectrum(offs, 8, vals, valid, 0, int(go[g]), int(go[g + 1]), int(k), int(bool(auto_k)),
-                                   int(min_cov), km.ctypes.data_as(ctypes.c_void_p), ex.ctypes.data_as(ctypes.c_void_p),
-                                   cn.ctypes.data_as(ctypes.c_void_p), cap, st.ctypes.data_as(ctypes.c_void_p))
-        assert m >= 0
-        his.append(km[0:2 * m:2])
-        los.append(km[1:2 * m:2])
-        exs.append(ex[:m])
-        cns.append(cn[:m])
-        stats[g] = st
-        out_off[g + 1] = out_off[g] + m
+    out_off[1:] = np.cumsum(counts)
     cat = lambda xs, dt: np.concatenate(xs).astype(dt) if xs else np.zeros(0, dt)
     return {"kmer_hi": cat(his, np.uint64), "kmer_lo": cat(los, np.uint64), "exts": cat(exs, np.uint8),
             "counts": cat(cns, np.uint16), "group_offsets": out_off, "stats": stats}

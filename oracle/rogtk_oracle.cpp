@@ -28,8 +28,10 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <iterator>
 #include <map>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -290,12 +292,14 @@ void oracle_hamming_batch(const void* offsets, int offset_width, const uint8_t* 
 // regular code; then components of irregular strings only, in byte-lexicographic order of
 // their smallest string. Null rows get no id (out_valid = 0).
 // umi_len <= 0: L = byte length of the first non-null row.
-// Returns the number of clusters, or -1 on bad arguments.
-int64_t oracle_umi_cluster(const void* offsets, int offset_width, const uint8_t* values,
-                           const uint8_t* validity, int64_t validity_offset, int64_t n,
-                           int umi_len, int max_distance, uint32_t* cluster_id, uint8_t* out_valid,
-                           int* resolved_len) {
+// Returns the number of clusters, or -1 on bad arguments. oracle_umi_cluster_mt splits the
+// row passes and the edge search over `threads` host threads (same result for any count).
+int64_t oracle_umi_cluster_mt(const void* offsets, int offset_width, const uint8_t* values,
+                              const uint8_t* validity, int64_t validity_offset, int64_t n, int umi_len,
+                              int max_distance, uint32_t* cluster_id, uint8_t* out_valid, int* resolved_len,
+                              int threads) {
     if (max_distance < 0 || max_distance > 1) return -1;
+    if (threads < 1) threads = 1;
     int L = umi_len;
     if (L <= 0) {
         L = 0;
@@ -309,29 +313,58 @@ int64_t oracle_umi_cluster(const void* offsets, int offset_width, const uint8_t*
     }
     if (resolved_len) *resolved_len = L;
     const bool packable = L >= 1 && L <= 32;
+    // row chunks / index ranges per thread (results do not depend on the split: every
+    // union-find root is its component's smallest vertex)
+    auto parallel = [&](int64_t count, auto&& fn) {
+        const int t = (int)std::max<int64_t>(1, std::min<int64_t>(threads, count / 4096 + 1));
+        std::vector<std::thread> pool;
+        for (int k = 0; k < t; ++k)
+            pool.emplace_back([&, k] { fn(k, count * k / t, count * (k + 1) / t); });
+        for (auto& th : pool) th.join();
+        return t;
+    };
     std::vector<uint64_t> codes((size_t)n, 0);
     std::vector<uint8_t> cls((size_t)n, 0);  // 0 null, 1 regular, 2 irregular
-    std::vector<uint64_t> distinct;
-    for (int64_t i = 0; i < n; ++i) {
-        if (!row_valid(validity, validity_offset, i)) continue;
-        int64_t st, len;
-        row_span(offsets, offset_width, i, &st, &len);
-        const uint8_t* s = values + st;
-        bool reg = packable && len == L;
-        uint64_t c = 0;
-        for (int64_t j = 0; reg && j < len; ++j) {
-            int b = s[j] == 'A' ? 0 : s[j] == 'C' ? 1 : s[j] == 'G' ? 2 : s[j] == 'T' ? 3 : -1;
-            if (b < 0) reg = false;
-            c = (c << 2) | (uint64_t)(b & 3);
+    std::vector<std::vector<uint64_t>> part((size_t)threads);
+    const int tp = parallel(n, [&](int k, int64_t lo, int64_t hi) {
+        std::vector<uint64_t>& mine = part[(size_t)k];
+        for (int64_t i = lo; i < hi; ++i) {
+            if (!row_valid(validity, validity_offset, i)) continue;
+            int64_t st, len;
+            row_span(offsets, offset_width, i, &st, &len);
+            const uint8_t* s = values + st;
+            bool reg = packable && len == L;
+            uint64_t c = 0;
+            for (int64_t j = 0; reg && j < len; ++j) {
+                int b = s[j] == 'A' ? 0 : s[j] == 'C' ? 1 : s[j] == 'G' ? 2 : s[j] == 'T' ? 3 : -1;
+                if (b < 0) reg = false;
+                c = (c << 2) | (uint64_t)(b & 3);
+            }
+            cls[(size_t)i] = reg ? 1 : 2;
+            if (reg) {
+                codes[(size_t)i] = c;
+                mine.push_back(c);
+            }
         }
-        cls[i] = reg ? 1 : 2;
-        if (reg) {
-            codes[i] = c;
-            distinct.push_back(c);
-        }
+        std::sort(mine.begin(), mine.end());
+        mine.erase(std::unique(mine.begin(), mine.end()), mine.end());
+    });
+    // merge the sorted per-thread sets pairwise
+    for (int width = 1; width < tp; width *= 2) {
+        std::vector<std::thread> pool;
+        for (int k = 0; k + width < tp; k += 2 * width)
+            pool.emplace_back([&, k, width] {
+                std::vector<uint64_t> m;
+                m.reserve(part[(size_t)k].size() + part[(size_t)(k + width)].size());
+                std::set_union(part[(size_t)k].begin(), part[(size_t)k].end(), part[(size_t)(k + width)].begin(),
+                               part[(size_t)(k + width)].end(), std::back_inserter(m));
+                part[(size_t)k].swap(m);
+                std::vector<uint64_t>().swap(part[(size_t)(k + width)]);
+            });
+        for (auto& th : pool) th.join();
     }
-    std::sort(distinct.begin(), distinct.end());
-    distinct.erase(std::unique(distinct.begin(), distinct.end()), distinct.end());
+    std::vector<uint64_t> distinct;
+    distinct.swap(part[0]);
     const size_t D = distinct.size();
     std::vector<uint32_t> parent(D);
     for (size_t i = 0; i < D; ++i) parent[i] = (uint32_t)i;
@@ -339,26 +372,37 @@ int64_t oracle_umi_cluster(const void* offsets, int offset_width, const uint8_t*
         while (parent[x] != x) { parent[x] = parent[parent[x]]; x = parent[x]; }
         return x;
     };
+    auto unite = [&](uint32_t x, uint32_t y) {
+        uint32_t a = find(x), b = find(y);
+        if (a == b) return;
+        if (a < b) std::swap(a, b);
+        parent[a] = b;  // hook larger root under smaller: root = smallest vertex
+    };
     if (max_distance == 1) {
-        for (size_t i = 0; i < D; ++i) {
-            const uint64_t c = distinct[i];
-            for (int p = 0; p < L; ++p)
-                for (uint64_t d = 1; d <= 3; ++d) {
-                    uint64_t nb = c ^ (d << (2 * p));
-                    if (nb >= c) continue;
-                    auto it = std::lower_bound(distinct.begin(), distinct.end(), nb);
-                    if (it == distinct.end() || *it != nb) continue;
-                    uint32_t a = find((uint32_t)i), b = find((uint32_t)(it - distinct.begin()));
-                    if (a == b) continue;
-                    if (a < b) std::swap(a, b);
-                    parent[a] = b;  // hook larger root under smaller: root = min index
-                }
-        }
+        // regular ~ regular: the Hamming-1 neighbours of every distinct code (edges found
+        // in parallel, united serially)
+        std::vector<std::vector<std::pair<uint32_t, uint32_t>>> edges((size_t)threads);
+        parallel((int64_t)D, [&](int k, int64_t lo, int64_t hi) {
+            auto& e = edges[(size_t)k];
+            for (int64_t i = lo; i < hi; ++i) {
+                const uint64_t c = distinct[(size_t)i];
+                for (int p = 0; p < L; ++p)
+                    for (uint64_t d = 1; d <= 3; ++d) {
+                        uint64_t nb = c ^ (d << (2 * p));
+                        if (nb >= c) continue;
+                        auto it = std::lower_bound(distinct.begin(), distinct.end(), nb);
+                        if (it == distinct.end() || *it != nb) continue;
+                        e.emplace_back((uint32_t)i, (uint32_t)(it - distinct.begin()));
+                    }
+            }
+        });
+        for (auto& e : edges)
+            for (auto& pr : e) unite(pr.first, pr.second);
     }
     // irregular distinct strings, byte-lexicographic: vertices D + j
     std::map<std::string, uint32_t> irregular;
     for (int64_t i = 0; i < n; ++i)
-        if (cls[i] == 2) {
+        if (cls[(size_t)i] == 2) {
             int64_t st, len;
             row_span(offsets, offset_width, i, &st, &len);
             irregular.emplace(std::string((const char*)values + st, (size_t)len), 0);
@@ -371,15 +415,9 @@ int64_t oracle_umi_cluster(const void* offsets, int offset_width, const uint8_t*
     const size_t I = istr.size();
     parent.resize(D + I);
     for (size_t j = 0; j < I; ++j) parent[D + j] = (uint32_t)(D + j);
-    auto unite = [&](uint32_t x, uint32_t y) {
-        uint32_t a = find(x), b = find(y);
-        if (a == b) return;
-        if (a < b) std::swap(a, b);
-        parent[a] = b;  // root = smallest vertex: regular codes first, then strings
-    };
     if (max_distance == 1) {
         // irregular ~ irregular: equal length, equal except at one position p -> same
-        // (length, p, string without byte p) key; link each to the first string seen
+        // (p, string without byte p) key; link each to the first string seen
         std::map<std::pair<size_t, std::string>, uint32_t> first;
         for (size_t j = 0; j < I; ++j) {
             const std::string& s = *istr[j];
@@ -423,19 +461,31 @@ int64_t oracle_umi_cluster(const void* offsets, int offset_width, const uint8_t*
         if (r == i) label[i] = next++;
         else label[i] = label[r];  // r < i already labelled
     }
-    for (int64_t i = 0; i < n; ++i) {
-        if (out_valid) out_valid[i] = cls[i] != 0;
-        if (cls[i] == 0) { cluster_id[i] = 0; continue; }
-        if (cls[i] == 1) {
-            size_t idx = (size_t)(std::lower_bound(distinct.begin(), distinct.end(), codes[i]) - distinct.begin());
-            cluster_id[i] = label[idx];
-        } else {
-            int64_t st, len;
-            row_span(offsets, offset_width, i, &st, &len);
-            cluster_id[i] = label[D + irregular[std::string((const char*)values + st, (size_t)len)]];
+    parallel(n, [&](int, int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; ++i) {
+            if (out_valid) out_valid[i] = cls[(size_t)i] != 0;
+            if (cls[(size_t)i] == 0) {
+                cluster_id[i] = 0;
+            } else if (cls[(size_t)i] == 1) {
+                size_t idx = (size_t)(std::lower_bound(distinct.begin(), distinct.end(), codes[(size_t)i]) -
+                                      distinct.begin());
+                cluster_id[i] = label[idx];
+            } else {
+                int64_t st, len;
+                row_span(offsets, offset_width, i, &st, &len);
+                cluster_id[i] = label[D + irregular.at(std::string((const char*)values + st, (size_t)len))];
+            }
         }
-    }
+    });
     return (int64_t)next;
+}
+
+int64_t oracle_umi_cluster(const void* offsets, int offset_width, const uint8_t* values,
+                           const uint8_t* validity, int64_t validity_offset, int64_t n,
+                           int umi_len, int max_distance, uint32_t* cluster_id, uint8_t* out_valid,
+                           int* resolved_len) {
+    return oracle_umi_cluster_mt(offsets, offset_width, values, validity, validity_offset, n, umi_len, max_distance,
+                                 cluster_id, out_valid, resolved_len, 1);
 }
 
 // Entropy term table entry as the reference computes it: p = c/t; p*log2(p).

@@ -149,6 +149,12 @@ SIGNATURES = {
     "rogtk_kmer_spectrum_dev": [_vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _i64, _vp, _vp, _vp, _vp,
                                 _vp, _P_I64, _vp],
     "rogtk_kmer_path_stats": [_P_I64],
+    "rogtk_read_block_words": [_i64],
+    "rogtk_host_alloc": [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)],
+    "rogtk_host_free": [_vp],
+    "rogtk_pack_reads": [_vp, _vp, _vp, _i64, _i64, _i32, _vp, _vp],
+    "rogtk_kmer_spectrum_blocks": [_vp, _i32, _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _i64, _vp,
+                                   _vp, _vp, _vp, _vp, _P_I64, _vp],
     "rogtk_kmer_spectrum_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i32, _i32, _i64, _i64, _vp,
                                  _vp, _vp, _vp, _vp],
     "rogtk_assemble_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _i32, _i64, ctypes.c_char_p, ctypes.c_char_p,
@@ -168,6 +174,7 @@ SIGNATURES = {
     "rogtk_profile_select": [ctypes.c_char_p],
     "rogtk_profile_reset": [],
     "rogtk_profile_read": [ctypes.c_char_p, _P_F64, _P_I64],
+    "rogtk_profile_read_span": [ctypes.c_char_p, _P_F64, _P_I64],
 }
 
 # functions returning void

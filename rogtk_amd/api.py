@@ -57,12 +57,38 @@ def _ptr(a: Optional[np.ndarray]):
     return None if a is None else ctypes.c_void_p(a.ctypes.data)
 
 
+class _PinnedBlock:
+    """A rogtk_host_alloc block (pinned host memory: direct DMA for the D2H of results),
+    returned to the library's cache when the last array over it is collected."""
+
+    def __init__(self, nbytes: int):
+        p = ctypes.c_void_p()
+        _lib.call("rogtk_host_alloc", nbytes, ctypes.byref(p))
+        self.ptr, self.nbytes = p.value, nbytes
+
+    def __del__(self):
+        try:
+            _lib.hip().rogtk_host_free(ctypes.c_void_p(self.ptr))
+        except Exception:
+            pass
+
+
+def _out(n: int, dtype, zero: bool = False) -> np.ndarray:
+    """Output array of n elements in pinned host memory (numpy views keep it alive)."""
+    nbytes = max(n, 1) * np.dtype(dtype).itemsize
+    blk = _PinnedBlock(nbytes)
+    a = np.frombuffer(pa.foreign_buffer(blk.ptr, nbytes, base=blk), dtype=dtype)
+    if zero:
+        a[:] = 0
+    return a
+
+
 def _complexity_chunk(ch, want: tuple):
     n = ch.n
     out = {}
     for name, typ in FIELDS:
         if name in want:
-            out[name] = np.empty(max(n, 1), dtype=np.uint32 if name == "longest_homopolymer_run" else np.float64)
+            out[name] = _out(n, np.uint32 if name == "longest_homopolymer_run" else np.float64)
     sc = _lib.UmiScores(*[_ptr(out.get(name)) for name in _FIELD_NAMES])
     o, v, val = ch.ptrs()
     _lib.call("rogtk_umi_complexity_host", o, ch.offset_width, v, ch.values.size, val,
@@ -121,14 +147,14 @@ def _hamming(column, target, max_distance, want_dist):
     arrays = []
     for ch in chunks(column):
         n = ch.n
-        dist = np.empty(max(n, 1), dtype=np.uint32) if want_dist else None
-        bits = None if want_dist else np.zeros(max((n + 7) // 8, 1), dtype=np.uint8)
+        dist = _out(n, np.uint32) if want_dist else None
+        bits = None if want_dist else _out((n + 7) // 8, np.uint8)
         o, v, val = ch.ptrs()
         _lib.call("rogtk_hamming_host", o, ch.offset_width, v, ch.values.size, val, ch.validity_offset,
                   n, _ptr(tb), len(t), maxd, _ptr(dist), _ptr(bits))
         vbuf = validity_buffer(ch)
         if want_dist:
-            arrays.append(pa.Array.from_buffers(pa.uint32(), n, [vbuf, pa.py_buffer(dist[:n].copy())]))
+            arrays.append(pa.Array.from_buffers(pa.uint32(), n, [vbuf, pa.py_buffer(dist)]))
         else:
             arrays.append(pa.Array.from_buffers(pa.bool_(), n, [vbuf, pa.py_buffer(bits)]))
     return concat(arrays, pa.uint32() if want_dist else pa.bool_())
@@ -147,13 +173,13 @@ def umi_cluster(column: ColumnLike, umi_len: int = 0, max_distance: int = 1):
     assert len(chs) == 1
     ch = chs[0]
     n = ch.n
-    cid = np.empty(max(n, 1), dtype=np.uint32)
+    cid = _out(n, np.uint32)
     nclu = ctypes.c_int64(0)
     rl = ctypes.c_int(0)
     o, v, val = ch.ptrs()
     _lib.call("rogtk_umi_cluster_host", o, ch.offset_width, v, ch.values.size, val, ch.validity_offset,
               n, int(umi_len), int(max_distance), _ptr(cid), ctypes.byref(nclu), ctypes.byref(rl))
-    out = pa.Array.from_buffers(pa.uint32(), n, [validity_buffer(ch), pa.py_buffer(cid[:n].copy())])
+    out = pa.Array.from_buffers(pa.uint32(), n, [validity_buffer(ch), pa.py_buffer(cid)])
     return out, int(nclu.value), int(rl.value)
 
 

@@ -15,6 +15,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "rogtk_internal.h"
@@ -49,6 +50,45 @@ struct ProfRec {
 std::vector<ProfRec> g_prof_pending;
 double g_prof_ms[K_COUNT_] = {0};
 int64_t g_prof_n[K_COUNT_] = {0};
+// in-kernel spans: one u64 tick count per launch in a device result array
+constexpr int kSpanSlots = 1 << 14;
+uint64_t* g_span_dev = nullptr;  // kSpanSlots results
+std::vector<KernelId> g_span_ids;  // kernel of each used slot
+double g_span_ms[K_COUNT_] = {0};
+int64_t g_span_n[K_COUNT_] = {0};
+double g_span_tick_ms = 0;  // wall_clock64 period in ms
+
+__global__ void k_span_reduce(const uint64_t* __restrict__ t, int64_t nb, uint64_t* __restrict__ out) {
+    __shared__ uint64_t s_lo[256], s_hi[256];
+    uint64_t lo = ~0ull, hi = 0;
+    for (int64_t b = threadIdx.x; b < nb; b += blockDim.x) {
+        lo = min(lo, t[2 * b]);
+        hi = max(hi, t[2 * b + 1]);
+    }
+    s_lo[threadIdx.x] = lo;
+    s_hi[threadIdx.x] = hi;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            s_lo[threadIdx.x] = min(s_lo[threadIdx.x], s_lo[threadIdx.x + o]);
+            s_hi[threadIdx.x] = max(s_hi[threadIdx.x], s_hi[threadIdx.x + o]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = s_hi[0] > s_lo[0] ? s_hi[0] - s_lo[0] : 0;
+}
+
+void span_drain_locked() {
+    if (g_span_ids.empty() || !g_span_dev) return;
+    std::vector<uint64_t> h(g_span_ids.size());
+    if (hipDeviceSynchronize() == hipSuccess &&
+        hipMemcpy(h.data(), g_span_dev, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess)
+        for (size_t i = 0; i < h.size(); ++i) {
+            g_span_ms[g_span_ids[i]] += (double)h[i] * g_span_tick_ms;
+            g_span_n[g_span_ids[i]] += 1;
+        }
+    g_span_ids.clear();
+}
 
 void prof_drain_locked() {
     for (auto& r : g_prof_pending) {
@@ -65,6 +105,35 @@ void prof_drain_locked() {
 }  // namespace
 
 bool profiling_on() { return g_prof.load(std::memory_order_relaxed); }
+
+uint64_t* span_begin(KernelId id, int64_t n_blocks, hipStream_t s) {
+    if (!g_prof.load(std::memory_order_relaxed) || !((g_prof_mask.load(std::memory_order_relaxed) >> id) & 1u))
+        return nullptr;
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    if (!g_span_dev) {
+        int dev = 0, khz = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0 ||
+            hipMalloc((void**)&g_span_dev, kSpanSlots * 8) != hipSuccess) {
+            g_span_dev = nullptr;
+            return nullptr;
+        }
+        g_span_tick_ms = 1.0 / (double)khz;
+    }
+    if ((int)g_span_ids.size() >= kSpanSlots) span_drain_locked();
+    uint64_t* t = nullptr;
+    if (hipMallocAsync((void**)&t, (size_t)std::max<int64_t>(n_blocks, 1) * 16, s) != hipSuccess) return nullptr;
+    return t;
+}
+
+void span_end(KernelId id, uint64_t* tspan, int64_t n_blocks, hipStream_t s) {
+    if (!tspan) return;
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    const size_t slot = g_span_ids.size();
+    g_span_ids.push_back(id);
+    hipLaunchKernelGGL(k_span_reduce, dim3(1), dim3(256), 0, s, tspan, n_blocks, g_span_dev + slot);
+    (void)hipFreeAsync(tspan, s);
+}
 
 ProfScope::ProfScope(KernelId id, hipStream_t stream, bool exact) : id_(id), stream_(stream), exact_(exact) {
     if (!g_prof.load(std::memory_order_relaxed) || !((g_prof_mask.load(std::memory_order_relaxed) >> id) & 1u)) return;
@@ -221,13 +290,117 @@ int check_packed_alignment(const uint32_t* codes, const ScoreOut& o, const uint3
 }
 
 // --------------------------------------------- per-thread level-2 context
+// Host <-> device transfers of the level-2 entry points. Pinned host memory
+// (hipHostMalloc / rogtk_host_alloc / hipHostRegister) moves by direct DMA. Pageable
+// memory moves through two pinned staging buffers of the context, chunk by chunk, so
+// the DMA of one chunk overlaps the host copy of the other; the host copies of a chunk
+// are split over a few threads (a single thread's memcpy, and the first-touch page
+// faults of a fresh destination, cap a pageable copy well below the PCIe link).
+constexpr size_t kStageChunk = (size_t)32 << 20;
+
+int host_copy_threads() {
+    static const int t = [] {
+        const char* e = getenv("OMP_NUM_THREADS");
+        int v = e ? atoi(e) : 0;
+        const int hw = (int)std::thread::hardware_concurrency();
+        if (v <= 0) v = hw > 0 ? hw : 4;
+        return std::max(1, std::min(v, 8));
+    }();
+    return t;
+}
+
+void par_memcpy(void* dst, const void* src, size_t bytes) {
+    const int t = bytes >= ((size_t)4 << 20) ? host_copy_threads() : 1;
+    if (t <= 1) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    std::vector<std::thread> pool;
+    const size_t per = (bytes / t + 4095) / 4096 * 4096;
+    for (int k = 0; k < t; ++k) {
+        const size_t a = std::min(bytes, per * k), b = std::min(bytes, per * (k + 1));
+        if (a < b) pool.emplace_back([=] { std::memcpy((uint8_t*)dst + a, (const uint8_t*)src + a, b - a); });
+    }
+    for (auto& th : pool) th.join();
+}
+
+bool is_pinned(const void* p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
 struct HostCtx {
     int device = -1;
     hipStream_t stream = nullptr;
     DevBuf offsets, values, validity, codes, regbits, irr, nirr, target, out[8], ws, bitmap;
     int64_t ws_L = -1, ws_maxd = -1;
+    void* pin[2] = {nullptr, nullptr};  // staging for pageable host memory
+    hipEvent_t ev[2] = {nullptr, nullptr};
     ~HostCtx() {
+        for (int k = 0; k < 2; ++k) {
+            if (pin[k]) hipHostFree(pin[k]);
+            if (ev[k]) hipEventDestroy(ev[k]);
+        }
         if (stream) hipStreamDestroy(stream);
+    }
+    int staging() {
+        for (int k = 0; k < 2; ++k) {
+            if (!pin[k]) ROGTK_HIP_CHECK(hipHostMalloc(&pin[k], kStageChunk, hipHostMallocDefault));
+            if (!ev[k]) ROGTK_HIP_CHECK(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
+        }
+        return ROGTK_OK;
+    }
+    // device -> host; complete on return
+    int d2h(void* dst, const void* src, size_t bytes) {
+        if (bytes == 0) return ROGTK_OK;
+        if (is_pinned(dst)) {
+            ROGTK_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream));
+            ROGTK_HIP_CHECK(hipStreamSynchronize(stream));
+            return ROGTK_OK;
+        }
+        if (int rc = staging()) return rc;
+        size_t prev_off = 0, prev_len = 0;
+        int k = 0;
+        for (size_t off = 0; off < bytes; off += kStageChunk, k ^= 1) {
+            const size_t len = std::min(kStageChunk, bytes - off);
+            ROGTK_HIP_CHECK(hipMemcpyAsync(pin[k], (const uint8_t*)src + off, len, hipMemcpyDeviceToHost, stream));
+            ROGTK_HIP_CHECK(hipEventRecord(ev[k], stream));
+            if (off > 0) {  // the previous chunk: out of its staging buffer while this one moves
+                ROGTK_HIP_CHECK(hipEventSynchronize(ev[k ^ 1]));
+                par_memcpy((uint8_t*)dst + prev_off, pin[k ^ 1], prev_len);
+            }
+            prev_off = off;
+            prev_len = len;
+        }
+        ROGTK_HIP_CHECK(hipEventSynchronize(ev[k ^ 1]));
+        par_memcpy((uint8_t*)dst + prev_off, pin[k ^ 1], prev_len);
+        return ROGTK_OK;
+    }
+    // host -> device; enqueued on the stream (the host buffer may be reused on return)
+    int h2d(void* dst, const void* src, size_t bytes) {
+        if (bytes == 0) return ROGTK_OK;
+        if (is_pinned(src)) {
+            ROGTK_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
+            return ROGTK_OK;
+        }
+        if (int rc = staging()) return rc;
+        int k = 0;
+        int64_t i = 0;
+        for (size_t off = 0; off < bytes; off += kStageChunk, k ^= 1, ++i) {
+            const size_t len = std::min(kStageChunk, bytes - off);
+            if (i >= 2) ROGTK_HIP_CHECK(hipEventSynchronize(ev[k]));  // its DMA of two chunks ago is done
+            par_memcpy(pin[k], (const uint8_t*)src + off, len);
+            ROGTK_HIP_CHECK(hipMemcpyAsync((uint8_t*)dst + off, pin[k], len, hipMemcpyHostToDevice, stream));
+            ROGTK_HIP_CHECK(hipEventRecord(ev[k], stream));
+        }
+        // the staging buffers are reused by the next transfer only after these DMAs: every
+        // later use first waits on the events above (or the stream is synchronised)
+        ROGTK_HIP_CHECK(hipStreamSynchronize(stream));
+        return ROGTK_OK;
     }
 };
 
@@ -284,7 +457,7 @@ int upload_and_stage(HostCtx* c, const HostCol& h, int L_req, int* L_out, int64_
     const int64_t n = h.n;
     const int ow = h.ow;
     ROGTK_REQUIRE(c->offsets.ensure((size_t)(n + 1) * ow) == ROGTK_OK, ROGTK_E_HIP, "%s", rogtk_last_error());
-    ROGTK_HIP_CHECK(hipMemcpyAsync(c->offsets.p, h.offsets, (size_t)(n + 1) * ow, hipMemcpyHostToDevice, c->stream));
+    if (int rc = c->h2d(c->offsets.p, h.offsets, (size_t)(n + 1) * ow)) return rc;
     // values: upload [0, off(n)) so the device offsets stay valid as given
     const int64_t vbytes = std::max<int64_t>(h.off(n), 1);
     ROGTK_REQUIRE(h.off(n) <= h.values_len || h.values_len < 0, ROGTK_E_INVALID,
@@ -292,12 +465,12 @@ int upload_and_stage(HostCtx* c, const HostCol& h, int L_req, int* L_out, int64_
                   (long long)h.values_len);
     if (c->values.ensure((size_t)vbytes) != ROGTK_OK) return ROGTK_E_HIP;
     if (h.off(n) > 0)
-        ROGTK_HIP_CHECK(hipMemcpyAsync(c->values.p, h.values, (size_t)h.off(n), hipMemcpyHostToDevice, c->stream));
+        if (int rc = c->h2d(c->values.p, h.values, (size_t)h.off(n))) return rc;
     const uint8_t* dvalid = nullptr;
     if (h.validity) {
         const size_t vb = (size_t)((h.voff + n + 7) / 8);
         if (c->validity.ensure(vb) != ROGTK_OK) return ROGTK_E_HIP;
-        ROGTK_HIP_CHECK(hipMemcpyAsync(c->validity.p, h.validity, vb, hipMemcpyHostToDevice, c->stream));
+        if (int rc = c->h2d(c->validity.p, h.validity, vb)) return rc;
         dvalid = c->validity.as<uint8_t>();
     }
     int L = L_req > 0 ? L_req : h.first_len();
@@ -337,6 +510,60 @@ extern "C" {
 const char* rogtk_version(void) { return "rogtk-amd 0.1.0 (gfx950)"; }
 
 const char* rogtk_last_error(void) { return t_err; }
+
+// Pinned host memory for callers' output (and input) buffers: transfers from / to it
+// are direct DMA. Freed blocks are cached by size class (2 MiB multiples, up to 16 GiB
+// in all) because pinning fresh pages costs more than the copy it saves.
+namespace {
+std::mutex g_pin_mu;
+std::multimap<size_t, void*> g_pin_free;
+std::map<void*, size_t> g_pin_size;
+size_t g_pin_cached = 0;
+constexpr size_t kPinCacheMax = (size_t)16 << 30;
+}  // namespace
+
+int rogtk_host_alloc(size_t bytes, void** out) {
+    ROGTK_REQUIRE(out, ROGTK_E_INVALID, "host_alloc: NULL out");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
+        set_error("no HIP device available (librogtk_hip needs an MI355X / gfx950 GPU)");
+        return ROGTK_E_NODEVICE;
+    }
+    const size_t cls = (std::max<size_t>(bytes, 1) + ((size_t)2 << 20) - 1) / ((size_t)2 << 20) * ((size_t)2 << 20);
+    {
+        std::lock_guard<std::mutex> lk(g_pin_mu);
+        auto it = g_pin_free.find(cls);
+        if (it != g_pin_free.end()) {
+            *out = it->second;
+            g_pin_cached -= cls;
+            g_pin_free.erase(it);
+            return ROGTK_OK;
+        }
+    }
+    void* p = nullptr;
+    ROGTK_HIP_CHECK(hipHostMalloc(&p, cls, hipHostMallocDefault));
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    g_pin_size[p] = cls;
+    *out = p;
+    return ROGTK_OK;
+}
+
+int rogtk_host_free(void* p) {
+    if (!p) return ROGTK_OK;
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pin_size.find(p);
+    ROGTK_REQUIRE(it != g_pin_size.end(), ROGTK_E_INVALID, "host_free: not a rogtk_host_alloc block");
+    const size_t cls = it->second;
+    if (g_pin_cached + cls <= kPinCacheMax) {
+        g_pin_free.emplace(cls, p);
+        g_pin_cached += cls;
+    } else {
+        g_pin_size.erase(it);
+        ROGTK_HIP_CHECK(hipHostFree(p));
+    }
+    return ROGTK_OK;
+}
 
 int rogtk_device_count(int* out) {
     ROGTK_REQUIRE(out, ROGTK_E_INVALID, "out_count is NULL");
@@ -588,10 +815,9 @@ int rogtk_umi_complexity_host(const void* offsets, int offset_width, const uint8
     }
     for (int k = 0; k < 6; ++k)
         if (hptr[k])
-            ROGTK_HIP_CHECK(hipMemcpyAsync((void*)hptr[k], dptr[k], (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+            if (int rc = c->d2h((void*)hptr[k], dptr[k], (size_t)n * 8)) return rc;
     if (ho.longest)
-        ROGTK_HIP_CHECK(hipMemcpyAsync(ho.longest, dlong, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
-    ROGTK_HIP_CHECK(hipStreamSynchronize(c->stream));
+        if (int rc = c->d2h(ho.longest, dlong, (size_t)n * 4)) return rc;
     return ROGTK_OK;
 }
 
@@ -638,10 +864,9 @@ int rogtk_hamming_host(const void* offsets, int offset_width, const uint8_t* val
         if (rc) return rc;
     }
     if (distance)
-        ROGTK_HIP_CHECK(hipMemcpyAsync(distance, dd, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+        if (int rc = c->d2h(distance, dd, (size_t)n * 4)) return rc;
     if (within_bits)
-        ROGTK_HIP_CHECK(hipMemcpyAsync(within_bits, dw, (size_t)(n + 7) / 8, hipMemcpyDeviceToHost, c->stream));
-    ROGTK_HIP_CHECK(hipStreamSynchronize(c->stream));
+        if (int rc = c->d2h(within_bits, dw, (size_t)(n + 7) / 8)) return rc;
     return ROGTK_OK;
 }
 
@@ -750,9 +975,7 @@ int rogtk_umi_cluster_host(const void* offsets, int offset_width, const uint8_t*
                                 (n_irr || (L > kMaxPackedLen && L <= 32)) ? h.max_len() : 0, max_distance, did,
                                 n_clusters, c->stream))
         return rc;
-    ROGTK_HIP_CHECK(hipMemcpyAsync(cluster_id, did, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
-    ROGTK_HIP_CHECK(hipStreamSynchronize(c->stream));
-    return ROGTK_OK;
+    return c->d2h(cluster_id, did, (size_t)n * 4);
 }
 
 int rogtk_umi_cluster_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* validity, int64_t n,
@@ -809,11 +1032,28 @@ int rogtk_profile_select(const char* kernel) {
 int rogtk_profile_reset(void) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     prof_drain_locked();
+    span_drain_locked();
     for (int k = 0; k < K_COUNT_; ++k) {
         g_prof_ms[k] = 0;
         g_prof_n[k] = 0;
+        g_span_ms[k] = 0;
+        g_span_n[k] = 0;
     }
     return ROGTK_OK;
+}
+
+int rogtk_profile_read_span(const char* kernel, double* total_ms, int64_t* launches) {
+    ROGTK_REQUIRE(kernel && total_ms && launches, ROGTK_E_INVALID, "profile_read_span: NULL argument");
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    span_drain_locked();
+    for (int k = 0; k < K_COUNT_; ++k)
+        if (std::strcmp(kernel, kKernelNames[k]) == 0) {
+            *total_ms = g_span_ms[k];
+            *launches = g_span_n[k];
+            return ROGTK_OK;
+        }
+    set_error("profile_read_span: unknown kernel '%s'", kernel);
+    return ROGTK_E_INVALID;
 }
 
 int rogtk_profile_read(const char* kernel, double* total_ms, int64_t* launches) {

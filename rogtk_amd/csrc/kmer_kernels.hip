@@ -180,6 +180,150 @@ __global__ __launch_bounds__(kBlock) void k_row_stage(const uint8_t* __restrict_
     }
 }
 
+// ------------------------------------------------- reads as fixed-stride 2-bit blocks
+// A read column packed once, in column order (coalesced), into B-word blocks (B = 8, 16
+// or 32: one, two or four 64-B lines per row): word 0 = len (bits 0..31; 0xFFFFFFFF for
+// a null row) | ACGT-clean << 32 (fracture.rs:217-229, after upper-casing); words
+// 1..B-1 = the bases, 32 per word, first base most significant. The spectrum call then
+// gathers each grouped row as whole lines (k_row_gather) instead of re-reading its ASCII
+// bytes from a random place (k_row_meta + k_row_stage).
+constexpr int kPackRowsPerBlock = 256;
+constexpr int kPackInBytes = 40 * 1024;  // a workgroup's rows' bytes, staged in LDS
+
+template <int B>
+__global__ __launch_bounds__(kBlock) void k_pack_reads(const int64_t* __restrict__ offsets,
+                                                       const uint8_t* __restrict__ values,
+                                                       const uint8_t* __restrict__ validity, int64_t voff,
+                                                       int64_t n, uint64_t* __restrict__ blocks) {
+    constexpr int R = B == 32 ? 128 : kPackRowsPerBlock;  // rows per workgroup
+    __shared__ uint32_t in32[kPackInBytes / 4];
+    __shared__ uint64_t out[R * B];
+    const uint8_t* in8 = reinterpret_cast<const uint8_t*>(in32);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int64_t a = (int64_t)blockIdx.x * R; a < n; a += (int64_t)gridDim.x * R) {
+        const int nr = (int)min<int64_t>(R, n - a);
+        const int64_t b0 = offsets[a], b1 = offsets[a + nr];
+        const int64_t a4 = b0 & ~3ll;  // dword-aligned start
+        const bool staged = b1 - a4 <= kPackInBytes;
+        if (staged) {  // the rows' bytes, coalesced: dword loads (the column's tail is padded by whole dwords
+                       // only where they exist: bytes past b1 are not read)
+            const int64_t nw = (b1 - a4 + 3) >> 2;
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(values + a4);
+            const int64_t full = (b1 - a4) >> 2;  // dwords entirely inside [a4, b1)
+            for (int64_t i = tid; i < nw; i += kBlock) {
+                if (i < full) {
+                    in32[i] = src[i];
+                } else {  // the last partial dword, byte by byte
+                    uint32_t v = 0;
+                    for (int j = 0; j < 4; ++j) {
+                        const int64_t byte = a4 + 4 * i + j;
+                        if (byte < b1) v |= (uint32_t)values[byte] << (8 * j);
+                    }
+                    in32[i] = v;
+                }
+            }
+        }
+        __syncthreads();
+        for (int q = wave; q < nr; q += kWavesPerBlock) {
+            const int64_t r = a + q;
+            bool valid = true;
+            if (validity) {
+                const int64_t bit = voff + r;
+                valid = (validity[bit >> 3] >> (bit & 7)) & 1;
+            }
+            const int64_t st = offsets[r], len = offsets[r + 1] - st;
+            uint64_t* ob = out + q * B;
+            bool bad = false;
+            if (valid) {
+                for (int64_t j0 = 0; j0 < len; j0 += 64) {
+                    const bool in = j0 + lane < len;
+                    const uint8_t c = !in ? (uint8_t)'A' : staged ? in8[st - a4 + j0 + lane] : values[st + j0 + lane];
+                    const uint32_t bb = in ? base2(c) : 0u;
+                    bad |= in && !acgt(c);
+                    const uint64_t lo = __ballot(bb & 1u), hi = __ballot(bb & 2u);
+                    if (lane < 2) {
+                        const int64_t w = (j0 >> 5) + lane;
+                        const uint32_t l32 = (uint32_t)(lo >> (32 * lane)), h32 = (uint32_t)(hi >> (32 * lane));
+                        if (w * 32 < len)
+                            ob[1 + w] = (spread2(__builtin_bitreverse32(h32)) << 1) | spread2(__builtin_bitreverse32(l32));
+                    }
+                }
+            }
+            const bool clean = __ballot(bad) == 0;
+            const int used = valid ? (int)((len + 31) >> 5) : 0;
+            if (lane == 0) ob[0] = valid ? ((uint64_t)(uint32_t)len | ((uint64_t)clean << 32)) : 0xFFFFFFFFull;
+            if (lane >= 1 + used && lane < B) ob[lane] = 0;  // unused words: zero
+        }
+        __syncthreads();
+        // the workgroup's blocks in one contiguous, coalesced store
+        uint64_t* dst = blocks + a * B;
+        for (int i = tid; i < nr * B; i += kBlock) dst[i] = out[i];
+        __syncthreads();
+    }
+}
+
+// One wave per 64 grouped rows: each row's block (B words: B lanes, 64 / B rows per
+// wave-instruction, all of the trip's loads in flight before any is used), then its
+// bases to the grouped staging buffer at a fixed stride S = words per row (row r at
+// packed[r * S]), row lengths / observation counts for this call's effective k, and
+// n_sequences as one atomic per run of same-group rows (as k_row_stage).
+template <int B>
+__global__ __launch_bounds__(kBlock) void k_row_gather(const uint64_t* __restrict__ blocks,
+                                                       const int64_t* __restrict__ rows, int64_t n_rows, int K,
+                                                       int S, const uint8_t* __restrict__ gk,
+                                                       const uint32_t* __restrict__ row_group,
+                                                       uint64_t* __restrict__ packed, int64_t* __restrict__ row_obs,
+                                                       int32_t* __restrict__ row_len,
+                                                       unsigned long long* __restrict__ gstat) {
+    constexpr int RPI = 64 / B;  // rows per wave-instruction
+    const int lane = threadIdx.x & 63, w = lane & (B - 1), sub = lane / B;
+    const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
+    for (int64_t rb = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 64; rb < n_rows;
+         rb += waves * 64) {
+        const int64_t r = rb + lane;
+        const bool live = r < n_rows;
+        const int64_t my_pr = live ? (rows ? rows[r] : r) : 0;
+        const uint32_t my_g = live ? row_group[r] : 0u;
+        const bool my_k = live && gk[my_g] == K;
+        uint64_t v[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            const int q = j * RPI + sub;
+            const int64_t pr = __shfl(my_pr, q);
+            v[j] = rb + q < n_rows ? blocks[pr * B + w] : 0xFFFFFFFFull;
+        }
+        uint64_t okbits = 0;
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            const int q = j * RPI + sub;
+            const int64_t rr = rb + q;
+            const uint64_t meta = __shfl(v[j], lane & ~(B - 1));
+            const uint32_t len = (uint32_t)meta;
+            const bool inK = __shfl(my_k, q) && rr < n_rows && len != 0xFFFFFFFFu;
+            const bool ok = inK && ((meta >> 32) & 1ull);
+            if (rr < n_rows && w >= 1 && w <= S) packed[rr * S + (w - 1)] = v[j];
+            if (rr < n_rows && w == 0) {
+                const bool use = ok && (int64_t)len >= K;
+                row_obs[rr] = use ? (int64_t)len - K + 1 : 0;
+                row_len[rr] = use ? (int32_t)len : 0;
+            }
+            const uint64_t m = __ballot(w == 0 && ok);
+#pragma unroll
+            for (int t = 0; t < RPI; ++t) okbits |= ((m >> (t * B)) & 1ull) << (j * RPI + t);
+        }
+        if (live) {  // n_sequences: the first lane of each run of same-group rows adds the run's ok rows
+            const uint32_t g_prev = __shfl_up(my_g, 1);
+            const uint64_t heads = __ballot(lane == 0 || my_g != g_prev);
+            if ((heads >> lane) & 1ull) {
+                const uint64_t above = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
+                const uint64_t run = (above ? (above & (0ull - above)) - 1ull : ~0ull) & (~0ull << lane);
+                const int cnt = __popcll(okbits & run);
+                if (cnt) atomicAdd(gstat + 5 * (int64_t)my_g + 1, (unsigned long long)cnt);
+            }
+        }
+    }
+}
+
 // row -> group map: one wave per group writes its rows' group id (coalesced)
 __global__ __launch_bounds__(kBlock) void k_row_groups(const int64_t* __restrict__ go, int64_t G,
                                                        uint32_t* __restrict__ row_group) {
@@ -460,7 +604,7 @@ template <int CLS, int TB>
 __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDesc* __restrict__ gdesc, int64_t G,
                                                      uint8_t* __restrict__ gsmall, int K, int64_t min_cov,
                                                      const int32_t* __restrict__ row_len,
-                                                     const int64_t* __restrict__ woff,
+                                                     const int64_t* __restrict__ woff, int stride,
                                                      const uint64_t* __restrict__ packed,
                                                      const int64_t* __restrict__ cap_off,
                                                      uint64_t* __restrict__ t_kmer, uint8_t* __restrict__ t_ext,
@@ -511,7 +655,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
     auto load_rows = [&](const GroupDesc& dd) {
         if (tid < dd.nrows) {
             p_len = row_len[dd.r0 + tid];
-            p_w = (int32_t)(woff[dd.r0 + tid] - dd.w0);
+            p_w = stride ? tid * stride : (int32_t)(woff[dd.r0 + tid] - dd.w0);
         }
 #pragma unroll
         for (int j = 0; j < kWPT; ++j) {
@@ -841,7 +985,7 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
                                                            const uint8_t* __restrict__ gk, int K,
                                                            const int64_t* __restrict__ row_obs,
                                                            const int64_t* __restrict__ row_words,
-                                                           const int64_t* __restrict__ woff,
+                                                           const int64_t* __restrict__ woff, int stride,
                                                            uint8_t* __restrict__ gsmall, GroupDesc* __restrict__ gdesc) {
     const int lane = threadIdx.x & 63;
     const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
@@ -853,13 +997,14 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
         int64_t obs = 0, words = 0;
         for (int64_t r = go[g] + lane; r < go[g + 1]; r += 64) {
             obs += row_obs[r];
-            words += row_words[r];
+            if (!stride) words += row_words[r];
         }
         for (int m = 32; m > 0; m >>= 1) {
             obs += __shfl_xor(obs, m);
             words += __shfl_xor(words, m);
         }
         const int64_t nrows = go[g + 1] - go[g];
+        if (stride) words = nrows * stride;  // fixed-stride staging (k_row_gather)
         if (lane == 0) {
             uint8_t cls = 0;
             if (K <= 32 && obs > 0) {
@@ -868,7 +1013,7 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
                 else if (nrows <= LdsCfg<4>::kRows && words <= LdsCfg<4>::kWords) cls = 4;
             }
             gsmall[g] = cls;
-            if (cls) gdesc[g] = GroupDesc{go[g], woff[go[g]], (int32_t)nrows, (int32_t)words};
+            if (cls) gdesc[g] = GroupDesc{go[g], stride ? go[g] * stride : woff[go[g]], (int32_t)nrows, (int32_t)words};
         }
     }
 }
@@ -1040,6 +1185,9 @@ struct KIn {
     const int64_t* cap_off;
     unsigned long long* gstat;  // G x 5
     int64_t* gcount;            // G
+    const uint64_t* blocks = nullptr;  // the column as B-word 2-bit blocks (k_pack_reads), or NULL
+    int B = 0;                         // words per block
+    int S = 0;                         // 2-bit words per row to stage: ceil(max_len / 32) <= B - 1
 };
 
 template <int OW, bool WIDE>
@@ -1058,43 +1206,61 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
     const int wgrid = grid_for((n_rows + kWavesPerBlock - 1) / kWavesPerBlock * kBlock, 16384);
     hipLaunchKernelGGL(k_row_groups, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, go, G,
                        c->row_group.as<uint32_t>());
-    // stage: row spans -> word offsets -> one pass over the bytes (check + pack + counts)
-    hipLaunchKernelGGL((k_row_meta<OW>), dim3(grid_for(n_rows)), dim3(kBlock), 0, s, in.offsets, in.validity, in.voff,
-                       in.rows, n_rows, in.gk, K, c->row_group.as<uint32_t>(), c->row_st.as<int64_t>(),
-                       c->raw_len.as<int32_t>(), c->row_words.as<int64_t>());
-    if (int rc = cub_exsum_i64(c, c->row_words.as<int64_t>(), c->woff.as<int64_t>(), n_rows, s)) return rc;
-    {
-        int64_t wl[2] = {0, 0};
-        ROGTK_HIP_CHECK(hipMemcpyAsync(&wl[0], c->woff.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
-        ROGTK_HIP_CHECK(hipMemcpyAsync(&wl[1], c->row_words.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
-        ROGTK_HIP_CHECK(hipStreamSynchronize(s));
-        if (int rc = c->packed.ensure((size_t)std::max<int64_t>(wl[0] + wl[1], 1) * 8)) return rc;
+    const int stride = in.blocks ? in.S : 0;  // staged words per row (0: compact, woff)
+    if (in.blocks) {
+        // stage from the packed column: each grouped row's block as whole lines, its bases
+        // at a fixed stride (row r at packed[r * S]: no offsets, no scan)
+        if (int rc = c->packed.ensure((size_t)std::max<int64_t>(n_rows * stride, 1) * 8)) return rc;
+        const int ggrid = grid_for((n_rows + 63) / 64 * 64 / kWavesPerBlock, 16384);
+#define ROGTK_GATHER(BW)                                                                                       \
+    hipLaunchKernelGGL(k_row_gather<BW>, dim3(ggrid), dim3(kBlock), 0, s, in.blocks, in.rows, n_rows, K, stride,  \
+                       in.gk, c->row_group.as<uint32_t>(), c->packed.as<uint64_t>(), c->row_obs.as<int64_t>(),  \
+                       c->row_len.as<int32_t>(), gstat)
+        if (in.B == 8) ROGTK_GATHER(8);
+        else if (in.B == 16) ROGTK_GATHER(16);
+        else ROGTK_GATHER(32);
+#undef ROGTK_GATHER
+    } else {
+        // stage: row spans -> word offsets -> one pass over the bytes (check + pack + counts)
+        hipLaunchKernelGGL((k_row_meta<OW>), dim3(grid_for(n_rows)), dim3(kBlock), 0, s, in.offsets, in.validity,
+                           in.voff, in.rows, n_rows, in.gk, K, c->row_group.as<uint32_t>(), c->row_st.as<int64_t>(),
+                           c->raw_len.as<int32_t>(), c->row_words.as<int64_t>());
+        if (int rc = cub_exsum_i64(c, c->row_words.as<int64_t>(), c->woff.as<int64_t>(), n_rows, s)) return rc;
+        {
+            int64_t wl[2] = {0, 0};
+            ROGTK_HIP_CHECK(hipMemcpyAsync(&wl[0], c->woff.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
+            ROGTK_HIP_CHECK(
+                hipMemcpyAsync(&wl[1], c->row_words.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
+            ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+            if (int rc = c->packed.ensure((size_t)std::max<int64_t>(wl[0] + wl[1], 1) * 8)) return rc;
+        }
+        hipLaunchKernelGGL(k_row_stage, dim3(wgrid), dim3(kBlock), 0, s, in.values, n_rows, K,
+                           c->row_group.as<uint32_t>(), c->row_st.as<int64_t>(), c->raw_len.as<int32_t>(),
+                           c->woff.as<int64_t>(), c->packed.as<uint64_t>(), c->row_obs.as<int64_t>(),
+                           c->row_len.as<int32_t>(), gstat);
     }
-    hipLaunchKernelGGL(k_row_stage, dim3(wgrid), dim3(kBlock), 0, s, in.values, n_rows, K, c->row_group.as<uint32_t>(),
-                       c->row_st.as<int64_t>(), c->raw_len.as<int32_t>(), c->woff.as<int64_t>(),
-                       c->packed.as<uint64_t>(), c->row_obs.as<int64_t>(), c->row_len.as<int32_t>(), gstat);
     ROGTK_HIP_CHECK(hipGetLastError());
     if (c->lds_path && K <= 32) {
         // one workgroup per small group, straight from the packed rows
         if (int rc = c->gsmall.ensure((size_t)G)) return rc;
         if (int rc = c->gdesc.ensure((size_t)G * sizeof(GroupDesc))) return rc;
         hipLaunchKernelGGL(k_group_classify, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, go, G, in.gk, K,
-                           c->row_obs.as<int64_t>(), c->row_words.as<int64_t>(), c->woff.as<int64_t>(),
+                           c->row_obs.as<int64_t>(), c->row_words.as<int64_t>(), c->woff.as<int64_t>(), stride,
                            c->gsmall.as<uint8_t>(), c->gdesc.as<GroupDesc>());
         hipLaunchKernelGGL((k_kmer_lds<3, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)), dim3(kLdsBlock), 0, s,
                            c->gdesc.as<GroupDesc>(), G,
                            c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
-                           c->woff.as<int64_t>(), c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
+                           c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
                            c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
         hipLaunchKernelGGL((k_kmer_lds<1, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)), dim3(kLdsBlock), 0, s,
                            c->gdesc.as<GroupDesc>(), G,
                            c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
-                           c->woff.as<int64_t>(), c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
+                           c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
                            c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
         hipLaunchKernelGGL((k_kmer_lds<4, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 8192)), dim3(kLdsBlock), 0, s,
                            c->gdesc.as<GroupDesc>(), G,
                            c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
-                           c->woff.as<int64_t>(), c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
+                           c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
                            c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
         hipLaunchKernelGGL(k_drop_small_rows, dim3(grid_for(n_rows)), dim3(kBlock), 0, s, c->row_group.as<uint32_t>(),
                            c->gsmall.as<uint8_t>(), n_rows, c->row_obs.as<int64_t>());
@@ -1440,11 +1606,15 @@ int rogtk_group_by_key(const uint32_t* keys, int64_t n, int64_t* rows_out, int64
     return ROGTK_OK;
 }
 
-int rogtk_kmer_spectrum_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* validity,
-                            int64_t validity_offset, const int64_t* rows, int64_t n_rows,
-                            const int64_t* group_offsets, int64_t n_groups, int k, int64_t min_coverage,
-                            int64_t capacity, uint64_t* kmers, uint8_t* exts, uint16_t* counts,
-                            int64_t* entry_offsets, int64_t* group_stats, int64_t* n_entries, void* stream) {
+}  // extern "C"
+
+namespace rogtk {
+namespace {
+int spectrum_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* validity, int64_t validity_offset,
+                 const int64_t* rows, int64_t n_rows, const int64_t* group_offsets, int64_t n_groups, int k,
+                 int64_t min_coverage, int64_t capacity, uint64_t* kmers, uint8_t* exts, uint16_t* counts,
+                 int64_t* entry_offsets, int64_t* group_stats, int64_t* n_entries, void* stream,
+                 const uint64_t* blocks, int B, int S) {
     ROGTK_REQUIRE(offsets && values && group_offsets && entry_offsets && group_stats && n_entries, ROGTK_E_INVALID,
                   "kmer_dev: NULL argument");
     ROGTK_REQUIRE(n_rows >= 0 && n_groups >= 1 && min_coverage >= 0, ROGTK_E_INVALID,
@@ -1477,8 +1647,11 @@ int rogtk_kmer_spectrum_dev(const int64_t* offsets, const uint8_t* values, const
     if (int rc = c->t_cnt.ensure((size_t)tcap * 2)) return rc;
     c->last_lds_groups = c->last_global_groups = 0;
     if (K && n_rows > 0) {
-        const KIn in{offsets, values, validity, validity_offset, rows, group_offsets, c->gk.as<uint8_t>(),
-                     c->cap_off.as<int64_t>(), c->gstat.as<unsigned long long>(), c->gcount.as<int64_t>()};
+        KIn in{offsets, values, validity, validity_offset, rows, group_offsets, c->gk.as<uint8_t>(),
+               c->cap_off.as<int64_t>(), c->gstat.as<unsigned long long>(), c->gcount.as<int64_t>()};
+        in.blocks = blocks;
+        in.B = B;
+        in.S = S;
         if (int rc = run_any<8>(c, in, n_rows, G, K, min_coverage, s, nullptr)) return rc;
     }
     if (int rc = cub_exsum_i64(c, c->gcount.as<int64_t>(), entry_offsets, G, s)) return rc;
@@ -1498,6 +1671,62 @@ int rogtk_kmer_spectrum_dev(const int64_t* offsets, const uint8_t* values, const
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     return ROGTK_OK;
+}
+}  // namespace
+}  // namespace rogtk
+
+extern "C" {
+
+int rogtk_kmer_spectrum_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* validity,
+                            int64_t validity_offset, const int64_t* rows, int64_t n_rows,
+                            const int64_t* group_offsets, int64_t n_groups, int k, int64_t min_coverage,
+                            int64_t capacity, uint64_t* kmers, uint8_t* exts, uint16_t* counts,
+                            int64_t* entry_offsets, int64_t* group_stats, int64_t* n_entries, void* stream) {
+    return spectrum_dev(offsets, values, validity, validity_offset, rows, n_rows, group_offsets, n_groups, k,
+                        min_coverage, capacity, kmers, exts, counts, entry_offsets, group_stats, n_entries, stream,
+                        nullptr, 0, 0);
+}
+
+int rogtk_read_block_words(int64_t max_len) {
+    if (max_len < 0) return 0;
+    const int64_t words = 1 + (max_len + 31) / 32;  // meta + bases
+    return words <= 8 ? 8 : words <= 16 ? 16 : words <= 32 ? 32 : 0;
+}
+
+int rogtk_pack_reads(const int64_t* offsets, const uint8_t* values, const uint8_t* validity, int64_t validity_offset,
+                     int64_t n, int block_words, uint64_t* blocks, void* stream) {
+    ROGTK_REQUIRE(n >= 0 && (n == 0 || (offsets && values && blocks)), ROGTK_E_INVALID, "pack_reads: NULL argument");
+    ROGTK_REQUIRE(block_words == 8 || block_words == 16 || block_words == 32, ROGTK_E_INVALID,
+                  "pack_reads: block_words must be 8, 16 or 32 (rogtk_read_block_words)");
+    if (n == 0) return ROGTK_OK;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int rows_per_wg = block_words == 32 ? 128 : kPackRowsPerBlock;
+    const int g = (int)std::min<int64_t>((n + rows_per_wg - 1) / rows_per_wg, 8192);
+    if (block_words == 8)
+        hipLaunchKernelGGL(k_pack_reads<8>, dim3(g), dim3(kBlock), 0, s, offsets, values, validity, validity_offset, n,
+                           blocks);
+    else if (block_words == 16)
+        hipLaunchKernelGGL(k_pack_reads<16>, dim3(g), dim3(kBlock), 0, s, offsets, values, validity, validity_offset,
+                           n, blocks);
+    else
+        hipLaunchKernelGGL(k_pack_reads<32>, dim3(g), dim3(kBlock), 0, s, offsets, values, validity, validity_offset,
+                           n, blocks);
+    ROGTK_HIP_CHECK(hipGetLastError());
+    return ROGTK_OK;
+}
+
+int rogtk_kmer_spectrum_blocks(const uint64_t* blocks, int block_words, int64_t max_len, const int64_t* offsets,
+                               const uint8_t* values, const uint8_t* validity, int64_t validity_offset,
+                               const int64_t* rows, int64_t n_rows, const int64_t* group_offsets, int64_t n_groups,
+                               int k, int64_t min_coverage, int64_t capacity, uint64_t* kmers, uint8_t* exts,
+                               uint16_t* counts, int64_t* entry_offsets, int64_t* group_stats, int64_t* n_entries,
+                               void* stream) {
+    ROGTK_REQUIRE(blocks, ROGTK_E_INVALID, "kmer_blocks: NULL blocks");
+    ROGTK_REQUIRE(block_words == rogtk_read_block_words(max_len) && block_words > 0, ROGTK_E_INVALID,
+                  "kmer_blocks: block_words %d does not match max_len %lld", block_words, (long long)max_len);
+    return spectrum_dev(offsets, values, validity, validity_offset, rows, n_rows, group_offsets, n_groups, k,
+                        min_coverage, capacity, kmers, exts, counts, entry_offsets, group_stats, n_entries, stream,
+                        blocks, block_words, (int)std::max<int64_t>(1, (max_len + 31) / 32));
 }
 
 }  // extern "C"

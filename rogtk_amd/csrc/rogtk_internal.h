@@ -74,6 +74,25 @@ class ProfScope {
     hipEvent_t stop_ = nullptr;
 };
 
+// In-kernel span timing (profiling only): a kernel given a non-NULL tspan writes, from
+// thread 0 of every workgroup, the device wall clock (wall_clock64, constant rate) at
+// entry and, after a final barrier, at exit; span_end() reduces max(exit) - min(entry),
+// the kernel's execution span as rocprofv3's kernel trace sees it, without the stream
+// events' own fences. span_begin returns NULL when the kernel is not being profiled.
+uint64_t* span_begin(KernelId id, int64_t n_blocks, hipStream_t s);
+void span_end(KernelId id, uint64_t* tspan, int64_t n_blocks, hipStream_t s);
+#ifdef __HIP__
+__device__ __forceinline__ void span_enter(uint64_t* tspan) {
+    if (tspan && threadIdx.x == 0) tspan[2 * blockIdx.x] = wall_clock64();
+}
+__device__ __forceinline__ void span_exit(uint64_t* tspan) {
+    if (tspan) {
+        __syncthreads();
+        if (threadIdx.x == 0) tspan[2 * blockIdx.x + 1] = wall_clock64();
+    }
+}
+#endif
+
 // ------------------------------------------------- entropy / ratio tables
 // Triangular table T[t][c] = fl(fl(c/t) * log2(fl(c/t))) computed on the host
 // with glibc log2 (the function Rust's f64::log2 resolves to), T[t][0] = 0.

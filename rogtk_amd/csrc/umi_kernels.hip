@@ -184,7 +184,8 @@ __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restr
                                                           const ScoreOut O,
                                                           uint32_t* __restrict__ hd,
                                                           uint64_t* __restrict__ hw,
-                                                          uint8_t* __restrict__ pres) {
+                                                          uint8_t* __restrict__ pres, uint64_t* tspan) {
+    span_enter(tspan);  // profiling only (NULL otherwise)
     __shared__ double s_tab[4][kMaxPackedLen + 1];
     if (SCORE) {
         for (int t = threadIdx.x; t < 4 * (kMaxPackedLen + 1); t += kBlock) {
@@ -312,6 +313,7 @@ __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restr
             }
         }
     }
+    span_exit(tspan);
 }
 
 // ------------------------------------------------------------ byte path
@@ -513,11 +515,13 @@ int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int
     int g = grid_for((n + kRowsPerLane - 1) / kRowsPerLane);
     if (cap && g > cap) g = (int)cap;
     const int sel = (score ? 8 : 0) | (hamd ? 4 : 0) | (hamw ? 2 : 0) | (mark ? 1 : 0);
+    // profiling: the kernel's own execution span from in-kernel clocks (NULL otherwise)
+    uint64_t* tspan = (score || hamd || hamw) ? span_begin(K_SCORE_PACKED, g, s) : nullptr;
 #define ROGTK_SP(S, D, W, M)                                                                    \
     case (S * 8 + D * 4 + W * 2 + M):                                                          \
         hipExtLaunchKernelGGL((k_score_packed<S, D, W, M>), dim3(g), dim3(kBlock), 0, s,       \
                               prof.start(), prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, \
-                              presence);                                                         \
+                              presence, tspan);                                                  \
         break;
     // the bench / C2 configuration (12-bp UMIs, all fields + within bits) has a
     // length-specialised instance (ROGTK_SCORE_GENERIC=1: runtime-length kernel, A/B)
@@ -527,8 +531,9 @@ int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int
     }();
     if (!generic && p.L == 12 && sel == 8 + 2) {
         hipExtLaunchKernelGGL((k_score_packed<true, false, true, false, 12>), dim3(g), dim3(kBlock), 0, s,
-                              prof.start(), prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, presence);
+                              prof.start(), prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, presence, tspan);
         ROGTK_HIP_CHECK(hipGetLastError());
+        span_end(K_SCORE_PACKED, tspan, g, s);
         return ROGTK_OK;
     }
     switch (sel) {
@@ -540,6 +545,7 @@ int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int
     }
 #undef ROGTK_SP
     ROGTK_HIP_CHECK(hipGetLastError());
+    span_end(K_SCORE_PACKED, tspan, g, s);
     return ROGTK_OK;
 }
 

@@ -17,6 +17,7 @@ from __future__ import annotations
 import ctypes
 from typing import Dict, Optional
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -273,6 +274,96 @@ def kmer_spectrum_dev(offsets: torch.Tensor, values: torch.Tensor, group_offsets
     return {"kmers": km[:n], "exts": ex[:n], "counts": cn[:n], "entry_offsets": eo, "stats": st}
 
 
+class PackedReads:
+    """A read column as fixed-size 2-bit blocks in HBM (rogtk_pack_reads): block_words u64
+    per row (meta + bases), so a grouped row is staged as whole 64-B lines."""
+
+    def __init__(self, offsets: torch.Tensor, values: torch.Tensor, validity: Optional[torch.Tensor] = None,
+                 validity_offset: int = 0, max_len: Optional[int] = None, stream=None):
+        n = offsets.numel() - 1
+        if max_len is None:
+            max_len = int((offsets[1:] - offsets[:-1]).max().item()) if n else 0
+        self.max_len = int(max_len)
+        self.block_words = int(_lib.hip().rogtk_read_block_words(self.max_len))
+        if self.block_words == 0:
+            raise ValueError(f"reads up to {self.max_len} bases: too long for the block layout (max 992)")
+        self.n = n
+        self.blocks = torch.empty(max(n * self.block_words, 1), dtype=torch.int64, device=values.device)
+        _lib.call("rogtk_pack_reads", _p(offsets), _p(values), _p(validity), int(validity_offset), n,
+                  self.block_words, _p(self.blocks), _s(stream))
+
+
+def kmer_spectrum_blocks(packed: PackedReads, offsets: torch.Tensor, values: torch.Tensor,
+                         group_offsets: torch.Tensor, k: int, min_coverage: int, capacity: int,
+                         rows: Optional[torch.Tensor] = None, validity: Optional[torch.Tensor] = None,
+                         validity_offset: int = 0, stream=None):
+    """kmer_spectrum_dev over a PackedReads column (same outputs, bit-exact)."""
+    dev = values.device
+    G = group_offsets.numel() - 1
+    n_rows = rows.numel() if rows is not None else offsets.numel() - 1
+    cap = max(int(capacity), 1)
+    km = torch.empty((cap, 2), dtype=torch.int64, device=dev)
+    ex = torch.empty(cap, dtype=torch.uint8, device=dev)
+    cn = torch.empty(cap, dtype=torch.int16, device=dev)
+    eo = torch.empty(G + 1, dtype=torch.int64, device=dev)
+    st = torch.empty((G, 5), dtype=torch.int64, device=dev)
+    m = ctypes.c_int64(0)
+    _lib.call("rogtk_kmer_spectrum_blocks", _p(packed.blocks), packed.block_words, packed.max_len, _p(offsets),
+              _p(values), _p(validity), int(validity_offset), _p(rows), n_rows, _p(group_offsets), G, int(k),
+              int(min_coverage), cap, _p(km), _p(ex), _p(cn), _p(eo), _p(st), ctypes.byref(m), _s(stream))
+    n = int(m.value)
+    return {"kmers": km[:n], "exts": ex[:n], "counts": cn[:n], "entry_offsets": eo, "stats": st}
+
+
+def group_spectra(offsets: torch.Tensor, values: torch.Tensor, keys: torch.Tensor, k: int, min_coverage: int,
+                  batch_rows: int = 10_000_000, consume=None, stream=None, packed="auto"):
+    """The C3 front end after H3 (rogtk/__init__.py:206-214: group_by('umi') then
+    assemble per group): rows grouped by key (stable; e.g. H3 cluster ids), then k-mer
+    spectra (filter_kmers + CountFilter + censored exts, fracture.rs:105-116) over runs of
+    consecutive groups of at most batch_rows rows per call (a group is never split; a
+    larger group gets a call of its own). Output capacity per call = the rows' sum of
+    max(0, len - 3) (the kernels' per-group capacity offsets).
+    Returns (rows int64[n] in group order, group_offsets int64[G + 1], G, calls): with
+    consume=None, calls lists (g0, g1, result) per call, each result (kmer_spectrum_dev's
+    dict for groups g0..g1-1) copied to its own size so the next call can reuse the
+    capacity; else consume(g0, g1, result) is called per call (the result's buffers are
+    reused afterwards) and calls is empty.
+    packed: "auto" packs the column once into 2-bit blocks (PackedReads) when its reads
+    fit the block layout, and every call stages from the blocks; a PackedReads to reuse;
+    None for the ASCII staging path."""
+    if isinstance(packed, str):
+        try:
+            packed = PackedReads(offsets, values, stream=stream)
+        except ValueError:
+            packed = None
+    rows, go, G = group_by_key(keys, stream=stream)
+    if G == 0:
+        return rows, go, G, []
+    goh = go.cpu().numpy()
+    cap_rows = ((offsets[1:] - offsets[:-1]) - 3).clamp(min=0)
+    cuts = [0]
+    while cuts[-1] < G:
+        g0 = cuts[-1]
+        g1 = int(np.searchsorted(goh, goh[g0] + batch_rows, side="right")) - 1
+        cuts.append(min(G, max(g1, g0 + 1)))
+    calls = []
+    for g0, g1 in zip(cuts, cuts[1:]):
+        a, b = int(goh[g0]), int(goh[g1])
+        r = rows[a:b]
+        cap = int(cap_rows[r].sum().item())
+        if packed is not None:
+            res = kmer_spectrum_blocks(packed, offsets, values, go[g0:g1 + 1] - a, k, min_coverage, cap, rows=r,
+                                       stream=stream)
+        else:
+            res = kmer_spectrum_dev(offsets, values, go[g0:g1 + 1] - a, k, min_coverage, cap, rows=r, stream=stream)
+        if consume is not None:
+            consume(g0, g1, res)
+        else:
+            calls.append((g0, g1, {key: t.clone() for key, t in res.items()}))
+        del res
+    return rows, go, G, calls
+
+
 def profile_enable(on: bool = True) -> None:
     _lib.call("rogtk_profile_enable", 1 if on else 0)
 
@@ -290,4 +381,13 @@ def profile_read(kernel: str):
     ms = ctypes.c_double(0)
     n = ctypes.c_int64(0)
     _lib.call("rogtk_profile_read", kernel.encode(), ctypes.byref(ms), ctypes.byref(n))
+    return ms.value, n.value
+
+
+def profile_read_span(kernel: str):
+    """(total ms, launches) of the kernel's own execution spans (in-kernel clocks; the
+    kernels that support it: score_packed)."""
+    ms = ctypes.c_double(0)
+    n = ctypes.c_int64(0)
+    _lib.call("rogtk_profile_read_span", kernel.encode(), ctypes.byref(ms), ctypes.byref(n))
     return ms.value, n.value

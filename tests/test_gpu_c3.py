@@ -1,0 +1,266 @@
+"""GPU: BASELINE config C3's path — the one tools/bench_kmer.py measures — under the oracle.
+
+Pipeline (rogtk_amd.device): synth-v1 150-bp reads + 12-bp UMIs in HBM -> H3 exact UMI ids
+(cluster_batch, max_distance 0: the caller's group_by('umi'), rogtk/__init__.py:206-214)
+-> group_spectra (rogtk_group_by_key + rogtk_kmer_spectrum_dev over runs of consecutive
+groups, k = 17 -> effective 32, min_coverage 20 as rogtk/__init__.py:212) -> every group's
+(k-mer, censored exts, count) list and stats vs oracle/kmer_oracle.cpp (fracture.rs:105-146,
+217-256 + debruijn filter_kmers, restated).
+
+* 1M reads (~111k groups) plus injected groups that force every size class and hand-off:
+  15 / 40 / 100 unrelated reads (distinct k-mers past class 3's and class 1's tables),
+  250 and 700 reads of one template (class 4 and the global radix path), compared in full.
+* 100M reads (the C3 configuration, 11 spectrum calls): size-independent properties over
+  every group (n_sequences, node/terminal/isolated counts recomputed from the returned exts,
+  counts >= min_coverage, ascending k-mers), 300 random groups compared in full with the
+  oracle, and bitwise determinism of a second run.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+RL, UL, K, MINCOV = 150, 12, 17, 20
+THREADS = min(16, os.cpu_count() or 1)
+
+
+def _inject(reads, codes, rng):
+    """Overwrite rows with groups of chosen shapes (fresh UMI codes)."""
+    n = len(codes)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    rows = rng.choice(n, size=15 + 40 + 100 + 250 + 700, replace=False)
+    at = 0
+    used = set(np.unique(codes).tolist())
+    for size, kind in ((15, "random"), (40, "random"), (100, "random"), (250, "template"), (700, "template")):
+        sel = rows[at:at + size]
+        at += size
+        c = int(rng.integers(0, 4 ** UL))
+        while c in used:
+            c = int(rng.integers(0, 4 ** UL))
+        used.add(c)
+        codes[sel] = c
+        if kind == "random":
+            reads[sel] = acgt[rng.integers(0, 4, size=(size, RL))]
+        else:
+            tpl = acgt[rng.integers(0, 4, size=RL + 60)]
+            for j, r in enumerate(sel):
+                a = int(rng.integers(0, 60))
+                reads[r] = tpl[a:a + RL]
+                if rng.random() < 0.2:
+                    reads[r, int(rng.integers(RL))] = acgt[int(rng.integers(4))]
+
+
+def _run_c3(codes_h, reads_h, min_cov=MINCOV, batch_rows=10_000_000, packed="auto"):
+    import torch
+
+    from rogtk_amd import device as D
+
+    n = len(codes_h)
+    codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
+    values = torch.from_numpy(reads_h.reshape(-1)).cuda()
+    offsets = torch.arange(0, (n + 1) * RL, RL, dtype=torch.int64, device="cuda")
+    eng = D.ClusterEngine(UL, min(n, 4 ** UL), "cuda")
+    cid = torch.empty(n, dtype=torch.int32, device="cuda")
+    D.cluster_batch(eng, D.PackedBatch(codes, UL), cid, 0)
+    rows, go, G, calls = D.group_spectra(offsets, values, cid, K, min_cov, batch_rows=batch_rows, packed=packed)
+    torch.cuda.synchronize()
+    return rows, go, G, calls
+
+
+def _concat(calls, G):
+    km, ex, cn, st = [], [], [], []
+    eo = [np.zeros(1, np.int64)]
+    base = 0
+    for g0, g1, r in calls:
+        k = r["kmers"].cpu().numpy().view(np.uint64)
+        km.append(k)
+        ex.append(r["exts"].cpu().numpy())
+        cn.append(r["counts"].cpu().numpy().view(np.uint16))
+        st.append(r["stats"].cpu().numpy())
+        e = r["entry_offsets"].cpu().numpy()
+        eo.append(e[1:] + base)
+        base += int(e[-1])
+    km = np.concatenate(km) if km else np.zeros((0, 2), np.uint64)
+    return {"kmer_hi": km[:, 0], "kmer_lo": km[:, 1], "exts": np.concatenate(ex), "counts": np.concatenate(cn),
+            "group_offsets": np.concatenate(eo), "stats": np.concatenate(st)}
+
+
+@pytest.mark.parametrize("min_cov,batch_rows,packed", [(MINCOV, 10_000_000, "auto"), (2, 200_000, "auto"),
+                                                        (MINCOV, 10_000_000, None)])
+def test_c3_path_1m_vs_oracle(min_cov, batch_rows, packed):
+    """packed "auto": rows staged from the 2-bit block column (rogtk_pack_reads); None: from
+    the ASCII bytes."""
+    from oracle import pyoracle as P
+    from rogtk_amd import _lib
+    from rogtk_amd import synth
+    import ctypes
+
+    n = 1_000_000
+    rng = np.random.default_rng(17 + min_cov)
+    codes_h = synth.umi_codes(n, UL).copy()
+    reads_h = synth.reads(n, RL).copy()
+    _inject(reads_h, codes_h, rng)
+    _lib.call("rogtk_kmer_set_path", 1)
+    rows, go, G, calls = _run_c3(codes_h, reads_h, min_cov, batch_rows, packed)
+    ps = (ctypes.c_int64 * 2)()
+    _lib.call("rogtk_kmer_path_stats", ps)
+    order = np.argsort(codes_h, kind="stable")
+    assert np.array_equal(rows.cpu().numpy(), order)  # group_by: ids in code order, rows stable
+    _, starts = np.unique(codes_h[order], return_index=True)
+    goh = np.concatenate([starts, [n]]).astype(np.int64)
+    assert G == len(starts) and np.array_equal(go.cpu().numpy(), goh)
+    got = _concat(calls, G)
+    ref = P.kmer_spectrum(P.StrCol.from_fixed(reads_h[order]), K, min_cov, False, goh, threads=THREADS)
+    assert np.array_equal(got["group_offsets"], ref["group_offsets"])
+    assert np.array_equal(got["stats"], ref["stats"])
+    for f in ("kmer_hi", "kmer_lo", "exts", "counts"):
+        assert np.array_equal(got[f], ref[f]), f
+    assert G > 100_000 and len(calls) >= (1 if batch_rows >= n else 5)
+
+
+def _props(calls, min_cov):
+    """Size-independent properties of one run; returns (sum n_sequences, groups, a digest)."""
+    import torch
+
+    nseq, groups = 0, 0
+    digest = torch.zeros((), dtype=torch.int64, device="cuda")
+    for g0, g1, r in calls:
+        st = r["stats"].cpu().numpy()
+        eo = r["entry_offsets"].cpu().numpy()
+        ex = r["exts"].cpu().numpy()
+        cn = r["counts"].cpu().numpy().view(np.uint16)
+        km = r["kmers"].cpu().numpy().view(np.uint64)
+        assert (st[:, 0] == 32).all()
+        assert np.array_equal(st[:, 2], np.diff(eo))  # node_count = entries
+        l0, r0 = (ex & 0xF) == 0, (ex >> 4) == 0
+        gid = np.repeat(np.arange(len(eo) - 1), np.diff(eo))
+        assert np.array_equal(np.bincount(gid, weights=(l0 | r0), minlength=len(eo) - 1).astype(np.int64), st[:, 3])
+        assert np.array_equal(np.bincount(gid, weights=(l0 & r0), minlength=len(eo) - 1).astype(np.int64), st[:, 4])
+        assert (cn >= min_cov).all()
+        if len(km) > 1:  # ascending k-mers within a group (k_eff 32: the lo word)
+            same = gid[1:] == gid[:-1]
+            assert (km[1:, 1][same] > km[:-1, 1][same]).all()
+        nseq += int(st[:, 1].sum())
+        groups += len(st)
+        for t in (r["kmers"], r["exts"].to(torch.int64), r["counts"].to(torch.int64)):
+            v = t.reshape(-1).to(torch.int64)
+            w = torch.arange(1, v.numel() + 1, device=v.device, dtype=torch.int64) * 0x9E3779B1
+            digest += (v * w).sum()
+    return nseq, groups, int(digest.item())
+
+
+def test_c3_full_size_100m_properties():
+    import torch
+
+    from oracle import pyoracle as P
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+
+    n = 100_000_000
+    codes_h = synth.umi_codes(n, UL)
+    values = torch.empty(n * RL, dtype=torch.uint8, device="cuda")
+    chunk = 5_000_000
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        values[a * RL:b * RL] = torch.from_numpy(synth.reads(n, RL, start=a, count=b - a).reshape(-1)).cuda()
+    print("C3 100M: reads in HBM", flush=True)
+    codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
+    offsets = torch.arange(0, (n + 1) * RL, RL, dtype=torch.int64, device="cuda")
+    eng = D.ClusterEngine(UL, min(n, 4 ** UL), "cuda")
+    cid = torch.empty(n, dtype=torch.int32, device="cuda")
+    results = []
+    for run in range(2):
+        D.cluster_batch(eng, D.PackedBatch(codes, UL), cid, 0)
+        rows, go, G, calls = D.group_spectra(offsets, values, cid, K, MINCOV)
+        torch.cuda.synchronize()
+        results.append(_props(calls, MINCOV) + (G, len(calls)))
+        print(f"C3 100M run {run}: {results[-1]}", flush=True)
+        if run == 0:
+            # 300 random groups in full against the oracle
+            rng = np.random.default_rng(3)
+            goh = go.cpu().numpy()
+            pick = np.sort(rng.choice(G, size=300, replace=False))
+            rows_h = rows.cpu().numpy()
+            sub_rows, sub_go = [], [0]
+            for g in pick:
+                rr = rows_h[goh[g]:goh[g + 1]]
+                sub_rows.append(rr)
+                sub_go.append(sub_go[-1] + len(rr))
+            sub_rows = np.concatenate(sub_rows)
+            reads_sub = values.view(n, RL)[torch.from_numpy(sub_rows).cuda()].cpu().numpy()
+            ref = P.kmer_spectrum(P.StrCol.from_fixed(reads_sub), K, MINCOV, False, np.array(sub_go), threads=THREADS)
+            starts = np.concatenate([[0], np.cumsum([len(c[2]["stats"]) for c in calls])])
+            for j, g in enumerate(pick):
+                ci = int(np.searchsorted(starts, g, side="right")) - 1
+                r = calls[ci][2]
+                lg = g - starts[ci]
+                eo = r["entry_offsets"][lg:lg + 2].cpu().numpy()
+                a, b = int(eo[0]), int(eo[1])
+                ra, rb = int(ref["group_offsets"][j]), int(ref["group_offsets"][j + 1])
+                assert np.array_equal(r["stats"][lg].cpu().numpy(), ref["stats"][j])
+                km = r["kmers"][a:b].cpu().numpy().view(np.uint64)
+                assert np.array_equal(km[:, 0], ref["kmer_hi"][ra:rb]) and np.array_equal(km[:, 1], ref["kmer_lo"][ra:rb])
+                assert np.array_equal(r["exts"][a:b].cpu().numpy(), ref["exts"][ra:rb])
+                assert np.array_equal(r["counts"][a:b].cpu().numpy().view(np.uint16), ref["counts"][ra:rb])
+        del calls, rows, go
+    assert results[0] == results[1]  # bitwise deterministic (digest of every output array)
+    nseq, groups, _, G, ncalls = results[0]
+    assert nseq == n and groups == G and ncalls >= 10
+
+
+@pytest.mark.parametrize("lo,hi,bw", [(0, 150, 8), (100, 420, 16), (300, 990, 32)])
+def test_packed_blocks_match_oracle(lo, hi, bw):
+    """rogtk_pack_reads + rogtk_kmer_spectrum_blocks on ragged reads (empty rows, nulls, N,
+    lowercase, every block size) vs the oracle, for several k and both LDS and radix paths."""
+    import torch
+
+    from oracle import pyoracle as P
+    from rogtk_amd import _lib
+    from rogtk_amd import device as D
+
+    rng = np.random.default_rng(lo + hi)
+    groups, items, go = 400, [], [0]
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    for g in range(groups):
+        tpl = acgt[rng.integers(0, 4, size=hi + 50)]
+        for _ in range(int(rng.integers(1, 40 if g % 50 else 600))):
+            r = rng.random()
+            if r < 0.03:
+                items.append(None)
+                continue
+            L = int(rng.integers(lo, hi + 1))
+            a = int(rng.integers(0, 50))
+            x = bytearray(tpl[a:a + L].tobytes())
+            if r < 0.06 and L:
+                x[int(rng.integers(L))] = ord("N")
+            elif r < 0.09:
+                x = x.lower()
+            items.append(bytes(x))
+        go.append(len(items))
+    n = len(items)
+    lens = np.array([0 if x is None else len(x) for x in items], np.int64)
+    off = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)])).cuda()
+    vals = torch.from_numpy(np.frombuffer(b"".join(x for x in items if x is not None) or b"\0", np.uint8).copy()).cuda()
+    valid = np.array([x is not None for x in items])
+    vbits = torch.from_numpy(np.packbits(np.concatenate([valid, np.zeros(7, bool)]), bitorder="little")).cuda()
+    pk = D.PackedReads(off, vals, validity=vbits)
+    assert pk.block_words == bw
+    gsel = torch.tensor(go, dtype=torch.int64).cuda()
+    col = P.StrCol.from_list(items)
+    for k, mc in ((13, 2), (17, 1), (33, 2)):
+        ref = P.kmer_spectrum(col, k, mc, False, np.array(go), threads=THREADS)
+        for path in (1, 0):
+            _lib.call("rogtk_kmer_set_path", path)
+            cap = int(np.clip(lens - 3, 0, None).sum())
+            got = D.kmer_spectrum_blocks(pk, off, vals, gsel, k, mc, cap, validity=vbits)
+            torch.cuda.synchronize()
+            km = got["kmers"].cpu().numpy().view(np.uint64)
+            assert np.array_equal(got["entry_offsets"].cpu().numpy(), ref["group_offsets"]), (k, path)
+            assert np.array_equal(got["stats"].cpu().numpy(), ref["stats"]), (k, path)
+            assert np.array_equal(km[:, 0], ref["kmer_hi"]) and np.array_equal(km[:, 1], ref["kmer_lo"]), (k, path)
+            assert np.array_equal(got["exts"].cpu().numpy(), ref["exts"]), (k, path)
+            assert np.array_equal(got["counts"].cpu().numpy().view(np.uint16), ref["counts"]), (k, path)
+    _lib.call("rogtk_kmer_set_path", 1)

@@ -174,6 +174,21 @@ def test_cluster_irregular_bridges_regular_clusters():
     assert len({ids[b"ACG"], ids[b"ACGTA"], ids[b"acgt"], 0}) == 4 and k == 4
 
 
+def test_cluster_oracle_threads_identical():
+    """oracle_umi_cluster_mt (bench.py's multi-threaded CPU baseline) == the serial oracle."""
+    from conftest import irregular_families
+    from rogtk_amd import synth
+
+    cols = [P.StrCol.from_fixed(synth.umi_ascii(300_000, 12, p_n=1e-3, p_lower=5e-4)),
+            P.StrCol.from_list(irregular_families(9, 3000, 10))]
+    for col in cols:
+        for md in (0, 1):
+            ref = P.umi_cluster(col, 0, md, threads=1)
+            for t in (2, 7, 16):
+                got = P.umi_cluster(col, 0, md, threads=t)
+                assert got[2] == ref[2] and np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
+
+
 @pytest.mark.parametrize("seed,L", [(1, 4), (2, 6), (3, 12), (4, 20), (5, 33)])
 def test_cluster_oracle_vs_bruteforce_irregular_families(seed, L):
     from conftest import irregular_families

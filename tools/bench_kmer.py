@@ -4,11 +4,12 @@
 One step = one batch of synthetic 150-bp reads with 12-bp UMIs, resident in HBM:
   H3 exact UMI ids    (mark -> bitmap -> resolve(max_distance 0) -> assign; the
                        caller-side group_by('umi') of rogtk/__init__.py:206-214)
-  group_by            rogtk_group_by_key: stable radix sort of the ids -> row
-                       permutation + group offsets
-  k-mer spectra       rogtk_kmer_spectrum_dev, k = 17 (effective 32), min_coverage
+  group_spectra       rogtk_amd.device.group_spectra: rogtk_group_by_key (stable radix
+                       sort of the ids -> row permutation + group offsets), then
+                       rogtk_kmer_spectrum_dev, k = 17 (effective 32), min_coverage
                        20 (rogtk/__init__.py:212): filter_kmers + CountFilter +
-                       censored exts per group (LDS path for small groups)
+                       censored exts per group (LDS path for small groups), in calls of
+                       <= 10M rows; tests/test_gpu_c3.py checks this path vs the oracle
 Prints one JSON line: reads/s over the timed steps, per-phase HIP-event times and
 the LDS / global path split. Not the driver's bench (bench.py is C2).
 
@@ -40,6 +41,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--global-only", action="store_true", help="route every group through the radix-sort path")
+    ap.add_argument("--ascii", action="store_true",
+                    help="stage grouped rows from their ASCII bytes (no rogtk_pack_reads block column)")
     ap.add_argument("--group-batch-rows", type=int, default=10_000_000,
                     help="k-mer spectra run over consecutive groups of at most this many rows per call "
                          "(bounds the output capacity: 19 B x (read_len - 3) per row)")
@@ -59,48 +62,38 @@ def main():
     eng = D.ClusterEngine(L, min(n, 4 ** L), dev)
     cid = torch.empty(n, dtype=torch.int32, device=dev)
     br = min(n, args.group_batch_rows)
-    cap = br * max(0, RL - 3)
     _lib.call("rogtk_kmer_set_path", 0 if args.global_only else 1)
     ev = lambda: torch.cuda.Event(enable_timing=True)
-    phases = {"cluster": 0.0, "group_by": 0.0, "kmer": 0.0}
+    phases = {"cluster": 0.0, "group_by+kmer": 0.0}
     out = None
     path_groups = [0, 0]
 
     def step(record):
         nonlocal out
-        e0, e1, e2, e3 = ev(), ev(), ev(), ev()
+        e0, e1, e3 = ev(), ev(), ev()
         e0.record()
         D.cluster_batch(eng, batch, cid, 0)
         e1.record()
-        rows, go, G = D.group_by_key(cid)
-        e2.record()
         path_groups[:] = [0, 0]
-        # consecutive groups of <= br rows per spectrum call (a group is never split)
-        goh = go.cpu().numpy()
-        cuts = [0]
-        while cuts[-1] < G:
-            g0 = cuts[-1]
-            g1 = int(np.searchsorted(goh, goh[g0] + br, side="right")) - 1
-            cuts.append(min(G, max(g1, g0 + 1)))
-        valid, stats = 0, []
-        for g0, g1 in zip(cuts, cuts[1:]):
-            a, b = int(goh[g0]), int(goh[g1])
-            r = D.kmer_spectrum_dev(offsets, reads, go[g0:g1 + 1] - a, args.k, args.min_coverage, cap,
-                                    rows=rows[a:b])
-            valid += int(r["entry_offsets"][-1].item())
-            stats.append(r["stats"])
-            del r  # the next call reuses the output capacity (torch caching allocator)
+        acc = {"valid": 0, "stats": [], "calls": 0}
+
+        def consume(g0, g1, r):  # per spectrum call (the same path tests/test_gpu_c3.py checks)
+            acc["valid"] += int(r["entry_offsets"][-1].item())
+            acc["stats"].append(r["stats"].clone())
+            acc["calls"] += 1
             ps = (ctypes.c_int64 * 2)()
             _lib.call("rogtk_kmer_path_stats", ps)
             path_groups[0] += ps[0]
             path_groups[1] += ps[1]
-        out = {"n_calls": len(cuts) - 1, "valid": valid, "stats": torch.cat(stats)}
+
+        _, _, G, _ = D.group_spectra(offsets, reads, cid, args.k, args.min_coverage, batch_rows=br, consume=consume,
+                                     packed=None if args.ascii else "auto")
+        out = {"n_calls": acc["calls"], "valid": acc["valid"], "stats": torch.cat(acc["stats"])}
         e3.record()
         torch.cuda.synchronize()
         if record:
             phases["cluster"] += e0.elapsed_time(e1)
-            phases["group_by"] += e1.elapsed_time(e2)
-            phases["kmer"] += e2.elapsed_time(e3)
+            phases["group_by+kmer"] += e1.elapsed_time(e3)
         return G
 
     for _ in range(args.warmup):
@@ -118,6 +111,7 @@ def main():
         "value": round(n * args.steps / el, 1), "unit": "reads/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 3),
         "config": {"workload": "C3: H3 exact UMI ids -> group_by -> k-mer spectra per group",
+                   "staging": "ASCII rows" if args.ascii else "2-bit block column (rogtk_pack_reads, once per step)",
                    "reads": n, "read_len": RL, "umi_len": L, "k": args.k, "k_eff": int(st[:, 0].max()),
                    "min_coverage": args.min_coverage, "groups": G, "lds_groups": paths[0],
                    "global_groups": paths[1], "valid_kmers": out["valid"], "spectrum_calls": out["n_calls"],
