@@ -93,6 +93,10 @@ def parse():
     ap.add_argument("--reuse-gate", choices=("auto", "score", "resolve"), default="auto",
                     help="slot reuse: the main stream (score) or only the resolve waits for the slot's last assign")
     ap.add_argument("--prio", type=str, default="0,0,0", help="stream priorities main,resolve,assign (-1 = high)")
+    ap.add_argument("--mark-first", action="store_true",
+                    help="main stream order mark -> score (the resolve overlaps the score kernel)")
+    ap.add_argument("--late-assign", action="store_true",
+                    help="host order: enqueue batch k-1's assign after batch k's resolve (round-2 default)")
     return ap.parse_args()
 
 
@@ -288,7 +292,8 @@ def main():
                        priorities=tuple(int(x) for x in args.prio.split(",")), mark=args.mark,
                        score_alone=not args.overlap_score, exchange=exchange,
                        resolve_streams=args.resolve_streams, assign_on=args.assign_on,
-                       split_resolve=args.split_resolve, reuse_gate=args.reuse_gate)
+                       split_resolve=args.split_resolve, reuse_gate=args.reuse_gate,
+                       assign_early=not args.late_assign, mark_first=args.mark_first)
 
     def step():
         pipe.submit(batch)

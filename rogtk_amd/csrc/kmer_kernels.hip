@@ -198,15 +198,28 @@ __global__ __launch_bounds__(kBlock) void k_pack_reads(const int64_t* __restrict
     constexpr int R = B == 32 ? 128 : kPackRowsPerBlock;  // rows per workgroup
     __shared__ uint32_t in32[kPackInBytes / 4];
     __shared__ uint64_t out[R * B];
+    __shared__ int64_t s_off[R + 1];
+    __shared__ uint8_t s_valid[R];
     const uint8_t* in8 = reinterpret_cast<const uint8_t*>(in32);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int64_t a = (int64_t)blockIdx.x * R; a < n; a += (int64_t)gridDim.x * R) {
         const int nr = (int)min<int64_t>(R, n - a);
-        const int64_t b0 = offsets[a], b1 = offsets[a + nr];
+        // the rows' offsets and validity in LDS (coalesced; the row loop below then has no
+        // dependent global loads)
+        for (int i = tid; i <= nr; i += kBlock) s_off[i] = offsets[a + i];
+        for (int i = tid; i < nr; i += kBlock) {
+            bool v = true;
+            if (validity) {
+                const int64_t bit = voff + a + i;
+                v = (validity[bit >> 3] >> (bit & 7)) & 1;
+            }
+            s_valid[i] = v ? 1 : 0;
+        }
+        __syncthreads();
+        const int64_t b0 = s_off[0], b1 = s_off[nr];
         const int64_t a4 = b0 & ~3ll;  // dword-aligned start
         const bool staged = b1 - a4 <= kPackInBytes;
-        if (staged) {  // the rows' bytes, coalesced: dword loads (the column's tail is padded by whole dwords
-                       // only where they exist: bytes past b1 are not read)
+        if (staged) {  // the rows' bytes, coalesced dword loads (no byte past b1 is read)
             const int64_t nw = (b1 - a4 + 3) >> 2;
             const uint32_t* src = reinterpret_cast<const uint32_t*>(values + a4);
             const int64_t full = (b1 - a4) >> 2;  // dwords entirely inside [a4, b1)
@@ -225,13 +238,8 @@ __global__ __launch_bounds__(kBlock) void k_pack_reads(const int64_t* __restrict
         }
         __syncthreads();
         for (int q = wave; q < nr; q += kWavesPerBlock) {
-            const int64_t r = a + q;
-            bool valid = true;
-            if (validity) {
-                const int64_t bit = voff + r;
-                valid = (validity[bit >> 3] >> (bit & 7)) & 1;
-            }
-            const int64_t st = offsets[r], len = offsets[r + 1] - st;
+            const bool valid = s_valid[q];
+            const int64_t st = s_off[q], len = s_off[q + 1] - st;
             uint64_t* ob = out + q * B;
             bool bad = false;
             if (valid) {

@@ -321,8 +321,8 @@ def group_spectra(offsets: torch.Tensor, values: torch.Tensor, keys: torch.Tenso
     assemble per group): rows grouped by key (stable; e.g. H3 cluster ids), then k-mer
     spectra (filter_kmers + CountFilter + censored exts, fracture.rs:105-116) over runs of
     consecutive groups of at most batch_rows rows per call (a group is never split; a
-    larger group gets a call of its own). Output capacity per call = the rows' sum of
-    max(0, len - 3) (the kernels' per-group capacity offsets).
+    larger group gets a call of its own). Output capacity per call = its rows x
+    max(0, longest row - 3).
     Returns (rows int64[n] in group order, group_offsets int64[G + 1], G, calls): with
     consume=None, calls lists (g0, g1, result) per call, each result (kmer_spectrum_dev's
     dict for groups g0..g1-1) copied to its own size so the next call can reuse the
@@ -340,7 +340,10 @@ def group_spectra(offsets: torch.Tensor, values: torch.Tensor, keys: torch.Tenso
     if G == 0:
         return rows, go, G, []
     goh = go.cpu().numpy()
-    cap_rows = ((offsets[1:] - offsets[:-1]) - 3).clamp(min=0)
+    # output capacity per call: rows x (longest row - 3) bounds the valid entries (each
+    # row adds at most len - 3 k-mers, k_eff >= 4)
+    max_len = packed.max_len if packed is not None else int((offsets[1:] - offsets[:-1]).max().item())
+    per_row = max(0, max_len - 3)
     cuts = [0]
     while cuts[-1] < G:
         g0 = cuts[-1]
@@ -350,7 +353,7 @@ def group_spectra(offsets: torch.Tensor, values: torch.Tensor, keys: torch.Tenso
     for g0, g1 in zip(cuts, cuts[1:]):
         a, b = int(goh[g0]), int(goh[g1])
         r = rows[a:b]
-        cap = int(cap_rows[r].sum().item())
+        cap = (b - a) * per_row
         if packed is not None:
             res = kmer_spectrum_blocks(packed, offsets, values, go[g0:g1 + 1] - a, k, min_coverage, cap, rows=r,
                                        stream=stream)

@@ -57,7 +57,8 @@ class UmiPipeline:
                  target: Optional[bytes] = b"ACGTACGTACGT", max_hamming: int = 1, max_distance: int = 1,
                  group=None, with_scores: bool = True, priorities=(0, 0, 0), mark: str = "auto",
                  on_assigned=None, score_alone: bool = False, exchange=None, resolve_streams: int = 1,
-                 assign_on: str = "separate", split_resolve: bool = False, reuse_gate: str = "auto"):
+                 assign_on: str = "separate", split_resolve: bool = False, reuse_gate: str = "auto",
+                 assign_early: bool = True, mark_first: bool = False):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
@@ -89,6 +90,15 @@ class UmiPipeline:
         # on_assigned(slot, batch): called with the assign stream current, after the
         # batch's assign and before its slot may be reused (e.g. to copy outputs out)
         self.on_assigned = on_assigned
+        # assign_early: batch k-1's assign is enqueued right after batch k's score kernel
+        # (host order), not after batch k's resolve (the host's enqueue of a resolve takes
+        # longer than the GPU needs to reach the assign)
+        self.assign_early = assign_early
+        # mark_first: batch k's presence bitmap (mark) runs before its score kernel on the
+        # main stream, so its resolve overlaps the score instead of following it
+        if mark_first and self.fused_mark:
+            raise ValueError("mark_first needs a separate mark (not mark='fused')")
+        self.mark_first = mark_first
         # score_alone: assign of the previous batch waits for this batch's score kernel,
         # so the HBM-bound score overlaps only the latency-bound resolve kernels
         self.score_alone = score_alone
@@ -147,11 +157,41 @@ class UmiPipeline:
         gate_resolve = self.reuse_gate == "resolve"
         if slot.assigned is not None and not gate_resolve:
             self.main.wait_event(slot.assigned)
+        if self.mark_first:
+            # the presence bitmap needs only the codes: mark first, so the latency-bound
+            # resolve of this batch starts while its score kernel streams
+            resolved = self._mark_resolve(slot, batch, gate_resolve)
+            self._score(slot, batch)
+        else:
+            self._score(slot, batch)
+            resolved = None
+        if self.assign_early:
+            # the previous batch's assign goes in right behind this batch's score kernel,
+            # before the ~20 launches of this batch's mark + resolve: the GPU can start it
+            # as soon as its resolve and this score are done instead of waiting for the
+            # host to get through this batch's enqueues
+            while self.queue and len(self.queue) >= max(self.lag, 1):
+                self._assign_oldest()
+        if resolved is None:
+            resolved = self._mark_resolve(slot, batch, gate_resolve)
+        slot.resolved = resolved
+        self.queue.append((slot, batch, resolved))
+        if not self.assign_early or self.lag == 0:
+            while len(self.queue) > self.lag:
+                self._assign_oldest()
+        self.k += 1
+        return slot
+
+    def _score(self, slot: _Slot, batch: D.PackedBatch):
         D.score_packed(batch, slot.scores, self.target, self.max_hamming, None, slot.within,
                        cluster=slot.eng if self.fused_mark else None, stream=self.main)
         if self.score_alone:
             self.last_scored = torch.cuda.Event()
             self.last_scored.record(self.main)
+
+    def _mark_resolve(self, slot: _Slot, batch: D.PackedBatch, gate_resolve: bool):
+        """Presence bitmap (main stream), [exchange], resolve (resolve stream); returns the
+        resolve's completion event."""
         if gate_resolve and slot.resolved is not None:
             self.main.wait_event(slot.resolved)  # the previous resolve read the bitmap
         if self.sort_mark:
@@ -188,12 +228,7 @@ class UmiPipeline:
                 slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr)
             resolved = torch.cuda.Event()
             resolved.record(sr)
-        slot.resolved = resolved
-        self.queue.append((slot, batch, resolved))
-        while len(self.queue) > self.lag:
-            self._assign_oldest()
-        self.k += 1
-        return slot
+        return resolved
 
     def _settle(self, slot: _Slot, stream=None):
         """The slot's previous batch is final: its resolve converged (or is completed now,

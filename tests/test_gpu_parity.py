@@ -527,8 +527,10 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assig
 
 @pytest.mark.parametrize("spec", [1, 4])
 @pytest.mark.parametrize("depth,nb", [(2, 5), (3, 3), (1, 2)])
-@pytest.mark.parametrize("assign_on,gate", [("separate", "auto"), ("separate", "resolve"), ("resolve", "auto")])
-def test_pipeline_deferred_assign(rg, depth, nb, spec, assign_on, gate):
+@pytest.mark.parametrize("assign_on,gate,order", [("separate", "auto", "score_first"), ("separate", "resolve", "score_first"),
+                                                  ("resolve", "auto", "score_first"), ("separate", "auto", "mark_first"),
+                                                  ("separate", "auto", "late_assign")])
+def test_pipeline_deferred_assign(rg, depth, nb, spec, assign_on, gate, order):
     """No on_assigned hook: assigns are enqueued before their resolve's flags are checked;
     with 1 speculative round every batch needs the deferred completion (rounds + labels +
     the assign again) when its slot comes round or at drain. With reuse_gate "resolve",
@@ -545,7 +547,8 @@ def test_pipeline_deferred_assign(rg, depth, nb, spec, assign_on, gate):
     try:
         D.set_spec_rounds(spec)
         pipe = UmiPipeline(L, n, n, "cuda", depth=depth, target=b"ACGTACGTACGT", max_distance=1,
-                           assign_on=assign_on, reuse_gate=gate, score_alone=depth == 2)
+                           assign_on=assign_on, reuse_gate=gate, score_alone=depth == 2,
+                           mark_first=order == "mark_first", assign_early=order != "late_assign")
         keep, last = [], {}
         for k, s in enumerate(seeds):
             codes = torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda()
@@ -822,3 +825,39 @@ def test_slice_bucket_overflow_falls_back(rg, L, skew):
             assert torch.equal(ref, got), skew
     finally:
         D.set_mark_method(D.MARK_AUTO)
+
+
+def test_level2_transfers_pinned_and_pageable(rg):
+    """The level-2 entry points move data by direct DMA for pinned buffers (rogtk_host_alloc:
+    the Python API's results) and through the pinned staging chunks (32 MiB) for pageable
+    ones: 6M rows (72 MB of values, 48 MB per f64 field) give the same bytes both ways and
+    equal the oracle on a sample."""
+    import ctypes
+
+    from rogtk_amd import _lib
+    from rogtk_amd import synth
+
+    n, L = 6_000_000, 12
+    asc = synth.umi_ascii(n, L, p_n=1e-4)
+    offs = np.arange(0, (n + 1) * L, L, dtype=np.int64)
+    vals = asc.reshape(-1)
+    col = pa.Array.from_buffers(pa.large_binary(), n, [None, pa.py_buffer(offs), pa.py_buffer(vals)])
+    pinned = rg.umi_complexity_scores(col)  # results in rogtk_host_alloc blocks
+    out = {name: np.zeros(n, dtype=np.uint32 if name == "longest_homopolymer_run" else np.float64)
+           for name, _ in rg.FIELDS}
+    sc = _lib.UmiScores(*[ctypes.c_void_p(out[name].ctypes.data) for name, _ in rg.FIELDS])
+    _lib.call("rogtk_umi_complexity_host", ctypes.c_void_p(offs.ctypes.data), 8, ctypes.c_void_p(vals.ctypes.data),
+              vals.size, None, 0, n, ctypes.byref(sc))
+    for name, _ in rg.FIELDS:
+        a = _np(pinned.field(name))
+        assert np.array_equal(a.view(np.uint64) if a.dtype == np.float64 else a,
+                              out[name].view(np.uint64) if out[name].dtype == np.float64 else out[name]), name
+    idx = np.random.default_rng(1).choice(n, size=20_000, replace=False)
+    ref = P().umi_complexity(P().StrCol.from_fixed(asc[idx]))
+    _assert_scores_equal({k: v[idx] for k, v in out.items()}, ref, np.ones(len(idx), bool))
+    cid_p, k_p, _ = rg.umi_cluster(col, L, 1)
+    cid = np.zeros(n, np.uint32)
+    nk, rl = ctypes.c_int64(0), ctypes.c_int(0)
+    _lib.call("rogtk_umi_cluster_host", ctypes.c_void_p(offs.ctypes.data), 8, ctypes.c_void_p(vals.ctypes.data),
+              vals.size, None, 0, n, L, 1, ctypes.c_void_p(cid.ctypes.data), ctypes.byref(nk), ctypes.byref(rl))
+    assert nk.value == k_p and np.array_equal(_np(cid_p).astype(np.uint32), cid)

@@ -12,3 +12,6 @@ done
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 rm -rf gpurun_out/prof_c3 && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python3 tools/bench_kmer.py --reads 100000000 --steps 2 --warmup 1 > gpurun_out/prof_c3.log 2>&1
 echo "prof rc=$?"
+timeout -k 10 200 python tools/host_submit_time.py separate > gpurun_out/host_submit.log 2>&1; echo "host_submit rc=$?"; tail -15 gpurun_out/host_submit.log
+rm -rf gpurun_out/prof_tl && timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/prof_tl -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-profile --no-cpu-baseline --no-end-to-end > gpurun_out/prof_tl.log 2>&1
+echo "timeline rc=$?"
