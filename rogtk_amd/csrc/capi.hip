@@ -452,6 +452,34 @@ struct HostCol {
     }
 };
 
+// Longest row of a device column (irregular rows' radix-sort / byte-path width).
+template <class O>
+__global__ void k_max_len(const O* __restrict__ off, int64_t n, unsigned long long* out) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long m = 0;
+    if (r < n) m = (unsigned long long)((int64_t)off[r + 1] - (int64_t)off[r]);
+    for (int d = 32; d; d >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, d));
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
+}
+
+// max_len of the column already uploaded to c->offsets (device reduction; one sync)
+int device_max_len(HostCtx* c, int ow, int64_t n, int64_t* out) {
+    if (int rc = c->nirr.ensure(16)) return rc;
+    unsigned long long* slot = c->nirr.as<unsigned long long>() + 1;
+    ROGTK_HIP_CHECK(hipMemsetAsync(slot, 0, 8, c->stream));
+    const dim3 g((unsigned)((n + 255) / 256));
+    if (ow == 4)
+        hipLaunchKernelGGL(k_max_len<int32_t>, g, dim3(256), 0, c->stream, c->offsets.as<int32_t>(), n, slot);
+    else
+        hipLaunchKernelGGL(k_max_len<int64_t>, g, dim3(256), 0, c->stream, c->offsets.as<int64_t>(), n, slot);
+    ROGTK_HIP_CHECK(hipGetLastError());
+    unsigned long long h = 0;
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&h, slot, 8, hipMemcpyDeviceToHost, c->stream));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(c->stream));
+    *out = (int64_t)h;
+    return ROGTK_OK;
+}
+
 // Upload a host column and stage it; returns the resolved packed length in *L.
 int upload_and_stage(HostCtx* c, const HostCol& h, int L_req, int* L_out, int64_t* n_irr_host) {
     const int64_t n = h.n;
@@ -479,7 +507,7 @@ int upload_and_stage(HostCtx* c, const HostCol& h, int L_req, int* L_out, int64_
     if (c->codes.ensure((size_t)std::max<int64_t>(n, 4) * 4) != ROGTK_OK ||
         c->regbits.ensure((size_t)std::max<int64_t>(words, 1) * 8) != ROGTK_OK ||
         c->irr.ensure((size_t)std::max<int64_t>(n, 1) * 8) != ROGTK_OK ||
-        c->nirr.ensure(8) != ROGTK_OK)
+        c->nirr.ensure(16) != ROGTK_OK)
         return ROGTK_E_HIP;
     ROGTK_HIP_CHECK(hipMemsetAsync(c->nirr.p, 0, 8, c->stream));
     int rc = launch_stage(c->offsets.p, ow, c->values.as<uint8_t>(), dvalid, h.voff, n, L,
@@ -784,8 +812,10 @@ int rogtk_umi_complexity_host(const void* offsets, int offset_width, const uint8
     if (int rc = host_ctx(&c)) return rc;
     int L = 0;
     int64_t n_irr = 0;
-    const int64_t max_len = h.max_len();
     if (int rc = upload_and_stage(c, h, 0, &L, &n_irr)) return rc;
+    int64_t max_len = 0;  // only the byte path (irregular rows) needs it
+    if (n_irr > 0)
+        if (int rc = device_max_len(c, offset_width, n, &max_len)) return rc;
     const ScoreOut ho = to_score_out(out);
     // device outputs
     double* dptr[6] = {nullptr};
@@ -836,8 +866,10 @@ int rogtk_hamming_host(const void* offsets, int offset_width, const uint8_t* val
     if (int rc = host_ctx(&c)) return rc;
     int L = 0;
     int64_t n_irr = 0;
-    const int64_t max_len = h.max_len();
     if (int rc = upload_and_stage(c, h, 0, &L, &n_irr)) return rc;
+    int64_t max_len = 0;  // only the byte path (irregular rows) needs it
+    if (n_irr > 0)
+        if (int rc = device_max_len(c, offset_width, n, &max_len)) return rc;
     uint32_t* dd = nullptr;
     uint64_t* dw = nullptr;
     if (distance) {
@@ -872,14 +904,6 @@ int rogtk_hamming_host(const void* offsets, int offset_width, const uint8_t* val
 
 namespace {
 
-// Longest row of a device column (irregular rows' radix-sort width).
-__global__ void k_max_len(const int64_t* __restrict__ off, int64_t n, unsigned long long* out) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    unsigned long long m = 0;
-    if (r < n) m = (unsigned long long)(off[r + 1] - off[r]);
-    for (int d = 32; d; d >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, d));
-    if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
-}
 
 // H3 over a column already staged into c->codes / regbits / irr (n_irr irregular rows):
 // regular rows through the cluster engine, then the irregular rows (exact bytes, or for
@@ -970,10 +994,12 @@ int rogtk_umi_cluster_host(const void* offsets, int offset_width, const uint8_t*
     if (int rc = upload_and_stage(c, h, L, &L, &n_irr)) return rc;
     if (int rc = c->out[0].ensure((size_t)std::max<int64_t>(n, 4) * 4)) return rc;
     uint32_t* did = c->out[0].as<uint32_t>();
+    int64_t max_len = 0;  // irregular rows and the long engine need it
+    if (n_irr || (L > kMaxPackedLen && L <= 32))
+        if (int rc = device_max_len(c, offset_width, n, &max_len)) return rc;
     if (int rc = cluster_staged(c, c->offsets.p, offset_width, c->values.as<uint8_t>(),
-                                h.validity ? c->validity.as<uint8_t>() : nullptr, h.voff, n, L, n_irr,
-                                (n_irr || (L > kMaxPackedLen && L <= 32)) ? h.max_len() : 0, max_distance, did,
-                                n_clusters, c->stream))
+                                h.validity ? c->validity.as<uint8_t>() : nullptr, h.voff, n, L, n_irr, max_len,
+                                max_distance, did, n_clusters, c->stream))
         return rc;
     return c->d2h(cluster_id, did, (size_t)n * 4);
 }
@@ -999,7 +1025,7 @@ int rogtk_umi_cluster_dev(const int64_t* offsets, const uint8_t* values, const u
     if (int rc = launch_stage(offsets, 8, values, validity, 0, n, umi_len, c->codes.as<uint32_t>(),
                               c->regbits.as<uint64_t>(), c->irr.as<int64_t>(), c->nirr.as<unsigned long long>(), s))
         return rc;
-    hipLaunchKernelGGL(k_max_len, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, offsets, n,
+    hipLaunchKernelGGL(k_max_len<int64_t>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, offsets, n,
                        c->nirr.as<unsigned long long>() + 1);
     ROGTK_HIP_CHECK(hipGetLastError());
     int64_t hv[2];

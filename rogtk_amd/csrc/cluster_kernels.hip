@@ -398,15 +398,14 @@ __device__ __forceinline__ uint64_t comps_any(const WordComps& w, uint64_t seed,
 // dense 68 -> 51 us; the LP = 8 tiling now takes those spaces, so it was dropped - its
 // empty launch cost ~5 us of every resolve.)
 
+// One tile of TW words at word `base` (the body of k_local_cc / k_local_cc_loop).
 template <int CAP, int TW, int LP>
-__global__ __launch_bounds__(TW) void k_local_cc(const uint4* __restrict__ RT, int64_t words, int L,
-                                                 uint32_t* __restrict__ f, uint32_t* __restrict__ D,
-                                                 uint32_t* __restrict__ UR, uint64_t* __restrict__ lroot,
-                                                 int64_t rwords,
-                                                 int64_t max_distinct,
-                                                 unsigned long long* __restrict__ stats) {
+__device__ __forceinline__ void local_cc_tile(const int64_t base, const uint4* __restrict__ RT, int64_t words, int L,
+                                              uint32_t* __restrict__ f, uint32_t* __restrict__ D,
+                                              uint32_t* __restrict__ UR, uint64_t* __restrict__ lroot,
+                                              int64_t rwords, int64_t max_distinct,
+                                              unsigned long long* __restrict__ stats) {
     constexpr int kLrb = CAP / 64 + 2;
-    if (((int)stats[S_P0] == 8 ? 8 : 7) != LP) return;  // the other tiling
     __shared__ uint64_t wb[TW];
     __shared__ uint64_t wcm[kWordComps][TW];  // listed component masks per word
     __shared__ uint32_t lpre[TW];
@@ -416,7 +415,6 @@ __global__ __launch_bounds__(TW) void k_local_cc(const uint4* __restrict__ RT, i
     __shared__ uint64_t lrb[kLrb];  // local-root bits of the block's index range
     __shared__ uint32_t s_wave[TW / 64];
     const int t = threadIdx.x;
-    const int64_t base = (int64_t)blockIdx.x * TW;
     const int nw = (int)min<int64_t>(TW, words - base);
     const uint4 e = t < nw ? RT[base + t] : make_uint4(0, 0, 0, 0);
     const uint64_t m = rt_word(e);
@@ -630,6 +628,34 @@ __global__ __launch_bounds__(TW) void k_local_cc(const uint4* __restrict__ RT, i
     LCC_T(3);
 }
 
+template <int CAP, int TW, int LP>
+__global__ __launch_bounds__(TW) void k_local_cc(const uint4* __restrict__ RT, int64_t words, int L,
+                                                 uint32_t* __restrict__ f, uint32_t* __restrict__ D,
+                                                 uint32_t* __restrict__ UR, uint64_t* __restrict__ lroot,
+                                                 int64_t rwords, int64_t max_distinct,
+                                                 unsigned long long* __restrict__ stats) {
+    if (((int)stats[S_P0] == 8 ? 8 : 7) != LP) return;  // the other tiling
+    local_cc_tile<CAP, TW, LP>((int64_t)blockIdx.x * TW, RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats);
+}
+
+// The same over a capped grid (grid-stride over the tiles): when the other tiling takes
+// the batch, its few workgroups exit at once instead of 4^L / (64 TW) of them each waiting
+// for 64 KB of LDS beside a concurrent kernel (measured 28-31 us for the empty launch in
+// the pipeline, 5 us alone)
+template <int CAP, int TW, int LP>
+__global__ __launch_bounds__(TW) void k_local_cc_loop(const uint4* __restrict__ RT, int64_t words, int L,
+                                                      uint32_t* __restrict__ f, uint32_t* __restrict__ D,
+                                                      uint32_t* __restrict__ UR, uint64_t* __restrict__ lroot,
+                                                      int64_t rwords, int64_t max_distinct,
+                                                      unsigned long long* __restrict__ stats) {
+    if (((int)stats[S_P0] == 8 ? 8 : 7) != LP) return;  // the other tiling
+    const int64_t tiles = (words + TW - 1) / TW;
+    for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+        local_cc_tile<CAP, TW, LP>(tile * TW, RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats);
+        __syncthreads();  // the next tile reuses the LDS
+    }
+}
+
 // ROGTK_LOCAL8=0: never the 8-position local tiling (A/B)
 inline bool local8_enabled() {
     static const bool on = [] {
@@ -648,8 +674,23 @@ inline void launch_local_cc(const uint4* RT, int64_t words, int L, uint32_t* f, 
                            dim3((unsigned)((words + kLocal8Words - 1) / kLocal8Words)), dim3(kLocal8Words), 0, s, RT,
                            words, L, f, D, UR, lroot, rwords, max_distinct, stats);
     const int64_t lblocks = (words + kLocalWords - 1) / kLocalWords;
-    hipLaunchKernelGGL((k_local_cc<kLocalCodes, kLocalWords, 7>), dim3((unsigned)lblocks), dim3(kBlock), 0, s, RT,
-                       words, L, f, D, UR, lroot, rwords, max_distinct, stats);
+    // ROGTK_LCC_LOOP=1: the 7-position instance as a grid-stride loop over 2 workgroups per
+    // CU (A/B; measured slower in the pipeline: 0.383 / 0.407 vs 0.366 / 0.383 ms/step)
+    static const int64_t cap = [] {
+        const char* e = getenv("ROGTK_LCC_LOOP");
+        if (!(e && e[0] == '1')) return (int64_t)0;
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return (int64_t)2 * cus;  // 64 KB of LDS each: two per CU
+    }();
+    if (cap && lblocks > cap && L >= 8 && local8_enabled())
+        hipLaunchKernelGGL((k_local_cc_loop<kLocalCodes, kLocalWords, 7>), dim3((unsigned)cap), dim3(kBlock), 0, s,
+                           RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats);
+    else
+        hipLaunchKernelGGL((k_local_cc<kLocalCodes, kLocalWords, 7>), dim3((unsigned)lblocks), dim3(kBlock), 0, s,
+                           RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats);
 }
 
 // --------------------------------------------------------------- global CC
@@ -1305,7 +1346,7 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
                                                        const uint32_t* __restrict__ rblkoff,
                                                        uint32_t* __restrict__ wlab, uint64_t* __restrict__ wexc,
                                                        uint32_t* __restrict__ labelcode, uint32_t* __restrict__ ilab,
-                                                       int use_exc) {
+                                                       uint32_t* __restrict__ wlab2, int use_exc) {
     for (int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x; w < words; w += (int64_t)gridDim.x * kBlock) {
         const uint32_t ur = UR[w];
         uint32_t root = kNone;
@@ -1353,13 +1394,24 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
         // the word stays unlabelled) get their own label (f[i] is their root: they are
         // live); a uniform word (ur != kNone) always has a label
         uint64_t per_code = lab == kNone ? m : exc;
+        // a word whose exceptions all lie in ONE other component also gets that label
+        // (wlab2): assign then reads it from a 1 MB table instead of gathering per code
+        uint32_t lab2 = kNone;
+        bool one2 = lab != kNone;
         while (per_code) {
             const int b = __ffsll((long long)per_code) - 1;
             per_code &= per_code - 1;
             const uint32_t i = e.z + (uint32_t)__popcll(m & ((1ull << b) - 1ull));
-            if ((int64_t)i >= max_distinct) continue;
-            put_label((uint64_t)w * 64 + b, i, root_label(f[i], rbits, rpref, rblkoff), labelcode, ilab);
+            if ((int64_t)i >= max_distinct) {
+                one2 = false;
+                continue;
+            }
+            const uint32_t li = root_label(f[i], rbits, rpref, rblkoff);
+            put_label((uint64_t)w * 64 + b, i, li, labelcode, ilab);
+            if (lab2 == kNone) lab2 = li;
+            else if (li != lab2) one2 = false;
         }
+        if (wlab2) wlab2[w] = (exc && one2) ? lab2 : kNone;
     }
 }
 
@@ -1367,10 +1419,12 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
 // the word's most frequent component, bit 31 set when some of its codes (wexc[w]) belong
 // to other components. Only flagged words cost a second (2 MB-table) load.
 __device__ __forceinline__ uint32_t word_label_of(const uint32_t* __restrict__ wlab,
-                                                  const uint64_t* __restrict__ wexc, uint64_t c) {
+                                                  const uint64_t* __restrict__ wexc,
+                                                  const uint32_t* __restrict__ wlab2, uint64_t c) {
     const uint32_t wl = wlab[c >> 6];
     if (wl == kNone || !(wl >> 31)) return wl;
-    return ((wexc[c >> 6] >> (c & 63)) & 1ull) ? kNone : (wl & 0x7FFFFFFFu);
+    if (!((wexc[c >> 6] >> (c & 63)) & 1ull)) return wl & 0x7FFFFFFFu;
+    return wlab2 ? wlab2[c >> 6] : kNone;  // the word's other component, or per code
 }
 
 // MODE 0: labelcode[code]; MODE 1: flab[rank(code)] (labels by index, ilab).
@@ -1386,7 +1440,8 @@ __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ labelcode,
                                                    const uint32_t* __restrict__ flab,
                                                    const uint4* __restrict__ RT, const uint32_t* __restrict__ wlab,
-                                                   const uint64_t* __restrict__ wexc, uint32_t* __restrict__ out) {
+                                                   const uint64_t* __restrict__ wexc,
+                                                   const uint32_t* __restrict__ wlab2, uint32_t* __restrict__ out) {
     constexpr int64_t kTile = 256 * G;  // rows per wave and trip
     const int lane = threadIdx.x & 63;
     const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
@@ -1414,7 +1469,7 @@ __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ 
             for (int k = 0; k < 4; ++k) {
                 id[g][k] = 0xFFFFFFFFu;
                 if ((reg[g] >> k) & 1u) {
-                    const uint32_t wl = wlab ? word_label_of(wlab, wexc, c[g][k]) : kNone;
+                    const uint32_t wl = wlab ? word_label_of(wlab, wexc, wlab2, c[g][k]) : kNone;
                     id[g][k] = wl != kNone ? wl
                                : MODE == 0 ? labelcode[c[g][k]]
                                            : flab[rt_rank(RT[c[g][k] >> 6], c[g][k])];
@@ -1440,14 +1495,15 @@ __global__ __launch_bounds__(kBlock) void k_lookup(const uint64_t* __restrict__ 
                                                    const uint32_t* __restrict__ labelcode,
                                                    const uint32_t* __restrict__ flab, const uint4* __restrict__ RT,
                                                    const uint32_t* __restrict__ wlab,
-                                                   const uint64_t* __restrict__ wexc, uint32_t* __restrict__ out) {
+                                                   const uint64_t* __restrict__ wexc,
+                                                   const uint32_t* __restrict__ wlab2, uint32_t* __restrict__ out) {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nq; i += (int64_t)gridDim.x * kBlock) {
         const uint64_t c = q[i];
         uint32_t lab = kNone;
         if (c < nbits) {
             const uint4 e = RT[c >> 6];
             if ((rt_word(e) >> (c & 63)) & 1ull) {
-                const uint32_t wl = wlab ? word_label_of(wlab, wexc, c) : kNone;
+                const uint32_t wl = wlab ? word_label_of(wlab, wexc, wlab2, c) : kNone;
                 lab = wl != kNone ? wl : MODE == 0 ? labelcode[c] : flab[rt_rank(e, (uint32_t)c)];
             }
         }
@@ -1470,7 +1526,7 @@ struct WsPtrs {
     uint4* RT;
     uint32_t *wpref, *blksum, *blkoff, *D, *f, *UR;
     uint64_t *rbits, *lroot;
-    uint32_t *rpref, *rblksum, *rblkoff, *labelcode, *ilab;
+    uint32_t *rpref, *rblksum, *rblkoff, *labelcode, *ilab, *wlab2;
     uint64_t* active;
     unsigned long long* epoch;  // resolves published (k_roots_scan)
     uint2* edges;             // two lists of ecap pairs
@@ -1495,6 +1551,7 @@ inline WsPtrs ws_ptrs(const ClusterLayout& cl, uint8_t* ws) {
     p.rpref = (uint32_t*)(ws + cl.off_rpref);
     p.rblksum = (uint32_t*)(ws + cl.off_rblksum);
     p.rblkoff = (uint32_t*)(ws + cl.off_rblkoff);
+    p.wlab2 = (uint32_t*)(ws + cl.off_wlab2);
     p.labelcode = cl.label_by_code ? (uint32_t*)(ws + cl.off_labelcode) : nullptr;
     p.ilab = cl.label_by_code ? nullptr : (uint32_t*)(ws + cl.off_ilab);
     p.active = (uint64_t*)(ws + cl.off_active);
@@ -1560,6 +1617,7 @@ int cluster_layout(int L, int64_t max_distinct, ClusterLayout* o) {
     c.off_rpref = take(c.rwords * 4);
     c.off_rblksum = take(c.rblocks * 4);
     c.off_rblkoff = take((c.rblocks + 1) * 4);
+    c.off_wlab2 = take(c.words * 4);  // second label of two-component words (k_word_label)
     c.off_labelcode = c.label_by_code ? take((int64_t)c.nbits * 4) : off;
     c.off_ilab = c.label_by_code ? off : take(max_distinct * 4);
     // hook-round frontier: one bit per (position, word group) task, two generations
@@ -1794,7 +1852,7 @@ int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
         }();
         hipLaunchKernelGGL(k_word_label, dim3(grid_for(cl.words, kPersistentGrid)), dim3(kBlock), 0, s, p.f, p.UR,
                            cl.words, p.RT, cl.max_distinct, p.rbits, p.rpref, p.rblkoff, p.wpref, p.G, p.labelcode,
-                           p.ilab, use_exc);
+                           p.ilab, p.wlab2, use_exc);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     return ROGTK_OK;
@@ -2099,10 +2157,10 @@ int launch_cluster_lookup(const ClusterLayout& cl, const uint8_t* ws, const uint
     const int g = grid_for(nq, 4096);
     if (cl.label_by_code)
         hipLaunchKernelGGL(k_lookup<0>, dim3(g), dim3(kBlock), 0, s, q, nq, cl.nbits, p.labelcode, p.D, p.RT, wlab,
-                           wexc, lab);
+                           wexc, wlab ? p.wlab2 : nullptr, lab);
     else
         hipLaunchKernelGGL(k_lookup<1>, dim3(g), dim3(kBlock), 0, s, q, nq, cl.nbits, p.labelcode, p.ilab, p.RT, wlab,
-                           wexc, lab);
+                           wexc, wlab ? p.wlab2 : nullptr, lab);
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
 }
@@ -2135,9 +2193,14 @@ int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, bool word_labels, c
         return v == 1 || v == 4 ? v : 2;
     }();
     const int g = grid_for((n + 4 * groups - 1) / (4 * groups), cap);
+    // ROGTK_WLAB2=0: exceptions of two-component words gathered per code (A/B)
+    static const bool use_wlab2 = [] {
+        const char* e = getenv("ROGTK_WLAB2");
+        return !(e && e[0] == '0');
+    }();
 #define ROGTK_ASSIGN_LAUNCH(M, G)                                                                                 \
     hipLaunchKernelGGL((k_assign<M, G>), dim3(g), dim3(kBlock), 0, s, codes, regular_bits, n, p.labelcode,       \
-                       M == 0 ? p.D : p.ilab, p.RT, wlab, wexc, cluster_id)
+                       M == 0 ? p.D : p.ilab, p.RT, wlab, wexc, wlab && use_wlab2 ? p.wlab2 : nullptr, cluster_id)
     if (cl.label_by_code) {
         if (groups == 1) ROGTK_ASSIGN_LAUNCH(0, 1);
         else if (groups == 4) ROGTK_ASSIGN_LAUNCH(0, 4);

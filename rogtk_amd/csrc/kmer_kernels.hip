@@ -187,34 +187,38 @@ __global__ __launch_bounds__(kBlock) void k_row_stage(const uint8_t* __restrict_
 // 1..B-1 = the bases, 32 per word, first base most significant. The spectrum call then
 // gathers each grouped row as whole lines (k_row_gather) instead of re-reading its ASCII
 // bytes from a random place (k_row_meta + k_row_stage).
-constexpr int kPackRowsPerBlock = 256;
 constexpr int kPackInBytes = 40 * 1024;  // a workgroup's rows' bytes, staged in LDS
+
+// per byte of v: 0x80 where the byte is zero (exact, no borrow between bytes)
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t v) {
+    const uint32_t t = (v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+    return ~(t | v | 0x7F7F7F7Fu);
+}
+// 4 bytes (first base in the low byte) -> 8 bits of 2-bit codes (first base most
+// significant), and the 0x80 marks of bytes that are not A/C/G/T in either case
+__device__ __forceinline__ uint32_t pack4(uint32_t x, uint32_t& notacgt) {
+    const uint32_t c = ((x >> 1) ^ (x >> 2)) & 0x03030303u;  // base2 of every byte
+    const uint32_t u = x | 0x20202020u;                       // A/C/G/T -> a/c/g/t (only those map there)
+    const uint32_t ok = zero_bytes(u ^ 0x61616161u) | zero_bytes(u ^ 0x63636363u) | zero_bytes(u ^ 0x67676767u) |
+                        zero_bytes(u ^ 0x74747474u);
+    notacgt = ~ok & 0x80808080u;
+    return ((c & 0xFFu) << 6) | (((c >> 8) & 0xFFu) << 4) | (((c >> 16) & 0xFFu) << 2) | (c >> 24);
+}
 
 template <int B>
 __global__ __launch_bounds__(kBlock) void k_pack_reads(const int64_t* __restrict__ offsets,
                                                        const uint8_t* __restrict__ values,
                                                        const uint8_t* __restrict__ validity, int64_t voff,
                                                        int64_t n, uint64_t* __restrict__ blocks) {
-    constexpr int R = B == 32 ? 128 : kPackRowsPerBlock;  // rows per workgroup
-    __shared__ uint32_t in32[kPackInBytes / 4];
-    __shared__ uint64_t out[R * B];
+    constexpr int R = kBlock;  // rows per workgroup: a lane per row
+    constexpr int OS = B + 1;  // LDS stride of a row's block (odd: fewer bank conflicts)
+    __shared__ uint32_t in32[kPackInBytes / 4 + 2];
+    __shared__ uint64_t out[R * OS];
     __shared__ int64_t s_off[R + 1];
-    __shared__ uint8_t s_valid[R];
-    const uint8_t* in8 = reinterpret_cast<const uint8_t*>(in32);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x;
     for (int64_t a = (int64_t)blockIdx.x * R; a < n; a += (int64_t)gridDim.x * R) {
         const int nr = (int)min<int64_t>(R, n - a);
-        // the rows' offsets and validity in LDS (coalesced; the row loop below then has no
-        // dependent global loads)
         for (int i = tid; i <= nr; i += kBlock) s_off[i] = offsets[a + i];
-        for (int i = tid; i < nr; i += kBlock) {
-            bool v = true;
-            if (validity) {
-                const int64_t bit = voff + a + i;
-                v = (validity[bit >> 3] >> (bit & 7)) & 1;
-            }
-            s_valid[i] = v ? 1 : 0;
-        }
         __syncthreads();
         const int64_t b0 = s_off[0], b1 = s_off[nr];
         const int64_t a4 = b0 & ~3ll;  // dword-aligned start
@@ -235,37 +239,54 @@ __global__ __launch_bounds__(kBlock) void k_pack_reads(const int64_t* __restrict
                     in32[i] = v;
                 }
             }
+            if (tid < 2) in32[nw + tid] = 0;  // the funnel shift below may read one dword past
         }
         __syncthreads();
-        for (int q = wave; q < nr; q += kWavesPerBlock) {
-            const bool valid = s_valid[q];
-            const int64_t st = s_off[q], len = s_off[q + 1] - st;
-            uint64_t* ob = out + q * B;
-            bool bad = false;
-            if (valid) {
-                for (int64_t j0 = 0; j0 < len; j0 += 64) {
-                    const bool in = j0 + lane < len;
-                    const uint8_t c = !in ? (uint8_t)'A' : staged ? in8[st - a4 + j0 + lane] : values[st + j0 + lane];
-                    const uint32_t bb = in ? base2(c) : 0u;
-                    bad |= in && !acgt(c);
-                    const uint64_t lo = __ballot(bb & 1u), hi = __ballot(bb & 2u);
-                    if (lane < 2) {
-                        const int64_t w = (j0 >> 5) + lane;
-                        const uint32_t l32 = (uint32_t)(lo >> (32 * lane)), h32 = (uint32_t)(hi >> (32 * lane));
-                        if (w * 32 < len)
-                            ob[1 + w] = (spread2(__builtin_bitreverse32(h32)) << 1) | spread2(__builtin_bitreverse32(l32));
-                    }
-                }
+        if (tid < nr) {  // this lane's row, entirely in registers: no cross-lane steps
+            const int64_t r = a + tid;
+            bool valid = true;
+            if (validity) {
+                const int64_t bit = voff + r;
+                valid = (validity[bit >> 3] >> (bit & 7)) & 1;
             }
-            const bool clean = __ballot(bad) == 0;
+            const int64_t st = s_off[tid], len = s_off[tid + 1] - st;
+            uint64_t* ob = out + tid * OS;
+            uint32_t bad = 0;
             const int used = valid ? (int)((len + 31) >> 5) : 0;
-            if (lane == 0) ob[0] = valid ? ((uint64_t)(uint32_t)len | ((uint64_t)clean << 32)) : 0xFFFFFFFFull;
-            if (lane >= 1 + used && lane < B) ob[lane] = 0;  // unused words: zero
+            const int64_t rel = st - a4;
+            const uint32_t sh = (uint32_t)(rel & 3) * 8;
+            for (int w = 0; w < used; ++w) {
+                uint64_t acc = 0;
+#pragma unroll
+                for (int d = 0; d < 8; ++d) {
+                    const int64_t j = (int64_t)w * 32 + d * 4;  // first byte of these 4
+                    const int64_t left = len - j;                // bytes of the row from j on
+                    uint32_t x = 0;
+                    if (left > 0) {
+                        if (staged) {  // in32[q + 1] exists: the row's bytes end inside in32[.. nw]
+                            const int64_t q = (rel + j) >> 2;
+                            const uint64_t two = ((uint64_t)in32[q + 1] << 32) | in32[q];
+                            x = (uint32_t)(two >> sh);
+                        } else {
+                            for (int t = 0; t < 4; ++t)
+                                if (j + t < len) x |= (uint32_t)values[st + j + t] << (8 * t);
+                        }
+                    }
+                    const uint32_t inmask = left >= 4 ? 0xFFFFFFFFu : left <= 0 ? 0u : (1u << (8 * left)) - 1u;
+                    x = (x & inmask) | (0x41414141u & ~inmask);  // past the end: 'A' (code 0, valid)
+                    uint32_t nb;
+                    acc = (acc << 8) | pack4(x, nb);
+                    bad |= nb;
+                }
+                ob[1 + w] = acc;
+            }
+            for (int w = used; w < B - 1; ++w) ob[1 + w] = 0;
+            ob[0] = valid ? ((uint64_t)(uint32_t)len | ((uint64_t)(bad == 0) << 32)) : 0xFFFFFFFFull;
         }
         __syncthreads();
         // the workgroup's blocks in one contiguous, coalesced store
         uint64_t* dst = blocks + a * B;
-        for (int i = tid; i < nr * B; i += kBlock) dst[i] = out[i];
+        for (int i = tid; i < nr * B; i += kBlock) dst[i] = out[(i / B) * OS + (i % B)];
         __syncthreads();
     }
 }
@@ -1708,7 +1729,7 @@ int rogtk_pack_reads(const int64_t* offsets, const uint8_t* values, const uint8_
                   "pack_reads: block_words must be 8, 16 or 32 (rogtk_read_block_words)");
     if (n == 0) return ROGTK_OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const int rows_per_wg = block_words == 32 ? 128 : kPackRowsPerBlock;
+    const int rows_per_wg = kBlock;
     const int g = (int)std::min<int64_t>((n + rows_per_wg - 1) / rows_per_wg, 8192);
     if (block_words == 8)
         hipLaunchKernelGGL(k_pack_reads<8>, dim3(g), dim3(kBlock), 0, s, offsets, values, validity, validity_offset, n,

@@ -204,7 +204,7 @@ struct ClusterLayout {
     bool label_by_code;  // dense label table indexed by code (L <= 13)
     // byte offsets into the workspace
     int64_t off_stats, off_presence, off_bitmap, off_rt, off_wpref, off_blksum, off_blkoff, off_D, off_f, off_ur,
-        off_rbits, off_lroot, off_rpref, off_rblksum, off_rblkoff, off_labelcode, off_ilab, off_active,
+        off_rbits, off_lroot, off_rpref, off_rblksum, off_rblkoff, off_wlab2, off_labelcode, off_ilab, off_active,
         active_words, off_edges, ecap, off_epoch, total;
 };
 int cluster_layout(int L, int64_t max_distinct, ClusterLayout* out);

@@ -58,7 +58,7 @@ class UmiPipeline:
                  group=None, with_scores: bool = True, priorities=(0, 0, 0), mark: str = "auto",
                  on_assigned=None, score_alone: bool = False, exchange=None, resolve_streams: int = 1,
                  assign_on: str = "separate", split_resolve: bool = False, reuse_gate: str = "auto",
-                 assign_early: bool = True, mark_first: bool = False):
+                 assign_early: bool = True, mark_first="auto"):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
@@ -95,7 +95,12 @@ class UmiPipeline:
         # longer than the GPU needs to reach the assign)
         self.assign_early = assign_early
         # mark_first: batch k's presence bitmap (mark) runs before its score kernel on the
-        # main stream, so its resolve overlaps the score instead of following it
+        # main stream, so its resolve overlaps the score instead of following it (round 3:
+        # 0.367-0.369 vs 0.398-0.408 ms/step at 10M reads, interleaved on one box; the score
+        # kernel then also runs beside fewer resolve kernels: 99 vs 130 us). "auto": on
+        # unless the mark is fused into the score kernel
+        if mark_first == "auto":
+            mark_first = not self.fused_mark
         if mark_first and self.fused_mark:
             raise ValueError("mark_first needs a separate mark (not mark='fused')")
         self.mark_first = mark_first
@@ -159,12 +164,14 @@ class UmiPipeline:
             self.main.wait_event(slot.assigned)
         if self.mark_first:
             # the presence bitmap needs only the codes: mark first, so the latency-bound
-            # resolve of this batch starts while its score kernel streams
-            resolved = self._mark_resolve(slot, batch, gate_resolve)
+            # resolve of this batch starts while its score kernel streams (host order:
+            # mark, score, the previous assign, then the ~15 launches of the resolve, so no
+            # GPU queue waits for the host)
+            marked = self._mark(slot, batch, gate_resolve)
             self._score(slot, batch)
         else:
             self._score(slot, batch)
-            resolved = None
+            marked = None
         if self.assign_early:
             # the previous batch's assign goes in right behind this batch's score kernel,
             # before the ~20 launches of this batch's mark + resolve: the GPU can start it
@@ -172,8 +179,9 @@ class UmiPipeline:
             # host to get through this batch's enqueues
             while self.queue and len(self.queue) >= max(self.lag, 1):
                 self._assign_oldest()
-        if resolved is None:
-            resolved = self._mark_resolve(slot, batch, gate_resolve)
+        if marked is None:
+            marked = self._mark(slot, batch, gate_resolve)
+        resolved = self._resolve(slot, marked, gate_resolve)
         slot.resolved = resolved
         self.queue.append((slot, batch, resolved))
         if not self.assign_early or self.lag == 0:
@@ -189,9 +197,9 @@ class UmiPipeline:
             self.last_scored = torch.cuda.Event()
             self.last_scored.record(self.main)
 
-    def _mark_resolve(self, slot: _Slot, batch: D.PackedBatch, gate_resolve: bool):
-        """Presence bitmap (main stream), [exchange], resolve (resolve stream); returns the
-        resolve's completion event."""
+    def _mark(self, slot: _Slot, batch: D.PackedBatch, gate_resolve: bool):
+        """Presence bitmap of the batch on the main stream; returns its event (with the
+        split resolve: after phase 1 of the resolve, also on the main stream)."""
         if gate_resolve and slot.resolved is not None:
             self.main.wait_event(slot.resolved)  # the previous resolve read the bitmap
         if self.sort_mark:
@@ -200,13 +208,21 @@ class UmiPipeline:
             if not self.fused_mark:
                 slot.eng.mark(batch, stream=self.main)
             slot.eng.build_local_bitmap(stream=self.main)
-        sr = self.s_resolves[self.k % len(self.s_resolves)]
         if self.split_resolve:
             with torch.cuda.stream(self.main):
                 bitmaps, nb = self.exchange(slot.eng.local_bitmap)
                 slot.eng.resolve(bitmaps, nb, self.max_distance, stream=self.main, phase=1)
         marked = torch.cuda.Event()
         marked.record(self.main)
+        self._split_bitmaps = (bitmaps, nb) if self.split_resolve else None
+        return marked
+
+    def _resolve(self, slot: _Slot, marked, gate_resolve: bool):
+        """[exchange on the comm stream], the resolve on a resolve stream after `marked`;
+        returns the resolve's completion event."""
+        sr = self.s_resolves[self.k % len(self.s_resolves)]
+        if self.split_resolve:
+            bitmaps, nb = self._split_bitmaps
         if self.s_comm is not None:
             with torch.cuda.stream(self.s_comm):
                 self.s_comm.wait_event(marked)

@@ -548,7 +548,8 @@ def test_pipeline_deferred_assign(rg, depth, nb, spec, assign_on, gate, order):
         D.set_spec_rounds(spec)
         pipe = UmiPipeline(L, n, n, "cuda", depth=depth, target=b"ACGTACGTACGT", max_distance=1,
                            assign_on=assign_on, reuse_gate=gate, score_alone=depth == 2,
-                           mark_first=order == "mark_first", assign_early=order != "late_assign")
+                           mark_first=order != "score_first" and order != "late_assign",
+                           assign_early=order != "late_assign")
         keep, last = [], {}
         for k, s in enumerate(seeds):
             codes = torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda()
