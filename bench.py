@@ -64,6 +64,13 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip in-run HIP-event kernel timing")
+    ap.add_argument("--sustain-seconds", type=float, default=4.0,
+                    help="after the timed region, run the same pipelined steps for this long (untimed by the "
+                         "contract; reported as 'sustained') so the GPU stays busy long enough for external "
+                         "utilisation sampling; 0 = skip")
+    ap.add_argument("--settle-seconds", type=float, default=1.0,
+                    help="after the W warmup steps, more untimed steps until this many seconds have passed "
+                         "(GPU clocks at steady state before the timed region); 0 = none")
     ap.add_argument("--no-end-to-end", action="store_true",
                     help="skip the host Arrow in -> host Arrow out measurement (level-2 entry points)")
     ap.add_argument("--iso-launches", type=int, default=10, help="isolated score-kernel launches after timing")
@@ -81,9 +88,9 @@ def parse():
                          "step time at N=W minus RCCL time. Never used by the driver.")
     ap.add_argument("--global-mode", choices=("uf", "rounds", "rounds1f", "edges"), default="rounds",
                     help="H3 global CC phase: one-pass union-find or hook + jump rounds")
-    ap.add_argument("--assign-on", choices=("resolve", "separate"), default="separate",
-                    help="assign of batch k on its own stream one batch later (default) or behind its "
-                         "resolve on the resolve stream (deferred assign)")
+    ap.add_argument("--assign-on", choices=("resolve", "separate", "main"), default="main",
+                    help="assign of batch k on its own stream one batch later (default), on the main stream "
+                         "behind batch k+1's score kernel, or behind its resolve on the resolve stream")
     ap.add_argument("--split-resolve", action="store_true",
                     help="local phase of the resolve on the main stream, global phase on the resolve stream")
     ap.add_argument("--resolve-streams", type=int, default=1,
@@ -93,8 +100,14 @@ def parse():
     ap.add_argument("--reuse-gate", choices=("auto", "score", "resolve"), default="auto",
                     help="slot reuse: the main stream (score) or only the resolve waits for the slot's last assign")
     ap.add_argument("--prio", type=str, default="0,0,0", help="stream priorities main,resolve,assign (-1 = high)")
-    ap.add_argument("--mark-first", action="store_true",
-                    help="main stream order mark -> score (the resolve overlaps the score kernel)")
+    ap.add_argument("--score-first", action="store_true",
+                    help="main stream order score -> mark (round-2 order; default: mark -> score, so the "
+                         "resolve overlaps the score kernel)")
+    ap.add_argument("--mark-stream", action="store_true",
+                    help="presence-bitmap mark on a stream of its own (overlaps score + assign)")
+    ap.add_argument("--torch-events", action="store_true",
+                    help="cross-stream hand-offs through torch events (system-scope release) instead of the "
+                         "library's device-scope StreamEvents")
     ap.add_argument("--late-assign", action="store_true",
                     help="host order: enqueue batch k-1's assign after batch k's resolve (round-2 default)")
     return ap.parse_args()
@@ -293,7 +306,8 @@ def main():
                        score_alone=not args.overlap_score, exchange=exchange,
                        resolve_streams=args.resolve_streams, assign_on=args.assign_on,
                        split_resolve=args.split_resolve, reuse_gate=args.reuse_gate,
-                       assign_early=not args.late_assign, mark_first=args.mark_first)
+                       assign_early=not args.late_assign, mark_first=False if args.score_first else "auto",
+                       device_events=not args.torch_events, mark_stream=args.mark_stream)
 
     def step():
         pipe.submit(batch)
@@ -302,6 +316,19 @@ def main():
         step()
     pipe.drain()
     torch.cuda.synchronize()
+    # untimed settle: more of the same steps until --settle-seconds have passed since the
+    # warmup began, so the timed region starts at the GPU's steady-state clocks (a 20-step
+    # region is ~8 ms; the first milliseconds of activity run slower)
+    settle_steps = 0
+    if args.settle_seconds > 0:
+        t_s = time.perf_counter()
+        while time.perf_counter() - t_s < args.settle_seconds:
+            for _ in range(25):
+                step()
+            settle_steps += 25
+            torch.cuda.synchronize()
+        pipe.drain()
+        torch.cuda.synchronize()
     if not args.no_profile:
         # only the roofline kernel is bracketed inside the timed region: every bracketed
         # launch adds two event records to its stream (measured: +0.055 ms/step when all
@@ -334,6 +361,28 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     stats = pipe.slots[0].eng.stats()
+    # Sustained run (outside the timed region): the same steps back to back for a few
+    # seconds, all ranks together; reported beside `value` as a steady-state check
+    sustained = None
+    if args.sustain_seconds > 0:
+        barrier(world)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        k_sus = 0
+        while time.perf_counter() - t1 < args.sustain_seconds:
+            for _ in range(50):
+                step()
+            k_sus += 50
+            torch.cuda.synchronize()  # bounds the queue; a drain per 50 steps
+        pipe.drain()
+        torch.cuda.synchronize()
+        el_sus = time.perf_counter() - t1
+        if world > 1:
+            t = torch.tensor([el_sus], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el_sus = float(t.item())
+        sustained = {"value": round(n_total * k_sus / el_sus, 1), "steps": k_sus, "seconds": round(el_sus, 2),
+                     "ms_per_step": round(1000 * el_sus / k_sus, 4)}
 
     # Outside the timed region: a few more pipelined steps with every kernel bracketed,
     # for the per-phase breakdown (kernels_us; these steps are not timed).
@@ -394,6 +443,13 @@ def main():
                                  if kernels["score_packed"]["event_avg_us"] else None),
                 "measured_over": f"timed region, {args.depth} batches in flight (kernel overlaps the resolve "
                                  f"of the previous batch" + (" and assign" if args.overlap_score else "") + ")"}
+        # the whole step against the same roofline: SURVEY §8d's 60 B/read (4 B code in;
+        # 48 + 4 B of H1 fields, 4 B cluster id out) + the within bit + the 4^L tables once
+        # per batch (presence bitmap 4^L / 8 B + labels 4^L x 4 B read and written)
+        step_bytes = count * (60 + 0.125) + (4 ** L) // 8 + 2 * 4 * (4 ** L)
+        roof["step"] = {"algorithmic_bytes": int(step_bytes), "achieved": round(step_bytes / (el / args.steps) / 1e9, 1),
+                        "frac": round(step_bytes / (el / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+                        "note": "whole pipelined step (all kernels, ms_per_step) vs SURVEY §8d's algorithmic bytes"}
         if iso:
             a_iso = count * bpr / (iso * 1e-6) / 1e9
             roof["isolated"] = {"avg_us": round(iso, 2), "achieved": round(a_iso, 1),
@@ -436,6 +492,8 @@ def main():
                                   + (f" (rank 0 of {args.emulate_ranks} EMULATED on one GPU, no RCCL)"
                                      if args.emulate_ranks > 1 else "")},
         "roofline": roof,
+        "sustained": sustained,
+        "settle": {"seconds": args.settle_seconds, "steps": settle_steps} if settle_steps else None,
         "end_to_end": e2e,
         "cpu_baseline": cpu,
         "kernels_us": breakdown,

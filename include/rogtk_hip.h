@@ -58,6 +58,16 @@ int rogtk_device_count(int* out_count);
  * calling thread's pinned buffers). Blocks are cached for reuse after rogtk_host_free. */
 int rogtk_host_alloc(size_t bytes, void** out);
 int rogtk_host_free(void* p);
+/* Stream-ordering events for pipelines of these kernels (plumbing, no reference
+ * counterpart): never timed, and with flags & 1 released at device scope only (no
+ * system-scope cache write-back at each record; host readers must synchronise the
+ * stream or device instead). rogtk_event_query: *done = 1 once the event has fired. */
+int rogtk_event_create(int flags, void** out);
+int rogtk_event_destroy(void* ev);
+int rogtk_event_record(void* ev, void* stream);
+int rogtk_stream_wait_event(void* stream, void* ev);
+int rogtk_event_query(void* ev, int* done);
+int rogtk_event_synchronize(void* ev);
 
 /*
  * Output set of UMI complexity scoring: ComplexityScore (umi_score.rs:5-13)

@@ -152,6 +152,12 @@ SIGNATURES = {
     "rogtk_read_block_words": [_i64],
     "rogtk_host_alloc": [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)],
     "rogtk_host_free": [_vp],
+    "rogtk_event_create": [_i32, ctypes.POINTER(ctypes.c_void_p)],
+    "rogtk_event_destroy": [_vp],
+    "rogtk_event_record": [_vp, _vp],
+    "rogtk_stream_wait_event": [_vp, _vp],
+    "rogtk_event_query": [_vp, _P_I32],
+    "rogtk_event_synchronize": [_vp],
     "rogtk_pack_reads": [_vp, _vp, _vp, _i64, _i64, _i32, _vp, _vp],
     "rogtk_kmer_spectrum_blocks": [_vp, _i32, _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _i64, _vp,
                                    _vp, _vp, _vp, _vp, _P_I64, _vp],

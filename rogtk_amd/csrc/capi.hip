@@ -50,16 +50,31 @@ struct ProfRec {
 std::vector<ProfRec> g_prof_pending;
 double g_prof_ms[K_COUNT_] = {0};
 int64_t g_prof_n[K_COUNT_] = {0};
-// in-kernel spans: one u64 tick count per launch in a device result array
+// in-kernel spans: each profiled launch writes (entry, exit) ticks per workgroup into a
+// slice of one preallocated device arena; the min/max reductions run only at drain time
+// (profile_read_span / reset / a full arena), so a profiled launch adds no allocation,
+// no kernel and no stream dependency to the pipeline it measures
 constexpr int kSpanSlots = 1 << 14;
-uint64_t* g_span_dev = nullptr;  // kSpanSlots results
-std::vector<KernelId> g_span_ids;  // kernel of each used slot
+constexpr size_t kSpanArenaBytes = size_t(256) << 20;  // ~400 launches of 10M rows
+uint64_t* g_span_dev = nullptr;    // kSpanSlots results
+uint64_t* g_span_arena = nullptr;  // per-workgroup ticks of the pending launches
+size_t g_span_used = 0;            // bytes of the arena handed out
+struct SpanRec {
+    KernelId id;
+    size_t off;  // u64 offset of the launch's ticks in the arena
+    int64_t nb;  // workgroups
+};
+std::vector<SpanRec> g_span_pending;
 double g_span_ms[K_COUNT_] = {0};
 int64_t g_span_n[K_COUNT_] = {0};
 double g_span_tick_ms = 0;  // wall_clock64 period in ms
 
-__global__ void k_span_reduce(const uint64_t* __restrict__ t, int64_t nb, uint64_t* __restrict__ out) {
+// one workgroup per pending launch: max(exit) - min(entry) over its workgroups
+__global__ void k_span_reduce(const uint64_t* __restrict__ arena, const int64_t* __restrict__ desc,
+                              uint64_t* __restrict__ out) {
     __shared__ uint64_t s_lo[256], s_hi[256];
+    const uint64_t* t = arena + desc[2 * blockIdx.x];
+    const int64_t nb = desc[2 * blockIdx.x + 1];
     uint64_t lo = ~0ull, hi = 0;
     for (int64_t b = threadIdx.x; b < nb; b += blockDim.x) {
         lo = min(lo, t[2 * b]);
@@ -75,19 +90,50 @@ __global__ void k_span_reduce(const uint64_t* __restrict__ t, int64_t nb, uint64
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) *out = s_hi[0] > s_lo[0] ? s_hi[0] - s_lo[0] : 0;
+    if (threadIdx.x == 0) out[blockIdx.x] = s_hi[0] > s_lo[0] ? s_hi[0] - s_lo[0] : 0;
 }
 
 void span_drain_locked() {
-    if (g_span_ids.empty() || !g_span_dev) return;
-    std::vector<uint64_t> h(g_span_ids.size());
-    if (hipDeviceSynchronize() == hipSuccess &&
-        hipMemcpy(h.data(), g_span_dev, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess)
-        for (size_t i = 0; i < h.size(); ++i) {
-            g_span_ms[g_span_ids[i]] += (double)h[i] * g_span_tick_ms;
-            g_span_n[g_span_ids[i]] += 1;
+    if (g_span_pending.empty() || !g_span_dev) return;
+    const size_t n = g_span_pending.size();
+    std::vector<int64_t> desc(2 * n);
+    for (size_t i = 0; i < n; ++i) {
+        desc[2 * i] = (int64_t)g_span_pending[i].off;
+        desc[2 * i + 1] = g_span_pending[i].nb;
+    }
+    std::vector<uint64_t> h(n);
+    int64_t* d_desc = nullptr;
+    bool ok = hipDeviceSynchronize() == hipSuccess && hipMalloc((void**)&d_desc, desc.size() * 8) == hipSuccess;
+    if (ok) {
+        ok = hipMemcpy(d_desc, desc.data(), desc.size() * 8, hipMemcpyHostToDevice) == hipSuccess;
+        if (ok) {
+            hipLaunchKernelGGL(k_span_reduce, dim3((unsigned)n), dim3(256), 0, 0, g_span_arena, d_desc, g_span_dev);
+            ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+                 hipMemcpy(h.data(), g_span_dev, n * 8, hipMemcpyDeviceToHost) == hipSuccess;
         }
-    g_span_ids.clear();
+        (void)hipFree(d_desc);
+    }
+    if (ok)
+        for (size_t i = 0; i < n; ++i) {
+            g_span_ms[g_span_pending[i].id] += (double)h[i] * g_span_tick_ms;
+            g_span_n[g_span_pending[i].id] += 1;
+        }
+    g_span_pending.clear();
+    g_span_used = 0;
+}
+
+// timing events are reused (no create / destroy per profiled launch) and released at
+// device scope: a system-scope release would write the L2 back at every bracketed launch
+std::vector<hipEvent_t> g_prof_free;
+
+hipEvent_t prof_event_locked() {
+    if (!g_prof_free.empty()) {
+        hipEvent_t e = g_prof_free.back();
+        g_prof_free.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    return hipEventCreateWithFlags(&e, hipEventDisableSystemFence) == hipSuccess ? e : nullptr;
 }
 
 void prof_drain_locked() {
@@ -97,8 +143,8 @@ void prof_drain_locked() {
             g_prof_ms[r.id] += ms;
             g_prof_n[r.id] += 1;
         }
-        hipEventDestroy(r.a);
-        hipEventDestroy(r.b);
+        g_prof_free.push_back(r.a);
+        g_prof_free.push_back(r.b);
     }
     g_prof_pending.clear();
 }
@@ -107,6 +153,7 @@ void prof_drain_locked() {
 bool profiling_on() { return g_prof.load(std::memory_order_relaxed); }
 
 uint64_t* span_begin(KernelId id, int64_t n_blocks, hipStream_t s) {
+    (void)s;
     if (!g_prof.load(std::memory_order_relaxed) || !((g_prof_mask.load(std::memory_order_relaxed) >> id) & 1u))
         return nullptr;
     std::lock_guard<std::mutex> lk(g_prof_mu);
@@ -118,33 +165,38 @@ uint64_t* span_begin(KernelId id, int64_t n_blocks, hipStream_t s) {
             g_span_dev = nullptr;
             return nullptr;
         }
+        if (hipMalloc((void**)&g_span_arena, kSpanArenaBytes) != hipSuccess) {
+            (void)hipFree(g_span_dev);
+            g_span_dev = g_span_arena = nullptr;
+            return nullptr;
+        }
         g_span_tick_ms = 1.0 / (double)khz;
     }
-    if ((int)g_span_ids.size() >= kSpanSlots) span_drain_locked();
-    uint64_t* t = nullptr;
-    if (hipMallocAsync((void**)&t, (size_t)std::max<int64_t>(n_blocks, 1) * 16, s) != hipSuccess) return nullptr;
+    const size_t need = (size_t)std::max<int64_t>(n_blocks, 1) * 16;
+    if (need > kSpanArenaBytes) return nullptr;  // not timed
+    if ((int)g_span_pending.size() >= kSpanSlots || g_span_used + need > kSpanArenaBytes) span_drain_locked();
+    uint64_t* t = g_span_arena + g_span_used / 8;
+    g_span_used += (need + 255) & ~size_t(255);
     return t;
 }
 
 void span_end(KernelId id, uint64_t* tspan, int64_t n_blocks, hipStream_t s) {
+    (void)s;
     if (!tspan) return;
     std::lock_guard<std::mutex> lk(g_prof_mu);
-    const size_t slot = g_span_ids.size();
-    g_span_ids.push_back(id);
-    hipLaunchKernelGGL(k_span_reduce, dim3(1), dim3(256), 0, s, tspan, n_blocks, g_span_dev + slot);
-    (void)hipFreeAsync(tspan, s);
+    g_span_pending.push_back({id, (size_t)(tspan - g_span_arena), std::max<int64_t>(n_blocks, 1)});
 }
 
 ProfScope::ProfScope(KernelId id, hipStream_t stream, bool exact) : id_(id), stream_(stream), exact_(exact) {
     if (!g_prof.load(std::memory_order_relaxed) || !((g_prof_mask.load(std::memory_order_relaxed) >> id) & 1u)) return;
-    if (hipEventCreate(&start_) != hipSuccess) {
-        start_ = nullptr;
-        return;
-    }
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    start_ = prof_event_locked();
+    if (!start_) return;
     if (exact_) {  // both events ride on the dispatch packet (hipExtLaunchKernelGGL)
-        if (hipEventCreate(&stop_) != hipSuccess) {
-            hipEventDestroy(start_);
-            start_ = stop_ = nullptr;
+        stop_ = prof_event_locked();
+        if (!stop_) {
+            g_prof_free.push_back(start_);
+            start_ = nullptr;
         }
         return;
     }
@@ -153,15 +205,16 @@ ProfScope::ProfScope(KernelId id, hipStream_t stream, bool exact) : id_(id), str
 
 ProfScope::~ProfScope() {
     if (!start_) return;
+    std::lock_guard<std::mutex> lk(g_prof_mu);
     hipEvent_t stop = stop_;
     if (!exact_) {
-        if (hipEventCreate(&stop) != hipSuccess) {
-            hipEventDestroy(start_);
+        stop = prof_event_locked();
+        if (!stop) {
+            g_prof_free.push_back(start_);
             return;
         }
         hipEventRecord(stop, stream_);
     }
-    std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof_pending.push_back({id_, start_, stop});
 }
 
@@ -1033,6 +1086,55 @@ int rogtk_umi_cluster_dev(const int64_t* offsets, const uint8_t* values, const u
     ROGTK_HIP_CHECK(hipStreamSynchronize(s));
     return cluster_staged(c, offsets, 8, values, validity, 0, n, umi_len, hv[0], hv[1], max_distance, cluster_id,
                           n_clusters, s);
+}
+
+// --------------------------------------------------------------- stream events
+int rogtk_event_create(int flags, void** out) {
+    ROGTK_REQUIRE(out, ROGTK_E_INVALID, "event_create: NULL out");
+    *out = nullptr;
+    ROGTK_REQUIRE((flags & ~1) == 0, ROGTK_E_INVALID, "event_create: unknown flags %d", flags);
+    hipEvent_t e = nullptr;
+    const unsigned f = hipEventDisableTiming | ((flags & 1) ? hipEventDisableSystemFence : 0u);
+    ROGTK_HIP_CHECK(hipEventCreateWithFlags(&e, f));
+    *out = e;
+    return ROGTK_OK;
+}
+
+int rogtk_event_destroy(void* ev) {
+    if (!ev) return ROGTK_OK;
+    ROGTK_HIP_CHECK(hipEventDestroy((hipEvent_t)ev));
+    return ROGTK_OK;
+}
+
+int rogtk_event_record(void* ev, void* stream) {
+    ROGTK_REQUIRE(ev, ROGTK_E_INVALID, "event_record: NULL event");
+    ROGTK_HIP_CHECK(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream));
+    return ROGTK_OK;
+}
+
+int rogtk_stream_wait_event(void* stream, void* ev) {
+    ROGTK_REQUIRE(ev, ROGTK_E_INVALID, "stream_wait_event: NULL event");
+    ROGTK_HIP_CHECK(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev, 0));
+    return ROGTK_OK;
+}
+
+int rogtk_event_query(void* ev, int* done) {
+    ROGTK_REQUIRE(ev && done, ROGTK_E_INVALID, "event_query: NULL argument");
+    const hipError_t e = hipEventQuery((hipEvent_t)ev);
+    if (e == hipErrorNotReady) {
+        (void)hipGetLastError();
+        *done = 0;
+        return ROGTK_OK;
+    }
+    ROGTK_HIP_CHECK(e);
+    *done = 1;
+    return ROGTK_OK;
+}
+
+int rogtk_event_synchronize(void* ev) {
+    ROGTK_REQUIRE(ev, ROGTK_E_INVALID, "event_synchronize: NULL event");
+    ROGTK_HIP_CHECK(hipEventSynchronize((hipEvent_t)ev));
+    return ROGTK_OK;
 }
 
 // --------------------------------------------------------------- profiling

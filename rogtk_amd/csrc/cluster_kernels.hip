@@ -1518,6 +1518,18 @@ inline int grid_for(int64_t lanes, int64_t cap = 0) {
     return (int)g;
 }
 
+// ROGTK_WLAB2=1: a second word label (the one other component of a word's exceptions),
+// written by k_word_label and read by k_assign / k_lookup before the per-code gather.
+// A/B, off by default: the 1 MB table cost the assign more L2 misses than the per-code
+// gathers it saves (round 3: 129-130 vs 115-117 us per 10M-row assign, same box)
+inline bool wlab2_on() {
+    static const bool on = [] {
+        const char* e = getenv("ROGTK_WLAB2");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 struct WsPtrs {
     unsigned long long* stats;
     unsigned int* flags;
@@ -1852,7 +1864,7 @@ int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
         }();
         hipLaunchKernelGGL(k_word_label, dim3(grid_for(cl.words, kPersistentGrid)), dim3(kBlock), 0, s, p.f, p.UR,
                            cl.words, p.RT, cl.max_distinct, p.rbits, p.rpref, p.rblkoff, p.wpref, p.G, p.labelcode,
-                           p.ilab, p.wlab2, use_exc);
+                           p.ilab, wlab2_on() ? p.wlab2 : nullptr, use_exc);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     return ROGTK_OK;
@@ -2157,10 +2169,10 @@ int launch_cluster_lookup(const ClusterLayout& cl, const uint8_t* ws, const uint
     const int g = grid_for(nq, 4096);
     if (cl.label_by_code)
         hipLaunchKernelGGL(k_lookup<0>, dim3(g), dim3(kBlock), 0, s, q, nq, cl.nbits, p.labelcode, p.D, p.RT, wlab,
-                           wexc, wlab ? p.wlab2 : nullptr, lab);
+                           wexc, wlab && wlab2_on() ? p.wlab2 : nullptr, lab);
     else
         hipLaunchKernelGGL(k_lookup<1>, dim3(g), dim3(kBlock), 0, s, q, nq, cl.nbits, p.labelcode, p.ilab, p.RT, wlab,
-                           wexc, wlab ? p.wlab2 : nullptr, lab);
+                           wexc, wlab && wlab2_on() ? p.wlab2 : nullptr, lab);
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
 }
@@ -2193,14 +2205,9 @@ int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, bool word_labels, c
         return v == 1 || v == 4 ? v : 2;
     }();
     const int g = grid_for((n + 4 * groups - 1) / (4 * groups), cap);
-    // ROGTK_WLAB2=0: exceptions of two-component words gathered per code (A/B)
-    static const bool use_wlab2 = [] {
-        const char* e = getenv("ROGTK_WLAB2");
-        return !(e && e[0] == '0');
-    }();
 #define ROGTK_ASSIGN_LAUNCH(M, G)                                                                                 \
     hipLaunchKernelGGL((k_assign<M, G>), dim3(g), dim3(kBlock), 0, s, codes, regular_bits, n, p.labelcode,       \
-                       M == 0 ? p.D : p.ilab, p.RT, wlab, wexc, wlab && use_wlab2 ? p.wlab2 : nullptr, cluster_id)
+                       M == 0 ? p.D : p.ilab, p.RT, wlab, wexc, wlab && wlab2_on() ? p.wlab2 : nullptr, cluster_id)
     if (cl.label_by_code) {
         if (groups == 1) ROGTK_ASSIGN_LAUNCH(0, 1);
         else if (groups == 4) ROGTK_ASSIGN_LAUNCH(0, 4);

@@ -35,6 +35,52 @@ def _s(stream: Optional[torch.cuda.Stream] = None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
+class StreamEvent:
+    """Stream-ordering event (rogtk_event_*): never timed; device_scope=True releases at
+    device scope only, so a record does not write the L2 back to memory (torch's events
+    release at system scope). Same record / wait / synchronize / query shape as
+    torch.cuda.Event, for the pipeline's cross-stream hand-offs."""
+
+    __slots__ = ("_ev",)
+
+    def __init__(self, device_scope: bool = True):
+        h = ctypes.c_void_p()
+        _lib.call("rogtk_event_create", 1 if device_scope else 0, ctypes.byref(h))
+        self._ev = h
+
+    def record(self, stream: Optional[torch.cuda.Stream] = None):
+        _lib.call("rogtk_event_record", self._ev, _s(stream))
+
+    def wait(self, stream: Optional[torch.cuda.Stream] = None):
+        """`stream` waits for this event's last record."""
+        _lib.call("rogtk_stream_wait_event", _s(stream), self._ev)
+
+    def query(self) -> bool:
+        done = ctypes.c_int32(0)
+        _lib.call("rogtk_event_query", self._ev, ctypes.byref(done))
+        return bool(done.value)
+
+    def synchronize(self):
+        _lib.call("rogtk_event_synchronize", self._ev)
+
+    def __del__(self):
+        ev = getattr(self, "_ev", None)
+        if ev is not None and ev.value:
+            try:
+                _lib.call("rogtk_event_destroy", ev)
+            except Exception:  # interpreter shutdown
+                pass
+            self._ev = None
+
+
+def wait_for(stream: torch.cuda.Stream, ev) -> None:
+    """`stream` waits for `ev` (a StreamEvent or a torch.cuda.Event)."""
+    if isinstance(ev, StreamEvent):
+        ev.wait(stream)
+    else:
+        stream.wait_event(ev)
+
+
 class PackedBatch:
     """The packed SoA of one batch (device tensors)."""
 

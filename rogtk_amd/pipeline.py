@@ -48,8 +48,8 @@ class _Slot:
         self.scores = D.alloc_scores(n_max, dev) if with_scores else None
         self.within = torch.empty(max((n_max + 63) // 64, 1), dtype=torch.int64, device=dev)
         self.cid = torch.empty(max(n_max, 4), dtype=torch.int32, device=dev)
-        self.assigned: Optional[torch.cuda.Event] = None
-        self.resolved: Optional[torch.cuda.Event] = None
+        self.assigned = None  # D.StreamEvent or torch.cuda.Event (UmiPipeline.device_events)
+        self.resolved = None
 
 
 class UmiPipeline:
@@ -57,8 +57,9 @@ class UmiPipeline:
                  target: Optional[bytes] = b"ACGTACGTACGT", max_hamming: int = 1, max_distance: int = 1,
                  group=None, with_scores: bool = True, priorities=(0, 0, 0), mark: str = "auto",
                  on_assigned=None, score_alone: bool = False, exchange=None, resolve_streams: int = 1,
-                 assign_on: str = "separate", split_resolve: bool = False, reuse_gate: str = "auto",
-                 assign_early: bool = True, mark_first="auto"):
+                 assign_on: str = "main", split_resolve: bool = False, reuse_gate: str = "auto",
+                 assign_early: bool = True, mark_first="auto", device_events: bool = True,
+                 mark_stream: bool = False):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
@@ -82,7 +83,10 @@ class UmiPipeline:
             raise ValueError("resolve_streams must be >= 1 and < depth")
         self.s_resolves = [torch.cuda.Stream(dev, priority=priorities[1]) for _ in range(resolve_streams)]
         self.s_resolve = self.s_resolves[0]
-        self.s_assign = torch.cuda.Stream(dev, priority=priorities[2])
+        # assign_on "main": the assign of batch k-1 runs on the main stream right behind
+        # batch k's score kernel, so the serial cycle mark -> score -> assign -> mark has
+        # no cross-stream hop (each cost ~20-25 us of idle GPU in the round-3 timeline)
+        self.s_assign = self.main if assign_on == "main" else torch.cuda.Stream(dev, priority=priorities[2])
         self.queue = deque()
         # assign lags resolve by one batch only when a second slot exists: with one
         # slot the next batch's resolve would overwrite the tables assign reads
@@ -104,6 +108,21 @@ class UmiPipeline:
         if mark_first and self.fused_mark:
             raise ValueError("mark_first needs a separate mark (not mark='fused')")
         self.mark_first = mark_first
+        # device_events: the cross-stream hand-offs use StreamEvents released at device
+        # scope (rogtk_event_*) instead of torch events, whose system-scope release writes
+        # the L2 back at every record (round 3: each record / wait between two kernels of
+        # the step cost ~20 us of idle GPU in the kernel timeline)
+        self.device_events = device_events
+        # mark_stream: the presence bitmap of batch k on a stream of its own (it reads only
+        # the codes and writes the slot's local bitmap, which nothing but the slot's
+        # previous resolve reads), so the main stream carries only score + assign and the
+        # mark overlaps them; the resolve then waits for the mark and for the slot's
+        # previous assign explicitly
+        if mark_stream and (split_resolve or self.fused_mark or assign_on == "resolve"):
+            raise ValueError("mark_stream needs a separate mark, split_resolve=False and assign_on != 'resolve'")
+        self.s_mark = torch.cuda.Stream(dev, priority=priorities[0]) if mark_stream else self.main
+        if mark_stream:
+            self.mark_first = True
         # score_alone: assign of the previous batch waits for this batch's score kernel,
         # so the HBM-bound score overlaps only the latency-bound resolve kernels
         self.score_alone = score_alone
@@ -122,8 +141,8 @@ class UmiPipeline:
         # stream as a deferred assign (no host wait for the resolve's flags), so it never
         # competes with the latency-bound resolve kernels of the next batch; the flags
         # are checked when the slot comes round again (or at drain)
-        if assign_on not in ("resolve", "separate"):
-            raise ValueError("assign_on must be 'resolve' or 'separate'")
+        if assign_on not in ("resolve", "separate", "main"):
+            raise ValueError("assign_on must be 'resolve', 'separate' or 'main'")
         self.assign_on = assign_on
         # split_resolve: the local phase of batch k's resolve (rank tables + LDS-local
         # components, a function of its bitmaps only) runs on the main stream behind its
@@ -154,14 +173,24 @@ class UmiPipeline:
         may be built from the speculative rounds (slot.assigned / last_assigned mark that
         assign, not a settled one); the slot is settled before its reuse."""
         slot = self.slots[self.k % len(self.slots)]
-        self.main.wait_stream(torch.cuda.current_stream(self.main.device))  # batch producer -> main
+        producer = torch.cuda.current_stream(self.main.device)  # batch producer -> main
+        if self.device_events:
+            ready = D.StreamEvent()
+            ready.record(producer)
+            ready.wait(self.main)
+            if self.s_mark is not self.main:
+                ready.wait(self.s_mark)
+        else:
+            self.main.wait_stream(producer)
+            if self.s_mark is not self.main:
+                self.s_mark.wait_stream(producer)
         if self.assign_on == "resolve":
             return self._submit_assign_on_resolve(slot, batch)
         if self.on_assigned is None:
             self._settle(slot, self.s_assign)
         gate_resolve = self.reuse_gate == "resolve"
-        if slot.assigned is not None and not gate_resolve:
-            self.main.wait_event(slot.assigned)
+        if slot.assigned is not None and not gate_resolve and self.s_assign is not self.main:
+            D.wait_for(self.main, slot.assigned)
         if self.mark_first:
             # the presence bitmap needs only the codes: mark first, so the latency-bound
             # resolve of this batch starts while its score kernel streams (host order:
@@ -190,30 +219,35 @@ class UmiPipeline:
         self.k += 1
         return slot
 
+    def _event(self):
+        return D.StreamEvent() if self.device_events else torch.cuda.Event()
+
     def _score(self, slot: _Slot, batch: D.PackedBatch):
         D.score_packed(batch, slot.scores, self.target, self.max_hamming, None, slot.within,
                        cluster=slot.eng if self.fused_mark else None, stream=self.main)
-        if self.score_alone:
-            self.last_scored = torch.cuda.Event()
+        if self.score_alone and self.s_assign is not self.main:
+            self.last_scored = self._event()
             self.last_scored.record(self.main)
 
     def _mark(self, slot: _Slot, batch: D.PackedBatch, gate_resolve: bool):
-        """Presence bitmap of the batch on the main stream; returns its event (with the
-        split resolve: after phase 1 of the resolve, also on the main stream)."""
-        if gate_resolve and slot.resolved is not None:
-            self.main.wait_event(slot.resolved)  # the previous resolve read the bitmap
+        """Presence bitmap of the batch on the mark stream (the main stream unless
+        mark_stream); returns its event (with the split resolve: after phase 1 of the
+        resolve, on the main stream)."""
+        ms = self.s_mark
+        if (gate_resolve or ms is not self.main) and slot.resolved is not None:
+            D.wait_for(ms, slot.resolved)  # the previous resolve read the bitmap
         if self.sort_mark:
-            slot.eng.mark_bitmap(batch, stream=self.main)
+            slot.eng.mark_bitmap(batch, stream=ms)
         else:
             if not self.fused_mark:
-                slot.eng.mark(batch, stream=self.main)
-            slot.eng.build_local_bitmap(stream=self.main)
+                slot.eng.mark(batch, stream=ms)
+            slot.eng.build_local_bitmap(stream=ms)
         if self.split_resolve:
             with torch.cuda.stream(self.main):
                 bitmaps, nb = self.exchange(slot.eng.local_bitmap)
                 slot.eng.resolve(bitmaps, nb, self.max_distance, stream=self.main, phase=1)
-        marked = torch.cuda.Event()
-        marked.record(self.main)
+        marked = self._event()
+        marked.record(ms)
         self._split_bitmaps = (bitmaps, nb) if self.split_resolve else None
         return marked
 
@@ -225,24 +259,24 @@ class UmiPipeline:
             bitmaps, nb = self._split_bitmaps
         if self.s_comm is not None:
             with torch.cuda.stream(self.s_comm):
-                self.s_comm.wait_event(marked)
+                D.wait_for(self.s_comm, marked)
                 bitmaps, nb = self.exchange(slot.eng.local_bitmap)
-                gathered = torch.cuda.Event()
+                gathered = self._event()
                 gathered.record(self.s_comm)
         with torch.cuda.stream(sr):
-            sr.wait_event(marked)
-            if gate_resolve and slot.assigned is not None:
-                sr.wait_event(slot.assigned)  # assign(k - depth) reads the tables rewritten here
+            D.wait_for(sr, marked)
+            if (gate_resolve or self.s_mark is not self.main) and slot.assigned is not None:
+                D.wait_for(sr, slot.assigned)  # assign(k - depth) reads the tables rewritten here
             if self.split_resolve:
                 slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr, phase=2)
             else:
                 if self.s_comm is not None:
-                    sr.wait_event(gathered)
+                    D.wait_for(sr, gathered)
                     bitmaps.record_stream(sr)  # allocated on the comm stream
                 else:
                     bitmaps, nb = self.exchange(slot.eng.local_bitmap)
                 slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr)
-            resolved = torch.cuda.Event()
+            resolved = self._event()
             resolved.record(sr)
         return resolved
 
@@ -253,14 +287,14 @@ class UmiPipeline:
         if slot.assigned is None:
             return
         if slot.eng.sync(stream=stream):
-            slot.assigned = torch.cuda.Event()
+            slot.assigned = self._event()
             slot.assigned.record(stream)
             self.last_assigned = slot.assigned
 
     def _submit_assign_on_resolve(self, slot: _Slot, batch: D.PackedBatch):
         self._settle(slot)
         if slot.assigned is not None:
-            self.main.wait_event(slot.assigned)
+            D.wait_for(self.main, slot.assigned)
         D.score_packed(batch, slot.scores, self.target, self.max_hamming, None, slot.within,
                        cluster=slot.eng if self.fused_mark else None, stream=self.main)
         if self.sort_mark:
@@ -269,17 +303,17 @@ class UmiPipeline:
             if not self.fused_mark:
                 slot.eng.mark(batch, stream=self.main)
             slot.eng.build_local_bitmap(stream=self.main)
-        marked = torch.cuda.Event()
+        marked = self._event()
         marked.record(self.main)
         sr = self.s_resolve
         with torch.cuda.stream(sr):
-            sr.wait_event(marked)
+            D.wait_for(sr, marked)
             bitmaps, nb = self.exchange(slot.eng.local_bitmap)
             slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr)
             slot.eng.assign(batch, slot.cid, stream=sr, deferred=self.on_assigned is None)
             if self.on_assigned is not None:
                 self.on_assigned(slot, batch)
-            slot.assigned = torch.cuda.Event()
+            slot.assigned = self._event()
             slot.assigned.record(sr)
         self.last_assigned = slot.assigned
         self.k += 1
@@ -287,9 +321,9 @@ class UmiPipeline:
 
     def _assign_oldest(self):
         slot, batch, resolved = self.queue.popleft()
-        self.s_assign.wait_event(resolved)
-        if self.score_alone and self.last_scored is not None:
-            self.s_assign.wait_event(self.last_scored)
+        D.wait_for(self.s_assign, resolved)
+        if self.score_alone and self.last_scored is not None and self.s_assign is not self.main:
+            D.wait_for(self.s_assign, self.last_scored)
         # without a consumer hook the assign is deferred (no host wait for the resolve's
         # flags: the host would otherwise stall behind the resolve stream's queue and
         # enqueue the next batch late); the slot is settled before its reuse / at drain
@@ -297,7 +331,7 @@ class UmiPipeline:
         if self.on_assigned is not None:
             with torch.cuda.stream(self.s_assign):
                 self.on_assigned(slot, batch)
-        slot.assigned = torch.cuda.Event()
+        slot.assigned = self._event()
         slot.assigned.record(self.s_assign)
         self.last_assigned = slot.assigned
 
@@ -307,9 +341,9 @@ class UmiPipeline:
         non-converged case); the current stream then waits for it. Returns slot.cid."""
         while any(q[0] is slot for q in self.queue):
             self._assign_oldest()
-        self._settle(slot, self.s_assign if self.assign_on == "separate" else None)
+        self._settle(slot, self.s_assign if self.assign_on != "resolve" else None)
         if slot.assigned is not None:
-            torch.cuda.current_stream(self.main.device).wait_event(slot.assigned)
+            D.wait_for(torch.cuda.current_stream(self.main.device), slot.assigned)
         return slot.cid
 
     def drain(self):
@@ -319,9 +353,9 @@ class UmiPipeline:
                 self._settle(slot)
         while self.queue:
             self._assign_oldest()
-        if self.assign_on == "separate" and self.on_assigned is None:
+        if self.assign_on != "resolve" and self.on_assigned is None:
             for slot in self.slots:
                 self._settle(slot, self.s_assign)
         if self.last_assigned is not None:
-            self.main.wait_event(self.last_assigned)
+            D.wait_for(self.main, self.last_assigned)
         torch.cuda.current_stream(self.main.device).wait_stream(self.main)

@@ -1,0 +1,88 @@
+"""GPU: every A/B environment knob of the H1-H3 device path gives the oracle's outputs.
+
+The knobs (DESIGN.md §7 "A/B switches") are read once per process, so each setting runs
+in a child process (one at a time; a few seconds each) over the same synthetic batch; the
+parent compares the child's cluster ids, H1 fields and within bits with the oracle.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N, L = 400_003, 12
+
+CHILD = r"""
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, {root!r})
+from rogtk_amd import device as D
+from rogtk_amd import synth
+from rogtk_amd.pipeline import UmiPipeline
+n, L = {n}, {L}
+codes_h = synth.umi_codes(n, L)
+codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
+batch = D.PackedBatch(codes, L)
+out = {{}}
+def grab(slot, b):
+    out["cid"] = slot.cid[:n].clone()
+    out["within"] = slot.within.clone()
+    out["comb"] = slot.scores["combined_score"][:n].clone()
+    out["run"] = slot.scores["longest_homopolymer_run"][:n].clone()
+pipe = UmiPipeline(L, n, n, "cuda", depth=2, target=b"ACGTACGTACGT", max_distance=1, on_assigned=grab,
+                   score_alone=True, assign_on={assign_on!r})
+pipe.submit(batch)
+pipe.drain()
+torch.cuda.synchronize()
+np.savez({path!r}, **{{k: v.cpu().numpy() for k, v in out.items()}})
+"""
+
+KNOBS = [
+    ({"ROGTK_WLAB2": "1"}, "separate"),
+    ({"ROGTK_LCC_LOOP": "1"}, "separate"),
+    ({"ROGTK_LOCAL8": "0"}, "separate"),
+    ({"ROGTK_SLICE_BUCKETS": "0"}, "separate"),
+    ({"ROGTK_WORD_EXC": "0"}, "separate"),
+    ({"ROGTK_LABEL_BY_INDEX": "1"}, "separate"),
+    ({"ROGTK_ASSIGN_GROUPS": "1", "ROGTK_ASSIGN_BLOCKS": "0"}, "separate"),
+    ({"ROGTK_ASSIGN_GROUPS": "4"}, "main"),
+    ({"ROGTK_SCORE_GENERIC": "1", "ROGTK_SCORE_BLOCKS": "512"}, "main"),
+    ({"ROGTK_RESOLVE_GRAPH": "1"}, "separate"),
+]
+
+
+@pytest.fixture(scope="module")
+def reference():
+    from oracle import pyoracle as P
+    from rogtk_amd import synth
+
+    codes_h = synth.umi_codes(N, L)
+    col = P.StrCol.from_fixed(synth.codes_to_ascii(codes_h, L))
+    ref = P.umi_complexity(col)
+    _, rw, _ = P.hamming(col, b"ACGTACGTACGT", 1)
+    rc, _, _, _ = P.umi_cluster(col, L, 1)
+    return ref, rw, rc
+
+
+@pytest.mark.parametrize("knobs,assign_on", KNOBS, ids=lambda v: ",".join(f"{k}={x}" for k, x in v.items())
+                         if isinstance(v, dict) else v)
+def test_knob_matches_oracle(reference, tmp_path, knobs, assign_on):
+    ref, rw, rc = reference
+    path = str(tmp_path / "out.npz")
+    env = dict(os.environ, **knobs)
+    r = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT, n=N, L=L, path=path, assign_on=assign_on)],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    z = np.load(path)
+    assert np.array_equal(z["cid"].view(np.uint32), rc)
+    assert np.array_equal(z["comb"].view(np.uint64), ref["combined_score"].view(np.uint64))
+    assert np.array_equal(z["run"].view(np.uint32), ref["longest_homopolymer_run"])
+    bits = np.unpackbits(z["within"].view(np.uint8), bitorder="little")[:N].astype(bool)
+    assert np.array_equal(bits, rw)

@@ -488,7 +488,7 @@ def test_full_size_c2_properties(rg):
 @pytest.mark.parametrize("depth,nb,alone", [(4, 4, False), (2, 5, False), (1, 3, False), (3, 7, False),
                                              (2, 6, True), (3, 5, True)])
 @pytest.mark.parametrize("mark", ["xcd", "fused", "sort"])
-@pytest.mark.parametrize("assign_on", ["resolve", "separate"])
+@pytest.mark.parametrize("assign_on", ["resolve", "separate", "main", "main_mark_stream"])
 def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assign_on):
     """rogtk_amd.pipeline (3 streams, `depth` batches in flight) == the sequential device
     path for EVERY batch (outputs copied out by the on_assigned hook before slot reuse)."""
@@ -501,13 +501,18 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assig
     n, L = 300_001, 12
     seeds = [synth.DEFAULT_SEED + 17 * k for k in range(nb)]
     outs = []
+    mark_stream = assign_on == "main_mark_stream"
+    if mark_stream:
+        if mark == "fused":
+            pytest.skip("a fused mark has no stream of its own")
+        assign_on = "main"
 
     def grab(slot, batch):
         outs.append((slot.cid[:n].clone(), slot.within.clone(), slot.scores["combined_score"][:n].clone(),
                      slot.scores["longest_homopolymer_run"][:n].clone()))
 
     pipe = UmiPipeline(L, n, n, "cuda", depth=depth, target=b"ACGTACGTACGT", max_distance=1, mark=mark,
-                       on_assigned=grab, score_alone=alone, assign_on=assign_on)
+                       on_assigned=grab, score_alone=alone, assign_on=assign_on, mark_stream=mark_stream)
     keep = []
     for s in seeds:
         codes = torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda()
@@ -529,7 +534,9 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assig
 @pytest.mark.parametrize("depth,nb", [(2, 5), (3, 3), (1, 2)])
 @pytest.mark.parametrize("assign_on,gate,order", [("separate", "auto", "score_first"), ("separate", "resolve", "score_first"),
                                                   ("resolve", "auto", "score_first"), ("separate", "auto", "mark_first"),
-                                                  ("separate", "auto", "late_assign")])
+                                                  ("separate", "auto", "late_assign"),
+                                                  ("main", "auto", "mark_first"), ("main", "auto", "score_first"),
+                                                  ("main", "auto", "mark_stream")])
 def test_pipeline_deferred_assign(rg, depth, nb, spec, assign_on, gate, order):
     """No on_assigned hook: assigns are enqueued before their resolve's flags are checked;
     with 1 speculative round every batch needs the deferred completion (rounds + labels +
@@ -549,7 +556,7 @@ def test_pipeline_deferred_assign(rg, depth, nb, spec, assign_on, gate, order):
         pipe = UmiPipeline(L, n, n, "cuda", depth=depth, target=b"ACGTACGTACGT", max_distance=1,
                            assign_on=assign_on, reuse_gate=gate, score_alone=depth == 2,
                            mark_first=order != "score_first" and order != "late_assign",
-                           assign_early=order != "late_assign")
+                           assign_early=order != "late_assign", mark_stream=order == "mark_stream")
         keep, last = [], {}
         for k, s in enumerate(seeds):
             codes = torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda()
@@ -570,7 +577,8 @@ def test_pipeline_deferred_assign(rg, depth, nb, spec, assign_on, gate, order):
         assert np.array_equal(slot.within.cpu().numpy()[:len(hw)], hw.cpu().numpy()), k
 
 
-def test_pipeline_settle_gives_final_ids(rg):
+@pytest.mark.parametrize("assign_on,dev_ev", [("separate", True), ("main", True), ("separate", False)])
+def test_pipeline_settle_gives_final_ids(rg, assign_on, dev_ev):
     """settle(slot) right after submit (1 speculative round: every batch needs the deferred
     completion) returns the final ids of that batch, mid-stream."""
     import torch
@@ -583,7 +591,8 @@ def test_pipeline_settle_gives_final_ids(rg):
     seeds = [synth.DEFAULT_SEED + 31 * k for k in range(4)]
     try:
         D.set_spec_rounds(1)
-        pipe = UmiPipeline(L, n, n, "cuda", depth=2, target=b"ACGTACGTACGT", max_distance=1, score_alone=True)
+        pipe = UmiPipeline(L, n, n, "cuda", depth=2, target=b"ACGTACGTACGT", max_distance=1, score_alone=True,
+                           assign_on=assign_on, device_events=dev_ev)
         keep, got = [], []
         for s in seeds:
             codes = torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda()
