@@ -103,6 +103,9 @@ def parse():
     ap.add_argument("--score-first", action="store_true",
                     help="main stream order score -> mark (round-2 order; default: mark -> score, so the "
                          "resolve overlaps the score kernel)")
+    ap.add_argument("--fused-assign", action="store_true",
+                    help="score kernel after the batch's resolve, writing the cluster ids too (one pass over the "
+                         "codes; main stream: mark(k), score+assign(k-depth+1))")
     ap.add_argument("--mark-stream", action="store_true",
                     help="presence-bitmap mark on a stream of its own (overlaps score + assign)")
     ap.add_argument("--torch-events", action="store_true",
@@ -243,9 +246,11 @@ def cpu_baseline_threads(codes_h: np.ndarray, L: int, md: int, threads: int = 0)
                       f"{os.cpu_count()} cores): H1+H2 {t1 - t0:.2f} s, H3 (threaded union-find) {t2 - t1:.2f} s"}
 
 
-def load_traffic(reads_per_launch: int):
-    """Per-launch HBM bytes of k_score_packed from the latest committed PMC summary made
-    at the same reads per launch, if any."""
+def load_traffic(reads_per_launch: int, fused: bool = False):
+    """Per-launch HBM bytes of k_score_packed (its fused score + assign instance when
+    `fused`) from the latest committed PMC summary made at the same reads per launch, if
+    any."""
+    key = "score_assign_hbm_bytes_per_launch" if fused else "score_packed_hbm_bytes_per_launch"
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
     for path in reversed(files):
         try:
@@ -253,8 +258,8 @@ def load_traffic(reads_per_launch: int):
                 j = json.load(f)
         except Exception:
             continue
-        if j.get("reads_per_launch", 10_000_000) == reads_per_launch and j.get("score_packed_hbm_bytes_per_launch"):
-            return j["score_packed_hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+        if j.get("reads_per_launch", 10_000_000) == reads_per_launch and j.get(key):
+            return j[key], os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -307,7 +312,8 @@ def main():
                        resolve_streams=args.resolve_streams, assign_on=args.assign_on,
                        split_resolve=args.split_resolve, reuse_gate=args.reuse_gate,
                        assign_early=not args.late_assign, mark_first=False if args.score_first else "auto",
-                       device_events=not args.torch_events, mark_stream=args.mark_stream)
+                       device_events=not args.torch_events, mark_stream=args.mark_stream,
+                       fused_assign=args.fused_assign)
 
     def step():
         pipe.submit(batch)
@@ -411,7 +417,10 @@ def main():
         D.profile_reset()
         D.profile_enable(True)
         for _ in range(args.iso_launches):
-            D.score_packed(batch, slot.scores, TARGET, 1, None, slot.within)
+            if args.fused_assign:
+                D.score_assign_packed(batch, slot.eng, slot.cid, slot.scores, TARGET, 1, None, slot.within)
+            else:
+                D.score_packed(batch, slot.scores, TARGET, 1, None, slot.within)
         torch.cuda.synchronize()
         D.profile_enable(False)
         ms, launches = D.profile_read_span("score_packed")
@@ -426,12 +435,12 @@ def main():
     value = n_total * args.steps / el if args.emulate_ranks == 1 else n * args.emulate_ranks * args.steps / el
     # roofline of the dominant kernel: algorithmic bytes per read of k_score_packed
     #   in: 4 B packed code; out: 6 x 8 B f64 fields + 4 B longest run + 1/8 B within bit
-    bpr = 4 + 48 + 4 + 0.125
+    bpr = 4 + 48 + 4 + 0.125 + (4 if args.fused_assign else 0)  # + the u32 cluster id when fused
     roof = None
     if "score_packed" in kernels:
         avg_s = kernels["score_packed"]["avg_us"] * 1e-6
         achieved = count * bpr / avg_s / 1e9
-        traffic, src = load_traffic(count)
+        traffic, src = load_traffic(count, fused=args.fused_assign)
         roof = {"kernel": "k_score_packed", "bound": "hbm", "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "traffic_source": src,

@@ -118,6 +118,19 @@ int rogtk_umi_score_packed(const uint32_t* codes, const uint64_t* regular_bits, 
                            uint32_t* hamming_distance, uint64_t* hamming_within_bits,
                            void* cluster_ws, int64_t cluster_max_distinct, void* stream);
 
+/* rogtk_umi_score_packed + rogtk_cluster_assign[_deferred] of the same rows in ONE pass
+ * over the codes (cluster_ws resolved by rogtk_cluster_resolve; deferred != 0 as
+ * rogtk_cluster_assign_deferred): the assign half of the H3 hot path
+ * (expressions.rs:1034-1082, its per-row id lookup) fused into the H1/H2 kernel, which
+ * already streams the codes. Same outputs as the two calls; falls back to them where the
+ * workspace has no word labels. No presence mark (cluster_ws is the resolved workspace). */
+int rogtk_umi_score_assign_packed(const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
+                                  int umi_len, const rogtk_umi_scores* scores, const uint8_t* target,
+                                  int64_t target_len, uint32_t max_distance, uint32_t* hamming_distance,
+                                  uint64_t* hamming_within_bits, const void* cluster_ws,
+                                  int64_t cluster_max_distinct, uint32_t* cluster_id, int deferred,
+                                  void* stream);
+
 /*
  * Byte path: the same outputs for an explicit list of rows of a device Arrow
  * string column (rows[0 .. *n_rows_dev), at most max_rows), computed straight

@@ -95,6 +95,8 @@ _P_F64 = ctypes.POINTER(ctypes.c_double)
 SIGNATURES = {
     "rogtk_device_count": [_P_I32],
     "rogtk_stage_strings": [_vp, _i32, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp],
+    "rogtk_umi_score_assign_packed": [_vp, _vp, _i64, _i32, _P_SCORES, _vp, _i64, _u32, _vp, _vp, _vp, _i64, _vp,
+                                      _i32, _vp],
     "rogtk_umi_score_packed": [_vp, _vp, _i64, _i32, _P_SCORES, _vp, _i64, _u32, _vp, _vp, _vp,
                                _i64, _vp],
     "rogtk_umi_score_rows": [_vp, _i32, _vp, _vp, _vp, _i64, _i64, _P_SCORES, _vp, _i64, _u32, _vp,

@@ -693,6 +693,42 @@ int rogtk_umi_score_packed(const uint32_t* codes, const uint64_t* regular_bits, 
                                presence, as_stream(stream));
 }
 
+int rogtk_umi_score_assign_packed(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
+                                  const rogtk_umi_scores* scores, const uint8_t* target, int64_t target_len,
+                                  uint32_t max_distance, uint32_t* hamming_distance,
+                                  uint64_t* hamming_within_bits, const void* cluster_ws,
+                                  int64_t cluster_max_distinct, uint32_t* cluster_id, int deferred,
+                                  void* stream) {
+    ROGTK_REQUIRE(umi_len >= 1 && umi_len <= kMaxPackedLen, ROGTK_E_UNSUPPORTED,
+                  "packed path: umi_len %d outside 1..%d", umi_len, kMaxPackedLen);
+    ROGTK_REQUIRE(n >= 0, ROGTK_E_INVALID, "n must be >= 0");
+    ROGTK_REQUIRE(n == 0 || (codes && cluster_id), ROGTK_E_INVALID, "codes / cluster_id is NULL");
+    ROGTK_REQUIRE(cluster_ws, ROGTK_E_INVALID, "score_assign: cluster_ws is NULL");
+    ROGTK_REQUIRE(target_len >= 0, ROGTK_E_INVALID, "target_len must be >= 0");
+    ROGTK_REQUIRE(aligned16(codes) && aligned16(cluster_id), ROGTK_E_INVALID,
+                  "score_assign: codes/cluster_id must be 16-byte aligned");
+    const ScoreOut o = to_score_out(scores);
+    if (int rc = check_packed_alignment(codes, o, hamming_distance)) return rc;
+    ClusterLayout cl;
+    if (int rc = cluster_layout(umi_len, cluster_max_distinct, &cl)) return rc;
+    PackedParams p;
+    build_packed_params(umi_len, &p);
+    encode_target(target, target_len, umi_len, max_distance, &p);
+    hipStream_t s = as_stream(stream);
+    AssignIn a;
+    if (int rc = cluster_assign_prepare(cl, (const uint8_t*)cluster_ws, codes, regular_bits, n, cluster_id, s,
+                                        deferred != 0, &a))
+        return rc;
+    const bool any = any_score(o) || (p.ham_mode && (hamming_distance || hamming_within_bits));
+    if (a.out && any)  // one pass: scores, Hamming and ids
+        return launch_score_packed(codes, regular_bits, n, p, o, hamming_distance, hamming_within_bits, nullptr, s,
+                                   &a);
+    if (int rc = launch_score_packed(codes, regular_bits, n, p, o, hamming_distance, hamming_within_bits, nullptr, s))
+        return rc;
+    return launch_cluster_assign(cl, (const uint8_t*)cluster_ws, codes, regular_bits, n, cluster_id, s,
+                                 deferred != 0);
+}
+
 int rogtk_umi_score_rows(const void* offsets, int offset_width, const uint8_t* values,
                          const int64_t* rows, const int64_t* n_rows_dev, int64_t max_rows,
                          int64_t max_len, const rogtk_umi_scores* scores, const uint8_t* target,

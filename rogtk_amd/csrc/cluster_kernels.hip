@@ -2153,6 +2153,40 @@ int launch_cluster_assign(const ClusterLayout& cl, const uint8_t* ws, const uint
     return enqueue_assign(cl, p, wl, codes, regular_bits, n, cluster_id, s);
 }
 
+int cluster_assign_prepare(const ClusterLayout& cl, const uint8_t* ws, const uint32_t* codes,
+                           const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id, hipStream_t s,
+                           bool deferred, AssignIn* a) {
+    a->wlab = nullptr;
+    a->wexc = nullptr;
+    a->labelcode = nullptr;
+    a->out = nullptr;
+    if (!deferred)
+        if (int rc = cluster_finish(ws, s)) return rc;
+    bool wl = false;
+    {
+        std::lock_guard<std::mutex> lk(g_rs_mu);
+        auto it = g_rs.find(ws);
+        if (it != g_rs.end()) {
+            wl = it->second.word_labels;
+            if (deferred && it->second.pending) {  // re-run as a plain assign if not converged
+                auto& d = it->second.deferred;
+                d.on = true;
+                d.codes = codes;
+                d.regbits = regular_bits;
+                d.n = n;
+                d.cid = cluster_id;
+            }
+        }
+    }
+    if (!wl || !cl.label_by_code || wlab2_on()) return ROGTK_OK;
+    WsPtrs p = ws_ptrs(cl, const_cast<uint8_t*>(ws));
+    a->wlab = p.wpref;
+    a->wexc = p.G;
+    a->labelcode = p.labelcode;
+    a->out = cluster_id;
+    return ROGTK_OK;
+}
+
 int launch_cluster_lookup(const ClusterLayout& cl, const uint8_t* ws, const uint64_t* q, int64_t nq, uint32_t* lab,
                           hipStream_t s) {
     if (nq <= 0) return ROGTK_OK;
@@ -2317,8 +2351,9 @@ constexpr int kSliceBlock = 1024;
 constexpr int kSliceChunks = 16;   // a multiple of the 8 XCDs
 constexpr int kSliceLog2 = 20;     // codes per slice (LDS bits)
 constexpr int kMaxSlices = 16;     // 4^12 / 2^20
-constexpr int kBucketRows = 8192;  // rows per segment workgroup (8 per lane)
+constexpr int kBucketRows = 8192;  // rows per segment workgroup (8 per lane; default)
 constexpr int kSegCap = 2048;      // codes per (slice, workgroup) segment: 4x the mean share at 16 slices
+constexpr int kMinBucketRows = 2048;  // smallest bucket instance (temp sizing)
 
 // Segment mode (segs != nullptr, written by k_slice_bucket): workgroup (s, c) reads only
 // slice s's segments of the bucket workgroups of chunk c (every code is read once in
@@ -2329,7 +2364,8 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_mark(const uint32_t* __re
                                                             uint64_t* __restrict__ out, int64_t words,
                                                             const uint32_t* __restrict__ segs = nullptr,
                                                             const uint32_t* __restrict__ seglen = nullptr,
-                                                            int nbuckets = 0) {
+                                                            int nbuckets = 0, int bucket_rows = kBucketRows,
+                                                            int seg_cap = kSegCap) {
     __shared__ uint32_t sbits[(1u << kSliceLog2) / 32];  // 128 KB: the slice's bits (2^slice_log2 used)
     const int c = blockIdx.x % chunks, sl = blockIdx.x / chunks;
     const uint32_t sw32 = (1u << slice_log2) >> 5;
@@ -2342,15 +2378,16 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_mark(const uint32_t* __re
         // (its workgroup overflowed): then this chunk's rows are read instead
         const int b0 = (int)((int64_t)c * nbuckets / chunks), b1 = (int)((int64_t)(c + 1) * nbuckets / chunks);
         bool over = false;
-        for (int b = b0 + (int)threadIdx.x; b < b1; b += kSliceBlock) over |= seglen[(int64_t)sl * nbuckets + b] > kSegCap;
-        r0 = (int64_t)b0 * kBucketRows;
-        r1 = min(n, (int64_t)b1 * kBucketRows);
+        for (int b = b0 + (int)threadIdx.x; b < b1; b += kSliceBlock)
+            over |= seglen[(int64_t)sl * nbuckets + b] > (uint32_t)seg_cap;
+        r0 = (int64_t)b0 * bucket_rows;
+        r1 = min(n, (int64_t)b1 * bucket_rows);
         if (!__syncthreads_or(over)) {
             // one wave per segment: 256 codes per pass of 16-B loads
             const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
             for (int b = b0 + wave; b < b1; b += kSliceBlock / 64) {
                 const uint32_t len = seglen[(int64_t)sl * nbuckets + b];
-                const uint32_t* seg = segs + ((int64_t)sl * nbuckets + b) * kSegCap;
+                const uint32_t* seg = segs + ((int64_t)sl * nbuckets + b) * seg_cap;
                 for (uint32_t i = 4 * lane; i < len; i += 256) {
                     const uint4 v = *reinterpret_cast<const uint4*>(seg + i);
                     const uint32_t cc[4] = {v.x, v.y, v.z, v.w};
@@ -2413,11 +2450,13 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_mark(const uint32_t* __re
 // that would overflow is not stored (its length says so), and the slice pass reads the
 // rows of that chunk instead.
 constexpr int kBucketThreads = 1024;  // 8 rows per lane: short rank chains per wave
+template <int kBucketRows, int kBucketThreads>
 __global__ __launch_bounds__(kBucketThreads) void k_slice_bucket(const uint32_t* __restrict__ codes,
                                                          const uint64_t* __restrict__ regbits, int64_t n,
                                                          int slice_log2, int nslices, uint32_t* __restrict__ segs,
                                                          uint32_t* __restrict__ seglen, int nbuckets) {
     __shared__ unsigned int cnt[kMaxSlices], lbase[kMaxSlices + 1];
+    constexpr int kSegCap = kBucketRows / 4;  // 4x the mean share at 16 slices
     __shared__ uint32_t stage[kBucketRows];
     const int t = threadIdx.x, lane = t & 63;
     if (t < kMaxSlices) cnt[t] = 0;
@@ -2505,10 +2544,23 @@ __global__ __launch_bounds__(kBlock) void k_or_partials(const uint64_t* __restri
 // chunks of the slice mark for n rows (1 = the slices write the bitmap directly)
 inline int slice_chunks(int64_t n) { return n >= (1 << 20) ? kSliceChunks : 1; }
 inline int slices_of(int L) { return 1 << (2 * L - std::min(2 * L, kSliceLog2)); }
-inline int64_t seg_buckets(int64_t n) { return (n + kBucketRows - 1) / kBucketRows; }
+inline int64_t seg_buckets(int64_t n, int rows = kBucketRows) { return (n + rows - 1) / rows; }
+// ROGTK_BUCKET_ROWS=2048|4096|8192: rows per bucket workgroup (256 / 512 / 1024 threads,
+// 8 rows per lane; A/B, default 8192)
+inline int bucket_rows() {
+    static const int r = [] {
+        const char* e = getenv("ROGTK_BUCKET_ROWS");
+        const int v = e ? atoi(e) : kBucketRows;
+        return v == 2048 || v == 4096 ? v : kBucketRows;
+    }();
+    return r;
+}
 // segments + their lengths of the segment mode
 inline int64_t seg_bytes(int64_t n) {
-    return ((int64_t)kMaxSlices * seg_buckets(n) * kSegCap * 4) + ((int64_t)kMaxSlices * seg_buckets(n) * 4 + 255) / 256 * 256;
+    // segments: slices x buckets x rows/4 codes = 4n codes for every bucket size; lengths
+    // for the smallest bucket instance
+    return ((int64_t)kMaxSlices * seg_buckets(n) * kSegCap * 4) +
+           ((int64_t)kMaxSlices * seg_buckets(n, kMinBucketRows) * 4 + 255) / 256 * 256;
 }
 // ROGTK_SLICE_BUCKETS=0: slices read all rows (A/B)
 inline bool slice_buckets_on() {
@@ -2581,17 +2633,26 @@ int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bi
         uint64_t* dst = chunks > 1 ? (uint64_t*)temp : bitmap;
         const uint32_t* segs = nullptr;
         uint32_t* seglen = nullptr;
-        const int nb = (int)seg_buckets(n);
+        const int brows = bucket_rows(), bcap = brows / 4;
+        const int nb = (int)seg_buckets(n, brows);
         if (chunks > 1 && slices > 1 && slices <= kMaxSlices && slice_buckets_on()) {
             // segment pass: every slice workgroup then reads only its slice's codes (the
             // chunks of all rows were read once per slice: 16x at L = 12, from L2)
             segs = (const uint32_t*)((uint8_t*)temp + (int64_t)chunks * words * 8);
-            seglen = (uint32_t*)((uint8_t*)segs + (int64_t)kMaxSlices * nb * kSegCap * 4);
-            hipLaunchKernelGGL(k_slice_bucket, dim3((unsigned)nb), dim3(kBucketThreads), 0, s, codes, regular_bits, n, slog,
-                               slices, (uint32_t*)segs, seglen, nb);
+            seglen = (uint32_t*)((uint8_t*)segs + (int64_t)kMaxSlices * nb * bcap * 4);
+            if (brows == 2048)
+                hipLaunchKernelGGL((k_slice_bucket<2048, 256>), dim3((unsigned)nb), dim3(256), 0, s, codes, regular_bits,
+                                   n, slog, slices, (uint32_t*)segs, seglen, nb);
+            else if (brows == 4096)
+                hipLaunchKernelGGL((k_slice_bucket<4096, 512>), dim3((unsigned)nb), dim3(512), 0, s, codes, regular_bits,
+                                   n, slog, slices, (uint32_t*)segs, seglen, nb);
+            else
+                hipLaunchKernelGGL((k_slice_bucket<kBucketRows, kBucketThreads>), dim3((unsigned)nb),
+                                   dim3(kBucketThreads), 0, s, codes, regular_bits, n, slog, slices, (uint32_t*)segs,
+                                   seglen, nb);
         }
         hipLaunchKernelGGL(k_slice_mark, dim3((unsigned)(slices * chunks)), dim3(kSliceBlock), 0, s, codes, regular_bits,
-                           n, slog, chunks, chunk_rows, dst, words, segs, (const uint32_t*)seglen, nb);
+                           n, slog, chunks, chunk_rows, dst, words, segs, (const uint32_t*)seglen, nb, brows, bcap);
         if (chunks > 1)
             hipLaunchKernelGGL(k_or_partials, dim3(grid_for(words, 4096)), dim3(kBlock), 0, s, dst, chunks, words,
                                bitmap);

@@ -178,6 +178,15 @@ void encode_target(const uint8_t* target, int64_t target_len, int L, uint32_t ma
                    PackedParams* p);
 int build_packed_params(int L, PackedParams* p);
 
+// Tables of a fused score + assign (k_score_packed<..., ASG>): a resolved cluster
+// workspace's word labels, exception masks and per-code labels, and the id output.
+struct AssignIn {
+    const uint32_t* wlab;
+    const uint64_t* wexc;
+    const uint32_t* labelcode;
+    uint32_t* out;  // nullptr: no assign in the score pass
+};
+
 // ------------------------------------------------------ kernel launchers
 int launch_stage(const void* offsets, int offset_width, const uint8_t* values,
                  const uint8_t* validity, int64_t validity_offset, int64_t n, int L,
@@ -185,7 +194,7 @@ int launch_stage(const void* offsets, int offset_width, const uint8_t* values,
                  unsigned long long* n_irregular, hipStream_t s);
 int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
                         const PackedParams& p, const ScoreOut& o, uint32_t* hd, uint64_t* hw,
-                        uint8_t* presence, hipStream_t s);
+                        uint8_t* presence, hipStream_t s, const AssignIn* asg = nullptr);
 int launch_score_rows(const void* offsets, int offset_width, const uint8_t* values,
                       const int64_t* rows, const int64_t* n_rows_dev, int64_t max_rows,
                       const double* lut, int64_t lut_max, const ScoreOut& o,
@@ -245,6 +254,13 @@ int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bi
                                uint64_t* bitmap, void* temp, int64_t temp_bytes, hipStream_t s);
 // phases: 1 = rank tables + local CC, 2 = global rounds + labels (after phase 1 of the
 // same bitmaps), 3 = both
+// The assign half of a fused score + assign: completes (deferred = false) or registers
+// (deferred = true, as launch_cluster_assign) the assign of codes into cluster_id, and
+// fills *a with the tables when the fused kernel can label these rows (word labels,
+// labels by code); a->out == nullptr otherwise (the caller then uses launch_cluster_assign).
+int cluster_assign_prepare(const ClusterLayout& cl, const uint8_t* ws, const uint32_t* codes,
+                           const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id, hipStream_t s,
+                           bool deferred, AssignIn* a);
 int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t* bitmaps,
                            int n_bitmaps, int max_distance, hipStream_t s, int phases = 3);
 // Waits for an asynchronous resolve's round flags and completes it if needed.

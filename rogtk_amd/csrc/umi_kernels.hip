@@ -177,14 +177,20 @@ __device__ __forceinline__ uint32_t hamming_code(uint32_t code, const PackedPara
     return (uint32_t)__popc((x | (x >> 1)) & P.cmplo) + P.always_mismatch;
 }
 
-template <bool SCORE, bool HAMD, bool HAMW, bool MARK, int LT = 0>
+// ASG: also the H3 cluster id of every row (the assign of a resolved workspace, fused
+// into the pass that streams the codes): the word label (1 MB table, L2-resident) is
+// gathered right after the code load, so its latency hides behind the scoring; flagged
+// words read their exception mask, exception codes the per-code label table
+// (k_assign in cluster_kernels.hip is the standalone form, identical ids).
+template <bool SCORE, bool HAMD, bool HAMW, bool MARK, int LT = 0, bool ASG = false>
 __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restrict__ codes,
                                                           const uint64_t* __restrict__ regbits,
                                                           int64_t n, const PackedParams P,
                                                           const ScoreOut O,
                                                           uint32_t* __restrict__ hd,
                                                           uint64_t* __restrict__ hw,
-                                                          uint8_t* __restrict__ pres, uint64_t* tspan) {
+                                                          uint8_t* __restrict__ pres, const AssignIn A,
+                                                          uint64_t* tspan) {
     span_enter(tspan);  // profiling only (NULL otherwise)
     __shared__ double s_tab[4][kMaxPackedLen + 1];
     if (SCORE) {
@@ -222,6 +228,12 @@ __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restr
                     if (!regbits || ((regbits[rr[k] >> 6] >> (rr[k] & 63)) & 1u)) reg |= 1u << k;
                 }
             }
+        }
+
+        uint32_t wl[kRowsPerLane];
+        if (ASG) {
+#pragma unroll
+            for (int k = 0; k < kRowsPerLane; ++k) wl[k] = ((reg >> k) & 1u) ? A.wlab[c[k] >> 6] : 0xFFFFFFFFu;
         }
 
         uint32_t wnib = 0;
@@ -293,6 +305,25 @@ __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restr
 #pragma unroll
                 for (int k = 0; k < kRowsPerLane; ++k)
                     if ((reg >> k) & 1u) pres[c[k]] = 1;  // benign same-value race
+            }
+            if (ASG) {
+                // word_label_of (cluster_kernels.hip): bit 31 flags a word with exceptions
+#pragma unroll
+                for (int k = 0; k < kRowsPerLane; ++k)
+                    if (wl[k] != 0xFFFFFFFFu && (wl[k] >> 31))
+                        wl[k] = ((A.wexc[c[k] >> 6] >> (c[k] & 63)) & 1ull) ? 0xFFFFFFFFu : (wl[k] & 0x7FFFFFFFu);
+                uint32_t id[kRowsPerLane];
+#pragma unroll
+                for (int k = 0; k < kRowsPerLane; ++k)
+                    id[k] = !((reg >> k) & 1u) ? 0xFFFFFFFFu : wl[k] != 0xFFFFFFFFu ? wl[k] : A.labelcode[c[k]];
+                if (full) {
+                    stream_store(u32x2_t{id[0], id[1]}, reinterpret_cast<u32x2_t*>(A.out + rA));
+                    stream_store(u32x2_t{id[2], id[3]}, reinterpret_cast<u32x2_t*>(A.out + rB));
+                } else {
+                    const int64_t rr[4] = {rA, rA + 1, rB, rB + 1};
+                    for (int k = 0; k < kRowsPerLane; ++k)
+                        if (rr[k] < n) A.out[rr[k]] = id[k];
+                }
             }
         }
         if (HAMW) {
@@ -499,11 +530,15 @@ int launch_stage(const void* offsets, int offset_width, const uint8_t* values,
 
 int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
                         const PackedParams& p, const ScoreOut& o, uint32_t* hd, uint64_t* hw,
-                        uint8_t* presence, hipStream_t s) {
+                        uint8_t* presence, hipStream_t s, const AssignIn* asg) {
     if (n <= 0) return ROGTK_OK;
+    const AssignIn A = asg ? *asg : AssignIn{nullptr, nullptr, nullptr, nullptr};
+    const bool fused = A.out != nullptr;
     const bool score = any_score(o), hamd = p.ham_mode && hd, hamw = p.ham_mode && hw,
                mark = presence != nullptr;
     if (!score && !hamd && !hamw && !mark) return ROGTK_OK;
+    ROGTK_REQUIRE(!fused || (!mark && (score || hamd || hamw)), ROGTK_E_UNSUPPORTED,
+                  "score_packed: a fused assign needs a score / Hamming output and no presence mark");
     // exact: the profiling events ride on the dispatch packet (kernel execution time only,
     // comparable with rocprofv3's kernel trace; bench.py's roofline.frac)
     ProfScope prof(score || hamd || hamw ? K_SCORE_PACKED : K_MARK, s, true);
@@ -521,7 +556,13 @@ int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int
     case (S * 8 + D * 4 + W * 2 + M):                                                          \
         hipExtLaunchKernelGGL((k_score_packed<S, D, W, M>), dim3(g), dim3(kBlock), 0, s,       \
                               prof.start(), prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, \
-                              presence, tspan);                                                  \
+                              presence, A, tspan);                                               \
+        break;
+#define ROGTK_SPA(S, D, W)                                                                      \
+    case (S * 8 + D * 4 + W * 2):                                                              \
+        hipExtLaunchKernelGGL((k_score_packed<S, D, W, false, 0, true>), dim3(g), dim3(kBlock), 0, s, \
+                              prof.start(), prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, \
+                              presence, A, tspan);                                               \
         break;
     // the bench / C2 configuration (12-bp UMIs, all fields + within bits) has a
     // length-specialised instance (ROGTK_SCORE_GENERIC=1: runtime-length kernel, A/B)
@@ -530,19 +571,34 @@ int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int
         return e && e[0] == '1';
     }();
     if (!generic && p.L == 12 && sel == 8 + 2) {
-        hipExtLaunchKernelGGL((k_score_packed<true, false, true, false, 12>), dim3(g), dim3(kBlock), 0, s,
-                              prof.start(), prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, presence, tspan);
+        if (fused)
+            hipExtLaunchKernelGGL((k_score_packed<true, false, true, false, 12, true>), dim3(g), dim3(kBlock), 0, s,
+                                  prof.start(), prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, presence, A,
+                                  tspan);
+        else
+            hipExtLaunchKernelGGL((k_score_packed<true, false, true, false, 12>), dim3(g), dim3(kBlock), 0, s,
+                                  prof.start(), prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, presence, A,
+                                  tspan);
         ROGTK_HIP_CHECK(hipGetLastError());
         span_end(K_SCORE_PACKED, tspan, g, s);
         return ROGTK_OK;
     }
-    switch (sel) {
-        ROGTK_SP(0, 0, 0, 1) ROGTK_SP(0, 0, 1, 0) ROGTK_SP(0, 0, 1, 1) ROGTK_SP(0, 1, 0, 0)
-        ROGTK_SP(0, 1, 0, 1) ROGTK_SP(0, 1, 1, 0) ROGTK_SP(0, 1, 1, 1) ROGTK_SP(1, 0, 0, 0)
-        ROGTK_SP(1, 0, 0, 1) ROGTK_SP(1, 0, 1, 0) ROGTK_SP(1, 0, 1, 1) ROGTK_SP(1, 1, 0, 0)
-        ROGTK_SP(1, 1, 0, 1) ROGTK_SP(1, 1, 1, 0) ROGTK_SP(1, 1, 1, 1)
-        default: break;
+    if (fused) {
+        switch (sel) {
+            ROGTK_SPA(0, 0, 1) ROGTK_SPA(0, 1, 0) ROGTK_SPA(0, 1, 1) ROGTK_SPA(1, 0, 0)
+            ROGTK_SPA(1, 0, 1) ROGTK_SPA(1, 1, 0) ROGTK_SPA(1, 1, 1)
+            default: break;
+        }
+    } else {
+        switch (sel) {
+            ROGTK_SP(0, 0, 0, 1) ROGTK_SP(0, 0, 1, 0) ROGTK_SP(0, 0, 1, 1) ROGTK_SP(0, 1, 0, 0)
+            ROGTK_SP(0, 1, 0, 1) ROGTK_SP(0, 1, 1, 0) ROGTK_SP(0, 1, 1, 1) ROGTK_SP(1, 0, 0, 0)
+            ROGTK_SP(1, 0, 0, 1) ROGTK_SP(1, 0, 1, 0) ROGTK_SP(1, 0, 1, 1) ROGTK_SP(1, 1, 0, 0)
+            ROGTK_SP(1, 1, 0, 1) ROGTK_SP(1, 1, 1, 0) ROGTK_SP(1, 1, 1, 1)
+            default: break;
+        }
     }
+#undef ROGTK_SPA
 #undef ROGTK_SP
     ROGTK_HIP_CHECK(hipGetLastError());
     span_end(K_SCORE_PACKED, tspan, g, s);

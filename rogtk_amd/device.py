@@ -143,6 +143,26 @@ def score_packed(batch: PackedBatch, scores: Optional[Dict[str, torch.Tensor]] =
               cluster.max_distinct if cluster is not None else 0, _s(stream))
 
 
+def score_assign_packed(batch: PackedBatch, engine: "ClusterEngine", cluster_id: torch.Tensor,
+                        scores: Optional[Dict[str, torch.Tensor]] = None, target: Optional[bytes] = None,
+                        max_distance: int = 1, hamming_distance: Optional[torch.Tensor] = None,
+                        hamming_within_bits: Optional[torch.Tensor] = None, deferred: bool = False,
+                        stream=None) -> None:
+    """score_packed + engine.assign(batch, cluster_id) in one pass over the codes (the
+    engine's resolve must have been enqueued; deferred as in ClusterEngine.assign)."""
+    t = None
+    tl = 0
+    if target is not None:
+        tb = target.encode() if isinstance(target, str) else bytes(target)
+        t = ctypes.create_string_buffer(tb, max(len(tb), 1))
+        tl = len(tb)
+    if cluster_id.dtype != torch.int32 or cluster_id.numel() < batch.n or not cluster_id.is_contiguous():
+        raise ValueError("cluster_id: contiguous int32 with >= n elements")
+    _lib.call("rogtk_umi_score_assign_packed", _p(batch.codes), _p(batch.regular_bits), batch.n, batch.umi_len,
+              _scores_struct(scores), t, tl, max_distance, _p(hamming_distance), _p(hamming_within_bits),
+              _p(engine.ws), engine.max_distinct, _p(cluster_id), 1 if deferred else 0, _s(stream))
+
+
 def score_rows(offsets: torch.Tensor, values: torch.Tensor, rows: torch.Tensor,
                n_rows_dev: Optional[torch.Tensor], max_rows: int, max_len: int,
                scores: Optional[Dict[str, torch.Tensor]] = None, target: Optional[bytes] = None,

@@ -59,7 +59,7 @@ class UmiPipeline:
                  on_assigned=None, score_alone: bool = False, exchange=None, resolve_streams: int = 1,
                  assign_on: str = "main", split_resolve: bool = False, reuse_gate: str = "auto",
                  assign_early: bool = True, mark_first="auto", device_events: bool = True,
-                 mark_stream: bool = False):
+                 mark_stream: bool = False, fused_assign: bool = False):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
@@ -123,6 +123,16 @@ class UmiPipeline:
         self.s_mark = torch.cuda.Stream(dev, priority=priorities[0]) if mark_stream else self.main
         if mark_stream:
             self.mark_first = True
+        # fused_assign: batch k's score kernel runs only after its resolve and also writes
+        # its cluster ids (rogtk_umi_score_assign_packed: one pass over the codes instead of
+        # a score pass and an assign pass). The main stream then runs mark(k) and
+        # score+assign(k - depth + 1), so the resolve of a batch overlaps depth - 1 marks
+        # and score+assign passes of earlier batches.
+        if fused_assign and (mark_stream or split_resolve or self.fused_mark or assign_on == "resolve"
+                             or depth < 2 or not with_scores):
+            raise ValueError("fused_assign needs depth >= 2, scores, a separate mark on the main stream and "
+                             "assign_on != 'resolve'")
+        self.fused_assign = fused_assign
         # score_alone: assign of the previous batch waits for this batch's score kernel,
         # so the HBM-bound score overlaps only the latency-bound resolve kernels
         self.score_alone = score_alone
@@ -186,6 +196,8 @@ class UmiPipeline:
                 self.s_mark.wait_stream(producer)
         if self.assign_on == "resolve":
             return self._submit_assign_on_resolve(slot, batch)
+        if self.fused_assign:
+            return self._submit_fused(slot, batch)
         if self.on_assigned is None:
             self._settle(slot, self.s_assign)
         gate_resolve = self.reuse_gate == "resolve"
@@ -319,6 +331,32 @@ class UmiPipeline:
         self.k += 1
         return slot
 
+    def _submit_fused(self, slot: _Slot, batch: D.PackedBatch):
+        # the slot's previous batch (k - depth) had its score+assign enqueued on the main
+        # stream in an earlier submit, before this mark: the main stream orders the reuse
+        if self.on_assigned is None:
+            self._settle(slot, self.main)
+        marked = self._mark(slot, batch, False)
+        while len(self.queue) >= len(self.slots) - 1:
+            self._score_assign_oldest()
+        resolved = self._resolve(slot, marked, False)
+        slot.resolved = resolved
+        self.queue.append((slot, batch, resolved))
+        self.k += 1
+        return slot
+
+    def _score_assign_oldest(self):
+        slot, batch, resolved = self.queue.popleft()
+        D.wait_for(self.main, resolved)
+        D.score_assign_packed(batch, slot.eng, slot.cid, slot.scores, self.target, self.max_hamming, None,
+                              slot.within, deferred=self.on_assigned is None, stream=self.main)
+        if self.on_assigned is not None:
+            with torch.cuda.stream(self.main):
+                self.on_assigned(slot, batch)
+        slot.assigned = self._event()
+        slot.assigned.record(self.main)
+        self.last_assigned = slot.assigned
+
     def _assign_oldest(self):
         slot, batch, resolved = self.queue.popleft()
         D.wait_for(self.s_assign, resolved)
@@ -340,7 +378,7 @@ class UmiPipeline:
         for its resolve's flags, re-runs the rounds, labels and assign in the rare
         non-converged case); the current stream then waits for it. Returns slot.cid."""
         while any(q[0] is slot for q in self.queue):
-            self._assign_oldest()
+            self._score_assign_oldest() if self.fused_assign else self._assign_oldest()
         self._settle(slot, self.s_assign if self.assign_on != "resolve" else None)
         if slot.assigned is not None:
             D.wait_for(torch.cuda.current_stream(self.main.device), slot.assigned)
@@ -352,7 +390,7 @@ class UmiPipeline:
             for slot in self.slots:
                 self._settle(slot)
         while self.queue:
-            self._assign_oldest()
+            self._score_assign_oldest() if self.fused_assign else self._assign_oldest()
         if self.assign_on != "resolve" and self.on_assigned is None:
             for slot in self.slots:
                 self._settle(slot, self.s_assign)

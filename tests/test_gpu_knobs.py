@@ -16,7 +16,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-N, L = 400_003, 12
+N, L = 1_100_007, 12  # >= 2^20 rows: the slice mark runs its segment (bucket) pass
 
 CHILD = r"""
 import sys
@@ -49,6 +49,8 @@ KNOBS = [
     ({"ROGTK_LCC_LOOP": "1"}, "separate"),
     ({"ROGTK_LOCAL8": "0"}, "separate"),
     ({"ROGTK_SLICE_BUCKETS": "0"}, "separate"),
+    ({"ROGTK_BUCKET_ROWS": "2048"}, "main"),
+    ({"ROGTK_BUCKET_ROWS": "4096"}, "main"),
     ({"ROGTK_WORD_EXC": "0"}, "separate"),
     ({"ROGTK_LABEL_BY_INDEX": "1"}, "separate"),
     ({"ROGTK_ASSIGN_GROUPS": "1", "ROGTK_ASSIGN_BLOCKS": "0"}, "separate"),

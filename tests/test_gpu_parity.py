@@ -439,6 +439,61 @@ def test_device_pipeline_vs_oracle(rg):
     assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc)
 
 
+@pytest.mark.parametrize("L,fields,ham,deferred,spec", [(12, "all", "within", False, 0), (12, "all", "within", True, 1),
+                                                        (12, None, "both", True, 0), (10, "all", "both", False, 0),
+                                                        (9, "comb", None, True, 1)])
+def test_score_assign_fused_vs_oracle(rg, L, fields, ham, deferred, spec):
+    """rogtk_umi_score_assign_packed (score + H3 ids in one pass over the codes; the L=12
+    instance and the generic one, deferred with 1 speculative round = the re-run path)
+    equals the oracle row by row."""
+    import torch
+
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+
+    n = 700_001
+    codes_h = synth.umi_codes(n, L, seed=synth.DEFAULT_SEED + L)
+    codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
+    batch = D.PackedBatch(codes, L)
+    scores = None
+    if fields == "all":
+        scores = D.alloc_scores(n, codes.device)
+    elif fields == "comb":
+        scores = {"combined_score": torch.empty(n, dtype=torch.float64, device="cuda")}
+    hd = torch.empty(n, dtype=torch.int32, device="cuda") if ham == "both" else None
+    hw = torch.empty((n + 63) // 64, dtype=torch.int64, device="cuda") if ham else None
+    target = b"ACGTACGTACGTACGT"[:L] if ham else None
+    cid = torch.full((n,), -7, dtype=torch.int32, device="cuda")
+    eng = D.ClusterEngine(L, min(n, 4 ** L), "cuda")
+    try:
+        D.set_spec_rounds(spec)
+        eng.mark_bitmap(batch)
+        eng.resolve(eng.local_bitmap, 1, 1)
+        D.score_assign_packed(batch, eng, cid, scores, target, 1, hd, hw, deferred=deferred)
+        eng.sync()
+        torch.cuda.synchronize()
+    finally:
+        D.set_spec_rounds(0)
+    col = P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L))
+    rc, _, _, _ = P().umi_cluster(col, L, 1)
+    assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc)
+    if scores is not None:
+        ref = P().umi_complexity(col)
+        for f, t in scores.items():
+            g = t.cpu().numpy()
+            r = ref[f]
+            if r.dtype == np.float64:
+                assert np.array_equal(g.view(np.uint64), r.view(np.uint64)), f
+            else:
+                assert np.array_equal(g.view(np.uint32), r), f
+    if ham:
+        rd, rw, _ = P().hamming(col, target, 1)
+        if hd is not None:
+            assert np.array_equal(hd.cpu().numpy().view(np.uint32), rd)
+        bits = np.unpackbits(hw.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+        assert np.array_equal(bits, rw)
+
+
 @pytest.mark.parametrize("shards", [2, 4, 8])
 def test_sharded_resolve_matches_single(rg, shards):
     """N-rank exchange emulated on one GPU: ids identical to the single-batch run."""
@@ -488,7 +543,7 @@ def test_full_size_c2_properties(rg):
 @pytest.mark.parametrize("depth,nb,alone", [(4, 4, False), (2, 5, False), (1, 3, False), (3, 7, False),
                                              (2, 6, True), (3, 5, True)])
 @pytest.mark.parametrize("mark", ["xcd", "fused", "sort"])
-@pytest.mark.parametrize("assign_on", ["resolve", "separate", "main", "main_mark_stream"])
+@pytest.mark.parametrize("assign_on", ["resolve", "separate", "main", "main_mark_stream", "main_fused"])
 def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assign_on):
     """rogtk_amd.pipeline (3 streams, `depth` batches in flight) == the sequential device
     path for EVERY batch (outputs copied out by the on_assigned hook before slot reuse)."""
@@ -502,9 +557,12 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assig
     seeds = [synth.DEFAULT_SEED + 17 * k for k in range(nb)]
     outs = []
     mark_stream = assign_on == "main_mark_stream"
-    if mark_stream:
+    fused = assign_on == "main_fused"
+    if mark_stream or fused:
         if mark == "fused":
-            pytest.skip("a fused mark has no stream of its own")
+            pytest.skip("a mark fused into the score kernel has no stream / pass of its own")
+        if fused and depth < 2:
+            pytest.skip("the fused score + assign needs depth >= 2")
         assign_on = "main"
 
     def grab(slot, batch):
@@ -512,7 +570,8 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assig
                      slot.scores["longest_homopolymer_run"][:n].clone()))
 
     pipe = UmiPipeline(L, n, n, "cuda", depth=depth, target=b"ACGTACGTACGT", max_distance=1, mark=mark,
-                       on_assigned=grab, score_alone=alone, assign_on=assign_on, mark_stream=mark_stream)
+                       on_assigned=grab, score_alone=alone, assign_on=assign_on, mark_stream=mark_stream,
+                       fused_assign=fused)
     keep = []
     for s in seeds:
         codes = torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda()
@@ -536,7 +595,7 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assig
                                                   ("resolve", "auto", "score_first"), ("separate", "auto", "mark_first"),
                                                   ("separate", "auto", "late_assign"),
                                                   ("main", "auto", "mark_first"), ("main", "auto", "score_first"),
-                                                  ("main", "auto", "mark_stream")])
+                                                  ("main", "auto", "mark_stream"), ("main", "auto", "fused")])
 def test_pipeline_deferred_assign(rg, depth, nb, spec, assign_on, gate, order):
     """No on_assigned hook: assigns are enqueued before their resolve's flags are checked;
     with 1 speculative round every batch needs the deferred completion (rounds + labels +
@@ -551,12 +610,15 @@ def test_pipeline_deferred_assign(rg, depth, nb, spec, assign_on, gate, order):
 
     n, L = 200_003, 12
     seeds = [synth.DEFAULT_SEED + 29 * k for k in range(nb)]
+    if order == "fused" and depth < 2:
+        pytest.skip("the fused score + assign needs depth >= 2")
     try:
         D.set_spec_rounds(spec)
         pipe = UmiPipeline(L, n, n, "cuda", depth=depth, target=b"ACGTACGTACGT", max_distance=1,
                            assign_on=assign_on, reuse_gate=gate, score_alone=depth == 2,
                            mark_first=order != "score_first" and order != "late_assign",
-                           assign_early=order != "late_assign", mark_stream=order == "mark_stream")
+                           assign_early=order != "late_assign", mark_stream=order == "mark_stream",
+                           fused_assign=order == "fused")
         keep, last = [], {}
         for k, s in enumerate(seeds):
             codes = torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda()
