@@ -205,29 +205,33 @@ __device__ __forceinline__ uint32_t pack4(uint32_t x, uint32_t& notacgt) {
     return ((c & 0xFFu) << 6) | (((c >> 8) & 0xFFu) << 4) | (((c >> 16) & 0xFFu) << 2) | (c >> 24);
 }
 
-template <int B>
-__global__ __launch_bounds__(kBlock) void k_pack_reads(const int64_t* __restrict__ offsets,
-                                                       const uint8_t* __restrict__ values,
-                                                       const uint8_t* __restrict__ validity, int64_t voff,
-                                                       int64_t n, uint64_t* __restrict__ blocks) {
-    constexpr int R = kBlock;  // rows per workgroup: a lane per row
+// R rows per workgroup, a lane per row (R threads). DIRECT: each lane stores its row's
+// block itself (16-B stores; the lanes' blocks are consecutive, so a wave covers
+// 64 * 8 * B contiguous bytes and L2 merges the lines) instead of staging the blocks in
+// LDS for one coalesced store: less LDS per workgroup, more workgroups per CU.
+template <int B, int R = kBlock, bool DIRECT = false>
+__global__ __launch_bounds__(R) void k_pack_reads(const int64_t* __restrict__ offsets,
+                                                  const uint8_t* __restrict__ values,
+                                                  const uint8_t* __restrict__ validity, int64_t voff,
+                                                  int64_t n, uint64_t* __restrict__ blocks) {
     constexpr int OS = B + 1;  // LDS stride of a row's block (odd: fewer bank conflicts)
-    __shared__ uint32_t in32[kPackInBytes / 4 + 2];
-    __shared__ uint64_t out[R * OS];
+    constexpr int kIn = kPackInBytes * R / kBlock;  // staged bytes: 160 per row
+    __shared__ uint32_t in32[kIn / 4 + 2];
+    __shared__ uint64_t out[DIRECT ? 1 : R * OS];
     __shared__ int64_t s_off[R + 1];
     const int tid = threadIdx.x;
     for (int64_t a = (int64_t)blockIdx.x * R; a < n; a += (int64_t)gridDim.x * R) {
         const int nr = (int)min<int64_t>(R, n - a);
-        for (int i = tid; i <= nr; i += kBlock) s_off[i] = offsets[a + i];
+        for (int i = tid; i <= nr; i += R) s_off[i] = offsets[a + i];
         __syncthreads();
         const int64_t b0 = s_off[0], b1 = s_off[nr];
         const int64_t a4 = b0 & ~3ll;  // dword-aligned start
-        const bool staged = b1 - a4 <= kPackInBytes;
+        const bool staged = b1 - a4 <= kIn;
         if (staged) {  // the rows' bytes, coalesced dword loads (no byte past b1 is read)
             const int64_t nw = (b1 - a4 + 3) >> 2;
             const uint32_t* src = reinterpret_cast<const uint32_t*>(values + a4);
             const int64_t full = (b1 - a4) >> 2;  // dwords entirely inside [a4, b1)
-            for (int64_t i = tid; i < nw; i += kBlock) {
+            for (int64_t i = tid; i < nw; i += R) {
                 if (i < full) {
                     in32[i] = src[i];
                 } else {  // the last partial dword, byte by byte
@@ -249,45 +253,63 @@ __global__ __launch_bounds__(kBlock) void k_pack_reads(const int64_t* __restrict
                 const int64_t bit = voff + r;
                 valid = (validity[bit >> 3] >> (bit & 7)) & 1;
             }
-            const int64_t st = s_off[tid], len = s_off[tid + 1] - st;
-            uint64_t* ob = out + tid * OS;
+            const int64_t st = s_off[tid];
+            const int len = (int)(s_off[tid + 1] - st);
             uint32_t bad = 0;
-            const int used = valid ? (int)((len + 31) >> 5) : 0;
-            const int64_t rel = st - a4;
+            const int used = valid ? (len + 31) >> 5 : 0;
+            const int rel = (int)(st - a4);
             const uint32_t sh = (uint32_t)(rel & 3) * 8;
-            for (int w = 0; w < used; ++w) {
+            // DIRECT: 16-B stores of word pairs (2k, 2k+1); word 1 waits for the meta word
+            uint64_t w1 = 0, pend = 0;
+            uint64_t* const ob = DIRECT ? blocks + r * B : out + tid * OS;
+#pragma unroll 1
+            for (int w = 0; w < B - 1; ++w) {
                 uint64_t acc = 0;
+                if (w < used) {
 #pragma unroll
-                for (int d = 0; d < 8; ++d) {
-                    const int64_t j = (int64_t)w * 32 + d * 4;  // first byte of these 4
-                    const int64_t left = len - j;                // bytes of the row from j on
-                    uint32_t x = 0;
-                    if (left > 0) {
-                        if (staged) {  // in32[q + 1] exists: the row's bytes end inside in32[.. nw]
-                            const int64_t q = (rel + j) >> 2;
-                            const uint64_t two = ((uint64_t)in32[q + 1] << 32) | in32[q];
-                            x = (uint32_t)(two >> sh);
-                        } else {
-                            for (int t = 0; t < 4; ++t)
-                                if (j + t < len) x |= (uint32_t)values[st + j + t] << (8 * t);
+                    for (int d = 0; d < 8; ++d) {
+                        const int j = w * 32 + d * 4;  // first byte of these 4
+                        const int left = len - j;      // bytes of the row from j on
+                        uint32_t x = 0;
+                        if (left > 0) {
+                            if (staged) {  // in32[q + 1] exists: the row's bytes end inside in32[.. nw]
+                                const int q = (rel + j) >> 2;
+                                const uint64_t two = ((uint64_t)in32[q + 1] << 32) | in32[q];
+                                x = (uint32_t)(two >> sh);
+                            } else {
+                                for (int t = 0; t < 4; ++t)
+                                    if (j + t < len) x |= (uint32_t)values[st + j + t] << (8 * t);
+                            }
                         }
+                        const uint32_t inmask = left >= 4 ? 0xFFFFFFFFu : left <= 0 ? 0u : (1u << (8 * left)) - 1u;
+                        x = (x & inmask) | (0x41414141u & ~inmask);  // past the end: 'A' (code 0, valid)
+                        uint32_t nb;
+                        acc = (acc << 8) | pack4(x, nb);
+                        bad |= nb;
                     }
-                    const uint32_t inmask = left >= 4 ? 0xFFFFFFFFu : left <= 0 ? 0u : (1u << (8 * left)) - 1u;
-                    x = (x & inmask) | (0x41414141u & ~inmask);  // past the end: 'A' (code 0, valid)
-                    uint32_t nb;
-                    acc = (acc << 8) | pack4(x, nb);
-                    bad |= nb;
                 }
-                ob[1 + w] = acc;
+                if (!DIRECT) {
+                    ob[1 + w] = acc;
+                } else if (w == 0) {
+                    w1 = acc;
+                } else if (w & 1) {  // block word w + 1 is even: it starts a pair
+                    pend = acc;
+                } else {
+                    *reinterpret_cast<ulonglong2*>(ob + w) = make_ulonglong2(pend, acc);
+                }
             }
-            for (int w = used; w < B - 1; ++w) ob[1 + w] = 0;
-            ob[0] = valid ? ((uint64_t)(uint32_t)len | ((uint64_t)(bad == 0) << 32)) : 0xFFFFFFFFull;
+            const uint64_t meta = valid ? ((uint64_t)(uint32_t)len | ((uint64_t)(bad == 0) << 32)) : 0xFFFFFFFFull;
+            if (DIRECT)
+                *reinterpret_cast<ulonglong2*>(ob) = make_ulonglong2(meta, w1);
+            else
+                ob[0] = meta;
         }
         __syncthreads();
-        // the workgroup's blocks in one contiguous, coalesced store
-        uint64_t* dst = blocks + a * B;
-        for (int i = tid; i < nr * B; i += kBlock) dst[i] = out[(i / B) * OS + (i % B)];
-        __syncthreads();
+        if (!DIRECT) {  // the workgroup's blocks in one contiguous, coalesced store
+            uint64_t* dst = blocks + a * B;
+            for (int i = tid; i < nr * B; i += R) dst[i] = out[(i / B) * OS + (i % B)];
+            __syncthreads();
+        }
     }
 }
 
@@ -1729,17 +1751,44 @@ int rogtk_pack_reads(const int64_t* offsets, const uint8_t* values, const uint8_
                   "pack_reads: block_words must be 8, 16 or 32 (rogtk_read_block_words)");
     if (n == 0) return ROGTK_OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const int rows_per_wg = kBlock;
-    const int g = (int)std::min<int64_t>((n + rows_per_wg - 1) / rows_per_wg, 8192);
-    if (block_words == 8)
-        hipLaunchKernelGGL(k_pack_reads<8>, dim3(g), dim3(kBlock), 0, s, offsets, values, validity, validity_offset, n,
-                           blocks);
-    else if (block_words == 16)
-        hipLaunchKernelGGL(k_pack_reads<16>, dim3(g), dim3(kBlock), 0, s, offsets, values, validity, validity_offset,
-                           n, blocks);
-    else
-        hipLaunchKernelGGL(k_pack_reads<32>, dim3(g), dim3(kBlock), 0, s, offsets, values, validity, validity_offset,
-                           n, blocks);
+    // ROGTK_PACK=0|1|2|3: 256 rows per workgroup with the blocks staged in LDS for one
+    // coalesced store (0), or stored by their lanes with 256 / 128 / 64 rows per
+    // workgroup (1 / 2 / 3). Default 3 (round 3, 100M 150-bp reads: 12.6 vs 18.8 ms;
+    // C3 86.7-91.0 vs 94.6-95.6 ms per step, interleaved): a one-wave workgroup stages
+    // 10.5 KB, so ~14 waves per CU keep loads in flight instead of 8
+    static const int variant = [] {
+        const char* e = getenv("ROGTK_PACK");
+        const int v = e ? atoi(e) : 3;
+        return v >= 0 && v <= 3 ? v : 3;
+    }();
+    const int rows_per_wg = variant <= 1 ? 256 : variant == 2 ? 128 : 64;
+    const int g = (int)std::min<int64_t>((n + rows_per_wg - 1) / rows_per_wg, (int64_t)8192 * 256 / rows_per_wg);
+#define ROGTK_PACK_LAUNCH(BW)                                                                                        \
+    switch (variant) {                                                                                              \
+        case 1:                                                                                                     \
+            hipLaunchKernelGGL((k_pack_reads<BW, 256, true>), dim3(g), dim3(256), 0, s, offsets, values, validity,   \
+                               validity_offset, n, blocks);                                                         \
+            break;                                                                                                  \
+        case 2:                                                                                                     \
+            hipLaunchKernelGGL((k_pack_reads<BW, 128, true>), dim3(g), dim3(128), 0, s, offsets, values, validity,   \
+                               validity_offset, n, blocks);                                                         \
+            break;                                                                                                  \
+        case 3:                                                                                                     \
+            hipLaunchKernelGGL((k_pack_reads<BW, 64, true>), dim3(g), dim3(64), 0, s, offsets, values, validity,     \
+                               validity_offset, n, blocks);                                                         \
+            break;                                                                                                  \
+        default:                                                                                                    \
+            hipLaunchKernelGGL((k_pack_reads<BW, 256, false>), dim3(g), dim3(256), 0, s, offsets, values, validity,  \
+                               validity_offset, n, blocks);                                                         \
+    }
+    if (block_words == 8) {
+        ROGTK_PACK_LAUNCH(8)
+    } else if (block_words == 16) {
+        ROGTK_PACK_LAUNCH(16)
+    } else {
+        ROGTK_PACK_LAUNCH(32)
+    }
+#undef ROGTK_PACK_LAUNCH
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
 }

@@ -88,3 +88,50 @@ def test_knob_matches_oracle(reference, tmp_path, knobs, assign_on):
     assert np.array_equal(z["run"].view(np.uint32), ref["longest_homopolymer_run"])
     bits = np.unpackbits(z["within"].view(np.uint8), bitorder="little")[:N].astype(bool)
     assert np.array_equal(bits, rw)
+
+
+PACK_CHILD = r"""
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, {root!r})
+from rogtk_amd import device as D
+z = np.load({src!r})
+offs = torch.from_numpy(z["offsets"]).cuda()
+vals = torch.from_numpy(z["values"]).cuda()
+valid = torch.from_numpy(z["validity"]).cuda()
+pk = D.PackedReads(offs, vals, valid, 3)
+torch.cuda.synchronize()
+np.save({path!r}, pk.blocks.cpu().numpy())
+"""
+
+
+@pytest.mark.parametrize("variant", ["0", "1", "2"])
+def test_pack_variant_blocks_identical(tmp_path, variant):
+    """rogtk_pack_reads under every ROGTK_PACK variant writes the default variant's blocks
+    bit for bit (ragged, null, N / lowercase rows, a validity offset)."""
+    import torch
+
+    from rogtk_amd import device as D
+
+    rng = np.random.default_rng(7)
+    n = 70_001
+    lens = rng.integers(0, 200, n)
+    lens[::97] = 0
+    offs = np.zeros(n + 1, np.int64)
+    offs[1:] = np.cumsum(lens)
+    vals = rng.choice(np.frombuffer(b"ACGTACGTACGTNacgt", np.uint8), int(offs[-1]))
+    vbits = rng.random(n + 3) > 0.05
+    validity = np.packbits(vbits, bitorder="little")
+    src = str(tmp_path / "col.npz")
+    np.savez(src, offsets=offs, values=vals, validity=validity)
+    ref = D.PackedReads(torch.from_numpy(offs).cuda(), torch.from_numpy(vals).cuda(),
+                        torch.from_numpy(validity).cuda(), 3)
+    torch.cuda.synchronize()
+    ref_blocks = ref.blocks.cpu().numpy()
+    path = str(tmp_path / "blocks.npy")
+    env = dict(os.environ, ROGTK_PACK=variant)
+    r = subprocess.run([sys.executable, "-c", PACK_CHILD.format(root=ROOT, src=src, path=path)], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert np.array_equal(np.load(path), ref_blocks)
