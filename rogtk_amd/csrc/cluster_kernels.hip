@@ -2348,7 +2348,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_bitmap(const uint32_t* __re
 // c % 8 under the round-robin placement (measured exact; speed only), so their repeated
 // reads of the chunk hit that XCD's L2. No sort, no scattered global stores.
 constexpr int kSliceBlock = 1024;
-constexpr int kSliceChunks = 16;   // a multiple of the 8 XCDs
+constexpr int kSliceChunks = 8;    // a multiple of the 8 XCDs (round 3: 8 vs 16 chunks 0.318-0.327 vs 0.322-0.345 ms/step)
 constexpr int kSliceLog2 = 20;     // codes per slice (LDS bits)
 constexpr int kMaxSlices = 16;     // 4^12 / 2^20
 constexpr int kBucketRows = 8192;  // rows per segment workgroup (8 per lane; default)
@@ -2542,7 +2542,18 @@ __global__ __launch_bounds__(kBlock) void k_or_partials(const uint64_t* __restri
 }
 
 // chunks of the slice mark for n rows (1 = the slices write the bitmap directly)
-inline int slice_chunks(int64_t n) { return n >= (1 << 20) ? kSliceChunks : 1; }
+// ROGTK_SLICE_CHUNKS=1|2|4|16: chunks of >= 2^20 rows (A/B; default 8). With 1 chunk the
+// slice workgroups write the bitmap directly (no partials, no OR pass: 16 workgroups,
+// measured 2x slower)
+inline int slice_chunks(int64_t n) {
+    static const int c = [] {
+        const char* e = getenv("ROGTK_SLICE_CHUNKS");
+        const int v = e ? atoi(e) : kSliceChunks;
+        return v == 1 || v == 2 || v == 4 || v == 8 || v == 16 ? v : kSliceChunks;
+    }();
+    return n >= (1 << 20) ? c : 1;
+}
+inline bool slice_segments(int64_t n) { return n >= (1 << 20); }  // the bucket pass runs
 inline int slices_of(int L) { return 1 << (2 * L - std::min(2 * L, kSliceLog2)); }
 inline int64_t seg_buckets(int64_t n, int rows = kBucketRows) { return (n + rows - 1) / rows; }
 // ROGTK_BUCKET_ROWS=2048|4096|8192: rows per bucket workgroup (256 / 512 / 1024 threads,
@@ -2602,8 +2613,8 @@ int cluster_mark_bitmap_temp(int64_t n, int L, int64_t* bytes) {
     const int64_t sort_bytes = 2 * ((nn * 4 + 255) / 256 * 256) + (int64_t)part_sort_temp(nn) + 256;
     const int64_t words = ((int64_t)1 << (2 * L)) / 64;
     int64_t slice_bytes = 0;
-    if (L <= 12 && slice_chunks(nn) > 1) {
-        slice_bytes = (int64_t)slice_chunks(nn) * words * 8;
+    if (L <= 12 && slice_segments(nn)) {
+        slice_bytes = slice_chunks(nn) > 1 ? (int64_t)slice_chunks(nn) * words * 8 : 0;
         if (slices_of(L) > 1) slice_bytes += seg_bytes(nn);
     }
     *bytes = std::max(sort_bytes, slice_bytes);
@@ -2635,10 +2646,10 @@ int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bi
         uint32_t* seglen = nullptr;
         const int brows = bucket_rows(), bcap = brows / 4;
         const int nb = (int)seg_buckets(n, brows);
-        if (chunks > 1 && slices > 1 && slices <= kMaxSlices && slice_buckets_on()) {
+        if (slice_segments(n) && slices > 1 && slices <= kMaxSlices && slice_buckets_on()) {
             // segment pass: every slice workgroup then reads only its slice's codes (the
             // chunks of all rows were read once per slice: 16x at L = 12, from L2)
-            segs = (const uint32_t*)((uint8_t*)temp + (int64_t)chunks * words * 8);
+            segs = (const uint32_t*)((uint8_t*)temp + (chunks > 1 ? (int64_t)chunks * words * 8 : 0));
             seglen = (uint32_t*)((uint8_t*)segs + (int64_t)kMaxSlices * nb * bcap * 4);
             if (brows == 2048)
                 hipLaunchKernelGGL((k_slice_bucket<2048, 256>), dim3((unsigned)nb), dim3(256), 0, s, codes, regular_bits,

@@ -51,6 +51,9 @@ KNOBS = [
     ({"ROGTK_SLICE_BUCKETS": "0"}, "separate"),
     ({"ROGTK_BUCKET_ROWS": "2048"}, "main"),
     ({"ROGTK_BUCKET_ROWS": "4096"}, "main"),
+    ({"ROGTK_SLICE_CHUNKS": "1"}, "main"),
+    ({"ROGTK_SLICE_CHUNKS": "16"}, "separate"),
+    ({"ROGTK_SLICE_CHUNKS": "2", "ROGTK_BUCKET_ROWS": "2048"}, "main"),
     ({"ROGTK_WORD_EXC": "0"}, "separate"),
     ({"ROGTK_LABEL_BY_INDEX": "1"}, "separate"),
     ({"ROGTK_ASSIGN_GROUPS": "1", "ROGTK_ASSIGN_BLOCKS": "0"}, "separate"),
