@@ -367,6 +367,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     stats = pipe.slots[0].eng.stats()
+    h3_rounds = pipe.slots[0].eng.rounds()  # global hook rounds the last resolve needed
     # Sustained run (outside the timed region): the same steps back to back for a few
     # seconds, all ranks together; reported beside `value` as a steady-state check
     sustained = None
@@ -491,6 +492,7 @@ def main():
                    "total_reads": n_total,
                    "reads_per_gpu": count, "umi_len": L, "max_distance": md,
                    "n_distinct": stats["n_distinct"], "n_clusters": stats["n_clusters"],
+                   "h3_rounds": h3_rounds,
                    "h3_global": {"uf": "one-pass union-find", "rounds": "hook+jump rounds",
                                  "rounds1f": "root-chasing hook rounds + one flatten",
                                  "edges": "one clique sweep + rounds over the crossing edges"}[args.global_mode],

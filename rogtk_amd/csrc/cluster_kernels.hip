@@ -56,6 +56,7 @@ constexpr int kMarkChunks = 256;  // row chunks of the XCD-partitioned kernels; 
 constexpr int kScanWords = 1024;  // words per scan block (4 per thread)
 constexpr int kLocal8Words = 1024;  // words per 8-position local tile (= one scan block)
 constexpr int kLocal8Cap = 8192;    // present codes an 8-position tile may hold
+constexpr int kLocal8BigCap = 16384;  // the same for the denser instance (1 workgroup per CU)
 constexpr int kMaxRounds = 64;
 constexpr int kRoundBatch = 4;
 
@@ -64,7 +65,10 @@ constexpr int kRoundBatch = 4;
 // S_EDGE_OVF: the edge list of the global phase (mode 4) overflowed its capacity.
 // S_P0: the first code position of the global phase (7, or 8 when every 4^8-code tile
 // fits the 8-position local CC), chosen on the device by the first scan
-enum StatSlot { S_NDISTINCT = 0, S_NCLUSTERS = 1, S_OVERFLOW = 2, S_ERROR = 3, S_ROUNDS = 4, S_EDGE_OVF = 5, S_P0 = 6 };
+// S_LCAP: with S_P0 = 8, which 8-position instance takes the tiles (0: <= 8192 codes per
+// tile, 1: <= 16384, e.g. the union bitmap of 2-4 ranks' 10M-read batches)
+enum StatSlot { S_NDISTINCT = 0, S_NCLUSTERS = 1, S_OVERFLOW = 2, S_ERROR = 3, S_ROUNDS = 4, S_EDGE_OVF = 5, S_P0 = 6,
+                S_LCAP = 7 };
 // stats (8 x int64), round flags (u32 per round) at byte 64, edge-list counts (u32 per
 // round, +1) after them
 constexpr int kFlagsOff = 64;
@@ -202,7 +206,8 @@ __global__ __launch_bounds__(kBlock) void k_scan_blocks(const uint32_t* __restri
                                                         int64_t nblocks, uint32_t* __restrict__ blkoff,
                                                         unsigned long long* __restrict__ stats,
                                                         int slot, int copy_slot, int zero_stats,
-                                                        int64_t per_live = 0, int p0_L = 0) {
+                                                        int64_t per_live = 0, int p0_L = 0,
+                                                        bool local8_big_on = true) {
     __shared__ uint32_t s_wave[kBlock / 64];
     __shared__ unsigned int s_max;
     if (per_live > 0) nblocks = min<int64_t>(nblocks, ((int64_t)stats[S_NDISTINCT] + per_live - 1) / per_live);
@@ -214,7 +219,11 @@ __global__ __launch_bounds__(kBlock) void k_scan_blocks(const uint32_t* __restri
         for (int64_t b = threadIdx.x; b < nblocks; b += kBlock) mx = max(mx, blksum[b]);
         atomicMax(&s_max, mx);
         __syncthreads();
-        if (threadIdx.x == 0) stats[S_P0] = (p0_L >= 8 && s_max <= (unsigned int)kLocal8Cap) ? 8 : 7;
+        if (threadIdx.x == 0) {
+            const bool big = s_max > (unsigned int)kLocal8Cap && local8_big_on;
+            stats[S_P0] = (p0_L >= 8 && s_max <= (unsigned int)(big ? kLocal8BigCap : kLocal8Cap)) ? 8 : 7;
+            stats[S_LCAP] = big ? 1 : 0;
+        }
     }
 }
 
@@ -635,6 +644,7 @@ __global__ __launch_bounds__(TW) void k_local_cc(const uint4* __restrict__ RT, i
                                                  int64_t rwords, int64_t max_distinct,
                                                  unsigned long long* __restrict__ stats) {
     if (((int)stats[S_P0] == 8 ? 8 : 7) != LP) return;  // the other tiling
+    if (LP == 8 && (int)stats[S_LCAP] != (CAP > kLocal8Cap ? 1 : 0)) return;  // the other 8-position instance
     local_cc_tile<CAP, TW, LP>((int64_t)blockIdx.x * TW, RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats);
 }
 
@@ -665,14 +675,28 @@ inline bool local8_enabled() {
     return on;
 }
 
+// ROGTK_LOCAL8_BIG=0: no 8-position instance for tiles of 8193..16384 codes (A/B)
+inline bool local8_big_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("ROGTK_LOCAL8_BIG");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // Every instance of k_local_cc (each exits early for the tiles of the others).
 inline void launch_local_cc(const uint4* RT, int64_t words, int L, uint32_t* f, uint32_t* D, uint32_t* UR,
                             uint64_t* lroot, int64_t rwords, int64_t max_distinct, unsigned long long* stats,
                             hipStream_t s) {
-    if (L >= 8 && local8_enabled())
+    if (L >= 8 && local8_enabled()) {
         hipLaunchKernelGGL((k_local_cc<kLocal8Cap, kLocal8Words, 8>),
                            dim3((unsigned)((words + kLocal8Words - 1) / kLocal8Words)), dim3(kLocal8Words), 0, s, RT,
                            words, L, f, D, UR, lroot, rwords, max_distinct, stats);
+        if (local8_big_enabled())
+            hipLaunchKernelGGL((k_local_cc<kLocal8BigCap, kLocal8Words, 8>),
+                               dim3((unsigned)((words + kLocal8Words - 1) / kLocal8Words)), dim3(kLocal8Words), 0, s,
+                               RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats);
+    }
     const int64_t lblocks = (words + kLocalWords - 1) / kLocalWords;
     // ROGTK_LCC_LOOP=1: the 7-position instance as a grid-stride loop over 2 workgroups per
     // CU (A/B; measured slower in the pipeline: 0.383 / 0.407 vs 0.366 / 0.383 ms/step)
@@ -1713,6 +1737,10 @@ namespace {
 
 constexpr int kSpecRounds = 4;  // speculative global rounds (synth-v1 needs 3-4)
 std::atomic<int> g_spec_rounds{kSpecRounds};
+// rogtk_cluster_set_spec_rounds(0) (the default): a workspace whose previous resolve needed
+// more rounds than the default launches one more than that, so denser batches (e.g. the union bitmap of many
+// ranks) do not fall back to the host-synchronous completion every time
+std::atomic<bool> g_spec_adaptive{true};
 // global phase of max_distance 1: bulk-synchronous hook + jump rounds (default) or a
 // one-pass lock-free union-find. Measured on MI355X at 10M synth-v1 reads (1.08M
 // distinct, a few giant components): rounds 115 us of kernels, union-find 194 us
@@ -1753,6 +1781,7 @@ struct ResolveState {
     int mode = 0;  // global mode of the pending resolve
     bool pending = false;
     int rounds = 0;  // hook rounds the last resolve needed (the converged round included)
+    int needed = 0;  // the same, kept across launches (adaptive speculative rounds)
     bool word_labels = false;  // wpref holds word labels (max_distance 1)
     ClusterLayout cl{};
     // an assign enqueued before the flags were checked (rogtk_cluster_assign_deferred)
@@ -1900,7 +1929,7 @@ int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bi
                            p.blksum);
         hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, p.blksum, cl.blocks, p.blkoff,
                            p.stats, (int)S_NDISTINCT, max_distance == 0 ? (int)S_NCLUSTERS : -1, 1, (int64_t)0,
-                           local8_enabled() ? cl.L : 0);
+                           local8_enabled() ? cl.L : 0, local8_big_enabled());
     }
     if (phases & 1) {
         ProfScope prof(K_COMPACT, s);
@@ -1978,7 +2007,8 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
     st.cl = cl;
     st.word_labels = max_distance == 1;
     const int mode = g_global_mode.load();
-    const int spec = g_spec_rounds.load();
+    int spec = g_spec_rounds.load();
+    if (g_spec_adaptive.load() && st.needed > spec) spec = std::min(st.needed + 1, kMaxRounds);
     const bool rounds = max_distance == 1 && cl.L > kLocalPos && mode != kGlobalUnionFind;
     if (rounds && !st.hstats) {
         ROGTK_HIP_CHECK(hipHostMalloc((void**)&st.hstats, kStatsBytes + 64, hipHostMallocMapped | hipHostMallocCoherent));
@@ -2049,6 +2079,7 @@ int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone) 
             st.pending = false;
             st.deferred.on = false;
             st.rounds = z + 1;
+            st.needed = st.rounds;
             return ROGTK_OK;
         }
     }
@@ -2078,7 +2109,7 @@ int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone) 
         ROGTK_HIP_CHECK(hipStreamSynchronize(s));
         const int z = first_zero(hflags, st.launched, to);
         converged = z >= 0;
-        if (converged) st.rounds = z + 1;
+        if (converged) st.rounds = st.needed = z + 1;
         st.launched = to;
     }
     st.pending = false;
@@ -2097,6 +2128,7 @@ int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone) 
 int cluster_set_spec_rounds(int n) {
     ROGTK_REQUIRE(n >= 0 && n <= kMaxRounds, ROGTK_E_INVALID, "spec rounds %d outside 0..%d", n, kMaxRounds);
     g_spec_rounds.store(n == 0 ? kSpecRounds : n);
+    g_spec_adaptive.store(n == 0);
     return ROGTK_OK;
 }
 

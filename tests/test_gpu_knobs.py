@@ -60,6 +60,7 @@ KNOBS = [
     ({"ROGTK_ASSIGN_GROUPS": "4"}, "main"),
     ({"ROGTK_SCORE_GENERIC": "1", "ROGTK_SCORE_BLOCKS": "512"}, "main"),
     ({"ROGTK_RESOLVE_GRAPH": "1"}, "separate"),
+    ({"ROGTK_LOCAL8_BIG": "0"}, "main"),
 ]
 
 

@@ -494,6 +494,35 @@ def test_score_assign_fused_vs_oracle(rg, L, fields, ham, deferred, spec):
         assert np.array_equal(bits, rw)
 
 
+@pytest.mark.parametrize("n_codes,expect_p0", [(3_400_000, 8), (5_500_000, 7), (900_000, 8)])
+def test_dense_space_local_tilings_vs_oracle(rg, n_codes, expect_p0):
+    """Uniform random 12-bp codes at 19% / 28% / 5% density: the 8-position local CC for
+    tiles of 8193..16384 codes (the union bitmap of 2-4 ranks), the 7-position one above
+    that, the 8192-code instance below; ids equal the oracle's union-find."""
+    import torch
+
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+
+    rng = np.random.default_rng(n_codes)
+    codes_h = rng.integers(0, 4 ** 12, n_codes, dtype=np.uint32)
+    codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
+    batch = D.PackedBatch(codes, 12)
+    cid = torch.empty(n_codes, dtype=torch.int32, device="cuda")
+    eng = D.ClusterEngine(12, n_codes, "cuda")
+    eng.mark_bitmap(batch)
+    eng.resolve(eng.local_bitmap, 1, 1)
+    eng.assign(batch, cid)
+    stats = eng.stats()
+    torch.cuda.synchronize()
+    rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, 12)), 12, 1)
+    assert stats["n_clusters"] == rk
+    assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc)
+    # which tiling ran: the workspace's stats block (slot 6 = first global position)
+    p0 = int(eng.ws[48:56].cpu().numpy().view(np.int64)[0])
+    assert p0 == expect_p0
+
+
 @pytest.mark.parametrize("shards", [2, 4, 8])
 def test_sharded_resolve_matches_single(rg, shards):
     """N-rank exchange emulated on one GPU: ids identical to the single-batch run."""
