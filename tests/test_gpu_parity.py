@@ -217,12 +217,15 @@ def test_cluster_lengths(rg, L, md):
     assert np.array_equal(g[rv].astype(np.uint32), rc[rv])
 
 
-@pytest.mark.parametrize("L,n,want_p0", [(9, 20_000, 8), (9, 120_000, 7), (8, 6_000, 8), (8, 30_000, 7),
-                                          (10, 150_000, 8), (12, 200_000, 8)])
-def test_local_tiling_both_paths(rg, L, n, want_p0):
+@pytest.mark.parametrize("L,n,want_p0,want_lcap", [(9, 20_000, 8, 0), (9, 120_000, 8, 1), (9, 300_000, 7, 1),
+                                                    (8, 6_000, 8, 0), (8, 30_000, 8, 1), (8, 60_000, 7, 1),
+                                                    (10, 150_000, 8, 0), (10, 600_000, 7, 1), (12, 200_000, 8, 0)])
+def test_local_tiling_both_paths(rg, L, n, want_p0, want_lcap):
     """The local phase covers positions 0..7 (4^8-code tiles) when every tile holds at most
-    8192 distinct codes and 0..6 otherwise (decided on the device, stats[S_P0]): uniformly
-    random codes of a few densities take each path, and the ids equal the oracle."""
+    16384 distinct codes (the 8192-code instance, S_LCAP 0, or the 16384-code one, S_LCAP 1)
+    and 0..6 otherwise (decided on the device, stats[S_P0]): random codes of a few densities
+    take each path (the wanted values follow from the densest tile, checked below), and the
+    ids equal the oracle."""
     import torch
 
     from rogtk_amd import device as D
@@ -235,14 +238,18 @@ def test_local_tiling_both_paths(rg, L, n, want_p0):
     pos = rng.integers(0, L, size=n).astype(np.uint64)
     codes_h = np.where(flip, codes_h ^ (rng.integers(1, 4, size=n).astype(np.uint64) << (2 * pos)), codes_h)
     codes_h = codes_h.astype(np.uint32)
+    densest = int(np.bincount(np.unique(codes_h) >> 16).max())
+    assert (8 if densest <= 16384 else 7) == want_p0 and (1 if densest > 8192 else 0) == want_lcap
     codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
     batch = D.PackedBatch(codes, L)
     eng = D.ClusterEngine(L, min(n, 4 ** L), "cuda")
     cid = torch.empty(n, dtype=torch.int32, device="cuda")
     D.cluster_batch(eng, batch, cid, 1)
     torch.cuda.synchronize()
-    p0 = int(eng.ws[:64].view(torch.int64)[6].item())
-    assert p0 == want_p0
+    st = eng.ws[:64].view(torch.int64)
+    assert int(st[6].item()) == want_p0
+    if want_p0 == 8:
+        assert int(st[7].item()) == want_lcap
     rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L)), L, 1)
     assert eng.stats()["n_clusters"] == rk
     assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc)
