@@ -26,6 +26,8 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -365,40 +367,69 @@ std::mutex g_pin_mu;
 PinnedBuf g_pin_cache;
 
 struct Bgzf {
-    double t_read = 0, t_inflate = 0, t_move = 0;  // diagnostics (rogtk_bam_timers)
+    // diagnostics (rogtk_bam_timers), seconds on the caller's thread: t_read file reads,
+    // t_move framing of blocks + buffer moves (includes t_read), t_inflate inflating or
+    // waiting for the read-ahead thread; t_read_bg: reads overlapped with an inflate;
+    // t_ahead: busy seconds of the read-ahead thread
+    double t_read = 0, t_inflate = 0, t_move = 0, t_ahead = 0, t_read_bg = 0;
     FILE* f = nullptr;
     int threads = 1;
     bool file_eof = false;
-    std::vector<uint8_t> comp;  // compressed bytes not yet inflated
+    std::vector<uint8_t> comp;  // compressed bytes not yet inflated: [0, comp_len)
     size_t comp_len = 0;
     PinnedBuf buf;              // uncompressed stream: [pos, end)
     size_t pos = 0, end = 0;
     std::string err;
+    // compressed bytes read per step (ROGTK_BAM_CHUNK overrides, read at open: tests use
+    // small chunks to cover many read-ahead steps and buffer moves with small files)
+    size_t chunk = [] {
+        const char* e = getenv("ROGTK_BAM_CHUNK");
+        const long long v = e ? atoll(e) : 0;
+        return v >= 4096 ? (size_t)v : (size_t)(32u << 20);
+    }();
 
-    // Inflate the next chunk of whole blocks and append it after `end`. Keeps the bytes
-    // from `keep_from` on (they move to the front). Returns false at end of input.
-    bool more(size_t keep_from, size_t chunk = 32u << 20) {
-        if (!err.empty()) return false;
-        // read compressed bytes
-        double t0 = now_s();
-        if (!file_eof) {
-            if (comp.size() < comp_len + chunk) comp.resize(comp_len + chunk);
-            const size_t got = fread(comp.data() + comp_len, 1, chunk, f);
-            comp_len += got;
-            if (got < chunk) file_eof = true;
-        }
-        t_read += now_s() - t0;
-        // frame whole BGZF blocks
-        struct Blk {
-            size_t c0, clen, out;
-            uint32_t isize;
-        };
-        std::vector<Blk> blks;
-        size_t o = 0, total = 0;
+    // Read-ahead (ROGTK_BAM_READAHEAD=0: off). While the caller frames, decodes and uses
+    // a batch, one thread keeps reading and inflating whole chunks into buf behind `end`
+    // ([end, ahead_end)) until the buffer is full or the file ends; the caller takes what
+    // has arrived and joins the thread only to compact the buffer. While it runs, only
+    // the thread touches comp / comp_len / file_eof / f and the bytes past `end`; the
+    // caller reads [pos, end) and moves pos.
+    bool readahead = [] {
+        const char* e = getenv("ROGTK_BAM_READAHEAD");
+        return !(e && e[0] == '0');
+    }();
+    std::thread ahead;
+    bool ahead_on = false;
+    std::mutex ahead_mu;
+    std::condition_variable ahead_cv;
+    size_t ahead_end = 0;     // guarded by ahead_mu
+    bool ahead_done = false;  // guarded by ahead_mu
+    std::string ahead_err;    // set by the thread, read after join
+
+    struct Blk {
+        size_t c0, clen, out;
+        uint32_t isize;
+    };
+
+    ~Bgzf() { stop_ahead(); }
+
+    void read_comp() {
+        if (file_eof) return;
+        if (comp.size() < comp_len + chunk) comp.resize(comp_len + chunk);
+        const size_t got = fread(comp.data() + comp_len, 1, chunk, f);
+        comp_len += got;
+        if (got < chunk) file_eof = true;
+    }
+
+    // Frame the whole BGZF blocks at the start of comp. false + e set on a malformed block.
+    static bool frame(const std::vector<uint8_t>& comp, size_t comp_len, std::vector<Blk>& blks, size_t& o,
+                      size_t& total, std::string& e) {
+        blks.clear();
+        o = total = 0;
         while (o + 18 <= comp_len) {
             const uint8_t* h = comp.data() + o;
             if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) {
-                err = "not a BGZF file (bad gzip block header)";
+                e = "not a BGZF file (bad gzip block header)";
                 return false;
             }
             const size_t xlen = h[10] | (h[11] << 8);
@@ -411,7 +442,7 @@ struct Bgzf {
                 x += 4 + slen;
             }
             if (bsize == 0) {
-                err = "BGZF block without a BC (BSIZE) subfield";
+                e = "BGZF block without a BC (BSIZE) subfield";
                 return false;
             }
             if (o + bsize > comp_len) break;
@@ -419,13 +450,145 @@ struct Bgzf {
             const uint32_t isize = t[0] | (t[1] << 8) | (t[2] << 16) | ((uint32_t)t[3] << 24);
             const size_t c0 = o + 12 + xlen;
             if (bsize < 12 + xlen + 8) {
-                err = "corrupt BGZF block (BSIZE too small)";
+                e = "corrupt BGZF block (BSIZE too small)";
                 return false;
             }
             blks.push_back({c0, bsize - 12 - xlen - 8, total, isize});
             total += isize;
             o += bsize;
         }
+        return true;
+    }
+
+    // Inflate blks (framed from comp) into dst on `threads` threads. The calling thread
+    // reads the next compressed chunk meanwhile (past comp_len: room is made first, so
+    // no worker's input moves), then drops the consumed [0, o) from comp.
+    bool inflate_blocks(const std::vector<Blk>& blks, size_t o, uint8_t* dst, std::string& e, double* t_rd) {
+        std::atomic<size_t> next{0};
+        std::atomic<bool> bad{false};
+        auto work = [&] {
+            z_stream zs;
+            memset(&zs, 0, sizeof zs);
+            if (inflateInit2(&zs, -15) != Z_OK) {
+                bad = true;
+                return;
+            }
+            for (size_t b; (b = next.fetch_add(1)) < blks.size();) {
+                const Blk& k = blks[b];
+                inflateReset(&zs);
+                zs.next_in = comp.data() + k.c0;
+                zs.avail_in = (uInt)k.clen;
+                zs.next_out = dst + k.out;
+                zs.avail_out = k.isize;
+                const int rc = ::inflate(&zs, Z_FINISH);
+                if (rc != Z_STREAM_END || zs.avail_out != 0) bad = true;
+            }
+            inflateEnd(&zs);
+        };
+        const bool read_next = !file_eof && comp_len - o < chunk;
+        if (read_next && comp.size() < comp_len + chunk) comp.resize(comp_len + chunk);
+        const int nt = (int)std::min<size_t>((size_t)std::max(threads, 1), blks.size());
+        std::vector<std::thread> th;
+        for (int t = (read_next ? 0 : 1); t < nt; ++t) th.emplace_back(work);
+        if (read_next) {
+            const double t0 = now_s();
+            read_comp();
+            *t_rd += now_s() - t0;
+        }
+        work();
+        for (auto& t : th) t.join();
+        if (bad) {
+            e = "BGZF inflate failed (corrupt deflate stream)";
+            return false;
+        }
+        memmove(comp.data(), comp.data() + o, comp_len - o);
+        comp_len -= o;
+        return true;
+    }
+
+    void start_ahead() {
+        if (!readahead || ahead_on || !err.empty() || (file_eof && comp_len == 0)) return;
+        ahead_end = end;
+        ahead_done = false;
+        ahead_on = true;
+        ahead = std::thread([this, e0 = end] {
+            const double t0 = now_s();
+            double t_rd = 0;
+            std::vector<Blk> blks;
+            size_t e = e0;
+            std::string er;
+            for (;;) {
+                if (comp_len < chunk && !file_eof) read_comp();
+                size_t o = 0, total = 0;
+                if (!frame(comp, comp_len, blks, o, total, er)) break;
+                if (blks.empty()) {  // end of input, or a block longer than what is buffered
+                    if (file_eof) break;
+                    read_comp();
+                    continue;
+                }
+                if (e + total > buf.cap) break;
+                if (!inflate_blocks(blks, o, buf.p + e, er, &t_rd)) break;
+                e += total;
+                std::lock_guard<std::mutex> lk(ahead_mu);
+                ahead_end = e;
+                ahead_cv.notify_all();
+            }
+            std::lock_guard<std::mutex> lk(ahead_mu);
+            ahead_err = er;
+            ahead_done = true;
+            t_ahead += now_s() - t0;
+            ahead_cv.notify_all();
+        });
+    }
+
+    void stop_ahead() {
+        if (!ahead_on) return;
+        ahead.join();
+        ahead_on = false;
+        end = std::max(end, ahead_end);
+        if (err.empty() && !ahead_err.empty()) err = ahead_err;
+        ahead_err.clear();
+    }
+
+    // Make more bytes available after `end`, keeping the bytes from `keep_from` on (they
+    // may move to the front). Returns false at end of input or on error.
+    bool more(size_t keep_from) {
+        if (!err.empty()) return false;
+        if (ahead_on) {
+            const double t0 = now_s();
+            bool done;
+            size_t ae;
+            {
+                std::unique_lock<std::mutex> lk(ahead_mu);
+                ahead_cv.wait(lk, [&] { return ahead_done || ahead_end > end; });
+                done = ahead_done;
+                ae = ahead_end;
+            }
+            t_inflate += now_s() - t0;
+            if (!done) {  // the thread carries on behind the new end
+                end = ae;
+                return true;
+            }
+            const size_t before = end;
+            stop_ahead();
+            if (!err.empty()) return false;
+            if (end > before) {
+                start_ahead();
+                return true;
+            }
+            // the thread stopped with nothing new: buffer full (or end of input); go on here
+        }
+        // read compressed bytes
+        double t0 = now_s();
+        if (comp_len < chunk) read_comp();
+        std::vector<Blk> blks;
+        size_t o = 0, total = 0;
+        for (;;) {
+            if (!frame(comp, comp_len, blks, o, total, err)) return false;
+            if (!blks.empty() || file_eof) break;
+            read_comp();  // a block longer than what is buffered (small ROGTK_BAM_CHUNK)
+        }
+        t_read += now_s() - t0;
         if (blks.empty()) {
             if (file_eof && comp_len > 0) err = "truncated BGZF block at end of file";
             return false;
@@ -454,42 +617,10 @@ struct Bgzf {
         // inflate blocks in parallel
         const double t1 = now_s();
         t_move += t1 - t0;
-        std::atomic<size_t> next{0};
-        std::atomic<bool> bad{false};
-        uint8_t* dst = buf.p + end;
-        auto work = [&] {
-            z_stream zs;
-            memset(&zs, 0, sizeof zs);
-            if (inflateInit2(&zs, -15) != Z_OK) {
-                bad = true;
-                return;
-            }
-            for (size_t b; (b = next.fetch_add(1)) < blks.size();) {
-                const Blk& k = blks[b];
-                inflateReset(&zs);
-                zs.next_in = comp.data() + k.c0;
-                zs.avail_in = (uInt)k.clen;
-                zs.next_out = dst + k.out;
-                zs.avail_out = k.isize;
-                const int rc = inflate(&zs, Z_FINISH);
-                if (rc != Z_STREAM_END || zs.avail_out != 0) bad = true;
-            }
-            inflateEnd(&zs);
-        };
-        const int nt = (int)std::min<size_t>((size_t)std::max(threads, 1), blks.size());
-        std::vector<std::thread> th;
-        for (int t = 1; t < nt; ++t) th.emplace_back(work);
-        work();
-        for (auto& t : th) t.join();
-        if (bad) {
-            err = "BGZF inflate failed (corrupt deflate stream)";
-            return false;
-        }
+        if (!inflate_blocks(blks, o, buf.p + end, err, &t_read_bg)) return false;
         t_inflate += now_s() - t1;
         end += total;
-        // keep the partial trailing block
-        memmove(comp.data(), comp.data() + o, comp_len - o);
-        comp_len -= o;
+        start_ahead();
         return true;
     }
     // at least n bytes available from pos + rel (compacting [pos, end) to the front)
@@ -516,6 +647,7 @@ struct BamReader {
     // host outputs (pinned)
     PinnedBuf h_off[4], h_val[4], h_valid[5], h_u32[3];
     ~BamReader() {
+        z.stop_ahead();  // the read-ahead thread uses the file and the stream buffer
         if (z.f) fclose(z.f);
         {
             std::lock_guard<std::mutex> lk(g_pin_mu);

@@ -174,6 +174,27 @@ def test_synth_bam_umis_and_large_batches(tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("readahead", ["1", "0"])
+@pytest.mark.parametrize("chunk", ["4096", "70000", "1000000"])
+def test_bgzf_readahead_and_chunks(edge_bam, tmp_path, monkeypatch, readahead, chunk):
+    """The BGZF read-ahead thread (default) and the synchronous path give the oracle's
+    records for every compressed chunk size: chunks smaller than one block (4096), a few
+    blocks per chunk (many read-ahead steps and buffer moves per batch) and whole files."""
+    from rogtk_amd.bam import BamReader, iter_bam_batches
+    monkeypatch.setenv("ROGTK_BAM_READAHEAD", readahead)
+    monkeypatch.setenv("ROGTK_BAM_CHUNK", chunk)
+    p = str(tmp_path / "s.bam")
+    synth_bam.synth_bam(p, 40_000, level=1)
+    for path, mode, batch in ((p, "htslib", 7_000), (edge_bam, "noodles", 333)):
+        ref = _expect(pybam.bam_rows(path, mode), True, True)
+        got = _rows_of(iter_bam_batches(path, batch, mode=mode), mode)
+        assert len(got) == len(ref)
+        assert got == ref
+    with BamReader(p, n_threads=3) as r:  # a reader closed mid-file joins its read-ahead thread
+        assert r.next_batch(100, "htslib").num_rows == 100
+
+
+@pytest.mark.gpu
 def test_converters_write_the_reference_schema(edge_bam, tmp_path):
     import pyarrow.parquet as pq
     from rogtk_amd import bam as B
