@@ -111,6 +111,9 @@ def parse():
     ap.add_argument("--torch-events", action="store_true",
                     help="cross-stream hand-offs through torch events (system-scope release) instead of the "
                          "library's device-scope StreamEvents")
+    ap.add_argument("--mark-parts", action="store_true",
+                    help="leave the mark's per-chunk partial bitmaps unmerged; the resolve's scan ORs them "
+                         "(one kernel fewer on the main stream; measured slower)")
     ap.add_argument("--late-assign", action="store_true",
                     help="host order: enqueue batch k-1's assign after batch k's resolve (round-2 default)")
     return ap.parse_args()
@@ -313,7 +316,7 @@ def main():
                        split_resolve=args.split_resolve, reuse_gate=args.reuse_gate,
                        assign_early=not args.late_assign, mark_first=False if args.score_first else "auto",
                        device_events=not args.torch_events, mark_stream=args.mark_stream,
-                       fused_assign=args.fused_assign)
+                       fused_assign=args.fused_assign, mark_parts=args.mark_parts)
 
     def step():
         pipe.submit(batch)

@@ -224,6 +224,15 @@ int rogtk_cluster_mark_bitmap_temp_bytes(int64_t n, int umi_len, int64_t* bytes)
 int rogtk_cluster_set_mark_method(int method);
 int rogtk_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
                               uint64_t* bitmap_out, void* temp, int64_t temp_bytes, void* stream);
+/* The same, except that where the code-slice method would merge per-chunk partial
+ * bitmaps in a last pass, it stops before that pass: *n_parts partial bitmaps of
+ * rogtk_cluster_bitmap_words() words each then lie at the start of temp, and their OR is
+ * the presence bitmap (rogtk_cluster_resolve takes them as its n_bitmaps bitmaps and ORs
+ * them while it scans, so the merge costs no pass and no kernel boundary of its own).
+ * *n_parts = 0: the bitmap is in bitmap_out, as with rogtk_cluster_mark_bitmap. */
+int rogtk_cluster_mark_bitmap_parts(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
+                                    uint64_t* bitmap_out, void* temp, int64_t temp_bytes, int* n_parts,
+                                    void* stream);
 /* Global phase of max_distance 1 (positions 7..L-1), process-wide: 2 = bulk-synchronous
  * hook + jump rounds with speculative launch and deferred completion (default; 0
  * restores it), 1 = one-pass lock-free CAS union-find, 3 = hook rounds that chase

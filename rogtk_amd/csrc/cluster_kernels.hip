@@ -153,14 +153,18 @@ __global__ __launch_bounds__(kBlock) void k_scan_words(const uint64_t* __restric
     const int64_t w0 = (int64_t)blockIdx.x * kScanWords + 4 * threadIdx.x;
     uint32_t c[4];
     uint32_t tsum = 0;
+    uint64_t v[4] = {0, 0, 0, 0};
+    for (int r = 0; r < n_bitmaps; ++r) {  // the 4 words of a bitmap loaded together
+        const uint64_t* b = bitmaps + (int64_t)r * words;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (w0 + k < live) v[k] |= b[w0 + k];
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int64_t w = w0 + k;
-        uint64_t v = 0;
-        if (w < live)
-            for (int r = 0; r < n_bitmaps; ++r) v |= bitmaps[(int64_t)r * words + w];
-        if (G && w < words) G[w] = v;
-        c[k] = (uint32_t)__popcll(v);
+        if (G && w < words) G[w] = v[k];
+        c[k] = (uint32_t)__popcll(v[k]);
         tsum += c[k];
     }
     uint32_t total;
@@ -238,6 +242,157 @@ __global__ __launch_bounds__(kBlock) void k_rt(const uint64_t* __restrict__ G, i
     if (w < zero_words) zero[w] = 0;
     const uint64_t m = G[w];
     RT[w] = make_uint4((uint32_t)m, (uint32_t)(m >> 32), blkoff[w / kScanWords] + wpref[w], 0u);
+}
+
+// ---- single-pass scan (decoupled look-back): k_scan_words + k_scan_blocks + k_rt in one
+// launch, two kernel boundaries fewer on the resolve chain. Block b publishes its popcount
+// total in lb[b] (tag << 34 | status << 32 | value; status 1 = aggregate, 2 = inclusive
+// prefix), then wave 0 reads the predecessors 64 at a time, newest first, until one holds
+// an inclusive prefix. Status and value share one 64-bit word, so relaxed device-scope
+// atomics suffice (no release / acquire fences: on gfx950 those write back / invalidate
+// the whole L2, which the kernels running beside the resolve share). Workgroups are
+// dispatched in order, so every predecessor is resident or done: the waits end. The tag
+// (per workspace, new for every launch) makes flags of earlier launches invalid without a
+// clearing pass; a wait that never ends (it cannot, short of a bug) gives up after ~4M
+// polls and flags the launch's error word instead of hanging the queue.
+constexpr uint64_t kLbAgg = 1, kLbIncl = 2;
+constexpr int kLbMaxPolls = 1 << 22;
+
+__device__ __forceinline__ uint64_t lb_word(uint32_t tag, uint64_t status, uint32_t v) {
+    return ((uint64_t)tag << 34) | (status << 32) | v;
+}
+
+// Exclusive prefix of `total` over blocks 0..blockIdx.x-1 (every thread of the block gets
+// it). A wait that gives up stores the tag into lb[gridDim.x] (the launch's error word).
+__device__ uint32_t lookback_excl(uint64_t* lb, uint32_t tag, uint32_t total, uint32_t* s_x) {
+    const int b = blockIdx.x;
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        if (b == 0) {
+            if (lane == 0) {
+                __hip_atomic_store(&lb[0], lb_word(tag, kLbIncl, total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                *s_x = 0;
+            }
+        } else {
+            if (lane == 0)
+                __hip_atomic_store(&lb[b], lb_word(tag, kLbAgg, total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t excl = 0;
+            int j = b - 1;
+            for (int polls = 0;; ++polls) {
+                const int idx = j - lane;
+                const uint64_t f = idx >= 0 ? __hip_atomic_load(&lb[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                            : lb_word(tag, kLbIncl, 0);
+                const uint64_t st = (f >> 32) & 3;
+                const bool ready = (uint32_t)(f >> 34) == tag && st != 0;
+                const uint64_t incl = __ballot(ready && st == kLbIncl);
+                const int fi = incl ? __ffsll((unsigned long long)incl) - 1 : 63;  // lanes 0..fi are needed
+                const uint64_t need = fi == 63 ? ~0ull : ((2ull << fi) - 1);
+                if (__ballot(!ready) & need) {
+                    if (polls >= kLbMaxPolls) {
+                        if (lane == 0)
+                            __hip_atomic_store(&lb[gridDim.x], (uint64_t)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                uint32_t v = lane <= fi ? (uint32_t)f : 0u;
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+                excl += v;
+                if (incl) break;
+                j -= 64;
+            }
+            if (lane == 0) {
+                __hip_atomic_store(&lb[b], lb_word(tag, kLbIncl, excl + total), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                *s_x = excl;
+            }
+        }
+    }
+    __syncthreads();
+    return *s_x;
+}
+
+// OR of n_bitmaps shard bitmaps -> RT[w] = {word, rank of its first code} directly (no G,
+// in-block prefixes or block offsets in HBM); lroot's first zero_words words zeroed. The
+// last block clears the stats block and writes n_distinct (slot, copy_slot) and the local
+// tiling choice (as k_scan_blocks with p0_L).
+__global__ __launch_bounds__(kBlock) void k_scan_rt(const uint64_t* __restrict__ bitmaps, int n_bitmaps,
+                                                    int64_t words, uint4* __restrict__ RT,
+                                                    uint64_t* __restrict__ zero, int64_t zero_words,
+                                                    uint64_t* agg, uint64_t* lb, uint32_t tag,
+                                                    unsigned long long* __restrict__ stats, int slot, int copy_slot,
+                                                    int p0_L, bool local8_big_on) {
+    __shared__ uint32_t s_wave[kBlock / 64];
+    __shared__ uint32_t s_x;
+    __shared__ unsigned int s_max;
+    const int64_t w0 = (int64_t)blockIdx.x * kScanWords + 4 * threadIdx.x;
+    uint64_t v[4] = {0, 0, 0, 0};
+    if (w0 + 4 <= words) {  // a thread's 4 words: two 16-byte loads per bitmap, all in flight
+        for (int r = 0; r < n_bitmaps; ++r) {
+            const uint4* bm = reinterpret_cast<const uint4*>(bitmaps + (int64_t)r * words + w0);
+            const uint4 x = bm[0], y = bm[1];
+            v[0] |= x.x | ((uint64_t)x.y << 32);
+            v[1] |= x.z | ((uint64_t)x.w << 32);
+            v[2] |= y.x | ((uint64_t)y.y << 32);
+            v[3] |= y.z | ((uint64_t)y.w << 32);
+        }
+    } else {
+        for (int r = 0; r < n_bitmaps; ++r)
+            for (int k = 0; k < 4; ++k)
+                if (w0 + k < words) v[k] |= bitmaps[(int64_t)r * words + w0 + k];
+    }
+    uint32_t c[4], tsum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        c[k] = (uint32_t)__popcll(v[k]);
+        tsum += c[k];
+        if (w0 + k < zero_words) zero[w0 + k] = 0;
+    }
+    uint32_t total;
+    uint32_t ex = block_excl_scan(tsum, s_wave, total);
+    if (threadIdx.x == 0)  // the block's total, tagged, for the last block's maximum
+        __hip_atomic_store(&agg[blockIdx.x], ((uint64_t)tag << 32) | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ex += lookback_excl(lb, tag, total, &s_x);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t w = w0 + k;
+        if (w < words) RT[w] = make_uint4((uint32_t)v[k], (uint32_t)(v[k] >> 32), ex, 0u);
+        ex += c[k];
+    }
+    if (blockIdx.x != gridDim.x - 1) return;
+    // the last block: every predecessor published (its inclusive prefix needed them all)
+    const uint32_t n_distinct = s_x + total;
+    if (threadIdx.x == 0) s_max = 0;
+    __syncthreads();
+    unsigned int mx = 0;
+    for (int64_t b = threadIdx.x; b < gridDim.x; b += kBlock) {
+        uint64_t a = __hip_atomic_load(&agg[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int polls = 0; (uint32_t)(a >> 32) != tag && polls < kLbMaxPolls; ++polls) {
+            __builtin_amdgcn_s_sleep(1);
+            a = __hip_atomic_load(&agg[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if ((uint32_t)(a >> 32) != tag)
+            __hip_atomic_store(&lb[gridDim.x], (uint64_t)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mx = max(mx, (unsigned int)a);
+    }
+    atomicMax(&s_max, mx);
+    __syncthreads();
+    const bool err = __hip_atomic_load(&lb[gridDim.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tag;
+    __syncthreads();
+    if (threadIdx.x < kStatsBytes / 8) stats[threadIdx.x] = 0;  // stats + round flags
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        stats[slot] = n_distinct;
+        if (copy_slot >= 0) stats[copy_slot] = n_distinct;
+        if (err) stats[S_ERROR] = 1;
+        if (p0_L > 0) {
+            const bool big = s_max > (unsigned int)kLocal8Cap && local8_big_on;
+            stats[S_P0] = (p0_L >= 8 && s_max <= (unsigned int)(big ? kLocal8BigCap : kLocal8Cap)) ? 8 : 7;
+            stats[S_LCAP] = big ? 1 : 0;
+        }
+    }
 }
 
 // D[rank] = code (the sorted distinct UMIs) and f[rank] = rank. Lane per code: the
@@ -642,9 +797,10 @@ __global__ __launch_bounds__(TW) void k_local_cc(const uint4* __restrict__ RT, i
                                                  uint32_t* __restrict__ f, uint32_t* __restrict__ D,
                                                  uint32_t* __restrict__ UR, uint64_t* __restrict__ lroot,
                                                  int64_t rwords, int64_t max_distinct,
-                                                 unsigned long long* __restrict__ stats) {
+                                                 unsigned long long* __restrict__ stats, bool any_cap = false) {
     if (((int)stats[S_P0] == 8 ? 8 : 7) != LP) return;  // the other tiling
-    if (LP == 8 && (int)stats[S_LCAP] != (CAP > kLocal8Cap ? 1 : 0)) return;  // the other 8-position instance
+    // the other 8-position instance (any_cap: this one was launched alone)
+    if (LP == 8 && !any_cap && (int)stats[S_LCAP] != (CAP > kLocal8Cap ? 1 : 0)) return;
     local_cc_tile<CAP, TW, LP>((int64_t)blockIdx.x * TW, RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats);
 }
 
@@ -684,11 +840,37 @@ inline bool local8_big_enabled() {
     return on;
 }
 
+// ROGTK_LOCAL8_SINGLE=1: when the 8-position tiles fit the chip at once, only the
+// 16384-code instance is launched (A/B; measured neutral to slower: 0.320-0.327 vs
+// 0.315-0.324 ms/step, profiles/r03z_resolve_ab.txt: its larger LDS keeps workgroups of
+// the concurrent score kernel off those CUs)
+inline bool local8_single_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("ROGTK_LOCAL8_SINGLE");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 // Every instance of k_local_cc (each exits early for the tiles of the others).
 inline void launch_local_cc(const uint4* RT, int64_t words, int L, uint32_t* f, uint32_t* D, uint32_t* UR,
                             uint64_t* lroot, int64_t rwords, int64_t max_distinct, unsigned long long* stats,
                             hipStream_t s) {
-    if (L >= 8 && local8_enabled()) {
+    // Tiles of the 8-position instances; ROGTK_LOCAL8_SINGLE=1: when they all fit on the
+    // chip at once (one workgroup per CU, e.g. 256 tiles at L = 12) the 16384-code
+    // instance alone takes every 8-position batch, saving one empty launch
+    const int64_t tiles8 = (words + kLocal8Words - 1) / kLocal8Words;
+    static const int64_t n_cus = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return (int64_t)cus;
+    }();
+    if (L >= 8 && local8_enabled() && local8_big_enabled() && tiles8 <= n_cus && local8_single_enabled()) {
+        hipLaunchKernelGGL((k_local_cc<kLocal8BigCap, kLocal8Words, 8>), dim3((unsigned)tiles8), dim3(kLocal8Words),
+                           0, s, RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats, true);
+    } else if (L >= 8 && local8_enabled()) {
         hipLaunchKernelGGL((k_local_cc<kLocal8Cap, kLocal8Words, 8>),
                            dim3((unsigned)((words + kLocal8Words - 1) / kLocal8Words)), dim3(kLocal8Words), 0, s, RT,
                            words, L, f, D, UR, lroot, rwords, max_distinct, stats);
@@ -1341,6 +1523,78 @@ __global__ __launch_bounds__(kBlock) void k_roots_scan(const uint32_t* __restric
     }
 }
 
+// k_roots_scan + the block-offset scan (k_scan_blocks) in one launch: after its in-block
+// prefix each workgroup takes its offset by the decoupled look-back of k_scan_rt (relaxed
+// device-scope atomics, tagged flags in lb), so rblkoff is written here and the last
+// workgroup writes the cluster count. One kernel boundary fewer on the resolve chain.
+__global__ __launch_bounds__(kBlock) void k_roots_scan_lb(const uint32_t* __restrict__ f,
+                                                          const uint64_t* __restrict__ lroot, int64_t max_distinct,
+                                                          int64_t rwords, uint64_t* __restrict__ rbits,
+                                                          uint32_t* __restrict__ rpref, uint32_t* __restrict__ rblkoff,
+                                                          unsigned long long* stats, unsigned long long* host,
+                                                          unsigned long long* epoch, uint64_t* lb, uint32_t tag) {
+    __shared__ uint32_t s_cnt[kRootWords];
+    __shared__ uint32_t s_total, s_x;
+    if (host && blockIdx.x == 0) {
+        for (int k = threadIdx.x; k < kStatsBytes / 8; k += kBlock)
+            __hip_atomic_store(host + k, stats[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned long long e = *epoch + 1;  // one publish per resolve: no race
+            *epoch = e;
+            __hip_atomic_store(host + kStatsBytes / 8, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    const int64_t nd = live_distinct(stats, max_distinct);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int kPerWave = kRootWords / (kBlock / 64);  // 16
+    const int64_t w0 = (int64_t)blockIdx.x * kRootWords + wave * kPerWave;
+    uint32_t fv[kPerWave];
+    uint64_t lr[kPerWave];
+#pragma unroll
+    for (int k = 0; k < kPerWave; ++k) {
+        const int64_t i = (w0 + k) * 64 + lane;
+        lr[k] = (w0 + k) * 64 < nd ? lroot[w0 + k] : 0ull;
+        fv[k] = i < nd ? f[i] : 0u;
+    }
+    uint64_t mine = 0;
+#pragma unroll
+    for (int k = 0; k < kPerWave; ++k) {
+        const int64_t i = (w0 + k) * 64 + lane;
+        const uint64_t m = __ballot(i < nd && ((lr[k] >> lane) & 1ull) && fv[k] == (uint32_t)i);
+        if (lane == k) mine = m;
+    }
+    if (lane < kPerWave) {
+        const int64_t w = w0 + lane;
+        if (w < rwords) rbits[w] = mine;
+        s_cnt[wave * kPerWave + lane] = (uint32_t)__popcll(mine);
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const uint32_t v = lane < kRootWords ? s_cnt[lane] : 0u;
+        uint32_t incl = v;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t t = __shfl_up(incl, off);
+            if (lane >= off) incl += t;
+        }
+        const int64_t w = (int64_t)blockIdx.x * kRootWords + lane;
+        if (lane < kRootWords && w < rwords) rpref[w] = incl - v;
+        if (lane == kRootWords - 1) s_total = incl;
+    }
+    __syncthreads();
+    const uint32_t total = s_total;
+    const uint32_t excl = lookback_excl(lb, tag, total, &s_x);
+    if (threadIdx.x == 0) {
+        rblkoff[blockIdx.x] = excl;
+        if (blockIdx.x == gridDim.x - 1) {
+            rblkoff[gridDim.x] = excl + total;
+            stats[S_NCLUSTERS] = excl + total;
+            if (__hip_atomic_load(&lb[gridDim.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tag) stats[S_ERROR] = 1;
+        }
+    }
+}
+
 __device__ __forceinline__ uint32_t root_label(uint32_t r, const uint64_t* __restrict__ rbits,
                                                const uint32_t* __restrict__ rpref,
                                                const uint32_t* __restrict__ rblkoff) {
@@ -1565,6 +1819,7 @@ struct WsPtrs {
     uint32_t *rpref, *rblksum, *rblkoff, *labelcode, *ilab, *wlab2;
     uint64_t* active;
     unsigned long long* epoch;  // resolves published (k_roots_scan)
+    uint64_t* lb;               // look-back flags of k_scan_rt (+ its error word)
     uint2* edges;             // two lists of ecap pairs
     unsigned int* ecnt;       // per-round list counts (stats block)
 };
@@ -1593,6 +1848,7 @@ inline WsPtrs ws_ptrs(const ClusterLayout& cl, uint8_t* ws) {
     p.active = (uint64_t*)(ws + cl.off_active);
     p.edges = (uint2*)(ws + cl.off_edges);
     p.epoch = (unsigned long long*)(ws + cl.off_epoch);
+    p.lb = (uint64_t*)(ws + cl.off_lb);
     p.ecnt = (unsigned int*)(ws + cl.off_stats + kEcntOff);
     return p;
 }
@@ -1669,6 +1925,8 @@ int cluster_layout(int L, int64_t max_distinct, ClusterLayout* o) {
                           : std::min<int64_t>(std::max<int64_t>(max_distinct / 2, 65536), 1ll << 25);
     c.off_edges = take(2 * std::max<int64_t>(c.ecap, 1) * 8);
     c.off_epoch = take(8);
+    // look-back flags + error word + tagged block totals (k_scan_rt)
+    c.off_lb = take((2 * std::max(c.blocks, c.rblocks) + 1) * 8);
     c.total = off;
     *o = c;
     return ROGTK_OK;
@@ -1783,6 +2041,7 @@ struct ResolveState {
     int rounds = 0;  // hook rounds the last resolve needed (the converged round included)
     int needed = 0;  // the same, kept across launches (adaptive speculative rounds)
     bool word_labels = false;  // wpref holds word labels (max_distance 1)
+    uint32_t scan_tag = 0;     // the last k_scan_rt launch's look-back tag (1..2^30-1)
     ClusterLayout cl{};
     // an assign enqueued before the flags were checked (rogtk_cluster_assign_deferred)
     struct {
@@ -1874,8 +2133,14 @@ int enqueue_post_rounds(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
 // host_stats != nullptr: k_roots_scan also publishes the stats block (the resolve's
 // first labels pass; never the re-run after extra rounds, which the host waits for)
 int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
-                   unsigned long long* host_stats = nullptr) {
-    {
+                   unsigned long long* host_stats = nullptr, uint32_t tag = 0) {
+    if (tag) {
+        ProfScope prof(K_FLATTEN, s);
+        hipLaunchKernelGGL(k_roots_scan_lb, dim3((unsigned)cl.rblocks), dim3(kBlock), 0, s, p.f, p.lroot,
+                           cl.max_distinct, cl.rwords, p.rbits, p.rpref, p.rblkoff, p.stats, host_stats, p.epoch,
+                           p.lb, tag);
+        ROGTK_HIP_CHECK(hipGetLastError());
+    } else {
         ProfScope prof(K_FLATTEN, s);
         hipLaunchKernelGGL(k_roots_scan, dim3((unsigned)cl.rblocks), dim3(kBlock), 0, s, p.f, p.lroot,
                            cl.max_distinct, cl.rwords, p.rbits, p.rpref, p.rblksum,
@@ -1919,10 +2184,44 @@ namespace {
 // Returns the number of speculative rounds launched (0: no global rounds), -1 on error.
 // phases: bit 0 = the rank tables and the local CC (a function of the bitmaps only),
 // bit 1 = the global rounds, the flags publish and the labels.
+// ROGTK_FUSED_SCAN=0: the rank tables by three kernels (scan words, scan blocks, RT)
+// instead of the single-pass k_scan_rt (A/B)
+bool fused_scan_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("ROGTK_FUSED_SCAN");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+// ROGTK_ROOTS_LB=1: the look-back k_roots_scan_lb instead of the roots scan + a separate
+// block-offset scan (A/B; measured slower: 0.332-0.341 vs 0.315-0.324 ms/step,
+// profiles/r03z_resolve_ab.txt)
+bool roots_lb_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("ROGTK_ROOTS_LB");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bitmaps, int n_bitmaps,
                     int max_distance, int mode, int spec, unsigned long long* host_stats, hipStream_t s,
-                    int phases = 3) {
-    if (phases & 1) {
+                    int phases = 3, uint32_t scan_tag = 0) {
+    if ((phases & 1) && scan_tag) {  // single pass: RT, n_distinct and the tiling in one launch
+        ProfScope prof(K_SCAN, s);
+        hipLaunchKernelGGL(k_scan_rt, dim3((unsigned)cl.blocks), dim3(kBlock), 0, s, bitmaps, n_bitmaps, cl.words,
+                           p.RT, p.lroot, max_distance == 0 ? (int64_t)0 : cl.rwords,
+                           p.lb + std::max(cl.blocks, cl.rblocks) + 1, p.lb, scan_tag,
+                           p.stats, (int)S_NDISTINCT, max_distance == 0 ? (int)S_NCLUSTERS : -1,
+                           local8_enabled() ? cl.L : 0, local8_big_enabled());
+        if (max_distance == 0) {
+            const int cgrid = grid_for((int64_t)std::min<uint64_t>(cl.nbits, 1ull << 30), 16384);
+            hipLaunchKernelGGL(k_build_d, dim3(cgrid), dim3(kBlock), 0, s, p.RT, cl.nbits, p.D, p.f, p.labelcode, p.ilab,
+                               cl.max_distinct, p.stats);
+            return hipGetLastError() == hipSuccess ? 0 : -1;  // labels = ranks (labelcode / ilab)
+        }
+    }
+    if ((phases & 1) && !scan_tag) {
         ProfScope prof(K_SCAN, s);
         hipLaunchKernelGGL(k_scan_words, dim3((unsigned)cl.blocks), dim3(kBlock), 0, s, bitmaps,
                            n_bitmaps, cl.words, (const unsigned long long*)nullptr, p.G, p.wpref,
@@ -1931,7 +2230,7 @@ int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bi
                            p.stats, (int)S_NDISTINCT, max_distance == 0 ? (int)S_NCLUSTERS : -1, 1, (int64_t)0,
                            local8_enabled() ? cl.L : 0, local8_big_enabled());
     }
-    if (phases & 1) {
+    if ((phases & 1) && !scan_tag) {
         ProfScope prof(K_COMPACT, s);
         hipLaunchKernelGGL(k_rt, dim3(grid_for(cl.words)), dim3(kBlock), 0, s, p.G, cl.words, p.wpref,
                            p.blkoff, p.RT, p.lroot, max_distance == 0 ? 0 : cl.rwords);
@@ -1965,11 +2264,11 @@ int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bi
             // k_roots_scan stores the flags into mapped host memory and then the resolve's
             // epoch (counted on the device): no copy-engine transfer, no event, no kernel
             // of its own (a D2H copy + event record cost ~15 us of the resolve chain)
-            if (enqueue_labels(cl, p, s, host_stats)) return -1;
+            if (enqueue_labels(cl, p, s, host_stats, scan_tag && roots_lb_enabled() ? scan_tag + 1 : 0u)) return -1;
             return hipGetLastError() == hipSuccess ? launched : -1;
         }
     }
-    if (enqueue_labels(cl, p, s)) return -1;
+    if (enqueue_labels(cl, p, s, nullptr, scan_tag && roots_lb_enabled() ? scan_tag + 1 : 0u)) return -1;
     return hipGetLastError() == hipSuccess ? launched : -1;
 }
 
@@ -1993,9 +2292,16 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
     if (st.pending && st.deferred.on) {  // a deferred assign must see its resolve complete first
         if (int rc = finish_locked(ws, st, s)) return rc;
     }
+    // a new look-back tag per single-pass scan (0 = the three-kernel scan)
+    // (two per resolve: k_scan_rt takes tag, k_roots_scan_lb tag + 1)
+    auto next_tag = [&]() -> uint32_t {
+        if (!fused_scan_enabled()) return 0;
+        st.scan_tag = st.scan_tag >= (1u << 30) - 2 ? 1u : st.scan_tag + 2;
+        return st.scan_tag;
+    };
     if (phases == 1) {  // the local phase alone; the global phase follows on another stream
         const int r = enqueue_resolve(cl, p, bitmaps, n_bitmaps, max_distance, g_global_mode.load(),
-                                      g_spec_rounds.load(), nullptr, s, 1);
+                                      g_spec_rounds.load(), nullptr, s, 1, next_tag());
         ROGTK_REQUIRE(r >= 0, ROGTK_E_HIP, "cluster: resolve launch failed (%s)", hipGetErrorString(hipGetLastError()));
         st.pending = false;
         st.deferred.on = false;
@@ -2016,10 +2322,11 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
         ROGTK_HIP_CHECK(hipHostGetDevicePointer((void**)&st.hstats_dev, st.hstats, 0));
     }
     unsigned long long* hs = (unsigned long long*)st.hstats_dev;
-    // The resolve is ~17 small kernels. With ROGTK_RESOLVE_GRAPH=1 the sequence (a
+    // The resolve is ~15 small kernels. With ROGTK_RESOLVE_GRAPH=1 the sequence (a
     // function of the workspace, the bitmaps pointer / count and the knobs) is captured
     // once into a hipGraph per such key and replayed with one launch (never while
-    // profiling: the per-phase events need the direct launches).
+    // profiling: the per-phase events need the direct launches). A replay cannot take a
+    // new look-back tag, so the graph holds the three-kernel scan.
     const GraphKey key{bitmaps, n_bitmaps, max_distance, mode, spec, cl.L, cl.max_distinct, cl.ecap};
     const bool graph = graphs_enabled() && !profiling_on() && phases == 3;
     int launched = 0;
@@ -2047,7 +2354,8 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
         ROGTK_HIP_CHECK(hipGraphLaunch(st.gexec, s));
         launched = st.glaunched;
     } else {
-        launched = enqueue_resolve(cl, p, bitmaps, n_bitmaps, max_distance, mode, spec, hs, s, phases);
+        launched = enqueue_resolve(cl, p, bitmaps, n_bitmaps, max_distance, mode, spec, hs, s, phases,
+                                   (phases & 1) ? next_tag() : 0u);
         ROGTK_REQUIRE(launched >= 0, ROGTK_E_HIP, "cluster: resolve launch failed (%s)",
                       hipGetErrorString(hipGetLastError()));
     }
@@ -2115,7 +2423,12 @@ int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone) 
     st.pending = false;
     ROGTK_REQUIRE(converged, ROGTK_E_HIP, "cluster: union rounds did not converge in %d rounds", kMaxRounds);
     if (int rc = enqueue_post_rounds(st.cl, p, s, st.mode)) return rc;
-    if (int rc = enqueue_labels(st.cl, p, s)) return rc;
+    uint32_t tag = 0;
+    if (fused_scan_enabled() && roots_lb_enabled()) {  // a fresh look-back tag for the relabel
+        st.scan_tag = st.scan_tag >= (1u << 30) - 2 ? 1u : st.scan_tag + 2;
+        tag = st.scan_tag;
+    }
+    if (int rc = enqueue_labels(st.cl, p, s, nullptr, tag)) return rc;
     if (st.deferred.on) {  // the assign that ran on the speculative labels, again
         st.deferred.on = false;
         return enqueue_assign(st.cl, p, st.word_labels, st.deferred.codes, st.deferred.regbits, st.deferred.n,
@@ -2654,7 +2967,8 @@ int cluster_mark_bitmap_temp(int64_t n, int L, int64_t* bytes) {
 }
 
 int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int L,
-                               uint64_t* bitmap, void* temp, int64_t temp_bytes, hipStream_t s) {
+                               uint64_t* bitmap, void* temp, int64_t temp_bytes, hipStream_t s, int* n_parts) {
+    if (n_parts) *n_parts = 0;
     int64_t need = 0;
     if (int rc = cluster_mark_bitmap_temp(n, L, &need)) return rc;
     ROGTK_REQUIRE((temp || n == 0) && temp_bytes >= need, ROGTK_E_INVALID, "temp_bytes %lld < %lld", (long long)temp_bytes,
@@ -2696,7 +3010,9 @@ int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bi
         }
         hipLaunchKernelGGL(k_slice_mark, dim3((unsigned)(slices * chunks)), dim3(kSliceBlock), 0, s, codes, regular_bits,
                            n, slog, chunks, chunk_rows, dst, words, segs, (const uint32_t*)seglen, nb, brows, bcap);
-        if (chunks > 1)
+        if (chunks > 1 && n_parts)
+            *n_parts = chunks;  // the caller's resolve ORs the partials (temp, chunk-major)
+        else if (chunks > 1)
             hipLaunchKernelGGL(k_or_partials, dim3(grid_for(words, 4096)), dim3(kBlock), 0, s, dst, chunks, words,
                                bitmap);
         ROGTK_HIP_CHECK(hipGetLastError());

@@ -214,7 +214,7 @@ struct ClusterLayout {
     // byte offsets into the workspace
     int64_t off_stats, off_presence, off_bitmap, off_rt, off_wpref, off_blksum, off_blkoff, off_D, off_f, off_ur,
         off_rbits, off_lroot, off_rpref, off_rblksum, off_rblkoff, off_wlab2, off_labelcode, off_ilab, off_active,
-        active_words, off_edges, ecap, off_epoch, total;
+        active_words, off_edges, ecap, off_epoch, off_lb, total;
 };
 int cluster_layout(int L, int64_t max_distinct, ClusterLayout* out);
 
@@ -251,7 +251,7 @@ int launch_cluster_local_bitmap(const ClusterLayout& cl, uint8_t* ws, uint64_t* 
 // presence bitmap straight from the codes by an 8-bit partition sort (7 <= L <= 13)
 int cluster_mark_bitmap_temp(int64_t n, int L, int64_t* bytes);
 int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int L,
-                               uint64_t* bitmap, void* temp, int64_t temp_bytes, hipStream_t s);
+                               uint64_t* bitmap, void* temp, int64_t temp_bytes, hipStream_t s, int* n_parts = nullptr);
 // phases: 1 = rank tables + local CC, 2 = global rounds + labels (after phase 1 of the
 // same bitmaps), 3 = both
 // The assign half of a fused score + assign: completes (deferred = false) or registers

@@ -208,15 +208,28 @@ class ClusterEngine:
         _lib.call("rogtk_cluster_mark", _p(batch.codes), _p(batch.regular_bits), batch.n, self.umi_len,
                   _p(self.ws), self.max_distinct, _s(stream))
 
-    def mark_bitmap(self, batch: PackedBatch, stream=None) -> torch.Tensor:
-        """mark + build_local_bitmap in one: partition sort + LDS bitmap (7 <= L <= 13)."""
+    def mark_bitmap(self, batch: PackedBatch, stream=None, parts: bool = False):
+        """mark + build_local_bitmap in one: code slices or partition sort + LDS bitmap
+        (7 <= L <= 13). Returns local_bitmap; with parts=True returns (bitmaps, n): the
+        per-chunk partial bitmaps in the engine's scratch when the slice method leaves them
+        unmerged (their OR is the bitmap; resolve(bitmaps, n) ORs them as it scans, valid
+        until this engine's next mark), else (local_bitmap, 1)."""
         need = ctypes.c_int64(0)
         _lib.call("rogtk_cluster_mark_bitmap_temp_bytes", batch.n, self.umi_len, ctypes.byref(need))
         if getattr(self, "_mark_temp", None) is None or self._mark_temp.numel() < need.value:
             self._mark_temp = torch.empty(need.value, dtype=torch.uint8, device=self.local_bitmap.device)
-        _lib.call("rogtk_cluster_mark_bitmap", _p(batch.codes), _p(batch.regular_bits), batch.n, self.umi_len,
-                  _p(self.local_bitmap), _p(self._mark_temp), self._mark_temp.numel(), _s(stream))
-        return self.local_bitmap
+        if not parts:
+            _lib.call("rogtk_cluster_mark_bitmap", _p(batch.codes), _p(batch.regular_bits), batch.n, self.umi_len,
+                      _p(self.local_bitmap), _p(self._mark_temp), self._mark_temp.numel(), _s(stream))
+            return self.local_bitmap
+        n_parts = ctypes.c_int(0)
+        _lib.call("rogtk_cluster_mark_bitmap_parts", _p(batch.codes), _p(batch.regular_bits), batch.n, self.umi_len,
+                  _p(self.local_bitmap), _p(self._mark_temp), self._mark_temp.numel(), ctypes.byref(n_parts),
+                  _s(stream))
+        if n_parts.value == 0:
+            return self.local_bitmap, 1
+        k = n_parts.value
+        return self._mark_temp[: k * self.words * 8].view(torch.int64), k
 
     def build_local_bitmap(self, stream=None) -> torch.Tensor:
         _lib.call("rogtk_cluster_local_bitmap", _p(self.ws), self.umi_len, self.max_distinct,

@@ -50,6 +50,7 @@ class _Slot:
         self.cid = torch.empty(max(n_max, 4), dtype=torch.int32, device=dev)
         self.assigned = None  # D.StreamEvent or torch.cuda.Event (UmiPipeline.device_events)
         self.resolved = None
+        self.parts = None  # (bitmaps, n): the batch's unmerged partial bitmaps (mark_parts)
 
 
 class UmiPipeline:
@@ -59,7 +60,7 @@ class UmiPipeline:
                  on_assigned=None, score_alone: bool = False, exchange=None, resolve_streams: int = 1,
                  assign_on: str = "main", split_resolve: bool = False, reuse_gate: str = "auto",
                  assign_early: bool = True, mark_first="auto", device_events: bool = True,
-                 mark_stream: bool = False, fused_assign: bool = False):
+                 mark_stream: bool = False, fused_assign: bool = False, mark_parts: bool = False):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
@@ -144,6 +145,14 @@ class UmiPipeline:
         # stream's chain (a substituted exchange may reuse one buffer: it stays in line)
         self.s_comm = (torch.cuda.Stream(dev) if exchange is None and not split_resolve and dist_world(group) > 1
                        else None)
+        # mark_parts (one rank, code-slice mark): the mark stops before merging its per-chunk
+        # partial bitmaps and the resolve ORs them while it scans (rogtk_cluster_mark_bitmap_parts),
+        # one kernel and one kernel boundary fewer on the main stream. Across ranks the merged
+        # bitmap is what the all-gather sends. Off by default: measured slower (round 3: the
+        # resolve chain, which then reads 8 bitmaps, is critical: 0.333-0.338 vs 0.318-0.327
+        # ms/step, profiles/r03z_mark_parts_ab.txt).
+        self.mark_parts = (mark_parts and self.sort_mark and exchange is None and not split_resolve
+                           and assign_on != "resolve" and dist_world(group) == 1)
         self.last_scored: Optional[torch.cuda.Event] = None
         self.k = 0
         self.last_assigned: Optional[torch.cuda.Event] = None
@@ -248,7 +257,10 @@ class UmiPipeline:
         ms = self.s_mark
         if (gate_resolve or ms is not self.main) and slot.resolved is not None:
             D.wait_for(ms, slot.resolved)  # the previous resolve read the bitmap
-        if self.sort_mark:
+        slot.parts = None
+        if self.mark_parts:
+            slot.parts = slot.eng.mark_bitmap(batch, stream=ms, parts=True)
+        elif self.sort_mark:
             slot.eng.mark_bitmap(batch, stream=ms)
         else:
             if not self.fused_mark:
@@ -285,6 +297,8 @@ class UmiPipeline:
                 if self.s_comm is not None:
                     D.wait_for(sr, gathered)
                     bitmaps.record_stream(sr)  # allocated on the comm stream
+                elif slot.parts is not None:
+                    bitmaps, nb = slot.parts  # the mark's scratch: rewritten only after this resolve
                 else:
                     bitmaps, nb = self.exchange(slot.eng.local_bitmap)
                 slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr)

@@ -61,6 +61,10 @@ KNOBS = [
     ({"ROGTK_SCORE_GENERIC": "1", "ROGTK_SCORE_BLOCKS": "512"}, "main"),
     ({"ROGTK_RESOLVE_GRAPH": "1"}, "separate"),
     ({"ROGTK_LOCAL8_BIG": "0"}, "main"),
+    ({"ROGTK_FUSED_SCAN": "0"}, "main"),
+    ({"ROGTK_FUSED_SCAN": "0", "ROGTK_LOCAL8": "0"}, "separate"),
+    ({"ROGTK_LOCAL8_SINGLE": "1"}, "main"),
+    ({"ROGTK_ROOTS_LB": "1"}, "separate"),
 ]
 
 

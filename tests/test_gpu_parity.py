@@ -625,6 +625,47 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assig
         assert np.array_equal(g_long, scores["longest_homopolymer_run"][:n].cpu().numpy()), k
 
 
+@pytest.mark.parametrize("mark_parts", [True, False])
+@pytest.mark.parametrize("assign_on", ["main", "separate", "main_mark_stream", "main_fused", "resolve"])
+def test_pipeline_mark_parts(rg, mark_parts, assign_on):
+    """>= 2^20 rows: the code-slice mark leaves one partial bitmap per row chunk; with
+    mark_parts (an option) the resolve ORs them while it scans instead of a merge pass.
+    Every batch's ids, scores and Hamming bits equal the sequential device path."""
+    import torch
+
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+    from rogtk_amd.pipeline import UmiPipeline
+
+    n, L, nb = 1_100_009, 12, 4
+    seeds = [synth.DEFAULT_SEED + 31 * k for k in range(nb)]
+    outs = []
+
+    def grab(slot, batch):
+        outs.append((slot.cid[:n].clone(), slot.within.clone(), slot.scores["combined_score"][:n].clone()))
+
+    mark_stream, fused = assign_on == "main_mark_stream", assign_on == "main_fused"
+    pipe = UmiPipeline(L, n, n, "cuda", depth=2, target=b"ACGTACGTACGT", max_distance=1, on_assigned=grab,
+                       assign_on="main" if mark_stream or fused else assign_on, mark_stream=mark_stream,
+                       fused_assign=fused, mark_parts=mark_parts)
+    assert pipe.mark_parts == (mark_parts and assign_on != "resolve")
+    keep = []
+    for s in seeds:
+        keep.append(D.PackedBatch(torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda(), L))
+        pipe.submit(keep[-1])
+        if pipe.mark_parts:
+            assert pipe.slots[(pipe.k - 1) % 2].parts[1] > 1  # partials, not the merged bitmap
+    pipe.drain()
+    torch.cuda.synchronize()
+    assert len(outs) == nb
+    for k in range(nb):
+        _, scores, _, hw, cid, _ = _device_run(n, seed=seeds[k])
+        g_cid, g_w, g_comb = (t.cpu().numpy() for t in outs[k])
+        assert np.array_equal(g_cid, cid.cpu().numpy()), k
+        assert np.array_equal(g_w, hw.cpu().numpy()), k
+        assert np.array_equal(g_comb.view(np.uint64), scores["combined_score"][:n].cpu().numpy().view(np.uint64)), k
+
+
 @pytest.mark.parametrize("spec", [1, 4])
 @pytest.mark.parametrize("depth,nb", [(2, 5), (3, 3), (1, 2)])
 @pytest.mark.parametrize("assign_on,gate,order", [("separate", "auto", "score_first"), ("separate", "resolve", "score_first"),
