@@ -339,7 +339,9 @@ int rogtk_umi_cluster_dev(const int64_t* offsets, const uint8_t* values, const u
  * censored Exts byte (low nibble left bases, high nibble right); counts[i] =
  * occurrences (u16, saturating). group_stats[5 g ..] = {k_eff (0 when k > 64),
  * n_sequences, node_count, terminal_count, isolated_count}.
- * capacity >= rogtk_kmer_capacity() always suffices (ROGTK_E_OVERFLOW otherwise). */
+ * capacity >= rogtk_kmer_capacity() always suffices (ROGTK_E_OVERFLOW otherwise); so does
+ * rogtk_kmer_capacity() / max(min_coverage, 1), since every valid k-mer takes at least
+ * min_coverage observations. */
 int rogtk_kmer_capacity(const void* offsets, int offset_width, int64_t n_rows, int64_t* capacity);
 /* Path selection for the calling thread (default 1): groups with <= 2048 k-mer
  * observations, rows <= 2048 bases and k_eff <= 32 run entirely in LDS (one

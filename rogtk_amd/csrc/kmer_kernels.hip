@@ -1077,11 +1077,19 @@ __global__ __launch_bounds__(kBlock) void k_drop_small_rows(const uint32_t* __re
         if (gsmall[row_group[r]]) row_obs[r] = 0;
 }
 
-// per-group capacity: sum over its rows of max(0, len - 3) (k_eff >= 4)
+// Per-group capacity: the group's k-mer observations are at most O = sum over its rows
+// of max(0, len - 3) (k_eff >= 4), and every valid k-mer takes at least min_cov of them
+// (count >= min_cov; the u16 count saturates only above that), so at most
+// O / max(min_cov, 1) entries are valid (20x less temporary and output space than O at
+// the usual floor of 20, so one call covers 100M reads)
+__device__ __host__ __forceinline__ int64_t valid_cap(int64_t obs, int64_t min_cov) {
+    return obs / (min_cov > 1 ? min_cov : 1);
+}
+
 __global__ __launch_bounds__(kBlock) void k_group_caps(const int64_t* __restrict__ offsets,
                                                        const int64_t* __restrict__ rows,
                                                        const int64_t* __restrict__ go, int64_t G,
-                                                       int64_t* __restrict__ caps) {
+                                                       int64_t* __restrict__ caps, int64_t min_cov) {
     const int lane = threadIdx.x & 63;
     const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
     for (int64_t g = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); g < G; g += waves) {
@@ -1092,7 +1100,7 @@ __global__ __launch_bounds__(kBlock) void k_group_caps(const int64_t* __restrict
             if (len >= 4) t += len - 3;
         }
         for (int m = 32; m > 0; m >>= 1) t += __shfl_xor(t, m);
-        if (lane == 0) caps[g] = t;
+        if (lane == 0) caps[g] = valid_cap(t, min_cov);
     }
 }
 
@@ -1534,7 +1542,7 @@ int rogtk_kmer_spectrum_host(const void* offsets, int offset_width, const uint8_
             const int64_t len = row_len(r);
             if (len >= 4) cap += len - 3;
         }
-        cap_off[g + 1] = cap_off[g] + cap;
+        cap_off[g + 1] = cap_off[g] + valid_cap(cap, min_coverage);
     }
     KmerCtx* c = nullptr;
     if (int rc = kmer_ctx(&c)) return rc;
@@ -1685,7 +1693,7 @@ int spectrum_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* v
     ROGTK_HIP_CHECK(hipMemsetAsync(c->gstat.p, 0, G * 5 * 8, s));
     ROGTK_HIP_CHECK(hipMemsetAsync(c->gcount.p, 0, G * 8, s));
     hipLaunchKernelGGL(k_group_caps, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, offsets, rows,
-                       group_offsets, G, c->caps.as<int64_t>());
+                       group_offsets, G, c->caps.as<int64_t>(), min_coverage);
     if (int rc = cub_exsum_i64(c, c->caps.as<int64_t>(), c->cap_off.as<int64_t>(), G, s)) return rc;
     hipLaunchKernelGGL(k_tail_sum, dim3(1), dim3(64), 0, s, c->cap_off.as<int64_t>(), c->caps.as<int64_t>(), G,
                        c->cap_off.as<int64_t>() + G);

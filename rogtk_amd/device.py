@@ -395,13 +395,14 @@ def kmer_spectrum_blocks(packed: PackedReads, offsets: torch.Tensor, values: tor
 
 
 def group_spectra(offsets: torch.Tensor, values: torch.Tensor, keys: torch.Tensor, k: int, min_coverage: int,
-                  batch_rows: int = 10_000_000, consume=None, stream=None, packed="auto"):
+                  batch_rows: int = 100_000_000, consume=None, stream=None, packed="auto"):
     """The C3 front end after H3 (rogtk/__init__.py:206-214: group_by('umi') then
     assemble per group): rows grouped by key (stable; e.g. H3 cluster ids), then k-mer
     spectra (filter_kmers + CountFilter + censored exts, fracture.rs:105-116) over runs of
     consecutive groups of at most batch_rows rows per call (a group is never split; a
     larger group gets a call of its own). Output capacity per call = its rows x
-    max(0, longest row - 3).
+    max(0, longest row - 3) / max(min_coverage, 1): every valid k-mer takes at least
+    min_coverage of the call's observations.
     Returns (rows int64[n] in group order, group_offsets int64[G + 1], G, calls): with
     consume=None, calls lists (g0, g1, result) per call, each result (kmer_spectrum_dev's
     dict for groups g0..g1-1) copied to its own size so the next call can reuse the
@@ -432,7 +433,7 @@ def group_spectra(offsets: torch.Tensor, values: torch.Tensor, keys: torch.Tenso
     for g0, g1 in zip(cuts, cuts[1:]):
         a, b = int(goh[g0]), int(goh[g1])
         r = rows[a:b]
-        cap = (b - a) * per_row
+        cap = (b - a) * per_row // max(int(min_coverage), 1)
         if packed is not None:
             res = kmer_spectrum_blocks(packed, offsets, values, go[g0:g1 + 1] - a, k, min_coverage, cap, rows=r,
                                        stream=stream)

@@ -248,3 +248,40 @@ def test_device_spectrum_with_grouping(rg, k, min_cov):
     assert np.array_equal(km[:, 0], ref["kmer_hi"]) and np.array_equal(km[:, 1], ref["kmer_lo"])
     assert np.array_equal(out["exts"].cpu().numpy(), ref["exts"])
     assert np.array_equal(out["counts"].cpu().numpy().view(np.uint16), ref["counts"])
+
+
+@pytest.mark.parametrize("k", [4, 9, 17, 32])
+def test_capacity_bound_tight(rg, k):
+    """Output capacity is sum(len - 3) / min_coverage per group (every valid k-mer takes at
+    least min_coverage observations). Groups of R identical reads at min_coverage R make
+    every distinct k-mer valid, the tightest case; a poly-A group has one k-mer seen
+    len - k + 1 times per read. Host path and the device block path (group_spectra, one
+    call) both equal the oracle."""
+    import torch
+
+    from rogtk_amd import device as D
+
+    rng = np.random.default_rng(100 + k)
+    R = 3
+    items, keys = [], []
+    for g in range(60):
+        r = _reads(rng, 1, 40, 220)[0]
+        items += [r] * R
+        keys += [g] * R
+    items += [b"A" * 150] * 2
+    keys += [60] * 2
+    go = np.r_[0, np.cumsum(np.bincount(keys))].astype(np.int64)
+    _check(rg, items, k, R, group_offsets=go)
+    lens = np.array([len(x) for x in items], dtype=np.int64)
+    offs = torch.from_numpy(np.r_[0, np.cumsum(lens)].astype(np.int64)).cuda()
+    vals = torch.from_numpy(np.frombuffer(b"".join(items), dtype=np.uint8).copy()).cuda()
+    kt = torch.from_numpy(np.array(keys, dtype=np.uint32).view(np.int32)).cuda()
+    rows, dgo, G, calls = D.group_spectra(offs, vals, kt, k, R)
+    assert G == 61 and len(calls) == 1
+    ref = P().kmer_spectrum(P().StrCol.from_list(items), k, R, False, go)  # keys already grouped
+    out = calls[0][2]
+    assert np.array_equal(out["entry_offsets"].cpu().numpy(), ref["group_offsets"])
+    assert np.array_equal(out["stats"].cpu().numpy(), ref["stats"])
+    km = out["kmers"].cpu().numpy().view(np.uint64)
+    assert np.array_equal(km[:, 0], ref["kmer_hi"]) and np.array_equal(km[:, 1], ref["kmer_lo"])
+    assert np.array_equal(out["counts"].cpu().numpy().view(np.uint16), ref["counts"])

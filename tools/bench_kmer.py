@@ -43,9 +43,9 @@ def main():
     ap.add_argument("--global-only", action="store_true", help="route every group through the radix-sort path")
     ap.add_argument("--ascii", action="store_true",
                     help="stage grouped rows from their ASCII bytes (no rogtk_pack_reads block column)")
-    ap.add_argument("--group-batch-rows", type=int, default=10_000_000,
+    ap.add_argument("--group-batch-rows", type=int, default=100_000_000,
                     help="k-mer spectra run over consecutive groups of at most this many rows per call "
-                         "(bounds the output capacity: 19 B x (read_len - 3) per row)")
+                         "(bounds the output capacity: 19 B x (read_len - 3) / min_coverage per row)")
     args = ap.parse_args()
     n, RL, L = args.reads, args.read_len, 12
     dev = torch.device("cuda", 0)
