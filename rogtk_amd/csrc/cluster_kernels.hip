@@ -1624,7 +1624,7 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
                                                        const uint32_t* __restrict__ rblkoff,
                                                        uint32_t* __restrict__ wlab, uint64_t* __restrict__ wexc,
                                                        uint32_t* __restrict__ labelcode, uint32_t* __restrict__ ilab,
-                                                       uint32_t* __restrict__ wlab2, int use_exc) {
+                                                       uint32_t* __restrict__ wlab2, int use_exc, int exc1_on) {
     for (int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x; w < words; w += (int64_t)gridDim.x * kBlock) {
         const uint32_t ur = UR[w];
         uint32_t root = kNone;
@@ -1661,11 +1661,16 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
                 }
             }
         }
-        // bit 31 flags a word with exceptions (labels < 2^31: umi_len <= 15; at 16 a word
+        // bit 31 flags a word with exceptions (labels < 2^30: umi_len <= 15; at 16 a word
         // with exceptions stays unlabelled and all its codes are labelled per code)
         if (exc && !use_exc) root = kNone;  // A/B: only uniform words labelled by word
         uint32_t lab = root != kNone ? root_label(root, rbits, rpref, rblkoff) : kNone;
-        if (exc && lab != kNone) lab = lab < 0x80000000u ? (lab | 0x80000000u) : kNone;
+        if (exc && lab != kNone) {  // encodings: decode_word_label (rogtk_internal.h)
+            if (exc1_on && !(exc & (exc - 1)) && lab < (1u << 24))
+                lab |= 0xC0000000u | ((uint32_t)(__ffsll((long long)exc) - 1) << 24);
+            else
+                lab = lab < 0x40000000u ? (lab | 0x80000000u) : kNone;
+        }
         wlab[w] = lab;
         wexc[w] = exc;
         // the codes the word label does not cover (its exceptions, or all of them when
@@ -1695,13 +1700,14 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
 
 // The label of code c from its word (kNone: label it per code): wlab[w] = the label of
 // the word's most frequent component, bit 31 set when some of its codes (wexc[w]) belong
-// to other components. Only flagged words cost a second (2 MB-table) load.
+// to other components (decode_word_label). Only words with two or more exception codes
+// cost a second (2 MB-table) load; a single exception code is named in the label.
 __device__ __forceinline__ uint32_t word_label_of(const uint32_t* __restrict__ wlab,
                                                   const uint64_t* __restrict__ wexc,
                                                   const uint32_t* __restrict__ wlab2, uint64_t c) {
     const uint32_t wl = wlab[c >> 6];
-    if (wl == kNone || !(wl >> 31)) return wl;
-    if (!((wexc[c >> 6] >> (c & 63)) & 1ull)) return wl & 0x7FFFFFFFu;
+    const uint32_t r = decode_word_label(wl, wexc, c);
+    if (r != kNone || wl == kNone) return r;
     return wlab2 ? wlab2[c >> 6] : kNone;  // the word's other component, or per code
 }
 
@@ -2156,9 +2162,14 @@ int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
             const char* e = getenv("ROGTK_WORD_EXC");
             return e && e[0] == '0' ? 0 : 1;
         }();
+        // ROGTK_WORD_EXC1=0: a word with one exception code also takes the mask load (A/B)
+        static const int exc1_on = [] {
+            const char* e = getenv("ROGTK_WORD_EXC1");
+            return e && e[0] == '0' ? 0 : 1;
+        }();
         hipLaunchKernelGGL(k_word_label, dim3(grid_for(cl.words, kPersistentGrid)), dim3(kBlock), 0, s, p.f, p.UR,
                            cl.words, p.RT, cl.max_distinct, p.rbits, p.rpref, p.rblkoff, p.wpref, p.G, p.labelcode,
-                           p.ilab, wlab2_on() ? p.wlab2 : nullptr, use_exc);
+                           p.ilab, wlab2_on() ? p.wlab2 : nullptr, use_exc, exc1_on);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     return ROGTK_OK;

@@ -307,11 +307,9 @@ __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restr
                     if ((reg >> k) & 1u) pres[c[k]] = 1;  // benign same-value race
             }
             if (ASG) {
-                // word_label_of (cluster_kernels.hip): bit 31 flags a word with exceptions
+                // word labels (decode_word_label, rogtk_internal.h)
 #pragma unroll
-                for (int k = 0; k < kRowsPerLane; ++k)
-                    if (wl[k] != 0xFFFFFFFFu && (wl[k] >> 31))
-                        wl[k] = ((A.wexc[c[k] >> 6] >> (c[k] & 63)) & 1ull) ? 0xFFFFFFFFu : (wl[k] & 0x7FFFFFFFu);
+                for (int k = 0; k < kRowsPerLane; ++k) wl[k] = decode_word_label(wl[k], A.wexc, c[k]);
                 uint32_t id[kRowsPerLane];
 #pragma unroll
                 for (int k = 0; k < kRowsPerLane; ++k)

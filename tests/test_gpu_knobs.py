@@ -65,6 +65,7 @@ KNOBS = [
     ({"ROGTK_FUSED_SCAN": "0", "ROGTK_LOCAL8": "0"}, "separate"),
     ({"ROGTK_LOCAL8_SINGLE": "1"}, "main"),
     ({"ROGTK_ROOTS_LB": "1"}, "separate"),
+    ({"ROGTK_WORD_EXC1": "0"}, "main"),
 ]
 
 
