@@ -376,12 +376,13 @@ __global__ __launch_bounds__(kBlock) void k_row_gather(const uint64_t* __restric
 }
 
 // row -> group map: one wave per group writes its rows' group id (coalesced)
+// 16 lanes per group (no shuffles: segments run independently)
 __global__ __launch_bounds__(kBlock) void k_row_groups(const int64_t* __restrict__ go, int64_t G,
                                                        uint32_t* __restrict__ row_group) {
-    const int lane = threadIdx.x & 63;
-    const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
-    for (int64_t g = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); g < G; g += waves)
-        for (int64_t r = go[g] + lane; r < go[g + 1]; r += 64) row_group[r] = (uint32_t)g;
+    const int sub = threadIdx.x & 15;
+    const int64_t step = (int64_t)gridDim.x * (kBlock / 16);
+    for (int64_t g = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / 16; g < G; g += step)
+        for (int64_t r = go[g] + sub; r < go[g + 1]; r += 16) row_group[r] = (uint32_t)g;
 }
 
 template <int OW, bool WIDE>
@@ -1032,40 +1033,72 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
 }
 
 // Per group of effective k K: observation, row and packed-word totals decide the path.
+// 16 lanes per group (a C3 group has ~10 rows: a wave per group left most lanes idle);
+// caps != NULL: also the group's output capacity (valid_cap of its observations)
+constexpr int kClsLanes = 16;
 __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __restrict__ go, int64_t G,
                                                            const uint8_t* __restrict__ gk, int K,
                                                            const int64_t* __restrict__ row_obs,
                                                            const int64_t* __restrict__ row_words,
                                                            const int64_t* __restrict__ woff, int stride,
-                                                           uint8_t* __restrict__ gsmall, GroupDesc* __restrict__ gdesc) {
-    const int lane = threadIdx.x & 63;
-    const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
-    for (int64_t g = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); g < G; g += waves) {
-        if (gk[g] != K) {
-            if (lane == 0) gsmall[g] = 0;
-            continue;
-        }
+                                                           uint8_t* __restrict__ gsmall, GroupDesc* __restrict__ gdesc,
+                                                           int64_t* __restrict__ caps, int64_t min_cov) {
+    const int sub = threadIdx.x & (kClsLanes - 1);
+    const int64_t step = (int64_t)gridDim.x * (kBlock / kClsLanes);
+    // every segment of a wave runs the same number of trips (the shuffles need the lanes)
+    const int64_t first = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / kClsLanes;
+    const int64_t wave_first = first - ((threadIdx.x & 63) / kClsLanes);
+    for (int64_t base = wave_first; base < G; base += step) {
+        const int64_t g = base + (first - wave_first);
+        const bool live = g < G && gk[g] == K;
         int64_t obs = 0, words = 0;
-        for (int64_t r = go[g] + lane; r < go[g + 1]; r += 64) {
-            obs += row_obs[r];
-            if (!stride) words += row_words[r];
-        }
-        for (int m = 32; m > 0; m >>= 1) {
+        if (live)
+            for (int64_t r = go[g] + sub; r < go[g + 1]; r += kClsLanes) {
+                obs += row_obs[r];
+                if (!stride) words += row_words[r];
+            }
+        for (int m = kClsLanes / 2; m > 0; m >>= 1) {
             obs += __shfl_xor(obs, m);
             words += __shfl_xor(words, m);
         }
+        if (sub != 0 || g >= G) continue;
+        if (!live) {
+            gsmall[g] = 0;
+            if (caps) caps[g] = 0;
+            continue;
+        }
         const int64_t nrows = go[g + 1] - go[g];
         if (stride) words = nrows * stride;  // fixed-stride staging (k_row_gather)
-        if (lane == 0) {
-            uint8_t cls = 0;
-            if (K <= 32 && obs > 0) {
-                if (nrows <= LdsCfg<3>::kRows && words <= LdsCfg<3>::kWords) cls = 3;
-                else if (nrows <= LdsCfg<1>::kRows && words <= LdsCfg<1>::kWords) cls = 1;
-                else if (nrows <= LdsCfg<4>::kRows && words <= LdsCfg<4>::kWords) cls = 4;
-            }
-            gsmall[g] = cls;
-            if (cls) gdesc[g] = GroupDesc{go[g], stride ? go[g] * stride : woff[go[g]], (int32_t)nrows, (int32_t)words};
+        uint8_t cls = 0;
+        if (K <= 32 && obs > 0) {
+            if (nrows <= LdsCfg<3>::kRows && words <= LdsCfg<3>::kWords) cls = 3;
+            else if (nrows <= LdsCfg<1>::kRows && words <= LdsCfg<1>::kWords) cls = 1;
+            else if (nrows <= LdsCfg<4>::kRows && words <= LdsCfg<4>::kWords) cls = 4;
         }
+        gsmall[g] = cls;
+        if (cls) gdesc[g] = GroupDesc{go[g], stride ? go[g] * stride : woff[go[g]], (int32_t)nrows, (int32_t)words};
+        if (caps) caps[g] = obs / (min_cov > 1 ? min_cov : 1);  // valid_cap
+    }
+}
+
+// rogtk_kmer_path_stats: groups of effective k K on the LDS path (gsmall != 0 after the
+// LDS kernels) and on the global path, counted on the device (no G-byte copy to the host)
+__global__ __launch_bounds__(kBlock) void k_path_counts(const uint8_t* __restrict__ gk, int K, int64_t G,
+                                                        const uint8_t* __restrict__ gsmall,
+                                                        unsigned long long* __restrict__ out2) {
+    unsigned long long lds = 0, glob = 0;
+    for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < G; g += (int64_t)gridDim.x * kBlock) {
+        if (gk[g] != K) continue;
+        if (gsmall && gsmall[g]) ++lds;
+        else ++glob;
+    }
+    for (int m = 32; m > 0; m >>= 1) {
+        lds += __shfl_xor(lds, m);
+        glob += __shfl_xor(glob, m);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (lds) atomicAdd(out2, lds);
+        if (glob) atomicAdd(out2 + 1, glob);
     }
 }
 
@@ -1099,6 +1132,22 @@ __global__ __launch_bounds__(kBlock) void k_group_caps(const int64_t* __restrict
             const int64_t len = offsets[pr + 1] - offsets[pr];
             if (len >= 4) t += len - 3;
         }
+        for (int m = 32; m > 0; m >>= 1) t += __shfl_xor(t, m);
+        if (lane == 0) caps[g] = valid_cap(t, min_cov);
+    }
+}
+
+// Per-group capacity from the staged rows' observation counts (contiguous per group): at
+// most obs / max(min_cov, 1) k-mers of a group are valid (valid_cap). The block path
+// computes it here, after staging, instead of by a gather of every row's length first.
+__global__ __launch_bounds__(kBlock) void k_group_caps_obs(const int64_t* __restrict__ go, int64_t G,
+                                                           const int64_t* __restrict__ row_obs, int64_t min_cov,
+                                                           int64_t* __restrict__ caps) {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
+    for (int64_t g = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); g < G; g += waves) {
+        int64_t t = 0;
+        for (int64_t r = go[g] + lane; r < go[g + 1]; r += 64) t += row_obs[r];
         for (int m = 32; m > 0; m >>= 1) t += __shfl_xor(t, m);
         if (lane == 0) caps[g] = valid_cap(t, min_cov);
     }
@@ -1247,6 +1296,8 @@ struct KIn {
     const uint64_t* blocks = nullptr;  // the column as B-word 2-bit blocks (k_pack_reads), or NULL
     int B = 0;                         // words per block
     int S = 0;                         // 2-bit words per row to stage: ceil(max_len / 32) <= B - 1
+    int64_t* cap_fill = nullptr;       // != NULL: per-group capacities computed here (into this
+                                       // scratch, then cap_off) from the staged rows' observations
 };
 
 template <int OW, bool WIDE>
@@ -1263,7 +1314,7 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
     if (int rc = c->raw_len.ensure(n_rows * 4)) return rc;
     if (int rc = c->obs_off.ensure(n_rows * 8)) return rc;
     const int wgrid = grid_for((n_rows + kWavesPerBlock - 1) / kWavesPerBlock * kBlock, 16384);
-    hipLaunchKernelGGL(k_row_groups, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, go, G,
+    hipLaunchKernelGGL(k_row_groups, dim3(grid_for(G * 16, 16384)), dim3(kBlock), 0, s, go, G,
                        c->row_group.as<uint32_t>());
     const int stride = in.blocks ? in.S : 0;  // staged words per row (0: compact, woff)
     if (in.blocks) {
@@ -1299,13 +1350,26 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
                            c->row_len.as<int32_t>(), gstat);
     }
     ROGTK_HIP_CHECK(hipGetLastError());
-    if (c->lds_path && K <= 32) {
-        // one workgroup per small group, straight from the packed rows
+    const bool lds = c->lds_path && K <= 32;
+    if (lds) {
+        // size classes (and, on the block path, the capacities from the staged rows)
         if (int rc = c->gsmall.ensure((size_t)G)) return rc;
         if (int rc = c->gdesc.ensure((size_t)G * sizeof(GroupDesc))) return rc;
-        hipLaunchKernelGGL(k_group_classify, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, go, G, in.gk, K,
-                           c->row_obs.as<int64_t>(), c->row_words.as<int64_t>(), c->woff.as<int64_t>(), stride,
-                           c->gsmall.as<uint8_t>(), c->gdesc.as<GroupDesc>());
+        hipLaunchKernelGGL(k_group_classify, dim3(grid_for(G * kClsLanes, 16384)), dim3(kBlock), 0, s, go, G, in.gk,
+                           K, c->row_obs.as<int64_t>(), c->row_words.as<int64_t>(), c->woff.as<int64_t>(), stride,
+                           c->gsmall.as<uint8_t>(), c->gdesc.as<GroupDesc>(), in.cap_fill, min_cov);
+    } else if (in.cap_fill) {
+        hipLaunchKernelGGL(k_group_caps_obs, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, go, G,
+                           c->row_obs.as<int64_t>(), min_cov, in.cap_fill);
+    }
+    if (in.cap_fill) {  // capacity offsets from the staged observation counts (before any output)
+        int64_t* co = const_cast<int64_t*>(in.cap_off);
+        if (int rc = cub_exsum_i64(c, in.cap_fill, co, G, s)) return rc;
+        hipLaunchKernelGGL(k_tail_sum, dim3(1), dim3(64), 0, s, co, in.cap_fill, G, co + G);
+        ROGTK_HIP_CHECK(hipGetLastError());
+    }
+    if (lds) {
+        // one workgroup per small group, straight from the packed rows
         hipLaunchKernelGGL((k_kmer_lds<3, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)), dim3(kLdsBlock), 0, s,
                            c->gdesc.as<GroupDesc>(), G,
                            c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
@@ -1326,20 +1390,18 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     if (int rc = cub_exsum_i64(c, c->row_obs.as<int64_t>(), c->obs_off.as<int64_t>(), n_rows, s)) return rc;
-    std::vector<uint8_t> small;
-    if (c->lds_path && K <= 32) {
-        small.resize(G);
-        ROGTK_HIP_CHECK(hipMemcpyAsync(small.data(), c->gsmall.p, G, hipMemcpyDeviceToHost, s));
-    }
-    int64_t last[2] = {0, 0};
+    if (int rc = c->scal.ensure(64)) return rc;
+    ROGTK_HIP_CHECK(hipMemsetAsync(c->scal.p, 0, 16, s));
+    hipLaunchKernelGGL(k_path_counts, dim3(grid_for(G, 4096)), dim3(kBlock), 0, s, in.gk, K, G,
+                       (c->lds_path && K <= 32) ? c->gsmall.as<uint8_t>() : nullptr,
+                       c->scal.as<unsigned long long>());
+    int64_t last[4] = {0, 0, 0, 0};
     ROGTK_HIP_CHECK(hipMemcpyAsync(&last[0], c->obs_off.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
     ROGTK_HIP_CHECK(hipMemcpyAsync(&last[1], c->row_obs.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&last[2], c->scal.p, 16, hipMemcpyDeviceToHost, s));
     ROGTK_HIP_CHECK(hipStreamSynchronize(s));
-    for (int64_t g = 0; g < G; ++g) {
-        if (gk_host && (*gk_host)[g] != K) continue;
-        if (!small.empty() && small[g]) ++c->last_lds_groups;
-        else ++c->last_global_groups;
-    }
+    c->last_lds_groups += last[2];
+    c->last_global_groups += last[3];
     const int64_t T = last[0] + last[1];
     if (T == 0) return ROGTK_OK;
     ROGTK_REQUIRE(T <= kMaxObsPerLaunch, ROGTK_E_UNSUPPORTED,
@@ -1692,14 +1754,20 @@ int spectrum_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* v
     ROGTK_HIP_CHECK(hipMemsetAsync(c->gk.p, K, G, s));
     ROGTK_HIP_CHECK(hipMemsetAsync(c->gstat.p, 0, G * 5 * 8, s));
     ROGTK_HIP_CHECK(hipMemsetAsync(c->gcount.p, 0, G * 8, s));
-    hipLaunchKernelGGL(k_group_caps, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, offsets, rows,
-                       group_offsets, G, c->caps.as<int64_t>(), min_coverage);
-    if (int rc = cub_exsum_i64(c, c->caps.as<int64_t>(), c->cap_off.as<int64_t>(), G, s)) return rc;
-    hipLaunchKernelGGL(k_tail_sum, dim3(1), dim3(64), 0, s, c->cap_off.as<int64_t>(), c->caps.as<int64_t>(), G,
-                       c->cap_off.as<int64_t>() + G);
     int64_t tcap = 0;
-    ROGTK_HIP_CHECK(hipMemcpyAsync(&tcap, c->cap_off.as<int64_t>() + G, 8, hipMemcpyDeviceToHost, s));
-    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    if (blocks) {
+        // block path: a row holds at most 32 S bases, so at most 32 S - K + 1 observations;
+        // the per-group capacities follow from the staged rows (run_class, cap_fill)
+        tcap = valid_cap(n_rows * std::max<int64_t>(0, 32 * (int64_t)S - (K ? K : 64) + 1), min_coverage);
+    } else {
+        hipLaunchKernelGGL(k_group_caps, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, offsets, rows,
+                           group_offsets, G, c->caps.as<int64_t>(), min_coverage);
+        if (int rc = cub_exsum_i64(c, c->caps.as<int64_t>(), c->cap_off.as<int64_t>(), G, s)) return rc;
+        hipLaunchKernelGGL(k_tail_sum, dim3(1), dim3(64), 0, s, c->cap_off.as<int64_t>(), c->caps.as<int64_t>(), G,
+                           c->cap_off.as<int64_t>() + G);
+        ROGTK_HIP_CHECK(hipMemcpyAsync(&tcap, c->cap_off.as<int64_t>() + G, 8, hipMemcpyDeviceToHost, s));
+        ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    }
     tcap = std::max<int64_t>(tcap, 1);
     if (int rc = c->t_kmer.ensure((size_t)tcap * 16)) return rc;
     if (int rc = c->t_ext.ensure((size_t)tcap)) return rc;
@@ -1711,6 +1779,7 @@ int spectrum_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* v
         in.blocks = blocks;
         in.B = B;
         in.S = S;
+        if (blocks) in.cap_fill = c->caps.as<int64_t>();
         if (int rc = run_any<8>(c, in, n_rows, G, K, min_coverage, s, nullptr)) return rc;
     }
     if (int rc = cub_exsum_i64(c, c->gcount.as<int64_t>(), entry_offsets, G, s)) return rc;
@@ -1764,6 +1833,8 @@ int rogtk_pack_reads(const int64_t* offsets, const uint8_t* values, const uint8_
     // workgroup (1 / 2 / 3). Default 3 (round 3, 100M 150-bp reads: 12.6 vs 18.8 ms;
     // C3 86.7-91.0 vs 94.6-95.6 ms per step, interleaved): a one-wave workgroup stages
     // 10.5 KB, so ~14 waves per CU keep loads in flight instead of 8
+    // (A word-parallel variant - B lanes per row, a lane per block word - measured neutral
+    // in round 3: 1.410-1.420 vs 1.411-1.417 G reads/s at 100M, profiles/r03z_c3_host_ab.txt)
     static const int variant = [] {
         const char* e = getenv("ROGTK_PACK");
         const int v = e ? atoi(e) : 3;

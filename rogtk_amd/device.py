@@ -419,19 +419,24 @@ def group_spectra(offsets: torch.Tensor, values: torch.Tensor, keys: torch.Tenso
     rows, go, G = group_by_key(keys, stream=stream)
     if G == 0:
         return rows, go, G, []
-    goh = go.cpu().numpy()
     # output capacity per call: rows x (longest row - 3) bounds the valid entries (each
     # row adds at most len - 3 k-mers, k_eff >= 4)
     max_len = packed.max_len if packed is not None else int((offsets[1:] - offsets[:-1]).max().item())
     per_row = max(0, max_len - 3)
-    cuts = [0]
-    while cuts[-1] < G:
-        g0 = cuts[-1]
-        g1 = int(np.searchsorted(goh, goh[g0] + batch_rows, side="right")) - 1
-        cuts.append(min(G, max(g1, g0 + 1)))
+    n_grouped = rows.numel()
+    if n_grouped <= batch_rows:  # one call: no copy of the group offsets to the host
+        cuts, bounds = [0, G], {0: 0, G: n_grouped}
+    else:
+        goh = go.cpu().numpy()
+        cuts = [0]
+        while cuts[-1] < G:
+            g0 = cuts[-1]
+            g1 = int(np.searchsorted(goh, goh[g0] + batch_rows, side="right")) - 1
+            cuts.append(min(G, max(g1, g0 + 1)))
+        bounds = {g: int(goh[g]) for g in cuts}
     calls = []
     for g0, g1 in zip(cuts, cuts[1:]):
-        a, b = int(goh[g0]), int(goh[g1])
+        a, b = bounds[g0], bounds[g1]
         r = rows[a:b]
         cap = (b - a) * per_row // max(int(min_coverage), 1)
         if packed is not None:
