@@ -220,10 +220,21 @@ __global__ __launch_bounds__(R) void k_pack_reads(const int64_t* __restrict__ of
     __shared__ uint64_t out[DIRECT ? 1 : R * OS];
     __shared__ int64_t s_off[R + 1];
     const int tid = threadIdx.x;
+    // the next trip's row offsets are loaded into registers while this trip runs, so a
+    // trip waits for one HBM round trip (its bytes) instead of two (offsets, then bytes)
+    int64_t pf0 = 0, pf1 = 0;
+    auto prefetch = [&](int64_t aa) {
+        const int nrr = (int)min<int64_t>(R, n - aa);
+        pf0 = tid <= nrr ? offsets[aa + tid] : 0;
+        pf1 = tid + R <= nrr ? offsets[aa + tid + R] : 0;
+    };
+    if ((int64_t)blockIdx.x * R < n) prefetch((int64_t)blockIdx.x * R);
     for (int64_t a = (int64_t)blockIdx.x * R; a < n; a += (int64_t)gridDim.x * R) {
         const int nr = (int)min<int64_t>(R, n - a);
-        for (int i = tid; i <= nr; i += R) s_off[i] = offsets[a + i];
+        if (tid <= nr) s_off[tid] = pf0;
+        if (tid + R <= nr) s_off[tid + R] = pf1;
         __syncthreads();
+        if (a + (int64_t)gridDim.x * R < n) prefetch(a + (int64_t)gridDim.x * R);
         const int64_t b0 = s_off[0], b1 = s_off[nr];
         const int64_t a4 = b0 & ~3ll;  // dword-aligned start
         const bool staged = b1 - a4 <= kIn;
@@ -762,13 +773,17 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
         if (i1 >= 0) load_rows(d1);  // in flight while this group is processed
         if (own2) d2 = gdesc[g0 + __ffsll((unsigned long long)own2) - 1];
         KT(1);
-        // every k-mer observation of the group, straight from the packed words in LDS
-        for (int ri = wave; ri < nrows; ri += kWaves) {
+        // every k-mer observation of the group, straight from the packed words in LDS.
+        // Work unit = (row, half): half h takes the row's positions 64 h + lane + 128 i, so
+        // a C3 group (~10 rows of 119 observations) deals 2 units per row over the 8 waves
+        // instead of whole rows (waves with two rows set the pace otherwise)
+        for (int u = wave; u < 2 * nrows; u += kWaves) {
+            const int ri = u >> 1;
             const int nobs = m_nobs[ri];
-            if (nobs == 0) continue;
+            if (nobs <= ((u & 1) << 6)) continue;
             const int len = m_len[ri];
             const uint64_t* rw = words + m_w[ri];
-            for (int p = lane; p < nobs; p += 64) {
+            for (int p = lane + ((u & 1) << 6); p < nobs; p += 128) {
                 const int b = 2 * (p & 31);
                 const uint64_t x0 = rw[p >> 5], x1 = rw[(p >> 5) + 1];
                 const uint64_t top = b ? (x0 << b) | (x1 >> (64 - b)) : x0;

@@ -88,7 +88,8 @@ def main():
 
         _, _, G, _ = D.group_spectra(offsets, reads, cid, args.k, args.min_coverage, batch_rows=br, consume=consume,
                                      packed=None if args.ascii else "auto")
-        out = {"n_calls": acc["calls"], "valid": acc["valid"], "stats": torch.cat(acc["stats"])}
+        out = {"n_calls": acc["calls"], "valid": acc["valid"],
+               "stats": acc["stats"][0] if len(acc["stats"]) == 1 else torch.cat(acc["stats"])}
         e3.record()
         torch.cuda.synchronize()
         if record:
