@@ -1661,15 +1661,20 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
                 }
             }
         }
-        // bit 31 flags a word with exceptions (labels < 2^30: umi_len <= 15; at 16 a word
-        // with exceptions stays unlabelled and all its codes are labelled per code)
+        // bit 31 flags a word with exceptions (mask form: labels < 2^29, umi_len <= 14; a
+        // larger label leaves the word unlabelled and all its codes are labelled per code)
         if (exc && !use_exc) root = kNone;  // A/B: only uniform words labelled by word
         uint32_t lab = root != kNone ? root_label(root, rbits, rpref, rblkoff) : kNone;
         if (exc && lab != kNone) {  // encodings: decode_word_label (rogtk_internal.h)
-            if (exc1_on && !(exc & (exc - 1)) && lab < (1u << 24))
+            const uint64_t rest = exc & (exc - 1);  // the exceptions past the first
+            if (exc1_on && !rest && lab < (1u << 24)) {
                 lab |= 0xC0000000u | ((uint32_t)(__ffsll((long long)exc) - 1) << 24);
-            else
-                lab = lab < 0x40000000u ? (lab | 0x80000000u) : kNone;
+            } else if (exc1_on && !(rest & (rest - 1)) && lab < (1u << 17)) {
+                lab |= 0xA0000000u | ((uint32_t)(__ffsll((long long)exc) - 1) << 17) |
+                       ((uint32_t)(__ffsll((long long)rest) - 1) << 23);
+            } else {
+                lab = lab < 0x20000000u ? (lab | 0x80000000u) : kNone;
+            }
         }
         wlab[w] = lab;
         wexc[w] = exc;
@@ -2162,7 +2167,7 @@ int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
             const char* e = getenv("ROGTK_WORD_EXC");
             return e && e[0] == '0' ? 0 : 1;
         }();
-        // ROGTK_WORD_EXC1=0: a word with one exception code also takes the mask load (A/B)
+        // ROGTK_WORD_EXC1=0: words with one or two exception codes also take the mask load (A/B)
         static const int exc1_on = [] {
             const char* e = getenv("ROGTK_WORD_EXC1");
             return e && e[0] == '0' ? 0 : 1;

@@ -134,13 +134,18 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 //   bit 31 clear        the label of every code of the word;
 //   bits 31 and 30 set  the label (bits 0..23) of every code but one exception code,
 //                       whose bit in the word is bits 24..29 (no mask load);
-//   bit 31 set, 30 clr  the label (bits 0..29) of the codes outside the word's
+//   bits 31, 29 set, 30 clear: the label (bits 0..16) of every code but two exception
+//                       codes, whose bits are bits 17..22 and 23..28 (no mask load);
+//   bit 31 set, 30, 29 clear: the label (bits 0..28) of the codes outside the word's
 //                       exception mask wexc[word].
 // Returns the code's label, or 0xFFFFFFFF when the code is labelled per code.
 __device__ __forceinline__ uint32_t decode_word_label(uint32_t wl, const uint64_t* __restrict__ wexc, uint64_t c) {
     if (wl == 0xFFFFFFFFu || !(wl >> 31)) return wl;
-    if ((wl >> 30) & 1u) return (uint32_t)(c & 63) == ((wl >> 24) & 63u) ? 0xFFFFFFFFu : (wl & 0xFFFFFFu);
-    return ((wexc[c >> 6] >> (c & 63)) & 1ull) ? 0xFFFFFFFFu : (wl & 0x3FFFFFFFu);
+    const uint32_t b = (uint32_t)(c & 63);
+    if ((wl >> 30) & 1u) return b == ((wl >> 24) & 63u) ? 0xFFFFFFFFu : (wl & 0xFFFFFFu);
+    if ((wl >> 29) & 1u)
+        return (b == ((wl >> 17) & 63u) || b == ((wl >> 23) & 63u)) ? 0xFFFFFFFFu : (wl & 0x1FFFFu);
+    return ((wexc[c >> 6] >> b) & 1ull) ? 0xFFFFFFFFu : (wl & 0x1FFFFFFFu);
 }
 
 // the score kernel's 52 B/row of outputs (ROGTK_NT_SCORE_STORE=0: plain stores)
