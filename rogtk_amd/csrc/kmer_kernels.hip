@@ -690,7 +690,11 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
     uint64_t* const vkey = ubuf;                                       // after the inserts
     uint32_t* const vinfo = reinterpret_cast<uint32_t*>(ubuf + kLdsObs);  // count | exts << 16 | pad << 31
     __shared__ uint32_t scan[kWaves];
-    __shared__ uint32_t s_claimed, s_term, s_iso, s_over;
+    __shared__ uint32_t s_claimed, s_term, s_iso, s_over, s_hit;
+    // s_hit: some k-mer's count reached min_cov during the inserts (counts grow by one per
+    // insert, so one insert sees exactly min_cov). Without it nothing is valid and the
+    // CountFilter pass, its scan and a barrier are skipped (most groups at the usual floor)
+    const uint32_t hit_at = min_cov <= 1 ? 1u : min_cov <= 0xFFFF ? (uint32_t)min_cov : 0u;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int hbits = 31 - __clz(kLdsSlots);
     const uint64_t kmask = K == 32 ? ~0ull : ((1ull << (2 * K)) - 1ull);
@@ -765,6 +769,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
         if (tid == 0) {
             words[nwords] = 0;
             s_term = 0;
+            s_hit = 0;
             s_iso = 0;
         }
         __syncthreads();
@@ -803,19 +808,23 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
                         slot = (slot + 1) & (kLdsSlots - 1);
                     }
                 }
-                if ((atomicAdd(&tinfo[slot], 1u) & 0xFFFFFFu) == 0) {
+                const uint32_t cnt0 = atomicAdd(&tinfo[slot], 1u) & 0xFFFFFFu;
+                if (cnt0 == 0) {
                     const uint32_t ci = atomicAdd(&s_claimed, 1u);
                     if (!kBounded || ci < (uint32_t)C::kClaim) claimed[ci] = (uint16_t)slot;
                     else s_over = 1;  // more distinct k-mers than the table takes
                 }
+                if (cnt0 + 1 == hit_at) s_hit = 1;
                 if (e) atomicOr(&tinfo[slot], e << 24);
             }
         }
         __syncthreads();
         KT(2);
+        const uint32_t ncl = s_claimed;
+        const bool hit = s_hit;
         if (kBounded) {
             const bool over = s_over;
-            __syncthreads();  // every thread has read the flag before it is cleared
+            __syncthreads();  // every thread has read the flags before they are cleared
             if (over) {
                 // the claimed list is incomplete: clear the whole table; the group goes
                 // to class 4 (from class 1) or the global path (the next group's first
@@ -832,9 +841,24 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
                 continue;
             }
         }
+        if (!hit) {
+            // no count reached min_cov: nothing passes CountFilter (as nv == 0 below,
+            // without the count pass): reset the touched slots, record the empty group
+            for (uint32_t i = tid; i < ncl; i += TB) {
+                const uint32_t sl = claimed[i];
+                tkey[sl] = kEmpty;
+                tinfo[sl] = 0;
+            }
+            if (tid == 0) {
+                gcount[g] = 0;
+                gstat[5 * g + 3] = 0;
+                gstat[5 * g + 4] = 0;
+                s_claimed = 0;
+            }
+            continue;
+        }
         // CountFilter + compaction over the claimed slots: wave-shuffle scan, one
         // barrier for the per-wave totals
-        const uint32_t ncl = s_claimed;
         const uint32_t per = (ncl + TB - 1) / TB;
         const uint32_t c0 = min(ncl, tid * per), c1 = min(ncl, c0 + per);
         uint32_t mine = 0;
