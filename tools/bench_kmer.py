@@ -107,6 +107,23 @@ def main():
     el = time.perf_counter() - t
     paths = path_groups
     st = out["stats"].cpu().numpy()
+    step_s = el / args.steps
+    obs_per_s = n * (RL - int(st[:, 0].max()) + 1) * args.steps / el
+    # C3 roofline. Algorithmic HBM bytes per read: the ASCII read once, its
+    # UMI code read and its cluster id written (RL + 8). Staged bytes per read as built:
+    # the pack pass (RL in, one 64-B block out), the grouped gather (64-B block in, 40 B
+    # staged + 12 B of row metadata). The step is bound by the LDS k-mer table, stated as
+    # k-mer observations per CU clock (256 CUs, 2.4 GHz).
+    alg_b, staged_b, peak = RL + 8, RL + 64 + 64 + 40 + 12, 8000.0
+    ach = lambda b: n * b / step_s / 1e9
+    roofline = {
+        "bound": "lds", "kernel": "k_kmer_lds<3>",
+        "obs_per_cu_clock": round(obs_per_s / (256 * 2.4e9), 3),
+        "step": {"bound": "hbm", "algorithmic_bytes_per_read": alg_b, "achieved": round(ach(alg_b), 1),
+                 "peak": peak, "unit": "GB/s", "frac": round(ach(alg_b) / peak, 4)},
+        "staged": {"bytes_per_read": staged_b, "achieved": round(ach(staged_b), 1), "peak": peak, "unit": "GB/s",
+                   "frac": round(ach(staged_b) / peak, 4)},
+    }
     line = {
         "metric": "reads/s UMI group_by + k-mer spectra (C3 front end), 150 bp reads, 12 bp UMI, 1 MI355X",
         "value": round(n * args.steps / el, 1), "unit": "reads/s", "n_gpus": 1, "steps": args.steps,
@@ -118,7 +135,8 @@ def main():
                    "global_groups": paths[1], "valid_kmers": out["valid"], "spectrum_calls": out["n_calls"],
                    "sequences": int(st[:, 1].sum())},
         "phases_ms": {k: round(v / args.steps, 3) for k, v in phases.items()},
-        "observations_per_s": round(n * (RL - int(st[:, 0].max()) + 1) * args.steps / el, 1),
+        "observations_per_s": round(obs_per_s, 1),
+        "roofline": roofline,
         "data": f"synthetic (synth-v1 reads + UMIs, {n // 10} molecules), generated in {gen_s:.1f} s, resident in HBM",
     }
     print(json.dumps(line), flush=True)
