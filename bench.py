@@ -26,6 +26,7 @@ With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N ra
 from __future__ import annotations
 
 import argparse
+import ctypes
 import glob
 import json
 import os
@@ -116,6 +117,11 @@ def parse():
                          "(one kernel fewer on the main stream; measured slower)")
     ap.add_argument("--late-assign", action="store_true",
                     help="host order: enqueue batch k-1's assign after batch k's resolve (round-2 default)")
+    ap.add_argument("--no-c3", action="store_true",
+                    help="skip the C3 line part (BASELINE configs[2]: 100M reads, k-mer spectra per UMI group; "
+                         "runs after C2 on rank 0 of a one-GPU run)")
+    ap.add_argument("--c3-reads", type=int, default=100_000_000)
+    ap.add_argument("--c3-steps", type=int, default=3)
     return ap.parse_args()
 
 
@@ -249,11 +255,146 @@ def cpu_baseline_threads(codes_h: np.ndarray, L: int, md: int, threads: int = 0)
                       f"{os.cpu_count()} cores): H1+H2 {t1 - t0:.2f} s, H3 (threaded union-find) {t2 - t1:.2f} s"}
 
 
-def load_traffic(reads_per_launch: int, fused: bool = False):
+def c3_workload(n: int = 100_000_000, steps: int = 3, warmup: int = 1, k: int = 17, min_coverage: int = 20,
+                read_len: int = 150, ascii: bool = False, global_only: bool = False,
+                group_batch_rows: int = 100_000_000, profile: bool = True) -> dict:
+    """BASELINE configs[2] (C3): n synthetic 150-bp reads with 12-bp UMIs resident in HBM;
+    one step = H3 exact UMI ids (the caller's group_by('umi'), rogtk/__init__.py:206-214)
+    -> rogtk_amd.device.group_spectra: stable group_by of the ids, then the k-mer spectra
+    of every group (filter_kmers + CountFilter + censored exts, fracture.rs:105-116),
+    k = 17 (effective 32, fracture.rs:246-256), min_coverage 20 (rogtk/__init__.py:212).
+    The same path tests/test_gpu_c3.py checks against the oracle. Timed steps run without
+    profiling; `profile` adds one untimed step with the pack / gather / k-mer kernels
+    bracketed by events on their dispatch packets (kernel execution time)."""
+    from rogtk_amd import _lib
+
+    RL, L = read_len, 12
+    dev = torch.device("cuda", torch.cuda.current_device())
+    t0 = time.time()
+    codes = torch.from_numpy(synth.umi_codes(n, L).view(np.int32)).to(dev)
+    reads = torch.empty(n * RL, dtype=torch.uint8, device=dev)
+    chunk = 2_000_000
+    for a in range(0, n, chunk):  # host generator (OpenMP), streamed to HBM
+        b = min(n, a + chunk)
+        reads[a * RL:b * RL] = torch.from_numpy(synth.reads(n, RL, start=a, count=b - a).reshape(-1)).to(dev)
+    offsets = torch.arange(0, (n + 1) * RL, RL, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    gen_s = time.time() - t0
+    batch = D.PackedBatch(codes, L)
+    eng = D.ClusterEngine(L, min(n, 4 ** L), dev)
+    cid = torch.empty(n, dtype=torch.int32, device=dev)
+    br = min(n, group_batch_rows)
+    _lib.call("rogtk_kmer_set_path", 0 if global_only else 1)
+    ev = lambda: torch.cuda.Event(enable_timing=True)
+    phases = {"cluster": 0.0, "group_by+kmer": 0.0}
+    acc = {}
+    path_groups = [0, 0]
+
+    def step(record):
+        e0, e1, e3 = ev(), ev(), ev()
+        e0.record()
+        D.cluster_batch(eng, batch, cid, 0)
+        e1.record()
+        path_groups[:] = [0, 0]
+        acc.update(valid=0, stats=[], calls=0)
+
+        def consume(g0, g1, r):  # per spectrum call
+            acc["valid"] += int(r["entry_offsets"][-1].item())
+            acc["stats"].append(r["stats"].clone())
+            acc["calls"] += 1
+            ps = (ctypes.c_int64 * 2)()
+            _lib.call("rogtk_kmer_path_stats", ps)
+            path_groups[0] += ps[0]
+            path_groups[1] += ps[1]
+
+        _, _, G, _ = D.group_spectra(offsets, reads, cid, k, min_coverage, batch_rows=br, consume=consume,
+                                     packed=None if ascii else "auto")
+        e3.record()
+        torch.cuda.synchronize()
+        if record:
+            phases["cluster"] += e0.elapsed_time(e1)
+            phases["group_by+kmer"] += e1.elapsed_time(e3)
+        return G
+
+    for _ in range(warmup):
+        step(False)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(steps):
+        G = step(True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t
+    st = (acc["stats"][0] if len(acc["stats"]) == 1 else torch.cat(acc["stats"])).cpu().numpy()
+    k_eff = int(st[:, 0].max())
+    step_s = el / steps
+    obs = n * (RL - k_eff + 1)  # k-mer observations per step (every read is ACGT, full length)
+    kernels = {}
+    if profile:
+        sel = ("pack_reads", "row_gather", "kmer_lds")
+        try:
+            D.profile_select(",".join(sel))
+        except Exception:  # a library without these kernel names (A/B of older builds)
+            sel = ()
+        D.profile_reset()
+        D.profile_enable(True)
+        step(False)
+        torch.cuda.synchronize()
+        D.profile_enable(False)
+        for kname in sel:
+            ms, launches = D.profile_read(kname)
+            if launches:
+                kernels[kname] = round(1000.0 * ms, 1)  # us per step (all launches of the step)
+        D.profile_select(None)
+    cu_clk = 256 * 2.4e9  # MI355X: 256 CUs at 2.4 GHz
+    peak = HBM_PEAK_GBS
+    # Algorithmic HBM bytes per read (DESIGN §3b): the ASCII read once, its UMI code read and
+    # its cluster id written (RL + 8). As built: pack (RL in, one 64-B block out), grouped
+    # gather (64-B block in, 40 B staged + 12 B of row metadata).
+    alg_b, staged_b = RL + 8, RL + 64 + 64 + 40 + 12
+    ach = lambda b: n * b / step_s / 1e9
+    out = {
+        "workload": f"C3: {n // 1_000_000}M reads x {RL} bp, 12-bp UMI; H3 exact ids -> group_by -> k-mer "
+                    f"spectra per group, k={k} (effective {k_eff}), min_coverage {min_coverage}",
+        "reads_per_s": round(n * steps / el, 1), "ms_per_step": round(1000 * step_s, 3), "steps": steps,
+        "warmup": warmup, "groups": G, "lds_groups": path_groups[0], "global_groups": path_groups[1],
+        "valid_kmers": acc["valid"], "spectrum_calls": acc["calls"],
+        "phases_ms": {kk: round(v / steps, 3) for kk, v in phases.items()},
+        "kernels_us": kernels,
+        "observations_per_s": round(obs / step_s, 1),
+        "obs_per_cu_clock": round(obs / step_s / cu_clk, 3),
+        "hbm_frac": round(ach(alg_b) / peak, 4),
+        "roofline": {
+            "step": {"bound": "hbm", "algorithmic_bytes_per_read": alg_b, "achieved": round(ach(alg_b), 1),
+                     "peak": peak, "unit": "GB/s", "frac": round(ach(alg_b) / peak, 4)},
+            "staged": {"bytes_per_read": staged_b, "achieved": round(ach(staged_b), 1), "peak": peak,
+                       "unit": "GB/s", "frac": round(ach(staged_b) / peak, 4)},
+        },
+        "data": f"synthetic (synth-v1 reads + UMIs, {n // 10} molecules), generated in {gen_s:.1f} s, "
+                "resident in HBM",
+    }
+    if "kmer_lds" in kernels:  # the insert kernel alone: observations per CU clock inside it
+        out["roofline"]["kmer_lds"] = {"bound": "lds", "kernel": "k_kmer_lds<3>", "us": kernels["kmer_lds"],
+                                       "obs_per_cu_clock": round(obs / (kernels["kmer_lds"] * 1e-6) / cu_clk, 3)}
+    if "pack_reads" in kernels:  # HBM stream: RL bytes in, one 64-B block out per read
+        a = n * (RL + 64) / (kernels["pack_reads"] * 1e-6) / 1e9
+        out["roofline"]["pack_reads"] = {"bound": "hbm", "kernel": "k_pack_reads", "us": kernels["pack_reads"],
+                                         "bytes_per_read": RL + 64, "achieved": round(a, 1), "peak": peak,
+                                         "unit": "GB/s", "frac": round(a / peak, 4)}
+    if "row_gather" in kernels:  # 64-B block in, 40 B staged + 12 B of row metadata out
+        a = n * (64 + 40 + 12) / (kernels["row_gather"] * 1e-6) / 1e9
+        out["roofline"]["row_gather"] = {"bound": "hbm", "kernel": "k_row_gather", "us": kernels["row_gather"],
+                                         "bytes_per_read": 116, "achieved": round(a, 1), "peak": peak,
+                                         "unit": "GB/s", "frac": round(a / peak, 4)}
+    del reads, codes, offsets, batch, eng, cid
+    torch.cuda.empty_cache()
+    return out
+
+
+def load_traffic(reads_per_launch: int, fused: bool = False, key: str = None):
     """Per-launch HBM bytes of k_score_packed (its fused score + assign instance when
-    `fused`) from the latest committed PMC summary made at the same reads per launch, if
-    any."""
-    key = "score_assign_hbm_bytes_per_launch" if fused else "score_packed_hbm_bytes_per_launch"
+    `fused`; another kernel's by `key`) from the latest committed PMC summary made at the
+    same reads per launch, if any."""
+    key = key or ("score_assign_hbm_bytes_per_launch" if fused else "score_packed_hbm_bytes_per_launch")
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
     for path in reversed(files):
         try:
@@ -339,10 +480,11 @@ def main():
         pipe.drain()
         torch.cuda.synchronize()
     if not args.no_profile:
-        # only the roofline kernel is bracketed inside the timed region: every bracketed
-        # launch adds two event records to its stream (measured: +0.055 ms/step when all
-        # kernels are bracketed)
-        D.profile_select("score_packed")
+        # only the two row-streaming kernels are timed inside the timed region, both by
+        # events on their dispatch packets (no packets of their own: the score kernel also
+        # by its in-kernel span); the other kernels' bracketing events would add packets
+        # to their streams (measured: +0.055 ms/step when all kernels are bracketed)
+        D.profile_select("score_packed,cluster_assign")
         D.profile_reset()
         D.profile_enable(True)
     barrier(world)
@@ -365,6 +507,9 @@ def main():
             # also time their own fences (~15 us more per launch)
             kernels["score_packed"] = {"avg_us": 1000.0 * sms / slaunches, "launches": slaunches,
                                        "event_avg_us": 1000.0 * ms / launches if launches else None}
+        ams, alaunches = D.profile_read("cluster_assign")
+        if alaunches:
+            kernels["cluster_assign"] = {"avg_us": 1000.0 * ams / alaunches, "launches": alaunches}
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -463,11 +608,35 @@ def main():
         roof["step"] = {"algorithmic_bytes": int(step_bytes), "achieved": round(step_bytes / (el / args.steps) / 1e9, 1),
                         "frac": round(step_bytes / (el / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
                         "note": "whole pipelined step (all kernels, ms_per_step) vs SURVEY §8d's algorithmic bytes"}
+        # the kernel with the largest share of the step's device time among the two that
+        # stream every row (the resolve kernels move a few MB each): its §8(d) bytes and
+        # its corrected PMC traffic
+        cands = {"k_score_packed": (kernels["score_packed"]["avg_us"], bpr, roof["traffic"])}
+        if "cluster_assign" in kernels and not args.fused_assign:
+            a_traffic, _ = load_traffic(count, key="assign_hbm_bytes_per_launch")
+            cands["k_assign"] = (kernels["cluster_assign"]["avg_us"], 8.0, a_traffic)
+        dk = max(cands, key=lambda k: cands[k][0])
+        d_us, d_bpr, d_traffic = cands[dk]
+        d_ach = count * d_bpr / (d_us * 1e-6) / 1e9
+        roof["dominant"] = {"kernel": dk, "avg_us": round(d_us, 2), "bytes_per_read": d_bpr,
+                            "algorithmic_bytes_per_launch": int(count * d_bpr), "achieved": round(d_ach, 1),
+                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(d_ach / HBM_PEAK_GBS, 4),
+                            "traffic": d_traffic,
+                            "traffic_ratio": round(d_traffic / (count * d_bpr), 3) if d_traffic else None,
+                            "per_step_us": {k: round(v[0], 2) for k, v in cands.items()},
+                            "timing": "HIP events on the kernel's dispatch packet, every launch of the timed region"}
         if iso:
             a_iso = count * bpr / (iso * 1e-6) / 1e9
             roof["isolated"] = {"avg_us": round(iso, 2), "achieved": round(a_iso, 1),
                                 "frac": round(a_iso / HBM_PEAK_GBS, 4), "launches": args.iso_launches,
                                 "note": "same kernel, same batch, launched alone after the timed region"}
+    sort_mark, fused_mark = pipe.sort_mark, pipe.fused_mark
+    c3 = None
+    if world == 1 and not args.no_c3 and args.emulate_ranks == 1:
+        del pipe, batch, codes
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        c3 = c3_workload(args.c3_reads, steps=args.c3_steps, warmup=1)
     e2e = None
     if not args.no_end_to_end and args.emulate_ranks == 1:
         e2e = end_to_end(codes_h[: min(count, 10_000_000)], L, md)
@@ -500,8 +669,8 @@ def main():
                                  "rounds1f": "root-chasing hook rounds + one flatten",
                                  "edges": "one clique sweep + rounds over the crossing edges"}[args.global_mode],
                    "h3_bitmap": ("LDS code slices" if args.mark in ("auto", "slices") and 7 <= L <= 12 else
-                                 "partition sort + LDS bitmap") if pipe.sort_mark else
-                                ("mark fused in score kernel" if pipe.fused_mark else "XCD-partitioned mark"),
+                                 "partition sort + LDS bitmap") if sort_mark else
+                                ("mark fused in score kernel" if fused_mark else "XCD-partitioned mark"),
                    "parallelism": f"dp{world} shard-by-record + presence-bitmap all-gather"
                                   + (f" (rank 0 of {args.emulate_ranks} EMULATED on one GPU, no RCCL)"
                                      if args.emulate_ranks > 1 else "")},
@@ -509,6 +678,7 @@ def main():
         "sustained": sustained,
         "settle": {"seconds": args.settle_seconds, "steps": settle_steps} if settle_steps else None,
         "end_to_end": e2e,
+        "c3": c3,
         "cpu_baseline": cpu,
         "kernels_us": breakdown,
     }

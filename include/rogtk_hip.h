@@ -212,6 +212,11 @@ int rogtk_cluster_rounds(const void* ws, void* stream, int* rounds);
  * (1..64; 0 restores the default of 4). Process-wide. Fewer rounds never change
  * results: the rest run when assign / stats find the flags not yet converged. */
 int rogtk_cluster_set_spec_rounds(int n);
+/* Tests: polls a block of the single-pass rank-table scan makes on a predecessor's
+ * look-back flag before it recounts its prefix from the bitmaps itself (>= 0; -1 restores
+ * the default of 2^22). Process-wide. Never changes results: 0 forces the recount in
+ * every block. */
+int rogtk_cluster_set_lookback_polls(int n);
 /* Local presence bitmap straight from the codes (7 <= umi_len <= 13), replacing
  * rogtk_cluster_mark + rogtk_cluster_local_bitmap: an 8-bit radix pass groups the codes
  * by code partition, then one workgroup per partition builds its slice of the bitmap in
@@ -586,7 +591,8 @@ int rogtk_plugin_kwargs_debug(const uint8_t* kwargs, int64_t len, char* out, int
 
 /* Launch-bracketing HIP events (on the launch stream) around the library's kernels. */
 int rogtk_profile_enable(int on);
-/* Restricts the bracketing to one kernel name (below); NULL or "" = every kernel. Each
+/* Restricts the bracketing to one kernel name (below) or a comma-separated list of them;
+ * NULL or "" = every kernel. Each
  * bracketed launch adds two event records to its stream, so a timed region should
  * select only the kernel it reports. */
 int rogtk_profile_select(const char* kernel);
@@ -594,7 +600,9 @@ int rogtk_profile_reset(void);
 /* Total device milliseconds and launch count recorded for `kernel` (synchronises
  * the recorded events). Kernel names: "stage", "score_packed", "score_rows",
  * "cluster_mark", "cluster_bitmap", "cluster_scan", "cluster_compact",
- * "cluster_union", "cluster_flatten", "cluster_label", "cluster_assign". */
+ * "cluster_union", "cluster_flatten", "cluster_label", "cluster_assign", "cluster_irregular",
+ * "bam_fields", "bam_scan", "bam_fill", "pack_reads", "row_gather", "kmer_lds" (the last
+ * three and score_packed: events on the dispatch packet = kernel execution time). */
 int rogtk_profile_read(const char* kernel, double* total_ms, int64_t* launches);
 /* Kernels that support it (k_score_packed) also time their own execution span while
  * profiled: max over workgroups of the exit clock - min of the entry clock (device

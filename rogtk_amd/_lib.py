@@ -115,6 +115,7 @@ SIGNATURES = {
     "rogtk_cluster_release": [_vp],
     "rogtk_cluster_rounds": [_vp, _vp, ctypes.POINTER(ctypes.c_int)],
     "rogtk_cluster_set_spec_rounds": [_i32],
+    "rogtk_cluster_set_lookback_polls": [_i32],
     "rogtk_cluster_set_global_mode": [_i32],
     "rogtk_cluster_set_edge_cap": [ctypes.c_int64],
     "rogtk_cluster_set_mark_method": [_i32],

@@ -37,7 +37,8 @@ const char* const kKernelNames[K_COUNT_] = {
     "stage",          "score_packed",   "score_rows",    "cluster_mark",
     "cluster_bitmap", "cluster_scan",   "cluster_compact", "cluster_union",
     "cluster_flatten", "cluster_label", "cluster_assign", "cluster_irregular",
-    "bam_fields",     "bam_scan",       "bam_fill"};
+    "bam_fields",     "bam_scan",       "bam_fill",      "pack_reads",
+    "row_gather",     "kmer_lds"};
 
 namespace {
 std::atomic<bool> g_prof{false};
@@ -870,6 +871,7 @@ int rogtk_cluster_rounds(const void* ws, void* stream, int* rounds) {
 }
 
 int rogtk_cluster_set_spec_rounds(int n) { return cluster_set_spec_rounds(n); }
+int rogtk_cluster_set_lookback_polls(int n) { return cluster_set_lookback_polls(n); }
 int rogtk_cluster_set_global_mode(int mode) { return cluster_set_global_mode(mode); }
 int rogtk_cluster_set_edge_cap(int64_t pairs) { return cluster_set_edge_cap(pairs); }
 int rogtk_cluster_set_mark_method(int method) { return cluster_set_mark_method(method); }
@@ -1191,13 +1193,23 @@ int rogtk_profile_select(const char* kernel) {
         g_prof_mask.store(~0u);
         return ROGTK_OK;
     }
-    for (int k = 0; k < K_COUNT_; ++k)
-        if (std::strcmp(kernel, kKernelNames[k]) == 0) {
-            g_prof_mask.store(1u << k);
-            return ROGTK_OK;
+    // one name or a comma-separated list
+    uint32_t mask = 0;
+    for (const char* p = kernel; *p;) {
+        const char* e = std::strchr(p, ',');
+        const size_t len = e ? (size_t)(e - p) : std::strlen(p);
+        int found = -1;
+        for (int k = 0; k < K_COUNT_; ++k)
+            if (std::strlen(kKernelNames[k]) == len && std::strncmp(p, kKernelNames[k], len) == 0) found = k;
+        if (found < 0) {
+            set_error("profile_select: unknown kernel '%.*s'", (int)len, p);
+            return ROGTK_E_INVALID;
         }
-    set_error("profile_select: unknown kernel '%s'", kernel);
-    return ROGTK_E_INVALID;
+        mask |= 1u << found;
+        p += len + (e ? 1 : 0);
+    }
+    g_prof_mask.store(mask);
+    return ROGTK_OK;
 }
 
 int rogtk_profile_reset(void) {

@@ -33,6 +33,7 @@
 //   roots   ballot root flags into an index-space bitmap; scan = dense cluster ids
 //   label   labelcode[code] (L <= 13) or ilab[i] := dense id (index space)
 //   assign  cluster_id[row] = label(code[row])
+#include <hip/hip_ext.h>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -251,10 +252,14 @@ __global__ __launch_bounds__(kBlock) void k_rt(const uint64_t* __restrict__ G, i
 // an inclusive prefix. Status and value share one 64-bit word, so relaxed device-scope
 // atomics suffice (no release / acquire fences: on gfx950 those write back / invalidate
 // the whole L2, which the kernels running beside the resolve share). Workgroups are
-// dispatched in order, so every predecessor is resident or done: the waits end. The tag
-// (per workspace, new for every launch) makes flags of earlier launches invalid without a
-// clearing pass; a wait that never ends (it cannot, short of a bug) gives up after ~4M
-// polls and flags the launch's error word instead of hanging the queue.
+// dispatched in order, so every predecessor is resident or done and the waits end. The
+// tag (per workspace, new for every launch) makes flags of earlier launches invalid
+// without a clearing pass.
+// A wait is still bounded (max_polls, ~4M polls of ~64 clocks by default): a block that
+// gives up computes its prefix itself from the input bitmaps (every block total is a
+// function of the bitmaps alone), so the result never depends on scheduling and no error
+// state exists. rogtk_cluster_set_lookback_polls(0) forces that path for every block
+// (tests/test_gpu_parity.py::test_lookback_fallback_exact).
 constexpr uint64_t kLbAgg = 1, kLbIncl = 2;
 constexpr int kLbMaxPolls = 1 << 22;
 
@@ -262,10 +267,29 @@ __device__ __forceinline__ uint64_t lb_word(uint32_t tag, uint64_t status, uint3
     return ((uint64_t)tag << 34) | (status << 32) | v;
 }
 
+// popcount of the OR of n_bitmaps bitmaps over words [w0, w1), summed over the block
+// (every thread gets the sum); the look-back's fallback
+__device__ uint32_t block_popcount_or(const uint64_t* __restrict__ bitmaps, int n_bitmaps, int64_t words,
+                                      int64_t w0, int64_t w1, uint32_t* s_wave) {
+    uint32_t c = 0;
+    for (int64_t w = w0 + threadIdx.x; w < w1; w += kBlock) {
+        uint64_t v = 0;
+        for (int r = 0; r < n_bitmaps; ++r) v |= bitmaps[(int64_t)r * words + w];
+        c += (uint32_t)__popcll(v);
+    }
+    uint32_t total;
+    (void)block_excl_scan(c, s_wave, total);
+    return total;
+}
+
 // Exclusive prefix of `total` over blocks 0..blockIdx.x-1 (every thread of the block gets
-// it). A wait that gives up stores the tag into lb[gridDim.x] (the launch's error word).
-__device__ uint32_t lookback_excl(uint64_t* lb, uint32_t tag, uint32_t total, uint32_t* s_x) {
+// it). A wait that reaches max_polls hands over to the block-wide fallback.
+__device__ uint32_t lookback_excl(uint64_t* lb, uint32_t tag, uint32_t total, int max_polls,
+                                  const uint64_t* __restrict__ bitmaps, int n_bitmaps, int64_t words,
+                                  uint32_t* s_x, uint32_t* s_gave_up, uint32_t* s_wave) {
     const int b = blockIdx.x;
+    if (threadIdx.x == 0) *s_gave_up = 0;
+    __syncthreads();
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         if (b == 0) {
@@ -277,6 +301,7 @@ __device__ uint32_t lookback_excl(uint64_t* lb, uint32_t tag, uint32_t total, ui
             if (lane == 0)
                 __hip_atomic_store(&lb[b], lb_word(tag, kLbAgg, total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             uint32_t excl = 0;
+            bool gave_up = false;
             int j = b - 1;
             for (int polls = 0;; ++polls) {
                 const int idx = j - lane;
@@ -288,9 +313,8 @@ __device__ uint32_t lookback_excl(uint64_t* lb, uint32_t tag, uint32_t total, ui
                 const int fi = incl ? __ffsll((unsigned long long)incl) - 1 : 63;  // lanes 0..fi are needed
                 const uint64_t need = fi == 63 ? ~0ull : ((2ull << fi) - 1);
                 if (__ballot(!ready) & need) {
-                    if (polls >= kLbMaxPolls) {
-                        if (lane == 0)
-                            __hip_atomic_store(&lb[gridDim.x], (uint64_t)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (polls >= max_polls) {
+                        gave_up = true;
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
@@ -304,13 +328,25 @@ __device__ uint32_t lookback_excl(uint64_t* lb, uint32_t tag, uint32_t total, ui
                 j -= 64;
             }
             if (lane == 0) {
-                __hip_atomic_store(&lb[b], lb_word(tag, kLbIncl, excl + total), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-                *s_x = excl;
+                if (gave_up) {
+                    *s_gave_up = 1;
+                } else {
+                    __hip_atomic_store(&lb[b], lb_word(tag, kLbIncl, excl + total), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    *s_x = excl;
+                }
             }
         }
     }
     __syncthreads();
+    if (*s_gave_up) {  // block-uniform: recount every word before this block
+        const uint32_t excl = block_popcount_or(bitmaps, n_bitmaps, words, 0, (int64_t)b * kScanWords, s_wave);
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(&lb[b], lb_word(tag, kLbIncl, excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *s_x = excl;
+        }
+        __syncthreads();
+    }
     return *s_x;
 }
 
@@ -323,9 +359,9 @@ __global__ __launch_bounds__(kBlock) void k_scan_rt(const uint64_t* __restrict__
                                                     uint64_t* __restrict__ zero, int64_t zero_words,
                                                     uint64_t* agg, uint64_t* lb, uint32_t tag,
                                                     unsigned long long* __restrict__ stats, int slot, int copy_slot,
-                                                    int p0_L, bool local8_big_on) {
+                                                    int p0_L, bool local8_big_on, int max_polls) {
     __shared__ uint32_t s_wave[kBlock / 64];
-    __shared__ uint32_t s_x;
+    __shared__ uint32_t s_x, s_gave_up;
     __shared__ unsigned int s_max;
     const int64_t w0 = (int64_t)blockIdx.x * kScanWords + 4 * threadIdx.x;
     uint64_t v[4] = {0, 0, 0, 0};
@@ -354,7 +390,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_rt(const uint64_t* __restrict__
     uint32_t ex = block_excl_scan(tsum, s_wave, total);
     if (threadIdx.x == 0)  // the block's total, tagged, for the last block's maximum
         __hip_atomic_store(&agg[blockIdx.x], ((uint64_t)tag << 32) | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ex += lookback_excl(lb, tag, total, &s_x);
+    ex += lookback_excl(lb, tag, total, max_polls, bitmaps, n_bitmaps, words, &s_x, &s_gave_up, s_wave);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int64_t w = w0 + k;
@@ -362,31 +398,37 @@ __global__ __launch_bounds__(kBlock) void k_scan_rt(const uint64_t* __restrict__
         ex += c[k];
     }
     if (blockIdx.x != gridDim.x - 1) return;
-    // the last block: every predecessor published (its inclusive prefix needed them all)
+    // the last block: the largest block total (a block whose total is not published within
+    // max_polls is recounted from the bitmaps by this thread)
     const uint32_t n_distinct = s_x + total;
     if (threadIdx.x == 0) s_max = 0;
     __syncthreads();
     unsigned int mx = 0;
     for (int64_t b = threadIdx.x; b < gridDim.x; b += kBlock) {
         uint64_t a = __hip_atomic_load(&agg[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int polls = 0; (uint32_t)(a >> 32) != tag && polls < kLbMaxPolls; ++polls) {
+        for (int polls = 0; (uint32_t)(a >> 32) != tag && polls < max_polls; ++polls) {
             __builtin_amdgcn_s_sleep(1);
             a = __hip_atomic_load(&agg[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if ((uint32_t)(a >> 32) != tag)
-            __hip_atomic_store(&lb[gridDim.x], (uint64_t)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        mx = max(mx, (unsigned int)a);
+        uint32_t t = (uint32_t)a;
+        if ((uint32_t)(a >> 32) != tag) {
+            t = 0;
+            const int64_t e = min<int64_t>(words, (b + 1) * kScanWords);
+            for (int64_t w = b * kScanWords; w < e; ++w) {
+                uint64_t x = 0;
+                for (int r = 0; r < n_bitmaps; ++r) x |= bitmaps[(int64_t)r * words + w];
+                t += (uint32_t)__popcll(x);
+            }
+        }
+        mx = max(mx, (unsigned int)t);
     }
     atomicMax(&s_max, mx);
-    __syncthreads();
-    const bool err = __hip_atomic_load(&lb[gridDim.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tag;
     __syncthreads();
     if (threadIdx.x < kStatsBytes / 8) stats[threadIdx.x] = 0;  // stats + round flags
     __syncthreads();
     if (threadIdx.x == 0) {
         stats[slot] = n_distinct;
         if (copy_slot >= 0) stats[copy_slot] = n_distinct;
-        if (err) stats[S_ERROR] = 1;
         if (p0_L > 0) {
             const bool big = s_max > (unsigned int)kLocal8Cap && local8_big_on;
             stats[S_P0] = (p0_L >= 8 && s_max <= (unsigned int)(big ? kLocal8BigCap : kLocal8Cap)) ? 8 : 7;
@@ -1523,78 +1565,6 @@ __global__ __launch_bounds__(kBlock) void k_roots_scan(const uint32_t* __restric
     }
 }
 
-// k_roots_scan + the block-offset scan (k_scan_blocks) in one launch: after its in-block
-// prefix each workgroup takes its offset by the decoupled look-back of k_scan_rt (relaxed
-// device-scope atomics, tagged flags in lb), so rblkoff is written here and the last
-// workgroup writes the cluster count. One kernel boundary fewer on the resolve chain.
-__global__ __launch_bounds__(kBlock) void k_roots_scan_lb(const uint32_t* __restrict__ f,
-                                                          const uint64_t* __restrict__ lroot, int64_t max_distinct,
-                                                          int64_t rwords, uint64_t* __restrict__ rbits,
-                                                          uint32_t* __restrict__ rpref, uint32_t* __restrict__ rblkoff,
-                                                          unsigned long long* stats, unsigned long long* host,
-                                                          unsigned long long* epoch, uint64_t* lb, uint32_t tag) {
-    __shared__ uint32_t s_cnt[kRootWords];
-    __shared__ uint32_t s_total, s_x;
-    if (host && blockIdx.x == 0) {
-        for (int k = threadIdx.x; k < kStatsBytes / 8; k += kBlock)
-            __hip_atomic_store(host + k, stats[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const unsigned long long e = *epoch + 1;  // one publish per resolve: no race
-            *epoch = e;
-            __hip_atomic_store(host + kStatsBytes / 8, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
-    const int64_t nd = live_distinct(stats, max_distinct);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    constexpr int kPerWave = kRootWords / (kBlock / 64);  // 16
-    const int64_t w0 = (int64_t)blockIdx.x * kRootWords + wave * kPerWave;
-    uint32_t fv[kPerWave];
-    uint64_t lr[kPerWave];
-#pragma unroll
-    for (int k = 0; k < kPerWave; ++k) {
-        const int64_t i = (w0 + k) * 64 + lane;
-        lr[k] = (w0 + k) * 64 < nd ? lroot[w0 + k] : 0ull;
-        fv[k] = i < nd ? f[i] : 0u;
-    }
-    uint64_t mine = 0;
-#pragma unroll
-    for (int k = 0; k < kPerWave; ++k) {
-        const int64_t i = (w0 + k) * 64 + lane;
-        const uint64_t m = __ballot(i < nd && ((lr[k] >> lane) & 1ull) && fv[k] == (uint32_t)i);
-        if (lane == k) mine = m;
-    }
-    if (lane < kPerWave) {
-        const int64_t w = w0 + lane;
-        if (w < rwords) rbits[w] = mine;
-        s_cnt[wave * kPerWave + lane] = (uint32_t)__popcll(mine);
-    }
-    __syncthreads();
-    if (wave == 0) {
-        const uint32_t v = lane < kRootWords ? s_cnt[lane] : 0u;
-        uint32_t incl = v;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t t = __shfl_up(incl, off);
-            if (lane >= off) incl += t;
-        }
-        const int64_t w = (int64_t)blockIdx.x * kRootWords + lane;
-        if (lane < kRootWords && w < rwords) rpref[w] = incl - v;
-        if (lane == kRootWords - 1) s_total = incl;
-    }
-    __syncthreads();
-    const uint32_t total = s_total;
-    const uint32_t excl = lookback_excl(lb, tag, total, &s_x);
-    if (threadIdx.x == 0) {
-        rblkoff[blockIdx.x] = excl;
-        if (blockIdx.x == gridDim.x - 1) {
-            rblkoff[gridDim.x] = excl + total;
-            stats[S_NCLUSTERS] = excl + total;
-            if (__hip_atomic_load(&lb[gridDim.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tag) stats[S_ERROR] = 1;
-        }
-    }
-}
-
 __device__ __forceinline__ uint32_t root_label(uint32_t r, const uint64_t* __restrict__ rbits,
                                                const uint32_t* __restrict__ rpref,
                                                const uint32_t* __restrict__ rblkoff) {
@@ -1624,7 +1594,7 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
                                                        const uint32_t* __restrict__ rblkoff,
                                                        uint32_t* __restrict__ wlab, uint64_t* __restrict__ wexc,
                                                        uint32_t* __restrict__ labelcode, uint32_t* __restrict__ ilab,
-                                                       uint32_t* __restrict__ wlab2, int use_exc, int exc1_on) {
+                                                       uint2* __restrict__ wxl, int use_exc, int exc1_on) {
     for (int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x; w < words; w += (int64_t)gridDim.x * kBlock) {
         const uint32_t ur = UR[w];
         uint32_t root = kNone;
@@ -1682,24 +1652,19 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
         // the word stays unlabelled) get their own label (f[i] is their root: they are
         // live); a uniform word (ur != kNone) always has a label
         uint64_t per_code = lab == kNone ? m : exc;
-        // a word whose exceptions all lie in ONE other component also gets that label
-        // (wlab2): assign then reads it from a 1 MB table instead of gathering per code
-        uint32_t lab2 = kNone;
-        bool one2 = lab != kNone;
-        while (per_code) {
+        uint32_t xl[2] = {kNone, kNone};  // the first two exceptions' labels (inline forms)
+        for (int j = 0; per_code; ++j) {
             const int b = __ffsll((long long)per_code) - 1;
             per_code &= per_code - 1;
             const uint32_t i = e.z + (uint32_t)__popcll(m & ((1ull << b) - 1ull));
-            if ((int64_t)i >= max_distinct) {
-                one2 = false;
-                continue;
-            }
+            if ((int64_t)i >= max_distinct) continue;
             const uint32_t li = root_label(f[i], rbits, rpref, rblkoff);
             put_label((uint64_t)w * 64 + b, i, li, labelcode, ilab);
-            if (lab2 == kNone) lab2 = li;
-            else if (li != lab2) one2 = false;
+            if (j < 2) xl[j] = li;
         }
-        if (wlab2) wlab2[w] = (exc && one2) ? lab2 : kNone;
+        // the inline forms' exception labels (decode_word_label): one 8-B store per such
+        // word, read only by exception rows
+        if (wxl && lab != kNone && (lab >> 31) && (lab & 0x60000000u)) wxl[w] = make_uint2(xl[0], xl[1]);
     }
 }
 
@@ -1709,11 +1674,8 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
 // cost a second (2 MB-table) load; a single exception code is named in the label.
 __device__ __forceinline__ uint32_t word_label_of(const uint32_t* __restrict__ wlab,
                                                   const uint64_t* __restrict__ wexc,
-                                                  const uint32_t* __restrict__ wlab2, uint64_t c) {
-    const uint32_t wl = wlab[c >> 6];
-    const uint32_t r = decode_word_label(wl, wexc, c);
-    if (r != kNone || wl == kNone) return r;
-    return wlab2 ? wlab2[c >> 6] : kNone;  // the word's other component, or per code
+                                                  const uint2* __restrict__ wxl, uint64_t c) {
+    return decode_word_label(wlab[c >> 6], wexc, wxl, c);
 }
 
 // MODE 0: labelcode[code]; MODE 1: flab[rank(code)] (labels by index, ilab).
@@ -1730,7 +1692,7 @@ __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ flab,
                                                    const uint4* __restrict__ RT, const uint32_t* __restrict__ wlab,
                                                    const uint64_t* __restrict__ wexc,
-                                                   const uint32_t* __restrict__ wlab2, uint32_t* __restrict__ out) {
+                                                   const uint2* __restrict__ wxl, uint32_t* __restrict__ out) {
     constexpr int64_t kTile = 256 * G;  // rows per wave and trip
     const int lane = threadIdx.x & 63;
     const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
@@ -1758,7 +1720,7 @@ __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ 
             for (int k = 0; k < 4; ++k) {
                 id[g][k] = 0xFFFFFFFFu;
                 if ((reg[g] >> k) & 1u) {
-                    const uint32_t wl = wlab ? word_label_of(wlab, wexc, wlab2, c[g][k]) : kNone;
+                    const uint32_t wl = wlab ? word_label_of(wlab, wexc, wxl, c[g][k]) : kNone;
                     id[g][k] = wl != kNone ? wl
                                : MODE == 0 ? labelcode[c[g][k]]
                                            : flab[rt_rank(RT[c[g][k] >> 6], c[g][k])];
@@ -1785,14 +1747,14 @@ __global__ __launch_bounds__(kBlock) void k_lookup(const uint64_t* __restrict__ 
                                                    const uint32_t* __restrict__ flab, const uint4* __restrict__ RT,
                                                    const uint32_t* __restrict__ wlab,
                                                    const uint64_t* __restrict__ wexc,
-                                                   const uint32_t* __restrict__ wlab2, uint32_t* __restrict__ out) {
+                                                   const uint2* __restrict__ wxl, uint32_t* __restrict__ out) {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nq; i += (int64_t)gridDim.x * kBlock) {
         const uint64_t c = q[i];
         uint32_t lab = kNone;
         if (c < nbits) {
             const uint4 e = RT[c >> 6];
             if ((rt_word(e) >> (c & 63)) & 1ull) {
-                const uint32_t wl = wlab ? word_label_of(wlab, wexc, wlab2, c) : kNone;
+                const uint32_t wl = wlab ? word_label_of(wlab, wexc, wxl, c) : kNone;
                 lab = wl != kNone ? wl : MODE == 0 ? labelcode[c] : flab[rt_rank(e, (uint32_t)c)];
             }
         }
@@ -1807,18 +1769,6 @@ inline int grid_for(int64_t lanes, int64_t cap = 0) {
     return (int)g;
 }
 
-// ROGTK_WLAB2=1: a second word label (the one other component of a word's exceptions),
-// written by k_word_label and read by k_assign / k_lookup before the per-code gather.
-// A/B, off by default: the 1 MB table cost the assign more L2 misses than the per-code
-// gathers it saves (round 3: 129-130 vs 115-117 us per 10M-row assign, same box)
-inline bool wlab2_on() {
-    static const bool on = [] {
-        const char* e = getenv("ROGTK_WLAB2");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-
 struct WsPtrs {
     unsigned long long* stats;
     unsigned int* flags;
@@ -1827,7 +1777,8 @@ struct WsPtrs {
     uint4* RT;
     uint32_t *wpref, *blksum, *blkoff, *D, *f, *UR;
     uint64_t *rbits, *lroot;
-    uint32_t *rpref, *rblksum, *rblkoff, *labelcode, *ilab, *wlab2;
+    uint32_t *rpref, *rblksum, *rblkoff, *labelcode, *ilab;
+    uint2* wxl;
     uint64_t* active;
     unsigned long long* epoch;  // resolves published (k_roots_scan)
     uint64_t* lb;               // look-back flags of k_scan_rt (+ its error word)
@@ -1853,7 +1804,7 @@ inline WsPtrs ws_ptrs(const ClusterLayout& cl, uint8_t* ws) {
     p.rpref = (uint32_t*)(ws + cl.off_rpref);
     p.rblksum = (uint32_t*)(ws + cl.off_rblksum);
     p.rblkoff = (uint32_t*)(ws + cl.off_rblkoff);
-    p.wlab2 = (uint32_t*)(ws + cl.off_wlab2);
+    p.wxl = (uint2*)(ws + cl.off_wxl);
     p.labelcode = cl.label_by_code ? (uint32_t*)(ws + cl.off_labelcode) : nullptr;
     p.ilab = cl.label_by_code ? nullptr : (uint32_t*)(ws + cl.off_ilab);
     p.active = (uint64_t*)(ws + cl.off_active);
@@ -1920,7 +1871,7 @@ int cluster_layout(int L, int64_t max_distinct, ClusterLayout* o) {
     c.off_rpref = take(c.rwords * 4);
     c.off_rblksum = take(c.rblocks * 4);
     c.off_rblkoff = take((c.rblocks + 1) * 4);
-    c.off_wlab2 = take(c.words * 4);  // second label of two-component words (k_word_label)
+    c.off_wxl = take(c.words * 8);  // the inline forms' exception labels (k_word_label)
     c.off_labelcode = c.label_by_code ? take((int64_t)c.nbits * 4) : off;
     c.off_ilab = c.label_by_code ? off : take(max_distinct * 4);
     // hook-round frontier: one bit per (position, word group) task, two generations
@@ -2020,6 +1971,7 @@ constexpr int kGlobalRounds = 2;
 constexpr int kGlobalRoundsOneFlatten = 3;  // hook rounds that chase roots, one flatten per batch
 constexpr int kGlobalEdges = 4;             // one clique sweep, then rounds over the crossing edges
 std::atomic<int> g_global_mode{kGlobalRounds};
+std::atomic<int> g_lb_polls{kLbMaxPolls};  // look-back polls before the recount (tests)
 
 // Host-side state of an in-flight resolve, keyed by workspace: the round flags are
 // copied asynchronously to pinned host memory so resolve never blocks the host;
@@ -2144,14 +2096,8 @@ int enqueue_post_rounds(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
 // host_stats != nullptr: k_roots_scan also publishes the stats block (the resolve's
 // first labels pass; never the re-run after extra rounds, which the host waits for)
 int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
-                   unsigned long long* host_stats = nullptr, uint32_t tag = 0) {
-    if (tag) {
-        ProfScope prof(K_FLATTEN, s);
-        hipLaunchKernelGGL(k_roots_scan_lb, dim3((unsigned)cl.rblocks), dim3(kBlock), 0, s, p.f, p.lroot,
-                           cl.max_distinct, cl.rwords, p.rbits, p.rpref, p.rblkoff, p.stats, host_stats, p.epoch,
-                           p.lb, tag);
-        ROGTK_HIP_CHECK(hipGetLastError());
-    } else {
+                   unsigned long long* host_stats = nullptr) {
+    {
         ProfScope prof(K_FLATTEN, s);
         hipLaunchKernelGGL(k_roots_scan, dim3((unsigned)cl.rblocks), dim3(kBlock), 0, s, p.f, p.lroot,
                            cl.max_distinct, cl.rwords, p.rbits, p.rpref, p.rblksum,
@@ -2174,7 +2120,7 @@ int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
         }();
         hipLaunchKernelGGL(k_word_label, dim3(grid_for(cl.words, kPersistentGrid)), dim3(kBlock), 0, s, p.f, p.UR,
                            cl.words, p.RT, cl.max_distinct, p.rbits, p.rpref, p.rblkoff, p.wpref, p.G, p.labelcode,
-                           p.ilab, wlab2_on() ? p.wlab2 : nullptr, use_exc, exc1_on);
+                           p.ilab, p.wxl, use_exc, exc1_on);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     return ROGTK_OK;
@@ -2209,17 +2155,6 @@ bool fused_scan_enabled() {
     }();
     return on;
 }
-// ROGTK_ROOTS_LB=1: the look-back k_roots_scan_lb instead of the roots scan + a separate
-// block-offset scan (A/B; measured slower: 0.332-0.341 vs 0.315-0.324 ms/step,
-// profiles/r03z_resolve_ab.txt)
-bool roots_lb_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("ROGTK_ROOTS_LB");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-
 int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bitmaps, int n_bitmaps,
                     int max_distance, int mode, int spec, unsigned long long* host_stats, hipStream_t s,
                     int phases = 3, uint32_t scan_tag = 0) {
@@ -2229,7 +2164,7 @@ int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bi
                            p.RT, p.lroot, max_distance == 0 ? (int64_t)0 : cl.rwords,
                            p.lb + std::max(cl.blocks, cl.rblocks) + 1, p.lb, scan_tag,
                            p.stats, (int)S_NDISTINCT, max_distance == 0 ? (int)S_NCLUSTERS : -1,
-                           local8_enabled() ? cl.L : 0, local8_big_enabled());
+                           local8_enabled() ? cl.L : 0, local8_big_enabled(), g_lb_polls.load());
         if (max_distance == 0) {
             const int cgrid = grid_for((int64_t)std::min<uint64_t>(cl.nbits, 1ull << 30), 16384);
             hipLaunchKernelGGL(k_build_d, dim3(cgrid), dim3(kBlock), 0, s, p.RT, cl.nbits, p.D, p.f, p.labelcode, p.ilab,
@@ -2280,11 +2215,11 @@ int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bi
             // k_roots_scan stores the flags into mapped host memory and then the resolve's
             // epoch (counted on the device): no copy-engine transfer, no event, no kernel
             // of its own (a D2H copy + event record cost ~15 us of the resolve chain)
-            if (enqueue_labels(cl, p, s, host_stats, scan_tag && roots_lb_enabled() ? scan_tag + 1 : 0u)) return -1;
+            if (enqueue_labels(cl, p, s, host_stats)) return -1;
             return hipGetLastError() == hipSuccess ? launched : -1;
         }
     }
-    if (enqueue_labels(cl, p, s, nullptr, scan_tag && roots_lb_enabled() ? scan_tag + 1 : 0u)) return -1;
+    if (enqueue_labels(cl, p, s, nullptr)) return -1;
     return hipGetLastError() == hipSuccess ? launched : -1;
 }
 
@@ -2309,10 +2244,9 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
         if (int rc = finish_locked(ws, st, s)) return rc;
     }
     // a new look-back tag per single-pass scan (0 = the three-kernel scan)
-    // (two per resolve: k_scan_rt takes tag, k_roots_scan_lb tag + 1)
     auto next_tag = [&]() -> uint32_t {
         if (!fused_scan_enabled()) return 0;
-        st.scan_tag = st.scan_tag >= (1u << 30) - 2 ? 1u : st.scan_tag + 2;
+        st.scan_tag = st.scan_tag >= (1u << 30) - 1 ? 1u : st.scan_tag + 1;
         return st.scan_tag;
     };
     if (phases == 1) {  // the local phase alone; the global phase follows on another stream
@@ -2439,12 +2373,7 @@ int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone) 
     st.pending = false;
     ROGTK_REQUIRE(converged, ROGTK_E_HIP, "cluster: union rounds did not converge in %d rounds", kMaxRounds);
     if (int rc = enqueue_post_rounds(st.cl, p, s, st.mode)) return rc;
-    uint32_t tag = 0;
-    if (fused_scan_enabled() && roots_lb_enabled()) {  // a fresh look-back tag for the relabel
-        st.scan_tag = st.scan_tag >= (1u << 30) - 2 ? 1u : st.scan_tag + 2;
-        tag = st.scan_tag;
-    }
-    if (int rc = enqueue_labels(st.cl, p, s, nullptr, tag)) return rc;
+    if (int rc = enqueue_labels(st.cl, p, s, nullptr)) return rc;
     if (st.deferred.on) {  // the assign that ran on the speculative labels, again
         st.deferred.on = false;
         return enqueue_assign(st.cl, p, st.word_labels, st.deferred.codes, st.deferred.regbits, st.deferred.n,
@@ -2458,6 +2387,12 @@ int cluster_set_spec_rounds(int n) {
     ROGTK_REQUIRE(n >= 0 && n <= kMaxRounds, ROGTK_E_INVALID, "spec rounds %d outside 0..%d", n, kMaxRounds);
     g_spec_rounds.store(n == 0 ? kSpecRounds : n);
     g_spec_adaptive.store(n == 0);
+    return ROGTK_OK;
+}
+
+int cluster_set_lookback_polls(int n) {
+    ROGTK_REQUIRE(n >= -1, ROGTK_E_INVALID, "look-back polls %d < -1", n);
+    g_lb_polls.store(n < 0 ? kLbMaxPolls : n);
     return ROGTK_OK;
 }
 
@@ -2519,6 +2454,7 @@ int cluster_assign_prepare(const ClusterLayout& cl, const uint8_t* ws, const uin
                            bool deferred, AssignIn* a) {
     a->wlab = nullptr;
     a->wexc = nullptr;
+    a->wxl = nullptr;
     a->labelcode = nullptr;
     a->out = nullptr;
     if (!deferred)
@@ -2539,10 +2475,11 @@ int cluster_assign_prepare(const ClusterLayout& cl, const uint8_t* ws, const uin
             }
         }
     }
-    if (!wl || !cl.label_by_code || wlab2_on()) return ROGTK_OK;
+    if (!wl || !cl.label_by_code) return ROGTK_OK;
     WsPtrs p = ws_ptrs(cl, const_cast<uint8_t*>(ws));
     a->wlab = p.wpref;
     a->wexc = p.G;
+    a->wxl = p.wxl;
     a->labelcode = p.labelcode;
     a->out = cluster_id;
     return ROGTK_OK;
@@ -2564,10 +2501,10 @@ int launch_cluster_lookup(const ClusterLayout& cl, const uint8_t* ws, const uint
     const int g = grid_for(nq, 4096);
     if (cl.label_by_code)
         hipLaunchKernelGGL(k_lookup<0>, dim3(g), dim3(kBlock), 0, s, q, nq, cl.nbits, p.labelcode, p.D, p.RT, wlab,
-                           wexc, wlab && wlab2_on() ? p.wlab2 : nullptr, lab);
+                           wexc, wlab ? p.wxl : nullptr, lab);
     else
         hipLaunchKernelGGL(k_lookup<1>, dim3(g), dim3(kBlock), 0, s, q, nq, cl.nbits, p.labelcode, p.ilab, p.RT, wlab,
-                           wexc, wlab && wlab2_on() ? p.wlab2 : nullptr, lab);
+                           wexc, wlab ? p.wxl : nullptr, lab);
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
 }
@@ -2578,7 +2515,7 @@ int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, bool word_labels, c
     if (n <= 0) return ROGTK_OK;
     const uint32_t* wlab = word_labels ? p.wpref : nullptr;
     const uint64_t* wexc = word_labels ? p.G : nullptr;
-    ProfScope prof(K_ASSIGN, s);
+    ProfScope prof(K_ASSIGN, s, true);  // events on the dispatch packet (kernel time only)
     // Two workgroups per CU, grid-stride: assign runs beside the next batch's resolve,
     // whose hook rounds are latency-bound; a full grid of gathers (40k waves at 10M rows)
     // slowed the concurrent hook round 0 from 31 to 94 us. Measured at 10M rows, 2-deep
@@ -2601,8 +2538,9 @@ int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, bool word_labels, c
     }();
     const int g = grid_for((n + 4 * groups - 1) / (4 * groups), cap);
 #define ROGTK_ASSIGN_LAUNCH(M, G)                                                                                 \
-    hipLaunchKernelGGL((k_assign<M, G>), dim3(g), dim3(kBlock), 0, s, codes, regular_bits, n, p.labelcode,       \
-                       M == 0 ? p.D : p.ilab, p.RT, wlab, wexc, wlab && wlab2_on() ? p.wlab2 : nullptr, cluster_id)
+    hipExtLaunchKernelGGL((k_assign<M, G>), dim3(g), dim3(kBlock), 0, s, prof.start(), prof.stop(), 0, codes,    \
+                          regular_bits, n, p.labelcode,                                                       \
+                       M == 0 ? p.D : p.ilab, p.RT, wlab, wexc, wlab ? p.wxl : nullptr, cluster_id)
     if (cl.label_by_code) {
         if (groups == 1) ROGTK_ASSIGN_LAUNCH(0, 1);
         else if (groups == 4) ROGTK_ASSIGN_LAUNCH(0, 4);

@@ -19,6 +19,7 @@
 //   runs    run heads -> run count (saturating) + OR of exts -> CountFilter
 //   censor  binary search of each extension's neighbour inside the group's valid run
 //   out     entries at the group's capacity offset; host packs them densely
+#include <hip/hip_ext.h>
 #include <hipcub/hipcub.hpp>
 
 #include <cmath>
@@ -242,17 +243,30 @@ __global__ __launch_bounds__(R) void k_pack_reads(const int64_t* __restrict__ of
             const int64_t nw = (b1 - a4 + 3) >> 2;
             const uint32_t* src = reinterpret_cast<const uint32_t*>(values + a4);
             const int64_t full = (b1 - a4) >> 2;  // dwords entirely inside [a4, b1)
-            for (int64_t i = tid; i < nw; i += R) {
-                if (i < full) {
-                    in32[i] = src[i];
-                } else {  // the last partial dword, byte by byte
-                    uint32_t v = 0;
-                    for (int j = 0; j < 4; ++j) {
-                        const int64_t byte = a4 + 4 * i + j;
-                        if (byte < b1) v |= (uint32_t)values[byte] << (8 * j);
-                    }
-                    in32[i] = v;
+            // kStageBatch loads per lane in flight before their LDS writes: a one-dword-per-
+            // iteration loop waits a whole HBM round trip per dword (s_waitcnt vmcnt(0)
+            // before every ds_write), ~38 of them per 64-row trip
+            constexpr int kStageBatch = 16;
+            for (int64_t i0 = 0; i0 < full; i0 += (int64_t)R * kStageBatch) {
+                uint32_t v[kStageBatch];
+#pragma unroll
+                for (int u = 0; u < kStageBatch; ++u) {
+                    const int64_t i = i0 + (int64_t)u * R + tid;
+                    v[u] = i < full ? src[i] : 0u;
                 }
+#pragma unroll
+                for (int u = 0; u < kStageBatch; ++u) {
+                    const int64_t i = i0 + (int64_t)u * R + tid;
+                    if (i < full) in32[i] = v[u];
+                }
+            }
+            if (full < nw && tid == 0) {  // the last partial dword, byte by byte
+                uint32_t v = 0;
+                for (int j = 0; j < 4; ++j) {
+                    const int64_t byte = a4 + 4 * full + j;
+                    if (byte < b1) v |= (uint32_t)values[byte] << (8 * j);
+                }
+                in32[full] = v;
             }
             if (tid < 2) in32[nw + tid] = 0;  // the funnel shift below may read one dword past
         }
@@ -1361,9 +1375,10 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
         // at a fixed stride (row r at packed[r * S]: no offsets, no scan)
         if (int rc = c->packed.ensure((size_t)std::max<int64_t>(n_rows * stride, 1) * 8)) return rc;
         const int ggrid = grid_for((n_rows + 63) / 64 * 64 / kWavesPerBlock, 16384);
+        ProfScope prof(K_ROW_GATHER, s, true);
 #define ROGTK_GATHER(BW)                                                                                       \
-    hipLaunchKernelGGL(k_row_gather<BW>, dim3(ggrid), dim3(kBlock), 0, s, in.blocks, in.rows, n_rows, K, stride,  \
-                       in.gk, c->row_group.as<uint32_t>(), c->packed.as<uint64_t>(), c->row_obs.as<int64_t>(),  \
+    hipExtLaunchKernelGGL(k_row_gather<BW>, dim3(ggrid), dim3(kBlock), 0, s, prof.start(), prof.stop(), 0,      \
+                       in.blocks, in.rows, n_rows, K, stride, in.gk, c->row_group.as<uint32_t>(), c->packed.as<uint64_t>(), c->row_obs.as<int64_t>(),  \
                        c->row_len.as<int32_t>(), gstat)
         if (in.B == 8) ROGTK_GATHER(8);
         else if (in.B == 16) ROGTK_GATHER(16);
@@ -1409,11 +1424,14 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
     }
     if (lds) {
         // one workgroup per small group, straight from the packed rows
-        hipLaunchKernelGGL((k_kmer_lds<3, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)), dim3(kLdsBlock), 0, s,
-                           c->gdesc.as<GroupDesc>(), G,
+        {
+            ProfScope prof(K_KMER_LDS, s, true);
+            hipExtLaunchKernelGGL((k_kmer_lds<3, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)),
+                                  dim3(kLdsBlock), 0, s, prof.start(), prof.stop(), 0, c->gdesc.as<GroupDesc>(), G,
                            c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
                            c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
                            c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
+        }
         hipLaunchKernelGGL((k_kmer_lds<1, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)), dim3(kLdsBlock), 0, s,
                            c->gdesc.as<GroupDesc>(), G,
                            c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
@@ -1881,22 +1899,23 @@ int rogtk_pack_reads(const int64_t* offsets, const uint8_t* values, const uint8_
     }();
     const int rows_per_wg = variant <= 1 ? 256 : variant == 2 ? 128 : 64;
     const int g = (int)std::min<int64_t>((n + rows_per_wg - 1) / rows_per_wg, (int64_t)8192 * 256 / rows_per_wg);
+ProfScope prof(K_PACK_READS, s, true);
 #define ROGTK_PACK_LAUNCH(BW)                                                                                        \
     switch (variant) {                                                                                              \
         case 1:                                                                                                     \
-            hipLaunchKernelGGL((k_pack_reads<BW, 256, true>), dim3(g), dim3(256), 0, s, offsets, values, validity,   \
+            hipExtLaunchKernelGGL((k_pack_reads<BW, 256, true>), dim3(g), dim3(256), 0, s, prof.start(), prof.stop(), 0, offsets, values, validity,   \
                                validity_offset, n, blocks);                                                         \
             break;                                                                                                  \
         case 2:                                                                                                     \
-            hipLaunchKernelGGL((k_pack_reads<BW, 128, true>), dim3(g), dim3(128), 0, s, offsets, values, validity,   \
+            hipExtLaunchKernelGGL((k_pack_reads<BW, 128, true>), dim3(g), dim3(128), 0, s, prof.start(), prof.stop(), 0, offsets, values, validity,   \
                                validity_offset, n, blocks);                                                         \
             break;                                                                                                  \
         case 3:                                                                                                     \
-            hipLaunchKernelGGL((k_pack_reads<BW, 64, true>), dim3(g), dim3(64), 0, s, offsets, values, validity,     \
+            hipExtLaunchKernelGGL((k_pack_reads<BW, 64, true>), dim3(g), dim3(64), 0, s, prof.start(), prof.stop(), 0, offsets, values, validity,     \
                                validity_offset, n, blocks);                                                         \
             break;                                                                                                  \
         default:                                                                                                    \
-            hipLaunchKernelGGL((k_pack_reads<BW, 256, false>), dim3(g), dim3(256), 0, s, offsets, values, validity,  \
+            hipExtLaunchKernelGGL((k_pack_reads<BW, 256, false>), dim3(g), dim3(256), 0, s, prof.start(), prof.stop(), 0, offsets, values, validity,  \
                                validity_offset, n, blocks);                                                         \
     }
     if (block_words == 8) {

@@ -309,7 +309,7 @@ __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restr
             if (ASG) {
                 // word labels (decode_word_label, rogtk_internal.h)
 #pragma unroll
-                for (int k = 0; k < kRowsPerLane; ++k) wl[k] = decode_word_label(wl[k], A.wexc, c[k]);
+                for (int k = 0; k < kRowsPerLane; ++k) wl[k] = decode_word_label(wl[k], A.wexc, A.wxl, c[k]);
                 uint32_t id[kRowsPerLane];
 #pragma unroll
                 for (int k = 0; k < kRowsPerLane; ++k)

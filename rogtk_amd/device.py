@@ -280,6 +280,12 @@ def set_spec_rounds(n: int) -> None:
     _lib.call("rogtk_cluster_set_spec_rounds", int(n))
 
 
+def set_lookback_polls(n: int) -> None:
+    """Look-back polls of the single-pass rank-table scan before a block recounts its
+    prefix from the bitmaps (-1 = default; 0 forces the recount); results never change."""
+    _lib.call("rogtk_cluster_set_lookback_polls", int(n))
+
+
 GLOBAL_UNION_FIND, GLOBAL_ROUNDS, GLOBAL_ROUNDS_ONE_FLATTEN, GLOBAL_EDGES = 1, 2, 3, 4
 
 

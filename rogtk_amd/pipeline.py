@@ -32,6 +32,7 @@ wait for batch k-1's flags moves onto the critical cycle: 0.487 vs 0.430 ms/step
 """
 from __future__ import annotations
 
+import os
 from collections import deque
 from typing import Optional
 
@@ -40,6 +41,9 @@ import torch
 from . import device as D
 from .dist import gather_bitmaps
 from .dist import world as dist_world
+
+
+_ON_MAIN = object()  # slot.assigned: the assign ran on the main stream, no event recorded
 
 
 class _Slot:
@@ -184,6 +188,19 @@ class UmiPipeline:
         if reuse_gate == "resolve" and (on_assigned is not None or split_resolve):
             raise ValueError("reuse_gate='resolve' needs on_assigned=None and split_resolve=False")
         self.reuse_gate = reuse_gate
+        # lazy_assigned: with the assign, the mark and the slot-reuse gate all on the main
+        # stream, nothing waits for a slot's assign through an event: resolve(k + depth),
+        # which rewrites the tables assign(k) reads, waits for mark(k + depth) on the main
+        # stream, which the host enqueues after assign(k) because assign lags its batch by
+        # `lag` < depth submits. So no event is recorded after the assign (each record or
+        # wait on the main stream costs ~12 us of device time in the round-3 timeline); one
+        # is recorded on demand by settle().
+        # (ROGTK_PIPE_EVENTS=all: record / wait every hand-off as before, A/B)
+        self.all_events = os.environ.get("ROGTK_PIPE_EVENTS", "") == "all"
+        self.lazy_assigned = (not self.all_events and self.s_assign is self.main and self.s_mark is self.main and reuse_gate == "score"
+                              and assign_on == "main" and not fused_assign and on_assigned is None)
+        if self.lazy_assigned:
+            assert self.lag < len(self.slots), "the main stream must order assign(k) before mark(k + depth)"
 
     def submit(self, batch: D.PackedBatch):
         """Enqueue one batch; returns its slot. Scores and Hamming outputs are valid once the
@@ -193,7 +210,9 @@ class UmiPipeline:
         assign, not a settled one); the slot is settled before its reuse."""
         slot = self.slots[self.k % len(self.slots)]
         producer = torch.cuda.current_stream(self.main.device)  # batch producer -> main
-        if self.device_events:
+        if not self.all_events and (producer == self.main or producer.query()):
+            pass  # nothing pending on the producer: no hand-off (saves an event wait per step)
+        elif self.device_events:
             ready = D.StreamEvent()
             ready.record(producer)
             ready.wait(self.main)
@@ -383,6 +402,10 @@ class UmiPipeline:
         if self.on_assigned is not None:
             with torch.cuda.stream(self.s_assign):
                 self.on_assigned(slot, batch)
+        if self.lazy_assigned:
+            slot.assigned = _ON_MAIN  # ordered by the main stream; an event only on demand
+            self.last_assigned = None
+            return
         slot.assigned = self._event()
         slot.assigned.record(self.s_assign)
         self.last_assigned = slot.assigned
@@ -394,6 +417,9 @@ class UmiPipeline:
         while any(q[0] is slot for q in self.queue):
             self._score_assign_oldest() if self.fused_assign else self._assign_oldest()
         self._settle(slot, self.s_assign if self.assign_on != "resolve" else None)
+        if slot.assigned is _ON_MAIN:
+            slot.assigned = self._event()
+            slot.assigned.record(self.main)
         if slot.assigned is not None:
             D.wait_for(torch.cuda.current_stream(self.main.device), slot.assigned)
         return slot.cid

@@ -45,7 +45,6 @@ np.savez({path!r}, **{{k: v.cpu().numpy() for k, v in out.items()}})
 """
 
 KNOBS = [
-    ({"ROGTK_WLAB2": "1"}, "separate"),
     ({"ROGTK_LCC_LOOP": "1"}, "separate"),
     ({"ROGTK_LOCAL8": "0"}, "separate"),
     ({"ROGTK_SLICE_BUCKETS": "0"}, "separate"),
@@ -64,7 +63,6 @@ KNOBS = [
     ({"ROGTK_FUSED_SCAN": "0"}, "main"),
     ({"ROGTK_FUSED_SCAN": "0", "ROGTK_LOCAL8": "0"}, "separate"),
     ({"ROGTK_LOCAL8_SINGLE": "1"}, "main"),
-    ({"ROGTK_ROOTS_LB": "1"}, "separate"),
     ({"ROGTK_WORD_EXC1": "0"}, "main"),
 ]
 

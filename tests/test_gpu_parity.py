@@ -319,17 +319,24 @@ def test_cluster_dev_matches_host_long_and_short(rg):
         assert np.array_equal(cid.cpu().numpy().view(np.uint32), _np(host).astype(np.uint32))
 
 
-@pytest.mark.parametrize("L", [4, 6, 8, 12, 13, 16, 20, 32, 33])
-def test_cluster_irregular_families(rg, L):
+@pytest.mark.parametrize("L,utf8", [(4, 0), (6, 0), (8, 0), (12, 0), (13, 0), (16, 0), (20, 0), (32, 0), (33, 0),
+                                    (6, 0.1), (12, 0.1), (24, 0.1)])
+def test_cluster_irregular_families(rg, L, utf8):
     """SURVEY §8a H3.2 for every engine: strings with N, lowercase bytes and other lengths
     get Hamming-1 edges to each other and to regular codes (and bridge regular clusters);
-    host and device-column paths vs the oracle and the O(d^2) brute force."""
+    host and device-column paths vs the oracle and the O(d^2) brute force. utf8 > 0 adds
+    multi-byte UTF-8 members: H3 compares bytes, so the appended pin pair
+    A^(L-2)+U+00E9 / A^L (H2.1 distance 1: chars zipped) stays in two clusters."""
     import ctypes
     import torch
     from conftest import irregular_families
     from rogtk_amd import _lib
 
-    umis = irregular_families(L, 400 if L <= 8 else 700, L)
+    umis = irregular_families(L + int(utf8 * 1000), 400 if L <= 8 else 700, L, p_utf8=utf8)
+    if utf8:
+        assert any(0xC3 in u for u in umis if u)
+        pin = pa.array(umis[-2:], type=pa.large_binary())
+        assert _np(rg.hamming_distance(pin, b"A" * L)).tolist() == [1, 0]  # H2.1: chars zipped
     col = P().StrCol.from_list(umis)
     for md in (0, 1):
         rc, rv, rk, _ = P().umi_cluster(col, L, md)
@@ -351,6 +358,8 @@ def test_cluster_irregular_families(rg, L):
                   ctypes.byref(nk), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
         assert nk.value == rk
         assert np.array_equal(cid.cpu().numpy().view(np.uint32)[rv], rc[rv])
+        if utf8 and md == 1:
+            assert ref[-2] != ref[-1]  # byte-wise: 2 mismatches, no edge
 
 
 @pytest.mark.parametrize("L", [12, 24])
@@ -443,6 +452,28 @@ def test_device_pipeline_vs_oracle(rg):
     assert np.array_equal(bits, rw)
     rc, _, rk, _ = P().umi_cluster(col, 12, 1)
     assert stats["n_clusters"] == rk and stats["overflow"] == 0
+    assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc)
+
+
+@pytest.mark.parametrize("polls", [0, 1, 3])
+@pytest.mark.parametrize("md", [0, 1])
+def test_lookback_fallback_exact(rg, polls, md):
+    """The single-pass scan's bounded look-back (k_scan_rt): a block whose wait gives up
+    recounts its prefix from the bitmaps, so ids stay exact (a give-up used to
+    leave a partial prefix behind an unread error flag). polls=0 forces the recount in
+    every block, 1 / 3 mix it with published prefixes."""
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+
+    n = 2_000_000
+    try:
+        D.set_lookback_polls(polls)
+        codes_h, _, _, _, cid, stats = _device_run(n, md=md)
+    finally:
+        D.set_lookback_polls(-1)
+    col = P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, 12))
+    rc, _, rk, _ = P().umi_cluster(col, 12, md)
+    assert stats["n_clusters"] == rk and stats["overflow"] == 0 and stats["error"] == 0
     assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc)
 
 

@@ -189,16 +189,24 @@ def test_cluster_oracle_threads_identical():
                 assert got[2] == ref[2] and np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
 
 
-@pytest.mark.parametrize("seed,L", [(1, 4), (2, 6), (3, 12), (4, 20), (5, 33)])
-def test_cluster_oracle_vs_bruteforce_irregular_families(seed, L):
+@pytest.mark.parametrize("seed,L,utf8", [(1, 4, 0), (2, 6, 0), (3, 12, 0), (4, 20, 0), (5, 33, 0), (6, 6, 0.1),
+                                         (7, 12, 0.1)])
+def test_cluster_oracle_vs_bruteforce_irregular_families(seed, L, utf8):
+    """utf8 > 0: multi-byte UTF-8 members; H3 is byte-wise, so the pin pair
+    A^(L-2)+U+00E9 / A^L has H2.1 distance 1 (py_hamming zips chars) but no H3 edge."""
     from conftest import irregular_families
 
-    umis = irregular_families(seed, 120 if L <= 6 else 250, L)
+    umis = irregular_families(seed, 120 if L <= 6 else 250, L, p_utf8=utf8)
     for md in (0, 1):
         ref, rk = P.py_cluster_bruteforce(umis, L, md)
         cid, valid, k, rl = P.umi_cluster(P.StrCol.from_list(umis), L, md)
         assert rl == L and k == rk
         assert [int(c) if v else None for c, v in zip(cid, valid)] == ref
+        if utf8 and md == 1:
+            assert ref[-2] != ref[-1]
+    if utf8:
+        d, _, _ = P.hamming(P.StrCol.from_list(umis[-2:]), b"A" * L, 1)
+        assert list(d) == [1, 0]
 
 
 # ---------------------------------------------------------------- H4 k-mer oracle

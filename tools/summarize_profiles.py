@@ -64,6 +64,10 @@ def main():
                      "KB*1024; FETCH_SIZE doubled (gfx950 reports half of wide streaming reads, "
                      "MI355X_MICROARCH.md HBM section); WRITE_SIZE exact for 16-B/lane streaming stores",
            "kernels": kernels}
+    asg = [k for k in kernels if k.startswith("k_assign")]
+    if asg:  # bench.py's roofline.dominant reads this when k_assign takes the most time
+        out["assign_hbm_bytes_per_launch"] = kernels[asg[0]]["hbm_bytes"]
+        out["assign_bytes_per_read"] = round(kernels[asg[0]]["hbm_bytes"] / reads, 2)
     if sp:
         out["score_packed_hbm_bytes_per_launch"] = kernels[sp[0]]["hbm_bytes"]
         out["score_packed_bytes_per_read"] = round(kernels[sp[0]]["hbm_bytes"] / reads, 2)
