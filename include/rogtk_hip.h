@@ -544,6 +544,29 @@ typedef struct rogtk_bam_batch {
     const uint8_t* u32_validity[3];
 } rogtk_bam_batch;
 int rogtk_bam_open(const char* path, int n_threads, void** reader);
+/* One file split over workers / ranks (the reference: discover_split_points +
+ * process_file_segment_with_pool, src/bam_htslib.rs:247-420, driven by
+ * bam_to_arrow_ipc_htslib_bgzf_blocks :521). HOST ONLY (no GPU needed):
+ *   rogtk_bam_split_points: points[0..*n_ranges] (n + 1 entries of room) = 0, BGZF block
+ *     starts at or after file_size * i / n (validated: the block header and the next one),
+ *     file_size; never inside the header's blocks; fewer ranges when the file is small.
+ *   rogtk_bam_find_record: the bytes to skip at the start of the stream inflated from the
+ *     block at c_begin before the first record that starts there: the tail of a record that
+ *     straddles the split (the first offset from which 16 records, or all up to the end of
+ *     the file, pass the SAMv1 structural checks).
+ * rogtk_bam_open_range: a reader (as rogtk_bam_open) of the records that START in the
+ *   blocks [c_begin, c_end) (c_end < 0 or past the file: to the end), after skipping
+ *   `skip` bytes of the first block's stream (0 for c_begin 0, where the header is read).
+ *   Its last record may run into the next range's blocks; once the range is exhausted
+ *   (*n_records == 0), rogtk_bam_range_tail gives how many bytes of it lie past c_end,
+ *   i.e. the next range's exact skip (-1: the range ran to the end of the file). A caller
+ *   that used rogtk_bam_find_record for a range checks its skip against the previous
+ *   range's tail (and re-reads the range with the tail on a mismatch). */
+int rogtk_bam_split_points(const char* path, int n, int64_t* points, int* n_ranges);
+int rogtk_bam_find_record(const char* path, int64_t c_begin, int64_t* skip);
+int rogtk_bam_open_range(const char* path, int n_threads, int64_t c_begin, int64_t c_end, int64_t skip,
+                         void** reader);
+int rogtk_bam_range_tail(void* reader, int64_t* tail);
 /* Binary header: reference names (lossy UTF-8) as offsets / values, and the SAM text. */
 int rogtk_bam_header(void* reader, int64_t* n_ref, const int64_t** name_offsets, const uint8_t** name_values,
                      const char** text, int64_t* text_len);
@@ -552,7 +575,9 @@ int rogtk_bam_header(void* reader, int64_t* n_ref, const int64_t** name_offsets,
 int rogtk_bam_next(void* reader, int64_t max_records, int mode, int include_sequence, int include_quality,
                    int64_t* n_records, rogtk_bam_batch* out);
 /* Same, but the batch stays in DEVICE memory (valid until the next call). The decode is
- * enqueued on `stream` (NULL: the reader's own stream, synchronised before return). */
+ * enqueued on `stream` without a host wait (the columns' value buffers are sized from
+ * host-known bounds; rogtk_bam_check reports corrupt records); NULL: the reader's own
+ * stream, synchronised before return. */
 int rogtk_bam_next_dev(void* reader, int64_t max_records, int mode, int include_sequence, int include_quality,
                        int64_t* n_records, rogtk_bam_batch* out, void* stream);
 /* The UMI column of a device batch for the H1-H3 engine (config C5): source 0 = the first
@@ -561,6 +586,24 @@ int rogtk_bam_next_dev(void* reader, int64_t max_records, int mode, int include_
  * ROGTK_E_OVERFLOW beyond), validity bitmap (ceil(n/64) u64 words). Synchronises `stream`. */
 int rogtk_bam_umi_dev(const rogtk_bam_batch* batch, int64_t n, int source, int umi_len, int sep, int64_t* offsets,
                       uint8_t* values, int64_t values_cap, uint8_t* validity, void* stream);
+/* The same appended to a column of several batches with NO host synchronisation (config C5
+ * overlaps the host's inflate with the GPU): rows go to offsets[row_base ..] (n + 1
+ * entries; row_base a multiple of 64, validity words from row_base / 64), values at the
+ * column's running byte count *base (a device int64, updated on the device). Rows that
+ * would pass values_cap are not written and counted in *overflow (a device u64). */
+int rogtk_bam_umi_append(const rogtk_bam_batch* batch, int64_t n, int source, int umi_len, int sep,
+                         int64_t* offsets, uint8_t* values, int64_t values_cap, uint8_t* validity, int64_t row_base,
+                         int64_t* base, unsigned long long* overflow, void* stream);
+/* A device string column (offsets from 0, n + 1 entries) appended the same way. */
+int rogtk_bam_append_strings(const int64_t* src_offsets, const uint8_t* src_values, int64_t n, int64_t* offsets,
+                             uint8_t* values, int64_t values_cap, int64_t row_base, int64_t* base,
+                             unsigned long long* overflow, void* stream);
+/* Raw record bytes of the reader's current batch (bounds a device batch's columns: name
+ * <= 3 x bytes + 7 per record, sequence / qualities <= bytes). */
+int rogtk_bam_batch_bytes(void* reader, int64_t* bytes);
+/* rogtk_bam_next_dev batches do not synchronise: this checks, once, that no record of
+ * the device-mode batches so far overran its block_size (synchronises `stream`). */
+int rogtk_bam_check(void* reader, void* stream);
 int rogtk_bam_close(void* reader);
 /* Diagnostics: seconds spent so far in {file read, buffer moves + block framing, BGZF
  * inflate, record framing, H2D + GPU decode, D2H of host batches}. */

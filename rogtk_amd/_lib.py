@@ -134,12 +134,20 @@ SIGNATURES = {
     "rogtk_umi_cluster_dev": [_vp, _vp, _vp, _i64, _i32, _i32, _vp, ctypes.POINTER(_i64), _vp],
     "rogtk_route_pack": [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp],
     "rogtk_bam_open": [ctypes.c_char_p, _i32, ctypes.POINTER(_vp)],
+    "rogtk_bam_open_range": [ctypes.c_char_p, _i32, _i64, _i64, _i64, ctypes.POINTER(_vp)],
+    "rogtk_bam_range_tail": [_vp, _P_I64],
+    "rogtk_bam_split_points": [ctypes.c_char_p, _i32, _P_I64, _P_I32],
+    "rogtk_bam_find_record": [ctypes.c_char_p, _i64, _P_I64],
     "rogtk_bam_header": [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp),
                          ctypes.POINTER(_i64)],
     "rogtk_bam_next": [_vp, _i64, _i32, _i32, _i32, ctypes.POINTER(_i64), ctypes.POINTER(BamBatch)],
     "rogtk_bam_next_dev": [_vp, _i64, _i32, _i32, _i32, ctypes.POINTER(_i64), ctypes.POINTER(BamBatch), _vp],
     "rogtk_bam_umi_dev": [ctypes.POINTER(BamBatch), _i64, _i32, _i32, _i32, _vp, _vp, _i64, _vp, _vp],
     "rogtk_bam_close": [_vp],
+    "rogtk_bam_umi_append": [ctypes.POINTER(BamBatch), _i64, _i32, _i32, _i32, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp],
+    "rogtk_bam_append_strings": [_vp, _vp, _i64, _vp, _vp, _i64, _i64, _vp, _vp, _vp],
+    "rogtk_bam_batch_bytes": [_vp, _P_I64],
+    "rogtk_bam_check": [_vp, _vp],
     "rogtk_bam_timers": [_vp, _vp],
     "rogtk_copy": [_vp, _vp, _i64, _vp],
     "rogtk_plugin_kwargs_debug": [ctypes.c_char_p, _i64, ctypes.c_char_p, _i64, ctypes.POINTER(_i64)],

@@ -74,12 +74,53 @@ def _validity(ptr: int, n: int):
     return (pa.py_buffer(bits), nulls) if nulls else (None, 0)
 
 
-class BamReader:
-    """A BAM file open for GPU decoding (rogtk_bam_open / _next / _close)."""
+def bam_split_points(path: str, n: int) -> List[int]:
+    """Compressed offsets [0, b_1, .., file_size] cutting one BAM file into <= n ranges at
+    BGZF block starts near file_size * i / n (the reference's discover_split_points,
+    src/bam_htslib.rs:247-290; never inside the header's blocks). Host only."""
+    pts = (ctypes.c_int64 * (max(int(n), 1) + 1))()
+    k = ctypes.c_int()
+    _lib.call("rogtk_bam_split_points", os.fsencode(path), max(int(n), 1), pts, ctypes.byref(k))
+    return [int(pts[i]) for i in range(k.value + 1)]
 
-    def __init__(self, path: str, n_threads: int = 0):
+
+def bam_find_record(path: str, c_begin: int) -> int:
+    """Bytes to skip in the stream inflated from the block at c_begin before the first
+    record that starts in it (chained SAMv1 structural checks). Host only."""
+    skip = ctypes.c_int64()
+    _lib.call("rogtk_bam_find_record", os.fsencode(path), int(c_begin), ctypes.byref(skip))
+    return int(skip.value)
+
+
+class BamReader:
+    """A BAM file open for GPU decoding (rogtk_bam_open / _next / _close); with rng =
+    (c_begin, c_end, skip) only the records that start in the blocks [c_begin, c_end)
+    (rogtk_bam_open_range)."""
+
+    def __init__(self, path: str, n_threads: int = 0, rng=None):
         self._h = ctypes.c_void_p()
-        _lib.call("rogtk_bam_open", os.fsencode(path), int(n_threads), ctypes.byref(self._h))
+        if rng is None:
+            _lib.call("rogtk_bam_open", os.fsencode(path), int(n_threads), ctypes.byref(self._h))
+        else:
+            c0, c1, skip = rng
+            _lib.call("rogtk_bam_open_range", os.fsencode(path), int(n_threads), int(c0), int(c1), int(skip),
+                      ctypes.byref(self._h))
+
+    def tail(self) -> int:
+        """Bytes of this range's last record past its end (the next range's skip; -1: the
+        range ran to the end of the file). Valid once the range is exhausted."""
+        t = ctypes.c_int64()
+        _lib.call("rogtk_bam_range_tail", self._h, ctypes.byref(t))
+        return int(t.value)
+
+    def batch_bytes(self) -> int:
+        t = ctypes.c_int64()
+        _lib.call("rogtk_bam_batch_bytes", self._h, ctypes.byref(t))
+        return int(t.value)
+
+    def check(self, stream) -> None:
+        """Device-mode batches: fail if a record overran its block_size (syncs `stream`)."""
+        _lib.call("rogtk_bam_check", self._h, ctypes.c_void_p(stream.cuda_stream))
 
     def close(self) -> None:
         if self._h:
@@ -323,62 +364,108 @@ def _next_dev(reader: BamReader, max_records: int, mode: str, include_sequence: 
     return int(n.value), b
 
 
+class _DevColumn:
+    """A growable device string column (int64 offsets, values, validity words) that device
+    batches are appended to without host synchronisation (rogtk_bam_umi_append /
+    rogtk_bam_append_strings: the running byte count lives on the device; capacities grow
+    from host-known bounds, by copies enqueued on the same stream)."""
+
+    def __init__(self, dev, stream, rows: int = 1 << 20, nbytes: int = 1 << 24):
+        import torch
+        self.dev, self.stream = dev, stream
+        self.off = torch.empty(rows + 1, dtype=torch.int64, device=dev)
+        self.val = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+        self.vw = torch.zeros(rows // 64 + 1, dtype=torch.int64, device=dev)
+        self.base = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.ovf = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.rows = 0
+        self.bound = 0  # host-side upper bound of the value bytes used
+
+    def _reserve(self, n: int, nbytes: int) -> None:
+        import torch
+        rows, bound = self.rows + n, self.bound + nbytes
+        if rows + 1 > self.off.numel():
+            o = torch.empty(max(2 * self.off.numel(), rows + 1), dtype=torch.int64, device=self.dev)
+            o[: self.off.numel()].copy_(self.off)
+            self.off = o
+        if rows // 64 + 1 > self.vw.numel():
+            w = torch.zeros(max(2 * self.vw.numel(), rows // 64 + 1), dtype=torch.int64, device=self.dev)
+            w[: self.vw.numel()].copy_(self.vw)
+            self.vw = w
+        if bound > self.val.numel():
+            v = torch.empty(max(2 * self.val.numel(), bound), dtype=torch.uint8, device=self.dev)
+            v[: self.val.numel()].copy_(self.val)
+            self.val = v
+
+    def append_umi(self, b, n: int, src: int, umi_len: int, sep: str, bound: int) -> None:
+        self._reserve(n, bound)
+        _lib.call("rogtk_bam_umi_append", ctypes.byref(b), n, src, int(umi_len), ord(sep),
+                  ctypes.c_void_p(self.off.data_ptr()), ctypes.c_void_p(self.val.data_ptr()), self.val.numel(),
+                  ctypes.c_void_p(self.vw.data_ptr()), self.rows, ctypes.c_void_p(self.base.data_ptr()),
+                  ctypes.c_void_p(self.ovf.data_ptr()), ctypes.c_void_p(self.stream.cuda_stream))
+        self.rows += n
+        self.bound += bound
+
+    def append_strings(self, off_ptr: int, val_ptr: int, n: int, bound: int) -> None:
+        self._reserve(n, bound)
+        _lib.call("rogtk_bam_append_strings", ctypes.c_void_p(off_ptr), ctypes.c_void_p(val_ptr), n,
+                  ctypes.c_void_p(self.off.data_ptr()), ctypes.c_void_p(self.val.data_ptr()), self.val.numel(),
+                  self.rows, ctypes.c_void_p(self.base.data_ptr()), ctypes.c_void_p(self.ovf.data_ptr()),
+                  ctypes.c_void_p(self.stream.cuda_stream))
+        self.rows += n
+        self.bound += bound
+
+    def finish(self):
+        """(offsets [n + 1], values, validity words, n) on the device: one host sync."""
+        import torch
+        n = self.rows
+        if n == 0:
+            z = torch.zeros(1, dtype=torch.int64, device=self.dev)
+            return z, torch.zeros(1, dtype=torch.uint8, device=self.dev), torch.zeros(1, dtype=torch.int64,
+                                                                                      device=self.dev), 0
+        tot, ovf = (int(x) for x in torch.cat([self.base, self.ovf]).cpu().tolist())
+        if ovf:
+            raise _lib.RogtkError(_lib.ROGTK_E_OVERFLOW, f"bam column: {ovf} rows past the value capacity")
+        return self.off[: n + 1], self.val[: max(tot, 1)], self.vw[: (n + 63) // 64], n
+
+    def to_host_strings(self) -> pa.Array:
+        off, val, _, n = self.finish()
+        o = off.cpu().numpy() if n else np.zeros(1, np.int64)
+        v = val.cpu().numpy()[: int(o[-1])] if n else np.zeros(0, np.uint8)
+        return pa.Array.from_buffers(pa.large_string(), n, [None, pa.py_buffer(o), pa.py_buffer(v)]).cast(pa.string())
+
+
 def bam_umis_dev(bam_path: str, umi_len: int = 12, source: str = "sequence", sep: str = "_",
-                 mode: str = "htslib", n_threads: int = 0, with_names: bool = False):
-    """Decode a BAM file on the GPU and return its UMI column in HBM (torch tensors:
-    int64 offsets [n + 1], uint8 values, int64 validity words), plus the read names
-    (host pyarrow array) when asked. UMI = the first umi_len bases of SEQ ("sequence")
-    or the read name after its last `sep` byte ("name", UMI-tools READNAME_<UMI>)."""
+                 mode: str = "htslib", n_threads: int = 0, with_names: bool = False, rng=None,
+                 return_tail: bool = False):
+    """Decode a BAM file (or the range rng = (c_begin, c_end, skip) of it) on the GPU and
+    return its UMI column in HBM (torch tensors: int64 offsets [n + 1], uint8 values, int64
+    validity words, n), plus the read names (host pyarrow array) when asked, plus the
+    range's tail when asked. UMI = the first umi_len bases of SEQ ("sequence") or the read
+    name after its last `sep` byte ("name", UMI-tools READNAME_<UMI>). The host never waits
+    for the GPU inside the file: batches are decoded and appended on the current stream
+    while the reader inflates the next ones; one sync at the end."""
     import torch
 
     stream = torch.cuda.current_stream()
     dev = torch.device("cuda", torch.cuda.current_device())
     src = UMI_SOURCES[source]
-    offs, vals, valids, counts, names = [], [], [], [], []
-    with BamReader(bam_path, n_threads) as r:
+    umi = _DevColumn(dev, stream, nbytes=(1 << 20) * max(int(umi_len), 1))
+    names = _DevColumn(dev, stream, nbytes=1 << 26) if with_names else None
+    with BamReader(bam_path, n_threads, rng) as r:
         while True:
             n, b = _next_dev(r, DECODE_RECORDS, mode, src == 0, stream)
             if n == 0:
                 break
-            cap = n * umi_len if src == 0 else max(int(_dev_total(b, 0, n, stream)), 1)
-            off = torch.empty(n + 1, dtype=torch.int64, device=dev)
-            val = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
-            vw = torch.empty((n + 63) // 64, dtype=torch.int64, device=dev)
-            _lib.call("rogtk_bam_umi_dev", ctypes.byref(b), n, src, int(umi_len), ord(sep), ctypes.c_void_p(off.data_ptr()),
-                      ctypes.c_void_p(val.data_ptr()), cap, ctypes.c_void_p(vw.data_ptr()),
-                      ctypes.c_void_p(stream.cuda_stream))
-            offs.append(off)
-            vals.append(val[: int(off[-1].item())])
-            valids.append(vw)
-            counts.append(n)
-            if with_names:
-                names.append(_dev_string_to_host(b, 0, n, stream))
-    return _concat_dev(offs, vals, valids, counts, dev), (pa.concat_arrays(names) if with_names and names else None)
-
-
-def _dev_total(b, c, n, stream) -> int:
-    import torch
-    t = torch.empty(1, dtype=torch.int64, device="cuda")
-    _memcpy_dtod(t.data_ptr(), b.offsets[c] + 8 * n, 8, stream)
-    return int(t.item())
-
-
-def _memcpy_dtod(dst: int, src: int, nbytes: int, stream) -> None:
-    _lib.call("rogtk_copy", ctypes.c_void_p(dst), ctypes.c_void_p(src), int(nbytes),
-              ctypes.c_void_p(stream.cuda_stream))
-
-
-def _dev_string_to_host(b, c, n, stream) -> pa.Array:
-    import torch
-    off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
-    _memcpy_dtod(off.data_ptr(), b.offsets[c], 8 * (n + 1), stream)
-    tot = int(off[-1].item())
-    val = torch.empty(max(tot, 1), dtype=torch.uint8, device="cuda")
-    if tot:
-        _memcpy_dtod(val.data_ptr(), b.values[c], tot, stream)
-    o = off.cpu().numpy()
-    v = val[:tot].cpu().numpy()
-    return pa.Array.from_buffers(pa.large_string(), n, [None, pa.py_buffer(o), pa.py_buffer(v)]).cast(pa.string())
+            raw = r.batch_bytes()
+            name_bound = 3 * raw + 7 * n  # lossy UTF-8: <= 3 bytes per byte; "unknown"
+            umi.append_umi(b, n, src, umi_len, sep, n * int(umi_len) if src == 0 else name_bound)
+            if names is not None:
+                names.append_strings(b.offsets[0], b.values[0], n, name_bound)
+        r.check(stream)
+        tail = r.tail()
+    out = umi.finish(), (names.to_host_strings() if names is not None else None)
+    return out + (tail,) if return_tail else out
 
 
 def _concat_dev(offs, vals, valids, counts, dev):
@@ -423,27 +510,79 @@ def _umi_table(off, val, vw, n, names, cid, n_clusters, extra=None) -> pa.Table:
     return t.replace_schema_metadata({"n_clusters": str(int(n_clusters))})
 
 
+def _umi_ranges(bam_paths: Sequence[str], per_file: int, split: bool):
+    """[(file index, range index, c_begin, c_end)]: each file cut into up to `per_file`
+    ranges at BGZF block starts (bam_split_points) when split, else whole files."""
+    out = []
+    for fi, p in enumerate(bam_paths):
+        pts = bam_split_points(p, per_file) if split and per_file > 1 else [0, -1]
+        out += [(fi, i, pts[i], pts[i + 1]) for i in range(len(pts) - 1)]
+    return out
+
+
 def bams_umi_cluster(bam_paths: Sequence[str], umi_len: int = 12, max_distance: int = 1, source: str = "sequence",
-                     sep: str = "_", mode: str = "htslib", n_threads: int = 0, group=None) -> pa.Table:
-    """Config C5 across ranks (one process per GPU): rank r decodes bam_paths[r::world] on
-    its GPU, and the ranks merge their UMI clusters with the all-to-all H3
-    (rogtk_amd.dist.umi_cluster_sharded). Returns this rank's rows {name, umi, cluster_id,
-    source}: ids are those of umi_cluster over all files' UMIs together (DESIGN.md §4:
-    they depend only on the set of distinct UMIs), identical on every rank."""
+                     sep: str = "_", mode: str = "htslib", n_threads: int = 0, group=None,
+                     split: bool = True, ranges_per_file: int = 0) -> pa.Table:
+    """Config C5 across ranks (one process per GPU): every file is cut into up to `world`
+    ranges at BGZF block starts (split=True; the reference's discover_split_points +
+    process_file_segment_with_pool, src/bam_htslib.rs:247-420), range j of the list goes to
+    rank j % world and is decoded on its GPU, and the ranks merge their UMI clusters with
+    the all-to-all H3 (rogtk_amd.dist.umi_cluster_sharded). A range after the first starts
+    at the first record that starts in its blocks: the rank finds it by chained record
+    checks, then every rank's guess is compared with the previous range's exact tail (one
+    all-reduce) and a range whose guess was wrong is decoded again from the tail, so the
+    rows are exactly the file's records whatever the guesses. Returns this rank's rows
+    {name, umi, cluster_id, source} in range order: ids are those of umi_cluster over all
+    files' UMIs together (they depend only on the set of distinct UMIs),
+    identical on every rank. ranges_per_file > 0 overrides the cut (default: world)."""
     import torch
 
     from . import dist as RD
 
     W = RD.world(group)
     r = torch.distributed.get_rank(group) if W > 1 else 0
-    mine = list(bam_paths)[r::W]
+    paths = list(bam_paths)
+    ranges = _umi_ranges(paths, ranges_per_file or W, split)
+    mine = [j for j in range(len(ranges)) if j % W == r]
     dev = torch.device("cuda", torch.cuda.current_device())
-    parts, names, srcs = [], [], []
-    for path in mine:
-        (off, val, vw, n), nm = bam_umis_dev(path, umi_len, source, sep, mode, n_threads, with_names=True)
-        parts.append((off, val, vw, n))
-        names.append(nm if nm is not None else pa.array([], pa.string()))
-        srcs.append(pa.array([path] * n, pa.string()))
+    res = {}  # range index -> (column, names, skip used, tail)
+
+    def decode(j, skip):
+        fi, i, c0, c1 = ranges[j]
+        try:
+            col, nm, tail = bam_umis_dev(paths[fi], umi_len, source, sep, mode, n_threads, with_names=True,
+                                         rng=None if (c0 == 0 and c1 < 0) else (c0, c1, skip), return_tail=True)
+        except _lib.RogtkError:
+            if ranges[j][1] == 0:
+                raise  # a range that starts with the header: a real error
+            col, nm, tail = None, None, -3  # a wrong guess can frame garbage: decode again below
+        res[j] = (col, nm, skip, tail)
+
+    for j in mine:
+        fi, i, c0, c1 = ranges[j]
+        decode(j, 0 if i == 0 else bam_find_record(paths[fi], c0))
+    # check every guessed skip against the previous range's tail (exact once that range's
+    # own start is); at most len(ranges) rounds, one in practice
+    for _ in range(len(ranges)):
+        t = torch.full((len(ranges), 2), -(2 ** 62), dtype=torch.int64)
+        for j in mine:
+            t[j, 0], t[j, 1] = res[j][2], res[j][3]
+        if W > 1:
+            tt = t.to(dev) if torch.distributed.get_backend(group) == "nccl" else t
+            torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX, group=group)
+            t = tt.cpu()
+        bad = [j for j in range(len(ranges))
+               if ranges[j][1] > 0 and (t[j, 0] != t[j - 1, 1] or t[j - 1, 1] < 0)]
+        if not bad:
+            break
+        for j in bad:
+            if j in mine and t[j - 1, 1] >= 0:
+                decode(j, int(t[j - 1, 1]))
+    else:
+        raise _lib.RogtkError(_lib.ROGTK_E_INVALID, "bam ranges: record boundaries did not settle")
+    parts = [res[j][0] for j in mine]
+    names = [res[j][1] if res[j][1] is not None else pa.array([], pa.string()) for j in mine]
+    srcs = [pa.array([paths[ranges[j][0]]] * res[j][0][3], pa.string()) for j in mine]
     off, val, vw, n = _concat_dev([p[0] for p in parts], [p[1] for p in parts], [p[2] for p in parts],
                                   [p[3] for p in parts], dev) if parts else _concat_dev([], [], [], [], dev)
     cid, k = RD.umi_cluster_sharded(off, val, n, umi_len, max_distance, validity=vw.view(torch.uint8), group=group)

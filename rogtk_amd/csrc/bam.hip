@@ -337,6 +337,32 @@ __global__ __launch_bounds__(256) void k_umi_fill(const uint8_t* __restrict__ sr
     for (int64_t i = 0; i < l; ++i) out[o + i] = src[a + i];
 }
 
+// Append mode (rogtk_bam_umi_append / rogtk_bam_append_strings): a batch's offsets, scanned
+// from 0, are moved to the column's running byte count *base (device), which then moves
+// to the new total; no host round trip. The copy kernels skip rows past cap and count them
+// in *ovf (checked once per column by the caller).
+__global__ __launch_bounds__(256) void k_add_base(int64_t* __restrict__ off, int64_t n1, const int64_t* __restrict__ base) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n1) off[i] += *base;
+}
+__global__ void k_set_base(const int64_t* __restrict__ off_end, int64_t* __restrict__ base) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *base = *off_end;
+}
+// one wave per row: out[off[r] ..] = src[start[r] ..] (len = off[r+1] - off[r])
+__global__ __launch_bounds__(256) void k_copy_rows(const uint8_t* __restrict__ src, const int64_t* __restrict__ start,
+                                                   const int64_t* __restrict__ off, int64_t n, int64_t cap,
+                                                   uint8_t* __restrict__ out, unsigned long long* __restrict__ ovf) {
+    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (r >= n) return;
+    const int64_t a = start[r], o = off[r], l = off[r + 1] - o;
+    if (o + l > cap) {
+        if (lane == 0) atomicAdd(ovf, 1ull);
+        return;
+    }
+    for (int64_t i = lane; i < l; i += 64) out[o + i] = src[a + i];
+}
+
 // ------------------------------------------------------------------ host
 struct PinnedBuf {
     uint8_t* p = nullptr;
@@ -407,9 +433,39 @@ struct Bgzf {
     std::string ahead_err;    // set by the thread, read after join
 
     struct Blk {
-        size_t c0, clen, out;
+        size_t h0, c0, clen, out;  // header and data offsets in comp, data bytes, offset in dst
         uint32_t isize;
     };
+
+    // Range reading (rogtk_bam_open_range): only records that START before the block at
+    // compressed offset c_end are this reader's. file_off = the file offset of comp[0];
+    // u_base = the stream position of buf[0] (stream positions count from the reader's
+    // first inflated byte); once the block at c_end is framed, u_limit = its stream
+    // position (limit_set). Past that block the reader inflates one block at a time, only
+    // as far as its last record needs.
+    int64_t file_off = 0;
+    int64_t c_end = -1;
+    uint64_t u_base = 0;
+    std::atomic<bool> limit_set{false};
+    std::atomic<uint64_t> u_limit{0};
+
+    // the blocks of comp the next inflate may take: those before c_end, or one block once
+    // the range end is reached (a record straddling it needs the next block's bytes)
+    size_t frame_cap() const {
+        if (c_end < 0) return SIZE_MAX;
+        return c_end > file_off ? (size_t)(c_end - file_off) : 0;
+    }
+
+    // Before inflating blks into dst: note the stream position of the block at c_end.
+    void note_limit(const std::vector<Blk>& blks, const uint8_t* dst) {
+        if (c_end < 0 || limit_set.load()) return;
+        for (const Blk& k : blks)
+            if (file_off + (int64_t)k.h0 >= c_end) {
+                u_limit.store(u_base + (uint64_t)(dst - buf.p) + k.out);
+                limit_set.store(true);
+                return;
+            }
+    }
 
     ~Bgzf() { stop_ahead(); }
 
@@ -422,11 +478,14 @@ struct Bgzf {
     }
 
     // Frame the whole BGZF blocks at the start of comp. false + e set on a malformed block.
+    // max_off: no block starting at or past it is framed, unless it is the first one (then
+    // exactly that block).
     static bool frame(const std::vector<uint8_t>& comp, size_t comp_len, std::vector<Blk>& blks, size_t& o,
-                      size_t& total, std::string& e) {
+                      size_t& total, std::string& e, size_t max_off = SIZE_MAX) {
         blks.clear();
         o = total = 0;
         while (o + 18 <= comp_len) {
+            if (o >= max_off && !blks.empty()) break;
             const uint8_t* h = comp.data() + o;
             if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) {
                 e = "not a BGZF file (bad gzip block header)";
@@ -453,9 +512,10 @@ struct Bgzf {
                 e = "corrupt BGZF block (BSIZE too small)";
                 return false;
             }
-            blks.push_back({c0, bsize - 12 - xlen - 8, total, isize});
+            blks.push_back({o, c0, bsize - 12 - xlen - 8, total, isize});
             total += isize;
             o += bsize;
+            if (o > max_off) break;  // the one block at or past max_off
         }
         return true;
     }
@@ -503,11 +563,12 @@ struct Bgzf {
         }
         memmove(comp.data(), comp.data() + o, comp_len - o);
         comp_len -= o;
+        file_off += (int64_t)o;
         return true;
     }
 
     void start_ahead() {
-        if (!readahead || ahead_on || !err.empty() || (file_eof && comp_len == 0)) return;
+        if (!readahead || ahead_on || !err.empty() || (file_eof && comp_len == 0) || limit_set.load()) return;
         ahead_end = end;
         ahead_done = false;
         ahead_on = true;
@@ -519,14 +580,16 @@ struct Bgzf {
             std::string er;
             for (;;) {
                 if (comp_len < chunk && !file_eof) read_comp();
+                if (limit_set.load()) break;  // past the range end: the caller reads on demand
                 size_t o = 0, total = 0;
-                if (!frame(comp, comp_len, blks, o, total, er)) break;
+                if (!frame(comp, comp_len, blks, o, total, er, frame_cap())) break;
                 if (blks.empty()) {  // end of input, or a block longer than what is buffered
                     if (file_eof) break;
                     read_comp();
                     continue;
                 }
                 if (e + total > buf.cap) break;
+                note_limit(blks, buf.p + e);
                 if (!inflate_blocks(blks, o, buf.p + e, er, &t_rd)) break;
                 e += total;
                 std::lock_guard<std::mutex> lk(ahead_mu);
@@ -584,7 +647,7 @@ struct Bgzf {
         std::vector<Blk> blks;
         size_t o = 0, total = 0;
         for (;;) {
-            if (!frame(comp, comp_len, blks, o, total, err)) return false;
+            if (!frame(comp, comp_len, blks, o, total, err, frame_cap())) return false;
             if (!blks.empty() || file_eof) break;
             read_comp();  // a block longer than what is buffered (small ROGTK_BAM_CHUNK)
         }
@@ -613,10 +676,12 @@ struct Bgzf {
             }
             pos -= keep_from;
             end = keep;
+            u_base += keep_from;
         }
         // inflate blocks in parallel
         const double t1 = now_s();
         t_move += t1 - t0;
+        note_limit(blks, buf.p + end);
         if (!inflate_blocks(blks, o, buf.p + end, err, &t_read_bg)) return false;
         t_inflate += now_s() - t1;
         end += total;
@@ -639,11 +704,22 @@ struct BamReader {
     std::vector<uint8_t> ref_val;
     int device = -1;
     hipStream_t stream = nullptr;
+    // range reading: bytes of this range's last record past the range end (the next
+    // range's skip), -1 until the range is exhausted / for a whole-file reader
+    int64_t tail = -1;
     // batch state
     int64_t n = 0;
     std::vector<int64_t> roff;  // record offsets relative to batch start (n + 1)
     DevBuf d_raw, d_roff, d_len[4], d_off[4], d_val[4], d_valid[5], d_start, d_end, d_flags, d_cid, d_ref_off,
         d_ref_val, d_bad, d_cub;
+    // device mode (rogtk_bam_next_dev): the value buffers are sized from host-known bounds
+    // (no host sync per batch); d_bad accumulates over the batches and is checked by
+    // rogtk_bam_check. copied: fires when the batch's H2D copy of the stream buffer is done
+    // (the next framing may move those bytes: it waits for it first).
+    bool bad_cleared = false;
+    hipEvent_t copied = nullptr;
+    bool copy_pending = false;
+    int32_t max_ref_len = 0;
     // host outputs (pinned)
     PinnedBuf h_off[4], h_val[4], h_valid[5], h_u32[3];
     ~BamReader() {
@@ -656,6 +732,7 @@ struct BamReader {
                 std::swap(z.buf.cap, g_pin_cache.cap);
             }
         }
+        if (copied) (void)hipEventDestroy(copied);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -718,6 +795,13 @@ int frame_batch(BamReader* R, int64_t max_records) {
                           "BAM: truncated record at end of file (%zu stray bytes)", z.end - z.pos - rel);
             break;  // clean end of file
         }
+        if (z.limit_set.load()) {  // a record that starts at or past the range end is the next range's
+            const uint64_t at = z.u_base + z.pos + rel, lim = z.u_limit.load();
+            if (at >= lim) {
+                R->tail = (int64_t)(at - lim);
+                break;
+            }
+        }
         const uint8_t* p = z.buf.p + z.pos + rel;
         const uint32_t bs = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
         ROGTK_REQUIRE(bs >= 32 && bs < (1u << 30), ROGTK_E_INVALID, "BAM: invalid record block_size %u", bs);
@@ -731,7 +815,12 @@ int frame_batch(BamReader* R, int64_t max_records) {
     return ROGTK_OK;
 }
 
-int decode_batch(BamReader* R, int mode, int include_seq, int include_qual) {
+// sync_totals: size the value buffers from the scanned totals (one host sync per batch:
+// the host path, which copies the columns back anyway) or from bounds known on the host
+// (device path: name <= 3 bytes per raw byte + 7 per record (U+FFFD per invalid byte,
+// "unknown"), chrom <= the longest reference name per record, sequence / qualities <= the
+// raw bytes), so that the host never waits for the GPU inside a file.
+int decode_batch(BamReader* R, int mode, int include_seq, int include_qual, bool sync_totals = true) {
     const int64_t n = R->n;
     hipStream_t s = R->stream;
     const int64_t bytes = R->roff[n];
@@ -740,6 +829,9 @@ int decode_batch(BamReader* R, int mode, int include_seq, int include_qual) {
         return ROGTK_E_HIP;
     if (bytes) ROGTK_HIP_CHECK(hipMemcpyAsync(R->d_raw.p, R->z.buf.p + R->z.pos, bytes, hipMemcpyHostToDevice, s));
     ROGTK_HIP_CHECK(hipMemcpyAsync(R->d_roff.p, R->roff.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, s));
+    if (!R->copied) ROGTK_HIP_CHECK(hipEventCreateWithFlags(&R->copied, hipEventDisableTiming));
+    ROGTK_HIP_CHECK(hipEventRecord(R->copied, s));
+    R->copy_pending = true;
     const int64_t words = (n + 63) / 64;
     for (int c = 0; c < 4; ++c) {
         if (R->d_len[c].ensure((size_t)(n + 1) * 8) != ROGTK_OK || R->d_off[c].ensure((size_t)(n + 1) * 8) != ROGTK_OK)
@@ -752,7 +844,10 @@ int decode_batch(BamReader* R, int mode, int include_seq, int include_qual) {
         R->d_flags.ensure((size_t)std::max<int64_t>(n, 1) * 4) != ROGTK_OK ||
         R->d_cid.ensure((size_t)std::max<int64_t>(n, 1) * 4) != ROGTK_OK || R->d_bad.ensure(8) != ROGTK_OK)
         return ROGTK_E_HIP;
-    ROGTK_HIP_CHECK(hipMemsetAsync(R->d_bad.p, 0, 8, s));
+    if (sync_totals || !R->bad_cleared) {
+        ROGTK_HIP_CHECK(hipMemsetAsync(R->d_bad.p, 0, 8, s));
+        R->bad_cleared = !sync_totals;
+    }
     FieldsOut fo;
     for (int c = 0; c < 4; ++c) fo.len[c] = R->d_len[c].as<int64_t>();
     for (int c = 0; c < 5; ++c) fo.valid[c] = R->d_valid[c].as<uint64_t>();
@@ -788,12 +883,20 @@ int decode_batch(BamReader* R, int mode, int include_seq, int include_qual) {
                                                          R->d_off[c].as<int64_t>(), (int)(n + 1), s));
     }
     int64_t tot[4];
-    unsigned long long bad = 0;
-    for (int c = 0; c < 4; ++c)
-        ROGTK_HIP_CHECK(hipMemcpyAsync(&tot[c], R->d_off[c].as<int64_t>() + n, 8, hipMemcpyDeviceToHost, s));
-    ROGTK_HIP_CHECK(hipMemcpyAsync(&bad, R->d_bad.p, 8, hipMemcpyDeviceToHost, s));
-    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
-    ROGTK_REQUIRE(bad == 0, ROGTK_E_INVALID, "BAM: %llu record(s) whose fields overrun their block_size", bad);
+    if (sync_totals) {
+        unsigned long long bad = 0;
+        for (int c = 0; c < 4; ++c)
+            ROGTK_HIP_CHECK(hipMemcpyAsync(&tot[c], R->d_off[c].as<int64_t>() + n, 8, hipMemcpyDeviceToHost, s));
+        ROGTK_HIP_CHECK(hipMemcpyAsync(&bad, R->d_bad.p, 8, hipMemcpyDeviceToHost, s));
+        ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+        R->copy_pending = false;
+        ROGTK_REQUIRE(bad == 0, ROGTK_E_INVALID, "BAM: %llu record(s) whose fields overrun their block_size", bad);
+    } else {
+        tot[0] = 3 * bytes + 7 * n;
+        tot[1] = (int64_t)R->max_ref_len * n;
+        tot[2] = include_seq ? bytes : 0;
+        tot[3] = include_qual ? bytes : 0;
+    }
     for (int c = 0; c < 4; ++c)
         if (R->d_val[c].ensure((size_t)std::max<int64_t>(tot[c], 1)) != ROGTK_OK) return ROGTK_E_HIP;
     FillIn fi;
@@ -824,6 +927,134 @@ int decode_batch(BamReader* R, int mode, int include_seq, int include_qual) {
     return ROGTK_OK;
 }
 
+// ------------------------------------------------ splitting one file (host only)
+// The reference splits a BAM at BGZF block boundaries near file_size * i / n
+// (discover_split_points, bam_htslib.rs:247-290; find_nearest_bgzf_boundary :293-320)
+// and seeks htslib to block << 16 (:377-393), i.e. it assumes a record starts there, which
+// BAM does not promise (records straddle blocks). Here a split point is also a block
+// start, but the range reader skips the tail of the record that straddles it: the skip
+// is found by chained record validation (rogtk_bam_find_record) and checked against the
+// previous range's tail (rogtk_bam_range_tail) by the caller, so results never depend on
+// a guess.
+
+// a complete, valid BGZF block header at p (n bytes available): its BSIZE, else 0
+size_t bgzf_block_at(const uint8_t* p, size_t n) {
+    if (n < 18 || p[0] != 31 || p[1] != 139 || p[2] != 8 || !(p[3] & 4)) return 0;
+    const size_t xlen = p[10] | (p[11] << 8);
+    if (12 + xlen > n) return 0;
+    size_t bsize = 0;
+    for (size_t x = 0; x + 4 <= xlen;) {
+        const uint8_t* sf = p + 12 + x;
+        const size_t slen = sf[2] | (sf[3] << 8);
+        if (sf[0] == 'B' && sf[1] == 'C' && slen == 2) bsize = (size_t)(sf[4] | (sf[5] << 8)) + 1;
+        x += 4 + slen;
+    }
+    return bsize >= 12 + xlen + 8 ? bsize : 0;
+}
+
+// Inflate whole BGZF blocks from file offset c0 until at least `want` bytes (or EOF).
+// block_end (optional): the file offset after each block, by its stream end position.
+bool inflate_from(FILE* f, int64_t c0, size_t want, std::vector<uint8_t>& out, std::string& err,
+                  std::vector<std::pair<size_t, int64_t>>* block_end = nullptr) {
+    out.clear();
+    if (fseeko(f, (off_t)c0, SEEK_SET) != 0) {
+        err = "seek failed";
+        return false;
+    }
+    std::vector<uint8_t> comp;
+    size_t clen = 0;
+    bool eof = false;
+    int64_t off = c0;
+    z_stream zs;
+    memset(&zs, 0, sizeof zs);
+    if (inflateInit2(&zs, -15) != Z_OK) {
+        err = "zlib init failed";
+        return false;
+    }
+    while (out.size() < want) {
+        if (clen < (1u << 17) && !eof) {
+            comp.resize(clen + (1u << 20));
+            const size_t got = fread(comp.data() + clen, 1, 1u << 20, f);
+            clen += got;
+            eof = got < (1u << 20);
+        }
+        const size_t bsize = bgzf_block_at(comp.data(), clen);
+        if (!bsize || bsize > clen) {
+            if (clen == 0 && eof) break;
+            err = "not a BGZF block at the split point";
+            inflateEnd(&zs);
+            return false;
+        }
+        const size_t xlen = comp[10] | (comp[11] << 8);
+        const uint8_t* t = comp.data() + bsize - 4;
+        const uint32_t isize = t[0] | (t[1] << 8) | (t[2] << 16) | ((uint32_t)t[3] << 24);
+        const size_t at = out.size();
+        out.resize(at + isize);
+        inflateReset(&zs);
+        zs.next_in = comp.data() + 12 + xlen;
+        zs.avail_in = (uInt)(bsize - 12 - xlen - 8);
+        zs.next_out = out.data() + at;
+        zs.avail_out = isize;
+        if (isize && (::inflate(&zs, Z_FINISH) != Z_STREAM_END || zs.avail_out != 0)) {
+            err = "BGZF inflate failed";
+            inflateEnd(&zs);
+            return false;
+        }
+        off += (int64_t)bsize;
+        if (block_end) block_end->push_back({out.size(), off});
+        memmove(comp.data(), comp.data() + bsize, clen - bsize);
+        clen -= bsize;
+        if (clen == 0 && eof) break;
+    }
+    inflateEnd(&zs);
+    return true;
+}
+
+inline uint32_t rd_u32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// The structural invariants of a record at d[o] (SAMv1 §4.2; loose on purpose: any refID,
+// pos and name bytes, as the decoders accept): block_size >= 32 and below 2^28, a
+// NUL-terminated read name, the variable fields inside block_size. Returns the record's
+// length, 0 when invalid, or SIZE_MAX when d ends inside the fixed fields.
+size_t record_ok(const uint8_t* d, size_t n, size_t o) {
+    if (o + 4 + 32 > n) return SIZE_MAX;
+    const uint32_t bs = rd_u32(d + o);
+    if (bs < 32 || bs >= (1u << 28)) return 0;
+    const uint8_t* b = d + o + 4;
+    const uint32_t l_name = b[8], n_cig = b[12] | (b[13] << 8), l_seq = rd_u32(b + 16);
+    if (l_name < 1 || (l_seq >> 31)) return 0;
+    if ((uint64_t)32 + l_name + 4ull * n_cig + (l_seq + 1ull) / 2 + l_seq > bs) return 0;
+    if (o + 4 + 32 + l_name <= n && b[32 + l_name - 1] != 0) return 0;
+    return 4 + (size_t)bs;
+}
+
+// The first offset in d from which `chain` consecutive records validate (or all records
+// up to the end of d, at least one of them complete); SIZE_MAX when none in [0, max_o).
+size_t first_record(const uint8_t* d, size_t n, size_t max_o, int chain, bool eof) {
+    if (n == 0) return eof ? 0 : SIZE_MAX;  // only empty blocks (the EOF marker) from here
+    for (size_t o = 0; o < max_o && o < n; ++o) {
+        size_t q = o;
+        int ok = 0;
+        bool good = true;
+        while (ok < chain) {
+            if (q == n && eof) break;  // the records end with the file
+            const size_t len = record_ok(d, n, q);
+            if (len == 0) {
+                good = false;
+                break;
+            }
+            if (len == SIZE_MAX || q + len > n) break;  // d ends inside this record
+            q += len;
+            ++ok;
+        }
+        if (good && ok >= 1) return o;
+        if (good && ok == 0 && o == n) return o;
+    }
+    return SIZE_MAX;
+}
+
 }  // namespace
 }  // namespace rogtk
 
@@ -831,8 +1062,95 @@ using namespace rogtk;
 
 extern "C" {
 
+int rogtk_bam_split_points(const char* path, int n, int64_t* points, int* n_ranges) {
+    ROGTK_REQUIRE(path && points && n_ranges && n >= 1, ROGTK_E_INVALID, "bam split: bad arguments");
+    FILE* f = fopen(path, "rb");
+    ROGTK_REQUIRE(f, ROGTK_E_INVALID, "Failed to open BAM file '%s'", path);
+    std::unique_ptr<FILE, int (*)(FILE*)> guard(f, fclose);
+    fseeko(f, 0, SEEK_END);
+    const int64_t size = (int64_t)ftello(f);
+    // the block holding the first record byte: no split point at or before it
+    std::vector<uint8_t> d;
+    std::vector<std::pair<size_t, int64_t>> ends;
+    std::string err;
+    size_t hlen = 0;
+    int64_t c_rec = 0;
+    for (size_t want = 1 << 16;; want *= 4) {
+        ROGTK_REQUIRE(inflate_from(f, 0, want, d, err, &ends), ROGTK_E_INVALID, "BAM %s: %s", path, err.c_str());
+        ROGTK_REQUIRE(d.size() >= 8 && memcmp(d.data(), "BAM\1", 4) == 0, ROGTK_E_INVALID, "not a BAM file (bad magic)");
+        size_t o = 8 + (size_t)rd_u32(d.data() + 4);
+        bool done = o + 4 <= d.size();
+        if (done) {
+            const uint32_t nref = rd_u32(d.data() + o);
+            o += 4;
+            for (uint32_t i = 0; i < nref && done; ++i) {
+                if (o + 4 > d.size()) done = false;
+                else o += 8 + (size_t)rd_u32(d.data() + o);
+            }
+            done = done && o <= d.size();
+        }
+        if (done) {
+            hlen = o;
+            break;
+        }
+        ROGTK_REQUIRE(d.size() >= want, ROGTK_E_INVALID, "BAM header: unexpected end of file");
+    }
+    for (const auto& e : ends)
+        if (e.first > hlen) break;
+        else c_rec = e.second;  // the first record byte lies in the block from here (or later)
+    int k = 0;
+    points[k++] = 0;
+    std::vector<uint8_t> win(1 << 18);
+    for (int i = 1; i < n; ++i) {
+        const int64_t target = size * i / n;
+        if (target <= std::max(c_rec, points[k - 1])) continue;
+        fseeko(f, (off_t)target, SEEK_SET);
+        const size_t got = fread(win.data(), 1, win.size(), f);
+        int64_t found = -1;
+        for (size_t j = 0; j + 18 <= got && found < 0; ++j) {
+            const size_t bs = bgzf_block_at(win.data() + j, got - j);
+            if (!bs) continue;
+            const int64_t at = target + (int64_t)j;
+            const bool next_ok = at + (int64_t)bs == size ||
+                                 (j + bs + 18 <= got && bgzf_block_at(win.data() + j + bs, got - j - bs) != 0);
+            if (next_ok) found = at;
+        }
+        // no split inside the EOF marker block (28 bytes) or after it
+        if (found > points[k - 1] && found > c_rec && found + 28 < size) points[k++] = found;
+    }
+    points[k] = size;
+    *n_ranges = k;
+    return ROGTK_OK;
+}
+
+int rogtk_bam_find_record(const char* path, int64_t c_begin, int64_t* skip) {
+    ROGTK_REQUIRE(path && skip && c_begin >= 0, ROGTK_E_INVALID, "bam find_record: bad arguments");
+    FILE* f = fopen(path, "rb");
+    ROGTK_REQUIRE(f, ROGTK_E_INVALID, "Failed to open BAM file '%s'", path);
+    std::unique_ptr<FILE, int (*)(FILE*)> guard(f, fclose);
+    std::vector<uint8_t> d;
+    std::string err;
+    // a straddling record is < 2^28 bytes; records this long are not expected in practice,
+    // so 4 MB of stream covers the skip and a chain of records after it
+    ROGTK_REQUIRE(inflate_from(f, c_begin, 4u << 20, d, err), ROGTK_E_INVALID, "BAM %s: %s", path, err.c_str());
+    const bool eof = d.size() < (4u << 20);
+    const size_t o = first_record(d.data(), d.size(), d.size() + 1, 16, eof);
+    ROGTK_REQUIRE(o != SIZE_MAX, ROGTK_E_INVALID, "BAM %s: no record start found after offset %lld", path,
+                  (long long)c_begin);
+    *skip = (int64_t)o;
+    return ROGTK_OK;
+}
+
 int rogtk_bam_open(const char* path, int n_threads, void** reader) {
+    return rogtk_bam_open_range(path, n_threads, 0, -1, 0, reader);
+}
+
+int rogtk_bam_open_range(const char* path, int n_threads, int64_t c_begin, int64_t c_end, int64_t skip,
+                         void** reader) {
     ROGTK_REQUIRE(path && reader, ROGTK_E_INVALID, "bam: NULL argument");
+    ROGTK_REQUIRE(c_begin >= 0 && skip >= 0 && (c_end < 0 || c_end > c_begin), ROGTK_E_INVALID,
+                  "bam range: bad range [%lld, %lld) / skip %lld", (long long)c_begin, (long long)c_end,
+                  (long long)skip);
     *reader = nullptr;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
@@ -850,8 +1168,39 @@ int rogtk_bam_open(const char* path, int n_threads, void** reader) {
     R->z.threads = n_threads > 0 ? n_threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     ROGTK_HIP_CHECK(hipGetDevice(&R->device));
     ROGTK_HIP_CHECK(hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking));
+    fseeko(R->z.f, 0, SEEK_END);
+    const int64_t fsize = (int64_t)ftello(R->z.f);
+    fseeko(R->z.f, 0, SEEK_SET);
+    if (c_end >= fsize) c_end = -1;  // the range runs to the end of the file
+    const bool ranged = c_begin > 0;
+    const bool ra = R->z.readahead;
+    const size_t chunk = R->z.chunk;
+    if (ranged) {  // the header only: no read-ahead into other ranges' bytes
+        R->z.readahead = false;
+        R->z.chunk = 1u << 20;
+    } else {
+        R->z.c_end = c_end;
+    }
     int rc = read_header(R.get());
     if (rc != ROGTK_OK) return rc;
+    if (ranged) {  // restart the stream at the range's first block
+        Bgzf& z = R->z;
+        z.stop_ahead();
+        z.readahead = ra;
+        z.chunk = chunk;
+        ROGTK_REQUIRE(fseeko(z.f, (off_t)c_begin, SEEK_SET) == 0, ROGTK_E_INVALID, "bam range: seek failed");
+        z.comp_len = 0;
+        z.file_eof = false;
+        z.file_off = c_begin;
+        z.pos = z.end = 0;
+        z.u_base = 0;
+        z.c_end = c_end;
+        ROGTK_REQUIRE(skip == 0 || z.ensure_rel(0, (size_t)skip), ROGTK_E_INVALID, "bam range: %s",
+                      z.err.empty() ? "skip past the end of the file" : z.err.c_str());
+        z.pos += (size_t)skip;
+    }
+    for (size_t i = 0; i + 1 < R->ref_off.size(); ++i)
+        R->max_ref_len = std::max<int32_t>(R->max_ref_len, (int32_t)(R->ref_off[i + 1] - R->ref_off[i]));
     const size_t rb = R->ref_off.size() * 8, vb = std::max<size_t>(R->ref_val.size(), 1);
     if (R->d_ref_off.ensure(rb) != ROGTK_OK || R->d_ref_val.ensure(vb) != ROGTK_OK) return ROGTK_E_HIP;
     ROGTK_HIP_CHECK(hipMemcpy(R->d_ref_off.p, R->ref_off.data(), rb, hipMemcpyHostToDevice));
@@ -873,11 +1222,16 @@ int rogtk_bam_header(void* reader, int64_t* n_ref, const int64_t** name_offsets,
     return ROGTK_OK;
 }
 
-static int bam_next_common(BamReader* R, int64_t max_records, int mode, int include_sequence, int include_quality) {
+static int bam_next_common(BamReader* R, int64_t max_records, int mode, int include_sequence, int include_quality,
+                           bool sync_totals = true) {
     ROGTK_REQUIRE(max_records > 0, ROGTK_E_INVALID, "bam: max_records must be > 0");
     ROGTK_REQUIRE(mode == ROGTK_BAM_NOODLES || mode == ROGTK_BAM_HTSLIB || mode == ROGTK_BAM_HTSLIB_BLOCKS,
                   ROGTK_E_INVALID, "bam: unknown mode %d", mode);
     ROGTK_HIP_CHECK(hipSetDevice(R->device));
+    if (R->copy_pending) {  // the previous batch's H2D copy still reads the stream buffer
+        ROGTK_HIP_CHECK(hipEventSynchronize(R->copied));
+        R->copy_pending = false;
+    }
     // release the previous batch's bytes
     R->z.pos += R->n ? (size_t)R->roff[R->n] : 0;
     R->n = 0;
@@ -887,7 +1241,7 @@ static int bam_next_common(BamReader* R, int64_t max_records, int mode, int incl
     const double t1 = now_s();
     R->t_frame += (t1 - t0) - (R->z.t_read + R->z.t_inflate + R->z.t_move - in0);
     if (rc != ROGTK_OK) return rc;
-    rc = decode_batch(R, mode, include_sequence, include_quality);
+    rc = decode_batch(R, mode, include_sequence, include_quality, sync_totals);
     R->t_decode += now_s() - t1;
     return rc;
 }
@@ -950,7 +1304,9 @@ int rogtk_bam_next_dev(void* reader, int64_t max_records, int mode, int include_
     // the batch is decoded on the caller's stream (ordered with what the caller does next)
     hipStream_t own = R->stream;
     if (stream) R->stream = reinterpret_cast<hipStream_t>(stream);
-    int rc = bam_next_common(R, max_records, mode, include_sequence, include_quality);
+    // no host sync inside a file: value buffers sized from host bounds, d_bad checked by
+    // rogtk_bam_check (a NULL stream keeps the synchronous behaviour)
+    int rc = bam_next_common(R, max_records, mode, include_sequence, include_quality, stream == nullptr);
     R->stream = own;
     if (rc != ROGTK_OK) return rc;
     memset(out, 0, sizeof *out);
@@ -994,7 +1350,7 @@ int rogtk_bam_umi_dev(const rogtk_bam_batch* batch, int64_t n, int source, int u
     ROGTK_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(cub.p, tb, len.as<int64_t>(), offsets, (int)(n + 1), s));
     int64_t total = 0;
     ROGTK_HIP_CHECK(hipMemcpyAsync(&total, offsets + n, 8, hipMemcpyDeviceToHost, s));
-    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));  // (rogtk_bam_umi_append: no sync)
     ROGTK_REQUIRE(total <= values_cap, ROGTK_E_OVERFLOW, "bam umi: %lld bytes exceed values_cap %lld",
                   (long long)total, (long long)values_cap);
     if (n > 0) {
@@ -1006,12 +1362,91 @@ int rogtk_bam_umi_dev(const rogtk_bam_batch* batch, int64_t n, int source, int u
     return ROGTK_OK;
 }
 
+int rogtk_bam_umi_append(const rogtk_bam_batch* batch, int64_t n, int source, int umi_len, int sep,
+                         int64_t* offsets, uint8_t* values, int64_t values_cap, uint8_t* validity, int64_t row_base,
+                         int64_t* base, unsigned long long* overflow, void* stream) {
+    ROGTK_REQUIRE(batch && offsets && values && validity && base && overflow, ROGTK_E_INVALID,
+                  "bam umi append: NULL argument");
+    ROGTK_REQUIRE(source == 0 || source == 1, ROGTK_E_INVALID, "bam umi: source must be 0 (sequence) or 1 (name)");
+    ROGTK_REQUIRE(source == 1 || umi_len > 0, ROGTK_E_INVALID, "bam umi: umi_len must be > 0");
+    ROGTK_REQUIRE(source == 1 || batch->offsets[2], ROGTK_E_INVALID, "bam umi: the batch has no sequence column");
+    ROGTK_REQUIRE(n >= 0 && row_base >= 0 && row_base % 64 == 0, ROGTK_E_INVALID,
+                  "bam umi append: n >= 0 and a row base that is a multiple of 64");
+    if (n == 0) return ROGTK_OK;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    thread_local DevBuf len, start, cub;
+    if (len.ensure((size_t)(n + 1) * 8) != ROGTK_OK || start.ensure((size_t)(n + 1) * 8) != ROGTK_OK)
+        return ROGTK_E_HIP;
+    int64_t* off = offsets + row_base;
+    const unsigned g = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(k_umi_len, dim3(g), dim3(256), 0, s, batch->offsets[2], (const uint64_t*)batch->validity[2],
+                       batch->offsets[0], batch->values[0], n, source, umi_len, sep, len.as<int64_t>(),
+                       start.as<int64_t>(), (uint64_t*)validity + row_base / 64);
+    ROGTK_HIP_CHECK(hipGetLastError());
+    ROGTK_HIP_CHECK(hipMemsetAsync(len.as<int64_t>() + n, 0, 8, s));
+    size_t tb = 0;
+    ROGTK_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, len.as<int64_t>(), off, (int)(n + 1), s));
+    if (cub.ensure(tb) != ROGTK_OK) return ROGTK_E_HIP;
+    ROGTK_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(cub.p, tb, len.as<int64_t>(), off, (int)(n + 1), s));
+    hipLaunchKernelGGL(k_add_base, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, s, off, n + 1,
+                       (const int64_t*)base);
+    hipLaunchKernelGGL(k_set_base, dim3(1), dim3(64), 0, s, (const int64_t*)(off + n), base);
+    const uint8_t* src = source == 0 ? batch->values[2] : batch->values[0];
+    hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)((n * 64 + 255) / 256)), dim3(256), 0, s, src, start.as<int64_t>(),
+                       (const int64_t*)off, n, values_cap, values, overflow);
+    ROGTK_HIP_CHECK(hipGetLastError());
+    return ROGTK_OK;
+}
+
+int rogtk_bam_append_strings(const int64_t* src_offsets, const uint8_t* src_values, int64_t n, int64_t* offsets,
+                             uint8_t* values, int64_t values_cap, int64_t row_base, int64_t* base,
+                             unsigned long long* overflow, void* stream) {
+    ROGTK_REQUIRE(src_offsets && src_values && offsets && values && base && overflow && n >= 0 && row_base >= 0,
+                  ROGTK_E_INVALID, "bam append strings: bad arguments");
+    if (n == 0) return ROGTK_OK;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int64_t* off = offsets + row_base;
+    ROGTK_HIP_CHECK(hipMemcpyAsync(off, src_offsets, (size_t)(n + 1) * 8, hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL(k_add_base, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, s, off, n + 1,
+                       (const int64_t*)base);
+    hipLaunchKernelGGL(k_set_base, dim3(1), dim3(64), 0, s, (const int64_t*)(off + n), base);
+    hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)((n * 64 + 255) / 256)), dim3(256), 0, s, src_values, src_offsets,
+                       (const int64_t*)off, n, values_cap, values, overflow);
+    ROGTK_HIP_CHECK(hipGetLastError());
+    return ROGTK_OK;
+}
+
+int rogtk_bam_batch_bytes(void* reader, int64_t* bytes) {
+    ROGTK_REQUIRE(reader && bytes, ROGTK_E_INVALID, "bam: NULL argument");
+    auto* R = static_cast<BamReader*>(reader);
+    *bytes = R->n ? R->roff[R->n] : 0;
+    return ROGTK_OK;
+}
+
+int rogtk_bam_check(void* reader, void* stream) {
+    ROGTK_REQUIRE(reader, ROGTK_E_INVALID, "bam: NULL reader");
+    auto* R = static_cast<BamReader*>(reader);
+    if (!R->bad_cleared) return ROGTK_OK;  // no device-mode batch, or every batch checked
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : R->stream;
+    unsigned long long bad = 0;
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&bad, R->d_bad.p, 8, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    ROGTK_REQUIRE(bad == 0, ROGTK_E_INVALID, "BAM: %llu record(s) whose fields overrun their block_size", bad);
+    return ROGTK_OK;
+}
+
 int rogtk_copy(void* dst, const void* src, int64_t bytes, void* stream) {
     ROGTK_REQUIRE(bytes >= 0 && (bytes == 0 || (dst && src)), ROGTK_E_INVALID, "copy: bad arguments");
     if (bytes == 0) return ROGTK_OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     ROGTK_HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDefault, s));
     ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    return ROGTK_OK;
+}
+
+int rogtk_bam_range_tail(void* reader, int64_t* tail) {
+    ROGTK_REQUIRE(reader && tail, ROGTK_E_INVALID, "bam: NULL argument");
+    *tail = static_cast<BamReader*>(reader)->tail;
     return ROGTK_OK;
 }
 

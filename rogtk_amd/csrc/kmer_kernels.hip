@@ -662,10 +662,6 @@ __device__ unsigned long long g_kmer_clk[8];
 #define KT(k) do { } while (0)
 #endif
 
-__device__ __forceinline__ uint32_t pk_base(const uint64_t* pk, int64_t p) {
-    return (uint32_t)(pk[p >> 5] >> (62 - 2 * (p & 31))) & 3u;
-}
-
 __device__ __forceinline__ bool kless(uint64_t ka, uint32_t ia, uint64_t kb, uint32_t ib) {
     return ka < kb || (ka == kb && (ia >> 31) < (ib >> 31));  // real entries before pads
 }
@@ -807,9 +803,14 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
                 const uint64_t x0 = rw[p >> 5], x1 = rw[(p >> 5) + 1];
                 const uint64_t top = b ? (x0 << b) | (x1 >> (64 - b)) : x0;
                 const uint64_t key = (top >> (64 - 2 * K)) & kmask;
+                // extension bases from the two words already loaded (k_eff <= 32: base p + K
+                // lies in x0 or x1); only a k-mer starting a word loads its left base
                 uint32_t e = 0;
-                if (p > 0) e |= 1u << pk_base(rw, p - 1);
-                if (p + K < len) e |= 1u << (4 + pk_base(rw, p + K));
+                if (p > 0) e |= 1u << (b ? (uint32_t)(x0 >> (64 - b)) & 3u : (uint32_t)rw[(p >> 5) - 1] & 3u);
+                if (p + K < len) {
+                    const int t = (p & 31) + K;
+                    e |= 1u << (4 + ((uint32_t)((t < 32 ? x0 : x1) >> (62 - 2 * (t & 31))) & 3u));
+                }
                 if (kBounded && __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
                 uint32_t slot;
                 if (key == kEmpty) {

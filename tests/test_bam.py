@@ -64,6 +64,61 @@ def edge_bam(tmp_path_factory):
 
 
 # ------------------------------------------------------------------ CPU
+def _stream_map(path):
+    """(compressed block offset -> stream offset of its first byte, the record starts in
+    the inflated stream) of a BAM file, from a plain walk of its blocks."""
+    import gzip
+    import struct
+
+    raw = open(path, "rb").read()
+    offs, o, u = {}, 0, 0
+    while o < len(raw):
+        bsize = struct.unpack_from("<H", raw, o + 16)[0] + 1
+        offs[o] = u
+        u += struct.unpack_from("<I", raw, o + bsize - 4)[0]
+        o += bsize
+    data = gzip.decompress(raw)
+    q = 8 + struct.unpack_from("<i", data, 4)[0]
+    nref = struct.unpack_from("<i", data, q)[0]
+    q += 4
+    for _ in range(nref):
+        q += 8 + struct.unpack_from("<i", data, q)[0]
+    starts = []
+    while q < len(data):
+        starts.append(q)
+        q += 4 + struct.unpack_from("<I", data, q)[0]
+    return offs, np.array(starts, dtype=np.int64)
+
+
+@pytest.mark.parametrize("block,long_names", [(997, False), (65280, False), (4093, True)])
+def test_split_points_and_record_starts(tmp_path, block, long_names):
+    """One BAM cut at BGZF block starts (the reference's discover_split_points,
+    bam_htslib.rs:247): every split point is a block start past the header's blocks, and
+    rogtk_bam_find_record finds exactly the first record that starts in each range (the
+    straddling record's tail skipped), for 2..17 ranges and records that span blocks.
+    Host-only entry points: no GPU."""
+    from rogtk_amd import bam as B
+
+    p = str(tmp_path / "s.bam")
+    recs = _random_records(11, 2500)
+    if long_names:  # records of 300-600 B spanning many small blocks
+        recs = [synth_bam.record_bytes(name=b"n" * 200 + str(i).encode(), seq="ACGT" * 60) for i in range(800)]
+    synth_bam.write_bam(p, REFS, recs, text="@HD\tVN:1.6\n", block=block)
+    offs, starts = _stream_map(p)
+    size = os.path.getsize(p)
+    for n in (1, 2, 3, 5, 8, 17):
+        pts = B.bam_split_points(p, n)
+        assert pts[0] == 0 and pts[-1] == size and len(pts) - 1 <= n
+        assert all(a < b for a, b in zip(pts, pts[1:]))
+        for c in pts[1:-1]:
+            assert c in offs
+            uo = offs[c]
+            assert uo > starts[0]  # past the header
+            nxt = starts[starts >= uo]
+            assert B.bam_find_record(p, c) == (int(nxt[0] - uo) if nxt.size else 0)
+
+
+
 def test_oracle_known_answers(tmp_path):
     p = str(tmp_path / "kat.bam")
     recs = [
@@ -149,6 +204,31 @@ def test_gpu_decode_matches_oracle(edge_bam, mode, max_records):
     assert len(got) == len(ref)
     bad = [i for i in range(len(ref)) if got[i] != ref[i]]
     assert not bad, (bad[:3], got[bad[0]], ref[bad[0]])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 5, 13])
+def test_gpu_range_readers_cover_the_file(edge_bam, n):
+    """The ranges of one file (split points + found record starts) decoded by range readers
+    are the whole file's rows exactly once, in order; each range's tail equals the next
+    range's skip (what bams_umi_cluster checks across ranks)."""
+    from rogtk_amd import bam as B
+    ref = _expect(pybam.bam_rows(edge_bam, "htslib_blocks"), True, True)
+    pts = B.bam_split_points(edge_bam, n)
+    got, tails, skips = [], [], []
+    for i in range(len(pts) - 1):
+        skip = 0 if i == 0 else B.bam_find_record(edge_bam, pts[i])
+        skips.append(skip)
+        with B.BamReader(edge_bam, 4, rng=(pts[i], pts[i + 1], skip)) as r:
+            while True:
+                rb = r.next_batch(101, "htslib_blocks")
+                if rb is None:
+                    break
+                got += _rows_of([rb], "htslib_blocks")
+            tails.append(r.tail())
+    assert len(pts) - 1 == n and tails[-1] == -1
+    assert tails[:-1] == skips[1:]
+    assert got == ref
 
 
 @pytest.mark.gpu

@@ -180,6 +180,73 @@ def test_bams_umi_cluster_sharded_matches_oracle(rg, tmp_path, world, md):
     assert seen == len(want)
 
 
+def _bam_split_worker(rank, world, port, paths, md, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rogtk_amd import bam as B
+        t = B.bams_umi_cluster(paths, umi_len=12, max_distance=md)
+        out_q.put((rank, t.column("source").to_pylist(), t.column("name").to_pylist(),
+                   t.column("cluster_id").to_pylist(), int(t.schema.metadata[b"n_clusters"])))
+    finally:
+        dist.destroy_process_group()
+
+
+def _check_bam_results(results, want, rk):
+    seen = set()
+    for rank, src, names, ids, k in results:
+        assert k == rk
+        for s, nm, c in zip(src, names, ids):
+            assert (s, nm) not in seen  # every record on exactly one rank
+            seen.add((s, nm))
+            wc, wv = want[(s, nm)]
+            assert (c is None) == (not wv)
+            if wv:
+                assert c == wc
+    assert seen == set(want)
+
+
+@pytest.mark.parametrize("md", [0, 1])
+def test_one_bam_split_over_two_ranks(rg, tmp_path, md):
+    """Config C5 with ONE BAM over 2 ranks: the file is cut at a BGZF block start, each rank
+    decodes its range (the second from the record it finds, checked against the first
+    range's tail), and every record gets the oracle's id."""
+    from rogtk_amd import synth_bam
+    p = os.path.join(str(tmp_path), "one.bam")
+    synth_bam.synth_bam(p, 30000, seed=0x524F47544B + 9, level=1)
+    want, rk = _bam_oracle([p], md)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bam_split_worker, args=(r, 2, port, [p], md, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    results = [q.get(timeout=100) for _ in range(2)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert all(len(r[1]) > 0 for r in results)  # both ranks decoded part of the file
+    _check_bam_results(results, want, rk)
+
+
+def test_bam_ranges_recover_from_wrong_record_guesses(rg, tmp_path, monkeypatch):
+    """A range whose guessed first record is wrong (forced here) is decoded again from the
+    previous range's exact tail: the rows and ids still equal the oracle's."""
+    from rogtk_amd import bam as B
+    from rogtk_amd import synth_bam
+    p = os.path.join(str(tmp_path), "g.bam")
+    synth_bam.synth_bam(p, 20000, seed=0x524F47544B + 5, level=1)
+    want, rk = _bam_oracle([p], 1)
+    real = B.bam_find_record
+    monkeypatch.setattr(B, "bam_find_record", lambda path, c: real(path, c) + 7)  # mid-record
+    t = B.bams_umi_cluster([p], umi_len=12, max_distance=1, ranges_per_file=4)
+    results = [(0, t.column("source").to_pylist(), t.column("name").to_pylist(),
+                t.column("cluster_id").to_pylist(), int(t.schema.metadata[b"n_clusters"]))]
+    _check_bam_results(results, want, rk)
+
+
 # ---- the streaming pipeline across ranks (the bench path at N > 1): bitmap all-gather on
 # its own stream, resolve of the merged bitmaps, labels of each rank's own reads
 
