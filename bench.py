@@ -125,6 +125,18 @@ def parse():
     return ap.parse_args()
 
 
+def emulated_shard_bitmap(n_total: int, r: int, W: int, L: int, dev) -> torch.Tensor:
+    """The presence bitmap rank r of W would all-gather for its shard of n_total synth-v1
+    reads (bench.py --emulate-ranks; tests/test_gpu_bench.py's emulated C4 rank)."""
+    s0, c0 = RD.shard_range(n_total, r, W)
+    eng = D.ClusterEngine(L, min(n_total, 4 ** L), dev)
+    cr = torch.from_numpy(synth.umi_codes(n_total, L, start=s0, count=c0).view(np.int32)).to(dev)
+    eng.mark(D.PackedBatch(cr, L))
+    bm = eng.build_local_bitmap().clone()
+    del cr, eng
+    return bm
+
+
 def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -426,16 +438,11 @@ def main():
         if world > 1:
             raise SystemExit("--emulate-ranks is a single-process tool")
         W = args.emulate_ranks
-        n_total = n * W
-        others = []
-        tmp = D.ClusterEngine(L, min(n_total, 4 ** L), dev)
-        for r in range(1, W):
-            s0, c0 = RD.shard_range(n_total, r, W)
-            cr = torch.from_numpy(synth.umi_codes(n_total, L, start=s0, count=c0).view(np.int32)).to(dev)
-            tmp.mark(D.PackedBatch(cr, L))
-            others.append(tmp.build_local_bitmap().clone())
-            del cr
-        del tmp
+        # C2: reads_per_gpu per emulated rank; C4: the fixed total split over the W ranks
+        n_total = (args.total_reads if args.reads_per_gpu is None else args.reads_per_gpu * W) \
+            if args.workload == "C4" else n * W
+        n = count = RD.shard_range(n_total, 0, W)[1]
+        others = [emulated_shard_bitmap(n_total, r, W, L, dev) for r in range(1, W)]
         codes_h = synth.umi_codes(n_total, L, start=0, count=n)  # rank 0's shard of the W-rank dataset
         codes = torch.from_numpy(codes_h.view(np.int32)).to(dev)
         batch = D.PackedBatch(codes, L)

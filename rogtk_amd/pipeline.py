@@ -47,10 +47,12 @@ _ON_MAIN = object()  # slot.assigned: the assign ran on the main stream, no even
 
 
 class _Slot:
-    def __init__(self, umi_len, max_distinct, n_max, dev, with_scores):
+    def __init__(self, umi_len, max_distinct, n_max, dev, with_scores, with_distance=False):
         self.eng = D.ClusterEngine(umi_len, max_distinct, dev)
         self.scores = D.alloc_scores(n_max, dev) if with_scores else None
         self.within = torch.empty(max((n_max + 63) // 64, 1), dtype=torch.int64, device=dev)
+        # H2 hamming_distance_expr column (expressions.rs:1048-1073), when asked
+        self.dist = torch.empty(max(n_max, 1), dtype=torch.int32, device=dev) if with_distance else None
         self.cid = torch.empty(max(n_max, 4), dtype=torch.int32, device=dev)
         self.assigned = None  # D.StreamEvent or torch.cuda.Event (UmiPipeline.device_events)
         self.resolved = None
@@ -64,7 +66,8 @@ class UmiPipeline:
                  on_assigned=None, score_alone: bool = False, exchange=None, resolve_streams: int = 1,
                  assign_on: str = "main", split_resolve: bool = False, reuse_gate: str = "auto",
                  assign_early: bool = True, mark_first="auto", device_events: bool = True,
-                 mark_stream: bool = False, fused_assign: bool = False, mark_parts: bool = False):
+                 mark_stream: bool = False, fused_assign: bool = False, mark_parts: bool = False,
+                 with_distance: bool = False):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
@@ -77,7 +80,7 @@ class UmiPipeline:
                              "or 'sort' (partition sort + LDS bitmap, umi_len 7..13)")
         self.sort_mark = mark == "sort"
         self.fused_mark = mark == "fused"
-        self.slots = [_Slot(umi_len, max_distinct, n_max, dev, with_scores) for _ in range(depth)]
+        self.slots = [_Slot(umi_len, max_distinct, n_max, dev, with_scores, with_distance) for _ in range(depth)]
         # priorities: (main, resolve, assign); lower = higher priority (torch convention)
         self.caller = torch.cuda.current_stream(dev)
         self.main = torch.cuda.Stream(dev, priority=priorities[0])
@@ -263,7 +266,7 @@ class UmiPipeline:
         return D.StreamEvent() if self.device_events else torch.cuda.Event()
 
     def _score(self, slot: _Slot, batch: D.PackedBatch):
-        D.score_packed(batch, slot.scores, self.target, self.max_hamming, None, slot.within,
+        D.score_packed(batch, slot.scores, self.target, self.max_hamming, slot.dist, slot.within,
                        cluster=slot.eng if self.fused_mark else None, stream=self.main)
         if self.score_alone and self.s_assign is not self.main:
             self.last_scored = self._event()
@@ -340,7 +343,7 @@ class UmiPipeline:
         self._settle(slot)
         if slot.assigned is not None:
             D.wait_for(self.main, slot.assigned)
-        D.score_packed(batch, slot.scores, self.target, self.max_hamming, None, slot.within,
+        D.score_packed(batch, slot.scores, self.target, self.max_hamming, slot.dist, slot.within,
                        cluster=slot.eng if self.fused_mark else None, stream=self.main)
         if self.sort_mark:
             slot.eng.mark_bitmap(batch, stream=self.main)
@@ -381,7 +384,7 @@ class UmiPipeline:
     def _score_assign_oldest(self):
         slot, batch, resolved = self.queue.popleft()
         D.wait_for(self.main, resolved)
-        D.score_assign_packed(batch, slot.eng, slot.cid, slot.scores, self.target, self.max_hamming, None,
+        D.score_assign_packed(batch, slot.eng, slot.cid, slot.scores, self.target, self.max_hamming, slot.dist,
                               slot.within, deferred=self.on_assigned is None, stream=self.main)
         if self.on_assigned is not None:
             with torch.cuda.stream(self.main):

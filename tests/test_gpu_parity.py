@@ -607,6 +607,49 @@ def test_full_size_c2_properties(rg):
                           scores["combined_score"][:n].cpu().numpy().view(np.uint64))
 
 
+def test_full_size_c2_bench_pipeline_all_outputs(rg):
+    """BASELINE C2 through the bench's own path: 10M reads, UmiPipeline with bench.py's
+    arguments (depth 2, slice-bucket mark, assign on the main stream, deferred assigns,
+    device events), three submits of the batch as the bench's steps do; every output of
+    both slots is compared: the 7 H1 fields, the H2 distance and within columns (distinct
+    codes broadcast back) and the H3 ids (oracle union-find on the 10M codes)."""
+    import torch
+
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+    from rogtk_amd.pipeline import UmiPipeline
+
+    n, L = 10_000_000, 12
+    codes_h = synth.umi_codes(n, L)
+    codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
+    batch = D.PackedBatch(codes, L)
+    pipe = UmiPipeline(L, min(n, 4 ** L), n, "cuda", depth=2, target=b"ACGTACGTACGT", max_distance=1,
+                       score_alone=True, with_distance=True)
+    for _ in range(3):
+        pipe.submit(batch)
+    pipe.drain()
+    torch.cuda.synchronize()
+    uniq, inv = np.unique(codes_h, return_inverse=True)
+    ucol = P().StrCol.from_fixed(synth.codes_to_ascii(uniq, L))
+    ref = P().umi_complexity(ucol)
+    rd, rw, _ = P().hamming(ucol, b"ACGTACGTACGT", 1)
+    rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L)), L, 1)
+    for slot in pipe.slots:
+        for f in P().FIELDS:
+            g = slot.scores[f][:n].cpu().numpy()
+            r = ref[f][inv]
+            if r.dtype == np.float64:
+                assert np.array_equal(g.view(np.uint64), r.view(np.uint64)), f
+            else:
+                assert np.array_equal(g.view(np.uint32), r), f
+        assert np.array_equal(slot.dist[:n].cpu().numpy().view(np.uint32), rd[inv])
+        bits = np.unpackbits(slot.within.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+        assert np.array_equal(bits, rw[inv])
+        st = slot.eng.stats()
+        assert st["n_distinct"] == len(uniq) and st["n_clusters"] == rk
+        assert np.array_equal(slot.cid[:n].cpu().numpy().view(np.uint32), rc)
+
+
 @pytest.mark.parametrize("depth,nb,alone", [(4, 4, False), (2, 5, False), (1, 3, False), (3, 7, False),
                                              (2, 6, True), (3, 5, True)])
 @pytest.mark.parametrize("mark", ["xcd", "fused", "sort"])
