@@ -68,7 +68,9 @@ constexpr int kRoundBatch = 4;
 // fits the 8-position local CC), chosen on the device by the first scan
 // S_LCAP: with S_P0 = 8, which 8-position instance takes the tiles (0: <= 8192 codes per
 // tile, 1: <= 16384, e.g. the union bitmap of 2-4 ranks' 10M-read batches)
-enum StatSlot { S_NDISTINCT = 0, S_NCLUSTERS = 1, S_OVERFLOW = 2, S_ERROR = 3, S_ROUNDS = 4, S_EDGE_OVF = 5, S_P0 = 6,
+// S_REDO: the one local-CC instance launched (chosen from the workspace's previous resolve)
+// does not take this bitmap's tiling: cluster_finish redoes the local and global phases.
+enum StatSlot { S_NDISTINCT = 0, S_NCLUSTERS = 1, S_OVERFLOW = 2, S_REDO = 3, S_ROUNDS = 4, S_EDGE_OVF = 5, S_P0 = 6,
                 S_LCAP = 7 };
 // stats (8 x int64), round flags (u32 per round) at byte 64, edge-list counts (u32 per
 // round, +1) after them
@@ -839,10 +841,16 @@ __global__ __launch_bounds__(TW) void k_local_cc(const uint4* __restrict__ RT, i
                                                  uint32_t* __restrict__ f, uint32_t* __restrict__ D,
                                                  uint32_t* __restrict__ UR, uint64_t* __restrict__ lroot,
                                                  int64_t rwords, int64_t max_distinct,
-                                                 unsigned long long* __restrict__ stats, bool any_cap = false) {
-    if (((int)stats[S_P0] == 8 ? 8 : 7) != LP) return;  // the other tiling
-    // the other 8-position instance (any_cap: this one was launched alone)
-    if (LP == 8 && !any_cap && (int)stats[S_LCAP] != (CAP > kLocal8Cap ? 1 : 0)) return;
+                                                 unsigned long long* __restrict__ stats, bool any_cap = false,
+                                                 bool alone = false) {
+    // the other tiling, or the other 8-position instance (any_cap: this one takes both caps)
+    const bool mine = ((int)stats[S_P0] == 8 ? 8 : 7) == LP &&
+                      (LP != 8 || any_cap || (int)stats[S_LCAP] == (CAP > kLocal8Cap ? 1 : 0));
+    if (!mine) {
+        // launched alone on the previous resolve's tiling, which this bitmap does not take
+        if (alone && blockIdx.x == 0 && threadIdx.x == 0) stats[S_REDO] = 1;
+        return;
+    }
     local_cc_tile<CAP, TW, LP>((int64_t)blockIdx.x * TW, RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats);
 }
 
@@ -895,9 +903,28 @@ inline bool local8_single_enabled() {
 }
 
 // Every instance of k_local_cc (each exits early for the tiles of the others).
+// choice (round 4): the instance the workspace's previous resolve used (0: 8 positions,
+// <= 8192 codes per tile; 1: 8 positions, <= 16384; 2: 7 positions), launched alone (one
+// launch instead of three: the others exit at once, but each costs a kernel boundary on
+// the resolve chain); it flags S_REDO when the bitmap needs another one. -1: all.
 inline void launch_local_cc(const uint4* RT, int64_t words, int L, uint32_t* f, uint32_t* D, uint32_t* UR,
                             uint64_t* lroot, int64_t rwords, int64_t max_distinct, unsigned long long* stats,
-                            hipStream_t s) {
+                            hipStream_t s, int choice = -1) {
+    if (choice >= 0) {
+        const int64_t tiles8 = (words + kLocal8Words - 1) / kLocal8Words;
+        if (choice == 0)
+            hipLaunchKernelGGL((k_local_cc<kLocal8Cap, kLocal8Words, 8>), dim3((unsigned)tiles8), dim3(kLocal8Words), 0,
+                               s, RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats, false, true);
+        else if (choice == 1)
+            hipLaunchKernelGGL((k_local_cc<kLocal8BigCap, kLocal8Words, 8>), dim3((unsigned)tiles8),
+                               dim3(kLocal8Words), 0, s, RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats,
+                               true, true);
+        else
+            hipLaunchKernelGGL((k_local_cc<kLocalCodes, kLocalWords, 7>),
+                               dim3((unsigned)((words + kLocalWords - 1) / kLocalWords)), dim3(kBlock), 0, s, RT,
+                               words, L, f, D, UR, lroot, rwords, max_distinct, stats, false, true);
+        return;
+    }
     // Tiles of the 8-position instances; ROGTK_LOCAL8_SINGLE=1: when they all fit on the
     // chip at once (one workgroup per CU, e.g. 256 tiles at L = 12) the 16384-code
     // instance alone takes every 8-position batch, saving one empty launch
@@ -999,30 +1026,37 @@ __device__ __forceinline__ uint32_t root_of(const uint32_t* f, uint32_t x) {
     return r;
 }
 
-template <bool CHASE>
-__global__ __launch_bounds__(kBlock) void k_hook_g(const uint4* __restrict__ RT, const uint32_t* __restrict__ UR,
-                                                   int64_t words, int L, int p0, uint32_t* f,
-                                                   unsigned int* __restrict__ flags, int round,
-                                                   uint64_t* __restrict__ active, int64_t active_words,
-                                                   const unsigned long long* __restrict__ stats) {
+// CHECK (round 4): a read-only round: does any group of the frontier still cross? Sets
+// flags[round] and hooks nothing, writes no frontier bits (a later real round `round`
+// reads the same frontier). k_roots_check runs it beside the roots scan: converged, the
+// forest is unchanged and the roots stand; otherwise the host runs round `round` for real
+// and relabels (cluster_finish), so the last speculative round costs no launches of its own.
+template <bool CHASE, bool CHECK>
+__device__ __forceinline__ void hook_block(const int64_t bid, const uint4* __restrict__ RT,
+                                           const uint32_t* __restrict__ UR, int64_t words, int L, int p0,
+                                           uint32_t* f, unsigned int* __restrict__ flags, int round,
+                                           uint64_t* __restrict__ active, int64_t active_words,
+                                           const unsigned long long* __restrict__ stats) {
     if (round > 0 && flags[round - 1] == 0) return;  // converged earlier
     p0 = max(p0, (int)stats[S_P0]);  // the local phase's last position + 1 (7 or 8)
     const int64_t per = words >> 2;
     const int64_t tasks = (int64_t)(L - p0) * per;
-    const int64_t u = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t u = bid * kBlock + threadIdx.x;
     const uint64_t* prev = active + (int64_t)((round - 1) & 1) * active_words;
     uint64_t* next = active + (int64_t)(round & 1) * active_words;
     const bool act = per > 0 && u < tasks && (round == 0 || ((prev[u >> 6] >> (u & 63)) & 1ull));
     if (!__syncthreads_or(act)) {
-        if ((threadIdx.x & 63) == 0 && (u >> 6) < active_words) next[u >> 6] = 0;
+        if (!CHECK && (threadIdx.x & 63) == 0 && (u >> 6) < active_words) next[u >> 6] = 0;
         return;
     }
     __shared__ HookTable T;
-    for (int k = threadIdx.x; k < kHookSlots; k += kBlock) {
-        T.key[k] = kNone;
-        T.val[k] = kNone;
+    if (!CHECK) {
+        for (int k = threadIdx.x; k < kHookSlots; k += kBlock) {
+            T.key[k] = kNone;
+            T.val[k] = kNone;
+        }
+        __syncthreads();
     }
-    __syncthreads();
     uint32_t last_x = kNone, last_mn = kNone;
     bool crossed = false;
     if (act) {
@@ -1083,7 +1117,7 @@ __global__ __launch_bounds__(kBlock) void k_hook_g(const uint4* __restrict__ RT,
                         if ((adj[a] >> b) & 1u) mn = root[b] < mn ? root[b] : mn;
                     x[0] = root[a];
                     x[1] = mn;
-                    crossed |= hook_roots(T, f, x, 2, last_x, last_mn);
+                    crossed |= CHECK ? x[0] != x[1] : hook_roots(T, f, x, 2, last_x, last_mn);
                 }
             } else {
                 uint64_t mm = multi;
@@ -1097,16 +1131,21 @@ __global__ __launch_bounds__(kBlock) void k_hook_g(const uint4* __restrict__ RT,
                         if ((m[v] >> b) & 1ull)
                             x[k++] = root[v] != kNone ? root[v]
                                                       : root_of<CHASE>(f, e[v].z + (uint32_t)__popcll(m[v] & below));
-                    crossed |= hook_roots(T, f, x, k, last_x, last_mn);
+                    if (CHECK) {
+                        for (int v = 1; v < k; ++v) crossed |= x[v] != x[0];
+                    } else {
+                        crossed |= hook_roots(T, f, x, k, last_x, last_mn);
+                    }
                 }
             }
         }
     }
     const uint64_t crossed_bits = __ballot(crossed);
     if ((threadIdx.x & 63) == 0) {
-        if ((u >> 6) < active_words) next[u >> 6] = crossed_bits;
+        if (!CHECK && (u >> 6) < active_words) next[u >> 6] = crossed_bits;
         if (crossed_bits) flags[round] = 1u;
     }
+    if (CHECK) return;
     __syncthreads();
     for (int k = threadIdx.x; k < kHookSlots; k += kBlock) {
         const uint32_t x = T.key[k];
@@ -1115,6 +1154,15 @@ __global__ __launch_bounds__(kBlock) void k_hook_g(const uint4* __restrict__ RT,
         // in 3 productive rounds, with "any proposal wins" in 4 (measured)
         if (T.val[k] < f[x]) atomicMin(f + x, T.val[k]);
     }
+}
+
+template <bool CHASE>
+__global__ __launch_bounds__(kBlock) void k_hook_g(const uint4* __restrict__ RT, const uint32_t* __restrict__ UR,
+                                                   int64_t words, int L, int p0, uint32_t* f,
+                                                   unsigned int* __restrict__ flags, int round,
+                                                   uint64_t* __restrict__ active, int64_t active_words,
+                                                   const unsigned long long* __restrict__ stats) {
+    hook_block<CHASE, false>(blockIdx.x, RT, UR, words, L, p0, f, flags, round, active, active_words, stats);
 }
 
 __device__ __forceinline__ int64_t live_distinct(const unsigned long long* stats, int64_t max_distinct) {
@@ -1508,27 +1556,30 @@ __global__ __launch_bounds__(kBlock) void k_edge_jump(const uint2* __restrict__ 
 // needs no copy or event. (Measured: letting the last workgroup to arrive scan the sums
 // instead - a device-scope fence + atomic per workgroup - made this kernel 64-137 us.)
 constexpr int kRootWords = 64;
-__global__ __launch_bounds__(kBlock) void k_roots_scan(const uint32_t* __restrict__ f,
-                                                       const uint64_t* __restrict__ lroot, int64_t max_distinct,
-                                                       int64_t rwords, uint64_t* __restrict__ rbits,
-                                                       uint32_t* __restrict__ rpref, uint32_t* rblksum,
-                                                       const unsigned long long* stats, unsigned long long* host,
-                                                       unsigned long long* epoch) {
-    __shared__ uint32_t s_cnt[kRootWords];
-    if (host && blockIdx.x == 0) {
-        for (int k = threadIdx.x; k < kStatsBytes / 8; k += kBlock)
-            __hip_atomic_store(host + k, stats[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const unsigned long long e = *epoch + 1;  // one publish per resolve: no race
-            *epoch = e;
-            __hip_atomic_store(host + kStatsBytes / 8, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+
+// the stats block (round flags final) into mapped host memory, then the resolve's epoch
+__device__ __forceinline__ void publish_stats(const unsigned long long* stats, unsigned long long* host,
+                                              unsigned long long* epoch) {
+    for (int k = threadIdx.x; k < kStatsBytes / 8; k += blockDim.x)
+        __hip_atomic_store(host + k, stats[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long e = *epoch + 1;  // one publish per resolve: no race
+        *epoch = e;
+        __hip_atomic_store(host + kStatsBytes / 8, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+__device__ __forceinline__ void roots_block(const int64_t bid, const uint32_t* __restrict__ f,
+                                            const uint64_t* __restrict__ lroot, int64_t max_distinct,
+                                            int64_t rwords, uint64_t* __restrict__ rbits,
+                                            uint32_t* __restrict__ rpref, uint32_t* rblksum,
+                                            const unsigned long long* stats) {
+    __shared__ uint32_t s_cnt[kRootWords];
     const int64_t nd = live_distinct(stats, max_distinct);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int kPerWave = kRootWords / (kBlock / 64);  // 16
-    const int64_t w0 = (int64_t)blockIdx.x * kRootWords + wave * kPerWave;
+    const int64_t w0 = bid * kRootWords + wave * kPerWave;
     uint32_t fv[kPerWave];
     uint64_t lr[kPerWave];
 #pragma unroll
@@ -1559,10 +1610,38 @@ __global__ __launch_bounds__(kBlock) void k_roots_scan(const uint32_t* __restric
             const uint32_t t = __shfl_up(incl, off);
             if (lane >= off) incl += t;
         }
-        const int64_t w = (int64_t)blockIdx.x * kRootWords + lane;
+        const int64_t w = bid * kRootWords + lane;
         if (lane < kRootWords && w < rwords) rpref[w] = incl - v;
-        if (lane == kRootWords - 1) rblksum[blockIdx.x] = incl;
+        if (lane == kRootWords - 1) rblksum[bid] = incl;
     }
+}
+
+__global__ __launch_bounds__(kBlock) void k_roots_scan(const uint32_t* __restrict__ f,
+                                                       const uint64_t* __restrict__ lroot, int64_t max_distinct,
+                                                       int64_t rwords, uint64_t* __restrict__ rbits,
+                                                       uint32_t* __restrict__ rpref, uint32_t* rblksum,
+                                                       const unsigned long long* stats, unsigned long long* host,
+                                                       unsigned long long* epoch) {
+    if (host && blockIdx.x == 0) publish_stats(stats, host, epoch);
+    roots_block(blockIdx.x, f, lroot, max_distinct, rwords, rbits, rpref, rblksum, stats);
+}
+
+// The roots scan (workgroups [0, rblocks)) and, beside it, the read-only check of hook
+// round `round` (the rest; hook_block<false, true>): one launch for the last speculative
+// round and the roots. The publish moves to k_word_label (the check's flag is final there).
+__global__ __launch_bounds__(kBlock) void k_roots_check(const uint32_t* __restrict__ f,
+                                                        const uint64_t* __restrict__ lroot, int64_t max_distinct,
+                                                        int64_t rwords, uint64_t* __restrict__ rbits,
+                                                        uint32_t* __restrict__ rpref, uint32_t* rblksum,
+                                                        const unsigned long long* stats, int64_t rblocks,
+                                                        const uint4* __restrict__ RT, const uint32_t* __restrict__ UR,
+                                                        int64_t words, int L, int p0, unsigned int* flags, int round,
+                                                        uint64_t* active, int64_t active_words) {
+    if ((int64_t)blockIdx.x < rblocks)
+        roots_block(blockIdx.x, f, lroot, max_distinct, rwords, rbits, rpref, rblksum, stats);
+    else
+        hook_block<false, true>((int64_t)blockIdx.x - rblocks, RT, UR, words, L, p0, const_cast<uint32_t*>(f), flags,
+                                round, active, active_words, stats);
 }
 
 __device__ __forceinline__ uint32_t root_label(uint32_t r, const uint64_t* __restrict__ rbits,
@@ -1586,6 +1665,9 @@ __device__ __forceinline__ void put_label(uint64_t c, uint32_t i, uint32_t lab, 
 // all of its codes in one component (their f are global roots then: they are live): in
 // the giant components of a 1-edit-saturated space most words end up uniform, and assign
 // then needs one L2-resident load per row instead of a gather from the 4^L table.
+// rblksum != nullptr (round 4): the roots scan's block sums are scanned by every workgroup
+// into LDS (dynamic, nrb_max + 1 u32) instead of by a k_scan_blocks launch of their own
+// (one kernel boundary fewer on the resolve chain); workgroup 0 writes the cluster count.
 __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restrict__ f,
                                                        const uint32_t* __restrict__ UR, int64_t words,
                                                        const uint4* __restrict__ RT, int64_t max_distinct,
@@ -1594,7 +1676,34 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
                                                        const uint32_t* __restrict__ rblkoff,
                                                        uint32_t* __restrict__ wlab, uint64_t* __restrict__ wexc,
                                                        uint32_t* __restrict__ labelcode, uint32_t* __restrict__ ilab,
-                                                       uint2* __restrict__ wxl, int use_exc, int exc1_on) {
+                                                       uint2* __restrict__ wxl, int use_exc, int exc1_on,
+                                                       const uint32_t* __restrict__ rblksum = nullptr,
+                                                       int64_t nrb_max = 0, unsigned long long* stats = nullptr,
+                                                       const unsigned long long* pstats = nullptr,
+                                                       unsigned long long* host = nullptr,
+                                                       unsigned long long* epoch = nullptr) {
+    extern __shared__ uint32_t s_roff[];
+    __shared__ uint32_t s_wave[kBlock / 64];
+    if (host && blockIdx.x == 0) publish_stats(pstats, host, epoch);  // after k_roots_check
+    if (rblksum) {
+        const int64_t nd = live_distinct(stats, max_distinct);
+        const int64_t nrb = min<int64_t>(nrb_max, (nd + (int64_t)kRootWords * 64 - 1) / ((int64_t)kRootWords * 64));
+        uint32_t carry = 0;
+        for (int64_t b0 = 0; b0 < nrb; b0 += kBlock) {
+            const int64_t b = b0 + threadIdx.x;
+            const uint32_t v = b < nrb ? rblksum[b] : 0u;
+            uint32_t total;
+            const uint32_t ex = block_excl_scan(v, s_wave, total);
+            if (b < nrb) s_roff[b] = carry + ex;
+            carry += total;
+        }
+        if (threadIdx.x == 0) {
+            s_roff[nrb] = carry;
+            if (blockIdx.x == 0) stats[S_NCLUSTERS] = carry;
+        }
+        __syncthreads();
+        rblkoff = s_roff;
+    }
     for (int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x; w < words; w += (int64_t)gridDim.x * kBlock) {
         const uint32_t ur = UR[w];
         uint32_t root = kNone;
@@ -2005,6 +2114,8 @@ struct ResolveState {
     int needed = 0;  // the same, kept across launches (adaptive speculative rounds)
     bool word_labels = false;  // wpref holds word labels (max_distance 1)
     uint32_t scan_tag = 0;     // the last k_scan_rt launch's look-back tag (1..2^30-1)
+    int lcc_choice = -1;       // the local-CC instance of the last resolve (launch_local_cc)
+    bool checked = false;      // flags[launched] holds a read-only check round (k_roots_check)
     ClusterLayout cl{};
     // an assign enqueued before the flags were checked (rogtk_cluster_assign_deferred)
     struct {
@@ -2093,17 +2204,40 @@ int enqueue_post_rounds(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
     return ROGTK_OK;
 }
 
+// ROGTK_FOLD_ROOT_SCAN=0: the roots scan's block offsets by a k_scan_blocks launch (A/B)
+bool fold_root_scan_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("ROGTK_FOLD_ROOT_SCAN");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // host_stats != nullptr: k_roots_scan also publishes the stats block (the resolve's
 // first labels pass; never the re-run after extra rounds, which the host waits for)
+// check_round >= 0: the read-only check of that hook round runs inside the roots scan's
+// launch (k_roots_check), and the stats publish moves to k_word_label.
 int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
-                   unsigned long long* host_stats = nullptr) {
+                   unsigned long long* host_stats = nullptr, int check_round = -1) {
+    // the block offsets of the roots scan in every k_word_label workgroup's LDS when they
+    // fit (<= 16K root blocks: 67M distinct codes), else a k_scan_blocks launch
+    const bool lds_off = (cl.rblocks + 1) * 4 <= 65536 && fold_root_scan_enabled();
     {
         ProfScope prof(K_FLATTEN, s);
-        hipLaunchKernelGGL(k_roots_scan, dim3((unsigned)cl.rblocks), dim3(kBlock), 0, s, p.f, p.lroot,
-                           cl.max_distinct, cl.rwords, p.rbits, p.rpref, p.rblksum,
-                           (const unsigned long long*)p.stats, host_stats, p.epoch);
-        hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, p.rblksum, cl.rblocks, p.rblkoff, p.stats,
-                           (int)S_NCLUSTERS, -1, 0, (int64_t)kRootWords * 64);
+        if (check_round >= 0) {
+            const int64_t tasks = (int64_t)(cl.L - kLocalPos) * (cl.words >> 2);
+            hipLaunchKernelGGL(k_roots_check, dim3((unsigned)(cl.rblocks + grid_for(tasks))), dim3(kBlock), 0, s, p.f,
+                               p.lroot, cl.max_distinct, cl.rwords, p.rbits, p.rpref, p.rblksum,
+                               (const unsigned long long*)p.stats, cl.rblocks, p.RT, p.UR, cl.words, cl.L, kLocalPos,
+                               p.flags, check_round, p.active, cl.active_words);
+        } else {
+            hipLaunchKernelGGL(k_roots_scan, dim3((unsigned)cl.rblocks), dim3(kBlock), 0, s, p.f, p.lroot,
+                               cl.max_distinct, cl.rwords, p.rbits, p.rpref, p.rblksum,
+                               (const unsigned long long*)p.stats, host_stats, p.epoch);
+        }
+        if (!lds_off)
+            hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, p.rblksum, cl.rblocks, p.rblkoff, p.stats,
+                               (int)S_NCLUSTERS, -1, 0, (int64_t)kRootWords * 64);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     {
@@ -2118,9 +2252,11 @@ int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
             const char* e = getenv("ROGTK_WORD_EXC1");
             return e && e[0] == '0' ? 0 : 1;
         }();
-        hipLaunchKernelGGL(k_word_label, dim3(grid_for(cl.words, kPersistentGrid)), dim3(kBlock), 0, s, p.f, p.UR,
-                           cl.words, p.RT, cl.max_distinct, p.rbits, p.rpref, p.rblkoff, p.wpref, p.G, p.labelcode,
-                           p.ilab, p.wxl, use_exc, exc1_on);
+        hipLaunchKernelGGL(k_word_label, dim3(grid_for(cl.words, kPersistentGrid)), dim3(kBlock),
+                           lds_off ? (size_t)(cl.rblocks + 1) * 4 : 0, s, p.f, p.UR, cl.words, p.RT, cl.max_distinct,
+                           p.rbits, p.rpref, p.rblkoff, p.wpref, p.G, p.labelcode, p.ilab, p.wxl, use_exc, exc1_on,
+                           lds_off ? p.rblksum : nullptr, (int64_t)cl.rblocks, lds_off ? p.stats : nullptr,
+                           (const unsigned long long*)p.stats, check_round >= 0 ? host_stats : nullptr, p.epoch);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     return ROGTK_OK;
@@ -2155,9 +2291,27 @@ bool fused_scan_enabled() {
     }();
     return on;
 }
+// ROGTK_FUSED_CHECK=0: the last speculative hook round as a hook + jump launch pair (A/B)
+bool fused_check_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("ROGTK_FUSED_CHECK");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+bool lcc_predict_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("ROGTK_LCC_PREDICT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bitmaps, int n_bitmaps,
                     int max_distance, int mode, int spec, unsigned long long* host_stats, hipStream_t s,
-                    int phases = 3, uint32_t scan_tag = 0) {
+                    int phases = 3, uint32_t scan_tag = 0, int lcc_choice = -1, bool* checked = nullptr) {
+    if (checked) *checked = false;
     if ((phases & 1) && scan_tag) {  // single pass: RT, n_distinct and the tiling in one launch
         ProfScope prof(K_SCAN, s);
         hipLaunchKernelGGL(k_scan_rt, dim3((unsigned)cl.blocks), dim3(kBlock), 0, s, bitmaps, n_bitmaps, cl.words,
@@ -2196,7 +2350,8 @@ int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bi
     int launched = 0;
     if (phases & 1) {
         ProfScope prof(K_UNION, s);
-        launch_local_cc(p.RT, cl.words, cl.L, p.f, p.D, p.UR, p.lroot, cl.rwords, cl.max_distinct, p.stats, s);
+        launch_local_cc(p.RT, cl.words, cl.L, p.f, p.D, p.UR, p.lroot, cl.rwords, cl.max_distinct, p.stats, s,
+                        lcc_choice);
         if (!(phases & 2)) return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     {
@@ -2209,13 +2364,20 @@ int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bi
             hipLaunchKernelGGL(k_flatten_live, dim3(grid_for(cl.max_distinct, kPersistentGrid)), dim3(kBlock), 0, s,
                                p.f, p.lroot, cl.max_distinct, p.stats);
         } else if (cl.L > kLocalPos) {
-            if (enqueue_rounds(cl, p, 0, spec, s, mode)) return -1;
+            // the last speculative round as a read-only check inside the roots scan's launch
+            // (round 4: two kernel boundaries fewer on the resolve chain; a round that still
+            // finds crossings runs for real in cluster_finish)
+            const bool fuse = checked && host_stats && mode == kGlobalRounds && spec >= 2 && fused_check_enabled();
+            const int real = fuse ? spec - 1 : spec;
+            if (enqueue_rounds(cl, p, 0, real, s, mode)) return -1;
             if (enqueue_post_rounds(cl, p, s, mode)) return -1;
-            launched = spec;
-            // k_roots_scan stores the flags into mapped host memory and then the resolve's
-            // epoch (counted on the device): no copy-engine transfer, no event, no kernel
-            // of its own (a D2H copy + event record cost ~15 us of the resolve chain)
-            if (enqueue_labels(cl, p, s, host_stats)) return -1;
+            launched = real;
+            if (fuse) *checked = true;
+            // k_roots_scan (or k_word_label after a check) stores the flags into mapped host
+            // memory and then the resolve's epoch (counted on the device): no copy-engine
+            // transfer, no event, no kernel of its own (a D2H copy + event record cost ~15 us
+            // of the resolve chain)
+            if (enqueue_labels(cl, p, s, host_stats, fuse ? real : -1)) return -1;
             return hipGetLastError() == hipSuccess ? launched : -1;
         }
     }
@@ -2226,6 +2388,8 @@ int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bi
 // ROGTK_RESOLVE_GRAPH=1: replay the resolve as a hipGraph (A/B knob, off by default:
 // measured 0.536 vs 0.411 ms/step at 10M - the graph replays ran without overlapping the
 // other streams' kernels, serialising the pipeline)
+// ROGTK_LCC_PREDICT=0: launch every local-CC instance (each exits at once for the tilings
+// of the others) instead of the previous resolve's alone (A/B)
 bool graphs_enabled() {
     static const bool on = [] {
         const char* e = getenv("ROGTK_RESOLVE_GRAPH");
@@ -2280,6 +2444,7 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
     const GraphKey key{bitmaps, n_bitmaps, max_distance, mode, spec, cl.L, cl.max_distinct, cl.ecap};
     const bool graph = graphs_enabled() && !profiling_on() && phases == 3;
     int launched = 0;
+    bool checked = false;
     if (graph) {
         if (!st.gexec || !(st.gkey == key)) {
             if (st.gexec) {
@@ -2304,8 +2469,10 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
         ROGTK_HIP_CHECK(hipGraphLaunch(st.gexec, s));
         launched = st.glaunched;
     } else {
+        // one local-CC instance, the previous resolve's (checked on the device: S_REDO)
+        const int choice = rounds && phases == 3 && lcc_predict_enabled() ? st.lcc_choice : -1;
         launched = enqueue_resolve(cl, p, bitmaps, n_bitmaps, max_distance, mode, spec, hs, s, phases,
-                                   (phases & 1) ? next_tag() : 0u);
+                                   (phases & 1) ? next_tag() : 0u, choice, &checked);
         ROGTK_REQUIRE(launched >= 0, ROGTK_E_HIP, "cluster: resolve launch failed (%s)",
                       hipGetErrorString(hipGetLastError()));
     }
@@ -2314,6 +2481,7 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
         ++st.epoch;  // k_publish_stats publishes the device count of resolves, which matches
         st.mode = mode;
         st.launched = launched;
+        st.checked = checked;
         st.pending = true;
     }
     return ROGTK_OK;
@@ -2331,9 +2499,15 @@ namespace {
 int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone) {
     if (int rc = wait_published(st)) return rc;
     unsigned int* hflags = (unsigned int*)(st.hstats + kFlagsOff);
-    const bool edge_ovf = st.mode == kGlobalEdges && ((const unsigned long long*)st.hstats)[S_EDGE_OVF] != 0;
-    if (!edge_ovf) {
-        if (int z = first_zero(hflags, 0, st.launched); z >= 0) {
+    const unsigned long long* hs = (const unsigned long long*)st.hstats;
+    const bool edge_ovf = st.mode == kGlobalEdges && hs[S_EDGE_OVF] != 0;
+    // the local-CC instance this bitmap's tiling takes: the next resolve launches it alone
+    st.lcc_choice = hs[S_P0] == 8 ? (int)hs[S_LCAP] : 2;
+    const bool redo = hs[S_REDO] != 0;
+    const int scanned = st.launched + (st.checked ? 1 : 0);  // a check round's flag too
+    st.checked = false;
+    if (!edge_ovf && !redo) {
+        if (int z = first_zero(hflags, 0, scanned); z >= 0) {
             st.pending = false;
             st.deferred.on = false;
             st.rounds = z + 1;
@@ -2344,7 +2518,21 @@ int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone) 
     // the speculative rounds were not enough: continue synchronously, then relabel
     if (redone) *redone = 1;
     WsPtrs p = ws_ptrs(st.cl, const_cast<uint8_t*>((const uint8_t*)ws));
-    if (edge_ovf) {
+    if (redo) {
+        // the launched local-CC instance did not take this tiling (nothing of the local or
+        // global phase stands): the local CC again (every instance; it reads only RT),
+        // then the global rounds from round 0
+        ProfScope prof(K_UNION, s);
+        launch_local_cc(p.RT, st.cl.words, st.cl.L, p.f, p.D, p.UR, p.lroot, st.cl.rwords, st.cl.max_distinct,
+                        p.stats, s, -1);
+        ROGTK_HIP_CHECK(hipGetLastError());
+        ROGTK_HIP_CHECK(hipMemsetAsync(p.stats + S_REDO, 0, 8, s));
+        ROGTK_HIP_CHECK(hipMemsetAsync(p.flags, 0, kMaxRounds * sizeof(unsigned int), s));
+        std::memset(hflags, 0, kMaxRounds * sizeof(unsigned int));
+        st.mode = st.mode == kGlobalEdges ? kGlobalRounds : st.mode;
+        st.launched = 0;
+    }
+    if (edge_ovf && !redo) {
         // the edge list overflowed (the round-0 hooks stand): stars again, then the
         // bitmap rounds from round 0
         ProfScope prof(K_UNION, s);

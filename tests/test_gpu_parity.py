@@ -561,6 +561,37 @@ def test_dense_space_local_tilings_vs_oracle(rg, n_codes, expect_p0):
     assert p0 == expect_p0
 
 
+@pytest.mark.parametrize("deferred", [False, True])
+def test_local_cc_prediction_redo(rg, deferred):
+    """One workspace, batches whose tilings change: sparse (8 positions, <= 8192 codes per
+    tile), 19% dense (8 positions, <= 16384), 28% dense (7 positions), sparse again. Each
+    resolve launches only the local-CC instance of the workspace's previous resolve; a
+    mismatch flags S_REDO and cluster_finish redoes the local and global phases (and the
+    deferred assign). Ids equal the oracle's every time."""
+    import torch
+
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+
+    sizes = [900_000, 3_400_000, 5_500_000, 900_000, 900_000]
+    eng = D.ClusterEngine(12, max(sizes), "cuda")
+    for i, n_codes in enumerate(sizes):
+        rng = np.random.default_rng(1000 + i)
+        codes_h = rng.integers(0, 4 ** 12, n_codes, dtype=np.uint32)
+        codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
+        batch = D.PackedBatch(codes, 12)
+        cid = torch.empty(n_codes, dtype=torch.int32, device="cuda")
+        eng.mark_bitmap(batch)
+        eng.resolve(eng.local_bitmap, 1, 1)
+        eng.assign(batch, cid, deferred=deferred)
+        eng.sync()
+        stats = eng.stats()
+        torch.cuda.synchronize()
+        rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, 12)), 12, 1)
+        assert stats["n_clusters"] == rk and stats["error"] == 0, i
+        assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc), i
+
+
 @pytest.mark.parametrize("shards", [2, 4, 8])
 def test_sharded_resolve_matches_single(rg, shards):
     """N-rank exchange emulated on one GPU: ids identical to the single-batch run."""
