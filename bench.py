@@ -117,6 +117,9 @@ def parse():
                          "(one kernel fewer on the main stream; measured slower)")
     ap.add_argument("--late-assign", action="store_true",
                     help="host order: enqueue batch k-1's assign after batch k's resolve (round-2 default)")
+    ap.add_argument("--assign-prev-fused", action="store_true",
+                    help="batch k's score kernel also writes batch k-1's cluster ids (one launch: score and "
+                         "assign tiles interleaved; rogtk_umi_score_assign_prev_packed)")
     ap.add_argument("--no-c3", action="store_true",
                     help="skip the C3 line part (BASELINE configs[2]: 100M reads, k-mer spectra per UMI group; "
                          "runs after C2 on rank 0 of a one-GPU run)")
@@ -464,7 +467,8 @@ def main():
                        split_resolve=args.split_resolve, reuse_gate=args.reuse_gate,
                        assign_early=not args.late_assign, mark_first=False if args.score_first else "auto",
                        device_events=not args.torch_events, mark_stream=args.mark_stream,
-                       fused_assign=args.fused_assign, mark_parts=args.mark_parts)
+                       fused_assign=args.fused_assign, mark_parts=args.mark_parts,
+                       assign_prev_fused=args.assign_prev_fused)
 
     def step():
         pipe.submit(batch)
@@ -591,13 +595,17 @@ def main():
     value = n_total * args.steps / el if args.emulate_ranks == 1 else n * args.emulate_ranks * args.steps / el
     # roofline of the dominant kernel: algorithmic bytes per read of k_score_packed
     #   in: 4 B packed code; out: 6 x 8 B f64 fields + 4 B longest run + 1/8 B within bit
-    bpr = 4 + 48 + 4 + 0.125 + (4 if args.fused_assign else 0)  # + the u32 cluster id when fused
+    # + the u32 cluster id when the score kernel assigns its own batch; + 4 B code in and
+    # 4 B id out when it assigns the previous batch (--assign-prev-fused)
+    bpr = 4 + 48 + 4 + 0.125 + (4 if args.fused_assign else 8 if args.assign_prev_fused else 0)
     roof = None
     if "score_packed" in kernels:
         avg_s = kernels["score_packed"]["avg_us"] * 1e-6
         achieved = count * bpr / avg_s / 1e9
-        traffic, src = load_traffic(count, fused=args.fused_assign)
-        roof = {"kernel": "k_score_packed", "bound": "hbm", "achieved": round(achieved, 1),
+        traffic, src = load_traffic(count, fused=args.fused_assign,
+                                    key="score_assign_prev_hbm_bytes_per_launch" if args.assign_prev_fused else None)
+        roof = {"kernel": "k_score_assign_prev" if args.assign_prev_fused else "k_score_packed", "bound": "hbm",
+                "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "traffic_source": src,
                 "algorithmic_bytes_per_launch": int(count * bpr), "bytes_per_read": bpr,
@@ -618,8 +626,8 @@ def main():
         # the kernel with the largest share of the step's device time among the two that
         # stream every row (the resolve kernels move a few MB each): its §8(d) bytes and
         # its corrected PMC traffic
-        cands = {"k_score_packed": (kernels["score_packed"]["avg_us"], bpr, roof["traffic"])}
-        if "cluster_assign" in kernels and not args.fused_assign:
+        cands = {roof["kernel"]: (kernels["score_packed"]["avg_us"], bpr, roof["traffic"])}
+        if "cluster_assign" in kernels and not args.fused_assign and not args.assign_prev_fused:
             a_traffic, _ = load_traffic(count, key="assign_hbm_bytes_per_launch")
             cands["k_assign"] = (kernels["cluster_assign"]["avg_us"], 8.0, a_traffic)
         dk = max(cands, key=lambda k: cands[k][0])

@@ -118,6 +118,20 @@ int rogtk_umi_score_packed(const uint32_t* codes, const uint64_t* regular_bits, 
                            uint32_t* hamming_distance, uint64_t* hamming_within_bits,
                            void* cluster_ws, int64_t cluster_max_distinct, void* stream);
 
+/* Batch k's scores (as rogtk_umi_score_packed) and batch k-1's cluster ids (as
+ * rogtk_cluster_assign_deferred on prev_ws, which batch k-1 was resolved in) in ONE launch:
+ * the score tiles' HBM writes and the assign tiles' table gathers overlap inside the CUs,
+ * and the stream pays one kernel boundary instead of two (the pipeline's main stream,
+ * rogtk_amd.pipeline assign_prev_fused). Read prev_cluster_id only after
+ * rogtk_cluster_sync(prev_ws). Falls back to two launches where the previous batch has
+ * no word labels (max_distance 0, or labels by rank). */
+int rogtk_umi_score_assign_prev_packed(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
+                                       const rogtk_umi_scores* scores, const uint8_t* target, int64_t target_len,
+                                       uint32_t max_distance, uint32_t* hamming_distance,
+                                       uint64_t* hamming_within_bits, const void* prev_ws,
+                                       int64_t prev_max_distinct, const uint32_t* prev_codes,
+                                       const uint64_t* prev_regular_bits, int64_t prev_n, uint32_t* prev_cluster_id,
+                                       void* stream);
 /* rogtk_umi_score_packed + rogtk_cluster_assign[_deferred] of the same rows in ONE pass
  * over the codes (cluster_ws resolved by rogtk_cluster_resolve; deferred != 0 as
  * rogtk_cluster_assign_deferred): the assign half of the H3 hot path
@@ -588,7 +602,7 @@ int rogtk_bam_umi_dev(const rogtk_bam_batch* batch, int64_t n, int source, int u
                       uint8_t* values, int64_t values_cap, uint8_t* validity, void* stream);
 /* The same appended to a column of several batches with NO host synchronisation (config C5
  * overlaps the host's inflate with the GPU): rows go to offsets[row_base ..] (n + 1
- * entries; row_base a multiple of 64, validity words from row_base / 64), values at the
+ * entries) and to validity bits from row_base (ORed into a zeroed bitmap), values at the
  * column's running byte count *base (a device int64, updated on the device). Rows that
  * would pass values_cap are not written and counted in *overflow (a device u64). */
 int rogtk_bam_umi_append(const rogtk_bam_batch* batch, int64_t n, int source, int umi_len, int sep,

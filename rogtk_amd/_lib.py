@@ -97,6 +97,8 @@ SIGNATURES = {
     "rogtk_stage_strings": [_vp, _i32, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp],
     "rogtk_umi_score_assign_packed": [_vp, _vp, _i64, _i32, _P_SCORES, _vp, _i64, _u32, _vp, _vp, _vp, _i64, _vp,
                                       _i32, _vp],
+    "rogtk_umi_score_assign_prev_packed": [_vp, _vp, _i64, _i32, _P_SCORES, _vp, _i64, _u32, _vp, _vp, _vp, _i64,
+                                           _vp, _vp, _i64, _vp, _vp],
     "rogtk_umi_score_packed": [_vp, _vp, _i64, _i32, _P_SCORES, _vp, _i64, _u32, _vp, _vp, _vp,
                                _i64, _vp],
     "rogtk_umi_score_rows": [_vp, _i32, _vp, _vp, _vp, _i64, _i64, _P_SCORES, _vp, _i64, _u32, _vp,

@@ -305,7 +305,7 @@ __global__ __launch_bounds__(256) void k_bam_fill(const uint8_t* __restrict__ ra
 __global__ __launch_bounds__(256) void k_umi_len(const int64_t* __restrict__ seq_off, const uint64_t* __restrict__ seq_valid,
                                                  const int64_t* __restrict__ name_off, const uint8_t* __restrict__ name_val,
                                                  int64_t n, int source, int umi_len, int sep, int64_t* len,
-                                                 int64_t* start, uint64_t* valid) {
+                                                 int64_t* start, uint64_t* valid, int64_t row_base = -1) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool v = false;
     if (r < n) {
@@ -326,7 +326,19 @@ __global__ __launch_bounds__(256) void k_umi_len(const int64_t* __restrict__ seq
         start[r] = a;
     }
     const uint64_t bits = __ballot(v);
-    if ((threadIdx.x & 63) == 0 && (r >> 6) * 64 < n) valid[r >> 6] = bits;
+    if ((threadIdx.x & 63) == 0 && (r >> 6) * 64 < n) {
+        if (row_base < 0) {
+            valid[r >> 6] = bits;
+        } else {  // append: the wave's 64 rows start at bit row_base + r of a zeroed bitmap
+            const int64_t g = row_base + r;
+            const int sh = (int)(g & 63);
+            if (bits) {
+                atomicOr((unsigned long long*)valid + (g >> 6), (unsigned long long)(bits << sh));
+                if (sh && (bits >> (64 - sh))) atomicOr((unsigned long long*)valid + (g >> 6) + 1,
+                                                        (unsigned long long)(bits >> (64 - sh)));
+            }
+        }
+    }
 }
 
 __global__ __launch_bounds__(256) void k_umi_fill(const uint8_t* __restrict__ src, const int64_t* __restrict__ start,
@@ -1370,8 +1382,7 @@ int rogtk_bam_umi_append(const rogtk_bam_batch* batch, int64_t n, int source, in
     ROGTK_REQUIRE(source == 0 || source == 1, ROGTK_E_INVALID, "bam umi: source must be 0 (sequence) or 1 (name)");
     ROGTK_REQUIRE(source == 1 || umi_len > 0, ROGTK_E_INVALID, "bam umi: umi_len must be > 0");
     ROGTK_REQUIRE(source == 1 || batch->offsets[2], ROGTK_E_INVALID, "bam umi: the batch has no sequence column");
-    ROGTK_REQUIRE(n >= 0 && row_base >= 0 && row_base % 64 == 0, ROGTK_E_INVALID,
-                  "bam umi append: n >= 0 and a row base that is a multiple of 64");
+    ROGTK_REQUIRE(n >= 0 && row_base >= 0, ROGTK_E_INVALID, "bam umi append: n and row_base must be >= 0");
     if (n == 0) return ROGTK_OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     thread_local DevBuf len, start, cub;
@@ -1381,7 +1392,7 @@ int rogtk_bam_umi_append(const rogtk_bam_batch* batch, int64_t n, int source, in
     const unsigned g = (unsigned)((n + 255) / 256);
     hipLaunchKernelGGL(k_umi_len, dim3(g), dim3(256), 0, s, batch->offsets[2], (const uint64_t*)batch->validity[2],
                        batch->offsets[0], batch->values[0], n, source, umi_len, sep, len.as<int64_t>(),
-                       start.as<int64_t>(), (uint64_t*)validity + row_base / 64);
+                       start.as<int64_t>(), (uint64_t*)validity, row_base);
     ROGTK_HIP_CHECK(hipGetLastError());
     ROGTK_HIP_CHECK(hipMemsetAsync(len.as<int64_t>() + n, 0, 8, s));
     size_t tb = 0;

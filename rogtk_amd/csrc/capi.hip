@@ -730,6 +730,45 @@ int rogtk_umi_score_assign_packed(const uint32_t* codes, const uint64_t* regular
                                  deferred != 0);
 }
 
+int rogtk_umi_score_assign_prev_packed(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
+                                       const rogtk_umi_scores* scores, const uint8_t* target, int64_t target_len,
+                                       uint32_t max_distance, uint32_t* hamming_distance,
+                                       uint64_t* hamming_within_bits, const void* prev_ws,
+                                       int64_t prev_max_distinct, const uint32_t* prev_codes,
+                                       const uint64_t* prev_regular_bits, int64_t prev_n, uint32_t* prev_cluster_id,
+                                       void* stream) {
+    ROGTK_REQUIRE(umi_len >= 1 && umi_len <= kMaxPackedLen, ROGTK_E_UNSUPPORTED,
+                  "packed path: umi_len %d outside 1..%d", umi_len, kMaxPackedLen);
+    ROGTK_REQUIRE(n >= 0 && prev_n >= 0, ROGTK_E_INVALID, "n must be >= 0");
+    ROGTK_REQUIRE(n == 0 || codes, ROGTK_E_INVALID, "codes is NULL");
+    ROGTK_REQUIRE(prev_ws && (prev_n == 0 || (prev_codes && prev_cluster_id)), ROGTK_E_INVALID,
+                  "score_assign_prev: NULL previous-batch argument");
+    ROGTK_REQUIRE(target_len >= 0, ROGTK_E_INVALID, "target_len must be >= 0");
+    ROGTK_REQUIRE(aligned16(codes) && aligned16(prev_codes) && aligned16(prev_cluster_id), ROGTK_E_INVALID,
+                  "score_assign_prev: codes / cluster ids must be 16-byte aligned");
+    const ScoreOut o = to_score_out(scores);
+    if (int rc = check_packed_alignment(codes, o, hamming_distance)) return rc;
+    ClusterLayout cl;
+    if (int rc = cluster_layout(umi_len, prev_max_distinct, &cl)) return rc;
+    PackedParams p;
+    build_packed_params(umi_len, &p);
+    encode_target(target, target_len, umi_len, max_distance, &p);
+    hipStream_t s = as_stream(stream);
+    // the previous batch's assign is deferred (no host wait for its resolve's flags)
+    AssignIn a;
+    if (int rc = cluster_assign_prepare(cl, (const uint8_t*)prev_ws, prev_codes, prev_regular_bits, prev_n,
+                                        prev_cluster_id, s, true, &a))
+        return rc;
+    if (a.out)
+        return launch_score_assign_prev(codes, regular_bits, n, p, o, hamming_distance, hamming_within_bits,
+                                        prev_codes, prev_regular_bits, prev_n, a, s);
+    // no word labels (max_distance 0) or labels by rank: two launches
+    if (int rc = launch_score_packed(codes, regular_bits, n, p, o, hamming_distance, hamming_within_bits, nullptr, s))
+        return rc;
+    return launch_cluster_assign(cl, (const uint8_t*)prev_ws, prev_codes, prev_regular_bits, prev_n, prev_cluster_id,
+                                 s, true);
+}
+
 int rogtk_umi_score_rows(const void* offsets, int offset_width, const uint8_t* values,
                          const int64_t* rows, const int64_t* n_rows_dev, int64_t max_rows,
                          int64_t max_len, const rogtk_umi_scores* scores, const uint8_t* target,

@@ -230,6 +230,9 @@ int launch_stage(const void* offsets, int offset_width, const uint8_t* values,
                  const uint8_t* validity, int64_t validity_offset, int64_t n, int L,
                  uint32_t* codes, uint64_t* regular_bits, int64_t* irregular_rows,
                  unsigned long long* n_irregular, hipStream_t s);
+int launch_score_assign_prev(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, const PackedParams& p,
+                             const ScoreOut& o, uint32_t* hd, uint64_t* hw, const uint32_t* codes2,
+                             const uint64_t* regular_bits2, int64_t n2, const AssignIn& a2, hipStream_t s);
 int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
                         const PackedParams& p, const ScoreOut& o, uint32_t* hd, uint64_t* hw,
                         uint8_t* presence, hipStream_t s, const AssignIn* asg = nullptr);

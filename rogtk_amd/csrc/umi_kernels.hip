@@ -182,29 +182,15 @@ __device__ __forceinline__ uint32_t hamming_code(uint32_t code, const PackedPara
 // gathered right after the code load, so its latency hides behind the scoring; flagged
 // words read their exception mask, exception codes the per-code label table
 // (k_assign in cluster_kernels.hip is the standalone form, identical ids).
-template <bool SCORE, bool HAMD, bool HAMW, bool MARK, int LT = 0, bool ASG = false>
-__global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restrict__ codes,
-                                                          const uint64_t* __restrict__ regbits,
-                                                          int64_t n, const PackedParams P,
-                                                          const ScoreOut O,
-                                                          uint32_t* __restrict__ hd,
-                                                          uint64_t* __restrict__ hw,
-                                                          uint8_t* __restrict__ pres, const AssignIn A,
-                                                          uint64_t* tspan) {
-    span_enter(tspan);  // profiling only (NULL otherwise)
-    __shared__ double s_tab[4][kMaxPackedLen + 1];
-    if (SCORE) {
-        for (int t = threadIdx.x; t < 4 * (kMaxPackedLen + 1); t += kBlock) {
-            const int a = t / (kMaxPackedLen + 1), c = t % (kMaxPackedLen + 1);
-            s_tab[a][c] = a == 0 ? P.sh[c] : a == 1 ? P.di[c] : a == 2 ? P.ling[c] : P.frac[c];
-        }
-        __syncthreads();
-    }
+// One 1024-row block tile of k_score_packed (and of the score part of k_score_assign_prev).
+template <bool SCORE, bool HAMD, bool HAMW, bool MARK, int LT, bool ASG>
+__device__ __forceinline__ void score_tile(const int64_t tile, const uint32_t* __restrict__ codes,
+                                           const uint64_t* __restrict__ regbits, int64_t n, const PackedParams& P,
+                                           const ScoreOut& O, uint32_t* __restrict__ hd, uint64_t* __restrict__ hw,
+                                           uint8_t* __restrict__ pres, const AssignIn& A,
+                                           const double (*s_tab)[kMaxPackedLen + 1]) {
     const int L = P.L;
-    // Wave tile of 256 rows; lane l owns rows {2l, 2l+1, 128+2l, 129+2l} so that every
-    // 16-B (double2) store instruction of the wave writes 1 KB of contiguous output.
-    // grid-stride over 1024-row block tiles (a capped grid keeps fewer waves in flight)
-    for (int64_t tile = blockIdx.x; tile * kBlock * kRowsPerLane < n; tile += gridDim.x) {
+    {
         const int lane = threadIdx.x & 63;
         const int64_t base = ((int64_t)tile * kBlock + (threadIdx.x & ~63)) * kRowsPerLane;
         const int64_t rA = base + 2 * lane, rB = rA + 128;
@@ -341,6 +327,102 @@ __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restr
                 if (wb * 64 < n) hw[wb] = w23;
             }
         }
+    }
+}
+
+// the packed parameter tables in LDS (shannon / dinucleotide terms, ling, fractions)
+__device__ __forceinline__ void stage_tables(const PackedParams& P, double (*s_tab)[kMaxPackedLen + 1]) {
+    for (int t = threadIdx.x; t < 4 * (kMaxPackedLen + 1); t += kBlock) {
+        const int a = t / (kMaxPackedLen + 1), c = t % (kMaxPackedLen + 1);
+        s_tab[a][c] = a == 0 ? P.sh[c] : a == 1 ? P.di[c] : a == 2 ? P.ling[c] : P.frac[c];
+    }
+    __syncthreads();
+}
+
+template <bool SCORE, bool HAMD, bool HAMW, bool MARK, int LT = 0, bool ASG = false>
+__global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restrict__ codes,
+                                                          const uint64_t* __restrict__ regbits,
+                                                          int64_t n, const PackedParams P,
+                                                          const ScoreOut O,
+                                                          uint32_t* __restrict__ hd,
+                                                          uint64_t* __restrict__ hw,
+                                                          uint8_t* __restrict__ pres, const AssignIn A,
+                                                          uint64_t* tspan) {
+    span_enter(tspan);  // profiling only (NULL otherwise)
+    __shared__ double s_tab[4][kMaxPackedLen + 1];
+    if (SCORE) stage_tables(P, s_tab);
+    // Wave tile of 256 rows; lane l owns rows {2l, 2l+1, 128+2l, 129+2l} so that every
+    // 16-B (double2) store instruction of the wave writes 1 KB of contiguous output.
+    // grid-stride over 1024-row block tiles (a capped grid keeps fewer waves in flight)
+    for (int64_t tile = blockIdx.x; tile * kBlock * kRowsPerLane < n; tile += gridDim.x)
+        score_tile<SCORE, HAMD, HAMW, MARK, LT, ASG>(tile, codes, regbits, n, P, O, hd, hw, pres, A, s_tab);
+    span_exit(tspan);
+}
+
+// The label of one present regular code from the resolved tables (MODE 0: per-code table).
+__device__ __forceinline__ uint32_t code_label(const AssignIn& A, uint32_t c) {
+    const uint32_t wl = decode_word_label(A.wlab[c >> 6], A.wexc, A.wxl, c);
+    return wl != 0xFFFFFFFFu ? wl : A.labelcode[c];
+}
+
+// 1024 rows of the previous batch's assign: lane l of wave w owns 4 consecutive rows, so
+// each 16-B load / store instruction of a wave covers 1 KB contiguous.
+__device__ __forceinline__ void assign_tile(const int64_t tile, const uint32_t* __restrict__ codes,
+                                            const uint64_t* __restrict__ regbits, int64_t n, const AssignIn& A) {
+    const int64_t r0 = tile * (kBlock * 4) + 4 * (int64_t)threadIdx.x;
+    if (r0 >= n) return;
+    uint32_t c[4] = {0, 0, 0, 0}, id[4];
+    uint32_t reg;
+    if (r0 + 4 <= n) {
+        const u32x4_t v = stream_load(reinterpret_cast<const u32x4_t*>(codes + r0));
+        c[0] = v.x; c[1] = v.y; c[2] = v.z; c[3] = v.w;
+        reg = regbits ? (uint32_t)(regbits[r0 >> 6] >> (r0 & 63)) & 0xFu : 0xFu;
+    } else {
+        reg = 0;
+        for (int k = 0; k < 4; ++k)
+            if (r0 + k < n) {
+                c[k] = codes[r0 + k];
+                if (!regbits || ((regbits[(r0 + k) >> 6] >> ((r0 + k) & 63)) & 1u)) reg |= 1u << k;
+            }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) id[k] = ((reg >> k) & 1u) ? code_label(A, c[k]) : 0xFFFFFFFFu;
+    if (r0 + 4 <= n) {
+        stream_store(u32x4_t{id[0], id[1], id[2], id[3]}, reinterpret_cast<u32x4_t*>(A.out + r0));
+    } else {
+        for (int k = 0; k < 4; ++k)
+            if (r0 + k < n) A.out[r0 + k] = id[k];
+    }
+}
+
+// Batch k's scores and batch k - 1's cluster ids in ONE launch (horizontal fusion, round
+// 4): the score tiles stream HBM writes while the assign tiles wait on L2 gathers, so
+// the two overlap inside the CUs, and the main stream pays one kernel boundary (~11 us
+// on gfx950) instead of two. Tiles are interleaved 1:1 (position 2i: score tile i, 2i+1:
+// assign tile i; past the shorter batch, the other role takes every position), so both
+// roles run from the first wave to the last and neither leaves a tail.
+template <bool SCORE, bool HAMD, bool HAMW, int LT>
+__global__ __launch_bounds__(kBlock) void k_score_assign_prev(const uint32_t* __restrict__ codes,
+                                                               const uint64_t* __restrict__ regbits, int64_t n,
+                                                               const PackedParams P, const ScoreOut O,
+                                                               uint32_t* __restrict__ hd, uint64_t* __restrict__ hw,
+                                                               const uint32_t* __restrict__ codes2,
+                                                               const uint64_t* __restrict__ regbits2, int64_t n2,
+                                                               const AssignIn A2, uint64_t* tspan) {
+    span_enter(tspan);
+    __shared__ double s_tab[4][kMaxPackedLen + 1];
+    const int64_t ts = (n + kBlock * kRowsPerLane - 1) / (kBlock * kRowsPerLane);
+    const int64_t ta = (n2 + kBlock * 4 - 1) / (kBlock * 4);
+    const int64_t both = 2 * min(ts, ta);
+    const int64_t b = blockIdx.x;
+    const bool is_score = b < both ? (b & 1) == 0 : ts > ta;
+    const int64_t t = b < both ? (b >> 1) : (b - both) + (ts > ta ? ta : ts);
+    if (is_score) {
+        if (SCORE) stage_tables(P, s_tab);
+        const AssignIn none{nullptr, nullptr, nullptr, nullptr, nullptr};
+        score_tile<SCORE, HAMD, HAMW, false, LT, false>(t, codes, regbits, n, P, O, hd, hw, nullptr, none, s_tab);
+    } else {
+        assign_tile(t, codes2, regbits2, n2, A2);
     }
     span_exit(tspan);
 }
@@ -523,6 +605,40 @@ int launch_stage(const void* offsets, int offset_width, const uint8_t* values,
         hipLaunchKernelGGL(k_stage<8>, dim3(g), dim3(kBlock), 0, s, offsets, values, validity,
                            validity_offset, n, L, codes, regular_bits, irregular_rows, n_irregular);
     ROGTK_HIP_CHECK(hipGetLastError());
+    return ROGTK_OK;
+}
+
+int launch_score_assign_prev(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, const PackedParams& p,
+                             const ScoreOut& o, uint32_t* hd, uint64_t* hw, const uint32_t* codes2,
+                             const uint64_t* regular_bits2, int64_t n2, const AssignIn& a2, hipStream_t s) {
+    const bool score = any_score(o), hamd = p.ham_mode && hd, hamw = p.ham_mode && hw;
+    ROGTK_REQUIRE(a2.out && a2.wlab && a2.labelcode, ROGTK_E_INVALID, "score_assign_prev: no word-label tables");
+    if (n <= 0 && n2 <= 0) return ROGTK_OK;
+    ProfScope prof(K_SCORE_PACKED, s, true);
+    const int64_t ts = (std::max<int64_t>(n, 0) + kBlock * kRowsPerLane - 1) / (kBlock * kRowsPerLane);
+    const int64_t ta = (std::max<int64_t>(n2, 0) + kBlock * 4 - 1) / (kBlock * 4);
+    const int g = (int)std::max<int64_t>(ts + ta, 1);
+    uint64_t* tspan = span_begin(K_SCORE_PACKED, g, s);
+    const int sel = (score ? 4 : 0) | (hamd ? 2 : 0) | (hamw ? 1 : 0);
+#define ROGTK_SAP(S, D, W, LT)                                                                                  \
+    hipExtLaunchKernelGGL((k_score_assign_prev<S, D, W, LT>), dim3(g), dim3(kBlock), 0, s, prof.start(),        \
+                          prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, codes2, regular_bits2, n2, a2, tspan)
+    if (p.L == 12 && sel == 4 + 1) ROGTK_SAP(true, false, true, 12);
+    else if (p.L == 12 && sel == 4 + 2 + 1) ROGTK_SAP(true, true, true, 12);
+    else
+        switch (sel) {
+            case 1: ROGTK_SAP(false, false, true, 0); break;
+            case 2: ROGTK_SAP(false, true, false, 0); break;
+            case 3: ROGTK_SAP(false, true, true, 0); break;
+            case 4: ROGTK_SAP(true, false, false, 0); break;
+            case 5: ROGTK_SAP(true, false, true, 0); break;
+            case 6: ROGTK_SAP(true, true, false, 0); break;
+            case 7: ROGTK_SAP(true, true, true, 0); break;
+            default: ROGTK_SAP(false, false, false, 0); break;
+        }
+#undef ROGTK_SAP
+    ROGTK_HIP_CHECK(hipGetLastError());
+    span_end(K_SCORE_PACKED, tspan, g, s);
     return ROGTK_OK;
 }
 

@@ -163,6 +163,28 @@ def score_assign_packed(batch: PackedBatch, engine: "ClusterEngine", cluster_id:
               _p(engine.ws), engine.max_distinct, _p(cluster_id), 1 if deferred else 0, _s(stream))
 
 
+def score_assign_prev_packed(batch: PackedBatch, scores: Optional[Dict[str, torch.Tensor]], target: Optional[bytes],
+                             max_distance: int, hamming_distance: Optional[torch.Tensor],
+                             hamming_within_bits: Optional[torch.Tensor], prev_engine: "ClusterEngine",
+                             prev_batch: PackedBatch, prev_cluster_id: torch.Tensor, stream=None) -> None:
+    """score_packed(batch) + prev_engine.assign(prev_batch, prev_cluster_id, deferred=True)
+    in ONE launch (rogtk_umi_score_assign_prev_packed: score tiles and assign tiles of the
+    two batches interleaved); read prev_cluster_id after prev_engine.sync()."""
+    t = None
+    tl = 0
+    if target is not None:
+        tb = target.encode() if isinstance(target, str) else bytes(target)
+        t = ctypes.create_string_buffer(tb, max(len(tb), 1))
+        tl = len(tb)
+    if prev_cluster_id.dtype != torch.int32 or prev_cluster_id.numel() < prev_batch.n or \
+            not prev_cluster_id.is_contiguous():
+        raise ValueError("prev_cluster_id: contiguous int32 with >= n elements")
+    _lib.call("rogtk_umi_score_assign_prev_packed", _p(batch.codes), _p(batch.regular_bits), batch.n, batch.umi_len,
+              _scores_struct(scores), t, tl, max_distance, _p(hamming_distance), _p(hamming_within_bits),
+              _p(prev_engine.ws), prev_engine.max_distinct, _p(prev_batch.codes), _p(prev_batch.regular_bits),
+              prev_batch.n, _p(prev_cluster_id), _s(stream))
+
+
 def score_rows(offsets: torch.Tensor, values: torch.Tensor, rows: torch.Tensor,
                n_rows_dev: Optional[torch.Tensor], max_rows: int, max_len: int,
                scores: Optional[Dict[str, torch.Tensor]] = None, target: Optional[bytes] = None,

@@ -67,7 +67,7 @@ class UmiPipeline:
                  assign_on: str = "main", split_resolve: bool = False, reuse_gate: str = "auto",
                  assign_early: bool = True, mark_first="auto", device_events: bool = True,
                  mark_stream: bool = False, fused_assign: bool = False, mark_parts: bool = False,
-                 with_distance: bool = False):
+                 with_distance: bool = False, assign_prev_fused: bool = False):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
@@ -204,6 +204,14 @@ class UmiPipeline:
                               and assign_on == "main" and not fused_assign and on_assigned is None)
         if self.lazy_assigned:
             assert self.lag < len(self.slots), "the main stream must order assign(k) before mark(k + depth)"
+        # assign_prev_fused (round 4): batch k's score kernel also assigns batch k-1's ids
+        # (rogtk_umi_score_assign_prev_packed: one launch, score and assign tiles
+        # interleaved) instead of a score launch and an assign launch on the main stream
+        if assign_prev_fused and not (assign_on == "main" and self.mark_first and not self.fused_mark
+                                      and not fused_assign and with_scores and self.s_mark is self.main):
+            raise ValueError("assign_prev_fused needs assign_on='main', the mark first on the main stream, scores "
+                             "and no fused_assign")
+        self.assign_prev_fused = assign_prev_fused
 
     def submit(self, batch: D.PackedBatch):
         """Enqueue one batch; returns its slot. Scores and Hamming outputs are valid once the
@@ -234,7 +242,13 @@ class UmiPipeline:
         gate_resolve = self.reuse_gate == "resolve"
         if slot.assigned is not None and not gate_resolve and self.s_assign is not self.main:
             D.wait_for(self.main, slot.assigned)
-        if self.mark_first:
+        if self.mark_first and self.assign_prev_fused:
+            marked = self._mark(slot, batch, gate_resolve)
+            if self.queue and len(self.queue) >= max(self.lag, 1):
+                self._score_assign_prev(slot, batch)
+            else:
+                self._score(slot, batch)
+        elif self.mark_first:
             # the presence bitmap needs only the codes: mark first, so the latency-bound
             # resolve of this batch starts while its score kernel streams (host order:
             # mark, score, the previous assign, then the ~15 launches of the resolve, so no
@@ -264,6 +278,22 @@ class UmiPipeline:
 
     def _event(self):
         return D.StreamEvent() if self.device_events else torch.cuda.Event()
+
+    def _score_assign_prev(self, slot: _Slot, batch: D.PackedBatch):
+        """Batch k's scores and the oldest queued batch's assign in one launch on main."""
+        pslot, pbatch, resolved = self.queue.popleft()
+        D.wait_for(self.main, resolved)
+        if self.on_assigned is not None:  # the consumer reads final ids: complete the resolve first
+            pslot.eng.sync(stream=self.main)
+        D.score_assign_prev_packed(batch, slot.scores, self.target, self.max_hamming, slot.dist, slot.within,
+                                   pslot.eng, pbatch, pslot.cid, stream=self.main)
+        if self.on_assigned is not None:
+            with torch.cuda.stream(self.main):
+                self.on_assigned(pslot, pbatch)
+        pslot.assigned = _ON_MAIN if self.lazy_assigned else self._event()
+        if not self.lazy_assigned:
+            pslot.assigned.record(self.main)
+            self.last_assigned = pslot.assigned
 
     def _score(self, slot: _Slot, batch: D.PackedBatch):
         D.score_packed(batch, slot.scores, self.target, self.max_hamming, slot.dist, slot.within,

@@ -638,7 +638,8 @@ def test_full_size_c2_properties(rg):
                           scores["combined_score"][:n].cpu().numpy().view(np.uint64))
 
 
-def test_full_size_c2_bench_pipeline_all_outputs(rg):
+@pytest.mark.parametrize("prevfused", [False, True])
+def test_full_size_c2_bench_pipeline_all_outputs(rg, prevfused):
     """BASELINE C2 through the bench's own path: 10M reads, UmiPipeline with bench.py's
     arguments (depth 2, slice-bucket mark, assign on the main stream, deferred assigns,
     device events), three submits of the batch as the bench's steps do; every output of
@@ -655,7 +656,7 @@ def test_full_size_c2_bench_pipeline_all_outputs(rg):
     codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
     batch = D.PackedBatch(codes, L)
     pipe = UmiPipeline(L, min(n, 4 ** L), n, "cuda", depth=2, target=b"ACGTACGTACGT", max_distance=1,
-                       score_alone=True, with_distance=True)
+                       score_alone=True, with_distance=True, assign_prev_fused=prevfused)
     for _ in range(3):
         pipe.submit(batch)
     pipe.drain()
@@ -684,7 +685,8 @@ def test_full_size_c2_bench_pipeline_all_outputs(rg):
 @pytest.mark.parametrize("depth,nb,alone", [(4, 4, False), (2, 5, False), (1, 3, False), (3, 7, False),
                                              (2, 6, True), (3, 5, True)])
 @pytest.mark.parametrize("mark", ["xcd", "fused", "sort"])
-@pytest.mark.parametrize("assign_on", ["resolve", "separate", "main", "main_mark_stream", "main_fused"])
+@pytest.mark.parametrize("assign_on", ["resolve", "separate", "main", "main_mark_stream", "main_fused",
+                                       "main_prevfused"])
 def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assign_on):
     """rogtk_amd.pipeline (3 streams, `depth` batches in flight) == the sequential device
     path for EVERY batch (outputs copied out by the on_assigned hook before slot reuse)."""
@@ -699,7 +701,8 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assig
     outs = []
     mark_stream = assign_on == "main_mark_stream"
     fused = assign_on == "main_fused"
-    if mark_stream or fused:
+    prevfused = assign_on == "main_prevfused"
+    if mark_stream or fused or prevfused:
         if mark == "fused":
             pytest.skip("a mark fused into the score kernel has no stream / pass of its own")
         if fused and depth < 2:
@@ -712,7 +715,7 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assig
 
     pipe = UmiPipeline(L, n, n, "cuda", depth=depth, target=b"ACGTACGTACGT", max_distance=1, mark=mark,
                        on_assigned=grab, score_alone=alone, assign_on=assign_on, mark_stream=mark_stream,
-                       fused_assign=fused)
+                       fused_assign=fused, assign_prev_fused=prevfused)
     keep = []
     for s in seeds:
         codes = torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda()

@@ -5,6 +5,7 @@
 #   AB_KEYS    space-separated JSON keys printed per run (dotted = nested) (default "ms_per_step value")
 #   AB_ENV_<name>  extra environment for that build's runs, e.g. AB_ENV_new="ROGTK_X=1"
 #   AB_SO_<name>   the library a name runs (default tools/ab/<name>.so), e.g. AB_SO_ev=new
+#   AB_ARGS_<name> extra arguments appended to AB_CMD for that name
 #   PRE_TESTS  optional pytest selection run first on the LAST build of AB_ORDER ("" = none)
 #   AB_T       per-run time limit in seconds (default 240)
 # Stops at the first failing step; leaves the last build of AB_ORDER installed.
@@ -27,7 +28,8 @@ for v in $ORDER; do
     i=$((i + 1))
     soname="AB_SO_$v"; cp tools/ab/${!soname:-$v}.so rogtk_amd/librogtk_hip.so
     envname="AB_ENV_$v"; extra=${!envname:-}
-    env $extra timeout -k 10 ${AB_T:-240} $CMD > gpurun_out/ab_${i}_$v.log 2>&1
+    argname="AB_ARGS_$v"; args=${!argname:-}
+    env $extra timeout -k 10 ${AB_T:-240} $CMD $args > gpurun_out/ab_${i}_$v.log 2>&1
     rc=$?; [ $rc -eq 0 ] || { echo "$v rc=$rc"; tail -5 gpurun_out/ab_${i}_$v.log; exit $rc; }
     python3 - "$v" "$KEYS" gpurun_out/ab_${i}_$v.log <<'EOF'
 import json, sys
