@@ -495,7 +495,10 @@ def main():
         # events on their dispatch packets (no packets of their own: the score kernel also
         # by its in-kernel span); the other kernels' bracketing events would add packets
         # to their streams (measured: +0.055 ms/step when all kernels are bracketed)
-        D.profile_select("score_packed,cluster_assign")
+        try:
+            D.profile_select("score_packed,cluster_assign")
+        except Exception:  # a library without kernel lists (A/B of older builds)
+            D.profile_select("score_packed")
         D.profile_reset()
         D.profile_enable(True)
     barrier(world)
@@ -710,12 +713,15 @@ def _rank_main(argv):
 if __name__ == "__main__":
     _args = parse()
     if _args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        # one process per GPU, started before anything touches the GPU (device_count()
-        # does not initialise HIP on this image)
+        # one process per GPU, started before anything touches the GPU
         from rogtk_amd.launch import run_local_ranks
 
-        # (ROGTK_DIST_BACKEND=gloo, tests only: ranks may share a GPU)
-        if os.environ.get("ROGTK_DIST_BACKEND", "nccl") == "nccl" and torch.cuda.device_count() < _args.gpus:
-            raise SystemExit(f"bench.py: --gpus {_args.gpus} but {torch.cuda.device_count()} GPU(s) visible")
+        from rogtk_amd.launch import visible_gpus
+
+        # (ROGTK_DIST_BACKEND=gloo, tests only: ranks may share a GPU). The count comes from
+        # the KFD topology in sysfs: no HIP call in this parent, whose children are spawned
+        n_vis = visible_gpus()
+        if os.environ.get("ROGTK_DIST_BACKEND", "nccl") == "nccl" and n_vis is not None and n_vis < _args.gpus:
+            raise SystemExit(f"bench.py: --gpus {_args.gpus} but {n_vis} GPU(s) visible")
         sys.exit(run_local_ranks(_args.gpus, _rank_main, (sys.argv[1:],)))
     main()

@@ -350,7 +350,8 @@ __global__ __launch_bounds__(kBlock) void k_row_gather(const uint64_t* __restric
                                                        const uint32_t* __restrict__ row_group,
                                                        uint64_t* __restrict__ packed, int64_t* __restrict__ row_obs,
                                                        int32_t* __restrict__ row_len,
-                                                       unsigned long long* __restrict__ gstat) {
+                                                       unsigned long long* __restrict__ gstat,
+                                                       unsigned long long* __restrict__ long_rows) {
     constexpr int RPI = 64 / B;  // rows per wave-instruction
     const int lane = threadIdx.x & 63, w = lane & (B - 1), sub = lane / B;
     const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
@@ -379,6 +380,9 @@ __global__ __launch_bounds__(kBlock) void k_row_gather(const uint64_t* __restric
             const bool ok = inK && ((meta >> 32) & 1ull);
             if (rr < n_rows && w >= 1 && w <= S) packed[rr * S + (w - 1)] = v[j];
             if (rr < n_rows && w == 0) {
+                // a row longer than S words (a max_len below the real lengths, or past the
+                // block) would read the next row's bases: counted, and the call fails
+                if (inK && (int64_t)len > 32 * (int64_t)S) atomicAdd(long_rows, 1ull);
                 const bool use = ok && (int64_t)len >= K;
                 row_obs[rr] = use ? (int64_t)len - K + 1 : 0;
                 row_len[rr] = use ? (int32_t)len : 0;
@@ -1278,6 +1282,7 @@ struct KmerCtx {
     DevBuf key_lo, key_hi, ext, grp, idx, perm_a, perm_b, tmp_u64, tmp_u32;
     DevBuf s_lo, s_hi, s_ext, s_grp, head, rid, r_valid, r_first, r_ext, r_cnt, vpos;
     DevBuf v_lo, v_hi, v_grp, v_ext, v_cnt, t_kmer, t_ext, t_cnt, o_kmer, o_ext, o_cnt, cub, gsmall, caps, scal;
+    DevBuf long_rows;  // block path: grouped rows longer than the staging stride (an error)
     bool lds_path = true;  // rogtk_kmer_set_path(): tests force the global path
     int64_t last_lds_groups = 0, last_global_groups = 0;  // rogtk_kmer_path_stats()
     ~KmerCtx() {
@@ -1380,7 +1385,7 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
 #define ROGTK_GATHER(BW)                                                                                       \
     hipExtLaunchKernelGGL(k_row_gather<BW>, dim3(ggrid), dim3(kBlock), 0, s, prof.start(), prof.stop(), 0,      \
                        in.blocks, in.rows, n_rows, K, stride, in.gk, c->row_group.as<uint32_t>(), c->packed.as<uint64_t>(), c->row_obs.as<int64_t>(),  \
-                       c->row_len.as<int32_t>(), gstat)
+                       c->row_len.as<int32_t>(), gstat, c->long_rows.as<unsigned long long>())
         if (in.B == 8) ROGTK_GATHER(8);
         else if (in.B == 16) ROGTK_GATHER(16);
         else ROGTK_GATHER(32);
@@ -1812,6 +1817,9 @@ int spectrum_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* v
     ROGTK_HIP_CHECK(hipMemsetAsync(c->gk.p, K, G, s));
     ROGTK_HIP_CHECK(hipMemsetAsync(c->gstat.p, 0, G * 5 * 8, s));
     ROGTK_HIP_CHECK(hipMemsetAsync(c->gcount.p, 0, G * 8, s));
+    if (int rc = c->long_rows.ensure(8)) return rc;
+    ROGTK_HIP_CHECK(hipMemsetAsync(c->long_rows.p, 0, 8, s));
+    unsigned long long long_rows = 0;
     int64_t tcap = 0;
     if (blocks) {
         // block path: a row holds at most 32 S bases, so at most 32 S - K + 1 observations;
@@ -1844,9 +1852,12 @@ int spectrum_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* v
     hipLaunchKernelGGL(k_tail_sum, dim3(1), dim3(64), 0, s, entry_offsets, c->gcount.as<int64_t>(), G,
                        entry_offsets + G);
     ROGTK_HIP_CHECK(hipMemcpyAsync(n_entries, entry_offsets + G, 8, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&long_rows, c->long_rows.p, 8, hipMemcpyDeviceToHost, s));
     hipLaunchKernelGGL(k_group_stats_out, dim3(grid_for(G)), dim3(kBlock), 0, s, c->gstat.as<unsigned long long>(),
                        c->gcount.as<int64_t>(), G, K, group_stats);
     ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    ROGTK_REQUIRE(long_rows == 0, ROGTK_E_INVALID,
+                  "kmer_blocks: %llu row(s) longer than max_len %d (the packed column's bound)", long_rows, 32 * S);
     ROGTK_REQUIRE(*n_entries <= capacity, ROGTK_E_OVERFLOW, "kmer_dev: %lld entries exceed capacity %lld",
                   (long long)*n_entries, (long long)capacity);
     if (*n_entries > 0) {

@@ -17,6 +17,29 @@ from multiprocessing.connection import wait
 from typing import Callable, Sequence
 
 
+def visible_gpus():
+    """GPUs this process could use, counted WITHOUT initialising HIP (the launcher must not
+    touch the GPU before it spawns the ranks): the KFD topology nodes with a GPU id,
+    narrowed by ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES. None
+    when the topology is not readable (the ranks then find out themselves)."""
+    n = 0
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        for node in os.listdir(root):
+            try:
+                with open(os.path.join(root, node, "gpu_id")) as f:
+                    n += int(f.read().strip() or 0) != 0
+            except (OSError, ValueError):
+                pass
+    except OSError:
+        return None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

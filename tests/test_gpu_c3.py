@@ -268,3 +268,25 @@ def test_packed_blocks_match_oracle(lo, hi, bw):
             assert np.array_equal(got["exts"].cpu().numpy(), ref["exts"]), (k, path)
             assert np.array_equal(got["counts"].cpu().numpy().view(np.uint16), ref["counts"]), (k, path)
     _lib.call("rogtk_kmer_set_path", 1)
+
+
+def test_packed_reads_max_len_too_small_fails_loudly():
+    """a PackedReads built with a max_len below the real row lengths used to
+    stage truncated rows at a stride the k-mer kernels overran; the spectrum call now
+    fails (rows longer than the stride are counted on the device)."""
+    import torch
+
+    from rogtk_amd import _lib
+    from rogtk_amd import device as D
+
+    rng = np.random.default_rng(5)
+    items = [bytes(rng.choice(list(b"ACGT"), size=150).astype(np.uint8)) for _ in range(40)]
+    lens = np.array([len(x) for x in items], np.int64)
+    off = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)])).cuda()
+    vals = torch.from_numpy(np.frombuffer(b"".join(items), np.uint8).copy()).cuda()
+    go = torch.tensor([0, 20, 40], dtype=torch.int64).cuda()
+    ok = D.PackedReads(off, vals)
+    D.kmer_spectrum_blocks(ok, off, vals, go, 17, 1, int((lens - 3).sum()))
+    short = D.PackedReads(off, vals, max_len=100)  # 150-bp rows packed with a 100-base bound
+    with pytest.raises(_lib.RogtkError, match="longer than max_len"):
+        D.kmer_spectrum_blocks(short, off, vals, go, 17, 1, int((lens - 3).sum()))
