@@ -120,6 +120,8 @@ def parse():
     ap.add_argument("--assign-prev-fused", action="store_true",
                     help="batch k's score kernel also writes batch k-1's cluster ids (one launch: score and "
                          "assign tiles interleaved; rogtk_umi_score_assign_prev_packed)")
+    ap.add_argument("--assign-lag", type=int, default=0,
+                    help="assign batch k-lag at batch k's submit (0: the pipeline's default, 1 per resolve stream)")
     ap.add_argument("--no-c3", action="store_true",
                     help="skip the C3 line part (BASELINE configs[2]: 100M reads, k-mer spectra per UMI group; "
                          "runs after C2 on rank 0 of a one-GPU run)")
@@ -468,7 +470,7 @@ def main():
                        assign_early=not args.late_assign, mark_first=False if args.score_first else "auto",
                        device_events=not args.torch_events, mark_stream=args.mark_stream,
                        fused_assign=args.fused_assign, mark_parts=args.mark_parts,
-                       assign_prev_fused=args.assign_prev_fused)
+                       assign_prev_fused=args.assign_prev_fused, assign_lag=args.assign_lag)
 
     def step():
         pipe.submit(batch)

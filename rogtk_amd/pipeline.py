@@ -67,7 +67,7 @@ class UmiPipeline:
                  assign_on: str = "main", split_resolve: bool = False, reuse_gate: str = "auto",
                  assign_early: bool = True, mark_first="auto", device_events: bool = True,
                  mark_stream: bool = False, fused_assign: bool = False, mark_parts: bool = False,
-                 with_distance: bool = False, assign_prev_fused: bool = False):
+                 with_distance: bool = False, assign_prev_fused: bool = False, assign_lag: int = 0):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
@@ -99,6 +99,12 @@ class UmiPipeline:
         # assign lags resolve by one batch only when a second slot exists: with one
         # slot the next batch's resolve would overwrite the tables assign reads
         self.lag = resolve_streams if depth > 1 else 0
+        # assign_lag > 0: batch k-lag's assign is enqueued at batch k's submit (a longer
+        # window for its resolve; needs depth > assign_lag, each slot waits one batch longer)
+        if assign_lag:
+            if not 0 < assign_lag < depth or assign_lag < resolve_streams:
+                raise ValueError("assign_lag must be in [resolve_streams, depth)")
+            self.lag = assign_lag
         # on_assigned(slot, batch): called with the assign stream current, after the
         # batch's assign and before its slot may be reused (e.g. to copy outputs out)
         self.on_assigned = on_assigned
