@@ -659,6 +659,15 @@ struct LdsCfg {
 };
 constexpr unsigned long long kEmpty = ~0ull;
 
+// ROGTK_KMER_INSERT=1: the class-3 LDS kernel's V = 1 insert loop (round-4 A/B; read once)
+inline int kmer_insert_v() {
+    static const int v = [] {
+        const char* e = getenv("ROGTK_KMER_INSERT");
+        return e && atoi(e) == 1 ? 1 : 0;
+    }();
+    return v;
+}
+
 #ifdef ROGTK_KMER_TIMING  // experiment builds only: per-phase clocks of k_kmer_lds (thread 0)
 __device__ unsigned long long g_kmer_clk[8];
 #define KT(k) do { if (tid == 0) { const unsigned long long now_ = wall_clock64(); kt_acc[k] += now_ - kt_last; kt_last = now_; } } while (0)
@@ -677,7 +686,11 @@ struct GroupDesc {
     int32_t nrows, nwords;
 };
 
-template <int CLS, int TB>
+// V = 1 (round 4, ROGTK_KMER_INSERT=1 while it is A/B'd): the insert loop issues its LDS
+// reads together (the overflow flag and the previous, current and next packed word, one
+// wait for all), takes the left extension base from the previous word without a divergent
+// branch, and hashes the 64-bit key with one 32-bit multiply instead of a 64-bit one
+template <int CLS, int TB, int V = 0>
 __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDesc* __restrict__ gdesc, int64_t G,
                                                      uint8_t* __restrict__ gsmall, int K, int64_t min_cov,
                                                      const int32_t* __restrict__ row_len,
@@ -804,23 +817,50 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
             const uint64_t* rw = words + m_w[ri];
             for (int p = lane + ((u & 1) << 6); p < nobs; p += 128) {
                 const int b = 2 * (p & 31);
-                const uint64_t x0 = rw[p >> 5], x1 = rw[(p >> 5) + 1];
+                uint32_t over = 0;
+                uint64_t x0, x1, xm = 0;
+                if constexpr (V == 1) {
+                    if (kBounded) over = __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    const int wi = p >> 5;
+                    x0 = rw[wi];
+                    x1 = rw[wi + 1];
+                    xm = rw[wi > 0 ? wi - 1 : 0];  // p == 0 (no left base) reads word 0 unused
+                } else {
+                    x0 = rw[p >> 5];
+                    x1 = rw[(p >> 5) + 1];
+                }
                 const uint64_t top = b ? (x0 << b) | (x1 >> (64 - b)) : x0;
                 const uint64_t key = (top >> (64 - 2 * K)) & kmask;
                 // extension bases from the two words already loaded (k_eff <= 32: base p + K
                 // lies in x0 or x1); only a k-mer starting a word loads its left base
                 uint32_t e = 0;
-                if (p > 0) e |= 1u << (b ? (uint32_t)(x0 >> (64 - b)) & 3u : (uint32_t)rw[(p >> 5) - 1] & 3u);
-                if (p + K < len) {
+                if constexpr (V == 1) {
+                    const uint32_t lb = b ? (uint32_t)(x0 >> (64 - b)) : (uint32_t)xm;
+                    e = p > 0 ? 1u << (lb & 3u) : 0u;
                     const int t = (p & 31) + K;
-                    e |= 1u << (4 + ((uint32_t)((t < 32 ? x0 : x1) >> (62 - 2 * (t & 31))) & 3u));
+                    const uint32_t rb = (uint32_t)((t < 32 ? x0 : x1) >> (62 - 2 * (t & 31))) & 3u;
+                    e |= p + K < len ? 1u << (4 + rb) : 0u;
+                    // the flag's branch stays behind the word reads (one LDS wait for all)
+                    asm volatile("" : "+v"(over) : "v"(x0), "v"(x1), "v"(xm));
+                    if (over) break;
+                } else {
+                    if (p > 0) e |= 1u << (b ? (uint32_t)(x0 >> (64 - b)) & 3u : (uint32_t)rw[(p >> 5) - 1] & 3u);
+                    if (p + K < len) {
+                        const int t = (p & 31) + K;
+                        e |= 1u << (4 + ((uint32_t)((t < 32 ? x0 : x1) >> (62 - 2 * (t & 31))) & 3u));
+                    }
+                    if (kBounded && __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
                 }
-                if (kBounded && __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
                 uint32_t slot;
                 if (key == kEmpty) {
                     slot = kLdsSlots;
                 } else {
-                    slot = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - hbits));
+                    if constexpr (V == 1) {
+                        const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
+                        slot = ((lo ^ __builtin_amdgcn_alignbit(hi, hi, 16)) * 0x9E3779B1u) >> (32 - hbits);
+                    } else {
+                        slot = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - hbits));
+                    }
                     while (true) {
                         const unsigned long long prev = atomicCAS(&tkey[slot], kEmpty, (unsigned long long)key);
                         if (prev == kEmpty || prev == key) break;
@@ -1428,16 +1468,23 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
         hipLaunchKernelGGL(k_tail_sum, dim3(1), dim3(64), 0, s, co, in.cap_fill, G, co + G);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
+    if (lds && kmer_insert_v() == 1) {
+        ProfScope prof(K_KMER_LDS, s, true);
+        hipExtLaunchKernelGGL((k_kmer_lds<3, kLdsBlock, 1>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)),
+                              dim3(kLdsBlock), 0, s, prof.start(), prof.stop(), 0, c->gdesc.as<GroupDesc>(), G,
+                              c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
+                              c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
+                              c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
+    } else if (lds) {
+        ProfScope prof(K_KMER_LDS, s, true);
+        hipExtLaunchKernelGGL((k_kmer_lds<3, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)),
+                              dim3(kLdsBlock), 0, s, prof.start(), prof.stop(), 0, c->gdesc.as<GroupDesc>(), G,
+                              c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
+                              c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
+                              c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
+    }
     if (lds) {
         // one workgroup per small group, straight from the packed rows
-        {
-            ProfScope prof(K_KMER_LDS, s, true);
-            hipExtLaunchKernelGGL((k_kmer_lds<3, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)),
-                                  dim3(kLdsBlock), 0, s, prof.start(), prof.stop(), 0, c->gdesc.as<GroupDesc>(), G,
-                           c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
-                           c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
-                           c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
-        }
         hipLaunchKernelGGL((k_kmer_lds<1, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)), dim3(kLdsBlock), 0, s,
                            c->gdesc.as<GroupDesc>(), G,
                            c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),

@@ -142,3 +142,69 @@ def test_pack_variant_blocks_identical(tmp_path, variant):
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     assert np.array_equal(np.load(path), ref_blocks)
+
+
+KMER_CHILD = r"""
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, {root!r})
+from rogtk_amd import device as D
+z = np.load({src!r})
+offs = torch.from_numpy(z["offsets"]).cuda()
+vals = torch.from_numpy(z["values"]).cuda()
+keys = torch.from_numpy(z["keys"]).cuda()
+out = {{}}
+for mc in (1, 3):
+    rows, go, G, calls = D.group_spectra(offs, vals, keys, 17, mc)
+    out[f"rows{{mc}}"] = rows.cpu().numpy()
+    for ci, (g0, g1, r) in enumerate(calls):
+        for name, t in r.items():
+            if isinstance(t, torch.Tensor):
+                out[f"{{mc}}_{{ci}}_{{name}}"] = t.cpu().numpy()
+np.savez({path!r}, **out)
+"""
+
+
+def _kmer_column(tmp_path):
+    """Families of a few template reads with substitutions (counts reach min_coverage in the
+    bigger ones), ragged lengths, and groups of many rows (every LDS class and the global
+    path)."""
+    rng = np.random.default_rng(11)
+    fam = rng.integers(1, 40, 6000)
+    fam[::500] = 300  # class 1 / 4 / global-path groups
+    n = int(fam.sum())
+    keys = np.repeat(np.arange(len(fam), dtype=np.int32), fam)
+    rng.shuffle(keys)
+    lens = np.where(rng.random(n) < 0.9, 150, rng.integers(20, 300, n))
+    tmpl = rng.integers(0, 4, (len(fam), 300))
+    offs = np.zeros(n + 1, np.int64)
+    offs[1:] = np.cumsum(lens)
+    vals = np.empty(int(offs[-1]), np.uint8)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    for i in range(n):
+        b = tmpl[keys[i], :lens[i]].copy()
+        m = rng.random(lens[i]) < 0.01
+        b[m] = rng.integers(0, 4, int(m.sum()))
+        vals[offs[i]:offs[i + 1]] = acgt[b]
+    src = str(tmp_path / "kcol.npz")
+    np.savez(src, offsets=offs, values=vals, keys=keys)
+    return src
+
+
+def test_kmer_insert_variant_identical(tmp_path):
+    """The class-3 LDS kernel's V = 1 insert loop (ROGTK_KMER_INSERT=1) writes the default
+    kernel's spectra bit for bit, over min_coverage 1 and 3."""
+    src = _kmer_column(tmp_path)
+    outs = []
+    for v in ("0", "1"):
+        path = str(tmp_path / f"k{v}.npz")
+        env = dict(os.environ, ROGTK_KMER_INSERT=v)
+        r = subprocess.run([sys.executable, "-c", KMER_CHILD.format(root=ROOT, src=src, path=path)], env=env,
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(dict(np.load(path)))
+    a, b = outs
+    assert sorted(a) == sorted(b)
+    for name in a:
+        assert np.array_equal(a[name], b[name]), name
