@@ -1676,7 +1676,7 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
                                                        const uint32_t* __restrict__ rblkoff,
                                                        uint32_t* __restrict__ wlab, uint64_t* __restrict__ wexc,
                                                        uint32_t* __restrict__ labelcode, uint32_t* __restrict__ ilab,
-                                                       uint2* __restrict__ wxl, int use_exc, int exc1_on,
+                                                       int xl, int use_exc, int exc1_on,
                                                        const uint32_t* __restrict__ rblksum = nullptr,
                                                        int64_t nrb_max = 0, unsigned long long* stats = nullptr,
                                                        const unsigned long long* pstats = nullptr,
@@ -1756,12 +1756,11 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
             }
         }
         wlab[w] = lab;
-        wexc[w] = exc;
         // the codes the word label does not cover (its exceptions, or all of them when
         // the word stays unlabelled) get their own label (f[i] is their root: they are
         // live); a uniform word (ur != kNone) always has a label
         uint64_t per_code = lab == kNone ? m : exc;
-        uint32_t xl[2] = {kNone, kNone};  // the first two exceptions' labels (inline forms)
+        uint32_t xls[2] = {kNone, kNone};  // the first two exceptions' labels (inline forms)
         for (int j = 0; per_code; ++j) {
             const int b = __ffsll((long long)per_code) - 1;
             per_code &= per_code - 1;
@@ -1769,11 +1768,12 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
             if ((int64_t)i >= max_distinct) continue;
             const uint32_t li = root_label(f[i], rbits, rpref, rblkoff);
             put_label((uint64_t)w * 64 + b, i, li, labelcode, ilab);
-            if (j < 2) xl[j] = li;
+            if (j < 2) xls[j] = li;
         }
-        // the inline forms' exception labels (decode_word_label): one 8-B store per such
-        // word, read only by exception rows
-        if (wxl && lab != kNone && (lab >> 31) && (lab & 0x60000000u)) wxl[w] = make_uint2(xl[0], xl[1]);
+        // the inline forms keep their exceptions' labels in the mask's place
+        // (decode_word_label), read only by exception rows
+        const bool inl = xl && lab != kNone && (lab >> 31) && (lab & 0x60000000u);
+        wexc[w] = inl ? (uint64_t)xls[0] | ((uint64_t)xls[1] << 32) : exc;
     }
 }
 
@@ -1783,8 +1783,8 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
 // cost a second (2 MB-table) load; a single exception code is named in the label.
 __device__ __forceinline__ uint32_t word_label_of(const uint32_t* __restrict__ wlab,
                                                   const uint64_t* __restrict__ wexc,
-                                                  const uint2* __restrict__ wxl, uint64_t c) {
-    return decode_word_label(wlab[c >> 6], wexc, wxl, c);
+                                                  int xl, uint64_t c) {
+    return decode_word_label(wlab[c >> 6], wexc, xl, c);
 }
 
 // MODE 0: labelcode[code]; MODE 1: flab[rank(code)] (labels by index, ilab).
@@ -1801,7 +1801,7 @@ __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ flab,
                                                    const uint4* __restrict__ RT, const uint32_t* __restrict__ wlab,
                                                    const uint64_t* __restrict__ wexc,
-                                                   const uint2* __restrict__ wxl, uint32_t* __restrict__ out) {
+                                                   int xl, uint32_t* __restrict__ out) {
     constexpr int64_t kTile = 256 * G;  // rows per wave and trip
     const int lane = threadIdx.x & 63;
     const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
@@ -1829,7 +1829,7 @@ __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ 
             for (int k = 0; k < 4; ++k) {
                 id[g][k] = 0xFFFFFFFFu;
                 if ((reg[g] >> k) & 1u) {
-                    const uint32_t wl = wlab ? word_label_of(wlab, wexc, wxl, c[g][k]) : kNone;
+                    const uint32_t wl = wlab ? word_label_of(wlab, wexc, xl, c[g][k]) : kNone;
                     id[g][k] = wl != kNone ? wl
                                : MODE == 0 ? labelcode[c[g][k]]
                                            : flab[rt_rank(RT[c[g][k] >> 6], c[g][k])];
@@ -1856,14 +1856,14 @@ __global__ __launch_bounds__(kBlock) void k_lookup(const uint64_t* __restrict__ 
                                                    const uint32_t* __restrict__ flab, const uint4* __restrict__ RT,
                                                    const uint32_t* __restrict__ wlab,
                                                    const uint64_t* __restrict__ wexc,
-                                                   const uint2* __restrict__ wxl, uint32_t* __restrict__ out) {
+                                                   int xl, uint32_t* __restrict__ out) {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nq; i += (int64_t)gridDim.x * kBlock) {
         const uint64_t c = q[i];
         uint32_t lab = kNone;
         if (c < nbits) {
             const uint4 e = RT[c >> 6];
             if ((rt_word(e) >> (c & 63)) & 1ull) {
-                const uint32_t wl = wlab ? word_label_of(wlab, wexc, wxl, c) : kNone;
+                const uint32_t wl = wlab ? word_label_of(wlab, wexc, xl, c) : kNone;
                 lab = wl != kNone ? wl : MODE == 0 ? labelcode[c] : flab[rt_rank(e, (uint32_t)c)];
             }
         }
@@ -1887,7 +1887,6 @@ struct WsPtrs {
     uint32_t *wpref, *blksum, *blkoff, *D, *f, *UR;
     uint64_t *rbits, *lroot;
     uint32_t *rpref, *rblksum, *rblkoff, *labelcode, *ilab;
-    uint2* wxl;
     uint64_t* active;
     unsigned long long* epoch;  // resolves published (k_roots_scan)
     uint64_t* lb;               // look-back flags of k_scan_rt (+ its error word)
@@ -1913,7 +1912,6 @@ inline WsPtrs ws_ptrs(const ClusterLayout& cl, uint8_t* ws) {
     p.rpref = (uint32_t*)(ws + cl.off_rpref);
     p.rblksum = (uint32_t*)(ws + cl.off_rblksum);
     p.rblkoff = (uint32_t*)(ws + cl.off_rblkoff);
-    p.wxl = (uint2*)(ws + cl.off_wxl);
     p.labelcode = cl.label_by_code ? (uint32_t*)(ws + cl.off_labelcode) : nullptr;
     p.ilab = cl.label_by_code ? nullptr : (uint32_t*)(ws + cl.off_ilab);
     p.active = (uint64_t*)(ws + cl.off_active);
@@ -1980,7 +1978,6 @@ int cluster_layout(int L, int64_t max_distinct, ClusterLayout* o) {
     c.off_rpref = take(c.rwords * 4);
     c.off_rblksum = take(c.rblocks * 4);
     c.off_rblkoff = take((c.rblocks + 1) * 4);
-    c.off_wxl = take(c.words * 8);  // the inline forms' exception labels (k_word_label)
     c.off_labelcode = c.label_by_code ? take((int64_t)c.nbits * 4) : off;
     c.off_ilab = c.label_by_code ? off : take(max_distinct * 4);
     // hook-round frontier: one bit per (position, word group) task, two generations
@@ -2204,6 +2201,15 @@ int enqueue_post_rounds(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
     return ROGTK_OK;
 }
 
+// ROGTK_WXL=0: the inline word-label forms' exception rows read the per-code table (A/B)
+static int xl_inline_enabled() {
+    static const int v = [] {
+        const char* e = getenv("ROGTK_WXL");
+        return e && atoi(e) == 0 ? 0 : 1;
+    }();
+    return v;
+}
+
 // ROGTK_FOLD_ROOT_SCAN=0: the roots scan's block offsets by a k_scan_blocks launch (A/B)
 bool fold_root_scan_enabled() {
     static const bool on = [] {
@@ -2254,7 +2260,7 @@ int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
         }();
         hipLaunchKernelGGL(k_word_label, dim3(grid_for(cl.words, kPersistentGrid)), dim3(kBlock),
                            lds_off ? (size_t)(cl.rblocks + 1) * 4 : 0, s, p.f, p.UR, cl.words, p.RT, cl.max_distinct,
-                           p.rbits, p.rpref, p.rblkoff, p.wpref, p.G, p.labelcode, p.ilab, p.wxl, use_exc, exc1_on,
+                           p.rbits, p.rpref, p.rblkoff, p.wpref, p.G, p.labelcode, p.ilab, xl_inline_enabled(), use_exc, exc1_on,
                            lds_off ? p.rblksum : nullptr, (int64_t)cl.rblocks, lds_off ? p.stats : nullptr,
                            (const unsigned long long*)p.stats, check_round >= 0 ? host_stats : nullptr, p.epoch);
         ROGTK_HIP_CHECK(hipGetLastError());
@@ -2642,7 +2648,7 @@ int cluster_assign_prepare(const ClusterLayout& cl, const uint8_t* ws, const uin
                            bool deferred, AssignIn* a) {
     a->wlab = nullptr;
     a->wexc = nullptr;
-    a->wxl = nullptr;
+    a->xl = 0;
     a->labelcode = nullptr;
     a->out = nullptr;
     if (!deferred)
@@ -2667,7 +2673,7 @@ int cluster_assign_prepare(const ClusterLayout& cl, const uint8_t* ws, const uin
     WsPtrs p = ws_ptrs(cl, const_cast<uint8_t*>(ws));
     a->wlab = p.wpref;
     a->wexc = p.G;
-    a->wxl = p.wxl;
+    a->xl = xl_inline_enabled();
     a->labelcode = p.labelcode;
     a->out = cluster_id;
     return ROGTK_OK;
@@ -2689,10 +2695,10 @@ int launch_cluster_lookup(const ClusterLayout& cl, const uint8_t* ws, const uint
     const int g = grid_for(nq, 4096);
     if (cl.label_by_code)
         hipLaunchKernelGGL(k_lookup<0>, dim3(g), dim3(kBlock), 0, s, q, nq, cl.nbits, p.labelcode, p.D, p.RT, wlab,
-                           wexc, wlab ? p.wxl : nullptr, lab);
+                           wexc, wlab ? xl_inline_enabled() : 0, lab);
     else
         hipLaunchKernelGGL(k_lookup<1>, dim3(g), dim3(kBlock), 0, s, q, nq, cl.nbits, p.labelcode, p.ilab, p.RT, wlab,
-                           wexc, wlab ? p.wxl : nullptr, lab);
+                           wexc, wlab ? xl_inline_enabled() : 0, lab);
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
 }
@@ -2728,7 +2734,7 @@ int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, bool word_labels, c
 #define ROGTK_ASSIGN_LAUNCH(M, G)                                                                                 \
     hipExtLaunchKernelGGL((k_assign<M, G>), dim3(g), dim3(kBlock), 0, s, prof.start(), prof.stop(), 0, codes,    \
                           regular_bits, n, p.labelcode,                                                       \
-                       M == 0 ? p.D : p.ilab, p.RT, wlab, wexc, wlab ? p.wxl : nullptr, cluster_id)
+                       M == 0 ? p.D : p.ilab, p.RT, wlab, wexc, wlab ? xl_inline_enabled() : 0, cluster_id)
     if (cl.label_by_code) {
         if (groups == 1) ROGTK_ASSIGN_LAUNCH(0, 1);
         else if (groups == 4) ROGTK_ASSIGN_LAUNCH(0, 4);

@@ -141,26 +141,28 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 //                       codes, whose bits are bits 17..22 and 23..28 (no mask load);
 //   bit 31 set, 30, 29 clear: the label (bits 0..28) of the codes outside the word's
 //                       exception mask wexc[word].
-// The labels of the one or two exception codes of the inline forms are wxl[word].x / .y
-// (8 B per word, round 4): an exception row then reads an L2-resident line instead of a
-// line of the 4^L-entry per-code table (64 MB at L = 12, which no L2 holds: one DRAM
-// round trip per exception row stalled the whole wave trip).
+// xl (round 4): the inline forms need no mask, so their wexc[word] holds the labels of
+// their one or two exception codes instead (low / high 32 bits): an exception row then
+// reads a line of the 2 MB word table (L2-resident beside the 1 MB label table) instead
+// of a line of the 4^L-entry per-code table (64 MB at L = 12: one DRAM round trip per
+// exception row stalled its whole wave trip). A separate 2 MB label array measured
+// slower (k_assign 100 -> 125-130 us): the three word tables no longer fit one XCD's L2.
 // Returns the code's label, or 0xFFFFFFFF when the code is labelled per code
-// (wxl == nullptr: the inline forms' exceptions too).
-__device__ __forceinline__ uint32_t decode_word_label(uint32_t wl, const uint64_t* __restrict__ wexc,
-                                                      const uint2* __restrict__ wxl, uint64_t c) {
+// (xl == 0: the inline forms' exceptions too).
+__device__ __forceinline__ uint32_t decode_word_label(uint32_t wl, const uint64_t* __restrict__ wexc, int xl,
+                                                      uint64_t c) {
     if (wl == 0xFFFFFFFFu || !(wl >> 31)) return wl;
     const uint32_t b = (uint32_t)(c & 63);
     if ((wl >> 30) & 1u) {
         if (b != ((wl >> 24) & 63u)) return wl & 0xFFFFFFu;
-        return wxl ? wxl[c >> 6].x : 0xFFFFFFFFu;
+        return xl ? (uint32_t)wexc[c >> 6] : 0xFFFFFFFFu;
     }
     if ((wl >> 29) & 1u) {
         const bool e0 = b == ((wl >> 17) & 63u), e1 = b == ((wl >> 23) & 63u);
         if (!e0 && !e1) return wl & 0x1FFFFu;
-        if (!wxl) return 0xFFFFFFFFu;
-        const uint2 x = wxl[c >> 6];
-        return e0 ? x.x : x.y;
+        if (!xl) return 0xFFFFFFFFu;
+        const uint64_t x = wexc[c >> 6];
+        return e0 ? (uint32_t)x : (uint32_t)(x >> 32);
     }
     return ((wexc[c >> 6] >> b) & 1ull) ? 0xFFFFFFFFu : (wl & 0x1FFFFFFFu);
 }
@@ -220,7 +222,7 @@ int build_packed_params(int L, PackedParams* p);
 struct AssignIn {
     const uint32_t* wlab;
     const uint64_t* wexc;
-    const uint2* wxl;
+    int xl;  // inline exception labels in wexc (decode_word_label)
     const uint32_t* labelcode;
     uint32_t* out;  // nullptr: no assign in the score pass
 };
@@ -254,7 +256,7 @@ struct ClusterLayout {
     bool label_by_code;  // dense label table indexed by code (L <= 13)
     // byte offsets into the workspace
     int64_t off_stats, off_presence, off_bitmap, off_rt, off_wpref, off_blksum, off_blkoff, off_D, off_f, off_ur,
-        off_rbits, off_lroot, off_rpref, off_rblksum, off_rblkoff, off_wxl, off_labelcode, off_ilab, off_active,
+        off_rbits, off_lroot, off_rpref, off_rblksum, off_rblkoff, off_labelcode, off_ilab, off_active,
         active_words, off_edges, ecap, off_epoch, off_lb, total;
 };
 int cluster_layout(int L, int64_t max_distinct, ClusterLayout* out);

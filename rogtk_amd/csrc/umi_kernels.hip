@@ -295,7 +295,7 @@ __device__ __forceinline__ void score_tile(const int64_t tile, const uint32_t* _
             if (ASG) {
                 // word labels (decode_word_label, rogtk_internal.h)
 #pragma unroll
-                for (int k = 0; k < kRowsPerLane; ++k) wl[k] = decode_word_label(wl[k], A.wexc, A.wxl, c[k]);
+                for (int k = 0; k < kRowsPerLane; ++k) wl[k] = decode_word_label(wl[k], A.wexc, A.xl, c[k]);
                 uint32_t id[kRowsPerLane];
 #pragma unroll
                 for (int k = 0; k < kRowsPerLane; ++k)
@@ -361,7 +361,7 @@ __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restr
 
 // The label of one present regular code from the resolved tables (MODE 0: per-code table).
 __device__ __forceinline__ uint32_t code_label(const AssignIn& A, uint32_t c) {
-    const uint32_t wl = decode_word_label(A.wlab[c >> 6], A.wexc, A.wxl, c);
+    const uint32_t wl = decode_word_label(A.wlab[c >> 6], A.wexc, A.xl, c);
     return wl != 0xFFFFFFFFu ? wl : A.labelcode[c];
 }
 
@@ -419,7 +419,7 @@ __global__ __launch_bounds__(kBlock) void k_score_assign_prev(const uint32_t* __
     const int64_t t = b < both ? (b >> 1) : (b - both) + (ts > ta ? ta : ts);
     if (is_score) {
         if (SCORE) stage_tables(P, s_tab);
-        const AssignIn none{nullptr, nullptr, nullptr, nullptr, nullptr};
+        const AssignIn none{nullptr, nullptr, 0, nullptr, nullptr};
         score_tile<SCORE, HAMD, HAMW, false, LT, false>(t, codes, regbits, n, P, O, hd, hw, nullptr, none, s_tab);
     } else {
         assign_tile(t, codes2, regbits2, n2, A2);
@@ -646,7 +646,7 @@ int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int
                         const PackedParams& p, const ScoreOut& o, uint32_t* hd, uint64_t* hw,
                         uint8_t* presence, hipStream_t s, const AssignIn* asg) {
     if (n <= 0) return ROGTK_OK;
-    const AssignIn A = asg ? *asg : AssignIn{nullptr, nullptr, nullptr, nullptr};
+    const AssignIn A = asg ? *asg : AssignIn{nullptr, nullptr, 0, nullptr};
     const bool fused = A.out != nullptr;
     const bool score = any_score(o), hamd = p.ham_mode && hd, hamw = p.ham_mode && hw,
                mark = presence != nullptr;
