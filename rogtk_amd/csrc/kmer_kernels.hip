@@ -659,11 +659,12 @@ struct LdsCfg {
 };
 constexpr unsigned long long kEmpty = ~0ull;
 
-// ROGTK_KMER_INSERT=1: the class-3 LDS kernel's V = 1 insert loop (round-4 A/B; read once)
+// ROGTK_KMER_INSERT=1 / 2: the class-3 LDS kernel's V = 1 / 2 insert loop (round-4 A/B; read once)
 inline int kmer_insert_v() {
     static const int v = [] {
         const char* e = getenv("ROGTK_KMER_INSERT");
-        return e && atoi(e) == 1 ? 1 : 0;
+        const int x = e ? atoi(e) : 0;
+        return x == 1 || x == 2 ? x : 0;
     }();
     return v;
 }
@@ -689,7 +690,11 @@ struct GroupDesc {
 // V = 1 (round 4, ROGTK_KMER_INSERT=1 while it is A/B'd): the insert loop issues its LDS
 // reads together (the overflow flag and the previous, current and next packed word, one
 // wait for all), takes the left extension base from the previous word without a divergent
-// branch, and hashes the 64-bit key with one 32-bit multiply instead of a 64-bit one
+// branch, and hashes the 64-bit key with one 32-bit multiply instead of a 64-bit one.
+// V = 2: V = 1's loop plus wave-private claimed lists: each wave appends its newly claimed
+// slots to its own segment of the list at an index it counts itself (ballot + mbcnt, no
+// LDS atomic and no round trip per trip), and resets its own segment afterwards; a wave
+// past its segment (kClaim / waves entries) takes the overflow exit like the shared cap
 template <int CLS, int TB, int V = 0>
 __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDesc* __restrict__ gdesc, int64_t G,
                                                      uint8_t* __restrict__ gsmall, int K, int64_t min_cov,
@@ -717,6 +722,8 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
     uint64_t* const vkey = ubuf;                                       // after the inserts
     uint32_t* const vinfo = reinterpret_cast<uint32_t*>(ubuf + kLdsObs);  // count | exts << 16 | pad << 31
     __shared__ uint32_t scan[kWaves];
+    __shared__ uint32_t s_wcnt[kWaves];  // V = 2: the waves' claimed counts
+    constexpr uint32_t kCapW = C::kClaim / kWaves;
     __shared__ uint32_t s_claimed, s_term, s_iso, s_over, s_hit;
     // s_hit: some k-mer's count reached min_cov during the inserts (counts grow by one per
     // insert, so one insert sees exactly min_cov). Without it nothing is valid and the
@@ -809,77 +816,179 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
         // Work unit = (row, half): half h takes the row's positions 64 h + lane + 128 i, so
         // a C3 group (~10 rows of 119 observations) deals 2 units per row over the 8 waves
         // instead of whole rows (waves with two rows set the pace otherwise)
-        for (int u = wave; u < 2 * nrows; u += kWaves) {
-            const int ri = u >> 1;
-            const int nobs = m_nobs[ri];
-            if (nobs <= ((u & 1) << 6)) continue;
-            const int len = m_len[ri];
-            const uint64_t* rw = words + m_w[ri];
-            for (int p = lane + ((u & 1) << 6); p < nobs; p += 128) {
-                const int b = 2 * (p & 31);
-                uint32_t over = 0;
-                uint64_t x0, x1, xm = 0;
-                if constexpr (V == 1) {
-                    if (kBounded) over = __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if constexpr (V == 2) {
+            // trips are wave-uniform (a unit's row and half are), so the claim count stays
+            // uniform: lanes past the row's end ride along inactive
+            uint32_t wcnt = 0;
+            bool whit = false, stop = false;
+            for (int u = wave; u < 2 * nrows && !stop; u += kWaves) {
+                const int ri = u >> 1;
+                const int nobs = m_nobs[ri];
+                const int h0 = (u & 1) << 6;
+                if (nobs <= h0) continue;
+                const int len = m_len[ri];
+                const uint64_t* rw = words + m_w[ri];
+                const int trips = (nobs - h0 + 127) >> 7;
+                for (int it = 0; it < trips; ++it) {
+                    const int p0 = lane + h0 + (it << 7);
+                    const bool act = p0 < nobs;
+                    const int p = act ? p0 : 0;
+                    const int b = 2 * (p & 31);
                     const int wi = p >> 5;
-                    x0 = rw[wi];
-                    x1 = rw[wi + 1];
-                    xm = rw[wi > 0 ? wi - 1 : 0];  // p == 0 (no left base) reads word 0 unused
-                } else {
-                    x0 = rw[p >> 5];
-                    x1 = rw[(p >> 5) + 1];
-                }
-                const uint64_t top = b ? (x0 << b) | (x1 >> (64 - b)) : x0;
-                const uint64_t key = (top >> (64 - 2 * K)) & kmask;
-                // extension bases from the two words already loaded (k_eff <= 32: base p + K
-                // lies in x0 or x1); only a k-mer starting a word loads its left base
-                uint32_t e = 0;
-                if constexpr (V == 1) {
+                    uint32_t over = __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    const uint64_t x0 = rw[wi], x1 = rw[wi + 1], xm = rw[wi > 0 ? wi - 1 : 0];
+                    const uint64_t top = b ? (x0 << b) | (x1 >> (64 - b)) : x0;
+                    const uint64_t key = (top >> (64 - 2 * K)) & kmask;
                     const uint32_t lb = b ? (uint32_t)(x0 >> (64 - b)) : (uint32_t)xm;
-                    e = p > 0 ? 1u << (lb & 3u) : 0u;
+                    uint32_t e = p > 0 ? 1u << (lb & 3u) : 0u;
                     const int t = (p & 31) + K;
                     const uint32_t rb = (uint32_t)((t < 32 ? x0 : x1) >> (62 - 2 * (t & 31))) & 3u;
                     e |= p + K < len ? 1u << (4 + rb) : 0u;
-                    // the flag's branch stays behind the word reads (one LDS wait for all)
                     asm volatile("" : "+v"(over) : "v"(x0), "v"(x1), "v"(xm));
-                    if (over) break;
-                } else {
-                    if (p > 0) e |= 1u << (b ? (uint32_t)(x0 >> (64 - b)) & 3u : (uint32_t)rw[(p >> 5) - 1] & 3u);
-                    if (p + K < len) {
-                        const int t = (p & 31) + K;
-                        e |= 1u << (4 + ((uint32_t)((t < 32 ? x0 : x1) >> (62 - 2 * (t & 31))) & 3u));
+                    if (over) {  // one LDS read for the wave: the same value in every lane
+                        stop = true;
+                        break;
                     }
-                    if (kBounded && __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+                    uint32_t slot = 0, cnt0 = 1;
+                    if (act) {
+                        if (key == kEmpty) {
+                            slot = kLdsSlots;
+                        } else {
+                            const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
+                            slot = ((lo ^ __builtin_amdgcn_alignbit(hi, hi, 16)) * 0x9E3779B1u) >> (32 - hbits);
+                            while (true) {
+                                const unsigned long long prev = atomicCAS(&tkey[slot], kEmpty, (unsigned long long)key);
+                                if (prev == kEmpty || prev == key) break;
+                                slot = (slot + 1) & (kLdsSlots - 1);
+                            }
+                        }
+                        cnt0 = atomicAdd(&tinfo[slot], 1u) & 0xFFFFFFu;
+                        if (e) atomicOr(&tinfo[slot], e << 24);
+                    }
+                    const bool first = act && cnt0 == 0;
+                    const uint64_t fb = __ballot(first);
+                    if (fb) {
+                        if (first) {
+                            const uint32_t idx = wcnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(fb >> 32),
+                                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)fb, 0u));
+                            if (idx < kCapW) claimed[wave * kCapW + idx] = (uint16_t)slot;
+                            else s_over = 1;  // this wave's segment is full
+                        }
+                        wcnt += (uint32_t)__popcll(fb);
+                    }
+                    whit |= __ballot(act && cnt0 + 1 == hit_at) != 0;
                 }
-                uint32_t slot;
-                if (key == kEmpty) {
-                    slot = kLdsSlots;
-                } else {
+            }
+            if (lane == 0) {
+                s_wcnt[wave] = min(wcnt, kCapW);
+                if (whit) s_hit = 1;
+            }
+        } else {
+            for (int u = wave; u < 2 * nrows; u += kWaves) {
+                const int ri = u >> 1;
+                const int nobs = m_nobs[ri];
+                if (nobs <= ((u & 1) << 6)) continue;
+                const int len = m_len[ri];
+                const uint64_t* rw = words + m_w[ri];
+                for (int p = lane + ((u & 1) << 6); p < nobs; p += 128) {
+                    const int b = 2 * (p & 31);
+                    uint32_t over = 0;
+                    uint64_t x0, x1, xm = 0;
                     if constexpr (V == 1) {
-                        const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
-                        slot = ((lo ^ __builtin_amdgcn_alignbit(hi, hi, 16)) * 0x9E3779B1u) >> (32 - hbits);
+                        if (kBounded) over = __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        const int wi = p >> 5;
+                        x0 = rw[wi];
+                        x1 = rw[wi + 1];
+                        xm = rw[wi > 0 ? wi - 1 : 0];  // p == 0 (no left base) reads word 0 unused
                     } else {
-                        slot = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - hbits));
+                        x0 = rw[p >> 5];
+                        x1 = rw[(p >> 5) + 1];
                     }
-                    while (true) {
-                        const unsigned long long prev = atomicCAS(&tkey[slot], kEmpty, (unsigned long long)key);
-                        if (prev == kEmpty || prev == key) break;
-                        slot = (slot + 1) & (kLdsSlots - 1);
+                    const uint64_t top = b ? (x0 << b) | (x1 >> (64 - b)) : x0;
+                    const uint64_t key = (top >> (64 - 2 * K)) & kmask;
+                    // extension bases from the two words already loaded (k_eff <= 32: base p + K
+                    // lies in x0 or x1); only a k-mer starting a word loads its left base
+                    uint32_t e = 0;
+                    if constexpr (V == 1) {
+                        const uint32_t lb = b ? (uint32_t)(x0 >> (64 - b)) : (uint32_t)xm;
+                        e = p > 0 ? 1u << (lb & 3u) : 0u;
+                        const int t = (p & 31) + K;
+                        const uint32_t rb = (uint32_t)((t < 32 ? x0 : x1) >> (62 - 2 * (t & 31))) & 3u;
+                        e |= p + K < len ? 1u << (4 + rb) : 0u;
+                        // the flag's branch stays behind the word reads (one LDS wait for all)
+                        asm volatile("" : "+v"(over) : "v"(x0), "v"(x1), "v"(xm));
+                        if (over) break;
+                    } else {
+                        if (p > 0) e |= 1u << (b ? (uint32_t)(x0 >> (64 - b)) & 3u : (uint32_t)rw[(p >> 5) - 1] & 3u);
+                        if (p + K < len) {
+                            const int t = (p & 31) + K;
+                            e |= 1u << (4 + ((uint32_t)((t < 32 ? x0 : x1) >> (62 - 2 * (t & 31))) & 3u));
+                        }
+                        if (kBounded && __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
                     }
+                    uint32_t slot;
+                    if (key == kEmpty) {
+                        slot = kLdsSlots;
+                    } else {
+                        if constexpr (V == 1) {
+                            const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
+                            slot = ((lo ^ __builtin_amdgcn_alignbit(hi, hi, 16)) * 0x9E3779B1u) >> (32 - hbits);
+                        } else {
+                            slot = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - hbits));
+                        }
+                        while (true) {
+                            const unsigned long long prev = atomicCAS(&tkey[slot], kEmpty, (unsigned long long)key);
+                            if (prev == kEmpty || prev == key) break;
+                            slot = (slot + 1) & (kLdsSlots - 1);
+                        }
+                    }
+                    const uint32_t cnt0 = atomicAdd(&tinfo[slot], 1u) & 0xFFFFFFu;
+                    if (cnt0 == 0) {
+                        const uint32_t ci = atomicAdd(&s_claimed, 1u);
+                        if (!kBounded || ci < (uint32_t)C::kClaim) claimed[ci] = (uint16_t)slot;
+                        else s_over = 1;  // more distinct k-mers than the table takes
+                    }
+                    if (cnt0 + 1 == hit_at) s_hit = 1;
+                    if (e) atomicOr(&tinfo[slot], e << 24);
                 }
-                const uint32_t cnt0 = atomicAdd(&tinfo[slot], 1u) & 0xFFFFFFu;
-                if (cnt0 == 0) {
-                    const uint32_t ci = atomicAdd(&s_claimed, 1u);
-                    if (!kBounded || ci < (uint32_t)C::kClaim) claimed[ci] = (uint16_t)slot;
-                    else s_over = 1;  // more distinct k-mers than the table takes
-                }
-                if (cnt0 + 1 == hit_at) s_hit = 1;
-                if (e) atomicOr(&tinfo[slot], e << 24);
             }
         }
         __syncthreads();
         KT(2);
-        const uint32_t ncl = s_claimed;
+        uint32_t ncl = 0;
+        if constexpr (V == 2) {
+#pragma unroll
+            for (int w2 = 0; w2 < kWaves; ++w2) ncl += s_wcnt[w2];
+        } else {
+            ncl = s_claimed;
+        }
+        // entry i of the claimed list (V = 2: the waves' segments in wave order)
+        auto cl_at = [&](uint32_t i) -> uint32_t {
+            if constexpr (V == 2) {
+                int w2 = 0;
+                for (uint32_t nw; i >= (nw = s_wcnt[w2]); ++w2) i -= nw;
+                return claimed[w2 * kCapW + i];
+            } else {
+                return claimed[i];
+            }
+        };
+        // reset the touched slots (V = 2: each wave its own segment)
+        auto reset_claimed = [&]() {
+            if constexpr (V == 2) {
+                const uint32_t nmine = s_wcnt[wave];
+                for (uint32_t j = lane; j < nmine; j += 64) {
+                    const uint32_t sl = claimed[wave * kCapW + j];
+                    tkey[sl] = kEmpty;
+                    tinfo[sl] = 0;
+                }
+            } else {
+                for (uint32_t i = tid; i < ncl; i += TB) {
+                    const uint32_t sl = claimed[i];
+                    tkey[sl] = kEmpty;
+                    tinfo[sl] = 0;
+                }
+            }
+        };
         const bool hit = s_hit;
         if (kBounded) {
             const bool over = s_over;
@@ -903,11 +1012,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
         if (!hit) {
             // no count reached min_cov: nothing passes CountFilter (as nv == 0 below,
             // without the count pass): reset the touched slots, record the empty group
-            for (uint32_t i = tid; i < ncl; i += TB) {
-                const uint32_t sl = claimed[i];
-                tkey[sl] = kEmpty;
-                tinfo[sl] = 0;
-            }
+            reset_claimed();
             if (tid == 0) {
                 gcount[g] = 0;
                 gstat[5 * g + 3] = 0;
@@ -922,7 +1027,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
         const uint32_t c0 = min(ncl, tid * per), c1 = min(ncl, c0 + per);
         uint32_t mine = 0;
         for (uint32_t i = c0; i < c1; ++i) {
-            const uint32_t c = tinfo[claimed[i]] & 0xFFFFFFu;
+            const uint32_t c = tinfo[cl_at(i)] & 0xFFFFFFu;
             if ((int64_t)min(c, 0xFFFFu) >= min_cov) ++mine;
         }
         uint32_t incl = 0;
@@ -947,11 +1052,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
             // nothing passed CountFilter: reset the touched slots and record the empty
             // group, no compaction, sort or further barrier (the next group's first
             // barrier orders these resets before its inserts)
-            for (uint32_t i = tid; i < ncl; i += TB) {
-                const uint32_t sl = claimed[i];
-                tkey[sl] = kEmpty;
-                tinfo[sl] = 0;
-            }
+            reset_claimed();
             if (tid == 0) {
                 gcount[g] = 0;
                 gstat[5 * g + 3] = 0;
@@ -963,11 +1064,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
         }
         if (nv > (uint32_t)kLdsObs) {
             // more valid k-mers than the sort buffer takes: the next class or the global path
-            for (uint32_t i = tid; i < ncl; i += TB) {
-                const uint32_t sl = claimed[i];
-                tkey[sl] = kEmpty;
-                tinfo[sl] = 0;
-            }
+            reset_claimed();
             if (tid == 0) {
                 gsmall[g] = CLS == 3 ? 1 : CLS == 1 ? 4 : 0;
                 s_claimed = 0;
@@ -976,7 +1073,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
         }
         uint32_t w = wbase + incl - mine;
         for (uint32_t i = c0; i < c1; ++i) {
-            const uint32_t sl = claimed[i];
+            const uint32_t sl = cl_at(i);
             const uint32_t info = tinfo[sl];
             const uint32_t c = info & 0xFFFFFFu;
             if ((int64_t)min(c, 0xFFFFu) >= min_cov) {
@@ -988,11 +1085,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
         __syncthreads();
         KT(4);
         // reset the touched slots for the next group (the table is not read again here)
-        for (uint32_t i = tid; i < ncl; i += TB) {
-            const uint32_t sl = claimed[i];
-            tkey[sl] = kEmpty;
-            tinfo[sl] = 0;
-        }
+        reset_claimed();
         const int64_t base = cap_off[g];
         if (nv <= 64) {
             // small valid set: wave 0 sorts it in registers (bitonic over shuffles),
@@ -1468,7 +1561,14 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
         hipLaunchKernelGGL(k_tail_sum, dim3(1), dim3(64), 0, s, co, in.cap_fill, G, co + G);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
-    if (lds && kmer_insert_v() == 1) {
+    if (lds && kmer_insert_v() == 2) {
+        ProfScope prof(K_KMER_LDS, s, true);
+        hipExtLaunchKernelGGL((k_kmer_lds<3, kLdsBlock, 2>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)),
+                              dim3(kLdsBlock), 0, s, prof.start(), prof.stop(), 0, c->gdesc.as<GroupDesc>(), G,
+                              c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
+                              c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
+                              c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
+    } else if (lds && kmer_insert_v() == 1) {
         ProfScope prof(K_KMER_LDS, s, true);
         hipExtLaunchKernelGGL((k_kmer_lds<3, kLdsBlock, 1>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)),
                               dim3(kLdsBlock), 0, s, prof.start(), prof.stop(), 0, c->gdesc.as<GroupDesc>(), G,

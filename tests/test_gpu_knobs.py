@@ -198,18 +198,19 @@ def _kmer_column(tmp_path):
 
 
 def test_kmer_insert_variant_identical(tmp_path):
-    """The class-3 LDS kernel's V = 1 insert loop (ROGTK_KMER_INSERT=1) writes the default
-    kernel's spectra bit for bit, over min_coverage 1 and 3."""
+    """The class-3 LDS kernel's V = 1 and V = 2 insert loops (ROGTK_KMER_INSERT=1 / 2) write
+    the default kernel's spectra bit for bit, over min_coverage 1 and 3."""
     src = _kmer_column(tmp_path)
     outs = []
-    for v in ("0", "1"):
+    for v in ("0", "1", "2"):
         path = str(tmp_path / f"k{v}.npz")
         env = dict(os.environ, ROGTK_KMER_INSERT=v)
         r = subprocess.run([sys.executable, "-c", KMER_CHILD.format(root=ROOT, src=src, path=path)], env=env,
                            capture_output=True, text=True, timeout=240)
         assert r.returncode == 0, r.stderr[-2000:]
         outs.append(dict(np.load(path)))
-    a, b = outs
-    assert sorted(a) == sorted(b)
-    for name in a:
-        assert np.array_equal(a[name], b[name]), name
+    a = outs[0]
+    for b in outs[1:]:
+        assert sorted(a) == sorted(b)
+        for name in a:
+            assert np.array_equal(a[name], b[name]), name
