@@ -2201,11 +2201,13 @@ int enqueue_post_rounds(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
     return ROGTK_OK;
 }
 
-// ROGTK_WXL=0: the inline word-label forms' exception rows read the per-code table (A/B)
+// ROGTK_WXL=1: the inline word-label forms keep their exception labels in the mask slot
+// (decode_word_label). Measured slower, so off by default: k_assign 125-128 us against
+// 100-101 with the per-code table (round 4, 10M rows, interleaved A/B)
 static int xl_inline_enabled() {
     static const int v = [] {
         const char* e = getenv("ROGTK_WXL");
-        return e && atoi(e) == 0 ? 0 : 1;
+        return e && atoi(e) == 1 ? 1 : 0;
     }();
     return v;
 }

@@ -145,8 +145,9 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 // their one or two exception codes instead (low / high 32 bits): an exception row then
 // reads a line of the 2 MB word table (L2-resident beside the 1 MB label table) instead
 // of a line of the 4^L-entry per-code table (64 MB at L = 12: one DRAM round trip per
-// exception row stalled its whole wave trip). A separate 2 MB label array measured
-// slower (k_assign 100 -> 125-130 us): the three word tables no longer fit one XCD's L2.
+// exception row stalled its whole wave trip). Measured slower, in both forms (this one
+// and a separate 2 MB label array): k_assign 100 -> 125-130 us, so off by default
+// (ROGTK_WXL=1 turns it on).
 // Returns the code's label, or 0xFFFFFFFF when the code is labelled per code
 // (xl == 0: the inline forms' exceptions too).
 __device__ __forceinline__ uint32_t decode_word_label(uint32_t wl, const uint64_t* __restrict__ wexc, int xl,

@@ -64,8 +64,8 @@ KNOBS = [
     ({"ROGTK_FUSED_SCAN": "0", "ROGTK_LOCAL8": "0"}, "separate"),
     ({"ROGTK_LOCAL8_SINGLE": "1"}, "main"),
     ({"ROGTK_WORD_EXC1": "0"}, "main"),
-    ({"ROGTK_WXL": "0"}, "main"),
-    ({"ROGTK_WXL": "0", "ROGTK_WORD_EXC1": "0"}, "separate"),
+    ({"ROGTK_WXL": "1"}, "main"),
+    ({"ROGTK_WXL": "1", "ROGTK_WORD_EXC1": "0"}, "separate"),
     ({"ROGTK_FUSED_CHECK": "0"}, "main"),
     ({"ROGTK_FOLD_ROOT_SCAN": "0"}, "main"),
     ({"ROGTK_LCC_PREDICT": "0"}, "separate"),
