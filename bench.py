@@ -569,7 +569,7 @@ def main():
         torch.cuda.synchronize()
         D.profile_enable(False)
         for k in ("score_packed", "cluster_mark", "cluster_bitmap", "cluster_scan", "cluster_compact", "cluster_union",
-                  "cluster_flatten", "cluster_label", "cluster_assign"):
+                  "cluster_flatten", "cluster_label", "cluster_assign", "cluster_resolve"):
             ms, launches = D.profile_read(k)
             if launches:
                 breakdown[k] = round(1000.0 * ms / launches, 2)

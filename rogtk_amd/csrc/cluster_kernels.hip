@@ -2429,6 +2429,7 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
         st.deferred.on = false;
         return ROGTK_OK;
     }
+    ProfScope prof_chain(K_RESOLVE, s);
     st.pending = false;
     st.deferred.on = false;
     st.rounds = 0;
