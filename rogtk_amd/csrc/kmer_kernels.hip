@@ -206,6 +206,54 @@ __device__ __forceinline__ uint32_t pack4(uint32_t x, uint32_t& notacgt) {
     return ((c & 0xFFu) << 6) | (((c >> 8) & 0xFFu) << 4) | (((c >> 16) & 0xFFu) << 2) | (c >> 24);
 }
 
+// Round 4: the repeat certificate of a row (block meta bit 33, set = certified). If no
+// 16-mer at an aligned position 16 j (16 j + 16 <= len) occurs again at any other position
+// of the row, no K-mer with K >= 31 occurs twice in it: an occurrence [p, p + K) holds the
+// whole aligned 16-mer [a, a + 16) for the multiple a of 16 in [p, p + K - 16] (K - 15 >= 16
+// consecutive integers), and a second occurrence at p + d holds it again at a + d != a.
+// A group whose rows are all certified and that has fewer than min_cov rows with
+// observations then has no k-mer counted min_cov times: nothing passes CountFilter, and
+// k_group_classify takes it off the LDS kernels (class kClsEmpty). Necessary-condition
+// check only: a pair found (even across the row's end padding) just withholds the bit.
+// One lane per row over its NW packed words; compares 16-mers as u32 (alignbit).
+template <int NW>
+__device__ __forceinline__ bool may_repeat16(const uint64_t (&wd)[NW], int len) {
+    constexpr int NA = (32 * NW - 16) / 16 + 1;  // aligned 16-mers the words can hold
+    uint32_t a[NA];
+    bool va[NA];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+        a[j] = (j & 1) ? (uint32_t)wd[j >> 1] : (uint32_t)(wd[j >> 1] >> 32);
+        va[j] = 16 * j + 16 <= len;
+    }
+    bool rep = false;
+#pragma unroll
+    for (int wi = 0; wi < NW; ++wi) {
+        if (!__ballot(32 * wi + 16 <= len)) break;  // no lane has a 16-mer starting in this word
+        const uint32_t h0 = (uint32_t)(wd[wi] >> 32), h1 = (uint32_t)wd[wi];
+        const uint32_t h2 = wi + 1 < NW ? (uint32_t)(wd[wi + 1] >> 32) : 0u;
+#pragma unroll
+        for (int t0 = 0; t0 < 32; t0 += 8) {  // 8 positions at a time (few live registers)
+            if (!__ballot(32 * wi + t0 + 16 <= len)) break;
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int t = t0 + u;
+                v[u] = t == 0 ? h0 : t == 16 ? h1 : t < 16 ? __builtin_amdgcn_alignbit(h0, h1, 32 - 2 * t)
+                                                          : __builtin_amdgcn_alignbit(h1, h2, 64 - 2 * t);
+            }
+#pragma unroll
+            for (int j = 0; j < NA; ++j) {
+                if (!__ballot(va[j])) break;  // aligned positions are valid in order
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (32 * wi + t0 + u != 16 * j) rep |= va[j] && v[u] == a[j];
+            }
+        }
+    }
+    return rep;
+}
+
 // R rows per workgroup, a lane per row (R threads). DIRECT: each lane stores its row's
 // block itself (16-B stores; the lanes' blocks are consecutive, so a wave covers
 // 64 * 8 * B contiguous bytes and L2 merges the lines) instead of staging the blocks in
@@ -287,6 +335,7 @@ __global__ __launch_bounds__(R) void k_pack_reads(const int64_t* __restrict__ of
             // DIRECT: 16-B stores of word pairs (2k, 2k+1); word 1 waits for the meta word
             uint64_t w1 = 0, pend = 0;
             uint64_t* const ob = DIRECT ? blocks + r * B : out + tid * OS;
+            uint64_t wd[B == 8 ? B - 1 : 1];  // B = 8: the row's words, for the repeat certificate
 #pragma unroll 1
             for (int w = 0; w < B - 1; ++w) {
                 uint64_t acc = 0;
@@ -313,6 +362,17 @@ __global__ __launch_bounds__(R) void k_pack_reads(const int64_t* __restrict__ of
                         bad |= nb;
                     }
                 }
+                if constexpr (B == 8) {
+                    switch (w) {  // static register indices in a rolled loop (w is uniform)
+                        case 0: wd[0] = acc; break;
+                        case 1: wd[1] = acc; break;
+                        case 2: wd[2] = acc; break;
+                        case 3: wd[3] = acc; break;
+                        case 4: wd[4] = acc; break;
+                        case 5: wd[5] = acc; break;
+                        default: wd[6] = acc; break;
+                    }
+                }
                 if (!DIRECT) {
                     ob[1 + w] = acc;
                 } else if (w == 0) {
@@ -323,7 +383,12 @@ __global__ __launch_bounds__(R) void k_pack_reads(const int64_t* __restrict__ of
                     *reinterpret_cast<ulonglong2*>(ob + w) = make_ulonglong2(pend, acc);
                 }
             }
-            const uint64_t meta = valid ? ((uint64_t)(uint32_t)len | ((uint64_t)(bad == 0) << 32)) : 0xFFFFFFFFull;
+            // bit 33: the repeat certificate (B = 8 only: rows of at most 224 bases)
+            bool norep = false;
+            if constexpr (B == 8) norep = valid && bad == 0 && !may_repeat16(wd, len);
+            const uint64_t meta = valid ? ((uint64_t)(uint32_t)len | ((uint64_t)(bad == 0) << 32) |
+                                           ((uint64_t)norep << 33))
+                                        : 0xFFFFFFFFull;
             if (DIRECT)
                 *reinterpret_cast<ulonglong2*>(ob) = make_ulonglong2(meta, w1);
             else
@@ -369,7 +434,7 @@ __global__ __launch_bounds__(kBlock) void k_row_gather(const uint64_t* __restric
             const int64_t pr = __shfl(my_pr, q);
             v[j] = rb + q < n_rows ? blocks[pr * B + w] : 0xFFFFFFFFull;
         }
-        uint64_t okbits = 0;
+        uint64_t okbits = 0, unc = 0;
 #pragma unroll
         for (int j = 0; j < B; ++j) {
             const int q = j * RPI + sub;
@@ -378,18 +443,23 @@ __global__ __launch_bounds__(kBlock) void k_row_gather(const uint64_t* __restric
             const uint32_t len = (uint32_t)meta;
             const bool inK = __shfl(my_k, q) && rr < n_rows && len != 0xFFFFFFFFu;
             const bool ok = inK && ((meta >> 32) & 1ull);
+            const bool use = ok && (int64_t)len >= K;
             if (rr < n_rows && w >= 1 && w <= S) packed[rr * S + (w - 1)] = v[j];
             if (rr < n_rows && w == 0) {
                 // a row longer than S words (a max_len below the real lengths, or past the
                 // block) would read the next row's bases: counted, and the call fails
                 if (inK && (int64_t)len > 32 * (int64_t)S) atomicAdd(long_rows, 1ull);
-                const bool use = ok && (int64_t)len >= K;
                 row_obs[rr] = use ? (int64_t)len - K + 1 : 0;
                 row_len[rr] = use ? (int32_t)len : 0;
             }
             const uint64_t m = __ballot(w == 0 && ok);
+            // rows with observations but without the repeat certificate (meta bit 33)
+            const uint64_t m2 = __ballot(w == 0 && use && !((meta >> 33) & 1ull));
 #pragma unroll
-            for (int t = 0; t < RPI; ++t) okbits |= ((m >> (t * B)) & 1ull) << (j * RPI + t);
+            for (int t = 0; t < RPI; ++t) {
+                okbits |= ((m >> (t * B)) & 1ull) << (j * RPI + t);
+                unc |= ((m2 >> (t * B)) & 1ull) << (j * RPI + t);
+            }
         }
         if (live) {  // n_sequences: the first lane of each run of same-group rows adds the run's ok rows
             const uint32_t g_prev = __shfl_up(my_g, 1);
@@ -399,6 +469,8 @@ __global__ __launch_bounds__(kBlock) void k_row_gather(const uint64_t* __restric
                 const uint64_t run = (above ? (above & (0ull - above)) - 1ull : ~0ull) & (~0ull << lane);
                 const int cnt = __popcll(okbits & run);
                 if (cnt) atomicAdd(gstat + 5 * (int64_t)my_g + 1, (unsigned long long)cnt);
+                const int ucnt = __popcll(unc & run);  // gstat[5 g + 2]: read by k_group_classify only
+                if (ucnt) atomicAdd(gstat + 5 * (int64_t)my_g + 2, (unsigned long long)ucnt);
             }
         }
     }
@@ -658,6 +730,15 @@ struct LdsCfg {
     static_assert(kSlots - kClaim > 512, "one in-flight insert per thread past the claim cap");
 };
 constexpr unsigned long long kEmpty = ~0ull;
+
+// ROGTK_KMER_CERT=0: no group skips the LDS kernels by the repeat certificate (A/B; read once)
+inline bool kmer_cert_on() {
+    static const bool on = [] {
+        const char* e = getenv("ROGTK_KMER_CERT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 
 // ROGTK_KMER_INSERT=1 / 2: the class-3 LDS kernel's V = 1 / 2 insert loop (round-4 A/B; read once)
 inline int kmer_insert_v() {
@@ -1227,13 +1308,17 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
 // 16 lanes per group (a C3 group has ~10 rows: a wave per group left most lanes idle);
 // caps != NULL: also the group's output capacity (valid_cap of its observations)
 constexpr int kClsLanes = 16;
+// a group with nothing valid by the repeat certificate: no LDS kernel takes it, its rows
+// leave the global path (k_drop_small_rows), its count and stats stay 0 (zeroed per call)
+constexpr uint8_t kClsEmpty = 5;
 __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __restrict__ go, int64_t G,
                                                            const uint8_t* __restrict__ gk, int K,
                                                            const int64_t* __restrict__ row_obs,
                                                            const int64_t* __restrict__ row_words,
                                                            const int64_t* __restrict__ woff, int stride,
                                                            uint8_t* __restrict__ gsmall, GroupDesc* __restrict__ gdesc,
-                                                           int64_t* __restrict__ caps, int64_t min_cov) {
+                                                           int64_t* __restrict__ caps, int64_t min_cov,
+                                                           const unsigned long long* __restrict__ gstat = nullptr) {
     const int sub = threadIdx.x & (kClsLanes - 1);
     const int64_t step = (int64_t)gridDim.x * (kBlock / kClsLanes);
     // every segment of a wave runs the same number of trips (the shuffles need the lanes)
@@ -1242,15 +1327,18 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
     for (int64_t base = wave_first; base < G; base += step) {
         const int64_t g = base + (first - wave_first);
         const bool live = g < G && gk[g] == K;
-        int64_t obs = 0, words = 0;
+        int64_t obs = 0, words = 0, used = 0;
         if (live)
             for (int64_t r = go[g] + sub; r < go[g + 1]; r += kClsLanes) {
-                obs += row_obs[r];
+                const int64_t o = row_obs[r];
+                obs += o;
+                used += o > 0;
                 if (!stride) words += row_words[r];
             }
         for (int m = kClsLanes / 2; m > 0; m >>= 1) {
             obs += __shfl_xor(obs, m);
             words += __shfl_xor(words, m);
+            used += __shfl_xor(used, m);
         }
         if (sub != 0 || g >= G) continue;
         if (!live) {
@@ -1261,14 +1349,19 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
         const int64_t nrows = go[g + 1] - go[g];
         if (stride) words = nrows * stride;  // fixed-stride staging (k_row_gather)
         uint8_t cls = 0;
-        if (K <= 32 && obs > 0) {
+        // the repeat certificate (k_pack_reads): every row with observations certified and
+        // fewer of them than min_cov -> no k-mer is counted min_cov times (K >= 31)
+        const bool empty = gstat && K >= 31 && K <= 32 && min_cov >= 2 && used < min_cov && gstat[5 * g + 2] == 0;
+        if (K <= 32 && obs > 0 && empty) {
+            cls = kClsEmpty;
+        } else if (K <= 32 && obs > 0) {
             if (nrows <= LdsCfg<3>::kRows && words <= LdsCfg<3>::kWords) cls = 3;
             else if (nrows <= LdsCfg<1>::kRows && words <= LdsCfg<1>::kWords) cls = 1;
             else if (nrows <= LdsCfg<4>::kRows && words <= LdsCfg<4>::kWords) cls = 4;
         }
         gsmall[g] = cls;
         if (cls) gdesc[g] = GroupDesc{go[g], stride ? go[g] * stride : woff[go[g]], (int32_t)nrows, (int32_t)words};
-        if (caps) caps[g] = obs / (min_cov > 1 ? min_cov : 1);  // valid_cap
+        if (caps) caps[g] = cls == kClsEmpty ? 0 : obs / (min_cov > 1 ? min_cov : 1);  // valid_cap
     }
 }
 
@@ -1550,7 +1643,8 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
         if (int rc = c->gdesc.ensure((size_t)G * sizeof(GroupDesc))) return rc;
         hipLaunchKernelGGL(k_group_classify, dim3(grid_for(G * kClsLanes, 16384)), dim3(kBlock), 0, s, go, G, in.gk,
                            K, c->row_obs.as<int64_t>(), c->row_words.as<int64_t>(), c->woff.as<int64_t>(), stride,
-                           c->gsmall.as<uint8_t>(), c->gdesc.as<GroupDesc>(), in.cap_fill, min_cov);
+                           c->gsmall.as<uint8_t>(), c->gdesc.as<GroupDesc>(), in.cap_fill, min_cov,
+                           stride && kmer_cert_on() ? gstat : nullptr);
     } else if (in.cap_fill) {
         hipLaunchKernelGGL(k_group_caps_obs, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, go, G,
                            c->row_obs.as<int64_t>(), min_cov, in.cap_fill);

@@ -290,3 +290,115 @@ def test_packed_reads_max_len_too_small_fails_loudly():
     short = D.PackedReads(off, vals, max_len=100)  # 150-bp rows packed with a 100-base bound
     with pytest.raises(_lib.RogtkError, match="longer than max_len"):
         D.kmer_spectrum_blocks(short, off, vals, go, 17, 1, int((lens - 3).sum()))
+
+
+def _py_norep(row: bytes) -> bool:
+    """Python restatement of the repeat certificate (kmer_kernels.hip may_repeat16): no
+    aligned 16-mer [16j, 16j + 16) of the row occurs again at another position."""
+    L = len(row)
+    for a in range(0, L - 15, 16):
+        s = row[a:a + 16]
+        for i in range(0, L - 15):
+            if i != a and row[i:i + 16] == s:
+                return False
+    return True
+
+
+def _cert_rows(rng, n, lo=20, hi=224):
+    """Rows of random ACGT with planted repeats: tandem copies of a 20-60-base unit, a
+    16-mer repeated once (certificate withheld, no 32-mer repeat), poly-A tails, N rows."""
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    out = []
+    for _ in range(n):
+        L = int(rng.integers(lo, hi + 1))
+        x = bytearray(acgt[rng.integers(0, 4, L)].tobytes())
+        r = rng.random()
+        if r < 0.15:  # tandem repeat: 32-mers repeat
+            u = int(rng.integers(20, 61))
+            unit = x[:u]
+            x = bytearray((bytes(unit) * (L // u + 1))[:L])
+        elif r < 0.30 and L >= 48:  # one 16-mer twice (a 32-mer does not repeat)
+            a = 16 * int(rng.integers(0, (L - 16) // 16 + 1))
+            i = int(rng.integers(0, L - 15))
+            x[i:i + 16] = x[a:a + 16]
+        elif r < 0.35:
+            x[-min(L, 20):] = b"A" * min(L, 20)
+        elif r < 0.38 and L:
+            x[int(rng.integers(L))] = ord("N")
+        out.append(bytes(x))
+    return out
+
+
+def test_repeat_certificate_bit():
+    """Block meta bit 33 (the repeat certificate of rogtk_pack_reads) is sound against the
+    Python restatement (set => no aligned 16-mer repeats), and withheld only rarely
+    beyond it (the kernel also compares windows that run into the row's end padding)."""
+    import torch
+
+    from rogtk_amd import device as D
+
+    rng = np.random.default_rng(33)
+    items = _cert_rows(rng, 4000)
+    lens = np.array([len(x) for x in items], np.int64)
+    off = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)])).cuda()
+    vals = torch.from_numpy(np.frombuffer(b"".join(items), np.uint8).copy()).cuda()
+    pk = D.PackedReads(off, vals)
+    assert pk.block_words == 8
+    meta = pk.blocks.view(-1, 8)[:, 0].cpu().numpy().view(np.uint64)
+    got = ((meta >> np.uint64(33)) & np.uint64(1)).astype(bool)
+    clean = np.array([all(c in b"ACGT" for c in x) for x in items])
+    want = np.array([c and _py_norep(x) for x, c in zip(items, clean)])
+    assert not np.any(got & ~want), np.nonzero(got & ~want)[0][:10]  # sound
+    assert np.all(~got[~clean])
+    assert (want & ~got).sum() <= 0.02 * want.sum()
+    assert want.sum() > 1000  # the random rows are certified
+
+
+@pytest.mark.parametrize("mc", [2, 3, 8, 20])
+def test_repeat_certificate_spectra(mc):
+    """Groups around the certificate's bound (rows with observations vs min_coverage),
+    with tandem repeats that reach min_coverage inside few rows, k = 17 and 31 (k_eff
+    32): spectra and stats identical to the oracle on the block path."""
+    import torch
+
+    from oracle import pyoracle as P
+    from rogtk_amd import _lib
+    from rogtk_amd import device as D
+
+    rng = np.random.default_rng(100 + mc)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    items, go = [], [0]
+    for g in range(600):
+        nrows = int(rng.integers(1, 2 * mc + 3))
+        tpl = bytearray(acgt[rng.integers(0, 4, 224)].tobytes())
+        if g % 5 == 0:  # tandem template: its 32-mers repeat inside every row
+            u = int(rng.integers(20, 61))
+            tpl = bytearray((bytes(tpl[:u]) * 12)[:224])
+        for _ in range(nrows):
+            L = int(rng.integers(100, 151)) if g % 3 else 150
+            x = bytearray(tpl[:L])
+            for _ in range(int(rng.integers(0, 3))):
+                x[int(rng.integers(L))] = int(acgt[rng.integers(0, 4)])
+            items.append(bytes(x))
+        go.append(len(items))
+    lens = np.array([len(x) for x in items], np.int64)
+    off = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)])).cuda()
+    vals = torch.from_numpy(np.frombuffer(b"".join(items), np.uint8).copy()).cuda()
+    pk = D.PackedReads(off, vals)
+    gsel = torch.tensor(go, dtype=torch.int64).cuda()
+    col = P.StrCol.from_list(items)
+    _lib.call("rogtk_kmer_set_path", 1)
+    for k in (17, 31):
+        ref = P.kmer_spectrum(col, k, mc, False, np.array(go), threads=THREADS)
+        got = D.kmer_spectrum_blocks(pk, off, vals, gsel, k, mc, int(np.clip(lens - 3, 0, None).sum()))
+        torch.cuda.synchronize()
+        km = got["kmers"].cpu().numpy().view(np.uint64)
+        assert np.array_equal(got["entry_offsets"].cpu().numpy(), ref["group_offsets"]), k
+        assert np.array_equal(got["stats"].cpu().numpy(), ref["stats"]), k
+        assert np.array_equal(km[:, 0], ref["kmer_hi"]) and np.array_equal(km[:, 1], ref["kmer_lo"]), k
+        assert np.array_equal(got["exts"].cpu().numpy(), ref["exts"]), k
+        assert np.array_equal(got["counts"].cpu().numpy().view(np.uint16), ref["counts"]), k
+        # the tandem groups have valid k-mers below min_coverage rows
+        if mc >= 3:
+            tandem = [g for g in range(0, 600, 5) if go[g + 1] - go[g] < mc]
+            assert sum(int(ref["group_offsets"][g + 1] - ref["group_offsets"][g]) > 0 for g in tandem) > 0

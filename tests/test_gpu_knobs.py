@@ -160,7 +160,7 @@ offs = torch.from_numpy(z["offsets"]).cuda()
 vals = torch.from_numpy(z["values"]).cuda()
 keys = torch.from_numpy(z["keys"]).cuda()
 out = {{}}
-for mc in (1, 3):
+for mc in (1, 3, 30):
     rows, go, G, calls = D.group_spectra(offs, vals, keys, 17, mc)
     out[f"rows{{mc}}"] = rows.cpu().numpy()
     for ci, (g0, g1, r) in enumerate(calls):
@@ -198,13 +198,14 @@ def _kmer_column(tmp_path):
 
 
 def test_kmer_insert_variant_identical(tmp_path):
-    """The class-3 LDS kernel's V = 1 and V = 2 insert loops (ROGTK_KMER_INSERT=1 / 2) write
-    the default kernel's spectra bit for bit, over min_coverage 1 and 3."""
+    """The class-3 LDS kernel's V = 1 and V = 2 insert loops (ROGTK_KMER_INSERT=1 / 2), and
+    the spectra without the repeat certificate (ROGTK_KMER_CERT=0), are the default's bit
+    for bit, over min_coverage 1 and 3."""
     src = _kmer_column(tmp_path)
     outs = []
-    for v in ("0", "1", "2"):
-        path = str(tmp_path / f"k{v}.npz")
-        env = dict(os.environ, ROGTK_KMER_INSERT=v)
+    for i, knobs in enumerate(({}, {"ROGTK_KMER_INSERT": "1"}, {"ROGTK_KMER_INSERT": "2"}, {"ROGTK_KMER_CERT": "0"})):
+        path = str(tmp_path / f"k{i}.npz")
+        env = dict(os.environ, **knobs)
         r = subprocess.run([sys.executable, "-c", KMER_CHILD.format(root=ROOT, src=src, path=path)], env=env,
                            capture_output=True, text=True, timeout=240)
         assert r.returncode == 0, r.stderr[-2000:]
