@@ -305,14 +305,14 @@ def c3_workload(n: int = 100_000_000, steps: int = 3, warmup: int = 1, k: int = 
     ev = lambda: torch.cuda.Event(enable_timing=True)
     phases = {"cluster": 0.0, "group_by+kmer": 0.0}
     acc = {}
-    path_groups = [0, 0]
+    path_groups = [0, 0, 0]
 
     def step(record):
         e0, e1, e3 = ev(), ev(), ev()
         e0.record()
         D.cluster_batch(eng, batch, cid, 0)
         e1.record()
-        path_groups[:] = [0, 0]
+        path_groups[:] = [0, 0, 0]
         acc.update(valid=0, stats=[], calls=0)
 
         def consume(g0, g1, r):  # per spectrum call
@@ -323,6 +323,12 @@ def c3_workload(n: int = 100_000_000, steps: int = 3, warmup: int = 1, k: int = 
             _lib.call("rogtk_kmer_path_stats", ps)
             path_groups[0] += ps[0]
             path_groups[1] += ps[1]
+            try:  # groups the repeat certificate took off the LDS kernels (round 4)
+                cg = ctypes.c_int64(0)
+                _lib.call("rogtk_kmer_certified_groups", ctypes.byref(cg))
+                path_groups[2] += cg.value
+            except Exception:  # an older library (A/B)
+                pass
 
         _, _, G, _ = D.group_spectra(offsets, reads, cid, k, min_coverage, batch_rows=br, consume=consume,
                                      packed=None if ascii else "auto")
@@ -374,6 +380,7 @@ def c3_workload(n: int = 100_000_000, steps: int = 3, warmup: int = 1, k: int = 
                     f"spectra per group, k={k} (effective {k_eff}), min_coverage {min_coverage}",
         "reads_per_s": round(n * steps / el, 1), "ms_per_step": round(1000 * step_s, 3), "steps": steps,
         "warmup": warmup, "groups": G, "lds_groups": path_groups[0], "global_groups": path_groups[1],
+        "certified_empty_groups": path_groups[2],
         "valid_kmers": acc["valid"], "spectrum_calls": acc["calls"],
         "phases_ms": {kk: round(v / steps, 3) for kk, v in phases.items()},
         "kernels_us": kernels,

@@ -405,6 +405,10 @@ int rogtk_group_by_key(const uint32_t* keys, int64_t n, int64_t* rows_out, int64
 /* Groups of the calling thread's last rogtk_kmer_spectrum_host call per path:
  * out2[0] = LDS path, out2[1] = global path (groups with k > 64 count in neither). */
 int rogtk_kmer_path_stats(int64_t* out2);
+/* Of those LDS-path groups, the ones taken off the LDS kernels by the repeat certificate
+ * (round 4: every row with observations certified free of repeated aligned 16-mers by
+ * rogtk_pack_reads, fewer such rows than min_coverage, k_eff 32: nothing valid). */
+int rogtk_kmer_certified_groups(int64_t* out);
 int rogtk_kmer_spectrum_host(const void* offsets, int offset_width, const uint8_t* values,
                              int64_t values_len, const uint8_t* validity, int64_t validity_offset,
                              int64_t n_rows, const int64_t* group_offsets, int64_t n_groups, int k,

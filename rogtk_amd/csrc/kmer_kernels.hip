@@ -1370,19 +1370,22 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
 __global__ __launch_bounds__(kBlock) void k_path_counts(const uint8_t* __restrict__ gk, int K, int64_t G,
                                                         const uint8_t* __restrict__ gsmall,
                                                         unsigned long long* __restrict__ out2) {
-    unsigned long long lds = 0, glob = 0;
+    unsigned long long lds = 0, glob = 0, cert = 0;
     for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < G; g += (int64_t)gridDim.x * kBlock) {
         if (gk[g] != K) continue;
         if (gsmall && gsmall[g]) ++lds;
         else ++glob;
+        if (gsmall && gsmall[g] == kClsEmpty) ++cert;
     }
     for (int m = 32; m > 0; m >>= 1) {
         lds += __shfl_xor(lds, m);
         glob += __shfl_xor(glob, m);
+        cert += __shfl_xor(cert, m);
     }
     if ((threadIdx.x & 63) == 0) {
         if (lds) atomicAdd(out2, lds);
         if (glob) atomicAdd(out2 + 1, glob);
+        if (cert) atomicAdd(out2 + 2, cert);  // out2[2]: of the LDS ones, empty by the certificate
     }
 }
 
@@ -1511,6 +1514,7 @@ struct KmerCtx {
     DevBuf long_rows;  // block path: grouped rows longer than the staging stride (an error)
     bool lds_path = true;  // rogtk_kmer_set_path(): tests force the global path
     int64_t last_lds_groups = 0, last_global_groups = 0;  // rogtk_kmer_path_stats()
+    int64_t last_cert_groups = 0;                         // rogtk_kmer_certified_groups()
     ~KmerCtx() {
         if (stream) hipStreamDestroy(stream);
     }
@@ -1695,17 +1699,18 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
     }
     if (int rc = cub_exsum_i64(c, c->row_obs.as<int64_t>(), c->obs_off.as<int64_t>(), n_rows, s)) return rc;
     if (int rc = c->scal.ensure(64)) return rc;
-    ROGTK_HIP_CHECK(hipMemsetAsync(c->scal.p, 0, 16, s));
+    ROGTK_HIP_CHECK(hipMemsetAsync(c->scal.p, 0, 24, s));
     hipLaunchKernelGGL(k_path_counts, dim3(grid_for(G, 4096)), dim3(kBlock), 0, s, in.gk, K, G,
                        (c->lds_path && K <= 32) ? c->gsmall.as<uint8_t>() : nullptr,
                        c->scal.as<unsigned long long>());
-    int64_t last[4] = {0, 0, 0, 0};
+    int64_t last[5] = {0, 0, 0, 0, 0};
     ROGTK_HIP_CHECK(hipMemcpyAsync(&last[0], c->obs_off.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
     ROGTK_HIP_CHECK(hipMemcpyAsync(&last[1], c->row_obs.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
-    ROGTK_HIP_CHECK(hipMemcpyAsync(&last[2], c->scal.p, 16, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&last[2], c->scal.p, 24, hipMemcpyDeviceToHost, s));
     ROGTK_HIP_CHECK(hipStreamSynchronize(s));
     c->last_lds_groups += last[2];
     c->last_global_groups += last[3];
+    c->last_cert_groups += last[4];
     const int64_t T = last[0] + last[1];
     if (T == 0) return ROGTK_OK;
     ROGTK_REQUIRE(T <= kMaxObsPerLaunch, ROGTK_E_UNSUPPORTED,
@@ -1832,6 +1837,14 @@ extern "C" int rogtk_kmer_timing(unsigned long long* out8) {
 }
 #endif
 
+int rogtk_kmer_certified_groups(int64_t* out) {
+    ROGTK_REQUIRE(out, ROGTK_E_INVALID, "kmer_certified_groups: NULL");
+    KmerCtx* c = nullptr;
+    if (int rc = kmer_ctx(&c)) return rc;
+    *out = c->last_cert_groups;
+    return ROGTK_OK;
+}
+
 int rogtk_kmer_path_stats(int64_t* out2) {
     ROGTK_REQUIRE(out2, ROGTK_E_INVALID, "kmer_path_stats: NULL");
     KmerCtx* c = nullptr;
@@ -1952,7 +1965,7 @@ int rogtk_kmer_spectrum_host(const void* offsets, int offset_width, const uint8_
     ROGTK_HIP_CHECK(hipMemcpyAsync(c->cap_off.p, cap_off.data(), (G + 1) * 8, hipMemcpyHostToDevice, s));
     ROGTK_HIP_CHECK(hipMemsetAsync(c->gstat.p, 0, G * 5 * 8, s));
     ROGTK_HIP_CHECK(hipMemsetAsync(c->gcount.p, 0, G * 8, s));
-    c->last_lds_groups = c->last_global_groups = 0;
+    c->last_lds_groups = c->last_global_groups = c->last_cert_groups = 0;
     const KIn in{c->offsets.as<int64_t>(), c->values.as<uint8_t>(), validity ? c->validity.as<uint8_t>() : nullptr,
                  0, nullptr, c->go.as<int64_t>(), c->gk.as<uint8_t>(), c->cap_off.as<int64_t>(),
                  c->gstat.as<unsigned long long>(), c->gcount.as<int64_t>()};
@@ -2079,7 +2092,7 @@ int spectrum_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* v
     if (int rc = c->t_kmer.ensure((size_t)tcap * 16)) return rc;
     if (int rc = c->t_ext.ensure((size_t)tcap)) return rc;
     if (int rc = c->t_cnt.ensure((size_t)tcap * 2)) return rc;
-    c->last_lds_groups = c->last_global_groups = 0;
+    c->last_lds_groups = c->last_global_groups = c->last_cert_groups = 0;
     if (K && n_rows > 0) {
         KIn in{offsets, values, validity, validity_offset, rows, group_offsets, c->gk.as<uint8_t>(),
                c->cap_off.as<int64_t>(), c->gstat.as<unsigned long long>(), c->gcount.as<int64_t>()};
