@@ -219,22 +219,24 @@ __device__ __forceinline__ uint32_t pack4(uint32_t x, uint32_t& notacgt) {
 template <int NW>
 __device__ __forceinline__ bool may_repeat16(const uint64_t (&wd)[NW], int len) {
     constexpr int NA = (32 * NW - 16) / 16 + 1;  // aligned 16-mers the words can hold
-    uint32_t a[NA];
-    bool va[NA];
+    // all in VALU, no lane masks: a pair matches when (v ^ a) + inv == 0, where inv = 1 for
+    // an aligned position past this row's end (a carry out of 0xFFFFFFFF + 1 also reads as
+    // a match: conservative), and the running minimum keeps any zero (v_xad + v_min3; the
+    // lane-mask form cost two scalar instructions per pair and doubled the pack kernel)
+    uint32_t a[NA], inv[NA];
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
         a[j] = (j & 1) ? (uint32_t)wd[j >> 1] : (uint32_t)(wd[j >> 1] >> 32);
-        va[j] = 16 * j + 16 <= len;
+        inv[j] = 16 * j + 16 <= len ? 0u : 1u;
     }
-    bool rep = false;
+    uint32_t acc = 0xFFFFFFFFu;
 #pragma unroll
     for (int wi = 0; wi < NW; ++wi) {
-        if (!__ballot(32 * wi + 16 <= len)) break;  // no lane has a 16-mer starting in this word
         const uint32_t h0 = (uint32_t)(wd[wi] >> 32), h1 = (uint32_t)wd[wi];
         const uint32_t h2 = wi + 1 < NW ? (uint32_t)(wd[wi + 1] >> 32) : 0u;
 #pragma unroll
         for (int t0 = 0; t0 < 32; t0 += 8) {  // 8 positions at a time (few live registers)
-            if (!__ballot(32 * wi + t0 + 16 <= len)) break;
+            if (!__ballot(32 * wi + t0 + 16 <= len)) break;  // no lane has a 16-mer from here on
             uint32_t v[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
@@ -244,14 +246,18 @@ __device__ __forceinline__ bool may_repeat16(const uint64_t (&wd)[NW], int len) 
             }
 #pragma unroll
             for (int j = 0; j < NA; ++j) {
-                if (!__ballot(va[j])) break;  // aligned positions are valid in order
+                if (!__ballot(inv[j] == 0)) break;  // aligned positions are valid in order
 #pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (32 * wi + t0 + u != 16 * j) rep |= va[j] && v[u] == a[j];
+                for (int u = 0; u < 8; u += 2) {
+                    const bool s0 = 32 * wi + t0 + u != 16 * j, s1 = 32 * wi + t0 + u + 1 != 16 * j;
+                    const uint32_t x0 = s0 ? (v[u] ^ a[j]) + inv[j] : 0xFFFFFFFFu;
+                    const uint32_t x1 = s1 ? (v[u + 1] ^ a[j]) + inv[j] : 0xFFFFFFFFu;
+                    acc = min(acc, min(x0, x1));
+                }
             }
         }
     }
-    return rep;
+    return acc == 0;
 }
 
 // R rows per workgroup, a lane per row (R threads). DIRECT: each lane stores its row's
