@@ -382,8 +382,11 @@ int rogtk_kmer_spectrum_dev(const int64_t* offsets, const uint8_t* values, const
                             int64_t* entry_offsets, int64_t* group_stats, int64_t* n_entries, void* stream);
 /* A read column (int64 offsets, uint8 values, optional validity) packed once, in column
  * order, into fixed-size 2-bit blocks of block_words u64 per row (blocks: n * block_words):
- * word 0 = byte length | ACGT-clean << 32 (0xFFFFFFFF for a null row), then the bases, 32
- * per word, first base most significant. block_words = rogtk_read_block_words(max_len):
+ * word 0 = byte length | ACGT-clean << 32 | repeat certificate << 33 (0xFFFFFFFF for a
+ * null row), then the bases, 32 per word, first base most significant. The certificate
+ * (block_words 8 only) says no 16-mer at an aligned position 16 j occurs again in the row,
+ * so no k-mer with k_eff 32 occurs twice; the spectrum call then skips groups of fewer
+ * such rows than min_coverage (nothing valid). block_words = rogtk_read_block_words(max_len):
  * 8, 16 or 32 (rows up to 224 / 480 / 992 bases), 0 when the column is too long. */
 int rogtk_read_block_words(int64_t max_len);
 int rogtk_pack_reads(const int64_t* offsets, const uint8_t* values, const uint8_t* validity, int64_t validity_offset,
