@@ -210,7 +210,8 @@ __device__ __forceinline__ uint32_t pack4(uint32_t x, uint32_t& notacgt) {
 // 16-mer at an aligned position 16 j (16 j + 16 <= len) occurs again at any other position
 // of the row, no K-mer with K >= 31 occurs twice in it: an occurrence [p, p + K) holds the
 // whole aligned 16-mer [a, a + 16) for the multiple a of 16 in [p, p + K - 16] (K - 15 >= 16
-// consecutive integers), and a second occurrence at p + d holds it again at a + d != a.
+// consecutive integers), and a second occurrence at p + d holds it again at a + d > a:
+// only positions after the aligned one are compared (about half the pairs).
 // A group whose rows are all certified and that has fewer than min_cov rows with
 // observations then has no k-mer counted min_cov times: nothing passes CountFilter, and
 // k_group_classify takes it off the LDS kernels (class kClsEmpty). Necessary-condition
@@ -249,7 +250,9 @@ __device__ __forceinline__ bool may_repeat16(const uint64_t (&wd)[NW], int len) 
                 if (!__ballot(inv[j] == 0)) break;  // aligned positions are valid in order
 #pragma unroll
                 for (int u = 0; u < 8; u += 2) {
-                    const bool s0 = 32 * wi + t0 + u != 16 * j, s1 = 32 * wi + t0 + u + 1 != 16 * j;
+                    // only positions past the aligned one: the first occurrence holds an
+                    // aligned 16-mer that the second holds again further on
+                    const bool s0 = 32 * wi + t0 + u > 16 * j, s1 = 32 * wi + t0 + u + 1 > 16 * j;
                     const uint32_t x0 = s0 ? (v[u] ^ a[j]) + inv[j] : 0xFFFFFFFFu;
                     const uint32_t x1 = s1 ? (v[u + 1] ^ a[j]) + inv[j] : 0xFFFFFFFFu;
                     acc = min(acc, min(x0, x1));

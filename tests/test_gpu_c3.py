@@ -294,12 +294,12 @@ def test_packed_reads_max_len_too_small_fails_loudly():
 
 def _py_norep(row: bytes) -> bool:
     """Python restatement of the repeat certificate (kmer_kernels.hip may_repeat16): no
-    aligned 16-mer [16j, 16j + 16) of the row occurs again at another position."""
+    aligned 16-mer [16j, 16j + 16) of the row occurs again at a later position."""
     L = len(row)
     for a in range(0, L - 15, 16):
         s = row[a:a + 16]
-        for i in range(0, L - 15):
-            if i != a and row[i:i + 16] == s:
+        for i in range(a + 1, L - 15):
+            if row[i:i + 16] == s:
                 return False
     return True
 
