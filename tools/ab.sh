@@ -13,7 +13,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 ORDER=${AB_ORDER:-base new base new}
-CMD=${AB_CMD:-python3 bench.py --steps 30 --warmup 3 --no-cpu-baseline --no-end-to-end --sustain-seconds 1}
+CMD=${AB_CMD:-python3 bench.py --steps 30 --warmup 3 --no-cpu-baseline --no-end-to-end --no-c3 --sustain-seconds 1}
 KEYS=${AB_KEYS:-ms_per_step value}
 last=${ORDER##* }
 cp rogtk_amd/librogtk_hip.so gpurun_out/.orig.so 2>/dev/null
