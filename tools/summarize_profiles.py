@@ -19,6 +19,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "gpurun_out", "prof_bench")
+# PROFILES_OUT: where the summaries go (default profiles/; on the GPU box a directory under
+# gpurun_out/, which is what comes back)
+OUT = os.environ.get("PROFILES_OUT", os.path.join(ROOT, "profiles"))
 
 
 def short(name):
@@ -40,9 +43,8 @@ def main():
     tag = sys.argv[1]
     reads = int(sys.argv[2]) if len(sys.argv) > 2 else 10_000_000
     n_iso = int(sys.argv[3]) if len(sys.argv) > 3 else 10
-    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-    shutil.copy(os.path.join(SRC, "trace", "run_kernel_stats.csv"),
-                os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
+    os.makedirs(OUT, exist_ok=True)
+    shutil.copy(os.path.join(SRC, "trace", "run_kernel_stats.csv"), os.path.join(OUT, f"{tag}_kernel_stats.csv"))
     stats = {short(r["Name"]): r for r in csv.DictReader(open(os.path.join(SRC, "trace", "run_kernel_stats.csv")))}
     fetch, nf = counters("fetch", "FETCH_SIZE")
     write, nw = counters("write", "WRITE_SIZE")
@@ -84,10 +86,10 @@ def main():
                  "pipeline_avg_us": round(sum(pipe) / len(pipe), 2), "pipeline_dispatches": len(pipe),
                  "isolated_avg_us": round(sum(iso) / len(iso), 2) if iso else None, "isolated_dispatches": len(iso),
                  "all_avg_us": round(sum(d) / len(d), 2)}
-        with open(os.path.join(ROOT, "profiles", f"{tag}_score_split.json"), "w") as f:
+        with open(os.path.join(OUT, f"{tag}_score_split.json"), "w") as f:
             json.dump(split, f, indent=1)
         print(json.dumps(split))
-    with open(os.path.join(ROOT, "profiles", f"{tag}_pmc.json"), "w") as f:
+    with open(os.path.join(OUT, f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1)[:3000])
 
