@@ -303,3 +303,67 @@ def test_pipeline_world2_matches_oracle(rg):
             assert len(outs) == len(seeds)
             got[start:start + len(outs[k])] = outs[k]
         assert np.array_equal(got, ref), k
+
+
+@pytest.mark.parametrize("n", [1_000_000, 4_000_000])
+def test_sharded_world1_matches_engine_at_scale(rg, n):
+    """The all-to-all H3 at world 1 on synth-v1 UMIs at the C5 sizes (1M and 4M rows,
+    N / lowercase families included) gives the single-GPU engine's ids and count."""
+    import pyarrow as pa
+
+    from rogtk_amd import dist as RD
+    from rogtk_amd import synth
+
+    umis = synth.umi_ascii(n, 12, p_n=1e-4, p_lower=1e-4)
+    offs = np.arange(0, 12 * (n + 1), 12, dtype=np.int64)
+    col = pa.Array.from_buffers(pa.large_binary(), n, [None, pa.py_buffer(offs), pa.py_buffer(umis.reshape(-1))])
+    eng, ek, _ = rg.umi_cluster(col, 12, 1)
+    e = np.asarray(eng.fill_null(0xFFFFFFFF).to_numpy(zero_copy_only=False)).astype(np.uint32)
+    off = torch.from_numpy(offs).cuda()
+    vals = torch.from_numpy(umis.reshape(-1).copy()).cuda()
+    cid, k = RD.umi_cluster_sharded(off, vals, n, 12, 1)
+    torch.cuda.synchronize()
+    got = cid.cpu().numpy().view(np.uint32)
+    bad = np.nonzero(got != e)[0]
+    detail = ""
+    if len(bad) or k != ek:  # which side is wrong: the oracle on the same column
+        from oracle import pyoracle as P
+
+        ref, valid, rk, _ = P.umi_cluster(P.StrCol.from_list([bytes(r) for r in umis]), 12, 1)
+        i = bad[:5]
+        detail = (f"{len(bad)} rows differ, k sharded {k} engine {ek} oracle {rk}; sharded wrong on "
+                  f"{int(np.count_nonzero(got[valid] != ref[valid]))}, engine wrong on "
+                  f"{int(np.count_nonzero(e[valid] != ref[valid]))}; first: " + ", ".join(
+                      f"{int(j)}:{bytes(umis[j])!r} {int(got[j])} vs {int(e[j])} (oracle {int(ref[j])})" for j in i))
+    assert k == ek and not len(bad), detail
+
+
+@pytest.mark.parametrize("n", [1_000_000, 4_000_000])
+def test_bam_ranges_match_whole_file_at_scale(rg, tmp_path, n):
+    """tools/bench_bam.py's C5 check at its size: one synthetic BAM cut into 4 ranges at
+    BGZF block starts gives the whole-file run's rows (names, UMIs) and cluster ids."""
+    from rogtk_amd import bam as B
+    from rogtk_amd import synth_bam
+
+    path = str(tmp_path / "c5.bam")
+    synth_bam.synth_bam(path, n, level=6, threads=16)
+    t1 = B.bam_umi_cluster(path, umi_len=12, max_distance=1, source="sequence", n_threads=16)
+    t4 = B.bams_umi_cluster([path], umi_len=12, max_distance=1, source="sequence", n_threads=16, ranges_per_file=4)
+    assert t1.num_rows == t4.num_rows == n
+    msgs = []
+    for c in ("name", "umi", "cluster_id"):
+        a, b = t1.column(c).combine_chunks(), t4.column(c).combine_chunks()
+        if not a.equals(b):
+            neq = np.nonzero(~np.asarray(pa_equal(a, b)))[0]
+            msgs.append(f"{c}: {len(neq)} rows differ, first {neq[:3].tolist()}: "
+                        f"{[a[int(i)].as_py() for i in neq[:3]]} vs {[b[int(i)].as_py() for i in neq[:3]]}")
+    k1, k4 = int(t1.schema.metadata[b"n_clusters"]), int(t4.schema.metadata[b"n_clusters"])
+    assert not msgs and k1 == k4, "; ".join(msgs) + f"; n_clusters {k1} vs {k4}"
+
+
+def pa_equal(a, b):
+    import pyarrow.compute as pc
+
+    eq = pc.equal(a, b)
+    both_null = pc.and_(pc.is_null(a), pc.is_null(b))
+    return pc.or_(pc.fill_null(eq, False), both_null).to_numpy(zero_copy_only=False)
