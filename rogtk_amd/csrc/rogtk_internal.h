@@ -270,14 +270,22 @@ struct DevBuf {
     ~DevBuf() {
         if (p) hipFree(p);
     }
+    // A buffer that grows may still be read by kernels enqueued earlier (the BAM device
+    // path never waits for the GPU inside a file): the device drains before the old
+    // allocation is freed (hipFree does not wait for them: a 1M-record BAM read its
+    // sequence values from a freed, reallocated buffer), and a regrown buffer takes 1.5x
+    // so that growing stays rare.
     int ensure(size_t bytes) {
         if (bytes <= cap && p) return ROGTK_OK;
+        size_t grow = 0;
         if (p) {
+            ROGTK_HIP_CHECK(hipDeviceSynchronize());
             hipFree(p);
             p = nullptr;
+            grow = cap + cap / 2;
             cap = 0;
         }
-        size_t want = std::max<size_t>(bytes, 256);
+        size_t want = std::max<size_t>(std::max(bytes, grow), 256);
         want = (want + 255) / 256 * 256;
         ROGTK_HIP_CHECK(hipMalloc(&p, want));
         cap = want;
