@@ -598,7 +598,7 @@ int rogtk_bam_next(void* reader, int64_t max_records, int mode, int include_sequ
 /* Same, but the batch stays in DEVICE memory (valid until the next call). The decode is
  * enqueued on `stream` without a host wait (the columns' value buffers are sized from
  * host-known bounds; rogtk_bam_check reports corrupt records); NULL: the reader's own
- * stream, synchronised before return. */
+ * stream, synchronised before return (use a real stream for the no-sync path). */
 int rogtk_bam_next_dev(void* reader, int64_t max_records, int mode, int include_sequence, int include_quality,
                        int64_t* n_records, rogtk_bam_batch* out, void* stream);
 /* The UMI column of a device batch for the H1-H3 engine (config C5): source 0 = the first

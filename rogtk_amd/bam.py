@@ -447,24 +447,34 @@ def bam_umis_dev(bam_path: str, umi_len: int = 12, source: str = "sequence", sep
     while the reader inflates the next ones; one sync at the end."""
     import torch
 
-    stream = torch.cuda.current_stream()
+    caller = torch.cuda.current_stream()
+    # the decode, the appends and their buffers on one real stream: a NULL (default) stream
+    # would make every batch synchronous (rogtk_bam_next_dev), and work on it is not ordered
+    # with the reader's own non-blocking stream
+    stream = caller if caller.cuda_stream else torch.cuda.Stream()
+    stream.wait_stream(caller)
     dev = torch.device("cuda", torch.cuda.current_device())
     src = UMI_SOURCES[source]
-    umi = _DevColumn(dev, stream, nbytes=(1 << 20) * max(int(umi_len), 1))
-    names = _DevColumn(dev, stream, nbytes=1 << 26) if with_names else None
-    with BamReader(bam_path, n_threads, rng) as r:
-        while True:
-            n, b = _next_dev(r, DECODE_RECORDS, mode, src == 0, stream)
-            if n == 0:
-                break
-            raw = r.batch_bytes()
-            name_bound = 3 * raw + 7 * n  # lossy UTF-8: <= 3 bytes per byte; "unknown"
-            umi.append_umi(b, n, src, umi_len, sep, n * int(umi_len) if src == 0 else name_bound)
-            if names is not None:
-                names.append_strings(b.offsets[0], b.values[0], n, name_bound)
-        r.check(stream)
-        tail = r.tail()
-    out = umi.finish(), (names.to_host_strings() if names is not None else None)
+    with torch.cuda.stream(stream):
+        umi = _DevColumn(dev, stream, nbytes=(1 << 20) * max(int(umi_len), 1))
+        names = _DevColumn(dev, stream, nbytes=1 << 26) if with_names else None
+        with BamReader(bam_path, n_threads, rng) as r:
+            while True:
+                n, b = _next_dev(r, DECODE_RECORDS, mode, src == 0, stream)
+                if n == 0:
+                    break
+                raw = r.batch_bytes()
+                name_bound = 3 * raw + 7 * n  # lossy UTF-8: <= 3 bytes per byte; "unknown"
+                umi.append_umi(b, n, src, umi_len, sep, n * int(umi_len) if src == 0 else name_bound)
+                if names is not None:
+                    names.append_strings(b.offsets[0], b.values[0], n, name_bound)
+            r.check(stream)
+            tail = r.tail()
+        out = umi.finish(), (names.to_host_strings() if names is not None else None)
+    caller.wait_stream(stream)
+    if stream is not caller:  # the column is used on the caller's stream from here on
+        for t in out[0][:3]:
+            t.record_stream(caller)
     return out + (tail,) if return_tail else out
 
 

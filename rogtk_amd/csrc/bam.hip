@@ -1319,6 +1319,10 @@ int rogtk_bam_next_dev(void* reader, int64_t max_records, int mode, int include_
     // no host sync inside a file: value buffers sized from host bounds, d_bad checked by
     // rogtk_bam_check (a NULL stream keeps the synchronous behaviour)
     int rc = bam_next_common(R, max_records, mode, include_sequence, include_quality, stream == nullptr);
+    // NULL: the batch is complete on return (the reader's own stream is non-blocking, so
+    // nothing the caller enqueues afterwards, e.g. on the null stream, is ordered after its
+    // fill kernel: a UMI append on the null stream read half-filled sequences)
+    if (rc == ROGTK_OK && !stream) rc = hipStreamSynchronize(own) == hipSuccess ? ROGTK_OK : ROGTK_E_HIP;
     R->stream = own;
     if (rc != ROGTK_OK) return rc;
     memset(out, 0, sizeof *out);

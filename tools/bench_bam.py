@@ -58,7 +58,7 @@ def main():
     algo_per_rec = rec_bytes + out_bytes
 
     torch.cuda.init()
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()  # a real stream: the NULL one makes every batch synchronous
 
     def decode_pass(profile: bool):
         D.profile_enable(profile)
