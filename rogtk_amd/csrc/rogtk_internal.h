@@ -271,10 +271,9 @@ struct DevBuf {
         if (p) hipFree(p);
     }
     // A buffer that grows may still be read by kernels enqueued earlier (the BAM device
-    // path never waits for the GPU inside a file): the device drains before the old
-    // allocation is freed (hipFree does not wait for them: a 1M-record BAM read its
-    // sequence values from a freed, reallocated buffer), and a regrown buffer takes 1.5x
-    // so that growing stays rare.
+    // path never waits for the GPU inside a file): as a guard the device drains before
+    // the old allocation is freed, and a regrown buffer takes 1.5x so that growing stays
+    // rare.
     int ensure(size_t bytes) {
         if (bytes <= cap && p) return ROGTK_OK;
         size_t grow = 0;
