@@ -353,7 +353,7 @@ def c3_workload(n: int = 100_000_000, steps: int = 3, warmup: int = 1, k: int = 
     obs = n * (RL - k_eff + 1)  # k-mer observations per step (every read is ACGT, full length)
     kernels = {}
     if profile:
-        sel = ("pack_reads", "row_cert", "row_gather", "kmer_lds")
+        sel = ("pack_reads", "row_gather", "kmer_lds")
         try:
             D.profile_select(",".join(sel))
         except Exception:  # a library without these kernel names (A/B of older builds)
@@ -404,12 +404,6 @@ def c3_workload(n: int = 100_000_000, steps: int = 3, warmup: int = 1, k: int = 
         out["roofline"]["pack_reads"] = {"bound": "hbm", "kernel": "k_pack_reads", "us": kernels["pack_reads"],
                                          "bytes_per_read": RL + 64, "achieved": round(a, 1), "peak": peak,
                                          "unit": "GB/s", "frac": round(a / peak, 4)}
-    if "row_cert" in kernels:  # the repeat certificate pass (§3b): 64-B block in, VALU-bound compares
-        a = n * 64 / (kernels["row_cert"] * 1e-6) / 1e9
-        out["roofline"]["row_cert"] = {"bound": "valu", "kernel": "k_row_cert", "us": kernels["row_cert"],
-                                       "bytes_per_read": 64, "achieved": round(a, 1), "peak": peak, "unit": "GB/s",
-                                       "frac": round(a / peak, 4),
-                                       "note": "about 640 (position, aligned 16-mer) compares per 150-bp read"}
     if "row_gather" in kernels:  # 64-B block in, 40 B staged + 12 B of row metadata out
         a = n * (64 + 40 + 12) / (kernels["row_gather"] * 1e-6) / 1e9
         out["roofline"]["row_gather"] = {"bound": "hbm", "kernel": "k_row_gather", "us": kernels["row_gather"],

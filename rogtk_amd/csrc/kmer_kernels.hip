@@ -263,25 +263,6 @@ __device__ __forceinline__ bool may_repeat16(const uint64_t (&wd)[NW], int len) 
     return acc == 0;
 }
 
-// The certificate pass over packed 8-word blocks (rows of at most 224 bases): a lane per
-// row loads its block (64 B: the wave's 4 KB are contiguous), and sets meta bit 33 for a
-// clean row that holds no repeated aligned 16-mer. A pass of its own after k_pack_reads:
-// inside the pack kernel (4 waves per SIMD, held by its LDS staging) its VALU work did not
-// overlap the HBM stream (pack 6.96 -> 10.7 ms per 100M reads); here it runs at full
-// occupancy on 40 B of bases per row.
-__global__ __launch_bounds__(kBlock) void k_row_cert(uint64_t* __restrict__ blocks, int64_t n) {
-    for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < n; r += (int64_t)gridDim.x * kBlock) {
-        const ulonglong2* b = reinterpret_cast<const ulonglong2*>(blocks + r * 8);
-        const ulonglong2 q0 = b[0], q1 = b[1], q2 = b[2], q3 = b[3];
-        const uint64_t meta = q0.x;
-        const uint64_t wd[7] = {q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
-        const uint32_t len = (uint32_t)meta;
-        const bool clean = len != 0xFFFFFFFFu && ((meta >> 32) & 1ull);
-        const bool rep = clean ? may_repeat16(wd, (int)len) : true;
-        if (!rep) blocks[r * 8] = meta | (1ull << 33);
-    }
-}
-
 // R rows per workgroup, a lane per row (R threads). DIRECT: each lane stores its row's
 // block itself (16-B stores; the lanes' blocks are consecutive, so a wave covers
 // 64 * 8 * B contiguous bytes and L2 merges the lines) instead of staging the blocks in
@@ -363,6 +344,7 @@ __global__ __launch_bounds__(R) void k_pack_reads(const int64_t* __restrict__ of
             // DIRECT: 16-B stores of word pairs (2k, 2k+1); word 1 waits for the meta word
             uint64_t w1 = 0, pend = 0;
             uint64_t* const ob = DIRECT ? blocks + r * B : out + tid * OS;
+            uint64_t wd[B == 8 ? B - 1 : 1];  // B = 8: the row's words, for the repeat certificate
 #pragma unroll 1
             for (int w = 0; w < B - 1; ++w) {
                 uint64_t acc = 0;
@@ -389,6 +371,17 @@ __global__ __launch_bounds__(R) void k_pack_reads(const int64_t* __restrict__ of
                         bad |= nb;
                     }
                 }
+                if constexpr (B == 8) {
+                    switch (w) {  // static register indices in a rolled loop (w is uniform)
+                        case 0: wd[0] = acc; break;
+                        case 1: wd[1] = acc; break;
+                        case 2: wd[2] = acc; break;
+                        case 3: wd[3] = acc; break;
+                        case 4: wd[4] = acc; break;
+                        case 5: wd[5] = acc; break;
+                        default: wd[6] = acc; break;
+                    }
+                }
                 if (!DIRECT) {
                     ob[1 + w] = acc;
                 } else if (w == 0) {
@@ -399,7 +392,12 @@ __global__ __launch_bounds__(R) void k_pack_reads(const int64_t* __restrict__ of
                     *reinterpret_cast<ulonglong2*>(ob + w) = make_ulonglong2(pend, acc);
                 }
             }
-            const uint64_t meta = valid ? ((uint64_t)(uint32_t)len | ((uint64_t)(bad == 0) << 32)) : 0xFFFFFFFFull;
+            // bit 33: the repeat certificate (B = 8 only: rows of at most 224 bases)
+            bool norep = false;
+            if constexpr (B == 8) norep = valid && bad == 0 && !may_repeat16(wd, len);
+            const uint64_t meta = valid ? ((uint64_t)(uint32_t)len | ((uint64_t)(bad == 0) << 32) |
+                                           ((uint64_t)norep << 33))
+                                        : 0xFFFFFFFFull;
             if (DIRECT)
                 *reinterpret_cast<ulonglong2*>(ob) = make_ulonglong2(meta, w1);
             else
@@ -2197,9 +2195,6 @@ ProfScope prof(K_PACK_READS, s, true);
     }
     if (block_words == 8) {
         ROGTK_PACK_LAUNCH(8)
-        ProfScope pc(K_ROW_CERT, s, true);
-        hipExtLaunchKernelGGL(k_row_cert, dim3(grid_for(n, 8192)), dim3(kBlock), 0, s, pc.start(), pc.stop(), 0,
-                              blocks, n);
     } else if (block_words == 16) {
         ROGTK_PACK_LAUNCH(16)
     } else {

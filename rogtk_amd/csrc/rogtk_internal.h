@@ -54,7 +54,6 @@ enum KernelId {
     K_ROW_GATHER,
     K_KMER_LDS,
     K_RESOLVE,  // the whole resolve chain of one batch (first launch to last, its stream)
-    K_ROW_CERT,
     K_COUNT_
 };
 extern const char* const kKernelNames[K_COUNT_];
