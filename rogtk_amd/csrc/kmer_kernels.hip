@@ -1244,6 +1244,59 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
         }
         uint32_t P = 2;
         while (P < nv) P <<= 1;
+        if (P == 128) {
+            // 65..128 valid entries (a family of min_cov or more reads, e.g. C3's uncertified
+            // groups: a 150-bp template has 119 k-mers): wave 0 sorts them in registers, two
+            // per lane (element lane and 64 + lane: partners j < 64 by shuffles, j = 64 inside
+            // the lane), one barrier instead of one per bitonic stage (28) with 7 waves idle
+            if (wave == 0) {
+                uint64_t ka = vkey[lane];
+                uint32_t ia = vinfo[lane];
+                uint64_t kb = (uint32_t)(64 + lane) < nv ? vkey[64 + lane] : kEmpty;
+                uint32_t ib = (uint32_t)(64 + lane) < nv ? vinfo[64 + lane] : (1u << 31);
+                for (uint32_t k2 = 2; k2 <= 128; k2 <<= 1) {
+                    for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
+                        if (j == 64) {  // elements lane and 64 + lane: k2 = 128, ascending
+                            if (kless(kb, ib, ka, ia)) {
+                                const uint64_t tk = ka;
+                                const uint32_t ti = ia;
+                                ka = kb;
+                                ia = ib;
+                                kb = tk;
+                                ib = ti;
+                            }
+                            continue;
+                        }
+                        const bool lower = (lane & (int)j) == 0;
+                        {
+                            const uint64_t ok = __shfl_xor(ka, (int)j);
+                            const uint32_t oi = __shfl_xor(ia, (int)j);
+                            const bool up = ((uint32_t)lane & k2) == 0;
+                            const bool other_less = kless(ok, oi, ka, ia);
+                            if ((lower == up) ? other_less : !other_less && !(ok == ka && oi == ia)) {
+                                ka = ok;
+                                ia = oi;
+                            }
+                        }
+                        {
+                            const uint64_t ok = __shfl_xor(kb, (int)j);
+                            const uint32_t oi = __shfl_xor(ib, (int)j);
+                            const bool up = ((uint32_t)(64 + lane) & k2) == 0;
+                            const bool other_less = kless(ok, oi, kb, ib);
+                            if ((lower == up) ? other_less : !other_less && !(ok == kb && oi == ib)) {
+                                kb = ok;
+                                ib = oi;
+                            }
+                        }
+                    }
+                }
+                vkey[lane] = ka;
+                vinfo[lane] = ia;
+                vkey[64 + lane] = kb;
+                vinfo[64 + lane] = ib;
+            }
+            __syncthreads();
+        } else {
         for (uint32_t i = nv + tid; i < P; i += TB) {
             vkey[i] = kEmpty;
             vinfo[i] = 1u << 31;
@@ -1267,6 +1320,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
                 }
                 __syncthreads();
             }
+        }
         }
         // remove_censored_exts + output at the group's capacity offset
         for (uint32_t i = tid; i < nv; i += TB) {
