@@ -120,6 +120,8 @@ def parse():
     ap.add_argument("--assign-prev-fused", action="store_true",
                     help="batch k's score kernel also writes batch k-1's cluster ids (one launch: score and "
                          "assign tiles interleaved; rogtk_umi_score_assign_prev_packed)")
+    ap.add_argument("--main-cu-every", type=int, default=0,
+                    help="main stream on a CU mask that leaves every M-th CU to the other streams (A/B; 0: all CUs)")
     ap.add_argument("--assign-lag", type=int, default=0,
                     help="assign batch k-lag at batch k's submit (0: the pipeline's default, 1 per resolve stream)")
     ap.add_argument("--no-c3", action="store_true",
@@ -477,7 +479,8 @@ def main():
                        assign_early=not args.late_assign, mark_first=False if args.score_first else "auto",
                        device_events=not args.torch_events, mark_stream=args.mark_stream,
                        fused_assign=args.fused_assign, mark_parts=args.mark_parts,
-                       assign_prev_fused=args.assign_prev_fused, assign_lag=args.assign_lag)
+                       assign_prev_fused=args.assign_prev_fused, assign_lag=args.assign_lag,
+                       main_stream=D.cu_mask_stream(args.main_cu_every) if args.main_cu_every else None)
 
     def step():
         pipe.submit(batch)

@@ -412,6 +412,10 @@ int rogtk_kmer_path_stats(int64_t* out2);
  * (round 4: every row with observations certified free of repeated aligned 16-mers by
  * rogtk_pack_reads, fewer such rows than min_coverage, k_eff 32: nothing valid). */
 int rogtk_kmer_certified_groups(int64_t* out);
+/* A HIP stream restricted to the CUs set in mask (bit i = CU i; `words` u32 words), and its
+ * destruction (pipeline A/B: CUs kept free of the main stream for the resolve chain). */
+int rogtk_stream_create_cu_mask(const uint32_t* mask, int words, void** out);
+int rogtk_stream_destroy(void* stream);
 int rogtk_kmer_spectrum_host(const void* offsets, int offset_width, const uint8_t* values,
                              int64_t values_len, const uint8_t* validity, int64_t validity_offset,
                              int64_t n_rows, const int64_t* group_offsets, int64_t n_groups, int k,

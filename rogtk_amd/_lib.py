@@ -164,6 +164,8 @@ SIGNATURES = {
                                 _vp, _P_I64, _vp],
     "rogtk_kmer_path_stats": [_P_I64],
     "rogtk_kmer_certified_groups": [_P_I64],
+    "rogtk_stream_create_cu_mask": [ctypes.POINTER(ctypes.c_uint32), _i32, ctypes.POINTER(_vp)],
+    "rogtk_stream_destroy": [_vp],
     "rogtk_read_block_words": [_i64],
     "rogtk_host_alloc": [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)],
     "rogtk_host_free": [_vp],

@@ -591,6 +591,22 @@ extern "C" {
 
 const char* rogtk_version(void) { return "rogtk-amd 0.1.0 (gfx950)"; }
 
+// A stream whose kernels run only on the CUs set in mask (bit i = CU i, `words` u32 words):
+// the pipeline can keep some CUs free of the main stream's streaming kernels, for the
+// latency-bound resolve chain on another stream (A/B knob). Destroy with rogtk_stream_destroy.
+int rogtk_stream_create_cu_mask(const uint32_t* mask, int words, void** out) {
+    ROGTK_REQUIRE(mask && words > 0 && out, ROGTK_E_INVALID, "stream_create_cu_mask: bad arguments");
+    hipStream_t s = nullptr;
+    ROGTK_HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask));
+    *out = (void*)s;
+    return ROGTK_OK;
+}
+
+int rogtk_stream_destroy(void* stream) {
+    if (stream) ROGTK_HIP_CHECK(hipStreamDestroy((hipStream_t)stream));
+    return ROGTK_OK;
+}
+
 const char* rogtk_last_error(void) { return t_err; }
 
 // Pinned host memory for callers' output (and input) buffers: transfers from / to it

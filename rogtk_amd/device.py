@@ -507,3 +507,21 @@ def profile_read_span(kernel: str):
     n = ctypes.c_int64(0)
     _lib.call("rogtk_profile_read_span", kernel.encode(), ctypes.byref(ms), ctypes.byref(n))
     return ms.value, n.value
+
+
+def cu_mask_stream(exclude_every: int, device=None):
+    """A stream whose kernels run on every CU except those with index % exclude_every ==
+    exclude_every - 1 (rogtk_stream_create_cu_mask): the pipeline's main stream can leave
+    those CUs to the resolve chain (A/B). The HIP stream lives for the process."""
+    import torch
+
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    n = torch.cuda.get_device_properties(dev).multi_processor_count
+    words = (n + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    for i in range(n):
+        if exclude_every <= 0 or i % exclude_every != exclude_every - 1:
+            mask[i // 32] |= 1 << (i % 32)
+    out = ctypes.c_void_p()
+    _lib.call("rogtk_stream_create_cu_mask", mask, words, ctypes.byref(out))
+    return torch.cuda.ExternalStream(out.value, device=dev)

@@ -67,7 +67,8 @@ class UmiPipeline:
                  assign_on: str = "main", split_resolve: bool = False, reuse_gate: str = "auto",
                  assign_early: bool = True, mark_first="auto", device_events: bool = True,
                  mark_stream: bool = False, fused_assign: bool = False, mark_parts: bool = False,
-                 with_distance: bool = False, assign_prev_fused: bool = False, assign_lag: int = 0):
+                 with_distance: bool = False, assign_prev_fused: bool = False, assign_lag: int = 0,
+                 main_stream=None):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
@@ -83,7 +84,8 @@ class UmiPipeline:
         self.slots = [_Slot(umi_len, max_distinct, n_max, dev, with_scores, with_distance) for _ in range(depth)]
         # priorities: (main, resolve, assign); lower = higher priority (torch convention)
         self.caller = torch.cuda.current_stream(dev)
-        self.main = torch.cuda.Stream(dev, priority=priorities[0])
+        # main_stream: a caller's stream for the main chain (e.g. device.cu_mask_stream)
+        self.main = main_stream if main_stream is not None else torch.cuda.Stream(dev, priority=priorities[0])
         self.main.wait_stream(self.caller)
         # resolve_streams > 1: consecutive batches resolve on different streams, so two
         # latency-bound resolve chains overlap (needs depth >= resolve_streams + 1)
