@@ -200,9 +200,12 @@ __device__ __forceinline__ uint32_t zero_bytes(uint32_t v) {
 __device__ __forceinline__ uint32_t pack4(uint32_t x, uint32_t& notacgt) {
     const uint32_t c = ((x >> 1) ^ (x >> 2)) & 0x03030303u;  // base2 of every byte
     const uint32_t u = x | 0x20202020u;                       // A/C/G/T -> a/c/g/t (only those map there)
-    const uint32_t ok = zero_bytes(u ^ 0x61616161u) | zero_bytes(u ^ 0x63636363u) | zero_bytes(u ^ 0x67676767u) |
-                        zero_bytes(u ^ 0x74747474u);
-    notacgt = ~ok & 0x80808080u;
+    // a byte is A/C/G/T iff it equals the letter its own 2-bit code names: one byte
+    // permute of "acgt" by the codes (v_perm_b32; the table in both sources, so either
+    // selector half reads it) and one zero-byte test, instead of four
+    constexpr uint32_t kAcgt = 0x74676361u;  // 'a' 'c' 'g' 't', byte 0 first
+    const uint32_t expect = __builtin_amdgcn_perm(kAcgt, kAcgt, c);
+    notacgt = ~zero_bytes(u ^ expect) & 0x80808080u;
     return ((c & 0xFFu) << 6) | (((c >> 8) & 0xFFu) << 4) | (((c >> 16) & 0xFFu) << 2) | (c >> 24);
 }
 
