@@ -1118,3 +1118,37 @@ def test_level2_transfers_pinned_and_pageable(rg):
     _lib.call("rogtk_umi_cluster_host", ctypes.c_void_p(offs.ctypes.data), 8, ctypes.c_void_p(vals.ctypes.data),
               vals.size, None, 0, n, L, 1, ctypes.c_void_p(cid.ctypes.data), ctypes.byref(nk), ctypes.byref(rl))
     assert nk.value == k_p and np.array_equal(_np(cid_p).astype(np.uint32), cid)
+
+
+@pytest.mark.parametrize("every", [8, 4])
+def test_pipeline_cu_mask_main_stream(rg, every):
+    """The main chain on a CU-masked stream (device.cu_mask_stream, bench --main-cu-every):
+    every batch's ids, scores and Hamming bits equal the sequential device path."""
+    import torch
+
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+    from rogtk_amd.pipeline import UmiPipeline
+
+    n, L, nb = 1_100_009, 12, 3
+    seeds = [synth.DEFAULT_SEED + 17 * k for k in range(nb)]
+    outs = []
+
+    def grab(slot, batch):
+        outs.append((slot.cid[:n].clone(), slot.within.clone(), slot.scores["combined_score"][:n].clone()))
+
+    pipe = UmiPipeline(L, n, n, "cuda", depth=2, target=b"ACGTACGTACGT", max_distance=1, on_assigned=grab,
+                       main_stream=D.cu_mask_stream(every))
+    keep = []
+    for s in seeds:
+        keep.append(D.PackedBatch(torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda(), L))
+        pipe.submit(keep[-1])
+    pipe.drain()
+    torch.cuda.synchronize()
+    assert len(outs) == nb
+    for k in range(nb):
+        _, scores, _, hw, cid, _ = _device_run(n, seed=seeds[k])
+        g_cid, g_w, g_comb = (t.cpu().numpy() for t in outs[k])
+        assert np.array_equal(g_cid, cid.cpu().numpy()), k
+        assert np.array_equal(g_w, hw.cpu().numpy()), k
+        assert np.array_equal(g_comb.view(np.uint64), scores["combined_score"][:n].cpu().numpy().view(np.uint64)), k
