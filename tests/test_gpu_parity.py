@@ -1152,3 +1152,38 @@ def test_pipeline_cu_mask_main_stream(rg, every):
         assert np.array_equal(g_cid, cid.cpu().numpy()), k
         assert np.array_equal(g_w, hw.cpu().numpy()), k
         assert np.array_equal(g_comb.view(np.uint64), scores["combined_score"][:n].cpu().numpy().view(np.uint64)), k
+
+
+@pytest.mark.parametrize("depth,rs,lag", [(3, 2, 0), (4, 2, 3), (4, 3, 0)])
+def test_pipeline_resolve_streams(rg, depth, rs, lag):
+    """resolve_streams > 1 (consecutive batches resolve on different streams) with the
+    default schedule, and with assign_lag: every batch's ids, scores and Hamming bits,
+    taken at its on_assigned hook, equal the sequential device path."""
+    import torch
+
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+    from rogtk_amd.pipeline import UmiPipeline
+
+    n, L, nb = 600_011, 12, 6
+    seeds = [synth.DEFAULT_SEED + 13 * k for k in range(nb)]
+    outs = []
+
+    def grab(slot, batch):
+        outs.append((slot.cid[:n].clone(), slot.within.clone(), slot.scores["combined_score"][:n].clone()))
+
+    pipe = UmiPipeline(L, n, n, "cuda", depth=depth, target=b"ACGTACGTACGT", max_distance=1, on_assigned=grab,
+                       resolve_streams=rs, assign_lag=lag)
+    keep = []
+    for s in seeds:
+        keep.append(D.PackedBatch(torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda(), L))
+        pipe.submit(keep[-1])
+    pipe.drain()
+    torch.cuda.synchronize()
+    assert len(outs) == nb
+    for k in range(nb):
+        _, scores, _, hw, cid, _ = _device_run(n, seed=seeds[k])
+        g_cid, g_w, g_comb = (t.cpu().numpy() for t in outs[k])
+        assert np.array_equal(g_cid, cid.cpu().numpy()), k
+        assert np.array_equal(g_w, hw.cpu().numpy()), k
+        assert np.array_equal(g_comb.view(np.uint64), scores["combined_score"][:n].cpu().numpy().view(np.uint64)), k
