@@ -220,8 +220,10 @@ __device__ __forceinline__ uint32_t pack4(uint32_t x, uint32_t& notacgt) {
 // k_group_classify takes it off the LDS kernels (class kClsEmpty). Necessary-condition
 // check only: a pair found (even across the row's end padding) just withholds the bit.
 // One lane per row over its NW packed words; compares 16-mers as u32 (alignbit).
+// lmax: a wave-uniform bound >= the length of every lane that calls (the loops' exits are
+// scalar branches, not a VALU compare + ballot per chunk and aligned position)
 template <int NW>
-__device__ __forceinline__ bool may_repeat16(const uint64_t (&wd)[NW], int len) {
+__device__ __forceinline__ bool may_repeat16(const uint64_t (&wd)[NW], int len, int lmax) {
     constexpr int NA = (32 * NW - 16) / 16 + 1;  // aligned 16-mers the words can hold
     // all in VALU, no lane masks: a pair matches when (v ^ a) + inv == 0, where inv = 1 for
     // an aligned position past this row's end (a carry out of 0xFFFFFFFF + 1 also reads as
@@ -240,7 +242,7 @@ __device__ __forceinline__ bool may_repeat16(const uint64_t (&wd)[NW], int len) 
         const uint32_t h2 = wi + 1 < NW ? (uint32_t)(wd[wi + 1] >> 32) : 0u;
 #pragma unroll
         for (int t0 = 0; t0 < 32; t0 += 8) {  // 8 positions at a time (few live registers)
-            if (!__ballot(32 * wi + t0 + 16 <= len)) break;  // no lane has a 16-mer from here on
+            if (32 * wi + t0 + 16 > lmax) break;  // no lane has a 16-mer from here on
             uint32_t v[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
@@ -250,16 +252,27 @@ __device__ __forceinline__ bool may_repeat16(const uint64_t (&wd)[NW], int len) 
             }
 #pragma unroll
             for (int j = 0; j < NA; ++j) {
-                if (!__ballot(inv[j] == 0)) break;  // aligned positions are valid in order
+                if (16 * j + 16 > lmax) break;  // aligned positions are valid in order
+                // only positions past the aligned one: the first occurrence holds an
+                // aligned 16-mer that the second holds again further on. The compared
+                // positions of this (chunk, j) are known at compile time: pairs of them
+                // fold into acc with one v_min3 each (a chain per (chunk, j); one chain
+                // over the chunk is rebalanced by the compiler into min + min3 pairs)
+                uint32_t pend = 0;
+                bool has = false;
 #pragma unroll
-                for (int u = 0; u < 8; u += 2) {
-                    // only positions past the aligned one: the first occurrence holds an
-                    // aligned 16-mer that the second holds again further on
-                    const bool s0 = 32 * wi + t0 + u > 16 * j, s1 = 32 * wi + t0 + u + 1 > 16 * j;
-                    const uint32_t x0 = s0 ? (v[u] ^ a[j]) + inv[j] : 0xFFFFFFFFu;
-                    const uint32_t x1 = s1 ? (v[u + 1] ^ a[j]) + inv[j] : 0xFFFFFFFFu;
-                    acc = min(acc, min(x0, x1));
+                for (int u = 0; u < 8; ++u) {
+                    if (!(32 * wi + t0 + u > 16 * j)) continue;
+                    const uint32_t x = (v[u] ^ a[j]) + inv[j];
+                    if (has) {
+                        acc = min(min(acc, pend), x);
+                        has = false;
+                    } else {
+                        pend = x;
+                        has = true;
+                    }
                 }
+                if (has) acc = min(acc, pend);
             }
         }
     }
@@ -270,6 +283,11 @@ __device__ __forceinline__ bool may_repeat16(const uint64_t (&wd)[NW], int len) 
 // block itself (16-B stores; the lanes' blocks are consecutive, so a wave covers
 // 64 * 8 * B contiguous bytes and L2 merges the lines) instead of staging the blocks in
 // LDS for one coalesced store: less LDS per workgroup, more workgroups per CU.
+// Software-pipelined (round 4): the next trip's bytes are loaded into registers (kVin
+// dwords per lane) before this trip's rows are packed, and written to LDS after them, so
+// each wave's HBM round trip hides behind its own VALU work (the repeat certificate made
+// the pack phase ~3.5 us per 64-row trip) instead of being added to it; the row offsets
+// are loaded two trips ahead.
 template <int B, int R = kBlock, bool DIRECT = false>
 __global__ __launch_bounds__(R) void k_pack_reads(const int64_t* __restrict__ offsets,
                                                   const uint8_t* __restrict__ values,
@@ -277,60 +295,82 @@ __global__ __launch_bounds__(R) void k_pack_reads(const int64_t* __restrict__ of
                                                   int64_t n, uint64_t* __restrict__ blocks) {
     constexpr int OS = B + 1;  // LDS stride of a row's block (odd: fewer bank conflicts)
     constexpr int kIn = kPackInBytes * R / kBlock;  // staged bytes: 160 per row
-    __shared__ uint32_t in32[kIn / 4 + 2];
+    constexpr int kVin = kIn / 4 / R;               // staged dwords per lane (40)
+    __shared__ uint32_t in32[kIn / 4 + 3];  // + the funnel shift's 2 zero dwords + a dummy slot
     __shared__ uint64_t out[DIRECT ? 1 : R * OS];
     __shared__ int64_t s_off[R + 1];
     const int tid = threadIdx.x;
-    // the next trip's row offsets are loaded into registers while this trip runs, so a
-    // trip waits for one HBM round trip (its bytes) instead of two (offsets, then bytes)
-    int64_t pf0 = 0, pf1 = 0;
-    auto prefetch = [&](int64_t aa) {
-        const int nrr = (int)min<int64_t>(R, n - aa);
-        pf0 = tid <= nrr ? offsets[aa + tid] : 0;
-        pf1 = tid + R <= nrr ? offsets[aa + tid + R] : 0;
+    const int64_t stride = (int64_t)gridDim.x * R;
+    // a trip's row offsets: lane t holds offsets[a + t] (t <= nr) and offsets[a + t + R]
+    // (t + R <= nr, i.e. lane 0 when the trip is full); b0 / b1 = offsets[a], offsets[a + nr]
+    // by uniform (scalar) loads
+    struct Offs {
+        int64_t o0, o1, b0, b1;
     };
-    if ((int64_t)blockIdx.x * R < n) prefetch((int64_t)blockIdx.x * R);
-    for (int64_t a = (int64_t)blockIdx.x * R; a < n; a += (int64_t)gridDim.x * R) {
+    auto load_offs = [&](int64_t aa) {
+        Offs f{0, 0, 0, 0};
+        if (aa < n) {
+            const int nrr = (int)min<int64_t>(R, n - aa);
+            f.o0 = offsets[aa + min(tid, nrr)];
+            f.o1 = offsets[aa + min(tid + R, nrr)];
+            f.b0 = offsets[aa];
+            f.b1 = offsets[aa + nrr];
+        }
+        return f;
+    };
+    // the bytes [a4, b1) of a trip, in kVin dword registers per lane (+ the last partial
+    // dword's bytes); only when they fit the staging area
+    uint32_t vin[kVin];
+    uint32_t tail = 0;
+    auto load_bytes = [&](int64_t b0, int64_t b1) {
+        const int64_t a4 = b0 & ~3ll;
+        if (b1 - a4 > kIn) return;  // not staged: read byte by byte below
+        const int full = (int)((b1 - a4) >> 2);
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(values + a4);
+        if (full > 0) {
+            // all kVin loads, clamped: no branch around a load (which would make the
+            // compiler keep vin in scratch), and every load is inside [a4, b1)
+#pragma unroll
+            for (int u = 0; u < kVin; ++u) vin[u] = src[min(u * R + tid, full - 1)];
+        }
+        if (4 * full < (int)(b1 - a4)) {  // the last partial dword, byte by byte (never past b1)
+            const uint8_t* tb = values + a4 + 4 * full;
+            const int left = (int)(b1 - a4) - 4 * full;
+            tail = tb[0];
+            if (left > 1) tail |= (uint32_t)tb[1] << 8;
+            if (left > 2) tail |= (uint32_t)tb[2] << 16;
+        }
+    };
+    int64_t a = (int64_t)blockIdx.x * R;
+    Offs cur = load_offs(a), nxt = load_offs(a + stride);
+    if (a < n) load_bytes(cur.b0, cur.b1);
+    for (; a < n; a += stride) {
         const int nr = (int)min<int64_t>(R, n - a);
-        if (tid <= nr) s_off[tid] = pf0;
-        if (tid + R <= nr) s_off[tid + R] = pf1;
-        __syncthreads();
-        if (a + (int64_t)gridDim.x * R < n) prefetch(a + (int64_t)gridDim.x * R);
-        const int64_t b0 = s_off[0], b1 = s_off[nr];
+        if (tid <= nr) s_off[tid] = cur.o0;
+        if (tid + R <= nr) s_off[tid + R] = cur.o1;
+        const int64_t b0 = cur.b0, b1 = cur.b1;
         const int64_t a4 = b0 & ~3ll;  // dword-aligned start
         const bool staged = b1 - a4 <= kIn;
-        if (staged) {  // the rows' bytes, coalesced dword loads (no byte past b1 is read)
-            const int64_t nw = (b1 - a4 + 3) >> 2;
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(values + a4);
-            const int64_t full = (b1 - a4) >> 2;  // dwords entirely inside [a4, b1)
-            // kStageBatch loads per lane in flight before their LDS writes: a one-dword-per-
-            // iteration loop waits a whole HBM round trip per dword (s_waitcnt vmcnt(0)
-            // before every ds_write), ~38 of them per 64-row trip
-            constexpr int kStageBatch = 16;
-            for (int64_t i0 = 0; i0 < full; i0 += (int64_t)R * kStageBatch) {
-                uint32_t v[kStageBatch];
+        if (staged) {
+            const int nw = (int)((b1 - a4 + 3) >> 2);
+            const int full = (int)((b1 - a4) >> 2);
+            // every lane writes all kVin registers: past `full` into a dummy slot (no branch)
 #pragma unroll
-                for (int u = 0; u < kStageBatch; ++u) {
-                    const int64_t i = i0 + (int64_t)u * R + tid;
-                    v[u] = i < full ? src[i] : 0u;
-                }
-#pragma unroll
-                for (int u = 0; u < kStageBatch; ++u) {
-                    const int64_t i = i0 + (int64_t)u * R + tid;
-                    if (i < full) in32[i] = v[u];
-                }
-            }
-            if (full < nw && tid == 0) {  // the last partial dword, byte by byte
-                uint32_t v = 0;
-                for (int j = 0; j < 4; ++j) {
-                    const int64_t byte = a4 + 4 * full + j;
-                    if (byte < b1) v |= (uint32_t)values[byte] << (8 * j);
-                }
-                in32[full] = v;
-            }
+            for (int u = 0; u < kVin; ++u) in32[u * R + tid < full ? u * R + tid : kIn / 4 + 2] = vin[u];
+            if (full < nw && tid == 0) in32[full] = tail;
             if (tid < 2) in32[nw + tid] = 0;  // the funnel shift below may read one dword past
         }
         __syncthreads();
+        // the next trip's bytes and the offsets of the one after, in flight while this trip
+        // is packed
+        const int64_t an = a + stride;
+        if (an < n) load_bytes(nxt.b0, nxt.b1);
+        const Offs nn = load_offs(an + stride);
+        // a wave-uniform bound on the rows' lengths (the certificate's loop exits)
+        int my_len = tid < nr ? (int)(s_off[tid + 1] - s_off[tid]) : 0;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) my_len = max(my_len, __shfl_xor(my_len, m, 64));
+        const int lmax = __builtin_amdgcn_readfirstlane(my_len);
         if (tid < nr) {  // this lane's row, entirely in registers: no cross-lane steps
             const int64_t r = a + tid;
             bool valid = true;
@@ -360,8 +400,7 @@ __global__ __launch_bounds__(R) void k_pack_reads(const int64_t* __restrict__ of
                         if (left > 0) {
                             if (staged) {  // in32[q + 1] exists: the row's bytes end inside in32[.. nw]
                                 const int q = (rel + j) >> 2;
-                                const uint64_t two = ((uint64_t)in32[q + 1] << 32) | in32[q];
-                                x = (uint32_t)(two >> sh);
+                                x = __builtin_amdgcn_alignbit(in32[q + 1], in32[q], sh);
                             } else {
                                 for (int t = 0; t < 4; ++t)
                                     if (j + t < len) x |= (uint32_t)values[st + j + t] << (8 * t);
@@ -397,7 +436,7 @@ __global__ __launch_bounds__(R) void k_pack_reads(const int64_t* __restrict__ of
             }
             // bit 33: the repeat certificate (B = 8 only: rows of at most 224 bases)
             bool norep = false;
-            if constexpr (B == 8) norep = valid && bad == 0 && !may_repeat16(wd, len);
+            if constexpr (B == 8) norep = valid && bad == 0 && !may_repeat16(wd, len, lmax);
             const uint64_t meta = valid ? ((uint64_t)(uint32_t)len | ((uint64_t)(bad == 0) << 32) |
                                            ((uint64_t)norep << 33))
                                         : 0xFFFFFFFFull;
@@ -412,6 +451,8 @@ __global__ __launch_bounds__(R) void k_pack_reads(const int64_t* __restrict__ of
             for (int i = tid; i < nr * B; i += R) dst[i] = out[(i / B) * OS + (i % B)];
             __syncthreads();
         }
+        cur = nxt;
+        nxt = nn;
     }
 }
 
