@@ -1564,22 +1564,39 @@ __global__ __launch_bounds__(kBlock) void k_group_stats_out(const unsigned long 
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_iota64(int64_t* __restrict__ out, int64_t n) {
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) out[i] = i;
-}
-
 __global__ __launch_bounds__(kBlock) void k_key_heads(const uint32_t* __restrict__ k, int64_t n,
                                                       uint32_t* __restrict__ head) {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
         head[i] = (i == 0 || k[i] != k[i - 1]) ? 1u : 0u;
 }
 
-__global__ __launch_bounds__(kBlock) void k_key_offsets(const uint32_t* __restrict__ head,
-                                                        const uint32_t* __restrict__ gid, int64_t n,
-                                                        int64_t* __restrict__ go) {
+__global__ __launch_bounds__(kBlock) void k_iota32(uint32_t* __restrict__ out, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+        out[i] = (uint32_t)i;
+}
+
+// the largest key (the radix sort then covers only its significant bits); *mx zeroed before
+__global__ __launch_bounds__(kBlock) void k_key_max(const uint32_t* __restrict__ k, int64_t n,
+                                                    uint32_t* __restrict__ mx) {
+    uint32_t m = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+        m = max(m, k[i]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(mx, m);
+}
+
+// the group offsets (an exclusive scan of the heads: a head's group = gid; row i's group =
+// gid + head - 1) and the sorted u32 row indices widened to int64
+__global__ __launch_bounds__(kBlock) void k_key_offsets_rows(const uint32_t* __restrict__ head,
+                                                             const uint32_t* __restrict__ gid,
+                                                             const uint32_t* __restrict__ rows32, int64_t n,
+                                                             int64_t* __restrict__ go, int64_t* __restrict__ rows) {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
-        if (head[i]) go[gid[i]] = i;                    // exclusive scan: a head's group = gid
-        if (i == n - 1) go[gid[i] + head[i]] = n;       // row i's group = gid + head - 1
+        const uint32_t h = head[i];
+        rows[i] = rows32[i];
+        if (h) go[gid[i]] = i;
+        if (i == n - 1) go[gid[i] + h] = n;
     }
 }
 
@@ -2129,19 +2146,30 @@ int rogtk_group_by_key(const uint32_t* keys, int64_t n, int64_t* rows_out, int64
     if (int rc = c->tmp_u32.ensure((size_t)n * 4)) return rc;
     if (int rc = c->head.ensure((size_t)n * 4)) return rc;
     if (int rc = c->rid.ensure((size_t)n * 4)) return rc;
-    if (int rc = c->obs_off.ensure((size_t)n * 8)) return rc;
+    if (int rc = c->obs_off.ensure((size_t)n * 8)) return rc;  // the u32 row indices, in and out
+    if (int rc = c->scal.ensure(64)) return rc;
     const int g = grid_for(n);
-    hipLaunchKernelGGL(k_iota64, dim3(g), dim3(kBlock), 0, s, c->obs_off.as<int64_t>(), n);
+    // round 4: u32 row indices through the sort (16 instead of 24 B per row and pass) and
+    // only the keys' significant bits (C3: ids < 2^23, 3 onesweep passes instead of 4)
+    uint32_t* const iota = c->obs_off.as<uint32_t>();
+    uint32_t* const rows32 = iota + n;
+    ROGTK_HIP_CHECK(hipMemsetAsync(c->scal.p, 0, 4, s));
+    hipLaunchKernelGGL(k_key_max, dim3(g), dim3(kBlock), 0, s, keys, n, c->scal.as<uint32_t>());
+    hipLaunchKernelGGL(k_iota32, dim3(g), dim3(kBlock), 0, s, iota, n);
+    uint32_t kmax = 0;
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&kmax, c->scal.p, 4, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    const int end_bit = kmax ? 32 - __builtin_clz(kmax) : 1;
     size_t bytes = 0;
-    ROGTK_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, keys, c->tmp_u32.as<uint32_t>(),
-                                                       c->obs_off.as<int64_t>(), rows_out, (int)n, 0, 32, s));
+    ROGTK_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, keys, c->tmp_u32.as<uint32_t>(), iota, rows32,
+                                                       (int)n, 0, end_bit, s));
     if (int rc = c->cub.ensure(bytes)) return rc;
-    ROGTK_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(c->cub.p, bytes, keys, c->tmp_u32.as<uint32_t>(),
-                                                       c->obs_off.as<int64_t>(), rows_out, (int)n, 0, 32, s));
+    ROGTK_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(c->cub.p, bytes, keys, c->tmp_u32.as<uint32_t>(), iota, rows32,
+                                                       (int)n, 0, end_bit, s));
     hipLaunchKernelGGL(k_key_heads, dim3(g), dim3(kBlock), 0, s, c->tmp_u32.as<uint32_t>(), n, c->head.as<uint32_t>());
     if (int rc = cub_exsum_u32(c, c->head.as<uint32_t>(), c->rid.as<uint32_t>(), n, s)) return rc;
-    hipLaunchKernelGGL(k_key_offsets, dim3(g), dim3(kBlock), 0, s, c->head.as<uint32_t>(), c->rid.as<uint32_t>(), n,
-                       group_offsets_out);
+    hipLaunchKernelGGL(k_key_offsets_rows, dim3(g), dim3(kBlock), 0, s, c->head.as<uint32_t>(), c->rid.as<uint32_t>(),
+                       rows32, n, group_offsets_out, rows_out);
     ROGTK_HIP_CHECK(hipGetLastError());
     uint32_t last[2];
     ROGTK_HIP_CHECK(hipMemcpyAsync(&last[0], c->rid.as<uint32_t>() + n - 1, 4, hipMemcpyDeviceToHost, s));

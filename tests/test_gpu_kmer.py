@@ -199,9 +199,11 @@ def test_group_by_key_device(rg):
     from rogtk_amd import device as D
 
     rng = np.random.default_rng(2)
-    for n, hi in ((1, 5), (1000, 7), (100_003, 50_000), (300_000, 0xFFFFFFFF)):
+    # key ranges: the sort covers only the largest key's significant bits (all-zero keys,
+    # a power-of-two bound, the full 32 bits with the null id)
+    for n, hi in ((1, 5), (1000, 7), (5000, 1), (200_003, 1 << 23), (100_003, 50_000), (300_000, 0xFFFFFFFF)):
         keys = rng.integers(0, hi, n, dtype=np.uint64).astype(np.uint32)
-        if n > 10:
+        if n > 10 and hi > 1 << 23:
             keys[:5] = 0xFFFFFFFF  # null ids group last
         rows, go, G = D.group_by_key(torch.from_numpy(keys.view(np.int32)).cuda())
         order = np.argsort(keys, kind="stable")
