@@ -287,16 +287,19 @@ __device__ __forceinline__ bool may_repeat16(const uint64_t (&wd)[NW], int len, 
 // dwords per lane) before this trip's rows are packed, and written to LDS after them, so
 // each wave's HBM round trip hides behind its own VALU work (the repeat certificate made
 // the pack phase ~3.5 us per 64-row trip) instead of being added to it; the row offsets
-// are loaded two trips ahead.
+// are loaded two trips ahead. R = 64: at least 3 waves per SIMD (<= 168 VGPRs: the 40 prefetch
+// registers sit beside the certificate's).
 template <int B, int R = kBlock, bool DIRECT = false>
-__global__ __launch_bounds__(R) void k_pack_reads(const int64_t* __restrict__ offsets,
+__global__ __launch_bounds__(R, R == 64 ? 3 : 1) void k_pack_reads(const int64_t* __restrict__ offsets,
                                                   const uint8_t* __restrict__ values,
                                                   const uint8_t* __restrict__ validity, int64_t voff,
                                                   int64_t n, uint64_t* __restrict__ blocks) {
     constexpr int OS = B + 1;  // LDS stride of a row's block (odd: fewer bank conflicts)
     constexpr int kIn = kPackInBytes * R / kBlock;  // staged bytes: 160 per row
     constexpr int kVin = kIn / 4 / R;               // staged dwords per lane (40)
-    __shared__ uint32_t in32[kIn / 4 + 3];  // + the funnel shift's 2 zero dwords + a dummy slot
+    // + the funnel shift's 2 zero dwords, a dummy slot, and slack for a word's 9-dword read
+    // past the last row's end (< 8 dwords past nw)
+    __shared__ uint32_t in32[kIn / 4 + 12];
     __shared__ uint64_t out[DIRECT ? 1 : R * OS];
     __shared__ int64_t s_off[R + 1];
     const int tid = threadIdx.x;
@@ -392,19 +395,24 @@ __global__ __launch_bounds__(R) void k_pack_reads(const int64_t* __restrict__ of
             for (int w = 0; w < B - 1; ++w) {
                 uint64_t acc = 0;
                 if (w < used) {
+                    // the word's 32 bytes: 9 staged dwords from (rel >> 2) + 8 w (read past the
+                    // row's end into the slack of in32: masked below)
+                    uint32_t t9[9];
+                    if (staged) {
+                        const int qb = (rel >> 2) + 8 * w;
+#pragma unroll
+                        for (int i = 0; i < 9; ++i) t9[i] = in32[qb + i];
+                    }
 #pragma unroll
                     for (int d = 0; d < 8; ++d) {
                         const int j = w * 32 + d * 4;  // first byte of these 4
                         const int left = len - j;      // bytes of the row from j on
                         uint32_t x = 0;
-                        if (left > 0) {
-                            if (staged) {  // in32[q + 1] exists: the row's bytes end inside in32[.. nw]
-                                const int q = (rel + j) >> 2;
-                                x = __builtin_amdgcn_alignbit(in32[q + 1], in32[q], sh);
-                            } else {
-                                for (int t = 0; t < 4; ++t)
-                                    if (j + t < len) x |= (uint32_t)values[st + j + t] << (8 * t);
-                            }
+                        if (staged) {
+                            x = __builtin_amdgcn_alignbit(t9[d + 1], t9[d], sh);
+                        } else if (left > 0) {
+                            for (int t = 0; t < 4; ++t)
+                                if (j + t < len) x |= (uint32_t)values[st + j + t] << (8 * t);
                         }
                         const uint32_t inmask = left >= 4 ? 0xFFFFFFFFu : left <= 0 ? 0u : (1u << (8 * left)) - 1u;
                         x = (x & inmask) | (0x41414141u & ~inmask);  // past the end: 'A' (code 0, valid)
