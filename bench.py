@@ -355,11 +355,15 @@ def c3_workload(n: int = 100_000_000, steps: int = 3, warmup: int = 1, k: int = 
     obs = n * (RL - k_eff + 1)  # k-mer observations per step (every read is ACGT, full length)
     kernels = {}
     if profile:
-        sel = ("pack_reads", "row_gather", "kmer_lds")
+        sel = ("pack_reads", "row_gather", "kmer_lds", "kmer_minimizer")
         try:
             D.profile_select(",".join(sel))
         except Exception:  # a library without these kernel names (A/B of older builds)
-            sel = ()
+            sel = sel[:3]
+            try:
+                D.profile_select(",".join(sel))
+            except Exception:
+                sel = ()
         D.profile_reset()
         D.profile_enable(True)
         step(False)

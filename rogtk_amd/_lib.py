@@ -159,6 +159,7 @@ SIGNATURES = {
                                _P_I32],
     "rogtk_kmer_capacity": [_vp, _i32, _i64, _P_I64],
     "rogtk_kmer_set_path": [_i32],
+    "rogtk_kmer_set_filter": [_i32],
     "rogtk_group_by_key": [_vp, _i64, _vp, _vp, _P_I64, _vp],
     "rogtk_kmer_spectrum_dev": [_vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _i64, _vp, _vp, _vp, _vp,
                                 _vp, _P_I64, _vp],

@@ -38,7 +38,7 @@ const char* const kKernelNames[K_COUNT_] = {
     "cluster_bitmap", "cluster_scan",   "cluster_compact", "cluster_union",
     "cluster_flatten", "cluster_label", "cluster_assign", "cluster_irregular",
     "bam_fields",     "bam_scan",       "bam_fill",      "pack_reads",
-    "row_gather",     "kmer_lds",      "cluster_resolve"};
+    "row_gather",     "kmer_lds",      "cluster_resolve", "kmer_minimizer"};
 
 namespace {
 std::atomic<bool> g_prof{false};

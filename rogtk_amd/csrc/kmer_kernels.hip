@@ -235,7 +235,8 @@ __device__ __forceinline__ bool may_repeat16(const uint64_t (&wd)[NW], int len, 
         a[j] = (j & 1) ? (uint32_t)wd[j >> 1] : (uint32_t)(wd[j >> 1] >> 32);
         inv[j] = 16 * j + 16 <= len ? 0u : 1u;
     }
-    uint32_t acc = 0xFFFFFFFFu;
+    // four running minima (by aligned position j & 3): four independent v_min3 chains
+    uint32_t acc4[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
 #pragma unroll
     for (int wi = 0; wi < NW; ++wi) {
         const uint32_t h0 = (uint32_t)(wd[wi] >> 32), h1 = (uint32_t)wd[wi];
@@ -265,18 +266,18 @@ __device__ __forceinline__ bool may_repeat16(const uint64_t (&wd)[NW], int len, 
                     if (!(32 * wi + t0 + u > 16 * j)) continue;
                     const uint32_t x = (v[u] ^ a[j]) + inv[j];
                     if (has) {
-                        acc = min(min(acc, pend), x);
+                        acc4[j & 3] = min(min(acc4[j & 3], pend), x);
                         has = false;
                     } else {
                         pend = x;
                         has = true;
                     }
                 }
-                if (has) acc = min(acc, pend);
+                if (has) acc4[j & 3] = min(acc4[j & 3], pend);
             }
         }
     }
-    return acc == 0;
+    return min(min(acc4[0], acc4[1]), min(acc4[2], acc4[3])) == 0;
 }
 
 // R rows per workgroup, a lane per row (R threads). DIRECT: each lane stores its row's
@@ -395,6 +396,7 @@ __global__ __launch_bounds__(R, R == 64 ? 3 : 1) void k_pack_reads(const int64_t
             for (int w = 0; w < B - 1; ++w) {
                 uint64_t acc = 0;
                 if (w < used) {
+                    uint32_t by[8];
                     // the word's 32 bytes: 9 staged dwords from (rel >> 2) + 8 w (read past the
                     // row's end into the slack of in32: masked below)
                     uint32_t t9[9];
@@ -417,9 +419,13 @@ __global__ __launch_bounds__(R, R == 64 ? 3 : 1) void k_pack_reads(const int64_t
                         const uint32_t inmask = left >= 4 ? 0xFFFFFFFFu : left <= 0 ? 0u : (1u << (8 * left)) - 1u;
                         x = (x & inmask) | (0x41414141u & ~inmask);  // past the end: 'A' (code 0, valid)
                         uint32_t nb;
-                        acc = (acc << 8) | pack4(x, nb);
+                        by[d] = pack4(x, nb);
                         bad |= nb;
                     }
+                    // the 8 bytes into the word as a tree (not a chain of 64-bit shifts)
+                    const uint32_t hi = (((by[0] << 8) | by[1]) << 16) | ((by[2] << 8) | by[3]);
+                    const uint32_t lo = (((by[4] << 8) | by[5]) << 16) | ((by[6] << 8) | by[7]);
+                    acc = ((uint64_t)hi << 32) | lo;
                 }
                 if constexpr (B == 8) {
                     switch (w) {  // static register indices in a rolled loop (w is uniform)
@@ -1480,6 +1486,203 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
     }
 }
 
+// The minimizer filter (below): off unless ROGTK_KMER_MZ=1 or rogtk_kmer_set_filter(1)
+std::atomic<int> g_kmer_mz{-1};
+inline bool kmer_mz_on() {
+    int v = g_kmer_mz.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char* e = getenv("ROGTK_KMER_MZ");
+        v = e && e[0] == '1' ? 1 : 0;
+        g_kmer_mz.store(v, std::memory_order_relaxed);
+    }
+    return v == 1;
+}
+
+// Round 4: the minimizer filter, a group-level certificate for class-3 groups whose rows
+// are all certified (no K-mer twice in a row, K in {31, 32}; counting is stranded). A
+// K-mer X counted min_cov times then occurs in min_cov distinct rows. Its minimizer m(X),
+// the smallest of its W = K - 15 16-mers (2-bit codes compared as u32: lexicographic
+// order), depends on X alone: every row that holds X has a window whose minimizer is
+// m(X). Per group, each row adds its windows' minimizers to a count (once per run of
+// consecutive windows that share one; one that returns after a gap is added again, which
+// only over-counts): if no count reaches min_cov, no K-mer does, and the group has nothing
+// valid (class kClsEmpty, as the row certificate gives it). About 13 distinct minimizers
+// per 150-bp row are counted instead of 119 k-mer inserts.
+// A lane per row (64 rows of the group at a time): its 16-mers in blocks of 16 positions
+// (one 32-bit half-word each), window minima as the suffix minimum of the first position's
+// block and the prefix minimum of the last position's block (van Herk / Gil-Werman), the
+// row's distinct minimizers appended to its own list in LDS; then the lists are counted in
+// a 512-slot table per wave. A group that reaches min_cov, or a row with more than kMzList
+// minimizers, or more than kMzClaim distinct ones in the group, keeps its class.
+constexpr int kMzWaves = 4;    // waves per workgroup, a group per wave at a time
+constexpr int kMzSlots = 512;  // per wave: u32 key (the minimizer) and u32 count; + the all-ones key's slot
+constexpr int kMzClaim = 384;  // distinct minimizers before the wave gives up (<= 448 claimed: never full)
+constexpr int kMzList = 29;    // a row's distinct minimizers (its list in LDS; odd: lanes spread over banks)
+__global__ __launch_bounds__(64 * kMzWaves) void k_minimizer_filter(const GroupDesc* __restrict__ gdesc, int64_t G,
+                                                                     uint8_t* __restrict__ gsmall, int K,
+                                                                     int64_t min_cov,
+                                                                     const int32_t* __restrict__ row_len, int stride,
+                                                                     const uint64_t* __restrict__ packed,
+                                                                     const unsigned long long* __restrict__ gstat) {
+    constexpr int NW = 7;       // B = 8 blocks: at most 7 base words (224 bases) per row
+    constexpr int NH = 2 * NW;  // 32-bit half-words: 16 positions each
+    __shared__ uint32_t s_key[kMzWaves][kMzSlots + 1];
+    __shared__ uint32_t s_cnt[kMzWaves][kMzSlots + 1];
+    __shared__ uint32_t s_list[kMzWaves][64 * kMzList];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t* const key = s_key[wv];
+    uint32_t* const cnt = s_cnt[wv];
+    uint32_t* const lst = s_list[wv] + lane * kMzList;
+    constexpr uint32_t kNone = 0xFFFFFFFFu;  // the empty key
+    for (int i = lane; i <= kMzSlots; i += 64) {
+        key[i] = kNone;
+        cnt[i] = 0;
+    }
+    const bool w17 = K == 32;  // windows of 17 16-mers (K = 32) or 16 (K = 31)
+    const uint32_t hit = (uint32_t)min_cov;
+    // the groups this wave filters, in order: class-3 groups whose rows are all certified
+    // (chunks of 64 ids, one ballot each); the next group's first 64 rows (length and
+    // words, a row per lane) are loaded into registers while the current one is filtered
+    const int64_t n_chunks = (G + 63) >> 6;
+    int64_t ch = (int64_t)blockIdx.x * kMzWaves + wv;
+    const int64_t ch_step = (int64_t)gridDim.x * kMzWaves;
+    uint64_t own = 0;
+    auto next_group = [&](int64_t& g) {  // wave-uniform; false when the wave's chunks are done
+        while (!own) {
+            if (ch >= n_chunks) return false;
+            const int64_t gl = (ch << 6) + lane;
+            const uint8_t c = gl < G ? gsmall[gl] : 0;
+            own = __ballot(c == 3 && gstat[5 * gl + 2] == 0);
+            if (!own) ch += ch_step;
+        }
+        g = (ch << 6) + __ffsll((unsigned long long)own) - 1;
+        own &= own - 1;
+        if (!own) ch += ch_step;
+        return true;
+    };
+    uint64_t nw_[NW];
+    int nlen = 0;
+    auto load = [&](const GroupDesc& e, int r0, uint64_t (&w)[NW], int& len) {
+        const int r = r0 + lane;
+        len = r < e.nrows ? row_len[e.r0 + r] : 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) w[i] = r < e.nrows && i < stride ? packed[e.w0 + (int64_t)r * stride + i] : 0ull;
+    };
+    GroupDesc d{0, 0, 0, 0}, dn{0, 0, 0, 0};
+    int64_t g = 0, gn = 0;
+    bool have = next_group(g);
+    if (have) {
+        d = gdesc[g];
+        load(d, 0, nw_, nlen);
+    }
+    while (have) {
+        uint64_t cw[NW];
+#pragma unroll
+        for (int i = 0; i < NW; ++i) cw[i] = nw_[i];
+        int clen = nlen;
+        const bool have_n = next_group(gn);
+        if (have_n) {
+            dn = gdesc[gn];
+            load(dn, 0, nw_, nlen);  // in flight while this group is filtered
+        }
+        bool stop = false;  // wave-uniform: a count reached min_cov, or too many minimizers
+        uint32_t claimed = 0;
+        for (int r0 = 0; r0 < d.nrows && !stop; r0 += 64) {
+            if (r0) load(d, r0, cw, clen);  // groups of more than 64 rows (rare)
+            // this lane's row: its distinct window minimizers into its list
+            const int nwin = clen >= K ? clen - K + 1 : 0;
+            uint32_t hw[NH];
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                hw[2 * i] = (uint32_t)(cw[i] >> 32);
+                hw[2 * i + 1] = (uint32_t)cw[i];
+            }
+            int nwmax = nwin;  // wave-uniform bound on the windows
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) nwmax = max(nwmax, __shfl_xor(nwmax, m, 64));
+            nwmax = __builtin_amdgcn_readfirstlane(nwmax);
+            int n = 0;
+            uint32_t mprev = 0;
+            // block b: windows 16 b .. 16 b + 15, from the suffix minima of block b's
+            // 16-mers and the prefix minima of block b + 1's
+            uint32_t suf[16];
+            suf[0] = hw[0];
+#pragma unroll
+            for (int t = 1; t < 16; ++t) suf[t] = __builtin_amdgcn_alignbit(hw[0], hw[1], 32 - 2 * t);
+#pragma unroll
+            for (int t = 14; t >= 0; --t) suf[t] = min(suf[t], suf[t + 1]);
+#pragma unroll
+            for (int b = 0; b + 1 < NH; ++b) {
+                if (16 * b >= nwmax) break;  // uniform
+                const uint32_t lo = hw[b + 1], hi2 = b + 2 < NH ? hw[b + 2] : 0u;
+                uint32_t pre[16], nsuf[16];
+                pre[0] = lo;
+#pragma unroll
+                for (int t = 1; t < 16; ++t) pre[t] = __builtin_amdgcn_alignbit(lo, hi2, 32 - 2 * t);
+#pragma unroll
+                for (int t = 0; t < 16; ++t) nsuf[t] = pre[t];
+#pragma unroll
+                for (int t = 1; t < 16; ++t) pre[t] = min(pre[t], pre[t - 1]);
+#pragma unroll
+                for (int t = 14; t >= 0; --t) nsuf[t] = min(nsuf[t], nsuf[t + 1]);
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    const int p = 16 * b + t;
+                    const uint32_t m = w17 ? min(suf[t], pre[t]) : t ? min(suf[t], pre[t - 1]) : suf[0];
+                    const bool f = p < nwin && (p == 0 || m != mprev);
+                    if (f) lst[min(n, kMzList - 1)] = m;
+                    n += f;
+                    mprev = m;
+                }
+#pragma unroll
+                for (int t = 0; t < 16; ++t) suf[t] = nsuf[t];
+            }
+            // count the lists in the group's table
+            int nmax = n;
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) nmax = max(nmax, __shfl_xor(nmax, m, 64));
+            nmax = __builtin_amdgcn_readfirstlane(nmax);
+            if (nmax > kMzList) {  // a row with too many minimizers: keep the class
+                stop = true;
+                break;
+            }
+            for (int k = 0; k < nmax; ++k) {
+                bool reached = false, fresh = false;
+                if (k < n) {
+                    const uint32_t m = lst[k];
+                    uint32_t slot = (uint32_t)kMzSlots;  // the all-ones key's own slot
+                    if (m != kNone) {
+                        slot = (m * 0x9E3779B1u) >> 23;  // 512 slots
+                        while (true) {
+                            const uint32_t prev = atomicCAS(&key[slot], kNone, m);
+                            if (prev == kNone || prev == m) {
+                                fresh = prev == kNone;
+                                break;
+                            }
+                            slot = (slot + 1) & (kMzSlots - 1);
+                        }
+                    }
+                    reached = atomicAdd(&cnt[slot], 1u) + 1u >= hit;
+                }
+                claimed += (uint32_t)__popcll(__ballot(fresh));
+                if (__ballot(reached) || claimed > (uint32_t)kMzClaim) {
+                    stop = true;
+                    break;
+                }
+            }
+        }
+        if (!stop && lane == 0) gsmall[g] = kClsEmpty;
+        for (int i = lane; i <= kMzSlots; i += 64) {  // the table for the next group
+            key[i] = kNone;
+            cnt[i] = 0;
+        }
+        __builtin_amdgcn_wave_barrier();
+        have = have_n;
+        g = gn;
+        d = dn;
+    }
+}
+
 // rogtk_kmer_path_stats: groups of effective k K on the LDS path (gsmall != 0 after the
 // LDS kernels) and on the global path, counted on the device (no G-byte copy to the host)
 __global__ __launch_bounds__(kBlock) void k_path_counts(const uint8_t* __restrict__ gk, int K, int64_t G,
@@ -1791,6 +1994,15 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
         hipLaunchKernelGGL(k_tail_sum, dim3(1), dim3(64), 0, s, co, in.cap_fill, G, co + G);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
+    if (lds && stride && gstat && kmer_cert_on() && kmer_mz_on() && (K == 31 || K == 32) && min_cov >= 2) {
+        ProfScope prof(K_KMER_MZ, s, true);
+        const int64_t chunks = (G + 63) / 64;
+        hipExtLaunchKernelGGL(k_minimizer_filter, dim3((unsigned)std::min<int64_t>((chunks + kMzWaves - 1) / kMzWaves, 4096)),
+                              dim3(64 * kMzWaves), 0, s, prof.start(), prof.stop(), 0, c->gdesc.as<GroupDesc>(), G,
+                              c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(), stride,
+                              c->packed.as<uint64_t>(), gstat);
+        ROGTK_HIP_CHECK(hipGetLastError());
+    }
     if (lds && kmer_insert_v() == 2) {
         ProfScope prof(K_KMER_LDS, s, true);
         hipExtLaunchKernelGGL((k_kmer_lds<3, kLdsBlock, 2>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)),
@@ -1956,6 +2168,11 @@ int rogtk_kmer_set_path(int lds_small_groups) {
     KmerCtx* c = nullptr;
     if (int rc = kmer_ctx(&c)) return rc;
     c->lds_path = lds_small_groups != 0;
+    return ROGTK_OK;
+}
+
+int rogtk_kmer_set_filter(int minimizer_filter) {
+    g_kmer_mz.store(minimizer_filter ? 1 : 0, std::memory_order_relaxed);
     return ROGTK_OK;
 }
 

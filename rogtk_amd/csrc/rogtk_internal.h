@@ -54,6 +54,7 @@ enum KernelId {
     K_ROW_GATHER,
     K_KMER_LDS,
     K_RESOLVE,  // the whole resolve chain of one batch (first launch to last, its stream)
+    K_KMER_MZ,  // the minimizer filter of the k-mer spectra (round 4)
     K_COUNT_
 };
 extern const char* const kKernelNames[K_COUNT_];

@@ -88,11 +88,12 @@ def _concat(calls, G):
             "group_offsets": np.concatenate(eo), "stats": np.concatenate(st)}
 
 
-@pytest.mark.parametrize("min_cov,batch_rows,packed", [(MINCOV, 10_000_000, "auto"), (2, 200_000, "auto"),
-                                                        (MINCOV, 10_000_000, None)])
-def test_c3_path_1m_vs_oracle(min_cov, batch_rows, packed):
+@pytest.mark.parametrize("min_cov,batch_rows,packed,filt", [(MINCOV, 10_000_000, "auto", 0), (2, 200_000, "auto", 0),
+                                                             (MINCOV, 10_000_000, None, 0),
+                                                             (MINCOV, 10_000_000, "auto", 1), (3, 200_000, "auto", 1)])
+def test_c3_path_1m_vs_oracle(min_cov, batch_rows, packed, filt):
     """packed "auto": rows staged from the 2-bit block column (rogtk_pack_reads); None: from
-    the ASCII bytes."""
+    the ASCII bytes. filt: with the minimizer filter (rogtk_kmer_set_filter)."""
     from oracle import pyoracle as P
     from rogtk_amd import _lib
     from rogtk_amd import synth
@@ -104,7 +105,11 @@ def test_c3_path_1m_vs_oracle(min_cov, batch_rows, packed):
     reads_h = synth.reads(n, RL).copy()
     _inject(reads_h, codes_h, rng)
     _lib.call("rogtk_kmer_set_path", 1)
-    rows, go, G, calls = _run_c3(codes_h, reads_h, min_cov, batch_rows, packed)
+    _lib.call("rogtk_kmer_set_filter", filt)
+    try:
+        rows, go, G, calls = _run_c3(codes_h, reads_h, min_cov, batch_rows, packed)
+    finally:
+        _lib.call("rogtk_kmer_set_filter", 0)
     ps = (ctypes.c_int64 * 2)()
     _lib.call("rogtk_kmer_path_stats", ps)
     order = np.argsort(codes_h, kind="stable")
@@ -402,3 +407,87 @@ def test_repeat_certificate_spectra(mc):
         if mc >= 3:
             tandem = [g for g in range(0, 600, 5) if go[g + 1] - go[g] < mc]
             assert sum(int(ref["group_offsets"][g + 1] - ref["group_offsets"][g]) > 0 for g in tandem) > 0
+
+
+@pytest.mark.parametrize("mc", [2, 5, 20])
+def test_minimizer_filter_spectra(mc):
+    """The minimizer filter (kmer_kernels.hip k_minimizer_filter, rogtk_kmer_set_filter) on groups with min_coverage
+    rows or more, all certified: mixtures of templates each below min_coverage copies
+    (nothing valid: the filter empties them), one template at min_coverage copies or more
+    read at shifted offsets with errors (valid k-mers: kept), and uncertified tandem /
+    poly-A rows (left alone); k = 17 and 31 (k_eff 32). Spectra and stats identical to the
+    oracle; the certified-empty count covers the mixtures."""
+    import ctypes
+
+    import torch
+
+    from oracle import pyoracle as P
+    from rogtk_amd import _lib
+    from rogtk_amd import device as D
+
+    rng = np.random.default_rng(300 + mc)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    rand = lambda n: bytearray(acgt[rng.integers(0, 4, n)].tobytes())
+    items, go, mixtures, kept = [], [0], [], []
+
+    def read(tpl, L, errs):
+        o = int(rng.integers(0, len(tpl) - L + 1))
+        x = bytearray(tpl[o:o + L])
+        for _ in range(errs):
+            x[int(rng.integers(L))] = int(acgt[rng.integers(0, 4)])
+        return bytes(x)
+
+    for g in range(400):
+        kind = g % 4
+        rows = []
+        if kind == 0:  # mixture: every template below min_coverage copies, mc rows or more
+            per = max(1, mc - 1)
+            while len(rows) < mc + int(rng.integers(0, 2 * mc + 2)):
+                tpl = rand(180)
+                rows += [read(tpl, int(rng.integers(90, 151)), int(rng.integers(0, 2)))
+                         for _ in range(int(rng.integers(1, per + 1)))]
+            mixtures.append(g)
+        elif kind == 1:  # one template at min_coverage copies or more, shifted, with errors
+            tpl = rand(200)
+            rows = [read(tpl, 150, int(rng.integers(0, 3))) for _ in range(mc + int(rng.integers(0, 6)))]
+            rows += [read(rand(160), 150, 0) for _ in range(int(rng.integers(0, 4)))]
+            kept.append(g)
+        elif kind == 2:  # uncertified rows: a tandem template
+            u = int(rng.integers(20, 50))
+            tpl = bytearray((bytes(rand(u)) * 10)[:200])
+            rows = [read(tpl, 150, 0) for _ in range(mc + int(rng.integers(0, 3)))]
+        else:  # a poly-A tail in one row of a mixture
+            rows = [read(rand(170), 150, 0) for _ in range(mc + 1)]
+            rows[0] = rows[0][:110] + b"A" * 40
+        items += rows
+        go.append(len(items))
+    lens = np.array([len(x) for x in items], np.int64)
+    off = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)])).cuda()
+    vals = torch.from_numpy(np.frombuffer(b"".join(items), np.uint8).copy()).cuda()
+    pk = D.PackedReads(off, vals)
+    gsel = torch.tensor(go, dtype=torch.int64).cuda()
+    col = P.StrCol.from_list(items)
+    _lib.call("rogtk_kmer_set_path", 1)
+    for k, filt in ((17, 1), (31, 1), (17, 0)):
+        ref = P.kmer_spectrum(col, k, mc, False, np.array(go), threads=THREADS)
+        _lib.call("rogtk_kmer_set_filter", filt)
+        try:
+            got = D.kmer_spectrum_blocks(pk, off, vals, gsel, k, mc, int(np.clip(lens - 3, 0, None).sum()))
+            torch.cuda.synchronize()
+        finally:
+            _lib.call("rogtk_kmer_set_filter", 0)
+        cg = ctypes.c_int64(0)
+        _lib.call("rogtk_kmer_certified_groups", ctypes.byref(cg))
+        km = got["kmers"].cpu().numpy().view(np.uint64)
+        assert np.array_equal(got["entry_offsets"].cpu().numpy(), ref["group_offsets"]), k
+        assert np.array_equal(got["stats"].cpu().numpy(), ref["stats"]), k
+        assert np.array_equal(km[:, 0], ref["kmer_hi"]) and np.array_equal(km[:, 1], ref["kmer_lo"]), k
+        assert np.array_equal(got["exts"].cpu().numpy(), ref["exts"]), k
+        assert np.array_equal(got["counts"].cpu().numpy().view(np.uint16), ref["counts"]), k
+        eo = ref["group_offsets"]
+        assert all(eo[g + 1] == eo[g] for g in mixtures)  # nothing valid in a mixture
+        assert sum(eo[g + 1] > eo[g] for g in kept) > len(kept) // 2  # the kept groups do have output
+        if filt:
+            assert cg.value >= len(mixtures), (cg.value, len(mixtures))  # the filter emptied them
+        else:
+            assert cg.value < len(mixtures) // 2, cg.value  # (the row certificate alone cannot)
