@@ -367,7 +367,7 @@ int rogtk_kmer_capacity(const void* offsets, int offset_width, int64_t n_rows, i
  * workgroup per group); 0 sends every group through the global radix-sort path.
  * Results are identical; tests use this to cover both paths. */
 int rogtk_kmer_set_path(int lds_small_groups);
-/* The minimizer filter (round 4; process-wide, default off, or ROGTK_KMER_MZ=1): on the
+/* The minimizer filter (round 4; process-wide, default on, ROGTK_KMER_MZ=0 turns it off): on the
  * block path, class-3 groups whose rows all carry the repeat certificate are checked for a
  * window minimizer shared by min_coverage rows; a group without one has no valid k-mer and
  * skips the LDS kernels (kmer_kernels.hip k_minimizer_filter). Results are identical. */

@@ -1486,13 +1486,13 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
     }
 }
 
-// The minimizer filter (below): off unless ROGTK_KMER_MZ=1 or rogtk_kmer_set_filter(1)
+// The minimizer filter (below): on unless ROGTK_KMER_MZ=0 or rogtk_kmer_set_filter(0)
 std::atomic<int> g_kmer_mz{-1};
 inline bool kmer_mz_on() {
     int v = g_kmer_mz.load(std::memory_order_relaxed);
     if (v < 0) {
         const char* e = getenv("ROGTK_KMER_MZ");
-        v = e && e[0] == '1' ? 1 : 0;
+        v = e && e[0] == '0' ? 0 : 1;
         g_kmer_mz.store(v, std::memory_order_relaxed);
     }
     return v == 1;
@@ -1517,7 +1517,7 @@ inline bool kmer_mz_on() {
 constexpr int kMzWaves = 4;    // waves per workgroup, a group per wave at a time
 constexpr int kMzSlots = 512;  // per wave: u32 key (the minimizer) and u32 count; + the all-ones key's slot
 constexpr int kMzClaim = 384;  // distinct minimizers before the wave gives up (<= 448 claimed: never full)
-constexpr int kMzList = 29;    // a row's distinct minimizers (its list in LDS; odd: lanes spread over banks)
+constexpr int kMzList = 28;    // a row's distinct minimizers (its list in LDS, + a spare slot: 29, odd, so lanes spread over banks)
 __global__ __launch_bounds__(64 * kMzWaves) void k_minimizer_filter(const GroupDesc* __restrict__ gdesc, int64_t G,
                                                                      uint8_t* __restrict__ gsmall, int K,
                                                                      int64_t min_cov,
@@ -1528,11 +1528,11 @@ __global__ __launch_bounds__(64 * kMzWaves) void k_minimizer_filter(const GroupD
     constexpr int NH = 2 * NW;  // 32-bit half-words: 16 positions each
     __shared__ uint32_t s_key[kMzWaves][kMzSlots + 1];
     __shared__ uint32_t s_cnt[kMzWaves][kMzSlots + 1];
-    __shared__ uint32_t s_list[kMzWaves][64 * kMzList];
+    __shared__ uint32_t s_list[kMzWaves][64 * (kMzList + 1)];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t* const key = s_key[wv];
     uint32_t* const cnt = s_cnt[wv];
-    uint32_t* const lst = s_list[wv] + lane * kMzList;
+    uint32_t* const lst = s_list[wv] + lane * (kMzList + 1);
     constexpr uint32_t kNone = 0xFFFFFFFFu;  // the empty key
     for (int i = lane; i <= kMzSlots; i += 64) {
         key[i] = kNone;
@@ -1540,24 +1540,56 @@ __global__ __launch_bounds__(64 * kMzWaves) void k_minimizer_filter(const GroupD
     }
     const bool w17 = K == 32;  // windows of 17 16-mers (K = 32) or 16 (K = 31)
     const uint32_t hit = (uint32_t)min_cov;
-    // the groups this wave filters, in order: class-3 groups whose rows are all certified
-    // (chunks of 64 ids, one ballot each); the next group's first 64 rows (length and
-    // words, a row per lane) are loaded into registers while the current one is filtered
+    // the groups this wave filters, in order: class-3 groups whose rows are all certified,
+    // in chunks of 64 ids: a chunk's classes, certificate counts and descriptors are one
+    // load per lane, issued a chunk ahead; the next group's first 64 rows (length and
+    // words, a row per lane) are loaded into registers while the current one is filtered,
+    // its descriptor read from the chunk's lanes (no dependent load between groups)
     const int64_t n_chunks = (G + 63) >> 6;
     int64_t ch = (int64_t)blockIdx.x * kMzWaves + wv;
     const int64_t ch_step = (int64_t)gridDim.x * kMzWaves;
-    uint64_t own = 0;
-    auto next_group = [&](int64_t& g) {  // wave-uniform; false when the wave's chunks are done
-        while (!own) {
-            if (ch >= n_chunks) return false;
-            const int64_t gl = (ch << 6) + lane;
-            const uint8_t c = gl < G ? gsmall[gl] : 0;
-            own = __ballot(c == 3 && gstat[5 * gl + 2] == 0);
-            if (!own) ch += ch_step;
+    struct Chunk {
+        bool cand;
+        int64_t r0, w0;
+        int32_t nrows, nwords;
+    };
+    auto chunk_load = [&](int64_t c) {
+        Chunk k{false, 0, 0, 0, 0};
+        const int64_t gl = (c << 6) + lane;
+        if (c < n_chunks && gl < G) {
+            const uint8_t cls = gsmall[gl];
+            const unsigned long long unc = gstat[5 * gl + 2];
+            const GroupDesc e = gdesc[gl];
+            k.cand = cls == 3 && unc == 0;
+            k.r0 = e.r0;
+            k.w0 = e.w0;
+            k.nrows = e.nrows;
+            k.nwords = e.nwords;
         }
-        g = (ch << 6) + __ffsll((unsigned long long)own) - 1;
+        return k;
+    };
+    auto rl64 = [](int64_t v, int i) {
+        return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), i) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)v, i));
+    };
+    Chunk cur = chunk_load(ch), nxt = chunk_load(ch + ch_step);
+    uint64_t own = __ballot(cur.cand);
+    int64_t cur_base = ch << 6;
+    // the next candidate group (wave-uniform); false when the wave's chunks are done
+    auto next_group = [&](int64_t& g, GroupDesc& e) {
+        while (!own) {
+            ch += ch_step;
+            if (ch >= n_chunks) return false;
+            cur = nxt;
+            cur_base = ch << 6;
+            nxt = chunk_load(ch + ch_step);
+            own = __ballot(cur.cand);
+        }
+        const int i = __ffsll((unsigned long long)own) - 1;
         own &= own - 1;
-        if (!own) ch += ch_step;
+        g = cur_base + i;
+        e = GroupDesc{rl64(cur.r0, i), rl64(cur.w0, i), __builtin_amdgcn_readlane(cur.nrows, i),
+                      __builtin_amdgcn_readlane(cur.nwords, i)};
         return true;
     };
     uint64_t nw_[NW];
@@ -1570,21 +1602,15 @@ __global__ __launch_bounds__(64 * kMzWaves) void k_minimizer_filter(const GroupD
     };
     GroupDesc d{0, 0, 0, 0}, dn{0, 0, 0, 0};
     int64_t g = 0, gn = 0;
-    bool have = next_group(g);
-    if (have) {
-        d = gdesc[g];
-        load(d, 0, nw_, nlen);
-    }
+    bool have = ch < n_chunks && next_group(g, d);
+    if (have) load(d, 0, nw_, nlen);
     while (have) {
         uint64_t cw[NW];
 #pragma unroll
         for (int i = 0; i < NW; ++i) cw[i] = nw_[i];
         int clen = nlen;
-        const bool have_n = next_group(gn);
-        if (have_n) {
-            dn = gdesc[gn];
-            load(dn, 0, nw_, nlen);  // in flight while this group is filtered
-        }
+        const bool have_n = next_group(gn, dn);
+        if (have_n) load(dn, 0, nw_, nlen);  // in flight while this group is filtered
         bool stop = false;  // wave-uniform: a count reached min_cov, or too many minimizers
         uint32_t claimed = 0;
         for (int r0 = 0; r0 < d.nrows && !stop; r0 += 64) {
@@ -1630,7 +1656,7 @@ __global__ __launch_bounds__(64 * kMzWaves) void k_minimizer_filter(const GroupD
                     const int p = 16 * b + t;
                     const uint32_t m = w17 ? min(suf[t], pre[t]) : t ? min(suf[t], pre[t - 1]) : suf[0];
                     const bool f = p < nwin && (p == 0 || m != mprev);
-                    if (f) lst[min(n, kMzList - 1)] = m;
+                    lst[min(n, kMzList)] = m;  // kept only when f (n moves on; n = kMzList: the spare slot): no branch
                     n += f;
                     mprev = m;
                 }

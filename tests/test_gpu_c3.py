@@ -109,7 +109,7 @@ def test_c3_path_1m_vs_oracle(min_cov, batch_rows, packed, filt):
     try:
         rows, go, G, calls = _run_c3(codes_h, reads_h, min_cov, batch_rows, packed)
     finally:
-        _lib.call("rogtk_kmer_set_filter", 0)
+        _lib.call("rogtk_kmer_set_filter", 1)
     ps = (ctypes.c_int64 * 2)()
     _lib.call("rogtk_kmer_path_stats", ps)
     order = np.argsort(codes_h, kind="stable")
@@ -475,7 +475,7 @@ def test_minimizer_filter_spectra(mc):
             got = D.kmer_spectrum_blocks(pk, off, vals, gsel, k, mc, int(np.clip(lens - 3, 0, None).sum()))
             torch.cuda.synchronize()
         finally:
-            _lib.call("rogtk_kmer_set_filter", 0)
+            _lib.call("rogtk_kmer_set_filter", 1)
         cg = ctypes.c_int64(0)
         _lib.call("rogtk_kmer_certified_groups", ctypes.byref(cg))
         km = got["kmers"].cpu().numpy().view(np.uint64)

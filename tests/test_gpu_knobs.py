@@ -199,12 +199,12 @@ def _kmer_column(tmp_path):
 
 def test_kmer_insert_variant_identical(tmp_path):
     """The class-3 LDS kernel's V = 1 and V = 2 insert loops (ROGTK_KMER_INSERT=1 / 2), and
-    the spectra without the repeat certificate (ROGTK_KMER_CERT=0) or with the minimizer
-    filter (ROGTK_KMER_MZ=1), are the default's bit for bit, over min_coverage 1 and 3.""" 
+    the spectra without the repeat certificate (ROGTK_KMER_CERT=0) or without the minimizer
+    filter (ROGTK_KMER_MZ=0), are the default's bit for bit, over min_coverage 1 and 3.""" 
     src = _kmer_column(tmp_path)
     outs = []
     for i, knobs in enumerate(({}, {"ROGTK_KMER_INSERT": "1"}, {"ROGTK_KMER_INSERT": "2"}, {"ROGTK_KMER_CERT": "0"},
-                               {"ROGTK_KMER_MZ": "1"})):
+                               {"ROGTK_KMER_MZ": "0"})):
         path = str(tmp_path / f"k{i}.npz")
         env = dict(os.environ, **knobs)
         r = subprocess.run([sys.executable, "-c", KMER_CHILD.format(root=ROOT, src=src, path=path)], env=env,
