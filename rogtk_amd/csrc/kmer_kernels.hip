@@ -1726,10 +1726,20 @@ __global__ __launch_bounds__(kBlock) void k_path_counts(const uint8_t* __restric
         glob += __shfl_xor(glob, m);
         cert += __shfl_xor(cert, m);
     }
+    // one atomic per workgroup and counter (per wave, 3 x 16K atomics on the same three
+    // words serialised at L2: 0.4 ms at 8.17M groups)
+    __shared__ unsigned long long s3[kWavesPerBlock][3];
+    const int wv = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
-        if (lds) atomicAdd(out2, lds);
-        if (glob) atomicAdd(out2 + 1, glob);
-        if (cert) atomicAdd(out2 + 2, cert);  // out2[2]: of the LDS ones, empty by the certificate
+        s3[wv][0] = lds;
+        s3[wv][1] = glob;
+        s3[wv][2] = cert;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        unsigned long long v = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) v += s3[w][threadIdx.x];
+        if (v) atomicAdd(out2 + threadIdx.x, v);  // out2[2]: of the LDS ones, empty by a certificate
     }
 }
 
@@ -1820,7 +1830,13 @@ __global__ __launch_bounds__(kBlock) void k_key_max(const uint32_t* __restrict__
         m = max(m, k[i]);
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
-    if ((threadIdx.x & 63) == 0 && m) atomicMax(mx, m);
+    __shared__ uint32_t s_m[kWavesPerBlock];  // one atomic per workgroup (not per wave)
+    if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kWavesPerBlock; ++w) m = max(m, s_m[w]);
+        if (m) atomicMax(mx, m);
+    }
 }
 
 // the group offsets (an exclusive scan of the heads: a head's group = gid; row i's group =
@@ -2063,24 +2079,30 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
                            c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
                            c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
                            c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
-        hipLaunchKernelGGL(k_drop_small_rows, dim3(grid_for(n_rows)), dim3(kBlock), 0, s, c->row_group.as<uint32_t>(),
-                           c->gsmall.as<uint8_t>(), n_rows, c->row_obs.as<int64_t>());
-        ROGTK_HIP_CHECK(hipGetLastError());
     }
-    if (int rc = cub_exsum_i64(c, c->row_obs.as<int64_t>(), c->obs_off.as<int64_t>(), n_rows, s)) return rc;
+    // the groups per path first: with none on the global path (the usual C3 call, every
+    // group in LDS or certified empty) its row drop and observation scan are skipped
     if (int rc = c->scal.ensure(64)) return rc;
     ROGTK_HIP_CHECK(hipMemsetAsync(c->scal.p, 0, 24, s));
-    hipLaunchKernelGGL(k_path_counts, dim3(grid_for(G, 4096)), dim3(kBlock), 0, s, in.gk, K, G,
+    hipLaunchKernelGGL(k_path_counts, dim3(grid_for(G, 1024)), dim3(kBlock), 0, s, in.gk, K, G,
                        (c->lds_path && K <= 32) ? c->gsmall.as<uint8_t>() : nullptr,
                        c->scal.as<unsigned long long>());
     int64_t last[5] = {0, 0, 0, 0, 0};
-    ROGTK_HIP_CHECK(hipMemcpyAsync(&last[0], c->obs_off.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
-    ROGTK_HIP_CHECK(hipMemcpyAsync(&last[1], c->row_obs.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
     ROGTK_HIP_CHECK(hipMemcpyAsync(&last[2], c->scal.p, 24, hipMemcpyDeviceToHost, s));
     ROGTK_HIP_CHECK(hipStreamSynchronize(s));
     c->last_lds_groups += last[2];
     c->last_global_groups += last[3];
     c->last_cert_groups += last[4];
+    if (last[3] == 0) return ROGTK_OK;
+    if (lds) {
+        hipLaunchKernelGGL(k_drop_small_rows, dim3(grid_for(n_rows)), dim3(kBlock), 0, s, c->row_group.as<uint32_t>(),
+                           c->gsmall.as<uint8_t>(), n_rows, c->row_obs.as<int64_t>());
+        ROGTK_HIP_CHECK(hipGetLastError());
+    }
+    if (int rc = cub_exsum_i64(c, c->row_obs.as<int64_t>(), c->obs_off.as<int64_t>(), n_rows, s)) return rc;
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&last[0], c->obs_off.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&last[1], c->row_obs.as<int64_t>() + n_rows - 1, 8, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
     const int64_t T = last[0] + last[1];
     if (T == 0) return ROGTK_OK;
     ROGTK_REQUIRE(T <= kMaxObsPerLaunch, ROGTK_E_UNSUPPORTED,
@@ -2405,7 +2427,7 @@ int rogtk_group_by_key(const uint32_t* keys, int64_t n, int64_t* rows_out, int64
     uint32_t* const iota = c->obs_off.as<uint32_t>();
     uint32_t* const rows32 = iota + n;
     ROGTK_HIP_CHECK(hipMemsetAsync(c->scal.p, 0, 4, s));
-    hipLaunchKernelGGL(k_key_max, dim3(g), dim3(kBlock), 0, s, keys, n, c->scal.as<uint32_t>());
+    hipLaunchKernelGGL(k_key_max, dim3(std::min(g, 1024)), dim3(kBlock), 0, s, keys, n, c->scal.as<uint32_t>());
     hipLaunchKernelGGL(k_iota32, dim3(g), dim3(kBlock), 0, s, iota, n);
     uint32_t kmax = 0;
     ROGTK_HIP_CHECK(hipMemcpyAsync(&kmax, c->scal.p, 4, hipMemcpyDeviceToHost, s));
