@@ -1508,16 +1508,30 @@ inline bool kmer_mz_on() {
 // only over-counts): if no count reaches min_cov, no K-mer does, and the group has nothing
 // valid (class kClsEmpty, as the row certificate gives it). About 13 distinct minimizers
 // per 150-bp row are counted instead of 119 k-mer inserts.
-// A lane per row (64 rows of the group at a time): its 16-mers in blocks of 16 positions
-// (one 32-bit half-word each), window minima as the suffix minimum of the first position's
-// block and the prefix minimum of the last position's block (van Herk / Gil-Werman), the
-// row's distinct minimizers appended to its own list in LDS; then the lists are counted in
-// a 512-slot table per wave. A group that reaches min_cov, or a row with more than kMzList
-// minimizers, or more than kMzClaim distinct ones in the group, keeps its class.
-constexpr int kMzWaves = 4;    // waves per workgroup, a group per wave at a time
-constexpr int kMzSlots = 512;  // per wave: u32 key (the minimizer) and u32 count; + the all-ones key's slot
-constexpr int kMzClaim = 384;  // distinct minimizers before the wave gives up (<= 448 claimed: never full)
+// A lane per row: its 16-mers in blocks of 16 positions (one 32-bit half-word each),
+// window minima as the suffix minimum of the first position's block and the prefix
+// minimum of the last position's block (van Herk / Gil-Werman), the row's distinct
+// minimizers appended to its own list in LDS; then the lists are counted in a table per
+// wave, keyed by (group, minimizer). A wave takes consecutive candidate groups together
+// (up to kMzG groups and 64 rows: ~2.5 C3 groups instead of one per wave pass); a group
+// of more than 64 rows runs alone, 64 rows at a time. A group with a count of min_cov, or
+// a row with more than kMzList minimizers, keeps its class; so does every group of a
+// batch with more than kMzClaim distinct keys.
+constexpr int kMzWaves = 2;    // waves per workgroup
+constexpr int kMzSlots = 512;  // per wave: u64 key (batch group << 32 | minimizer) and u32 count
+constexpr int kMzClaim = 384;  // distinct keys before the wave gives up (<= 448 claimed: never full)
 constexpr int kMzList = 28;    // a row's distinct minimizers (its list in LDS, + a spare slot: 29, odd, so lanes spread over banks)
+constexpr int kMzG = 8;        // groups per batch
+// a batch of groups, spread over the lanes: lane i < ng holds group i's id; each lane
+// holds its own row of the first pass (group index, row and word positions); uniform:
+// the group and row counts, and group 0's row and word bases (passes past 64 rows)
+struct MzBatch {
+    int ng, rows;
+    int64_t r00, w00;
+    int64_t g;      // lane i < ng: group i
+    int j;          // this lane's group in the batch
+    int64_t ri, wi;  // this lane's row: row_len index, first word index
+};
 __global__ __launch_bounds__(64 * kMzWaves) void k_minimizer_filter(const GroupDesc* __restrict__ gdesc, int64_t G,
                                                                      uint8_t* __restrict__ gsmall, int K,
                                                                      int64_t min_cov,
@@ -1526,35 +1540,33 @@ __global__ __launch_bounds__(64 * kMzWaves) void k_minimizer_filter(const GroupD
                                                                      const unsigned long long* __restrict__ gstat) {
     constexpr int NW = 7;       // B = 8 blocks: at most 7 base words (224 bases) per row
     constexpr int NH = 2 * NW;  // 32-bit half-words: 16 positions each
-    __shared__ uint32_t s_key[kMzWaves][kMzSlots + 1];
-    __shared__ uint32_t s_cnt[kMzWaves][kMzSlots + 1];
+    __shared__ unsigned long long s_key[kMzWaves][kMzSlots];
+    __shared__ uint32_t s_cnt[kMzWaves][kMzSlots];
     __shared__ uint32_t s_list[kMzWaves][64 * (kMzList + 1)];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t* const key = s_key[wv];
+    unsigned long long* const key = s_key[wv];
     uint32_t* const cnt = s_cnt[wv];
     uint32_t* const lst = s_list[wv] + lane * (kMzList + 1);
-    constexpr uint32_t kNone = 0xFFFFFFFFu;  // the empty key
-    for (int i = lane; i <= kMzSlots; i += 64) {
+    constexpr unsigned long long kNone = ~0ull;  // the empty key (a batch group index is < kMzG)
+    for (int i = lane; i < kMzSlots; i += 64) {
         key[i] = kNone;
         cnt[i] = 0;
     }
     const bool w17 = K == 32;  // windows of 17 16-mers (K = 32) or 16 (K = 31)
     const uint32_t hit = (uint32_t)min_cov;
-    // the groups this wave filters, in order: class-3 groups whose rows are all certified,
-    // in chunks of 64 ids: a chunk's classes, certificate counts and descriptors are one
-    // load per lane, issued a chunk ahead; the next group's first 64 rows (length and
-    // words, a row per lane) are loaded into registers while the current one is filtered,
-    // its descriptor read from the chunk's lanes (no dependent load between groups)
+    // the candidate groups, in order: class-3 groups whose rows are all certified, in
+    // chunks of 64 ids: a chunk's classes, certificate counts and descriptors are one
+    // load per lane, issued a chunk ahead
     const int64_t n_chunks = (G + 63) >> 6;
     int64_t ch = (int64_t)blockIdx.x * kMzWaves + wv;
     const int64_t ch_step = (int64_t)gridDim.x * kMzWaves;
     struct Chunk {
         bool cand;
         int64_t r0, w0;
-        int32_t nrows, nwords;
+        int32_t nrows;
     };
     auto chunk_load = [&](int64_t c) {
-        Chunk k{false, 0, 0, 0, 0};
+        Chunk k{false, 0, 0, 0};
         const int64_t gl = (c << 6) + lane;
         if (c < n_chunks && gl < G) {
             const uint8_t cls = gsmall[gl];
@@ -1564,7 +1576,6 @@ __global__ __launch_bounds__(64 * kMzWaves) void k_minimizer_filter(const GroupD
             k.r0 = e.r0;
             k.w0 = e.w0;
             k.nrows = e.nrows;
-            k.nwords = e.nwords;
         }
         return k;
     };
@@ -1573,13 +1584,18 @@ __global__ __launch_bounds__(64 * kMzWaves) void k_minimizer_filter(const GroupD
                          (uint32_t)__builtin_amdgcn_readlane((int)v, i));
     };
     Chunk cur = chunk_load(ch), nxt = chunk_load(ch + ch_step);
-    uint64_t own = __ballot(cur.cand);
+    uint64_t own = ch < n_chunks ? __ballot(cur.cand) : 0;
     int64_t cur_base = ch << 6;
+    bool done = ch >= n_chunks;
     // the next candidate group (wave-uniform); false when the wave's chunks are done
-    auto next_group = [&](int64_t& g, GroupDesc& e) {
+    auto next_group = [&](int64_t& g, int64_t& r0, int64_t& w0, int& nrows) {
         while (!own) {
+            if (done) return false;
             ch += ch_step;
-            if (ch >= n_chunks) return false;
+            if (ch >= n_chunks) {
+                done = true;
+                return false;
+            }
             cur = nxt;
             cur_base = ch << 6;
             nxt = chunk_load(ch + ch_step);
@@ -1588,33 +1604,78 @@ __global__ __launch_bounds__(64 * kMzWaves) void k_minimizer_filter(const GroupD
         const int i = __ffsll((unsigned long long)own) - 1;
         own &= own - 1;
         g = cur_base + i;
-        e = GroupDesc{rl64(cur.r0, i), rl64(cur.w0, i), __builtin_amdgcn_readlane(cur.nrows, i),
-                      __builtin_amdgcn_readlane(cur.nwords, i)};
+        r0 = rl64(cur.r0, i);
+        w0 = rl64(cur.w0, i);
+        nrows = __builtin_amdgcn_readlane(cur.nrows, i);
         return true;
     };
+    // batches: consecutive candidates while they fit 64 rows (a group of more rows alone)
+    bool have_p = false;
+    int64_t pg = 0, pr0 = 0, pw0 = 0;
+    int pn = 0;
+    auto form = [&](MzBatch& bt) {
+        bt.ng = 0;
+        bt.rows = 0;
+        bt.g = -1;
+        bt.j = 0;
+        bt.ri = bt.wi = 0;
+        while (true) {
+            if (!have_p) have_p = next_group(pg, pr0, pw0, pn);
+            if (!have_p) break;
+            if (bt.ng > 0 && (bt.ng == kMzG || bt.rows + pn > 64)) break;
+            if (bt.ng == 0) {
+                bt.r00 = pr0;
+                bt.w00 = pw0;
+            }
+            if (lane == bt.ng) bt.g = pg;
+            if (lane >= bt.rows && lane < bt.rows + pn) {
+                bt.j = bt.ng;
+                bt.ri = pr0 + (lane - bt.rows);
+                bt.wi = pw0 + (int64_t)(lane - bt.rows) * stride;
+            }
+            bt.rows += pn;
+            ++bt.ng;
+            have_p = false;
+            if (bt.rows > 64) break;  // a group of more than 64 rows: alone
+        }
+        return bt.ng > 0;
+    };
+    // this lane's row of pass p of a batch: its length and words
+    auto load = [&](const MzBatch& bt, int pass, uint64_t (&w)[NW], int& len) {
+        const bool live = 64 * pass + lane < bt.rows;
+        const int64_t ri = pass ? bt.r00 + 64 * pass + lane : bt.ri;
+        const int64_t wi = pass ? bt.w00 + (int64_t)(64 * pass + lane) * stride : bt.wi;
+        len = live ? row_len[ri] : 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) w[i] = live && i < stride ? packed[wi + i] : 0ull;
+    };
+    MzBatch cb, nb;
     uint64_t nw_[NW];
     int nlen = 0;
-    auto load = [&](const GroupDesc& e, int r0, uint64_t (&w)[NW], int& len) {
-        const int r = r0 + lane;
-        len = r < e.nrows ? row_len[e.r0 + r] : 0;
-#pragma unroll
-        for (int i = 0; i < NW; ++i) w[i] = r < e.nrows && i < stride ? packed[e.w0 + (int64_t)r * stride + i] : 0ull;
-    };
-    GroupDesc d{0, 0, 0, 0}, dn{0, 0, 0, 0};
-    int64_t g = 0, gn = 0;
-    bool have = ch < n_chunks && next_group(g, d);
-    if (have) load(d, 0, nw_, nlen);
+    bool have = form(cb);
+    if (have) load(cb, 0, nw_, nlen);
     while (have) {
         uint64_t cw[NW];
 #pragma unroll
         for (int i = 0; i < NW; ++i) cw[i] = nw_[i];
         int clen = nlen;
-        const bool have_n = next_group(gn, dn);
-        if (have_n) load(dn, 0, nw_, nlen);  // in flight while this group is filtered
-        bool stop = false;  // wave-uniform: a count reached min_cov, or too many minimizers
-        uint32_t claimed = 0;
-        for (int r0 = 0; r0 < d.nrows && !stop; r0 += 64) {
-            if (r0) load(d, r0, cw, clen);  // groups of more than 64 rows (rare)
+        const int cj = cb.j;  // pass 0's group; a multi-pass batch has one group (0)
+        const bool have_n = form(nb);
+        if (have_n) load(nb, 0, nw_, nlen);  // in flight while this batch is filtered
+        bool gave_up = false, split = false;
+        uint32_t claimed = 0, keep = 0;  // keep: groups with a row past kMzList minimizers
+        uint32_t reach_split = 0;        // split batches: the groups that keep their class
+        auto scan_reach_all = [&]() {
+            uint32_t reach = 0;
+            for (int i = lane; i < kMzSlots; i += 64)
+                if (cnt[i] >= hit) reach |= 1u << (uint32_t)(key[i] >> 32);
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) reach |= (uint32_t)__shfl_xor((int)reach, m, 64);
+            return (uint32_t)__builtin_amdgcn_readfirstlane((int)reach);
+        };
+        const int passes = (cb.rows + 63) >> 6;
+        for (int pass = 0; pass < passes && !gave_up; ++pass) {
+            if (pass) load(cb, pass, cw, clen);  // groups of more than 64 rows (rare)
             // this lane's row: its distinct window minimizers into its list
             const int nwin = clen >= K ? clen - K + 1 : 0;
             uint32_t hw[NH];
@@ -1663,49 +1724,96 @@ __global__ __launch_bounds__(64 * kMzWaves) void k_minimizer_filter(const GroupD
 #pragma unroll
                 for (int t = 0; t < 16; ++t) suf[t] = nsuf[t];
             }
-            // count the lists in the group's table
-            int nmax = n;
+            // a row with too many minimizers: its group keeps its class
+            const uint64_t over = __ballot(n > kMzList);
+            if (over) {
 #pragma unroll
-            for (int m = 32; m >= 1; m >>= 1) nmax = max(nmax, __shfl_xor(nmax, m, 64));
-            nmax = __builtin_amdgcn_readfirstlane(nmax);
-            if (nmax > kMzList) {  // a row with too many minimizers: keep the class
-                stop = true;
-                break;
+                for (int i = 0; i < kMzG; ++i)
+                    if (__ballot(n > kMzList && cj == i)) keep |= 1u << i;
             }
-            for (int k = 0; k < nmax; ++k) {
-                bool reached = false, fresh = false;
-                if (k < n) {
-                    const uint32_t m = lst[k];
-                    uint32_t slot = (uint32_t)kMzSlots;  // the all-ones key's own slot
-                    if (m != kNone) {
-                        slot = (m * 0x9E3779B1u) >> 23;  // 512 slots
+            const int nn = min(n, kMzList);
+            int nmax = nn, total = nn;
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) {
+                nmax = max(nmax, __shfl_xor(nmax, m, 64));
+                total += __shfl_xor(total, m, 64);
+            }
+            nmax = __builtin_amdgcn_readfirstlane(nmax);
+            total = __builtin_amdgcn_readfirstlane(total);
+            // the lists of the lanes in `sel` into the table; with a cap on the claims
+            // (none is needed while the keys inserted stay within kMzClaim)
+            auto insert = [&](bool sel, bool capped) {
+                uint32_t claimed_here = 0;
+                for (int k = 0; k < nmax; ++k) {
+                    bool fresh = false;
+                    if (sel && k < nn) {
+                        const uint32_t m = lst[k];
+                        const unsigned long long kk = ((unsigned long long)cj << 32) | m;
+                        uint32_t slot = ((m ^ (uint32_t)cj * 0x85EBCA77u) * 0x9E3779B1u) >> 23;  // 512 slots
                         while (true) {
-                            const uint32_t prev = atomicCAS(&key[slot], kNone, m);
-                            if (prev == kNone || prev == m) {
+                            const unsigned long long prev = atomicCAS(&key[slot], kNone, kk);
+                            if (prev == kNone || prev == kk) {
                                 fresh = prev == kNone;
                                 break;
                             }
                             slot = (slot + 1) & (kMzSlots - 1);
                         }
+                        atomicAdd(&cnt[slot], 1u);
                     }
-                    reached = atomicAdd(&cnt[slot], 1u) + 1u >= hit;
+                    if (capped) {
+                        claimed_here += (uint32_t)__popcll(__ballot(fresh));
+                        if (claimed + claimed_here > (uint32_t)kMzClaim) return claimed_here;
+                    }
                 }
-                claimed += (uint32_t)__popcll(__ballot(fresh));
-                if (__ballot(reached) || claimed > (uint32_t)kMzClaim) {
-                    stop = true;
-                    break;
+                return claimed_here;
+            };
+            auto scan_reach = [&]() {  // the table's groups with a count of min_cov
+                uint32_t reach = 0;
+                for (int i = lane; i < kMzSlots; i += 64)
+                    if (cnt[i] >= hit) reach |= 1u << (uint32_t)(key[i] >> 32);
+#pragma unroll
+                for (int m = 32; m >= 1; m >>= 1) reach |= (uint32_t)__shfl_xor((int)reach, m, 64);
+                return (uint32_t)__builtin_amdgcn_readfirstlane((int)reach);
+            };
+            auto reset = [&]() {
+                __builtin_amdgcn_wave_barrier();
+                for (int i = lane; i < kMzSlots; i += 64) {
+                    key[i] = kNone;
+                    cnt[i] = 0;
+                }
+                __builtin_amdgcn_wave_barrier();
+            };
+            if (cb.ng == 1) {  // one group (of up to 3 passes): claims capped over its passes
+                claimed += insert(true, true);
+                if (claimed > (uint32_t)kMzClaim) gave_up = true;
+            } else if (total <= kMzClaim || insert(true, true) <= (uint32_t)kMzClaim) {
+                // the whole batch in one table (inserted above when it may pass the cap)
+                if (total <= kMzClaim) insert(true, false);
+            } else {  // too many distinct keys for one table: the batch's groups one at a time
+                reset();
+                split = true;
+                for (int i = 0; i < cb.ng; ++i) {
+                    claimed = 0;
+                    claimed = insert(cj == i, true);
+                    __builtin_amdgcn_wave_barrier();
+                    if (claimed > (uint32_t)kMzClaim) reach_split |= 1u << i;  // gave up: keeps its class
+                    else reach_split |= scan_reach() & (1u << i);
+                    reset();
                 }
             }
         }
-        if (!stop && lane == 0) gsmall[g] = kClsEmpty;
-        for (int i = lane; i <= kMzSlots; i += 64) {  // the table for the next group
+        __builtin_amdgcn_wave_barrier();
+        if (!gave_up) {
+            const uint32_t reach = (split ? reach_split : scan_reach_all()) | keep;
+            if (lane < cb.ng && !((reach >> lane) & 1u)) gsmall[cb.g] = kClsEmpty;
+        }
+        for (int i = lane; i < kMzSlots; i += 64) {  // the table for the next batch
             key[i] = kNone;
             cnt[i] = 0;
         }
         __builtin_amdgcn_wave_barrier();
         have = have_n;
-        g = gn;
-        d = dn;
+        cb = nb;
     }
 }
 
