@@ -76,10 +76,9 @@ def parse():
                     help="skip the host Arrow in -> host Arrow out measurement (level-2 entry points)")
     ap.add_argument("--iso-launches", type=int, default=10, help="isolated score-kernel launches after timing")
     ap.add_argument("--depth", type=int, default=2, help="batches in flight (1 = no cross-batch overlap)")
-    ap.add_argument("--mark", choices=("auto", "xcd", "fused", "sort", "slices"), default="auto",
+    ap.add_argument("--mark", choices=("auto", "xcd", "sort", "slices"), default="auto",
                     help="H3 presence bitmap: auto (LDS code slices for umi_len 7..12, partition sort for 13), "
-                         "partition sort + LDS bitmap, LDS code slices, XCD-partitioned mark kernel, or mark "
-                         "fused into k_score_packed")
+                         "partition sort + LDS bitmap, LDS code slices, or the XCD-partitioned mark kernel")
     ap.add_argument("--overlap-score", action="store_true",
                     help="let assign of the previous batch overlap the score kernel (default: score overlaps "
                          "only the latency-bound resolve kernels)")
@@ -87,13 +86,9 @@ def parse():
                     help="(tools) on ONE GPU, act as rank 0 of W: the other W-1 shards' bitmaps are built once "
                          "before timing and the all-gather is replaced by a device copy; predicts per-rank "
                          "step time at N=W minus RCCL time. Never used by the driver.")
-    ap.add_argument("--global-mode", choices=("uf", "rounds", "rounds1f", "edges"), default="rounds",
-                    help="H3 global CC phase: one-pass union-find or hook + jump rounds")
     ap.add_argument("--assign-on", choices=("resolve", "separate", "main"), default="main",
                     help="assign of batch k on its own stream one batch later (default), on the main stream "
                          "behind batch k+1's score kernel, or behind its resolve on the resolve stream")
-    ap.add_argument("--split-resolve", action="store_true",
-                    help="local phase of the resolve on the main stream, global phase on the resolve stream")
     ap.add_argument("--resolve-streams", type=int, default=1,
                     help="resolve streams: consecutive batches resolve concurrently (needs depth > streams)")
     ap.add_argument("--spec-rounds", type=int, default=0,
@@ -112,16 +107,8 @@ def parse():
     ap.add_argument("--torch-events", action="store_true",
                     help="cross-stream hand-offs through torch events (system-scope release) instead of the "
                          "library's device-scope StreamEvents")
-    ap.add_argument("--mark-parts", action="store_true",
-                    help="leave the mark's per-chunk partial bitmaps unmerged; the resolve's scan ORs them "
-                         "(one kernel fewer on the main stream; measured slower)")
     ap.add_argument("--late-assign", action="store_true",
                     help="host order: enqueue batch k-1's assign after batch k's resolve (round-2 default)")
-    ap.add_argument("--assign-prev-fused", action="store_true",
-                    help="batch k's score kernel also writes batch k-1's cluster ids (one launch: score and "
-                         "assign tiles interleaved; rogtk_umi_score_assign_prev_packed)")
-    ap.add_argument("--main-cu-every", type=int, default=0,
-                    help="main stream on a CU mask that leaves every M-th CU to the other streams (A/B; 0: all CUs)")
     ap.add_argument("--assign-lag", type=int, default=0,
                     help="assign batch k-lag at batch k's submit (0: the pipeline's default, 1 per resolve stream)")
     ap.add_argument("--no-c3", action="store_true",
@@ -471,20 +458,15 @@ def main():
             return gathered, W
 
     D.set_mark_method({"sort": D.MARK_SORT, "slices": D.MARK_SLICES}.get(args.mark, D.MARK_AUTO))
-    D.set_global_mode({"uf": D.GLOBAL_UNION_FIND, "rounds": D.GLOBAL_ROUNDS,
-                       "rounds1f": D.GLOBAL_ROUNDS_ONE_FLATTEN, "edges": D.GLOBAL_EDGES}[args.global_mode])
     D.set_spec_rounds(args.spec_rounds)
     pipe = UmiPipeline(L, min(n_total, 4 ** L), count, dev, depth=args.depth, target=TARGET,
                        max_distance=md, group=None,
                        priorities=tuple(int(x) for x in args.prio.split(",")), mark=args.mark,
                        score_alone=not args.overlap_score, exchange=exchange,
                        resolve_streams=args.resolve_streams, assign_on=args.assign_on,
-                       split_resolve=args.split_resolve, reuse_gate=args.reuse_gate,
-                       assign_early=not args.late_assign, mark_first=False if args.score_first else "auto",
-                       device_events=not args.torch_events, mark_stream=args.mark_stream,
-                       fused_assign=args.fused_assign, mark_parts=args.mark_parts,
-                       assign_prev_fused=args.assign_prev_fused, assign_lag=args.assign_lag,
-                       main_stream=D.cu_mask_stream(args.main_cu_every) if args.main_cu_every else None)
+                       reuse_gate=args.reuse_gate, assign_early=not args.late_assign,
+                       mark_first=not args.score_first, device_events=not args.torch_events,
+                       mark_stream=args.mark_stream, fused_assign=args.fused_assign, assign_lag=args.assign_lag)
 
     def step():
         pipe.submit(batch)
@@ -614,16 +596,14 @@ def main():
     value = n_total * args.steps / el if args.emulate_ranks == 1 else n * args.emulate_ranks * args.steps / el
     # roofline of the dominant kernel: algorithmic bytes per read of k_score_packed
     #   in: 4 B packed code; out: 6 x 8 B f64 fields + 4 B longest run + 1/8 B within bit
-    # + the u32 cluster id when the score kernel assigns its own batch; + 4 B code in and
-    # 4 B id out when it assigns the previous batch (--assign-prev-fused)
-    bpr = 4 + 48 + 4 + 0.125 + (4 if args.fused_assign else 8 if args.assign_prev_fused else 0)
+    # + the u32 cluster id when the score kernel assigns its own batch (--fused-assign)
+    bpr = 4 + 48 + 4 + 0.125 + (4 if args.fused_assign else 0)
     roof = None
     if "score_packed" in kernels:
         avg_s = kernels["score_packed"]["avg_us"] * 1e-6
         achieved = count * bpr / avg_s / 1e9
-        traffic, src = load_traffic(count, fused=args.fused_assign,
-                                    key="score_assign_prev_hbm_bytes_per_launch" if args.assign_prev_fused else None)
-        roof = {"kernel": "k_score_assign_prev" if args.assign_prev_fused else "k_score_packed", "bound": "hbm",
+        traffic, src = load_traffic(count, fused=args.fused_assign)
+        roof = {"kernel": "k_score_packed", "bound": "hbm",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "traffic_source": src,
@@ -646,7 +626,7 @@ def main():
         # stream every row (the resolve kernels move a few MB each): its §8(d) bytes and
         # its corrected PMC traffic
         cands = {roof["kernel"]: (kernels["score_packed"]["avg_us"], bpr, roof["traffic"])}
-        if "cluster_assign" in kernels and not args.fused_assign and not args.assign_prev_fused:
+        if "cluster_assign" in kernels and not args.fused_assign:
             a_traffic, _ = load_traffic(count, key="assign_hbm_bytes_per_launch")
             cands["k_assign"] = (kernels["cluster_assign"]["avg_us"], 8.0, a_traffic)
         dk = max(cands, key=lambda k: cands[k][0])
@@ -664,7 +644,7 @@ def main():
             roof["isolated"] = {"avg_us": round(iso, 2), "achieved": round(a_iso, 1),
                                 "frac": round(a_iso / HBM_PEAK_GBS, 4), "launches": args.iso_launches,
                                 "note": "same kernel, same batch, launched alone after the timed region"}
-    sort_mark, fused_mark = pipe.sort_mark, pipe.fused_mark
+    sort_mark = pipe.sort_mark
     c3 = None
     if world == 1 and not args.no_c3 and args.emulate_ranks == 1:
         del pipe, batch, codes
@@ -699,12 +679,9 @@ def main():
                    "reads_per_gpu": count, "umi_len": L, "max_distance": md,
                    "n_distinct": stats["n_distinct"], "n_clusters": stats["n_clusters"],
                    "h3_rounds": h3_rounds,
-                   "h3_global": {"uf": "one-pass union-find", "rounds": "hook+jump rounds",
-                                 "rounds1f": "root-chasing hook rounds + one flatten",
-                                 "edges": "one clique sweep + rounds over the crossing edges"}[args.global_mode],
+                   "h3_global": "hook+jump rounds",
                    "h3_bitmap": ("LDS code slices" if args.mark in ("auto", "slices") and 7 <= L <= 12 else
-                                 "partition sort + LDS bitmap") if sort_mark else
-                                ("mark fused in score kernel" if fused_mark else "XCD-partitioned mark"),
+                                 "partition sort + LDS bitmap") if sort_mark else "XCD-partitioned mark",
                    "parallelism": f"dp{world} shard-by-record + presence-bitmap all-gather"
                                   + (f" (rank 0 of {args.emulate_ranks} EMULATED on one GPU, no RCCL)"
                                      if args.emulate_ranks > 1 else "")},

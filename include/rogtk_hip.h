@@ -107,7 +107,6 @@ int rogtk_stage_strings(const void* offsets, int offset_width, const uint8_t* va
  *                  hamming_within_bits[ceil(n/64)] (bit-packed Arrow boolean, LSB
  *                  order, distance <= max_distance)    expressions.rs:1048-1101
  *                  target = host bytes (any UTF-8); target == NULL skips H2
- *   H3 mark     -> cluster_ws presence table (NULL = skip), see rogtk_cluster_*
  * Rows whose regular bit is 0 get zeros everywhere (fix irregular rows up with
  * rogtk_umi_score_rows; null rows stay behind the caller's validity bitmap).
  * regular_bits == NULL means every row is regular.
@@ -115,23 +114,8 @@ int rogtk_stage_strings(const void* offsets, int offset_width, const uint8_t* va
 int rogtk_umi_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
                            int umi_len, const rogtk_umi_scores* scores,
                            const uint8_t* target, int64_t target_len, uint32_t max_distance,
-                           uint32_t* hamming_distance, uint64_t* hamming_within_bits,
-                           void* cluster_ws, int64_t cluster_max_distinct, void* stream);
+                           uint32_t* hamming_distance, uint64_t* hamming_within_bits, void* stream);
 
-/* Batch k's scores (as rogtk_umi_score_packed) and batch k-1's cluster ids (as
- * rogtk_cluster_assign_deferred on prev_ws, which batch k-1 was resolved in) in ONE launch:
- * the score tiles' HBM writes and the assign tiles' table gathers overlap inside the CUs,
- * and the stream pays one kernel boundary instead of two (the pipeline's main stream,
- * rogtk_amd.pipeline assign_prev_fused). Read prev_cluster_id only after
- * rogtk_cluster_sync(prev_ws). Falls back to two launches where the previous batch has
- * no word labels (max_distance 0, or labels by rank). */
-int rogtk_umi_score_assign_prev_packed(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
-                                       const rogtk_umi_scores* scores, const uint8_t* target, int64_t target_len,
-                                       uint32_t max_distance, uint32_t* hamming_distance,
-                                       uint64_t* hamming_within_bits, const void* prev_ws,
-                                       int64_t prev_max_distinct, const uint32_t* prev_codes,
-                                       const uint64_t* prev_regular_bits, int64_t prev_n, uint32_t* prev_cluster_id,
-                                       void* stream);
 /* rogtk_umi_score_packed + rogtk_cluster_assign[_deferred] of the same rows in ONE pass
  * over the codes (cluster_ws resolved by rogtk_cluster_resolve; deferred != 0 as
  * rogtk_cluster_assign_deferred): the assign half of the H3 hot path
@@ -193,12 +177,6 @@ int rogtk_cluster_local_bitmap(void* ws, int umi_len, int64_t max_distinct,
 int rogtk_cluster_resolve(void* ws, int umi_len, int64_t max_distinct,
                           const uint64_t* bitmaps, int n_bitmaps, int max_distance,
                           void* stream);
-/* rogtk_cluster_resolve in two halves, for callers that pipeline batches across
- * streams: phase 1 = rank tables + LDS-local components (needs only the bitmaps), phase 2
- * = global rounds + labels; phase 2 must follow phase 1 of the same workspace and bitmaps
- * (stream order or an event). Enqueue-only. */
-int rogtk_cluster_resolve_phase(void* ws, int umi_len, int64_t max_distinct, const uint64_t* bitmaps,
-                                int n_bitmaps, int max_distance, int phase, void* stream);
 /* cluster_id[i] for regular rows; 0xFFFFFFFF for the others. Completes a pending
  * resolve of this workspace first (host waits on that resolve's event). */
 int rogtk_cluster_assign(const void* ws, int umi_len, int64_t max_distinct,
@@ -243,25 +221,6 @@ int rogtk_cluster_mark_bitmap_temp_bytes(int64_t n, int umi_len, int64_t* bytes)
 int rogtk_cluster_set_mark_method(int method);
 int rogtk_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
                               uint64_t* bitmap_out, void* temp, int64_t temp_bytes, void* stream);
-/* The same, except that where the code-slice method would merge per-chunk partial
- * bitmaps in a last pass, it stops before that pass: *n_parts partial bitmaps of
- * rogtk_cluster_bitmap_words() words each then lie at the start of temp, and their OR is
- * the presence bitmap (rogtk_cluster_resolve takes them as its n_bitmaps bitmaps and ORs
- * them while it scans, so the merge costs no pass and no kernel boundary of its own).
- * *n_parts = 0: the bitmap is in bitmap_out, as with rogtk_cluster_mark_bitmap. */
-int rogtk_cluster_mark_bitmap_parts(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
-                                    uint64_t* bitmap_out, void* temp, int64_t temp_bytes, int* n_parts,
-                                    void* stream);
-/* Global phase of max_distance 1 (positions 7..L-1), process-wide: 2 = bulk-synchronous
- * hook + jump rounds with speculative launch and deferred completion (default; 0
- * restores it), 1 = one-pass lock-free CAS union-find, 3 = hook rounds that chase
- * roots with one flatten per batch of rounds, 4 = one sweep of the bitmap cliques that
- * lists the crossing local-root pairs, then rounds over that shrinking edge list (an
- * overflowing list falls back to mode 2). Identical results (A/B knob). */
-int rogtk_cluster_set_global_mode(int mode);
-/* Tests: edge-list capacity (pairs) of workspaces laid out from now on (mode 4);
- * 0 restores the default (max_distinct / 2, clamped to 2^16..2^25). Process-wide. */
-int rogtk_cluster_set_edge_cap(int64_t pairs);
 /* Releases the host-side resolve state kept for ws (call before freeing ws). */
 int rogtk_cluster_release(const void* ws);
 
@@ -417,10 +376,6 @@ int rogtk_kmer_path_stats(int64_t* out2);
  * (round 4: every row with observations certified free of repeated aligned 16-mers by
  * rogtk_pack_reads, fewer such rows than min_coverage, k_eff 32: nothing valid). */
 int rogtk_kmer_certified_groups(int64_t* out);
-/* A HIP stream restricted to the CUs set in mask (bit i = CU i; `words` u32 words), and its
- * destruction (pipeline A/B: CUs kept free of the main stream for the resolve chain). */
-int rogtk_stream_create_cu_mask(const uint32_t* mask, int words, void** out);
-int rogtk_stream_destroy(void* stream);
 int rogtk_kmer_spectrum_host(const void* offsets, int offset_width, const uint8_t* values,
                              int64_t values_len, const uint8_t* validity, int64_t validity_offset,
                              int64_t n_rows, const int64_t* group_offsets, int64_t n_groups, int k,

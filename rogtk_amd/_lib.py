@@ -97,10 +97,7 @@ SIGNATURES = {
     "rogtk_stage_strings": [_vp, _i32, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp],
     "rogtk_umi_score_assign_packed": [_vp, _vp, _i64, _i32, _P_SCORES, _vp, _i64, _u32, _vp, _vp, _vp, _i64, _vp,
                                       _i32, _vp],
-    "rogtk_umi_score_assign_prev_packed": [_vp, _vp, _i64, _i32, _P_SCORES, _vp, _i64, _u32, _vp, _vp, _vp, _i64,
-                                           _vp, _vp, _i64, _vp, _vp],
-    "rogtk_umi_score_packed": [_vp, _vp, _i64, _i32, _P_SCORES, _vp, _i64, _u32, _vp, _vp, _vp,
-                               _i64, _vp],
+    "rogtk_umi_score_packed": [_vp, _vp, _i64, _i32, _P_SCORES, _vp, _i64, _u32, _vp, _vp, _vp],
     "rogtk_umi_score_rows": [_vp, _i32, _vp, _vp, _vp, _i64, _i64, _P_SCORES, _vp, _i64, _u32, _vp,
                              _vp, _vp],
     "rogtk_cluster_workspace_size": [_i32, _i64, _P_I64],
@@ -109,7 +106,6 @@ SIGNATURES = {
     "rogtk_cluster_mark": [_vp, _vp, _i64, _i32, _vp, _i64, _vp],
     "rogtk_cluster_local_bitmap": [_vp, _i32, _i64, _vp, _vp],
     "rogtk_cluster_resolve": [_vp, _i32, _i64, _vp, _i32, _i32, _vp],
-    "rogtk_cluster_resolve_phase": [_vp, _i32, _i64, _vp, _i32, _i32, _i32, _vp],
     "rogtk_cluster_assign": [_vp, _i32, _i64, _vp, _vp, _i64, _vp, _vp],
     "rogtk_cluster_assign_deferred": [_vp, _i32, _i64, _vp, _vp, _i64, _vp, _vp],
     "rogtk_cluster_sync": [_vp, _vp, ctypes.POINTER(ctypes.c_int)],
@@ -118,8 +114,6 @@ SIGNATURES = {
     "rogtk_cluster_rounds": [_vp, _vp, ctypes.POINTER(ctypes.c_int)],
     "rogtk_cluster_set_spec_rounds": [_i32],
     "rogtk_cluster_set_lookback_polls": [_i32],
-    "rogtk_cluster_set_global_mode": [_i32],
-    "rogtk_cluster_set_edge_cap": [ctypes.c_int64],
     "rogtk_cluster_set_mark_method": [_i32],
     "rogtk_long_codes": [_vp, _i32, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp],
     "rogtk_unique_codes": [_vp, _vp, _i64, _i32, _vp, _P_I64, _vp],
@@ -132,7 +126,6 @@ SIGNATURES = {
     "rogtk_irregular_merge": [_vp, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _P_I64, _vp],
     "rogtk_cluster_mark_bitmap_temp_bytes": [_i64, _i32, _P_I64],
     "rogtk_cluster_mark_bitmap": [_vp, _vp, _i64, _i32, _vp, _vp, _i64, _vp],
-    "rogtk_cluster_mark_bitmap_parts": [_vp, _vp, _i64, _i32, _vp, _vp, _i64, _P_I32, _vp],
     "rogtk_umi_cluster_dev": [_vp, _vp, _vp, _i64, _i32, _i32, _vp, ctypes.POINTER(_i64), _vp],
     "rogtk_route_pack": [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp],
     "rogtk_bam_open": [ctypes.c_char_p, _i32, ctypes.POINTER(_vp)],
@@ -165,8 +158,6 @@ SIGNATURES = {
                                 _vp, _P_I64, _vp],
     "rogtk_kmer_path_stats": [_P_I64],
     "rogtk_kmer_certified_groups": [_P_I64],
-    "rogtk_stream_create_cu_mask": [ctypes.POINTER(ctypes.c_uint32), _i32, ctypes.POINTER(_vp)],
-    "rogtk_stream_destroy": [_vp],
     "rogtk_read_block_words": [_i64],
     "rogtk_host_alloc": [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)],
     "rogtk_host_free": [_vp],

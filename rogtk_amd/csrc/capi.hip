@@ -591,22 +591,6 @@ extern "C" {
 
 const char* rogtk_version(void) { return "rogtk-amd 0.1.0 (gfx950)"; }
 
-// A stream whose kernels run only on the CUs set in mask (bit i = CU i, `words` u32 words):
-// the pipeline can keep some CUs free of the main stream's streaming kernels, for the
-// latency-bound resolve chain on another stream (A/B knob). Destroy with rogtk_stream_destroy.
-int rogtk_stream_create_cu_mask(const uint32_t* mask, int words, void** out) {
-    ROGTK_REQUIRE(mask && words > 0 && out, ROGTK_E_INVALID, "stream_create_cu_mask: bad arguments");
-    hipStream_t s = nullptr;
-    ROGTK_HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask));
-    *out = (void*)s;
-    return ROGTK_OK;
-}
-
-int rogtk_stream_destroy(void* stream) {
-    if (stream) ROGTK_HIP_CHECK(hipStreamDestroy((hipStream_t)stream));
-    return ROGTK_OK;
-}
-
 const char* rogtk_last_error(void) { return t_err; }
 
 // Pinned host memory for callers' output (and input) buffers: transfers from / to it
@@ -688,8 +672,7 @@ int rogtk_stage_strings(const void* offsets, int offset_width, const uint8_t* va
 int rogtk_umi_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
                            int umi_len, const rogtk_umi_scores* scores, const uint8_t* target,
                            int64_t target_len, uint32_t max_distance, uint32_t* hamming_distance,
-                           uint64_t* hamming_within_bits, void* cluster_ws,
-                           int64_t cluster_max_distinct, void* stream) {
+                           uint64_t* hamming_within_bits, void* stream) {
     ROGTK_REQUIRE(umi_len >= 1 && umi_len <= kMaxPackedLen, ROGTK_E_UNSUPPORTED,
                   "packed path: umi_len %d outside 1..%d", umi_len, kMaxPackedLen);
     ROGTK_REQUIRE(n >= 0, ROGTK_E_INVALID, "n must be >= 0");
@@ -700,14 +683,8 @@ int rogtk_umi_score_packed(const uint32_t* codes, const uint64_t* regular_bits, 
     PackedParams p;
     build_packed_params(umi_len, &p);
     encode_target(target, target_len, umi_len, max_distance, &p);
-    uint8_t* presence = nullptr;
-    if (cluster_ws) {
-        ClusterLayout cl;
-        if (int rc = cluster_layout(umi_len, cluster_max_distinct, &cl)) return rc;
-        presence = (uint8_t*)cluster_ws + cl.off_presence;
-    }
     return launch_score_packed(codes, regular_bits, n, p, o, hamming_distance, hamming_within_bits,
-                               presence, as_stream(stream));
+                               as_stream(stream));
 }
 
 int rogtk_umi_score_assign_packed(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
@@ -738,51 +715,11 @@ int rogtk_umi_score_assign_packed(const uint32_t* codes, const uint64_t* regular
         return rc;
     const bool any = any_score(o) || (p.ham_mode && (hamming_distance || hamming_within_bits));
     if (a.out && any)  // one pass: scores, Hamming and ids
-        return launch_score_packed(codes, regular_bits, n, p, o, hamming_distance, hamming_within_bits, nullptr, s,
-                                   &a);
-    if (int rc = launch_score_packed(codes, regular_bits, n, p, o, hamming_distance, hamming_within_bits, nullptr, s))
+        return launch_score_packed(codes, regular_bits, n, p, o, hamming_distance, hamming_within_bits, s, &a);
+    if (int rc = launch_score_packed(codes, regular_bits, n, p, o, hamming_distance, hamming_within_bits, s))
         return rc;
     return launch_cluster_assign(cl, (const uint8_t*)cluster_ws, codes, regular_bits, n, cluster_id, s,
                                  deferred != 0);
-}
-
-int rogtk_umi_score_assign_prev_packed(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
-                                       const rogtk_umi_scores* scores, const uint8_t* target, int64_t target_len,
-                                       uint32_t max_distance, uint32_t* hamming_distance,
-                                       uint64_t* hamming_within_bits, const void* prev_ws,
-                                       int64_t prev_max_distinct, const uint32_t* prev_codes,
-                                       const uint64_t* prev_regular_bits, int64_t prev_n, uint32_t* prev_cluster_id,
-                                       void* stream) {
-    ROGTK_REQUIRE(umi_len >= 1 && umi_len <= kMaxPackedLen, ROGTK_E_UNSUPPORTED,
-                  "packed path: umi_len %d outside 1..%d", umi_len, kMaxPackedLen);
-    ROGTK_REQUIRE(n >= 0 && prev_n >= 0, ROGTK_E_INVALID, "n must be >= 0");
-    ROGTK_REQUIRE(n == 0 || codes, ROGTK_E_INVALID, "codes is NULL");
-    ROGTK_REQUIRE(prev_ws && (prev_n == 0 || (prev_codes && prev_cluster_id)), ROGTK_E_INVALID,
-                  "score_assign_prev: NULL previous-batch argument");
-    ROGTK_REQUIRE(target_len >= 0, ROGTK_E_INVALID, "target_len must be >= 0");
-    ROGTK_REQUIRE(aligned16(codes) && aligned16(prev_codes) && aligned16(prev_cluster_id), ROGTK_E_INVALID,
-                  "score_assign_prev: codes / cluster ids must be 16-byte aligned");
-    const ScoreOut o = to_score_out(scores);
-    if (int rc = check_packed_alignment(codes, o, hamming_distance)) return rc;
-    ClusterLayout cl;
-    if (int rc = cluster_layout(umi_len, prev_max_distinct, &cl)) return rc;
-    PackedParams p;
-    build_packed_params(umi_len, &p);
-    encode_target(target, target_len, umi_len, max_distance, &p);
-    hipStream_t s = as_stream(stream);
-    // the previous batch's assign is deferred (no host wait for its resolve's flags)
-    AssignIn a;
-    if (int rc = cluster_assign_prepare(cl, (const uint8_t*)prev_ws, prev_codes, prev_regular_bits, prev_n,
-                                        prev_cluster_id, s, true, &a))
-        return rc;
-    if (a.out)
-        return launch_score_assign_prev(codes, regular_bits, n, p, o, hamming_distance, hamming_within_bits,
-                                        prev_codes, prev_regular_bits, prev_n, a, s);
-    // no word labels (max_distance 0) or labels by rank: two launches
-    if (int rc = launch_score_packed(codes, regular_bits, n, p, o, hamming_distance, hamming_within_bits, nullptr, s))
-        return rc;
-    return launch_cluster_assign(cl, (const uint8_t*)prev_ws, prev_codes, prev_regular_bits, prev_n, prev_cluster_id,
-                                 s, true);
 }
 
 int rogtk_umi_score_rows(const void* offsets, int offset_width, const uint8_t* values,
@@ -868,18 +805,6 @@ int rogtk_cluster_resolve(void* ws, int umi_len, int64_t max_distinct, const uin
     return launch_cluster_resolve(cl, (uint8_t*)ws, bitmaps, n_bitmaps, max_distance, as_stream(stream));
 }
 
-int rogtk_cluster_resolve_phase(void* ws, int umi_len, int64_t max_distinct, const uint64_t* bitmaps,
-                                int n_bitmaps, int max_distance, int phase, void* stream) {
-    ClusterLayout cl;
-    if (int rc = cluster_layout(umi_len, max_distinct, &cl)) return rc;
-    ROGTK_REQUIRE(ws && bitmaps, ROGTK_E_INVALID, "ws/bitmaps is NULL");
-    ROGTK_REQUIRE(n_bitmaps >= 1, ROGTK_E_INVALID, "n_bitmaps must be >= 1");
-    ROGTK_REQUIRE(max_distance == 0 || max_distance == 1, ROGTK_E_UNSUPPORTED,
-                  "max_distance %d: only 0 (exact) and 1 (Hamming<=1 components) are supported", max_distance);
-    ROGTK_REQUIRE(phase == 1 || phase == 2, ROGTK_E_INVALID, "phase must be 1 or 2, got %d", phase);
-    return launch_cluster_resolve(cl, (uint8_t*)ws, bitmaps, n_bitmaps, max_distance, as_stream(stream), phase);
-}
-
 int rogtk_cluster_assign(const void* ws, int umi_len, int64_t max_distinct, const uint32_t* codes,
                          const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id,
                          void* stream) {
@@ -927,8 +852,6 @@ int rogtk_cluster_rounds(const void* ws, void* stream, int* rounds) {
 
 int rogtk_cluster_set_spec_rounds(int n) { return cluster_set_spec_rounds(n); }
 int rogtk_cluster_set_lookback_polls(int n) { return cluster_set_lookback_polls(n); }
-int rogtk_cluster_set_global_mode(int mode) { return cluster_set_global_mode(mode); }
-int rogtk_cluster_set_edge_cap(int64_t pairs) { return cluster_set_edge_cap(pairs); }
 int rogtk_cluster_set_mark_method(int method) { return cluster_set_mark_method(method); }
 int rogtk_cluster_mark_bitmap_temp_bytes(int64_t n, int umi_len, int64_t* bytes) {
     ROGTK_REQUIRE(bytes, ROGTK_E_INVALID, "null bytes");
@@ -940,14 +863,6 @@ int rogtk_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bit
     return launch_cluster_mark_bitmap(codes, regular_bits, n, umi_len, bitmap_out, temp, temp_bytes,
                                       as_stream(stream));
 }
-int rogtk_cluster_mark_bitmap_parts(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
-                                    uint64_t* bitmap_out, void* temp, int64_t temp_bytes, int* n_parts,
-                                    void* stream) {
-    ROGTK_REQUIRE((codes || n == 0) && bitmap_out && n_parts, ROGTK_E_INVALID, "null codes / bitmap_out / n_parts");
-    return launch_cluster_mark_bitmap(codes, regular_bits, n, umi_len, bitmap_out, temp, temp_bytes,
-                                      as_stream(stream), n_parts);
-}
-
 int rogtk_cluster_release(const void* ws) {
     if (ws) cluster_release(ws);
     return ROGTK_OK;
@@ -987,7 +902,7 @@ int rogtk_umi_complexity_host(const void* offsets, int offset_width, const uint8
     const bool packable = L >= 1 && L <= kMaxPackedLen;
     if (packable) {
         int rc = rogtk_umi_score_packed(c->codes.as<uint32_t>(), c->regbits.as<uint64_t>(), n, L, &ds,
-                                        nullptr, 0, 0, nullptr, nullptr, nullptr, 0, c->stream);
+                                        nullptr, 0, 0, nullptr, nullptr, c->stream);
         if (rc) return rc;
     }
     if (n_irr > 0) {
@@ -1036,8 +951,7 @@ int rogtk_hamming_host(const void* offsets, int offset_width, const uint8_t* val
     }
     if (L >= 1 && L <= kMaxPackedLen) {
         int rc = rogtk_umi_score_packed(c->codes.as<uint32_t>(), c->regbits.as<uint64_t>(), n, L,
-                                        nullptr, tg, target_len, max_distance, dd, dw, nullptr, 0,
-                                        c->stream);
+                                        nullptr, tg, target_len, max_distance, dd, dw, c->stream);
         if (rc) return rc;
     } else if (dw) {
         ROGTK_HIP_CHECK(hipMemsetAsync(dw, 0, (size_t)words * 8, c->stream));

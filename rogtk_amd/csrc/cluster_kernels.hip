@@ -63,20 +63,17 @@ constexpr int kRoundBatch = 4;
 
 // stats block (int64 slots): 0 n_distinct, 1 n_clusters, 2 overflow, 3 error,
 // 4 rounds run; round flags (u32 per round) follow at byte 64.
-// S_EDGE_OVF: the edge list of the global phase (mode 4) overflowed its capacity.
 // S_P0: the first code position of the global phase (7, or 8 when every 4^8-code tile
 // fits the 8-position local CC), chosen on the device by the first scan
 // S_LCAP: with S_P0 = 8, which 8-position instance takes the tiles (0: <= 8192 codes per
 // tile, 1: <= 16384, e.g. the union bitmap of 2-4 ranks' 10M-read batches)
 // S_REDO: the one local-CC instance launched (chosen from the workspace's previous resolve)
 // does not take this bitmap's tiling: cluster_finish redoes the local and global phases.
-enum StatSlot { S_NDISTINCT = 0, S_NCLUSTERS = 1, S_OVERFLOW = 2, S_REDO = 3, S_ROUNDS = 4, S_EDGE_OVF = 5, S_P0 = 6,
+enum StatSlot { S_NDISTINCT = 0, S_NCLUSTERS = 1, S_OVERFLOW = 2, S_REDO = 3, S_ROUNDS = 4, S_P0 = 6,
                 S_LCAP = 7 };
-// stats (8 x int64), round flags (u32 per round) at byte 64, edge-list counts (u32 per
-// round, +1) after them
+// stats (8 x int64; slot 5 unused), round flags (u32 per round) at byte 64
 constexpr int kFlagsOff = 64;
-constexpr int kEcntOff = kFlagsOff + 4 * kMaxRounds;
-constexpr int kStatsBytes = kEcntOff + 4 * (kMaxRounds + 2);
+constexpr int kStatsBytes = kFlagsOff + 4 * kMaxRounds;
 
 __device__ __forceinline__ uint64_t rt_word(const uint4 e) { return (uint64_t)e.x | ((uint64_t)e.y << 32); }
 
@@ -473,7 +470,7 @@ __device__ __forceinline__ uint64_t multi_of4(uint64_t a, uint64_t b, uint64_t c
 // component, the common case once the code space is dense), the live vertices as bits
 // of index space (lroot, zeroed before: the local roots and the codes of the other
 // words), and f over index space for the live vertices.
-#ifdef ROGTK_LCC_TIMING  // tools/local_cc_exp: per-phase clocks of k_local_cc
+#ifdef ROGTK_LCC_TIMING  // experiment builds (tools/lcc_timing.py): per-phase clocks of k_local_cc
 __device__ unsigned long long g_lcc_clk[8];
 #define LCC_T(k) do { __syncthreads(); if (threadIdx.x == 0) { const unsigned long long now_ = wall_clock64(); \
     atomicAdd(&g_lcc_clk[k], now_ - t_last_); t_last_ = now_; } } while (0)
@@ -623,15 +620,16 @@ __device__ __forceinline__ void local_cc_tile(const int64_t base, const uint4* _
     __shared__ uint64_t lrb[kLrb];  // local-root bits of the block's index range
     __shared__ uint32_t s_wave[TW / 64];
     const int t = threadIdx.x;
+#ifdef ROGTK_LCC_TIMING
+    const unsigned long long t_entry_ = wall_clock64();
+    unsigned long long t_last_ = t_entry_;
+#endif
     const int nw = (int)min<int64_t>(TW, words - base);
     const uint4 e = t < nw ? RT[base + t] : make_uint4(0, 0, 0, 0);
     const uint64_t m = rt_word(e);
     uint32_t nloc;
     const uint32_t ex = block_excl_scan<TW>((uint32_t)__popcll(m), s_wave, nloc);
     for (int k = t; k < kLrb; k += TW) lrb[k] = 0;
-#ifdef ROGTK_LCC_TIMING
-    unsigned long long t_last_ = wall_clock64();
-#endif
     const int lpos = L < LP ? L : LP;
     wb[t] = m;
     lpre[t] = ex;
@@ -834,6 +832,12 @@ __device__ __forceinline__ void local_cc_tile(const int64_t base, const uint4* _
         }
     }
     LCC_T(3);
+#ifdef ROGTK_LCC_TIMING
+    if (threadIdx.x == 0) {
+        atomicAdd(&g_lcc_clk[4], wall_clock64() - t_entry_);  // the workgroup's whole duration
+        atomicAdd(&g_lcc_clk[5], 1ull);                        // workgroups
+    }
+#endif
 }
 
 template <int CAP, int TW, int LP>
@@ -854,24 +858,6 @@ __global__ __launch_bounds__(TW) void k_local_cc(const uint4* __restrict__ RT, i
     local_cc_tile<CAP, TW, LP>((int64_t)blockIdx.x * TW, RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats);
 }
 
-// The same over a capped grid (grid-stride over the tiles): when the other tiling takes
-// the batch, its few workgroups exit at once instead of 4^L / (64 TW) of them each waiting
-// for 64 KB of LDS beside a concurrent kernel (measured 28-31 us for the empty launch in
-// the pipeline, 5 us alone)
-template <int CAP, int TW, int LP>
-__global__ __launch_bounds__(TW) void k_local_cc_loop(const uint4* __restrict__ RT, int64_t words, int L,
-                                                      uint32_t* __restrict__ f, uint32_t* __restrict__ D,
-                                                      uint32_t* __restrict__ UR, uint64_t* __restrict__ lroot,
-                                                      int64_t rwords, int64_t max_distinct,
-                                                      unsigned long long* __restrict__ stats) {
-    if (((int)stats[S_P0] == 8 ? 8 : 7) != LP) return;  // the other tiling
-    const int64_t tiles = (words + TW - 1) / TW;
-    for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-        local_cc_tile<CAP, TW, LP>(tile * TW, RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats);
-        __syncthreads();  // the next tile reuses the LDS
-    }
-}
-
 // ROGTK_LOCAL8=0: never the 8-position local tiling (A/B)
 inline bool local8_enabled() {
     static const bool on = [] {
@@ -886,18 +872,6 @@ inline bool local8_big_enabled() {
     static const bool on = [] {
         const char* e = getenv("ROGTK_LOCAL8_BIG");
         return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-// ROGTK_LOCAL8_SINGLE=1: when the 8-position tiles fit the chip at once, only the
-// 16384-code instance is launched (A/B; measured neutral to slower: 0.320-0.327 vs
-// 0.315-0.324 ms/step, profiles/r03z_resolve_ab.txt: its larger LDS keeps workgroups of
-// the concurrent score kernel off those CUs)
-inline bool local8_single_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("ROGTK_LOCAL8_SINGLE");
-        return e && e[0] == '1';
     }();
     return on;
 }
@@ -925,47 +899,16 @@ inline void launch_local_cc(const uint4* RT, int64_t words, int L, uint32_t* f, 
                                words, L, f, D, UR, lroot, rwords, max_distinct, stats, false, true);
         return;
     }
-    // Tiles of the 8-position instances; ROGTK_LOCAL8_SINGLE=1: when they all fit on the
-    // chip at once (one workgroup per CU, e.g. 256 tiles at L = 12) the 16384-code
-    // instance alone takes every 8-position batch, saving one empty launch
-    const int64_t tiles8 = (words + kLocal8Words - 1) / kLocal8Words;
-    static const int64_t n_cus = [] {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-        return (int64_t)cus;
-    }();
-    if (L >= 8 && local8_enabled() && local8_big_enabled() && tiles8 <= n_cus && local8_single_enabled()) {
-        hipLaunchKernelGGL((k_local_cc<kLocal8BigCap, kLocal8Words, 8>), dim3((unsigned)tiles8), dim3(kLocal8Words),
-                           0, s, RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats, true);
-    } else if (L >= 8 && local8_enabled()) {
-        hipLaunchKernelGGL((k_local_cc<kLocal8Cap, kLocal8Words, 8>),
-                           dim3((unsigned)((words + kLocal8Words - 1) / kLocal8Words)), dim3(kLocal8Words), 0, s, RT,
-                           words, L, f, D, UR, lroot, rwords, max_distinct, stats);
+    if (L >= 8 && local8_enabled()) {
+        const unsigned tiles8 = (unsigned)((words + kLocal8Words - 1) / kLocal8Words);
+        hipLaunchKernelGGL((k_local_cc<kLocal8Cap, kLocal8Words, 8>), dim3(tiles8), dim3(kLocal8Words), 0, s, RT,
+                           words, L, f, D, UR, lroot, rwords, max_distinct, stats, false, false);
         if (local8_big_enabled())
-            hipLaunchKernelGGL((k_local_cc<kLocal8BigCap, kLocal8Words, 8>),
-                               dim3((unsigned)((words + kLocal8Words - 1) / kLocal8Words)), dim3(kLocal8Words), 0, s,
-                               RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats);
+            hipLaunchKernelGGL((k_local_cc<kLocal8BigCap, kLocal8Words, 8>), dim3(tiles8), dim3(kLocal8Words), 0, s,
+                               RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats, false, false);
     }
-    const int64_t lblocks = (words + kLocalWords - 1) / kLocalWords;
-    // ROGTK_LCC_LOOP=1: the 7-position instance as a grid-stride loop over 2 workgroups per
-    // CU (A/B; measured slower in the pipeline: 0.383 / 0.407 vs 0.366 / 0.383 ms/step)
-    static const int64_t cap = [] {
-        const char* e = getenv("ROGTK_LCC_LOOP");
-        if (!(e && e[0] == '1')) return (int64_t)0;
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-        return (int64_t)2 * cus;  // 64 KB of LDS each: two per CU
-    }();
-    if (cap && lblocks > cap && L >= 8 && local8_enabled())
-        hipLaunchKernelGGL((k_local_cc_loop<kLocalCodes, kLocalWords, 7>), dim3((unsigned)cap), dim3(kBlock), 0, s,
-                           RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats);
-    else
-        hipLaunchKernelGGL((k_local_cc<kLocalCodes, kLocalWords, 7>), dim3((unsigned)lblocks), dim3(kBlock), 0, s,
-                           RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats);
+    hipLaunchKernelGGL((k_local_cc<kLocalCodes, kLocalWords, 7>), dim3((unsigned)((words + kLocalWords - 1) / kLocalWords)),
+                       dim3(kBlock), 0, s, RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats, false, false);
 }
 
 // --------------------------------------------------------------- global CC
@@ -1016,28 +959,23 @@ __device__ __forceinline__ bool hook_roots(HookTable& T, uint32_t* f, const uint
 // Frontier: a group whose members already share one root never crosses again (roots
 // only merge), so round k > 0 visits only the groups that crossed in round k - 1.
 // active holds two generations of one bit per task (written whole by ballots).
-// CHASE: the forest need not be stars (no jump between rounds): follow f to the root
-// (f only ever points at smaller ancestors, so the walk ends).
-template <bool CHASE>
-__device__ __forceinline__ uint32_t root_of(const uint32_t* f, uint32_t x) {
-    uint32_t r = f[x];
-    if (CHASE)
-        for (uint32_t q = f[r]; q != r; q = f[r]) r = q;
-    return r;
-}
 
 // CHECK (round 4): a read-only round: does any group of the frontier still cross? Sets
 // flags[round] and hooks nothing, writes no frontier bits (a later real round `round`
 // reads the same frontier). k_roots_check runs it beside the roots scan: converged, the
 // forest is unchanged and the roots stand; otherwise the host runs round `round` for real
 // and relabels (cluster_finish), so the last speculative round costs no launches of its own.
-template <bool CHASE, bool CHECK>
+template <bool CHECK>
 __device__ __forceinline__ void hook_block(const int64_t bid, const uint4* __restrict__ RT,
                                            const uint32_t* __restrict__ UR, int64_t words, int L, int p0,
                                            uint32_t* f, unsigned int* __restrict__ flags, int round,
                                            uint64_t* __restrict__ active, int64_t active_words,
                                            const unsigned long long* __restrict__ stats) {
     if (round > 0 && flags[round - 1] == 0) return;  // converged earlier
+    // the local-CC instance launched did not take this bitmap (S_REDO): f / UR / lroot hold
+    // stale or uninitialised values, so nothing may be read through them (cluster_finish
+    // redoes the local and global phases)
+    if (stats[S_REDO]) return;
     p0 = max(p0, (int)stats[S_P0]);  // the local phase's last position + 1 (7 or 8)
     const int64_t per = words >> 2;
     const int64_t tasks = (int64_t)(L - p0) * per;
@@ -1081,7 +1019,7 @@ __device__ __forceinline__ void hook_block(const int64_t bid, const uint4* __res
                 root[v] = kNone;
                 if (m[v] & multi) {
                     const uint32_t ur = UR[w0 + v * stride];
-                    if (ur != kNone) root[v] = root_of<CHASE>(f, ur);
+                    if (ur != kNone) root[v] = f[ur];
                     else all_uniform = false;
                 }
             }
@@ -1130,7 +1068,7 @@ __device__ __forceinline__ void hook_block(const int64_t bid, const uint4* __res
                     for (int v = 0; v < 4; ++v)
                         if ((m[v] >> b) & 1ull)
                             x[k++] = root[v] != kNone ? root[v]
-                                                      : root_of<CHASE>(f, e[v].z + (uint32_t)__popcll(m[v] & below));
+                                                      : f[e[v].z + (uint32_t)__popcll(m[v] & below)];
                     if (CHECK) {
                         for (int v = 1; v < k; ++v) crossed |= x[v] != x[0];
                     } else {
@@ -1156,13 +1094,12 @@ __device__ __forceinline__ void hook_block(const int64_t bid, const uint4* __res
     }
 }
 
-template <bool CHASE>
 __global__ __launch_bounds__(kBlock) void k_hook_g(const uint4* __restrict__ RT, const uint32_t* __restrict__ UR,
                                                    int64_t words, int L, int p0, uint32_t* f,
                                                    unsigned int* __restrict__ flags, int round,
                                                    uint64_t* __restrict__ active, int64_t active_words,
                                                    const unsigned long long* __restrict__ stats) {
-    hook_block<CHASE, false>(blockIdx.x, RT, UR, words, L, p0, f, flags, round, active, active_words, stats);
+    hook_block<false>(blockIdx.x, RT, UR, words, L, p0, f, flags, round, active, active_words, stats);
 }
 
 __device__ __forceinline__ int64_t live_distinct(const unsigned long long* stats, int64_t max_distinct) {
@@ -1177,7 +1114,7 @@ __global__ __launch_bounds__(kBlock) void k_jump(uint32_t* f, const uint64_t* __
                                                  int64_t max_distinct,
                                                  const unsigned long long* __restrict__ stats,
                                                  const unsigned int* __restrict__ flags, int round) {
-    if (flags[round] == 0) return;
+    if (flags[round] == 0 || stats[S_REDO]) return;  // S_REDO: f is not this bitmap's (hook_block)
     const int64_t nd = live_distinct(stats, max_distinct);
     const int lane = threadIdx.x & 63;
     const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
@@ -1189,360 +1126,6 @@ __global__ __launch_bounds__(kBlock) void k_jump(uint32_t* f, const uint64_t* __
         if (r == (uint32_t)i) continue;
         for (uint32_t p = f[r]; p != r; p = f[r]) r = p;
         f[i] = r;
-    }
-}
-
-// ------------------------------------------------- global CC, one-pass union-find
-// The same word-group clique sweep as k_hook_g, but every clique is merged at once
-// with a lock-free union-find over f (CAS link of the larger root under the smaller,
-// intermediate pointer jumping in find). After one pass every cross-tile edge has
-// both ends in one tree, so no rounds, no convergence flags and no host check.
-// Invariant: f[x] <= x, f[x] == x only at roots; path jumping writes an ancestor,
-// links happen only by CAS on a root, so trees stay acyclic and a component's root
-// is its smallest vertex (the label the rounds variant converges to).
-// Loads of f bypass the non-coherent vector L1 (agent-scope atomics): a stale read
-// only ever yields an ancestor, and a failed CAS returns the current parent.
-__device__ __forceinline__ uint32_t uf_ld(const uint32_t* p) {
-#ifdef ROGTK_UF_COHERENT
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-    return *p;  // may be stale in L1: only ever an ancestor
-#endif
-}
-
-__device__ __forceinline__ uint32_t uf_find(uint32_t* f, uint32_t x) {
-    uint32_t r = uf_ld(f + x);
-    if (r == x) return x;
-    uint32_t prev = x, next;
-    while (r != (next = uf_ld(f + r))) {
-        __hip_atomic_store(f + prev, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        prev = r;
-        r = next;
-    }
-    return r;
-}
-
-__device__ __forceinline__ void uf_union(uint32_t* f, uint32_t a, uint32_t b) {
-    a = uf_find(f, a);
-    b = uf_find(f, b);
-    while (a != b) {
-        if (a > b) {
-            const uint32_t t = a;
-            a = b;
-            b = t;
-        }
-        const uint32_t old = atomicCAS(f + b, b, a);  // link root b under a < b
-        if (old == b) return;
-        b = uf_find(f, old);  // b was linked meanwhile: continue from its new root
-        a = uf_find(f, a);
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_union_g(const uint4* __restrict__ RT, const uint32_t* __restrict__ UR,
-                                                    int64_t words, int L, int p0, uint32_t* f,
-                                                    const unsigned long long* __restrict__ stats) {
-    p0 = max(p0, (int)stats[S_P0]);
-    const int64_t per = words >> 2;
-    const int64_t tasks = (int64_t)(L - p0) * per;
-    const int64_t u = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (per == 0 || u >= tasks) return;
-    const int p = p0 + (int)(u / per);
-    const int64_t g = u % per;
-    const int s2 = 2 * p - 6;
-    const int64_t stride = 1ll << s2;
-    const int64_t w0 = ((g >> s2) << (s2 + 2)) | (g & (stride - 1));
-    uint4 e[4];
-    uint64_t m[4];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-        e[v] = RT[w0 + v * stride];
-        m[v] = rt_word(e[v]);
-    }
-    const uint64_t multi = multi_of4(m[0], m[1], m[2], m[3]);
-    if (!multi) return;
-    uint32_t ur[4];
-    bool all_uniform = true;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-        ur[v] = kNone;
-        if (m[v] & multi) {
-            ur[v] = UR[w0 + v * stride];
-            all_uniform &= ur[v] != kNone;
-        }
-    }
-    if (all_uniform) {
-        // whole words: the <= 6 word pairs that share a bit are the only links; find
-        // each member's root once and union only pairs whose roots differ
-        uint32_t r[4];
-#pragma unroll
-        for (int v = 0; v < 4; ++v) r[v] = (m[v] & multi) ? uf_find(f, ur[v]) : kNone;
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int b = a + 1; b < 4; ++b)
-                if ((m[a] & m[b]) && r[a] != r[b]) {
-                    uf_union(f, r[a], r[b]);
-                    r[a] = r[b] = uf_find(f, r[a] < r[b] ? r[a] : r[b]);
-                }
-        return;
-    }
-    uint64_t mm = multi;
-    while (mm) {
-        const int b = __ffsll((long long)mm) - 1;
-        mm &= mm - 1;
-        const uint64_t below = (1ull << b) - 1ull;
-        uint32_t x0 = kNone;
-#pragma unroll
-        for (int v = 0; v < 4; ++v)
-            if ((m[v] >> b) & 1ull) {
-                const uint32_t x = ur[v] != kNone ? ur[v] : e[v].z + (uint32_t)__popcll(m[v] & below);
-                if (x0 == kNone) x0 = x;
-                else uf_union(f, x0, x);
-            }
-    }
-}
-
-// Flatten after the union pass: every live vertex points at its root (stars).
-__global__ __launch_bounds__(kBlock) void k_flatten_live(uint32_t* f, const uint64_t* __restrict__ lroot,
-                                                         int64_t max_distinct,
-                                                         const unsigned long long* __restrict__ stats) {
-    const int64_t nd = live_distinct(stats, max_distinct);
-    const int lane = threadIdx.x & 63;
-    const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
-    for (int64_t w = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; w * 64 < nd; w += nwaves) {
-        const uint64_t lr = lroot[w];
-        const int64_t i = w * 64 + lane;
-        if (!((lr >> lane) & 1ull) || i >= nd) continue;
-        uint32_t r = f[i];
-        if (r == (uint32_t)i) continue;
-        for (uint32_t q = f[r]; q != r; q = f[r]) r = q;
-        f[i] = r;
-    }
-}
-
-// ------------------------------------------- global CC over an edge list (mode 4)
-// Round 0 (k_sweep_edges) walks the same word-group cliques as k_hook_g once: it finds
-// the local roots of each clique's members (UR or f after k_local_cc), keeps the pairs
-// of different roots in a per-workgroup LDS set (many cliques of a block share a pair),
-// hooks the larger root of every distinct pair under the smaller and appends
-// the pair to an edge list. Every later round (k_edge_hook) walks only the edges that
-// crossed in the round before: an edge whose ends share a root stays internal for good.
-// k_edge_jump compresses the surviving edges' ends to their roots between rounds, so
-// that a hook reads one f per end; one k_flatten_live after the last round makes every
-// live vertex point at its root for the labels. The set of hooks of a round is the one
-// of the bulk-synchronous rounds (roots only merge under the smallest proposal), so the
-// components - rooted at their smallest vertex - and the ids are the same.
-constexpr int kPairSlots = 2048;  // 16 KB of LDS per workgroup
-constexpr unsigned long long kNoPair = ~0ull;
-
-struct EdgeSink {
-    uint2* E;                  // output list {lo, hi}
-    unsigned int* cnt;         // its device count (may run past cap: then ovf is set)
-    unsigned int cap;
-    unsigned long long* ovf;   // stats[S_EDGE_OVF]
-    int plain_hooks;           // 1: hook by plain store (ROGTK_EDGE_PLAIN_HOOK=1, A/B)
-};
-
-// Hook root hi under lo. Default: memory-side atomicMin, so that the smallest proposal
-// wins (synth-v1 converges in the same 3 productive rounds as k_hook_g). With plain
-// stores any proposal may win (each written lo is a root of this round and smaller than
-// hi, so the forest stays acyclic and no tree splits; every losing pair is in the list of
-// crossing edges the next round re-checks): measured 1-2 more rounds, past the
-// speculative ones.
-__device__ __forceinline__ void hook_store(const EdgeSink& o, uint32_t* f, uint32_t lo, uint32_t hi) {
-    if (lo < f[hi]) {
-        if (o.plain_hooks) f[hi] = lo;
-        else atomicMin(f + hi, lo);
-    }
-}
-
-__device__ __forceinline__ void edge_append(const EdgeSink& o, uint32_t lo, uint32_t hi) {
-    const unsigned int at = atomicAdd(o.cnt, 1u);
-    if (at < o.cap) o.E[at] = make_uint2(lo, hi);
-    else *o.ovf = 1ull;
-}
-
-// LDS pair set: open addressing on the 64-bit key (lo << 32 | hi); a crowded table
-// sends the pair straight to the list (and to the hook), so nothing is dropped.
-__device__ __forceinline__ void pair_put(unsigned long long* T, const EdgeSink& o, uint32_t* f, uint32_t lo,
-                                         uint32_t hi) {
-    const unsigned long long k = ((unsigned long long)lo << 32) | hi;
-    uint32_t h = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 53);  // 11 bits
-    for (int probe = 0; probe < 32; ++probe, h = (h + 1) & (kPairSlots - 1)) {
-        unsigned long long cur = T[h];
-        if (cur == k) return;
-        if (cur == kNoPair) {
-            cur = atomicCAS(&T[h], kNoPair, k);
-            if (cur == kNoPair || cur == k) return;
-        }
-    }
-    hook_store(o, f, lo, hi);
-    edge_append(o, lo, hi);
-}
-
-__device__ __forceinline__ void pairs_init(unsigned long long* T) {
-    for (int k = threadIdx.x; k < kPairSlots; k += kBlock) T[k] = kNoPair;
-}
-
-// Hook every distinct pair of the block (larger root under the smaller) and append it
-// to the list with one atomicAdd per block.
-__device__ __forceinline__ void pairs_flush(unsigned long long* T, const EdgeSink& o, uint32_t* f,
-                                            uint32_t* s_wave, unsigned int* s_base) {
-    __syncthreads();
-    constexpr int kPer = kPairSlots / kBlock;  // contiguous slots per thread
-    unsigned long long mine[kPer];
-    uint32_t cnt = 0;
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-        mine[k] = T[threadIdx.x * kPer + k];
-        cnt += mine[k] != kNoPair;
-    }
-    uint32_t total;
-    uint32_t ex = block_excl_scan(cnt, s_wave, total);
-    if (threadIdx.x == 0) *s_base = total ? atomicAdd(o.cnt, total) : 0u;
-    __syncthreads();
-    if (!total) return;
-    const unsigned int base = *s_base;
-    if (threadIdx.x == 0 && (uint64_t)base + total > o.cap) *o.ovf = 1ull;
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-        if (mine[k] == kNoPair) continue;
-        const uint32_t lo = (uint32_t)(mine[k] >> 32), hi = (uint32_t)mine[k];
-        hook_store(o, f, lo, hi);
-        const uint64_t at = (uint64_t)base + ex++;
-        if (at < o.cap) o.E[at] = make_uint2(lo, hi);
-    }
-}
-
-__device__ __forceinline__ void put_clique(unsigned long long* T, const EdgeSink& o, uint32_t* f, const uint32_t* x,
-                                           int k, bool& crossed) {
-    uint32_t mn = kNone;
-    for (int v = 0; v < k; ++v) mn = x[v] < mn ? x[v] : mn;
-    for (int v = 0; v < k; ++v)
-        if (x[v] != mn) {
-            crossed = true;
-            pair_put(T, o, f, mn, x[v]);
-        }
-}
-
-// Round 0: positions p0..L-1 as word-group cliques (the tasks of k_hook_g).
-__global__ __launch_bounds__(kBlock) void k_sweep_edges(const uint4* __restrict__ RT, const uint32_t* __restrict__ UR,
-                                                        int64_t words, int L, int p0, uint32_t* f, EdgeSink o,
-                                                        unsigned int* __restrict__ flags,
-                                                        const unsigned long long* __restrict__ stats) {
-    p0 = max(p0, (int)stats[S_P0]);
-    __shared__ unsigned long long T[kPairSlots];
-    __shared__ uint32_t s_wave[kBlock / 64];
-    __shared__ unsigned int s_base;
-    pairs_init(T);
-    __syncthreads();
-    const int64_t per = words >> 2;
-    const int64_t tasks = (int64_t)(L - p0) * per;
-    const int64_t u = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    bool crossed = false;
-    if (per > 0 && u < tasks) {
-        const int p = p0 + (int)(u / per);
-        const int64_t g = u % per;
-        const int s2 = 2 * p - 6;
-        const int64_t stride = 1ll << s2;
-        const int64_t w0 = ((g >> s2) << (s2 + 2)) | (g & (stride - 1));
-        uint4 e[4];
-        uint64_t m[4];
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            e[v] = RT[w0 + v * stride];
-            m[v] = rt_word(e[v]);
-        }
-        const uint64_t multi = multi_of4(m[0], m[1], m[2], m[3]);
-        if (multi) {
-            uint32_t root[4];
-            bool all_uniform = true;
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                root[v] = kNone;
-                if (m[v] & multi) {
-                    root[v] = UR[w0 + v * stride];
-                    all_uniform &= root[v] != kNone;
-                }
-            }
-            uint32_t x[4];
-            if (all_uniform) {
-#pragma unroll
-                for (int a = 0; a < 4; ++a)
-#pragma unroll
-                    for (int b = a + 1; b < 4; ++b)
-                        if ((m[a] & m[b]) && root[a] != root[b]) {
-                            x[0] = root[a];
-                            x[1] = root[b];
-                            put_clique(T, o, f, x, 2, crossed);
-                        }
-            } else {
-                uint64_t mm = multi;
-                while (mm) {
-                    const int b = __ffsll((long long)mm) - 1;
-                    mm &= mm - 1;
-                    const uint64_t below = (1ull << b) - 1ull;
-                    int k = 0;
-#pragma unroll
-                    for (int v = 0; v < 4; ++v)
-                        if ((m[v] >> b) & 1ull)
-                            x[k++] = root[v] != kNone ? root[v] : f[e[v].z + (uint32_t)__popcll(m[v] & below)];
-                    put_clique(T, o, f, x, k, crossed);
-                }
-            }
-        }
-    }
-    if (__syncthreads_or(crossed) && threadIdx.x == 0) flags[0] = 1u;
-    pairs_flush(T, o, f, s_wave, &s_base);
-}
-
-// Round r >= 1 over the edges that crossed in round r - 1 (their ends are roots after
-// k_edge_jump); survivors go to the next list.
-__global__ __launch_bounds__(kBlock) void k_edge_hook(const uint2* __restrict__ Ein, const unsigned int* __restrict__ nin,
-                                                      EdgeSink o, uint32_t* f, unsigned int* __restrict__ flags,
-                                                      int round, const unsigned long long* __restrict__ stats) {
-    if (flags[round - 1] == 0) return;  // converged earlier
-    if (stats[S_EDGE_OVF]) {            // the host falls back to the rounds; never "converged" here
-        if (blockIdx.x == 0 && threadIdx.x == 0) flags[round] = 1u;
-        return;
-    }
-    const uint32_t n = min(*nin, o.cap);
-    if ((uint64_t)blockIdx.x * kBlock >= n) return;
-    __shared__ unsigned long long T[kPairSlots];
-    __shared__ uint32_t s_wave[kBlock / 64];
-    __shared__ unsigned int s_base;
-    pairs_init(T);
-    __syncthreads();
-    bool crossed = false;
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        const uint2 ed = Ein[i];
-        const uint32_t ra = f[ed.x], rb = f[ed.y];
-        if (ra != rb) {
-            crossed = true;
-            pair_put(T, o, f, min(ra, rb), max(ra, rb));
-        }
-    }
-    if (__syncthreads_or(crossed) && threadIdx.x == 0) flags[round] = 1u;
-    pairs_flush(T, o, f, s_wave, &s_base);
-}
-
-// Compress both ends of every edge that crossed in `round` to their roots.
-__global__ __launch_bounds__(kBlock) void k_edge_jump(const uint2* __restrict__ E, const unsigned int* __restrict__ n_p,
-                                                      unsigned int cap, uint32_t* f,
-                                                      const unsigned int* __restrict__ flags, int round,
-                                                      const unsigned long long* __restrict__ stats) {
-    if (flags[round] == 0 || stats[S_EDGE_OVF]) return;
-    const uint32_t n = min(*n_p, cap);
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        const uint2 ed = E[i];
-        const uint32_t xs[2] = {ed.x, ed.y};
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            uint32_t r = f[xs[k]];
-            if (r == xs[k]) continue;
-            for (uint32_t q = f[r]; q != r; q = f[r]) r = q;
-            f[xs[k]] = r;
-        }
     }
 }
 
@@ -1559,14 +1142,14 @@ constexpr int kRootWords = 64;
 
 // the stats block (round flags final) into mapped host memory, then the resolve's epoch
 __device__ __forceinline__ void publish_stats(const unsigned long long* stats, unsigned long long* host,
-                                              unsigned long long* epoch) {
+                                              unsigned long long epoch) {
     for (int k = threadIdx.x; k < kStatsBytes / 8; k += blockDim.x)
         __hip_atomic_store(host + k, stats[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __syncthreads();
     if (threadIdx.x == 0) {
-        const unsigned long long e = *epoch + 1;  // one publish per resolve: no race
-        *epoch = e;
-        __hip_atomic_store(host + kStatsBytes / 8, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        // the resolve's sequence number, passed by the host at enqueue (no device-side
+        // counter: nothing in the workspace has to survive between resolves)
+        __hip_atomic_store(host + kStatsBytes / 8, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1621,7 +1204,7 @@ __global__ __launch_bounds__(kBlock) void k_roots_scan(const uint32_t* __restric
                                                        int64_t rwords, uint64_t* __restrict__ rbits,
                                                        uint32_t* __restrict__ rpref, uint32_t* rblksum,
                                                        const unsigned long long* stats, unsigned long long* host,
-                                                       unsigned long long* epoch) {
+                                                       unsigned long long epoch) {
     if (host && blockIdx.x == 0) publish_stats(stats, host, epoch);
     roots_block(blockIdx.x, f, lroot, max_distinct, rwords, rbits, rpref, rblksum, stats);
 }
@@ -1640,7 +1223,7 @@ __global__ __launch_bounds__(kBlock) void k_roots_check(const uint32_t* __restri
     if ((int64_t)blockIdx.x < rblocks)
         roots_block(blockIdx.x, f, lroot, max_distinct, rwords, rbits, rpref, rblksum, stats);
     else
-        hook_block<false, true>((int64_t)blockIdx.x - rblocks, RT, UR, words, L, p0, const_cast<uint32_t*>(f), flags,
+        hook_block<true>((int64_t)blockIdx.x - rblocks, RT, UR, words, L, p0, const_cast<uint32_t*>(f), flags,
                                 round, active, active_words, stats);
 }
 
@@ -1676,15 +1259,16 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
                                                        const uint32_t* __restrict__ rblkoff,
                                                        uint32_t* __restrict__ wlab, uint64_t* __restrict__ wexc,
                                                        uint32_t* __restrict__ labelcode, uint32_t* __restrict__ ilab,
-                                                       int xl, int use_exc, int exc1_on,
+                                                       int exc1_on,
                                                        const uint32_t* __restrict__ rblksum = nullptr,
                                                        int64_t nrb_max = 0, unsigned long long* stats = nullptr,
                                                        const unsigned long long* pstats = nullptr,
                                                        unsigned long long* host = nullptr,
-                                                       unsigned long long* epoch = nullptr) {
+                                                       unsigned long long epoch = 0) {
     extern __shared__ uint32_t s_roff[];
     __shared__ uint32_t s_wave[kBlock / 64];
     if (host && blockIdx.x == 0) publish_stats(pstats, host, epoch);  // after k_roots_check
+    if (pstats[S_REDO]) return;  // f / UR are not this bitmap's (hook_block); cluster_finish relabels
     if (rblksum) {
         const int64_t nd = live_distinct(stats, max_distinct);
         const int64_t nrb = min<int64_t>(nrb_max, (nd + (int64_t)kRootWords * 64 - 1) / ((int64_t)kRootWords * 64));
@@ -1742,7 +1326,6 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
         }
         // bit 31 flags a word with exceptions (mask form: labels < 2^29, umi_len <= 14; a
         // larger label leaves the word unlabelled and all its codes are labelled per code)
-        if (exc && !use_exc) root = kNone;  // A/B: only uniform words labelled by word
         uint32_t lab = root != kNone ? root_label(root, rbits, rpref, rblkoff) : kNone;
         if (exc && lab != kNone) {  // encodings: decode_word_label (rogtk_internal.h)
             const uint64_t rest = exc & (exc - 1);  // the exceptions past the first
@@ -1760,20 +1343,15 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
         // the word stays unlabelled) get their own label (f[i] is their root: they are
         // live); a uniform word (ur != kNone) always has a label
         uint64_t per_code = lab == kNone ? m : exc;
-        uint32_t xls[2] = {kNone, kNone};  // the first two exceptions' labels (inline forms)
-        for (int j = 0; per_code; ++j) {
+        while (per_code) {
             const int b = __ffsll((long long)per_code) - 1;
             per_code &= per_code - 1;
             const uint32_t i = e.z + (uint32_t)__popcll(m & ((1ull << b) - 1ull));
             if ((int64_t)i >= max_distinct) continue;
             const uint32_t li = root_label(f[i], rbits, rpref, rblkoff);
             put_label((uint64_t)w * 64 + b, i, li, labelcode, ilab);
-            if (j < 2) xls[j] = li;
         }
-        // the inline forms keep their exceptions' labels in the mask's place
-        // (decode_word_label), read only by exception rows
-        const bool inl = xl && lab != kNone && (lab >> 31) && (lab & 0x60000000u);
-        wexc[w] = inl ? (uint64_t)xls[0] | ((uint64_t)xls[1] << 32) : exc;
+        wexc[w] = exc;
     }
 }
 
@@ -1782,9 +1360,8 @@ __global__ __launch_bounds__(kBlock) void k_word_label(const uint32_t* __restric
 // to other components (decode_word_label). Only words with two or more exception codes
 // cost a second (2 MB-table) load; a single exception code is named in the label.
 __device__ __forceinline__ uint32_t word_label_of(const uint32_t* __restrict__ wlab,
-                                                  const uint64_t* __restrict__ wexc,
-                                                  int xl, uint64_t c) {
-    return decode_word_label(wlab[c >> 6], wexc, xl, c);
+                                                  const uint64_t* __restrict__ wexc, uint64_t c) {
+    return decode_word_label(wlab[c >> 6], wexc, c);
 }
 
 // MODE 0: labelcode[code]; MODE 1: flab[rank(code)] (labels by index, ilab).
@@ -1800,8 +1377,7 @@ __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ labelcode,
                                                    const uint32_t* __restrict__ flab,
                                                    const uint4* __restrict__ RT, const uint32_t* __restrict__ wlab,
-                                                   const uint64_t* __restrict__ wexc,
-                                                   int xl, uint32_t* __restrict__ out) {
+                                                   const uint64_t* __restrict__ wexc, uint32_t* __restrict__ out) {
     constexpr int64_t kTile = 256 * G;  // rows per wave and trip
     const int lane = threadIdx.x & 63;
     const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
@@ -1829,7 +1405,7 @@ __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ 
             for (int k = 0; k < 4; ++k) {
                 id[g][k] = 0xFFFFFFFFu;
                 if ((reg[g] >> k) & 1u) {
-                    const uint32_t wl = wlab ? word_label_of(wlab, wexc, xl, c[g][k]) : kNone;
+                    const uint32_t wl = wlab ? word_label_of(wlab, wexc, c[g][k]) : kNone;
                     id[g][k] = wl != kNone ? wl
                                : MODE == 0 ? labelcode[c[g][k]]
                                            : flab[rt_rank(RT[c[g][k] >> 6], c[g][k])];
@@ -1855,15 +1431,14 @@ __global__ __launch_bounds__(kBlock) void k_lookup(const uint64_t* __restrict__ 
                                                    const uint32_t* __restrict__ labelcode,
                                                    const uint32_t* __restrict__ flab, const uint4* __restrict__ RT,
                                                    const uint32_t* __restrict__ wlab,
-                                                   const uint64_t* __restrict__ wexc,
-                                                   int xl, uint32_t* __restrict__ out) {
+                                                   const uint64_t* __restrict__ wexc, uint32_t* __restrict__ out) {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nq; i += (int64_t)gridDim.x * kBlock) {
         const uint64_t c = q[i];
         uint32_t lab = kNone;
         if (c < nbits) {
             const uint4 e = RT[c >> 6];
             if ((rt_word(e) >> (c & 63)) & 1ull) {
-                const uint32_t wl = wlab ? word_label_of(wlab, wexc, xl, c) : kNone;
+                const uint32_t wl = wlab ? word_label_of(wlab, wexc, c) : kNone;
                 lab = wl != kNone ? wl : MODE == 0 ? labelcode[c] : flab[rt_rank(e, (uint32_t)c)];
             }
         }
@@ -1888,10 +1463,7 @@ struct WsPtrs {
     uint64_t *rbits, *lroot;
     uint32_t *rpref, *rblksum, *rblkoff, *labelcode, *ilab;
     uint64_t* active;
-    unsigned long long* epoch;  // resolves published (k_roots_scan)
     uint64_t* lb;               // look-back flags of k_scan_rt (+ its error word)
-    uint2* edges;             // two lists of ecap pairs
-    unsigned int* ecnt;       // per-round list counts (stats block)
 };
 
 inline WsPtrs ws_ptrs(const ClusterLayout& cl, uint8_t* ws) {
@@ -1915,27 +1487,13 @@ inline WsPtrs ws_ptrs(const ClusterLayout& cl, uint8_t* ws) {
     p.labelcode = cl.label_by_code ? (uint32_t*)(ws + cl.off_labelcode) : nullptr;
     p.ilab = cl.label_by_code ? nullptr : (uint32_t*)(ws + cl.off_ilab);
     p.active = (uint64_t*)(ws + cl.off_active);
-    p.edges = (uint2*)(ws + cl.off_edges);
-    p.epoch = (unsigned long long*)(ws + cl.off_epoch);
     p.lb = (uint64_t*)(ws + cl.off_lb);
-    p.ecnt = (unsigned int*)(ws + cl.off_stats + kEcntOff);
     return p;
 }
 
 constexpr int64_t kPersistentGrid = 2048;  // 256 CUs x 8 blocks
 
 }  // namespace
-
-namespace {
-std::atomic<int64_t> g_edge_cap{0};  // 0: derived from max_distinct (rogtk_cluster_set_edge_cap)
-}  // namespace
-
-int cluster_set_edge_cap(int64_t pairs) {
-    ROGTK_REQUIRE(pairs >= 0 && pairs <= (1ll << 30), ROGTK_E_INVALID, "edge cap %lld outside 0..2^30",
-                  (long long)pairs);
-    g_edge_cap.store(pairs);
-    return ROGTK_OK;
-}
 
 int cluster_layout(int L, int64_t max_distinct, ClusterLayout* o) {
     ROGTK_REQUIRE(L >= 1 && L <= kMaxPackedLen, ROGTK_E_UNSUPPORTED,
@@ -1951,12 +1509,9 @@ int cluster_layout(int L, int64_t max_distinct, ClusterLayout* o) {
     c.blocks = (c.words + kScanWords - 1) / kScanWords;
     c.rwords = (max_distinct + 63) / 64;
     c.rblocks = (c.rwords + kRootWords - 1) / kRootWords;
-    // ROGTK_LABEL_BY_INDEX=1: labels by rank even for L <= 13 (A/B of the assign gather)
-    static const bool by_index = [] {
-        const char* e = getenv("ROGTK_LABEL_BY_INDEX");
-        return e && e[0] == '1';
-    }();
-    c.label_by_code = L <= 13 && !by_index;
+    // labels by code (a 4^L-entry table) up to L = 13 (64 MB at L = 12), else by rank (index
+    // space); by rank at L = 12 measured slower (two dependent gathers per exception row)
+    c.label_by_code = L <= 13;
     int64_t off = 0;
     auto take = [&](int64_t bytes) {
         const int64_t at = off;
@@ -1984,15 +1539,6 @@ int cluster_layout(int L, int64_t max_distinct, ClusterLayout* o) {
     const int64_t tasks = L > kLocalPos ? (int64_t)(L - kLocalPos) * (c.words >> 2) : 0;
     c.active_words = (tasks + 63) / 64;
     c.off_active = take(2 * std::max<int64_t>(c.active_words, 1) * 8);
-    // global phase over an edge list (mode 4): two lists of {lo, hi} root pairs. The
-    // capacity is a generous multiple of what synth-v1 needs (0.05 pairs per distinct
-    // UMI at 10M reads); an overflow falls back to the bitmap rounds.
-    const int64_t ecap_set = g_edge_cap.load();
-    c.ecap = L <= kLocalPos ? 0
-             : ecap_set   ? ecap_set
-                          : std::min<int64_t>(std::max<int64_t>(max_distinct / 2, 65536), 1ll << 25);
-    c.off_edges = take(2 * std::max<int64_t>(c.ecap, 1) * 8);
-    c.off_epoch = take(8);
     // look-back flags + error word + tagged block totals (k_scan_rt)
     c.off_lb = take((2 * std::max(c.blocks, c.rblocks) + 1) * 8);
     c.total = off;
@@ -2067,45 +1613,19 @@ std::atomic<int> g_spec_rounds{kSpecRounds};
 // more rounds than the default launches one more than that, so denser batches (e.g. the union bitmap of many
 // ranks) do not fall back to the host-synchronous completion every time
 std::atomic<bool> g_spec_adaptive{true};
-// global phase of max_distance 1: bulk-synchronous hook + jump rounds (default) or a
-// one-pass lock-free union-find. Measured on MI355X at 10M synth-v1 reads (1.08M
-// distinct, a few giant components): rounds 115 us of kernels, union-find 194 us
-// (CAS retries and dependent find chains on the hot roots; the rounds' LDS hook
-// table deduplicates them). Both are exact and give identical ids.
-constexpr int kGlobalUnionFind = 1;
-constexpr int kGlobalRounds = 2;
-constexpr int kGlobalRoundsOneFlatten = 3;  // hook rounds that chase roots, one flatten per batch
-constexpr int kGlobalEdges = 4;             // one clique sweep, then rounds over the crossing edges
-std::atomic<int> g_global_mode{kGlobalRounds};
 std::atomic<int> g_lb_polls{kLbMaxPolls};  // look-back polls before the recount (tests)
 
 // Host-side state of an in-flight resolve, keyed by workspace: the round flags are
 // copied asynchronously to pinned host memory so resolve never blocks the host;
 // assign (or rogtk_cluster_stats) checks them and only then, if the speculative
 // rounds were not enough, runs more rounds and relabels.
-struct GraphKey {
-    const uint64_t* bitmaps = nullptr;
-    int n_bitmaps = 0, max_distance = -1, mode = 0, spec = 0, L = 0;
-    int64_t max_distinct = 0, ecap = 0;
-    bool operator==(const GraphKey& o) const {
-        return bitmaps == o.bitmaps && n_bitmaps == o.n_bitmaps && max_distance == o.max_distance && mode == o.mode &&
-               spec == o.spec && L == o.L && max_distinct == o.max_distinct && ecap == o.ecap;
-    }
-};
-
 struct ResolveState {
-    // the stats block (round flags, edge overflow) published by k_roots_scan into
+    // the stats block (round flags, local-CC redo) published by k_roots_scan into
     // mapped, coherent host memory, followed by a sequence word = the resolve's epoch
     uint8_t* hstats = nullptr;
     uint8_t* hstats_dev = nullptr;  // its device address
-    uint64_t epoch = 0;             // resolves with rounds published so far (device: p.epoch)
-    // the resolve as a replayable graph (launch_cluster_resolve)
-    GraphKey gkey{};
-    hipGraphExec_t gexec = nullptr;
-    hipStream_t cap = nullptr;
-    int glaunched = 0;
+    uint64_t epoch = 0;             // resolves with rounds enqueued so far (the published sequence number)
     int launched = 0;
-    int mode = 0;  // global mode of the pending resolve
     bool pending = false;
     int rounds = 0;  // hook rounds the last resolve needed (the converged round included)
     int needed = 0;  // the same, kept across launches (adaptive speculative rounds)
@@ -2126,21 +1646,6 @@ struct ResolveState {
 std::mutex g_rs_mu;
 std::map<const void*, ResolveState> g_rs;
 
-EdgeSink edge_sink(const ClusterLayout& cl, const WsPtrs& p, int round) {
-    // the list produced by round r (the input of round r + 1) lives in buffer (r + 1) & 1
-    EdgeSink o;
-    o.E = p.edges + (int64_t)((round + 1) & 1) * cl.ecap;
-    o.cnt = p.ecnt + round + 1;
-    o.cap = (unsigned int)cl.ecap;
-    o.ovf = p.stats + S_EDGE_OVF;
-    static const int plain = [] {
-        const char* e = getenv("ROGTK_EDGE_PLAIN_HOOK");
-        return e && e[0] == '1' ? 1 : 0;
-    }();
-    o.plain_hooks = plain;
-    return o;
-}
-
 // Host side: spin until this resolve's stats are published (normally long done).
 int wait_published(const ResolveState& st) {
     const volatile unsigned long long* seq = (const volatile unsigned long long*)(st.hstats + kStatsBytes);
@@ -2154,71 +1659,17 @@ int wait_published(const ResolveState& st) {
     return ROGTK_OK;
 }
 
-int enqueue_rounds(const ClusterLayout& cl, const WsPtrs& p, int from, int to, hipStream_t s, int mode) {
+// Global hook + jump rounds [from, to) (each exits at once once a round found nothing).
+int enqueue_rounds(const ClusterLayout& cl, const WsPtrs& p, int from, int to, hipStream_t s) {
     const int pg = grid_for(cl.max_distinct, kPersistentGrid);
     const int64_t tasks = (int64_t)(cl.L - kLocalPos) * (cl.words >> 2);
-    if (mode == kGlobalEdges) {
-        const int eg = grid_for(cl.ecap, kPersistentGrid);
-        for (int k = from; k < to; ++k) {
-            const EdgeSink o = edge_sink(cl, p, k);
-            if (k == 0) {
-                hipLaunchKernelGGL(k_sweep_edges, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words,
-                                   cl.L, kLocalPos, p.f, o, p.flags, (const unsigned long long*)p.stats);
-            } else {
-                const uint2* ein = p.edges + (int64_t)(k & 1) * cl.ecap;
-                hipLaunchKernelGGL(k_edge_hook, dim3(eg), dim3(kBlock), 0, s, ein, p.ecnt + k, o, p.f, p.flags, k,
-                                   (const unsigned long long*)p.stats);
-            }
-            hipLaunchKernelGGL(k_edge_jump, dim3(eg), dim3(kBlock), 0, s, o.E, o.cnt, o.cap, p.f, p.flags, k,
-                               (const unsigned long long*)p.stats);
-        }
-    } else if (mode == kGlobalRoundsOneFlatten) {
-        // hooks chase to the roots themselves; one flatten after the batch of rounds
-        for (int k = from; k < to; ++k)
-            hipLaunchKernelGGL(k_hook_g<true>, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words, cl.L,
-                               kLocalPos, p.f, p.flags, k, p.active, cl.active_words,
-                               (const unsigned long long*)p.stats);
-        hipLaunchKernelGGL(k_flatten_live, dim3(pg), dim3(kBlock), 0, s, p.f, p.lroot, cl.max_distinct, p.stats);
-    } else {
-        for (int k = from; k < to; ++k) {
-            hipLaunchKernelGGL(k_hook_g<false>, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words,
-                               cl.L, kLocalPos, p.f, p.flags, k, p.active, cl.active_words,
-                               (const unsigned long long*)p.stats);
-            hipLaunchKernelGGL(k_jump, dim3(pg), dim3(kBlock), 0, s, p.f, p.lroot, cl.max_distinct, p.stats, p.flags,
-                               k);
-        }
+    for (int k = from; k < to; ++k) {
+        hipLaunchKernelGGL(k_hook_g, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words, cl.L, kLocalPos,
+                           p.f, p.flags, k, p.active, cl.active_words, (const unsigned long long*)p.stats);
+        hipLaunchKernelGGL(k_jump, dim3(pg), dim3(kBlock), 0, s, p.f, p.lroot, cl.max_distinct, p.stats, p.flags, k);
     }
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
-}
-
-// After the last round of the edge mode: every live vertex points at its root.
-int enqueue_post_rounds(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s, int mode) {
-    if (mode != kGlobalEdges) return ROGTK_OK;
-    hipLaunchKernelGGL(k_flatten_live, dim3(grid_for(cl.max_distinct, kPersistentGrid)), dim3(kBlock), 0, s, p.f,
-                       p.lroot, cl.max_distinct, p.stats);
-    ROGTK_HIP_CHECK(hipGetLastError());
-    return ROGTK_OK;
-}
-
-// ROGTK_WXL=1: the inline word-label forms keep their exception labels in the mask slot
-// (decode_word_label). Measured slower, so off by default: k_assign 125-128 us against
-// 100-101 with the per-code table (round 4, 10M rows, interleaved A/B)
-static int xl_inline_enabled() {
-    static const int v = [] {
-        const char* e = getenv("ROGTK_WXL");
-        return e && atoi(e) == 1 ? 1 : 0;
-    }();
-    return v;
-}
-
-// ROGTK_FOLD_ROOT_SCAN=0: the roots scan's block offsets by a k_scan_blocks launch (A/B)
-bool fold_root_scan_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("ROGTK_FOLD_ROOT_SCAN");
-        return !(e && e[0] == '0');
-    }();
-    return on;
 }
 
 // host_stats != nullptr: k_roots_scan also publishes the stats block (the resolve's
@@ -2226,10 +1677,10 @@ bool fold_root_scan_enabled() {
 // check_round >= 0: the read-only check of that hook round runs inside the roots scan's
 // launch (k_roots_check), and the stats publish moves to k_word_label.
 int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
-                   unsigned long long* host_stats = nullptr, int check_round = -1) {
+                   unsigned long long* host_stats = nullptr, int check_round = -1, uint64_t epoch = 0) {
     // the block offsets of the roots scan in every k_word_label workgroup's LDS when they
     // fit (<= 16K root blocks: 67M distinct codes), else a k_scan_blocks launch
-    const bool lds_off = (cl.rblocks + 1) * 4 <= 65536 && fold_root_scan_enabled();
+    const bool lds_off = (cl.rblocks + 1) * 4 <= 65536;
     {
         ProfScope prof(K_FLATTEN, s);
         if (check_round >= 0) {
@@ -2241,7 +1692,7 @@ int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
         } else {
             hipLaunchKernelGGL(k_roots_scan, dim3((unsigned)cl.rblocks), dim3(kBlock), 0, s, p.f, p.lroot,
                                cl.max_distinct, cl.rwords, p.rbits, p.rpref, p.rblksum,
-                               (const unsigned long long*)p.stats, host_stats, p.epoch);
+                               (const unsigned long long*)p.stats, host_stats, (unsigned long long)epoch);
         }
         if (!lds_off)
             hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, p.rblksum, cl.rblocks, p.rblkoff, p.stats,
@@ -2251,10 +1702,6 @@ int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
     {
         ProfScope prof(K_LABEL, s);
         // wpref and G (consumed into RT by k_rt) hold the word labels and exception masks
-        static const int use_exc = [] {  // ROGTK_WORD_EXC=0: words with exceptions stay unlabelled (A/B)
-            const char* e = getenv("ROGTK_WORD_EXC");
-            return e && e[0] == '0' ? 0 : 1;
-        }();
         // ROGTK_WORD_EXC1=0: words with one or two exception codes also take the mask load (A/B)
         static const int exc1_on = [] {
             const char* e = getenv("ROGTK_WORD_EXC1");
@@ -2262,9 +1709,10 @@ int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
         }();
         hipLaunchKernelGGL(k_word_label, dim3(grid_for(cl.words, kPersistentGrid)), dim3(kBlock),
                            lds_off ? (size_t)(cl.rblocks + 1) * 4 : 0, s, p.f, p.UR, cl.words, p.RT, cl.max_distinct,
-                           p.rbits, p.rpref, p.rblkoff, p.wpref, p.G, p.labelcode, p.ilab, xl_inline_enabled(), use_exc, exc1_on,
+                           p.rbits, p.rpref, p.rblkoff, p.wpref, p.G, p.labelcode, p.ilab, exc1_on,
                            lds_off ? p.rblksum : nullptr, (int64_t)cl.rblocks, lds_off ? p.stats : nullptr,
-                           (const unsigned long long*)p.stats, check_round >= 0 ? host_stats : nullptr, p.epoch);
+                           (const unsigned long long*)p.stats, check_round >= 0 ? host_stats : nullptr,
+                           (unsigned long long)epoch);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     return ROGTK_OK;
@@ -2286,12 +1734,9 @@ int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone =
 }  // namespace
 
 namespace {
-// The kernels of one resolve, enqueued on s (direct, or into a graph under capture).
-// Returns the number of speculative rounds launched (0: no global rounds), -1 on error.
-// phases: bit 0 = the rank tables and the local CC (a function of the bitmaps only),
-// bit 1 = the global rounds, the flags publish and the labels.
 // ROGTK_FUSED_SCAN=0: the rank tables by three kernels (scan words, scan blocks, RT)
-// instead of the single-pass k_scan_rt (A/B)
+// instead of the single-pass k_scan_rt (A/B; also what the look-back's fallback tests
+// compare against)
 bool fused_scan_enabled() {
     static const bool on = [] {
         const char* e = getenv("ROGTK_FUSED_SCAN");
@@ -2299,15 +1744,9 @@ bool fused_scan_enabled() {
     }();
     return on;
 }
-// ROGTK_FUSED_CHECK=0: the last speculative hook round as a hook + jump launch pair (A/B)
-bool fused_check_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("ROGTK_FUSED_CHECK");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
 
+// ROGTK_LCC_PREDICT=0: launch every local-CC instance (each exits at once for the tilings
+// of the others) instead of the previous resolve's alone (A/B)
 bool lcc_predict_enabled() {
     static const bool on = [] {
         const char* e = getenv("ROGTK_LCC_PREDICT");
@@ -2316,118 +1755,67 @@ bool lcc_predict_enabled() {
     return on;
 }
 
+// The kernels of one resolve, enqueued on s. Returns the number of speculative hook
+// rounds launched for real (0: no global rounds), -1 on error. scan_tag: the look-back tag
+// of k_scan_rt (0 = the three-kernel scan). lcc_choice >= 0: the local-CC instance to
+// launch alone (launch_local_cc). *checked: the last speculative round ran as a read-only
+// check inside the roots scan's launch.
 int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bitmaps, int n_bitmaps,
-                    int max_distance, int mode, int spec, unsigned long long* host_stats, hipStream_t s,
-                    int phases = 3, uint32_t scan_tag = 0, int lcc_choice = -1, bool* checked = nullptr) {
-    if (checked) *checked = false;
-    if ((phases & 1) && scan_tag) {  // single pass: RT, n_distinct and the tiling in one launch
-        ProfScope prof(K_SCAN, s);
-        hipLaunchKernelGGL(k_scan_rt, dim3((unsigned)cl.blocks), dim3(kBlock), 0, s, bitmaps, n_bitmaps, cl.words,
-                           p.RT, p.lroot, max_distance == 0 ? (int64_t)0 : cl.rwords,
-                           p.lb + std::max(cl.blocks, cl.rblocks) + 1, p.lb, scan_tag,
-                           p.stats, (int)S_NDISTINCT, max_distance == 0 ? (int)S_NCLUSTERS : -1,
-                           local8_enabled() ? cl.L : 0, local8_big_enabled(), g_lb_polls.load());
-        if (max_distance == 0) {
-            const int cgrid = grid_for((int64_t)std::min<uint64_t>(cl.nbits, 1ull << 30), 16384);
-            hipLaunchKernelGGL(k_build_d, dim3(cgrid), dim3(kBlock), 0, s, p.RT, cl.nbits, p.D, p.f, p.labelcode, p.ilab,
-                               cl.max_distinct, p.stats);
-            return hipGetLastError() == hipSuccess ? 0 : -1;  // labels = ranks (labelcode / ilab)
-        }
-    }
-    if ((phases & 1) && !scan_tag) {
-        ProfScope prof(K_SCAN, s);
-        hipLaunchKernelGGL(k_scan_words, dim3((unsigned)cl.blocks), dim3(kBlock), 0, s, bitmaps,
-                           n_bitmaps, cl.words, (const unsigned long long*)nullptr, p.G, p.wpref,
-                           p.blksum);
-        hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, p.blksum, cl.blocks, p.blkoff,
-                           p.stats, (int)S_NDISTINCT, max_distance == 0 ? (int)S_NCLUSTERS : -1, 1, (int64_t)0,
-                           local8_enabled() ? cl.L : 0, local8_big_enabled());
-    }
-    if ((phases & 1) && !scan_tag) {
-        ProfScope prof(K_COMPACT, s);
-        hipLaunchKernelGGL(k_rt, dim3(grid_for(cl.words)), dim3(kBlock), 0, s, p.G, cl.words, p.wpref,
-                           p.blkoff, p.RT, p.lroot, max_distance == 0 ? 0 : cl.rwords);
-        if (max_distance == 0) {
-            const int cgrid = grid_for((int64_t)std::min<uint64_t>(cl.nbits, 1ull << 30), 16384);
-            hipLaunchKernelGGL(k_build_d, dim3(cgrid), dim3(kBlock), 0, s, p.RT, cl.nbits, p.D, p.f, p.labelcode, p.ilab,
-                               cl.max_distinct, p.stats);
-            return hipGetLastError() == hipSuccess ? 0 : -1;  // labels = ranks (labelcode / ilab)
-        }
-    }
-    if (max_distance == 0) return 0;  // phase 2 of an exact resolve: nothing
-    int launched = 0;
-    if (phases & 1) {
-        ProfScope prof(K_UNION, s);
-        launch_local_cc(p.RT, cl.words, cl.L, p.f, p.D, p.UR, p.lroot, cl.rwords, cl.max_distinct, p.stats, s,
-                        lcc_choice);
-        if (!(phases & 2)) return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
+                    int max_distance, int spec, unsigned long long* host_stats, uint64_t epoch, hipStream_t s,
+                    uint32_t scan_tag, int lcc_choice, bool* checked) {
+    *checked = false;
     {
-        ProfScope prof(K_UNION, s);
-        if (cl.L > kLocalPos && mode == kGlobalUnionFind) {
-            // one-pass union-find: exact when the stream reaches the labels
-            const int64_t tasks = (int64_t)(cl.L - kLocalPos) * (cl.words >> 2);
-            hipLaunchKernelGGL(k_union_g, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words, cl.L,
-                               kLocalPos, p.f, (const unsigned long long*)p.stats);
-            hipLaunchKernelGGL(k_flatten_live, dim3(grid_for(cl.max_distinct, kPersistentGrid)), dim3(kBlock), 0, s,
-                               p.f, p.lroot, cl.max_distinct, p.stats);
-        } else if (cl.L > kLocalPos) {
-            // the last speculative round as a read-only check inside the roots scan's launch
-            // (round 4: two kernel boundaries fewer on the resolve chain; a round that still
-            // finds crossings runs for real in cluster_finish)
-            const bool fuse = checked && host_stats && mode == kGlobalRounds && spec >= 2 && fused_check_enabled();
-            const int real = fuse ? spec - 1 : spec;
-            if (enqueue_rounds(cl, p, 0, real, s, mode)) return -1;
-            if (enqueue_post_rounds(cl, p, s, mode)) return -1;
-            launched = real;
-            if (fuse) *checked = true;
-            // k_roots_scan (or k_word_label after a check) stores the flags into mapped host
-            // memory and then the resolve's epoch (counted on the device): no copy-engine
-            // transfer, no event, no kernel of its own (a D2H copy + event record cost ~15 us
-            // of the resolve chain)
-            if (enqueue_labels(cl, p, s, host_stats, fuse ? real : -1)) return -1;
-            return hipGetLastError() == hipSuccess ? launched : -1;
+        ProfScope prof(K_SCAN, s);
+        if (scan_tag) {  // single pass: RT, n_distinct and the tiling in one launch
+            hipLaunchKernelGGL(k_scan_rt, dim3((unsigned)cl.blocks), dim3(kBlock), 0, s, bitmaps, n_bitmaps, cl.words,
+                               p.RT, p.lroot, max_distance == 0 ? (int64_t)0 : cl.rwords,
+                               p.lb + std::max(cl.blocks, cl.rblocks) + 1, p.lb, scan_tag, p.stats, (int)S_NDISTINCT,
+                               max_distance == 0 ? (int)S_NCLUSTERS : -1, local8_enabled() ? cl.L : 0,
+                               local8_big_enabled(), g_lb_polls.load());
+        } else {
+            hipLaunchKernelGGL(k_scan_words, dim3((unsigned)cl.blocks), dim3(kBlock), 0, s, bitmaps, n_bitmaps,
+                               cl.words, (const unsigned long long*)nullptr, p.G, p.wpref, p.blksum);
+            hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, p.blksum, cl.blocks, p.blkoff, p.stats,
+                               (int)S_NDISTINCT, max_distance == 0 ? (int)S_NCLUSTERS : -1, 1, (int64_t)0,
+                               local8_enabled() ? cl.L : 0, local8_big_enabled());
+            hipLaunchKernelGGL(k_rt, dim3(grid_for(cl.words)), dim3(kBlock), 0, s, p.G, cl.words, p.wpref, p.blkoff,
+                               p.RT, p.lroot, max_distance == 0 ? 0 : cl.rwords);
         }
     }
-    if (enqueue_labels(cl, p, s, nullptr)) return -1;
-    return hipGetLastError() == hipSuccess ? launched : -1;
-}
-
-// ROGTK_RESOLVE_GRAPH=1: replay the resolve as a hipGraph (A/B knob, off by default:
-// measured 0.536 vs 0.411 ms/step at 10M - the graph replays ran without overlapping the
-// other streams' kernels, serialising the pipeline)
-// ROGTK_LCC_PREDICT=0: launch every local-CC instance (each exits at once for the tilings
-// of the others) instead of the previous resolve's alone (A/B)
-bool graphs_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("ROGTK_RESOLVE_GRAPH");
-        return e && e[0] == '1';
-    }();
-    return on;
+    if (max_distance == 0) {  // labels = ranks (labelcode / ilab)
+        const int cgrid = grid_for((int64_t)std::min<uint64_t>(cl.nbits, 1ull << 30), 16384);
+        hipLaunchKernelGGL(k_build_d, dim3(cgrid), dim3(kBlock), 0, s, p.RT, cl.nbits, p.D, p.f, p.labelcode, p.ilab,
+                           cl.max_distinct, p.stats);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+    ProfScope prof(K_UNION, s);
+    launch_local_cc(p.RT, cl.words, cl.L, p.f, p.D, p.UR, p.lroot, cl.rwords, cl.max_distinct, p.stats, s, lcc_choice);
+    if (cl.L <= kLocalPos) {
+        if (enqueue_labels(cl, p, s, nullptr)) return -1;
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+    // the last speculative round as a read-only check inside the roots scan's launch
+    // (round 4: two kernel boundaries fewer on the resolve chain; a round that still finds
+    // crossings runs for real in cluster_finish)
+    const bool fuse = host_stats && spec >= 2;
+    const int real = fuse ? spec - 1 : spec;
+    if (enqueue_rounds(cl, p, 0, real, s)) return -1;
+    *checked = fuse;
+    // k_roots_scan (or k_word_label after a check) stores the flags into mapped host memory
+    // and then the resolve's sequence number: no copy-engine transfer, no
+    // event, no kernel of its own (a D2H copy + event record cost ~15 us of the resolve chain)
+    if (enqueue_labels(cl, p, s, host_stats, fuse ? real : -1, epoch)) return -1;
+    return hipGetLastError() == hipSuccess ? real : -1;
 }
 }  // namespace
 
-int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t* bitmaps,
-                           int n_bitmaps, int max_distance, hipStream_t s, int phases) {
+int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t* bitmaps, int n_bitmaps,
+                           int max_distance, hipStream_t s) {
     WsPtrs p = ws_ptrs(cl, ws);
     std::lock_guard<std::mutex> lk(g_rs_mu);
     ResolveState& st = g_rs[ws];
     if (st.pending && st.deferred.on) {  // a deferred assign must see its resolve complete first
         if (int rc = finish_locked(ws, st, s)) return rc;
-    }
-    // a new look-back tag per single-pass scan (0 = the three-kernel scan)
-    auto next_tag = [&]() -> uint32_t {
-        if (!fused_scan_enabled()) return 0;
-        st.scan_tag = st.scan_tag >= (1u << 30) - 1 ? 1u : st.scan_tag + 1;
-        return st.scan_tag;
-    };
-    if (phases == 1) {  // the local phase alone; the global phase follows on another stream
-        const int r = enqueue_resolve(cl, p, bitmaps, n_bitmaps, max_distance, g_global_mode.load(),
-                                      g_spec_rounds.load(), nullptr, s, 1, next_tag());
-        ROGTK_REQUIRE(r >= 0, ROGTK_E_HIP, "cluster: resolve launch failed (%s)", hipGetErrorString(hipGetLastError()));
-        st.pending = false;
-        st.deferred.on = false;
-        return ROGTK_OK;
     }
     ProfScope prof_chain(K_RESOLVE, s);
     st.pending = false;
@@ -2435,60 +1823,29 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
     st.rounds = 0;
     st.cl = cl;
     st.word_labels = max_distance == 1;
-    const int mode = g_global_mode.load();
     int spec = g_spec_rounds.load();
     if (g_spec_adaptive.load() && st.needed > spec) spec = std::min(st.needed + 1, kMaxRounds);
-    const bool rounds = max_distance == 1 && cl.L > kLocalPos && mode != kGlobalUnionFind;
+    const bool rounds = max_distance == 1 && cl.L > kLocalPos;
     if (rounds && !st.hstats) {
         ROGTK_HIP_CHECK(hipHostMalloc((void**)&st.hstats, kStatsBytes + 64, hipHostMallocMapped | hipHostMallocCoherent));
         std::memset(st.hstats, 0, kStatsBytes + 64);
         ROGTK_HIP_CHECK(hipHostGetDevicePointer((void**)&st.hstats_dev, st.hstats, 0));
     }
-    unsigned long long* hs = (unsigned long long*)st.hstats_dev;
-    // The resolve is ~15 small kernels. With ROGTK_RESOLVE_GRAPH=1 the sequence (a
-    // function of the workspace, the bitmaps pointer / count and the knobs) is captured
-    // once into a hipGraph per such key and replayed with one launch (never while
-    // profiling: the per-phase events need the direct launches). A replay cannot take a
-    // new look-back tag, so the graph holds the three-kernel scan.
-    const GraphKey key{bitmaps, n_bitmaps, max_distance, mode, spec, cl.L, cl.max_distinct, cl.ecap};
-    const bool graph = graphs_enabled() && !profiling_on() && phases == 3;
-    int launched = 0;
-    bool checked = false;
-    if (graph) {
-        if (!st.gexec || !(st.gkey == key)) {
-            if (st.gexec) {
-                ROGTK_HIP_CHECK(hipStreamSynchronize(s));  // a replay may still be in flight
-                hipGraphExecDestroy(st.gexec);
-                st.gexec = nullptr;
-            }
-            if (!st.cap) ROGTK_HIP_CHECK(hipStreamCreateWithFlags(&st.cap, hipStreamNonBlocking));
-            hipGraph_t g = nullptr;
-            ROGTK_HIP_CHECK(hipStreamBeginCapture(st.cap, hipStreamCaptureModeThreadLocal));
-            const int r = enqueue_resolve(cl, p, bitmaps, n_bitmaps, max_distance, mode, spec, hs, st.cap);
-            const hipError_t ec = hipStreamEndCapture(st.cap, &g);
-            ROGTK_REQUIRE(r >= 0 && ec == hipSuccess && g, ROGTK_E_HIP, "cluster: resolve graph capture failed (%s)",
-                          hipGetErrorString(ec));
-            const hipError_t ei = hipGraphInstantiate(&st.gexec, g, nullptr, nullptr, 0);
-            hipGraphDestroy(g);
-            ROGTK_REQUIRE(ei == hipSuccess, ROGTK_E_HIP, "cluster: resolve graph instantiate failed (%s)",
-                          hipGetErrorString(ei));
-            st.gkey = key;
-            st.glaunched = r;
-        }
-        ROGTK_HIP_CHECK(hipGraphLaunch(st.gexec, s));
-        launched = st.glaunched;
-    } else {
-        // one local-CC instance, the previous resolve's (checked on the device: S_REDO)
-        const int choice = rounds && phases == 3 && lcc_predict_enabled() ? st.lcc_choice : -1;
-        launched = enqueue_resolve(cl, p, bitmaps, n_bitmaps, max_distance, mode, spec, hs, s, phases,
-                                   (phases & 1) ? next_tag() : 0u, choice, &checked);
-        ROGTK_REQUIRE(launched >= 0, ROGTK_E_HIP, "cluster: resolve launch failed (%s)",
-                      hipGetErrorString(hipGetLastError()));
+    // a new look-back tag per single-pass scan (0 = the three-kernel scan)
+    uint32_t tag = 0;
+    if (fused_scan_enabled()) {
+        st.scan_tag = st.scan_tag >= (1u << 30) - 1 ? 1u : st.scan_tag + 1;
+        tag = st.scan_tag;
     }
-    if (max_distance == 1 && cl.L > kLocalPos && mode == kGlobalUnionFind) st.rounds = 1;
+    // one local-CC instance, the previous resolve's (checked on the device: S_REDO)
+    const int choice = rounds && lcc_predict_enabled() ? st.lcc_choice : -1;
+    bool checked = false;
+    const int launched = enqueue_resolve(cl, p, bitmaps, n_bitmaps, max_distance, spec,
+                                         rounds ? (unsigned long long*)st.hstats_dev : nullptr, st.epoch + 1, s, tag,
+                                         choice, &checked);
+    ROGTK_REQUIRE(launched >= 0, ROGTK_E_HIP, "cluster: resolve launch failed (%s)", hipGetErrorString(hipGetLastError()));
     if (rounds) {
-        ++st.epoch;  // k_publish_stats publishes the device count of resolves, which matches
-        st.mode = mode;
+        ++st.epoch;  // the sequence number k_roots_scan / k_word_label publish (passed at enqueue)
         st.launched = launched;
         st.checked = checked;
         st.pending = true;
@@ -2509,13 +1866,12 @@ int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone) 
     if (int rc = wait_published(st)) return rc;
     unsigned int* hflags = (unsigned int*)(st.hstats + kFlagsOff);
     const unsigned long long* hs = (const unsigned long long*)st.hstats;
-    const bool edge_ovf = st.mode == kGlobalEdges && hs[S_EDGE_OVF] != 0;
     // the local-CC instance this bitmap's tiling takes: the next resolve launches it alone
     st.lcc_choice = hs[S_P0] == 8 ? (int)hs[S_LCAP] : 2;
     const bool redo = hs[S_REDO] != 0;
     const int scanned = st.launched + (st.checked ? 1 : 0);  // a check round's flag too
     st.checked = false;
-    if (!edge_ovf && !redo) {
+    if (!redo) {
         if (int z = first_zero(hflags, 0, scanned); z >= 0) {
             st.pending = false;
             st.deferred.on = false;
@@ -2532,24 +1888,12 @@ int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone) 
         // global phase stands): the local CC again (every instance; it reads only RT),
         // then the global rounds from round 0
         ProfScope prof(K_UNION, s);
+        ROGTK_HIP_CHECK(hipMemsetAsync(p.stats + S_REDO, 0, 8, s));
         launch_local_cc(p.RT, st.cl.words, st.cl.L, p.f, p.D, p.UR, p.lroot, st.cl.rwords, st.cl.max_distinct,
                         p.stats, s, -1);
         ROGTK_HIP_CHECK(hipGetLastError());
-        ROGTK_HIP_CHECK(hipMemsetAsync(p.stats + S_REDO, 0, 8, s));
         ROGTK_HIP_CHECK(hipMemsetAsync(p.flags, 0, kMaxRounds * sizeof(unsigned int), s));
         std::memset(hflags, 0, kMaxRounds * sizeof(unsigned int));
-        st.mode = st.mode == kGlobalEdges ? kGlobalRounds : st.mode;
-        st.launched = 0;
-    }
-    if (edge_ovf && !redo) {
-        // the edge list overflowed (the round-0 hooks stand): stars again, then the
-        // bitmap rounds from round 0
-        ProfScope prof(K_UNION, s);
-        hipLaunchKernelGGL(k_flatten_live, dim3(grid_for(st.cl.max_distinct, kPersistentGrid)), dim3(kBlock), 0, s,
-                           p.f, p.lroot, st.cl.max_distinct, p.stats);
-        ROGTK_HIP_CHECK(hipGetLastError());
-        ROGTK_HIP_CHECK(hipMemsetAsync(p.flags, 0, kMaxRounds * sizeof(unsigned int), s));
-        st.mode = kGlobalRounds;
         st.launched = 0;
     }
     bool converged = false;
@@ -2557,7 +1901,7 @@ int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone) 
         const int to = std::min(st.launched + kRoundBatch, kMaxRounds);
         {
             ProfScope prof(K_UNION, s);
-            if (int rc = enqueue_rounds(st.cl, p, st.launched, to, s, st.mode)) return rc;
+            if (int rc = enqueue_rounds(st.cl, p, st.launched, to, s)) return rc;
         }
         ROGTK_HIP_CHECK(hipMemcpyAsync(hflags + st.launched, p.flags + st.launched,
                                        (to - st.launched) * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
@@ -2569,7 +1913,6 @@ int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone) 
     }
     st.pending = false;
     ROGTK_REQUIRE(converged, ROGTK_E_HIP, "cluster: union rounds did not converge in %d rounds", kMaxRounds);
-    if (int rc = enqueue_post_rounds(st.cl, p, s, st.mode)) return rc;
     if (int rc = enqueue_labels(st.cl, p, s, nullptr)) return rc;
     if (st.deferred.on) {  // the assign that ran on the speculative labels, again
         st.deferred.on = false;
@@ -2593,13 +1936,6 @@ int cluster_set_lookback_polls(int n) {
     return ROGTK_OK;
 }
 
-int cluster_set_global_mode(int mode) {
-    ROGTK_REQUIRE(mode >= 0 && mode <= kGlobalEdges, ROGTK_E_INVALID, "global mode %d outside 0..%d", mode,
-                  kGlobalEdges);
-    g_global_mode.store(mode == 0 ? kGlobalRounds : mode);
-    return ROGTK_OK;
-}
-
 int cluster_rounds(const void* ws, hipStream_t s, int* rounds) {
     if (int rc = cluster_finish(ws, s)) return rc;
     std::lock_guard<std::mutex> lk(g_rs_mu);
@@ -2616,8 +1952,6 @@ void cluster_release(const void* ws) {
         if (it->second.pending) (void)wait_published(it->second);  // the kernel writes into it
         hipHostFree(it->second.hstats);
     }
-    if (it->second.gexec) hipGraphExecDestroy(it->second.gexec);
-    if (it->second.cap) hipStreamDestroy(it->second.cap);
     g_rs.erase(it);
 }
 
@@ -2651,7 +1985,6 @@ int cluster_assign_prepare(const ClusterLayout& cl, const uint8_t* ws, const uin
                            bool deferred, AssignIn* a) {
     a->wlab = nullptr;
     a->wexc = nullptr;
-    a->xl = 0;
     a->labelcode = nullptr;
     a->out = nullptr;
     if (!deferred)
@@ -2676,7 +2009,6 @@ int cluster_assign_prepare(const ClusterLayout& cl, const uint8_t* ws, const uin
     WsPtrs p = ws_ptrs(cl, const_cast<uint8_t*>(ws));
     a->wlab = p.wpref;
     a->wexc = p.G;
-    a->xl = xl_inline_enabled();
     a->labelcode = p.labelcode;
     a->out = cluster_id;
     return ROGTK_OK;
@@ -2698,10 +2030,10 @@ int launch_cluster_lookup(const ClusterLayout& cl, const uint8_t* ws, const uint
     const int g = grid_for(nq, 4096);
     if (cl.label_by_code)
         hipLaunchKernelGGL(k_lookup<0>, dim3(g), dim3(kBlock), 0, s, q, nq, cl.nbits, p.labelcode, p.D, p.RT, wlab,
-                           wexc, wlab ? xl_inline_enabled() : 0, lab);
+                           wexc, lab);
     else
         hipLaunchKernelGGL(k_lookup<1>, dim3(g), dim3(kBlock), 0, s, q, nq, cl.nbits, p.labelcode, p.ilab, p.RT, wlab,
-                           wexc, wlab ? xl_inline_enabled() : 0, lab);
+                           wexc, lab);
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
 }
@@ -2716,38 +2048,23 @@ int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, bool word_labels, c
     // Two workgroups per CU, grid-stride: assign runs beside the next batch's resolve,
     // whose hook rounds are latency-bound; a full grid of gathers (40k waves at 10M rows)
     // slowed the concurrent hook round 0 from 31 to 94 us. Measured at 10M rows, 2-deep
-    // pipeline: 0.425 ms/step full grid, 0.382-0.385 at 512 workgroups (256 CUs).
-    // ROGTK_ASSIGN_BLOCKS=k overrides (0: full grid; A/B).
+    // pipeline: 0.425 ms/step full grid, 0.382-0.385 at 512 workgroups (256 CUs); 4-row
+    // groups per lane and trip 1 / 4 instead of 2, or a full grid, measured slower (round 3)
     static const int64_t cap = [] {
-        const char* e = getenv("ROGTK_ASSIGN_BLOCKS");
-        if (e) return std::max<int64_t>(0, atoll(e));
         int dev = 0, cus = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
         return (int64_t)2 * cus;
     }();
-    // ROGTK_ASSIGN_GROUPS=1|2|4: 4-row groups per lane and trip (A/B; default 2)
-    static const int groups = [] {
-        const char* e = getenv("ROGTK_ASSIGN_GROUPS");
-        const int v = e ? atoi(e) : 2;
-        return v == 1 || v == 4 ? v : 2;
-    }();
-    const int g = grid_for((n + 4 * groups - 1) / (4 * groups), cap);
-#define ROGTK_ASSIGN_LAUNCH(M, G)                                                                                 \
-    hipExtLaunchKernelGGL((k_assign<M, G>), dim3(g), dim3(kBlock), 0, s, prof.start(), prof.stop(), 0, codes,    \
-                          regular_bits, n, p.labelcode,                                                       \
-                       M == 0 ? p.D : p.ilab, p.RT, wlab, wexc, wlab ? xl_inline_enabled() : 0, cluster_id)
-    if (cl.label_by_code) {
-        if (groups == 1) ROGTK_ASSIGN_LAUNCH(0, 1);
-        else if (groups == 4) ROGTK_ASSIGN_LAUNCH(0, 4);
-        else ROGTK_ASSIGN_LAUNCH(0, 2);
-    } else {
-        if (groups == 1) ROGTK_ASSIGN_LAUNCH(1, 1);
-        else if (groups == 4) ROGTK_ASSIGN_LAUNCH(1, 4);
-        else ROGTK_ASSIGN_LAUNCH(1, 2);
-    }
-#undef ROGTK_ASSIGN_LAUNCH
+    constexpr int kGroups = 2;
+    const int g = grid_for((n + 4 * kGroups - 1) / (4 * kGroups), cap);
+    if (cl.label_by_code)
+        hipExtLaunchKernelGGL((k_assign<0, kGroups>), dim3(g), dim3(kBlock), 0, s, prof.start(), prof.stop(), 0, codes,
+                              regular_bits, n, p.labelcode, p.D, p.RT, wlab, wexc, cluster_id);
+    else
+        hipExtLaunchKernelGGL((k_assign<1, kGroups>), dim3(g), dim3(kBlock), 0, s, prof.start(), prof.stop(), 0, codes,
+                              regular_bits, n, p.labelcode, p.ilab, p.RT, wlab, wexc, cluster_id);
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
 }
@@ -2848,8 +2165,7 @@ constexpr int kSliceChunks = 8;    // a multiple of the 8 XCDs (round 3: 8 vs 16
 constexpr int kSliceLog2 = 20;     // codes per slice (LDS bits)
 constexpr int kMaxSlices = 16;     // 4^12 / 2^20
 constexpr int kBucketRows = 8192;  // rows per segment workgroup (8 per lane; default)
-constexpr int kSegCap = 2048;      // codes per (slice, workgroup) segment: 4x the mean share at 16 slices
-constexpr int kMinBucketRows = 2048;  // smallest bucket instance (temp sizing)
+constexpr int kSegCap = kBucketRows / 4;  // codes per (slice, workgroup) segment: 4x the mean share at 16 slices
 
 // Segment mode (segs != nullptr, written by k_slice_bucket): workgroup (s, c) reads only
 // slice s's segments of the bucket workgroups of chunk c (every code is read once in
@@ -3037,37 +2353,17 @@ __global__ __launch_bounds__(kBlock) void k_or_partials(const uint64_t* __restri
     }
 }
 
-// chunks of the slice mark for n rows (1 = the slices write the bitmap directly)
-// ROGTK_SLICE_CHUNKS=1|2|4|16: chunks of >= 2^20 rows (A/B; default 8). With 1 chunk the
-// slice workgroups write the bitmap directly (no partials, no OR pass: 16 workgroups,
-// measured 2x slower)
-inline int slice_chunks(int64_t n) {
-    static const int c = [] {
-        const char* e = getenv("ROGTK_SLICE_CHUNKS");
-        const int v = e ? atoi(e) : kSliceChunks;
-        return v == 1 || v == 2 || v == 4 || v == 8 || v == 16 ? v : kSliceChunks;
-    }();
-    return n >= (1 << 20) ? c : 1;
-}
+// chunks of the slice mark for n rows (1 = the slices write the bitmap directly; with one
+// chunk at 10M rows only 16 workgroups run: measured 2x slower; 16 chunks measured slower
+// than 8, round 3)
+inline int slice_chunks(int64_t n) { return n >= (1 << 20) ? kSliceChunks : 1; }
 inline bool slice_segments(int64_t n) { return n >= (1 << 20); }  // the bucket pass runs
 inline int slices_of(int L) { return 1 << (2 * L - std::min(2 * L, kSliceLog2)); }
-inline int64_t seg_buckets(int64_t n, int rows = kBucketRows) { return (n + rows - 1) / rows; }
-// ROGTK_BUCKET_ROWS=2048|4096|8192: rows per bucket workgroup (256 / 512 / 1024 threads,
-// 8 rows per lane; A/B, default 8192)
-inline int bucket_rows() {
-    static const int r = [] {
-        const char* e = getenv("ROGTK_BUCKET_ROWS");
-        const int v = e ? atoi(e) : kBucketRows;
-        return v == 2048 || v == 4096 ? v : kBucketRows;
-    }();
-    return r;
-}
-// segments + their lengths of the segment mode
+inline int64_t seg_buckets(int64_t n) { return (n + kBucketRows - 1) / kBucketRows; }
+// segments + their lengths of the segment mode (bucket workgroups of 2048 / 4096 rows
+// measured neutral against 8192, round 3)
 inline int64_t seg_bytes(int64_t n) {
-    // segments: slices x buckets x rows/4 codes = 4n codes for every bucket size; lengths
-    // for the smallest bucket instance
-    return ((int64_t)kMaxSlices * seg_buckets(n) * kSegCap * 4) +
-           ((int64_t)kMaxSlices * seg_buckets(n, kMinBucketRows) * 4 + 255) / 256 * 256;
+    return ((int64_t)kMaxSlices * seg_buckets(n) * kSegCap * 4) + ((int64_t)kMaxSlices * seg_buckets(n) * 4 + 255) / 256 * 256;
 }
 // ROGTK_SLICE_BUCKETS=0: slices read all rows (A/B)
 inline bool slice_buckets_on() {
@@ -3118,8 +2414,7 @@ int cluster_mark_bitmap_temp(int64_t n, int L, int64_t* bytes) {
 }
 
 int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int L,
-                               uint64_t* bitmap, void* temp, int64_t temp_bytes, hipStream_t s, int* n_parts) {
-    if (n_parts) *n_parts = 0;
+                               uint64_t* bitmap, void* temp, int64_t temp_bytes, hipStream_t s) {
     int64_t need = 0;
     if (int rc = cluster_mark_bitmap_temp(n, L, &need)) return rc;
     ROGTK_REQUIRE((temp || n == 0) && temp_bytes >= need, ROGTK_E_INVALID, "temp_bytes %lld < %lld", (long long)temp_bytes,
@@ -3141,29 +2436,18 @@ int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bi
         uint64_t* dst = chunks > 1 ? (uint64_t*)temp : bitmap;
         const uint32_t* segs = nullptr;
         uint32_t* seglen = nullptr;
-        const int brows = bucket_rows(), bcap = brows / 4;
-        const int nb = (int)seg_buckets(n, brows);
+        const int nb = (int)seg_buckets(n);
         if (slice_segments(n) && slices > 1 && slices <= kMaxSlices && slice_buckets_on()) {
             // segment pass: every slice workgroup then reads only its slice's codes (the
             // chunks of all rows were read once per slice: 16x at L = 12, from L2)
             segs = (const uint32_t*)((uint8_t*)temp + (chunks > 1 ? (int64_t)chunks * words * 8 : 0));
-            seglen = (uint32_t*)((uint8_t*)segs + (int64_t)kMaxSlices * nb * bcap * 4);
-            if (brows == 2048)
-                hipLaunchKernelGGL((k_slice_bucket<2048, 256>), dim3((unsigned)nb), dim3(256), 0, s, codes, regular_bits,
-                                   n, slog, slices, (uint32_t*)segs, seglen, nb);
-            else if (brows == 4096)
-                hipLaunchKernelGGL((k_slice_bucket<4096, 512>), dim3((unsigned)nb), dim3(512), 0, s, codes, regular_bits,
-                                   n, slog, slices, (uint32_t*)segs, seglen, nb);
-            else
-                hipLaunchKernelGGL((k_slice_bucket<kBucketRows, kBucketThreads>), dim3((unsigned)nb),
-                                   dim3(kBucketThreads), 0, s, codes, regular_bits, n, slog, slices, (uint32_t*)segs,
-                                   seglen, nb);
+            seglen = (uint32_t*)((uint8_t*)segs + (int64_t)kMaxSlices * nb * kSegCap * 4);
+            hipLaunchKernelGGL((k_slice_bucket<kBucketRows, kBucketThreads>), dim3((unsigned)nb), dim3(kBucketThreads), 0,
+                               s, codes, regular_bits, n, slog, slices, (uint32_t*)segs, seglen, nb);
         }
         hipLaunchKernelGGL(k_slice_mark, dim3((unsigned)(slices * chunks)), dim3(kSliceBlock), 0, s, codes, regular_bits,
-                           n, slog, chunks, chunk_rows, dst, words, segs, (const uint32_t*)seglen, nb, brows, bcap);
-        if (chunks > 1 && n_parts)
-            *n_parts = chunks;  // the caller's resolve ORs the partials (temp, chunk-major)
-        else if (chunks > 1)
+                           n, slog, chunks, chunk_rows, dst, words, segs, (const uint32_t*)seglen, nb, kBucketRows, kSegCap);
+        if (chunks > 1)
             hipLaunchKernelGGL(k_or_partials, dim3(grid_for(words, 4096)), dim3(kBlock), 0, s, dst, chunks, words,
                                bitmap);
         ROGTK_HIP_CHECK(hipGetLastError());
@@ -3188,3 +2472,13 @@ int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bi
 }
 
 }  // namespace rogtk
+
+#ifdef ROGTK_LCC_TIMING
+// experiment builds only: the accumulated k_local_cc clocks (wall_clock64 ticks, summed
+// over workgroups: phases 0..3, whole workgroup, workgroup count), then zeroed
+extern "C" int rogtk_debug_lcc_clock(unsigned long long* out8) {
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(rogtk::g_lcc_clk), 64) != hipSuccess) return 1;
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(rogtk::g_lcc_clk), z, 64) == hipSuccess ? 0 : 1;
+}
+#endif

@@ -280,28 +280,28 @@ __device__ __forceinline__ bool may_repeat16(const uint64_t (&wd)[NW], int len, 
     return min(min(acc4[0], acc4[1]), min(acc4[2], acc4[3])) == 0;
 }
 
-// R rows per workgroup, a lane per row (R threads). DIRECT: each lane stores its row's
-// block itself (16-B stores; the lanes' blocks are consecutive, so a wave covers
-// 64 * 8 * B contiguous bytes and L2 merges the lines) instead of staging the blocks in
-// LDS for one coalesced store: less LDS per workgroup, more workgroups per CU.
+// R rows per workgroup (one wave), a lane per row. Each lane stores its row's block itself
+// (16-B stores; the lanes' blocks are consecutive, so a wave covers 64 * 8 * B contiguous
+// bytes and L2 merges the lines) instead of staging the blocks in LDS for one coalesced
+// store: less LDS per workgroup, more workgroups per CU (round 3, 100M 150-bp reads: 12.6
+// vs 18.8 ms for 256 rows with LDS-staged stores; 256- and 128-row workgroups with lane
+// stores were slower too; a word-parallel variant, B lanes per row, measured neutral).
 // Software-pipelined (round 4): the next trip's bytes are loaded into registers (kVin
 // dwords per lane) before this trip's rows are packed, and written to LDS after them, so
 // each wave's HBM round trip hides behind its own VALU work (the repeat certificate made
 // the pack phase ~3.5 us per 64-row trip) instead of being added to it; the row offsets
 // are loaded two trips ahead. R = 64: at least 3 waves per SIMD (<= 168 VGPRs: the 40 prefetch
 // registers sit beside the certificate's).
-template <int B, int R = kBlock, bool DIRECT = false>
-__global__ __launch_bounds__(R, R == 64 ? 3 : 1) void k_pack_reads(const int64_t* __restrict__ offsets,
+template <int B, int R = 64>
+__global__ __launch_bounds__(R, 3) void k_pack_reads(const int64_t* __restrict__ offsets,
                                                   const uint8_t* __restrict__ values,
                                                   const uint8_t* __restrict__ validity, int64_t voff,
                                                   int64_t n, uint64_t* __restrict__ blocks) {
-    constexpr int OS = B + 1;  // LDS stride of a row's block (odd: fewer bank conflicts)
     constexpr int kIn = kPackInBytes * R / kBlock;  // staged bytes: 160 per row
     constexpr int kVin = kIn / 4 / R;               // staged dwords per lane (40)
     // + the funnel shift's 2 zero dwords, a dummy slot, and slack for a word's 9-dword read
     // past the last row's end (< 8 dwords past nw)
     __shared__ uint32_t in32[kIn / 4 + 12];
-    __shared__ uint64_t out[DIRECT ? 1 : R * OS];
     __shared__ int64_t s_off[R + 1];
     const int tid = threadIdx.x;
     const int64_t stride = (int64_t)gridDim.x * R;
@@ -388,9 +388,9 @@ __global__ __launch_bounds__(R, R == 64 ? 3 : 1) void k_pack_reads(const int64_t
             const int used = valid ? (len + 31) >> 5 : 0;
             const int rel = (int)(st - a4);
             const uint32_t sh = (uint32_t)(rel & 3) * 8;
-            // DIRECT: 16-B stores of word pairs (2k, 2k+1); word 1 waits for the meta word
+            // 16-B stores of word pairs (2k, 2k+1); word 1 waits for the meta word
             uint64_t w1 = 0, pend = 0;
-            uint64_t* const ob = DIRECT ? blocks + r * B : out + tid * OS;
+            uint64_t* const ob = blocks + r * B;
             uint64_t wd[B == 8 ? B - 1 : 1];  // B = 8: the row's words, for the repeat certificate
 #pragma unroll 1
             for (int w = 0; w < B - 1; ++w) {
@@ -438,9 +438,7 @@ __global__ __launch_bounds__(R, R == 64 ? 3 : 1) void k_pack_reads(const int64_t
                         default: wd[6] = acc; break;
                     }
                 }
-                if (!DIRECT) {
-                    ob[1 + w] = acc;
-                } else if (w == 0) {
+                if (w == 0) {
                     w1 = acc;
                 } else if (w & 1) {  // block word w + 1 is even: it starts a pair
                     pend = acc;
@@ -454,17 +452,9 @@ __global__ __launch_bounds__(R, R == 64 ? 3 : 1) void k_pack_reads(const int64_t
             const uint64_t meta = valid ? ((uint64_t)(uint32_t)len | ((uint64_t)(bad == 0) << 32) |
                                            ((uint64_t)norep << 33))
                                         : 0xFFFFFFFFull;
-            if (DIRECT)
-                *reinterpret_cast<ulonglong2*>(ob) = make_ulonglong2(meta, w1);
-            else
-                ob[0] = meta;
+            *reinterpret_cast<ulonglong2*>(ob) = make_ulonglong2(meta, w1);
         }
         __syncthreads();
-        if (!DIRECT) {  // the workgroup's blocks in one contiguous, coalesced store
-            uint64_t* dst = blocks + a * B;
-            for (int i = tid; i < nr * B; i += R) dst[i] = out[(i / B) * OS + (i % B)];
-            __syncthreads();
-        }
         cur = nxt;
         nxt = nn;
     }
@@ -807,16 +797,6 @@ inline bool kmer_cert_on() {
     return on;
 }
 
-// ROGTK_KMER_INSERT=1 / 2: the class-3 LDS kernel's V = 1 / 2 insert loop (round-4 A/B; read once)
-inline int kmer_insert_v() {
-    static const int v = [] {
-        const char* e = getenv("ROGTK_KMER_INSERT");
-        const int x = e ? atoi(e) : 0;
-        return x == 1 || x == 2 ? x : 0;
-    }();
-    return v;
-}
-
 #ifdef ROGTK_KMER_TIMING  // experiment builds only: per-phase clocks of k_kmer_lds (thread 0)
 __device__ unsigned long long g_kmer_clk[8];
 #define KT(k) do { if (tid == 0) { const unsigned long long now_ = wall_clock64(); kt_acc[k] += now_ - kt_last; kt_last = now_; } } while (0)
@@ -835,15 +815,10 @@ struct GroupDesc {
     int32_t nrows, nwords;
 };
 
-// V = 1 (round 4, ROGTK_KMER_INSERT=1 while it is A/B'd): the insert loop issues its LDS
-// reads together (the overflow flag and the previous, current and next packed word, one
-// wait for all), takes the left extension base from the previous word without a divergent
-// branch, and hashes the 64-bit key with one 32-bit multiply instead of a 64-bit one.
-// V = 2: V = 1's loop plus wave-private claimed lists: each wave appends its newly claimed
-// slots to its own segment of the list at an index it counts itself (ballot + mbcnt, no
-// LDS atomic and no round trip per trip), and resets its own segment afterwards; a wave
-// past its segment (kClaim / waves entries) takes the overflow exit like the shared cap
-template <int CLS, int TB, int V = 0>
+// (Round 4 measured two other insert loops for class 3 - all LDS word reads of a trip behind
+// one wait with a 32-bit hash: +0.3%; wave-private claimed lists: 31% slower - removed in
+// round 5.)
+template <int CLS, int TB>
 __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDesc* __restrict__ gdesc, int64_t G,
                                                      uint8_t* __restrict__ gsmall, int K, int64_t min_cov,
                                                      const int32_t* __restrict__ row_len,
@@ -870,8 +845,6 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
     uint64_t* const vkey = ubuf;                                       // after the inserts
     uint32_t* const vinfo = reinterpret_cast<uint32_t*>(ubuf + kLdsObs);  // count | exts << 16 | pad << 31
     __shared__ uint32_t scan[kWaves];
-    __shared__ uint32_t s_wcnt[kWaves];  // V = 2: the waves' claimed counts
-    constexpr uint32_t kCapW = C::kClaim / kWaves;
     __shared__ uint32_t s_claimed, s_term, s_iso, s_over, s_hit;
     // s_hit: some k-mer's count reached min_cov during the inserts (counts grow by one per
     // insert, so one insert sees exactly min_cov). Without it nothing is valid and the
@@ -964,74 +937,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
         // Work unit = (row, half): half h takes the row's positions 64 h + lane + 128 i, so
         // a C3 group (~10 rows of 119 observations) deals 2 units per row over the 8 waves
         // instead of whole rows (waves with two rows set the pace otherwise)
-        if constexpr (V == 2) {
-            // trips are wave-uniform (a unit's row and half are), so the claim count stays
-            // uniform: lanes past the row's end ride along inactive
-            uint32_t wcnt = 0;
-            bool whit = false, stop = false;
-            for (int u = wave; u < 2 * nrows && !stop; u += kWaves) {
-                const int ri = u >> 1;
-                const int nobs = m_nobs[ri];
-                const int h0 = (u & 1) << 6;
-                if (nobs <= h0) continue;
-                const int len = m_len[ri];
-                const uint64_t* rw = words + m_w[ri];
-                const int trips = (nobs - h0 + 127) >> 7;
-                for (int it = 0; it < trips; ++it) {
-                    const int p0 = lane + h0 + (it << 7);
-                    const bool act = p0 < nobs;
-                    const int p = act ? p0 : 0;
-                    const int b = 2 * (p & 31);
-                    const int wi = p >> 5;
-                    uint32_t over = __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    const uint64_t x0 = rw[wi], x1 = rw[wi + 1], xm = rw[wi > 0 ? wi - 1 : 0];
-                    const uint64_t top = b ? (x0 << b) | (x1 >> (64 - b)) : x0;
-                    const uint64_t key = (top >> (64 - 2 * K)) & kmask;
-                    const uint32_t lb = b ? (uint32_t)(x0 >> (64 - b)) : (uint32_t)xm;
-                    uint32_t e = p > 0 ? 1u << (lb & 3u) : 0u;
-                    const int t = (p & 31) + K;
-                    const uint32_t rb = (uint32_t)((t < 32 ? x0 : x1) >> (62 - 2 * (t & 31))) & 3u;
-                    e |= p + K < len ? 1u << (4 + rb) : 0u;
-                    asm volatile("" : "+v"(over) : "v"(x0), "v"(x1), "v"(xm));
-                    if (over) {  // one LDS read for the wave: the same value in every lane
-                        stop = true;
-                        break;
-                    }
-                    uint32_t slot = 0, cnt0 = 1;
-                    if (act) {
-                        if (key == kEmpty) {
-                            slot = kLdsSlots;
-                        } else {
-                            const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
-                            slot = ((lo ^ __builtin_amdgcn_alignbit(hi, hi, 16)) * 0x9E3779B1u) >> (32 - hbits);
-                            while (true) {
-                                const unsigned long long prev = atomicCAS(&tkey[slot], kEmpty, (unsigned long long)key);
-                                if (prev == kEmpty || prev == key) break;
-                                slot = (slot + 1) & (kLdsSlots - 1);
-                            }
-                        }
-                        cnt0 = atomicAdd(&tinfo[slot], 1u) & 0xFFFFFFu;
-                        if (e) atomicOr(&tinfo[slot], e << 24);
-                    }
-                    const bool first = act && cnt0 == 0;
-                    const uint64_t fb = __ballot(first);
-                    if (fb) {
-                        if (first) {
-                            const uint32_t idx = wcnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(fb >> 32),
-                                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)fb, 0u));
-                            if (idx < kCapW) claimed[wave * kCapW + idx] = (uint16_t)slot;
-                            else s_over = 1;  // this wave's segment is full
-                        }
-                        wcnt += (uint32_t)__popcll(fb);
-                    }
-                    whit |= __ballot(act && cnt0 + 1 == hit_at) != 0;
-                }
-            }
-            if (lane == 0) {
-                s_wcnt[wave] = min(wcnt, kCapW);
-                if (whit) s_hit = 1;
-            }
-        } else {
+        {
             for (int u = wave; u < 2 * nrows; u += kWaves) {
                 const int ri = u >> 1;
                 const int nobs = m_nobs[ri];
@@ -1040,50 +946,23 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
                 const uint64_t* rw = words + m_w[ri];
                 for (int p = lane + ((u & 1) << 6); p < nobs; p += 128) {
                     const int b = 2 * (p & 31);
-                    uint32_t over = 0;
-                    uint64_t x0, x1, xm = 0;
-                    if constexpr (V == 1) {
-                        if (kBounded) over = __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        const int wi = p >> 5;
-                        x0 = rw[wi];
-                        x1 = rw[wi + 1];
-                        xm = rw[wi > 0 ? wi - 1 : 0];  // p == 0 (no left base) reads word 0 unused
-                    } else {
-                        x0 = rw[p >> 5];
-                        x1 = rw[(p >> 5) + 1];
-                    }
+                    const uint64_t x0 = rw[p >> 5], x1 = rw[(p >> 5) + 1];
                     const uint64_t top = b ? (x0 << b) | (x1 >> (64 - b)) : x0;
                     const uint64_t key = (top >> (64 - 2 * K)) & kmask;
                     // extension bases from the two words already loaded (k_eff <= 32: base p + K
                     // lies in x0 or x1); only a k-mer starting a word loads its left base
                     uint32_t e = 0;
-                    if constexpr (V == 1) {
-                        const uint32_t lb = b ? (uint32_t)(x0 >> (64 - b)) : (uint32_t)xm;
-                        e = p > 0 ? 1u << (lb & 3u) : 0u;
+                    if (p > 0) e |= 1u << (b ? (uint32_t)(x0 >> (64 - b)) & 3u : (uint32_t)rw[(p >> 5) - 1] & 3u);
+                    if (p + K < len) {
                         const int t = (p & 31) + K;
-                        const uint32_t rb = (uint32_t)((t < 32 ? x0 : x1) >> (62 - 2 * (t & 31))) & 3u;
-                        e |= p + K < len ? 1u << (4 + rb) : 0u;
-                        // the flag's branch stays behind the word reads (one LDS wait for all)
-                        asm volatile("" : "+v"(over) : "v"(x0), "v"(x1), "v"(xm));
-                        if (over) break;
-                    } else {
-                        if (p > 0) e |= 1u << (b ? (uint32_t)(x0 >> (64 - b)) & 3u : (uint32_t)rw[(p >> 5) - 1] & 3u);
-                        if (p + K < len) {
-                            const int t = (p & 31) + K;
-                            e |= 1u << (4 + ((uint32_t)((t < 32 ? x0 : x1) >> (62 - 2 * (t & 31))) & 3u));
-                        }
-                        if (kBounded && __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+                        e |= 1u << (4 + ((uint32_t)((t < 32 ? x0 : x1) >> (62 - 2 * (t & 31))) & 3u));
                     }
+                    if (kBounded && __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
                     uint32_t slot;
                     if (key == kEmpty) {
                         slot = kLdsSlots;
                     } else {
-                        if constexpr (V == 1) {
-                            const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
-                            slot = ((lo ^ __builtin_amdgcn_alignbit(hi, hi, 16)) * 0x9E3779B1u) >> (32 - hbits);
-                        } else {
-                            slot = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - hbits));
-                        }
+                        slot = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - hbits));
                         while (true) {
                             const unsigned long long prev = atomicCAS(&tkey[slot], kEmpty, (unsigned long long)key);
                             if (prev == kEmpty || prev == key) break;
@@ -1103,38 +982,14 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
         }
         __syncthreads();
         KT(2);
-        uint32_t ncl = 0;
-        if constexpr (V == 2) {
-#pragma unroll
-            for (int w2 = 0; w2 < kWaves; ++w2) ncl += s_wcnt[w2];
-        } else {
-            ncl = s_claimed;
-        }
-        // entry i of the claimed list (V = 2: the waves' segments in wave order)
-        auto cl_at = [&](uint32_t i) -> uint32_t {
-            if constexpr (V == 2) {
-                int w2 = 0;
-                for (uint32_t nw; i >= (nw = s_wcnt[w2]); ++w2) i -= nw;
-                return claimed[w2 * kCapW + i];
-            } else {
-                return claimed[i];
-            }
-        };
-        // reset the touched slots (V = 2: each wave its own segment)
+        const uint32_t ncl = s_claimed;
+        auto cl_at = [&](uint32_t i) -> uint32_t { return claimed[i]; };
+        // reset the touched slots
         auto reset_claimed = [&]() {
-            if constexpr (V == 2) {
-                const uint32_t nmine = s_wcnt[wave];
-                for (uint32_t j = lane; j < nmine; j += 64) {
-                    const uint32_t sl = claimed[wave * kCapW + j];
-                    tkey[sl] = kEmpty;
-                    tinfo[sl] = 0;
-                }
-            } else {
-                for (uint32_t i = tid; i < ncl; i += TB) {
-                    const uint32_t sl = claimed[i];
-                    tkey[sl] = kEmpty;
-                    tinfo[sl] = 0;
-                }
+            for (uint32_t i = tid; i < ncl; i += TB) {
+                const uint32_t sl = claimed[i];
+                tkey[sl] = kEmpty;
+                tinfo[sl] = 0;
             }
         };
         const bool hit = s_hit;
@@ -2153,21 +2008,7 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
                               c->packed.as<uint64_t>(), gstat);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
-    if (lds && kmer_insert_v() == 2) {
-        ProfScope prof(K_KMER_LDS, s, true);
-        hipExtLaunchKernelGGL((k_kmer_lds<3, kLdsBlock, 2>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)),
-                              dim3(kLdsBlock), 0, s, prof.start(), prof.stop(), 0, c->gdesc.as<GroupDesc>(), G,
-                              c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
-                              c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
-                              c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
-    } else if (lds && kmer_insert_v() == 1) {
-        ProfScope prof(K_KMER_LDS, s, true);
-        hipExtLaunchKernelGGL((k_kmer_lds<3, kLdsBlock, 1>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)),
-                              dim3(kLdsBlock), 0, s, prof.start(), prof.stop(), 0, c->gdesc.as<GroupDesc>(), G,
-                              c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
-                              c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
-                              c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
-    } else if (lds) {
+    if (lds) {
         ProfScope prof(K_KMER_LDS, s, true);
         hipExtLaunchKernelGGL((k_kmer_lds<3, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)),
                               dim3(kLdsBlock), 0, s, prof.start(), prof.stop(), 0, c->gdesc.as<GroupDesc>(), G,
@@ -2667,46 +2508,18 @@ int rogtk_pack_reads(const int64_t* offsets, const uint8_t* values, const uint8_
                   "pack_reads: block_words must be 8, 16 or 32 (rogtk_read_block_words)");
     if (n == 0) return ROGTK_OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    // ROGTK_PACK=0|1|2|3: 256 rows per workgroup with the blocks staged in LDS for one
-    // coalesced store (0), or stored by their lanes with 256 / 128 / 64 rows per
-    // workgroup (1 / 2 / 3). Default 3 (round 3, 100M 150-bp reads: 12.6 vs 18.8 ms;
-    // C3 86.7-91.0 vs 94.6-95.6 ms per step, interleaved): a one-wave workgroup stages
-    // 10.5 KB, so ~14 waves per CU keep loads in flight instead of 8
-    // (A word-parallel variant - B lanes per row, a lane per block word - measured neutral
-    // in round 3: 1.410-1.420 vs 1.411-1.417 G reads/s at 100M, profiles/r03z_c3_host_ab.txt)
-    static const int variant = [] {
-        const char* e = getenv("ROGTK_PACK");
-        const int v = e ? atoi(e) : 3;
-        return v >= 0 && v <= 3 ? v : 3;
-    }();
-    const int rows_per_wg = variant <= 1 ? 256 : variant == 2 ? 128 : 64;
-    const int g = (int)std::min<int64_t>((n + rows_per_wg - 1) / rows_per_wg, (int64_t)8192 * 256 / rows_per_wg);
-ProfScope prof(K_PACK_READS, s, true);
-#define ROGTK_PACK_LAUNCH(BW)                                                                                        \
-    switch (variant) {                                                                                              \
-        case 1:                                                                                                     \
-            hipExtLaunchKernelGGL((k_pack_reads<BW, 256, true>), dim3(g), dim3(256), 0, s, prof.start(), prof.stop(), 0, offsets, values, validity,   \
-                               validity_offset, n, blocks);                                                         \
-            break;                                                                                                  \
-        case 2:                                                                                                     \
-            hipExtLaunchKernelGGL((k_pack_reads<BW, 128, true>), dim3(g), dim3(128), 0, s, prof.start(), prof.stop(), 0, offsets, values, validity,   \
-                               validity_offset, n, blocks);                                                         \
-            break;                                                                                                  \
-        case 3:                                                                                                     \
-            hipExtLaunchKernelGGL((k_pack_reads<BW, 64, true>), dim3(g), dim3(64), 0, s, prof.start(), prof.stop(), 0, offsets, values, validity,     \
-                               validity_offset, n, blocks);                                                         \
-            break;                                                                                                  \
-        default:                                                                                                    \
-            hipExtLaunchKernelGGL((k_pack_reads<BW, 256, false>), dim3(g), dim3(256), 0, s, prof.start(), prof.stop(), 0, offsets, values, validity,  \
-                               validity_offset, n, blocks);                                                         \
-    }
-    if (block_words == 8) {
-        ROGTK_PACK_LAUNCH(8)
-    } else if (block_words == 16) {
-        ROGTK_PACK_LAUNCH(16)
-    } else {
-        ROGTK_PACK_LAUNCH(32)
-    }
+    constexpr int kRows = 64;  // one wave per workgroup (k_pack_reads)
+    const int g = (int)std::min<int64_t>((n + kRows - 1) / kRows, (int64_t)8192 * 256 / kRows);
+    ProfScope prof(K_PACK_READS, s, true);
+#define ROGTK_PACK_LAUNCH(BW)                                                                                       \
+    hipExtLaunchKernelGGL((k_pack_reads<BW, kRows>), dim3(g), dim3(kRows), 0, s, prof.start(), prof.stop(), 0, offsets, \
+                          values, validity, validity_offset, n, blocks)
+    if (block_words == 8)
+        ROGTK_PACK_LAUNCH(8);
+    else if (block_words == 16)
+        ROGTK_PACK_LAUNCH(16);
+    else
+        ROGTK_PACK_LAUNCH(32);
 #undef ROGTK_PACK_LAUNCH
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;

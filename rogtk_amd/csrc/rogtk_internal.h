@@ -143,30 +143,15 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 //                       codes, whose bits are bits 17..22 and 23..28 (no mask load);
 //   bit 31 set, 30, 29 clear: the label (bits 0..28) of the codes outside the word's
 //                       exception mask wexc[word].
-// xl (round 4): the inline forms need no mask, so their wexc[word] holds the labels of
-// their one or two exception codes instead (low / high 32 bits): an exception row then
-// reads a line of the 2 MB word table (L2-resident beside the 1 MB label table) instead
-// of a line of the 4^L-entry per-code table (64 MB at L = 12: one DRAM round trip per
-// exception row stalled its whole wave trip). Measured slower, in both forms (this one
-// and a separate 2 MB label array): k_assign 100 -> 125-130 us, so off by default
-// (ROGTK_WXL=1 turns it on).
-// Returns the code's label, or 0xFFFFFFFF when the code is labelled per code
-// (xl == 0: the inline forms' exceptions too).
-__device__ __forceinline__ uint32_t decode_word_label(uint32_t wl, const uint64_t* __restrict__ wexc, int xl,
-                                                      uint64_t c) {
+// Returns the code's label, or 0xFFFFFFFF when the code is labelled per code (the
+// exceptions). (Round 4 measured keeping the inline forms' exception labels in wexc
+// instead of the per-code table: k_assign 100 -> 125-130 us; removed in round 5.)
+__device__ __forceinline__ uint32_t decode_word_label(uint32_t wl, const uint64_t* __restrict__ wexc, uint64_t c) {
     if (wl == 0xFFFFFFFFu || !(wl >> 31)) return wl;
     const uint32_t b = (uint32_t)(c & 63);
-    if ((wl >> 30) & 1u) {
-        if (b != ((wl >> 24) & 63u)) return wl & 0xFFFFFFu;
-        return xl ? (uint32_t)wexc[c >> 6] : 0xFFFFFFFFu;
-    }
-    if ((wl >> 29) & 1u) {
-        const bool e0 = b == ((wl >> 17) & 63u), e1 = b == ((wl >> 23) & 63u);
-        if (!e0 && !e1) return wl & 0x1FFFFu;
-        if (!xl) return 0xFFFFFFFFu;
-        const uint64_t x = wexc[c >> 6];
-        return e0 ? (uint32_t)x : (uint32_t)(x >> 32);
-    }
+    if ((wl >> 30) & 1u) return b != ((wl >> 24) & 63u) ? (wl & 0xFFFFFFu) : 0xFFFFFFFFu;
+    if ((wl >> 29) & 1u)
+        return b != ((wl >> 17) & 63u) && b != ((wl >> 23) & 63u) ? (wl & 0x1FFFFu) : 0xFFFFFFFFu;
     return ((wexc[c >> 6] >> b) & 1ull) ? 0xFFFFFFFFu : (wl & 0x1FFFFFFFu);
 }
 
@@ -225,7 +210,6 @@ int build_packed_params(int L, PackedParams* p);
 struct AssignIn {
     const uint32_t* wlab;
     const uint64_t* wexc;
-    int xl;  // inline exception labels in wexc (decode_word_label)
     const uint32_t* labelcode;
     uint32_t* out;  // nullptr: no assign in the score pass
 };
@@ -235,12 +219,9 @@ int launch_stage(const void* offsets, int offset_width, const uint8_t* values,
                  const uint8_t* validity, int64_t validity_offset, int64_t n, int L,
                  uint32_t* codes, uint64_t* regular_bits, int64_t* irregular_rows,
                  unsigned long long* n_irregular, hipStream_t s);
-int launch_score_assign_prev(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, const PackedParams& p,
-                             const ScoreOut& o, uint32_t* hd, uint64_t* hw, const uint32_t* codes2,
-                             const uint64_t* regular_bits2, int64_t n2, const AssignIn& a2, hipStream_t s);
 int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
-                        const PackedParams& p, const ScoreOut& o, uint32_t* hd, uint64_t* hw,
-                        uint8_t* presence, hipStream_t s, const AssignIn* asg = nullptr);
+                        const PackedParams& p, const ScoreOut& o, uint32_t* hd, uint64_t* hw, hipStream_t s,
+                        const AssignIn* asg = nullptr);
 int launch_score_rows(const void* offsets, int offset_width, const uint8_t* values,
                       const int64_t* rows, const int64_t* n_rows_dev, int64_t max_rows,
                       const double* lut, int64_t lut_max, const ScoreOut& o,
@@ -260,7 +241,7 @@ struct ClusterLayout {
     // byte offsets into the workspace
     int64_t off_stats, off_presence, off_bitmap, off_rt, off_wpref, off_blksum, off_blkoff, off_D, off_f, off_ur,
         off_rbits, off_lroot, off_rpref, off_rblksum, off_rblkoff, off_labelcode, off_ilab, off_active,
-        active_words, off_edges, ecap, off_epoch, off_lb, total;
+        active_words, off_lb, total;
 };
 int cluster_layout(int L, int64_t max_distinct, ClusterLayout* out);
 
@@ -296,7 +277,7 @@ struct DevBuf {
 };
 
 
-// XCD-partitioned presence mark (standalone; k_score_packed<..., MARK> is the fused form).
+// XCD-partitioned presence mark (presence bytes; launch_cluster_local_bitmap turns them into bits).
 int launch_cluster_mark(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int L,
                         uint8_t* presence, hipStream_t s);
 int launch_cluster_local_bitmap(const ClusterLayout& cl, uint8_t* ws, uint64_t* bitmap_out,
@@ -304,9 +285,7 @@ int launch_cluster_local_bitmap(const ClusterLayout& cl, uint8_t* ws, uint64_t* 
 // presence bitmap straight from the codes by an 8-bit partition sort (7 <= L <= 13)
 int cluster_mark_bitmap_temp(int64_t n, int L, int64_t* bytes);
 int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int L,
-                               uint64_t* bitmap, void* temp, int64_t temp_bytes, hipStream_t s, int* n_parts = nullptr);
-// phases: 1 = rank tables + local CC, 2 = global rounds + labels (after phase 1 of the
-// same bitmaps), 3 = both
+                               uint64_t* bitmap, void* temp, int64_t temp_bytes, hipStream_t s);
 // The assign half of a fused score + assign: completes (deferred = false) or registers
 // (deferred = true, as launch_cluster_assign) the assign of codes into cluster_id, and
 // fills *a with the tables when the fused kernel can label these rows (word labels,
@@ -315,7 +294,7 @@ int cluster_assign_prepare(const ClusterLayout& cl, const uint8_t* ws, const uin
                            const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id, hipStream_t s,
                            bool deferred, AssignIn* a);
 int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t* bitmaps,
-                           int n_bitmaps, int max_distance, hipStream_t s, int phases = 3);
+                           int n_bitmaps, int max_distance, hipStream_t s);
 // Waits for an asynchronous resolve's round flags and completes it if needed.
 // *redone (nullable): 1 when more rounds (+ labels, + a deferred assign) were enqueued.
 int cluster_finish(const void* ws, hipStream_t s, int* redone = nullptr);
@@ -323,8 +302,6 @@ void cluster_release(const void* ws);
 int cluster_rounds(const void* ws, hipStream_t s, int* rounds);
 int cluster_set_spec_rounds(int n);
 int cluster_set_lookback_polls(int n);
-int cluster_set_global_mode(int mode);
-int cluster_set_edge_cap(int64_t pairs);
 int cluster_set_mark_method(int m);
 // deferred: enqueue without waiting for the resolve's flags (cluster_finish re-runs it
 // if the speculative rounds were not enough)

@@ -4,8 +4,9 @@
 //   k_stage         Arrow strings -> packed 2-bit SoA + regular bitmap + irregular list
 //   k_score_packed  THE hot kernel: one pass over the packed SoA computing all seven
 //                   complexity fields (umi_score.rs:17-43), Hamming distance/within
-//                   (expressions.rs:1048-1101) and the H3 presence mark. 4 rows per
-//                   lane: 16-B code loads, 2x16-B stores per f64 field, ballot-free
+//                   (expressions.rs:1048-1101), optionally the H3 cluster ids of a
+//                   resolved workspace. 4 rows per lane: 8-B code loads, 16-B stores
+//                   per f64 field, ballot-free
 //                   16-lane OR-reduction for the bit-packed Boolean output.
 //   k_score_rows    byte path for irregular rows (N, lowercase, other lengths, empty),
 //                   the reference's byte semantics restated per lane.
@@ -182,12 +183,12 @@ __device__ __forceinline__ uint32_t hamming_code(uint32_t code, const PackedPara
 // gathered right after the code load, so its latency hides behind the scoring; flagged
 // words read their exception mask, exception codes the per-code label table
 // (k_assign in cluster_kernels.hip is the standalone form, identical ids).
-// One 1024-row block tile of k_score_packed (and of the score part of k_score_assign_prev).
-template <bool SCORE, bool HAMD, bool HAMW, bool MARK, int LT, bool ASG>
+// One 1024-row block tile of k_score_packed.
+template <bool SCORE, bool HAMD, bool HAMW, int LT, bool ASG>
 __device__ __forceinline__ void score_tile(const int64_t tile, const uint32_t* __restrict__ codes,
                                            const uint64_t* __restrict__ regbits, int64_t n, const PackedParams& P,
                                            const ScoreOut& O, uint32_t* __restrict__ hd, uint64_t* __restrict__ hw,
-                                           uint8_t* __restrict__ pres, const AssignIn& A,
+                                           const AssignIn& A,
                                            const double (*s_tab)[kMaxPackedLen + 1]) {
     const int L = P.L;
     {
@@ -287,15 +288,10 @@ __device__ __forceinline__ void score_tile(const int64_t tile, const uint32_t* _
                     }
                 }
             }
-            if (MARK) {
-#pragma unroll
-                for (int k = 0; k < kRowsPerLane; ++k)
-                    if ((reg >> k) & 1u) pres[c[k]] = 1;  // benign same-value race
-            }
             if (ASG) {
                 // word labels (decode_word_label, rogtk_internal.h)
 #pragma unroll
-                for (int k = 0; k < kRowsPerLane; ++k) wl[k] = decode_word_label(wl[k], A.wexc, A.xl, c[k]);
+                for (int k = 0; k < kRowsPerLane; ++k) wl[k] = decode_word_label(wl[k], A.wexc, c[k]);
                 uint32_t id[kRowsPerLane];
 #pragma unroll
                 for (int k = 0; k < kRowsPerLane; ++k)
@@ -339,14 +335,13 @@ __device__ __forceinline__ void stage_tables(const PackedParams& P, double (*s_t
     __syncthreads();
 }
 
-template <bool SCORE, bool HAMD, bool HAMW, bool MARK, int LT = 0, bool ASG = false>
+template <bool SCORE, bool HAMD, bool HAMW, int LT = 0, bool ASG = false>
 __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restrict__ codes,
                                                           const uint64_t* __restrict__ regbits,
                                                           int64_t n, const PackedParams P,
                                                           const ScoreOut O,
                                                           uint32_t* __restrict__ hd,
-                                                          uint64_t* __restrict__ hw,
-                                                          uint8_t* __restrict__ pres, const AssignIn A,
+                                                          uint64_t* __restrict__ hw, const AssignIn A,
                                                           uint64_t* tspan) {
     span_enter(tspan);  // profiling only (NULL otherwise)
     __shared__ double s_tab[4][kMaxPackedLen + 1];
@@ -355,75 +350,7 @@ __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restr
     // 16-B (double2) store instruction of the wave writes 1 KB of contiguous output.
     // grid-stride over 1024-row block tiles (a capped grid keeps fewer waves in flight)
     for (int64_t tile = blockIdx.x; tile * kBlock * kRowsPerLane < n; tile += gridDim.x)
-        score_tile<SCORE, HAMD, HAMW, MARK, LT, ASG>(tile, codes, regbits, n, P, O, hd, hw, pres, A, s_tab);
-    span_exit(tspan);
-}
-
-// The label of one present regular code from the resolved tables (MODE 0: per-code table).
-__device__ __forceinline__ uint32_t code_label(const AssignIn& A, uint32_t c) {
-    const uint32_t wl = decode_word_label(A.wlab[c >> 6], A.wexc, A.xl, c);
-    return wl != 0xFFFFFFFFu ? wl : A.labelcode[c];
-}
-
-// 1024 rows of the previous batch's assign: lane l of wave w owns 4 consecutive rows, so
-// each 16-B load / store instruction of a wave covers 1 KB contiguous.
-__device__ __forceinline__ void assign_tile(const int64_t tile, const uint32_t* __restrict__ codes,
-                                            const uint64_t* __restrict__ regbits, int64_t n, const AssignIn& A) {
-    const int64_t r0 = tile * (kBlock * 4) + 4 * (int64_t)threadIdx.x;
-    if (r0 >= n) return;
-    uint32_t c[4] = {0, 0, 0, 0}, id[4];
-    uint32_t reg;
-    if (r0 + 4 <= n) {
-        const u32x4_t v = stream_load(reinterpret_cast<const u32x4_t*>(codes + r0));
-        c[0] = v.x; c[1] = v.y; c[2] = v.z; c[3] = v.w;
-        reg = regbits ? (uint32_t)(regbits[r0 >> 6] >> (r0 & 63)) & 0xFu : 0xFu;
-    } else {
-        reg = 0;
-        for (int k = 0; k < 4; ++k)
-            if (r0 + k < n) {
-                c[k] = codes[r0 + k];
-                if (!regbits || ((regbits[(r0 + k) >> 6] >> ((r0 + k) & 63)) & 1u)) reg |= 1u << k;
-            }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) id[k] = ((reg >> k) & 1u) ? code_label(A, c[k]) : 0xFFFFFFFFu;
-    if (r0 + 4 <= n) {
-        stream_store(u32x4_t{id[0], id[1], id[2], id[3]}, reinterpret_cast<u32x4_t*>(A.out + r0));
-    } else {
-        for (int k = 0; k < 4; ++k)
-            if (r0 + k < n) A.out[r0 + k] = id[k];
-    }
-}
-
-// Batch k's scores and batch k - 1's cluster ids in ONE launch (horizontal fusion, round
-// 4): the score tiles stream HBM writes while the assign tiles wait on L2 gathers, so
-// the two overlap inside the CUs, and the main stream pays one kernel boundary (~11 us
-// on gfx950) instead of two. Tiles are interleaved 1:1 (position 2i: score tile i, 2i+1:
-// assign tile i; past the shorter batch, the other role takes every position), so both
-// roles run from the first wave to the last and neither leaves a tail.
-template <bool SCORE, bool HAMD, bool HAMW, int LT>
-__global__ __launch_bounds__(kBlock) void k_score_assign_prev(const uint32_t* __restrict__ codes,
-                                                               const uint64_t* __restrict__ regbits, int64_t n,
-                                                               const PackedParams P, const ScoreOut O,
-                                                               uint32_t* __restrict__ hd, uint64_t* __restrict__ hw,
-                                                               const uint32_t* __restrict__ codes2,
-                                                               const uint64_t* __restrict__ regbits2, int64_t n2,
-                                                               const AssignIn A2, uint64_t* tspan) {
-    span_enter(tspan);
-    __shared__ double s_tab[4][kMaxPackedLen + 1];
-    const int64_t ts = (n + kBlock * kRowsPerLane - 1) / (kBlock * kRowsPerLane);
-    const int64_t ta = (n2 + kBlock * 4 - 1) / (kBlock * 4);
-    const int64_t both = 2 * min(ts, ta);
-    const int64_t b = blockIdx.x;
-    const bool is_score = b < both ? (b & 1) == 0 : ts > ta;
-    const int64_t t = b < both ? (b >> 1) : (b - both) + (ts > ta ? ta : ts);
-    if (is_score) {
-        if (SCORE) stage_tables(P, s_tab);
-        const AssignIn none{nullptr, nullptr, 0, nullptr, nullptr};
-        score_tile<SCORE, HAMD, HAMW, false, LT, false>(t, codes, regbits, n, P, O, hd, hw, nullptr, none, s_tab);
-    } else {
-        assign_tile(t, codes2, regbits2, n2, A2);
-    }
+        score_tile<SCORE, HAMD, HAMW, LT, ASG>(tile, codes, regbits, n, P, O, hd, hw, A, s_tab);
     span_exit(tspan);
 }
 
@@ -608,111 +535,49 @@ int launch_stage(const void* offsets, int offset_width, const uint8_t* values,
     return ROGTK_OK;
 }
 
-int launch_score_assign_prev(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, const PackedParams& p,
-                             const ScoreOut& o, uint32_t* hd, uint64_t* hw, const uint32_t* codes2,
-                             const uint64_t* regular_bits2, int64_t n2, const AssignIn& a2, hipStream_t s) {
-    const bool score = any_score(o), hamd = p.ham_mode && hd, hamw = p.ham_mode && hw;
-    ROGTK_REQUIRE(a2.out && a2.wlab && a2.labelcode, ROGTK_E_INVALID, "score_assign_prev: no word-label tables");
-    if (n <= 0 && n2 <= 0) return ROGTK_OK;
-    ProfScope prof(K_SCORE_PACKED, s, true);
-    const int64_t ts = (std::max<int64_t>(n, 0) + kBlock * kRowsPerLane - 1) / (kBlock * kRowsPerLane);
-    const int64_t ta = (std::max<int64_t>(n2, 0) + kBlock * 4 - 1) / (kBlock * 4);
-    const int g = (int)std::max<int64_t>(ts + ta, 1);
-    uint64_t* tspan = span_begin(K_SCORE_PACKED, g, s);
-    const int sel = (score ? 4 : 0) | (hamd ? 2 : 0) | (hamw ? 1 : 0);
-#define ROGTK_SAP(S, D, W, LT)                                                                                  \
-    hipExtLaunchKernelGGL((k_score_assign_prev<S, D, W, LT>), dim3(g), dim3(kBlock), 0, s, prof.start(),        \
-                          prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, codes2, regular_bits2, n2, a2, tspan)
-    if (p.L == 12 && sel == 4 + 1) ROGTK_SAP(true, false, true, 12);
-    else if (p.L == 12 && sel == 4 + 2 + 1) ROGTK_SAP(true, true, true, 12);
-    else
-        switch (sel) {
-            case 1: ROGTK_SAP(false, false, true, 0); break;
-            case 2: ROGTK_SAP(false, true, false, 0); break;
-            case 3: ROGTK_SAP(false, true, true, 0); break;
-            case 4: ROGTK_SAP(true, false, false, 0); break;
-            case 5: ROGTK_SAP(true, false, true, 0); break;
-            case 6: ROGTK_SAP(true, true, false, 0); break;
-            case 7: ROGTK_SAP(true, true, true, 0); break;
-            default: ROGTK_SAP(false, false, false, 0); break;
-        }
-#undef ROGTK_SAP
-    ROGTK_HIP_CHECK(hipGetLastError());
-    span_end(K_SCORE_PACKED, tspan, g, s);
-    return ROGTK_OK;
-}
-
 int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int64_t n,
-                        const PackedParams& p, const ScoreOut& o, uint32_t* hd, uint64_t* hw,
-                        uint8_t* presence, hipStream_t s, const AssignIn* asg) {
+                        const PackedParams& p, const ScoreOut& o, uint32_t* hd, uint64_t* hw, hipStream_t s,
+                        const AssignIn* asg) {
     if (n <= 0) return ROGTK_OK;
-    const AssignIn A = asg ? *asg : AssignIn{nullptr, nullptr, 0, nullptr};
+    const AssignIn A = asg ? *asg : AssignIn{nullptr, nullptr, nullptr, nullptr};
     const bool fused = A.out != nullptr;
-    const bool score = any_score(o), hamd = p.ham_mode && hd, hamw = p.ham_mode && hw,
-               mark = presence != nullptr;
-    if (!score && !hamd && !hamw && !mark) return ROGTK_OK;
-    ROGTK_REQUIRE(!fused || (!mark && (score || hamd || hamw)), ROGTK_E_UNSUPPORTED,
-                  "score_packed: a fused assign needs a score / Hamming output and no presence mark");
+    const bool score = any_score(o), hamd = p.ham_mode && hd, hamw = p.ham_mode && hw;
+    if (!score && !hamd && !hamw) return ROGTK_OK;
     // exact: the profiling events ride on the dispatch packet (kernel execution time only,
     // comparable with rocprofv3's kernel trace; bench.py's roofline.frac)
-    ProfScope prof(score || hamd || hamw ? K_SCORE_PACKED : K_MARK, s, true);
-    // ROGTK_SCORE_BLOCKS=k: at most k workgroups, grid-stride (A/B; default full grid)
-    static const int64_t cap = [] {
-        const char* e = getenv("ROGTK_SCORE_BLOCKS");
-        return e ? std::max<int64_t>(0, atoll(e)) : 0;
-    }();
-    int g = grid_for((n + kRowsPerLane - 1) / kRowsPerLane);
-    if (cap && g > cap) g = (int)cap;
-    const int sel = (score ? 8 : 0) | (hamd ? 4 : 0) | (hamw ? 2 : 0) | (mark ? 1 : 0);
+    ProfScope prof(K_SCORE_PACKED, s, true);
+    const int g = grid_for((n + kRowsPerLane - 1) / kRowsPerLane);
+    const int sel = (score ? 4 : 0) | (hamd ? 2 : 0) | (hamw ? 1 : 0);
     // profiling: the kernel's own execution span from in-kernel clocks (NULL otherwise)
-    uint64_t* tspan = (score || hamd || hamw) ? span_begin(K_SCORE_PACKED, g, s) : nullptr;
-#define ROGTK_SP(S, D, W, M)                                                                    \
-    case (S * 8 + D * 4 + W * 2 + M):                                                          \
-        hipExtLaunchKernelGGL((k_score_packed<S, D, W, M>), dim3(g), dim3(kBlock), 0, s,       \
-                              prof.start(), prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, \
-                              presence, A, tspan);                                               \
-        break;
-#define ROGTK_SPA(S, D, W)                                                                      \
-    case (S * 8 + D * 4 + W * 2):                                                              \
-        hipExtLaunchKernelGGL((k_score_packed<S, D, W, false, 0, true>), dim3(g), dim3(kBlock), 0, s, \
-                              prof.start(), prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, \
-                              presence, A, tspan);                                               \
+    uint64_t* tspan = span_begin(K_SCORE_PACKED, g, s);
+#define ROGTK_SP(S, D, W, ASG)                                                                    \
+    case (S * 4 + D * 2 + W):                                                                      \
+        hipExtLaunchKernelGGL((k_score_packed<S, D, W, 0, ASG>), dim3(g), dim3(kBlock), 0, s,      \
+                              prof.start(), prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, A, tspan); \
         break;
     // the bench / C2 configuration (12-bp UMIs, all fields + within bits) has a
-    // length-specialised instance (ROGTK_SCORE_GENERIC=1: runtime-length kernel, A/B)
-    static const bool generic = [] {
-        const char* e = getenv("ROGTK_SCORE_GENERIC");
-        return e && e[0] == '1';
-    }();
-    if (!generic && p.L == 12 && sel == 8 + 2) {
+    // length-specialised instance (the loops over bases unrolled; the generic kernel serves
+    // every other length and output set)
+    if (p.L == 12 && sel == 4 + 1) {
         if (fused)
-            hipExtLaunchKernelGGL((k_score_packed<true, false, true, false, 12, true>), dim3(g), dim3(kBlock), 0, s,
-                                  prof.start(), prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, presence, A,
-                                  tspan);
+            hipExtLaunchKernelGGL((k_score_packed<true, false, true, 12, true>), dim3(g), dim3(kBlock), 0, s,
+                                  prof.start(), prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, A, tspan);
         else
-            hipExtLaunchKernelGGL((k_score_packed<true, false, true, false, 12>), dim3(g), dim3(kBlock), 0, s,
-                                  prof.start(), prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, presence, A,
-                                  tspan);
-        ROGTK_HIP_CHECK(hipGetLastError());
-        span_end(K_SCORE_PACKED, tspan, g, s);
-        return ROGTK_OK;
-    }
-    if (fused) {
+            hipExtLaunchKernelGGL((k_score_packed<true, false, true, 12>), dim3(g), dim3(kBlock), 0, s,
+                                  prof.start(), prof.stop(), 0, codes, regular_bits, n, p, o, hd, hw, A, tspan);
+    } else if (fused) {
         switch (sel) {
-            ROGTK_SPA(0, 0, 1) ROGTK_SPA(0, 1, 0) ROGTK_SPA(0, 1, 1) ROGTK_SPA(1, 0, 0)
-            ROGTK_SPA(1, 0, 1) ROGTK_SPA(1, 1, 0) ROGTK_SPA(1, 1, 1)
+            ROGTK_SP(0, 0, 1, true) ROGTK_SP(0, 1, 0, true) ROGTK_SP(0, 1, 1, true) ROGTK_SP(1, 0, 0, true)
+            ROGTK_SP(1, 0, 1, true) ROGTK_SP(1, 1, 0, true) ROGTK_SP(1, 1, 1, true)
             default: break;
         }
     } else {
         switch (sel) {
-            ROGTK_SP(0, 0, 0, 1) ROGTK_SP(0, 0, 1, 0) ROGTK_SP(0, 0, 1, 1) ROGTK_SP(0, 1, 0, 0)
-            ROGTK_SP(0, 1, 0, 1) ROGTK_SP(0, 1, 1, 0) ROGTK_SP(0, 1, 1, 1) ROGTK_SP(1, 0, 0, 0)
-            ROGTK_SP(1, 0, 0, 1) ROGTK_SP(1, 0, 1, 0) ROGTK_SP(1, 0, 1, 1) ROGTK_SP(1, 1, 0, 0)
-            ROGTK_SP(1, 1, 0, 1) ROGTK_SP(1, 1, 1, 0) ROGTK_SP(1, 1, 1, 1)
+            ROGTK_SP(0, 0, 1, false) ROGTK_SP(0, 1, 0, false) ROGTK_SP(0, 1, 1, false) ROGTK_SP(1, 0, 0, false)
+            ROGTK_SP(1, 0, 1, false) ROGTK_SP(1, 1, 0, false) ROGTK_SP(1, 1, 1, false)
             default: break;
         }
     }
-#undef ROGTK_SPA
 #undef ROGTK_SP
     ROGTK_HIP_CHECK(hipGetLastError());
     span_end(K_SCORE_PACKED, tspan, g, s);

@@ -128,9 +128,8 @@ def stage_strings(offsets: torch.Tensor, values: torch.Tensor, n: int, umi_len: 
 def score_packed(batch: PackedBatch, scores: Optional[Dict[str, torch.Tensor]] = None,
                  target: Optional[bytes] = None, max_distance: int = 1,
                  hamming_distance: Optional[torch.Tensor] = None,
-                 hamming_within_bits: Optional[torch.Tensor] = None,
-                 cluster: Optional["ClusterEngine"] = None, stream=None) -> None:
-    """The fused hot kernel: H1 scores + H2 Hamming + H3 presence mark in one pass."""
+                 hamming_within_bits: Optional[torch.Tensor] = None, stream=None) -> None:
+    """The fused hot kernel: H1 scores + H2 Hamming in one pass over the codes."""
     t = None
     tl = 0
     if target is not None:
@@ -138,9 +137,7 @@ def score_packed(batch: PackedBatch, scores: Optional[Dict[str, torch.Tensor]] =
         t = ctypes.create_string_buffer(tb, max(len(tb), 1))
         tl = len(tb)
     _lib.call("rogtk_umi_score_packed", _p(batch.codes), _p(batch.regular_bits), batch.n, batch.umi_len,
-              _scores_struct(scores), t, tl, max_distance, _p(hamming_distance), _p(hamming_within_bits),
-              _p(cluster.ws) if cluster is not None else None,
-              cluster.max_distinct if cluster is not None else 0, _s(stream))
+              _scores_struct(scores), t, tl, max_distance, _p(hamming_distance), _p(hamming_within_bits), _s(stream))
 
 
 def score_assign_packed(batch: PackedBatch, engine: "ClusterEngine", cluster_id: torch.Tensor,
@@ -161,28 +158,6 @@ def score_assign_packed(batch: PackedBatch, engine: "ClusterEngine", cluster_id:
     _lib.call("rogtk_umi_score_assign_packed", _p(batch.codes), _p(batch.regular_bits), batch.n, batch.umi_len,
               _scores_struct(scores), t, tl, max_distance, _p(hamming_distance), _p(hamming_within_bits),
               _p(engine.ws), engine.max_distinct, _p(cluster_id), 1 if deferred else 0, _s(stream))
-
-
-def score_assign_prev_packed(batch: PackedBatch, scores: Optional[Dict[str, torch.Tensor]], target: Optional[bytes],
-                             max_distance: int, hamming_distance: Optional[torch.Tensor],
-                             hamming_within_bits: Optional[torch.Tensor], prev_engine: "ClusterEngine",
-                             prev_batch: PackedBatch, prev_cluster_id: torch.Tensor, stream=None) -> None:
-    """score_packed(batch) + prev_engine.assign(prev_batch, prev_cluster_id, deferred=True)
-    in ONE launch (rogtk_umi_score_assign_prev_packed: score tiles and assign tiles of the
-    two batches interleaved); read prev_cluster_id after prev_engine.sync()."""
-    t = None
-    tl = 0
-    if target is not None:
-        tb = target.encode() if isinstance(target, str) else bytes(target)
-        t = ctypes.create_string_buffer(tb, max(len(tb), 1))
-        tl = len(tb)
-    if prev_cluster_id.dtype != torch.int32 or prev_cluster_id.numel() < prev_batch.n or \
-            not prev_cluster_id.is_contiguous():
-        raise ValueError("prev_cluster_id: contiguous int32 with >= n elements")
-    _lib.call("rogtk_umi_score_assign_prev_packed", _p(batch.codes), _p(batch.regular_bits), batch.n, batch.umi_len,
-              _scores_struct(scores), t, tl, max_distance, _p(hamming_distance), _p(hamming_within_bits),
-              _p(prev_engine.ws), prev_engine.max_distinct, _p(prev_batch.codes), _p(prev_batch.regular_bits),
-              prev_batch.n, _p(prev_cluster_id), _s(stream))
 
 
 def score_rows(offsets: torch.Tensor, values: torch.Tensor, rows: torch.Tensor,
@@ -230,46 +205,28 @@ class ClusterEngine:
         _lib.call("rogtk_cluster_mark", _p(batch.codes), _p(batch.regular_bits), batch.n, self.umi_len,
                   _p(self.ws), self.max_distinct, _s(stream))
 
-    def mark_bitmap(self, batch: PackedBatch, stream=None, parts: bool = False):
+    def mark_bitmap(self, batch: PackedBatch, stream=None):
         """mark + build_local_bitmap in one: code slices or partition sort + LDS bitmap
-        (7 <= L <= 13). Returns local_bitmap; with parts=True returns (bitmaps, n): the
-        per-chunk partial bitmaps in the engine's scratch when the slice method leaves them
-        unmerged (their OR is the bitmap; resolve(bitmaps, n) ORs them as it scans, valid
-        until this engine's next mark), else (local_bitmap, 1)."""
+        (7 <= L <= 13). Returns local_bitmap."""
         need = ctypes.c_int64(0)
         _lib.call("rogtk_cluster_mark_bitmap_temp_bytes", batch.n, self.umi_len, ctypes.byref(need))
         if getattr(self, "_mark_temp", None) is None or self._mark_temp.numel() < need.value:
             self._mark_temp = torch.empty(need.value, dtype=torch.uint8, device=self.local_bitmap.device)
-        if not parts:
-            _lib.call("rogtk_cluster_mark_bitmap", _p(batch.codes), _p(batch.regular_bits), batch.n, self.umi_len,
-                      _p(self.local_bitmap), _p(self._mark_temp), self._mark_temp.numel(), _s(stream))
-            return self.local_bitmap
-        n_parts = ctypes.c_int(0)
-        _lib.call("rogtk_cluster_mark_bitmap_parts", _p(batch.codes), _p(batch.regular_bits), batch.n, self.umi_len,
-                  _p(self.local_bitmap), _p(self._mark_temp), self._mark_temp.numel(), ctypes.byref(n_parts),
-                  _s(stream))
-        if n_parts.value == 0:
-            return self.local_bitmap, 1
-        k = n_parts.value
-        return self._mark_temp[: k * self.words * 8].view(torch.int64), k
+        _lib.call("rogtk_cluster_mark_bitmap", _p(batch.codes), _p(batch.regular_bits), batch.n, self.umi_len,
+                  _p(self.local_bitmap), _p(self._mark_temp), self._mark_temp.numel(), _s(stream))
+        return self.local_bitmap
 
     def build_local_bitmap(self, stream=None) -> torch.Tensor:
         _lib.call("rogtk_cluster_local_bitmap", _p(self.ws), self.umi_len, self.max_distinct,
                   _p(self.local_bitmap), _s(stream))
         return self.local_bitmap
 
-    def resolve(self, bitmaps: torch.Tensor, n_bitmaps: int, max_distance: int, stream=None,
-                phase: int = 0) -> None:
-        """phase 0: the whole resolve; 1: rank tables + local components; 2: the global
-        rounds + labels (after phase 1 of the same bitmaps)."""
+    def resolve(self, bitmaps: torch.Tensor, n_bitmaps: int, max_distance: int, stream=None) -> None:
+        """Rank tables, components and labels of the OR of n_bitmaps bitmaps (enqueue-only)."""
         if bitmaps.numel() != n_bitmaps * self.words:
             raise ValueError("bitmaps must hold n_bitmaps * words int64 words")
-        if phase:
-            _lib.call("rogtk_cluster_resolve_phase", _p(self.ws), self.umi_len, self.max_distinct, _p(bitmaps),
-                      int(n_bitmaps), int(max_distance), int(phase), _s(stream))
-        else:
-            _lib.call("rogtk_cluster_resolve", _p(self.ws), self.umi_len, self.max_distinct, _p(bitmaps),
-                      int(n_bitmaps), int(max_distance), _s(stream))
+        _lib.call("rogtk_cluster_resolve", _p(self.ws), self.umi_len, self.max_distinct, _p(bitmaps),
+                  int(n_bitmaps), int(max_distance), _s(stream))
 
     def assign(self, batch: PackedBatch, cluster_id: torch.Tensor, stream=None, deferred: bool = False) -> None:
         """cluster ids of the batch's rows. deferred=True: no host wait for the resolve's
@@ -308,17 +265,6 @@ def set_lookback_polls(n: int) -> None:
     _lib.call("rogtk_cluster_set_lookback_polls", int(n))
 
 
-GLOBAL_UNION_FIND, GLOBAL_ROUNDS, GLOBAL_ROUNDS_ONE_FLATTEN, GLOBAL_EDGES = 1, 2, 3, 4
-
-
-def set_global_mode(mode: int) -> None:
-    """Global CC phase: 2 = hook + jump rounds over the bitmap cliques, speculative +
-    deferred (default, 0 restores it), 1 = one-pass CAS union-find, 3 = root-chasing
-    rounds + one flatten, 4 = one clique sweep + rounds over the crossing edges; all give
-    identical ids."""
-    _lib.call("rogtk_cluster_set_global_mode", int(mode))
-
-
 MARK_AUTO, MARK_SORT, MARK_SLICES = 0, 1, 2
 
 
@@ -326,11 +272,6 @@ def set_mark_method(method: int) -> None:
     """mark_bitmap method: 0 auto (LDS code slices for umi_len <= 12, partition sort for 13),
     1 partition sort, 2 code slices; identical bitmaps."""
     _lib.call("rogtk_cluster_set_mark_method", int(method))
-
-
-def set_edge_cap(pairs: int) -> None:
-    """(tests) Edge-list capacity of workspaces created from now on (mode 4); 0 = default."""
-    _lib.call("rogtk_cluster_set_edge_cap", int(pairs))
 
 
 def cluster_batch(engine: ClusterEngine, batch: PackedBatch, cluster_id: torch.Tensor,
@@ -507,21 +448,3 @@ def profile_read_span(kernel: str):
     n = ctypes.c_int64(0)
     _lib.call("rogtk_profile_read_span", kernel.encode(), ctypes.byref(ms), ctypes.byref(n))
     return ms.value, n.value
-
-
-def cu_mask_stream(exclude_every: int, device=None):
-    """A stream whose kernels run on every CU except those with index % exclude_every ==
-    exclude_every - 1 (rogtk_stream_create_cu_mask): the pipeline's main stream can leave
-    those CUs to the resolve chain (A/B). The HIP stream lives for the process."""
-    import torch
-
-    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
-    n = torch.cuda.get_device_properties(dev).multi_processor_count
-    words = (n + 31) // 32
-    mask = (ctypes.c_uint32 * words)()
-    for i in range(n):
-        if exclude_every <= 0 or i % exclude_every != exclude_every - 1:
-            mask[i // 32] |= 1 << (i % 32)
-    out = ctypes.c_void_p()
-    _lib.call("rogtk_stream_create_cu_mask", mask, words, ctypes.byref(out))
-    return torch.cuda.ExternalStream(out.value, device=dev)

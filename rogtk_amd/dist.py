@@ -21,17 +21,23 @@ import torch
 import torch.distributed as dist
 
 
+def collective(group=None) -> bool:
+    """A process group exists: the exchanges go through it (RCCL with backend "nccl"),
+    at world 1 too (tests/test_gpu_rccl.py runs the whole RCCL call sequence that way)."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def world(group=None) -> int:
-    if not (dist.is_available() and dist.is_initialized()):
+    if not collective(group):
         return 1
     return dist.get_world_size(group)
 
 
 def gather_bitmaps(local: torch.Tensor, group=None):
     """All-gather one bitmap per rank into a [world * words] tensor (rank-major)."""
-    n = world(group)
-    if n == 1:
+    if not collective(group):
         return local, 1
+    n = world(group)
     out = torch.empty(n * local.numel(), dtype=local.dtype, device=local.device)
     if dist.get_backend(group) == "nccl":
         dist.all_gather_into_tensor(out, local, group=group)
@@ -107,7 +113,7 @@ def route_rows(offsets: torch.Tensor, values: torch.Tensor, keys: torch.Tensor, 
     this rank now owns, ordered by source rank then source row."""
     W = world(group)
     n = keys.numel()
-    if W == 1:
+    if not collective(group):
         dev = keys.device
         return (offsets, values, keys, torch.zeros(n, dtype=torch.int32, device=dev),
                 torch.arange(n, dtype=torch.int64, device=dev))
@@ -260,7 +266,7 @@ def _a2a_var(t: torch.Tensor, send_counts, group=None):
     """Variable all-to-all of the rows of t (grouped by destination rank, send_counts[r]
     rows for rank r); returns the received rows, grouped by source rank."""
     W = world(group)
-    if W == 1:
+    if not collective(group):
         return t, [int(send_counts[0])]
     xd = _exchange_device(t, group)
     sc = torch.tensor([int(c) for c in send_counts], dtype=torch.int64, device=xd)
@@ -277,7 +283,7 @@ def _allgather_var(t: torch.Tensor, group=None):
     """All-gather of variable-length row blocks: the concatenation in rank order, and each
     rank's row count."""
     W = world(group)
-    if W == 1:
+    if not collective(group):
         return t, [t.shape[0]]
     xd = _exchange_device(t, group)
     nccl = dist.get_backend(group) == "nccl"

@@ -1,11 +1,10 @@
 """Streaming pipeline over packed batches: three HIP streams, `depth` batches in flight.
 
 The hot path has three phases with different limits on MI355X:
-  main stream     k_score_packed (H1 scores + H2 Hamming), then the local presence
-                  bitmap: by default an 8-bit partition sort of the codes + one LDS
-                  bitmap slice per partition (umi_len 7..13); else the XCD-partitioned
-                  presence mark (or the mark fused into k_score_packed) + the
-                  presence->bitmap pass: HBM-bandwidth bound
+  main stream     the local presence bitmap (umi_len 7..13: code slices in LDS, or a
+                  partition sort + one LDS bitmap slice per partition; else the
+                  XCD-partitioned presence mark + the presence->bitmap pass), then
+                  k_score_packed (H1 scores + H2 Hamming): HBM-bandwidth bound
   resolve stream  [RCCL all-gather of the bitmaps] + rank tables + LDS-local and
                   global connected components: latency bound (small tables, many
                   dependent steps)
@@ -32,7 +31,6 @@ wait for batch k-1's flags moves onto the critical cycle: 0.487 vs 0.430 ms/step
 """
 from __future__ import annotations
 
-import os
 from collections import deque
 from typing import Optional
 
@@ -40,7 +38,7 @@ import torch
 
 from . import device as D
 from .dist import gather_bitmaps
-from .dist import world as dist_world
+from .dist import collective as dist_collective
 
 
 _ON_MAIN = object()  # slot.assigned: the assign ran on the main stream, no event recorded
@@ -56,7 +54,6 @@ class _Slot:
         self.cid = torch.empty(max(n_max, 4), dtype=torch.int32, device=dev)
         self.assigned = None  # D.StreamEvent or torch.cuda.Event (UmiPipeline.device_events)
         self.resolved = None
-        self.parts = None  # (bitmaps, n): the batch's unmerged partial bitmaps (mark_parts)
 
 
 class UmiPipeline:
@@ -64,11 +61,9 @@ class UmiPipeline:
                  target: Optional[bytes] = b"ACGTACGTACGT", max_hamming: int = 1, max_distance: int = 1,
                  group=None, with_scores: bool = True, priorities=(0, 0, 0), mark: str = "auto",
                  on_assigned=None, score_alone: bool = False, exchange=None, resolve_streams: int = 1,
-                 assign_on: str = "main", split_resolve: bool = False, reuse_gate: str = "auto",
-                 assign_early: bool = True, mark_first="auto", device_events: bool = True,
-                 mark_stream: bool = False, fused_assign: bool = False, mark_parts: bool = False,
-                 with_distance: bool = False, assign_prev_fused: bool = False, assign_lag: int = 0,
-                 main_stream=None):
+                 assign_on: str = "main", reuse_gate: str = "auto", assign_early: bool = True,
+                 mark_first: bool = True, device_events: bool = True, mark_stream: bool = False,
+                 fused_assign: bool = False, with_distance: bool = False, assign_lag: int = 0):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
@@ -76,16 +71,14 @@ class UmiPipeline:
             mark = "sort" if 7 <= umi_len <= 13 else "xcd"
         if mark == "slices":  # the method of rogtk_cluster_mark_bitmap is a process-wide knob
             mark = "sort"
-        if mark not in ("xcd", "fused", "sort"):
-            raise ValueError("mark must be 'xcd' (XCD-partitioned mark kernel), 'fused' (inside k_score_packed) "
-                             "or 'sort' (partition sort + LDS bitmap, umi_len 7..13)")
+        if mark not in ("xcd", "sort"):
+            raise ValueError("mark must be 'xcd' (XCD-partitioned mark kernel) or 'sort' (code slices / partition "
+                             "sort + LDS bitmap, umi_len 7..13)")
         self.sort_mark = mark == "sort"
-        self.fused_mark = mark == "fused"
         self.slots = [_Slot(umi_len, max_distinct, n_max, dev, with_scores, with_distance) for _ in range(depth)]
         # priorities: (main, resolve, assign); lower = higher priority (torch convention)
         self.caller = torch.cuda.current_stream(dev)
-        # main_stream: a caller's stream for the main chain (e.g. device.cu_mask_stream)
-        self.main = main_stream if main_stream is not None else torch.cuda.Stream(dev, priority=priorities[0])
+        self.main = torch.cuda.Stream(dev, priority=priorities[0])
         self.main.wait_stream(self.caller)
         # resolve_streams > 1: consecutive batches resolve on different streams, so two
         # latency-bound resolve chains overlap (needs depth >= resolve_streams + 1)
@@ -117,12 +110,9 @@ class UmiPipeline:
         # mark_first: batch k's presence bitmap (mark) runs before its score kernel on the
         # main stream, so its resolve overlaps the score instead of following it (round 3:
         # 0.367-0.369 vs 0.398-0.408 ms/step at 10M reads, interleaved on one box; the score
-        # kernel then also runs beside fewer resolve kernels: 99 vs 130 us). "auto": on
-        # unless the mark is fused into the score kernel
-        if mark_first == "auto":
-            mark_first = not self.fused_mark
-        if mark_first and self.fused_mark:
-            raise ValueError("mark_first needs a separate mark (not mark='fused')")
+        # kernel then also runs beside fewer resolve kernels: 99 vs 130 us). (Round 4 also
+        # measured the presence mark fused into the score kernel as byte stores + a bitmap
+        # pass: 0.484 vs 0.305 ms/step; removed in round 5.)
         self.mark_first = mark_first
         # device_events: the cross-stream hand-offs use StreamEvents released at device
         # scope (rogtk_event_*) instead of torch events, whose system-scope release writes
@@ -134,8 +124,8 @@ class UmiPipeline:
         # previous resolve reads), so the main stream carries only score + assign and the
         # mark overlaps them; the resolve then waits for the mark and for the slot's
         # previous assign explicitly
-        if mark_stream and (split_resolve or self.fused_mark or assign_on == "resolve"):
-            raise ValueError("mark_stream needs a separate mark, split_resolve=False and assign_on != 'resolve'")
+        if mark_stream and assign_on == "resolve":
+            raise ValueError("mark_stream needs assign_on != 'resolve'")
         self.s_mark = torch.cuda.Stream(dev, priority=priorities[0]) if mark_stream else self.main
         if mark_stream:
             self.mark_first = True
@@ -144,9 +134,8 @@ class UmiPipeline:
         # a score pass and an assign pass). The main stream then runs mark(k) and
         # score+assign(k - depth + 1), so the resolve of a batch overlaps depth - 1 marks
         # and score+assign passes of earlier batches.
-        if fused_assign and (mark_stream or split_resolve or self.fused_mark or assign_on == "resolve"
-                             or depth < 2 or not with_scores):
-            raise ValueError("fused_assign needs depth >= 2, scores, a separate mark on the main stream and "
+        if fused_assign and (mark_stream or assign_on == "resolve" or depth < 2 or not with_scores):
+            raise ValueError("fused_assign needs depth >= 2, scores, the mark on the main stream and "
                              "assign_on != 'resolve'")
         self.fused_assign = fused_assign
         # score_alone: assign of the previous batch waits for this batch's score kernel,
@@ -158,16 +147,7 @@ class UmiPipeline:
         # across ranks the bitmap all-gather runs on its own stream, right behind the mark,
         # so it overlaps the previous batch's resolve instead of lengthening the resolve
         # stream's chain (a substituted exchange may reuse one buffer: it stays in line)
-        self.s_comm = (torch.cuda.Stream(dev) if exchange is None and not split_resolve and dist_world(group) > 1
-                       else None)
-        # mark_parts (one rank, code-slice mark): the mark stops before merging its per-chunk
-        # partial bitmaps and the resolve ORs them while it scans (rogtk_cluster_mark_bitmap_parts),
-        # one kernel and one kernel boundary fewer on the main stream. Across ranks the merged
-        # bitmap is what the all-gather sends. Off by default: measured slower (round 3: the
-        # resolve chain, which then reads 8 bitmaps, is critical: 0.333-0.338 vs 0.318-0.327
-        # ms/step, profiles/r03z_mark_parts_ab.txt).
-        self.mark_parts = (mark_parts and self.sort_mark and exchange is None and not split_resolve
-                           and assign_on != "resolve" and dist_world(group) == 1)
+        self.s_comm = torch.cuda.Stream(dev) if exchange is None and dist_collective(group) else None
         self.last_scored: Optional[torch.cuda.Event] = None
         self.k = 0
         self.last_assigned: Optional[torch.cuda.Event] = None
@@ -178,10 +158,6 @@ class UmiPipeline:
         if assign_on not in ("resolve", "separate", "main"):
             raise ValueError("assign_on must be 'resolve', 'separate' or 'main'")
         self.assign_on = assign_on
-        # split_resolve: the local phase of batch k's resolve (rank tables + LDS-local
-        # components, a function of its bitmaps only) runs on the main stream behind its
-        # mark, so it overlaps the global rounds of batch k-1 on the resolve stream
-        self.split_resolve = split_resolve
         if assign_on == "resolve" and resolve_streams != 1:
             raise ValueError("assign_on='resolve' uses one resolve stream")
         # reuse_gate: what waits for the assign of the slot's previous batch.
@@ -196,8 +172,8 @@ class UmiPipeline:
             raise ValueError("reuse_gate must be 'auto', 'score' or 'resolve'")
         if reuse_gate == "auto":
             reuse_gate = "score"
-        if reuse_gate == "resolve" and (on_assigned is not None or split_resolve):
-            raise ValueError("reuse_gate='resolve' needs on_assigned=None and split_resolve=False")
+        if reuse_gate == "resolve" and on_assigned is not None:
+            raise ValueError("reuse_gate='resolve' needs on_assigned=None")
         self.reuse_gate = reuse_gate
         # lazy_assigned: with the assign, the mark and the slot-reuse gate all on the main
         # stream, nothing waits for a slot's assign through an event: resolve(k + depth),
@@ -205,21 +181,11 @@ class UmiPipeline:
         # stream, which the host enqueues after assign(k) because assign lags its batch by
         # `lag` < depth submits. So no event is recorded after the assign (each record or
         # wait on the main stream costs ~12 us of device time in the round-3 timeline); one
-        # is recorded on demand by settle().
-        # (ROGTK_PIPE_EVENTS=all: record / wait every hand-off as before, A/B)
-        self.all_events = os.environ.get("ROGTK_PIPE_EVENTS", "") == "all"
-        self.lazy_assigned = (not self.all_events and self.s_assign is self.main and self.s_mark is self.main and reuse_gate == "score"
+        # is recorded on demand by settle(). (Recording every hand-off measured neutral.)
+        self.lazy_assigned = (self.s_assign is self.main and self.s_mark is self.main and reuse_gate == "score"
                               and assign_on == "main" and not fused_assign and on_assigned is None)
         if self.lazy_assigned:
             assert self.lag < len(self.slots), "the main stream must order assign(k) before mark(k + depth)"
-        # assign_prev_fused (round 4): batch k's score kernel also assigns batch k-1's ids
-        # (rogtk_umi_score_assign_prev_packed: one launch, score and assign tiles
-        # interleaved) instead of a score launch and an assign launch on the main stream
-        if assign_prev_fused and not (assign_on == "main" and self.mark_first and not self.fused_mark
-                                      and not fused_assign and with_scores and self.s_mark is self.main):
-            raise ValueError("assign_prev_fused needs assign_on='main', the mark first on the main stream, scores "
-                             "and no fused_assign")
-        self.assign_prev_fused = assign_prev_fused
 
     def submit(self, batch: D.PackedBatch):
         """Enqueue one batch; returns its slot. Scores and Hamming outputs are valid once the
@@ -229,7 +195,7 @@ class UmiPipeline:
         assign, not a settled one); the slot is settled before its reuse."""
         slot = self.slots[self.k % len(self.slots)]
         producer = torch.cuda.current_stream(self.main.device)  # batch producer -> main
-        if not self.all_events and (producer == self.main or producer.query()):
+        if producer == self.main or producer.query():
             pass  # nothing pending on the producer: no hand-off (saves an event wait per step)
         elif self.device_events:
             ready = D.StreamEvent()
@@ -250,13 +216,7 @@ class UmiPipeline:
         gate_resolve = self.reuse_gate == "resolve"
         if slot.assigned is not None and not gate_resolve and self.s_assign is not self.main:
             D.wait_for(self.main, slot.assigned)
-        if self.mark_first and self.assign_prev_fused:
-            marked = self._mark(slot, batch, gate_resolve)
-            if self.queue and len(self.queue) >= max(self.lag, 1):
-                self._score_assign_prev(slot, batch)
-            else:
-                self._score(slot, batch)
-        elif self.mark_first:
+        if self.mark_first:
             # the presence bitmap needs only the codes: mark first, so the latency-bound
             # resolve of this batch starts while its score kernel streams (host order:
             # mark, score, the previous assign, then the ~15 launches of the resolve, so no
@@ -287,60 +247,31 @@ class UmiPipeline:
     def _event(self):
         return D.StreamEvent() if self.device_events else torch.cuda.Event()
 
-    def _score_assign_prev(self, slot: _Slot, batch: D.PackedBatch):
-        """Batch k's scores and the oldest queued batch's assign in one launch on main."""
-        pslot, pbatch, resolved = self.queue.popleft()
-        D.wait_for(self.main, resolved)
-        if self.on_assigned is not None:  # the consumer reads final ids: complete the resolve first
-            pslot.eng.sync(stream=self.main)
-        D.score_assign_prev_packed(batch, slot.scores, self.target, self.max_hamming, slot.dist, slot.within,
-                                   pslot.eng, pbatch, pslot.cid, stream=self.main)
-        if self.on_assigned is not None:
-            with torch.cuda.stream(self.main):
-                self.on_assigned(pslot, pbatch)
-        pslot.assigned = _ON_MAIN if self.lazy_assigned else self._event()
-        if not self.lazy_assigned:
-            pslot.assigned.record(self.main)
-            self.last_assigned = pslot.assigned
-
     def _score(self, slot: _Slot, batch: D.PackedBatch):
-        D.score_packed(batch, slot.scores, self.target, self.max_hamming, slot.dist, slot.within,
-                       cluster=slot.eng if self.fused_mark else None, stream=self.main)
+        D.score_packed(batch, slot.scores, self.target, self.max_hamming, slot.dist, slot.within, stream=self.main)
         if self.score_alone and self.s_assign is not self.main:
             self.last_scored = self._event()
             self.last_scored.record(self.main)
 
     def _mark(self, slot: _Slot, batch: D.PackedBatch, gate_resolve: bool):
         """Presence bitmap of the batch on the mark stream (the main stream unless
-        mark_stream); returns its event (with the split resolve: after phase 1 of the
-        resolve, on the main stream)."""
+        mark_stream); returns its event."""
         ms = self.s_mark
         if (gate_resolve or ms is not self.main) and slot.resolved is not None:
             D.wait_for(ms, slot.resolved)  # the previous resolve read the bitmap
-        slot.parts = None
-        if self.mark_parts:
-            slot.parts = slot.eng.mark_bitmap(batch, stream=ms, parts=True)
-        elif self.sort_mark:
+        if self.sort_mark:
             slot.eng.mark_bitmap(batch, stream=ms)
         else:
-            if not self.fused_mark:
-                slot.eng.mark(batch, stream=ms)
+            slot.eng.mark(batch, stream=ms)
             slot.eng.build_local_bitmap(stream=ms)
-        if self.split_resolve:
-            with torch.cuda.stream(self.main):
-                bitmaps, nb = self.exchange(slot.eng.local_bitmap)
-                slot.eng.resolve(bitmaps, nb, self.max_distance, stream=self.main, phase=1)
         marked = self._event()
         marked.record(ms)
-        self._split_bitmaps = (bitmaps, nb) if self.split_resolve else None
         return marked
 
     def _resolve(self, slot: _Slot, marked, gate_resolve: bool):
         """[exchange on the comm stream], the resolve on a resolve stream after `marked`;
         returns the resolve's completion event."""
         sr = self.s_resolves[self.k % len(self.s_resolves)]
-        if self.split_resolve:
-            bitmaps, nb = self._split_bitmaps
         if self.s_comm is not None:
             with torch.cuda.stream(self.s_comm):
                 D.wait_for(self.s_comm, marked)
@@ -351,17 +282,12 @@ class UmiPipeline:
             D.wait_for(sr, marked)
             if (gate_resolve or self.s_mark is not self.main) and slot.assigned is not None:
                 D.wait_for(sr, slot.assigned)  # assign(k - depth) reads the tables rewritten here
-            if self.split_resolve:
-                slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr, phase=2)
+            if self.s_comm is not None:
+                D.wait_for(sr, gathered)
+                bitmaps.record_stream(sr)  # allocated on the comm stream
             else:
-                if self.s_comm is not None:
-                    D.wait_for(sr, gathered)
-                    bitmaps.record_stream(sr)  # allocated on the comm stream
-                elif slot.parts is not None:
-                    bitmaps, nb = slot.parts  # the mark's scratch: rewritten only after this resolve
-                else:
-                    bitmaps, nb = self.exchange(slot.eng.local_bitmap)
-                slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr)
+                bitmaps, nb = self.exchange(slot.eng.local_bitmap)
+            slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr)
             resolved = self._event()
             resolved.record(sr)
         return resolved
@@ -381,13 +307,11 @@ class UmiPipeline:
         self._settle(slot)
         if slot.assigned is not None:
             D.wait_for(self.main, slot.assigned)
-        D.score_packed(batch, slot.scores, self.target, self.max_hamming, slot.dist, slot.within,
-                       cluster=slot.eng if self.fused_mark else None, stream=self.main)
+        D.score_packed(batch, slot.scores, self.target, self.max_hamming, slot.dist, slot.within, stream=self.main)
         if self.sort_mark:
             slot.eng.mark_bitmap(batch, stream=self.main)
         else:
-            if not self.fused_mark:
-                slot.eng.mark(batch, stream=self.main)
+            slot.eng.mark(batch, stream=self.main)
             slot.eng.build_local_bitmap(stream=self.main)
         marked = self._event()
         marked.record(self.main)

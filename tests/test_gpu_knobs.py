@@ -45,29 +45,12 @@ np.savez({path!r}, **{{k: v.cpu().numpy() for k, v in out.items()}})
 """
 
 KNOBS = [
-    ({"ROGTK_LCC_LOOP": "1"}, "separate"),
     ({"ROGTK_LOCAL8": "0"}, "separate"),
     ({"ROGTK_SLICE_BUCKETS": "0"}, "separate"),
-    ({"ROGTK_BUCKET_ROWS": "2048"}, "main"),
-    ({"ROGTK_BUCKET_ROWS": "4096"}, "main"),
-    ({"ROGTK_SLICE_CHUNKS": "1"}, "main"),
-    ({"ROGTK_SLICE_CHUNKS": "16"}, "separate"),
-    ({"ROGTK_SLICE_CHUNKS": "2", "ROGTK_BUCKET_ROWS": "2048"}, "main"),
-    ({"ROGTK_WORD_EXC": "0"}, "separate"),
-    ({"ROGTK_LABEL_BY_INDEX": "1"}, "separate"),
-    ({"ROGTK_ASSIGN_GROUPS": "1", "ROGTK_ASSIGN_BLOCKS": "0"}, "separate"),
-    ({"ROGTK_ASSIGN_GROUPS": "4"}, "main"),
-    ({"ROGTK_SCORE_GENERIC": "1", "ROGTK_SCORE_BLOCKS": "512"}, "main"),
-    ({"ROGTK_RESOLVE_GRAPH": "1"}, "separate"),
     ({"ROGTK_LOCAL8_BIG": "0"}, "main"),
     ({"ROGTK_FUSED_SCAN": "0"}, "main"),
     ({"ROGTK_FUSED_SCAN": "0", "ROGTK_LOCAL8": "0"}, "separate"),
-    ({"ROGTK_LOCAL8_SINGLE": "1"}, "main"),
     ({"ROGTK_WORD_EXC1": "0"}, "main"),
-    ({"ROGTK_WXL": "1"}, "main"),
-    ({"ROGTK_WXL": "1", "ROGTK_WORD_EXC1": "0"}, "separate"),
-    ({"ROGTK_FUSED_CHECK": "0"}, "main"),
-    ({"ROGTK_FOLD_ROOT_SCAN": "0"}, "main"),
     ({"ROGTK_LCC_PREDICT": "0"}, "separate"),
 ]
 
@@ -100,53 +83,6 @@ def test_knob_matches_oracle(reference, tmp_path, knobs, assign_on):
     assert np.array_equal(z["run"].view(np.uint32), ref["longest_homopolymer_run"])
     bits = np.unpackbits(z["within"].view(np.uint8), bitorder="little")[:N].astype(bool)
     assert np.array_equal(bits, rw)
-
-
-PACK_CHILD = r"""
-import sys
-import numpy as np
-import torch
-sys.path.insert(0, {root!r})
-from rogtk_amd import device as D
-z = np.load({src!r})
-offs = torch.from_numpy(z["offsets"]).cuda()
-vals = torch.from_numpy(z["values"]).cuda()
-valid = torch.from_numpy(z["validity"]).cuda()
-pk = D.PackedReads(offs, vals, valid, 3)
-torch.cuda.synchronize()
-np.save({path!r}, pk.blocks.cpu().numpy())
-"""
-
-
-@pytest.mark.parametrize("variant", ["0", "1", "2"])
-def test_pack_variant_blocks_identical(tmp_path, variant):
-    """rogtk_pack_reads under every ROGTK_PACK variant writes the default variant's blocks
-    bit for bit (ragged, null, N / lowercase rows, a validity offset)."""
-    import torch
-
-    from rogtk_amd import device as D
-
-    rng = np.random.default_rng(7)
-    n = 70_001
-    lens = rng.integers(0, 200, n)
-    lens[::97] = 0
-    offs = np.zeros(n + 1, np.int64)
-    offs[1:] = np.cumsum(lens)
-    vals = rng.choice(np.frombuffer(b"ACGTACGTACGTNacgt", np.uint8), int(offs[-1]))
-    vbits = rng.random(n + 3) > 0.05
-    validity = np.packbits(vbits, bitorder="little")
-    src = str(tmp_path / "col.npz")
-    np.savez(src, offsets=offs, values=vals, validity=validity)
-    ref = D.PackedReads(torch.from_numpy(offs).cuda(), torch.from_numpy(vals).cuda(),
-                        torch.from_numpy(validity).cuda(), 3)
-    torch.cuda.synchronize()
-    ref_blocks = ref.blocks.cpu().numpy()
-    path = str(tmp_path / "blocks.npy")
-    env = dict(os.environ, ROGTK_PACK=variant)
-    r = subprocess.run([sys.executable, "-c", PACK_CHILD.format(root=ROOT, src=src, path=path)], env=env,
-                       capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stderr[-2000:]
-    assert np.array_equal(np.load(path), ref_blocks)
 
 
 KMER_CHILD = r"""
@@ -197,14 +133,14 @@ def _kmer_column(tmp_path):
     return src
 
 
-def test_kmer_insert_variant_identical(tmp_path):
-    """The class-3 LDS kernel's V = 1 and V = 2 insert loops (ROGTK_KMER_INSERT=1 / 2), and
-    the spectra without the repeat certificate (ROGTK_KMER_CERT=0) or without the minimizer
-    filter (ROGTK_KMER_MZ=0), are the default's bit for bit, over min_coverage 1 and 3.""" 
+def test_kmer_prune_knobs_identical(tmp_path):
+    """The spectra without the repeat certificate (ROGTK_KMER_CERT=0), without the minimizer
+    filter (ROGTK_KMER_MZ=0) or without both are the default's bit for bit, over
+    min_coverage 1, 3 and 30."""
     src = _kmer_column(tmp_path)
     outs = []
-    for i, knobs in enumerate(({}, {"ROGTK_KMER_INSERT": "1"}, {"ROGTK_KMER_INSERT": "2"}, {"ROGTK_KMER_CERT": "0"},
-                               {"ROGTK_KMER_MZ": "0"})):
+    for i, knobs in enumerate(({}, {"ROGTK_KMER_CERT": "0"}, {"ROGTK_KMER_MZ": "0"},
+                               {"ROGTK_KMER_CERT": "0", "ROGTK_KMER_MZ": "0"})):
         path = str(tmp_path / f"k{i}.npz")
         env = dict(os.environ, **knobs)
         r = subprocess.run([sys.executable, "-c", KMER_CHILD.format(root=ROOT, src=src, path=path)], env=env,

@@ -408,8 +408,8 @@ def _device_run(n, L=12, md=1, target=b"ACGTACGTACGT", seed=None, shards=1):
     cid = torch.empty(n, dtype=torch.int32, device="cuda")
     if shards == 1:
         eng = D.ClusterEngine(L, min(n, 4 ** L), "cuda")
-        D.score_packed(batch, scores, target, 1, hd, hw, cluster=eng)
-        D.cluster_batch(eng, batch, cid, md, marked=True)
+        D.score_packed(batch, scores, target, 1, hd, hw)
+        D.cluster_batch(eng, batch, cid, md)
         stats = eng.stats()
     else:
         # emulate `shards` ranks on one GPU: local bitmaps -> concatenation (= all-gather) -> resolve
@@ -421,7 +421,7 @@ def _device_run(n, L=12, md=1, target=b"ACGTACGTACGT", seed=None, shards=1):
             a, b = int(bounds[r]), int(bounds[r + 1])
             e = D.ClusterEngine(L, min(n, 4 ** L), "cuda")
             bt = D.PackedBatch(codes[a:b], L)
-            D.score_packed(bt, None, None, 1, None, None, cluster=e)
+            e.mark(bt)
             engs.append(e)
             bats.append((a, b, bt))
         gathered = torch.cat([e.build_local_bitmap().clone() for e in engs])
@@ -561,13 +561,17 @@ def test_dense_space_local_tilings_vs_oracle(rg, n_codes, expect_p0):
     assert p0 == expect_p0
 
 
+@pytest.mark.parametrize("poison", [False, True])
 @pytest.mark.parametrize("deferred", [False, True])
-def test_local_cc_prediction_redo(rg, deferred):
+def test_local_cc_prediction_redo(rg, deferred, poison):
     """One workspace, batches whose tilings change: sparse (8 positions, <= 8192 codes per
     tile), 19% dense (8 positions, <= 16384), 28% dense (7 positions), sparse again. Each
     resolve launches only the local-CC instance of the workspace's previous resolve; a
     mismatch flags S_REDO and cluster_finish redoes the local and global phases (and the
-    deferred assign). Ids equal the oracle's every time."""
+    deferred assign). Ids equal the oracle's every time. poison: the workspace is filled
+    with 0xFF bytes before every batch after the first, so the speculative kernels that
+    run behind a mismatched instance would read out-of-range parents if they did not stop
+    at S_REDO."""
     import torch
 
     from rogtk_amd import device as D
@@ -581,6 +585,8 @@ def test_local_cc_prediction_redo(rg, deferred):
         codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
         batch = D.PackedBatch(codes, 12)
         cid = torch.empty(n_codes, dtype=torch.int32, device="cuda")
+        if poison and i:
+            eng.ws.fill_(0xFF)
         eng.mark_bitmap(batch)
         eng.resolve(eng.local_bitmap, 1, 1)
         eng.assign(batch, cid, deferred=deferred)
@@ -638,8 +644,7 @@ def test_full_size_c2_properties(rg):
                           scores["combined_score"][:n].cpu().numpy().view(np.uint64))
 
 
-@pytest.mark.parametrize("prevfused", [False, True])
-def test_full_size_c2_bench_pipeline_all_outputs(rg, prevfused):
+def test_full_size_c2_bench_pipeline_all_outputs(rg):
     """BASELINE C2 through the bench's own path: 10M reads, UmiPipeline with bench.py's
     arguments (depth 2, slice-bucket mark, assign on the main stream, deferred assigns,
     device events), three submits of the batch as the bench's steps do; every output of
@@ -656,7 +661,7 @@ def test_full_size_c2_bench_pipeline_all_outputs(rg, prevfused):
     codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
     batch = D.PackedBatch(codes, L)
     pipe = UmiPipeline(L, min(n, 4 ** L), n, "cuda", depth=2, target=b"ACGTACGTACGT", max_distance=1,
-                       score_alone=True, with_distance=True, assign_prev_fused=prevfused)
+                       score_alone=True, with_distance=True)
     for _ in range(3):
         pipe.submit(batch)
     pipe.drain()
@@ -682,11 +687,9 @@ def test_full_size_c2_bench_pipeline_all_outputs(rg, prevfused):
         assert np.array_equal(slot.cid[:n].cpu().numpy().view(np.uint32), rc)
 
 
-@pytest.mark.parametrize("depth,nb,alone", [(4, 4, False), (2, 5, False), (1, 3, False), (3, 7, False),
-                                             (2, 6, True), (3, 5, True)])
-@pytest.mark.parametrize("mark", ["xcd", "fused", "sort"])
-@pytest.mark.parametrize("assign_on", ["resolve", "separate", "main", "main_mark_stream", "main_fused",
-                                       "main_prevfused"])
+@pytest.mark.parametrize("depth,nb,alone", [(4, 4, False), (2, 5, False), (1, 3, False), (3, 5, True)])
+@pytest.mark.parametrize("mark", ["xcd", "sort"])
+@pytest.mark.parametrize("assign_on", ["resolve", "separate", "main", "main_mark_stream", "main_fused"])
 def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assign_on):
     """rogtk_amd.pipeline (3 streams, `depth` batches in flight) == the sequential device
     path for EVERY batch (outputs copied out by the on_assigned hook before slot reuse)."""
@@ -701,10 +704,7 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assig
     outs = []
     mark_stream = assign_on == "main_mark_stream"
     fused = assign_on == "main_fused"
-    prevfused = assign_on == "main_prevfused"
-    if mark_stream or fused or prevfused:
-        if mark == "fused":
-            pytest.skip("a mark fused into the score kernel has no stream / pass of its own")
+    if mark_stream or fused:
         if fused and depth < 2:
             pytest.skip("the fused score + assign needs depth >= 2")
         assign_on = "main"
@@ -715,7 +715,7 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assig
 
     pipe = UmiPipeline(L, n, n, "cuda", depth=depth, target=b"ACGTACGTACGT", max_distance=1, mark=mark,
                        on_assigned=grab, score_alone=alone, assign_on=assign_on, mark_stream=mark_stream,
-                       fused_assign=fused, assign_prev_fused=prevfused)
+                       fused_assign=fused)
     keep = []
     for s in seeds:
         codes = torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda()
@@ -733,12 +733,11 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assig
         assert np.array_equal(g_long, scores["longest_homopolymer_run"][:n].cpu().numpy()), k
 
 
-@pytest.mark.parametrize("mark_parts", [True, False])
 @pytest.mark.parametrize("assign_on", ["main", "separate", "main_mark_stream", "main_fused", "resolve"])
-def test_pipeline_mark_parts(rg, mark_parts, assign_on):
-    """>= 2^20 rows: the code-slice mark leaves one partial bitmap per row chunk; with
-    mark_parts (an option) the resolve ORs them while it scans instead of a merge pass.
-    Every batch's ids, scores and Hamming bits equal the sequential device path."""
+def test_pipeline_segment_mark(rg, assign_on):
+    """>= 2^20 rows: the code-slice mark runs its segment (bucket) pass and merges one
+    partial bitmap per row chunk. Every batch's ids, scores and Hamming bits equal the
+    sequential device path."""
     import torch
 
     from rogtk_amd import device as D
@@ -755,14 +754,11 @@ def test_pipeline_mark_parts(rg, mark_parts, assign_on):
     mark_stream, fused = assign_on == "main_mark_stream", assign_on == "main_fused"
     pipe = UmiPipeline(L, n, n, "cuda", depth=2, target=b"ACGTACGTACGT", max_distance=1, on_assigned=grab,
                        assign_on="main" if mark_stream or fused else assign_on, mark_stream=mark_stream,
-                       fused_assign=fused, mark_parts=mark_parts)
-    assert pipe.mark_parts == (mark_parts and assign_on != "resolve")
+                       fused_assign=fused)
     keep = []
     for s in seeds:
         keep.append(D.PackedBatch(torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda(), L))
         pipe.submit(keep[-1])
-        if pipe.mark_parts:
-            assert pipe.slots[(pipe.k - 1) % 2].parts[1] > 1  # partials, not the merged bitmap
     pipe.drain()
     torch.cuda.synchronize()
     assert len(outs) == nb
@@ -877,10 +873,9 @@ def _chain_codes(rng, L, length, high_bases):
     return np.array([(c << shift0) | low for c in path], dtype=np.uint32)
 
 
-@pytest.mark.parametrize("gm", [2, 3, 4])
 @pytest.mark.parametrize("spec", [1, 2])
 @pytest.mark.parametrize("L", [12, 16])
-def test_deferred_rounds_match(rg, L, spec, gm):
+def test_deferred_rounds_match(rg, L, spec):
     """With fewer speculative rounds than the data needs, the rounds that assign runs
     after the (speculative) labels must give the same clusters: labels never clobber
     the forest."""
@@ -896,13 +891,11 @@ def test_deferred_rounds_match(rg, L, spec, gm):
     eng = D.ClusterEngine(L, n, "cuda")
     cid = torch.empty(n, dtype=torch.int32, device="cuda")
     try:
-        D.set_global_mode(gm)
         D.set_spec_rounds(spec)
         D.cluster_batch(eng, batch, cid, 1)
         rounds = eng.rounds()
     finally:
         D.set_spec_rounds(0)
-        D.set_global_mode(0)
     if spec == 1:
         assert rounds > spec  # the deferred path ran
     rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L)), L, 1)
@@ -910,12 +903,10 @@ def test_deferred_rounds_match(rg, L, spec, gm):
     assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc)
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3, 4])
 @pytest.mark.parametrize("L", [12, 16])
-def test_long_chains_need_extra_rounds(rg, L, mode):
-    """Long Hamming-1 paths (diameter >> speculative rounds) resolve exactly: the one-pass
-    union-find (mode 1) links them at once; with rounds (mode 2) the deferred completion in
-    assign must finish them."""
+def test_long_chains_need_extra_rounds(rg, L):
+    """Long Hamming-1 paths (diameter >> speculative rounds) resolve exactly: the deferred
+    completion in assign must finish them."""
     import torch
 
     from rogtk_amd import device as D
@@ -930,14 +921,10 @@ def test_long_chains_need_extra_rounds(rg, L, mode):
     batch = D.PackedBatch(codes, L)
     eng = D.ClusterEngine(L, n, "cuda")
     cid = torch.empty(n, dtype=torch.int32, device="cuda")
-    try:
-        D.set_global_mode(mode)
-        D.cluster_batch(eng, batch, cid, 1)
-        stats = eng.stats()
-        rounds = eng.rounds()
-    finally:
-        D.set_global_mode(0)
-    print(f"L={L} n={n} mode={mode} rounds={rounds}")
+    D.cluster_batch(eng, batch, cid, 1)
+    stats = eng.stats()
+    rounds = eng.rounds()
+    print(f"L={L} n={n} rounds={rounds}")
     rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L)), L, 1)
     assert stats["n_clusters"] == rk
     assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc)
@@ -946,9 +933,9 @@ def test_long_chains_need_extra_rounds(rg, L, mode):
 
 @pytest.mark.parametrize("n", [1_000_000, 6_000_000])
 @pytest.mark.parametrize("L", [10, 12, 14])
-def test_global_modes_identical(rg, L, n):
-    """Union-find (default) and hook + jump rounds give bit-identical ids on dense and
-    sparse code spaces (4^10 is saturated at these sizes, 4^14 is sparse)."""
+def test_dense_and_sparse_spaces(rg, L, n):
+    """Dense (4^10 saturated at these sizes) and sparse (4^14) code spaces: ids equal the
+    oracle's (1M) and are deterministic across two workspaces (6M)."""
     import torch
 
     from rogtk_amd import device as D
@@ -957,52 +944,17 @@ def test_global_modes_identical(rg, L, n):
     codes_h = synth.umi_codes(n, L, seed=L + n)
     codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
     batch = D.PackedBatch(codes, L)
-    out = {}
-    try:
-        for mode in (D.GLOBAL_ROUNDS, D.GLOBAL_UNION_FIND, D.GLOBAL_ROUNDS_ONE_FLATTEN, D.GLOBAL_EDGES):
-            D.set_global_mode(mode)
-            eng = D.ClusterEngine(L, min(n, 4 ** L), "cuda")
-            cid = torch.empty(n, dtype=torch.int32, device="cuda")
-            D.cluster_batch(eng, batch, cid, 1)
-            out[mode] = (cid.cpu().numpy(), eng.stats()["n_clusters"])
-    finally:
-        D.set_global_mode(0)
-    assert out[1][1] == out[2][1] == out[3][1] == out[4][1]
-    for m in (1, 3, 4):
-        assert np.array_equal(out[m][0], out[2][0]), m
-    if n <= 1_000_000:
-        rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L)), L, 1)
-        assert out[1][1] == rk
-        assert np.array_equal(out[1][0].view(np.uint32), rc)
-
-
-@pytest.mark.parametrize("cap", [1, 4096])
-@pytest.mark.parametrize("L", [10, 12, 16])
-def test_edge_list_overflow_falls_back(rg, L, cap):
-    """Mode 4 with an edge list far too small for the data: the overflow is detected and
-    the bitmap rounds finish from the round-0 hooks (flattened to stars), exactly."""
-    import torch
-
-    from rogtk_amd import device as D
-    from rogtk_amd import synth
-
-    n = 300_000
-    codes_h = synth.umi_codes(n, L, seed=5 + L)
-    codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
-    batch = D.PackedBatch(codes, L)
-    try:
-        D.set_global_mode(D.GLOBAL_EDGES)
-        D.set_edge_cap(cap)
+    out = []
+    for _ in range(2):
         eng = D.ClusterEngine(L, min(n, 4 ** L), "cuda")
         cid = torch.empty(n, dtype=torch.int32, device="cuda")
         D.cluster_batch(eng, batch, cid, 1)
-        stats = eng.stats()
-    finally:
-        D.set_edge_cap(0)
-        D.set_global_mode(0)
-    rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L)), L, 1)
-    assert stats["n_clusters"] == rk
-    assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc)
+        out.append((cid.cpu().numpy(), eng.stats()["n_clusters"]))
+    assert out[0][1] == out[1][1] and np.array_equal(out[0][0], out[1][0])
+    if n <= 1_000_000:
+        rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, L)), L, 1)
+        assert out[0][1] == rk
+        assert np.array_equal(out[0][0].view(np.uint32), rc)
 
 
 @pytest.mark.parametrize("n", [0, 1, 5000, 300_000, 3_000_000, 1_048_579])
@@ -1118,40 +1070,6 @@ def test_level2_transfers_pinned_and_pageable(rg):
     _lib.call("rogtk_umi_cluster_host", ctypes.c_void_p(offs.ctypes.data), 8, ctypes.c_void_p(vals.ctypes.data),
               vals.size, None, 0, n, L, 1, ctypes.c_void_p(cid.ctypes.data), ctypes.byref(nk), ctypes.byref(rl))
     assert nk.value == k_p and np.array_equal(_np(cid_p).astype(np.uint32), cid)
-
-
-@pytest.mark.parametrize("every", [8, 4])
-def test_pipeline_cu_mask_main_stream(rg, every):
-    """The main chain on a CU-masked stream (device.cu_mask_stream, bench --main-cu-every):
-    every batch's ids, scores and Hamming bits equal the sequential device path."""
-    import torch
-
-    from rogtk_amd import device as D
-    from rogtk_amd import synth
-    from rogtk_amd.pipeline import UmiPipeline
-
-    n, L, nb = 1_100_009, 12, 3
-    seeds = [synth.DEFAULT_SEED + 17 * k for k in range(nb)]
-    outs = []
-
-    def grab(slot, batch):
-        outs.append((slot.cid[:n].clone(), slot.within.clone(), slot.scores["combined_score"][:n].clone()))
-
-    pipe = UmiPipeline(L, n, n, "cuda", depth=2, target=b"ACGTACGTACGT", max_distance=1, on_assigned=grab,
-                       main_stream=D.cu_mask_stream(every))
-    keep = []
-    for s in seeds:
-        keep.append(D.PackedBatch(torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda(), L))
-        pipe.submit(keep[-1])
-    pipe.drain()
-    torch.cuda.synchronize()
-    assert len(outs) == nb
-    for k in range(nb):
-        _, scores, _, hw, cid, _ = _device_run(n, seed=seeds[k])
-        g_cid, g_w, g_comb = (t.cpu().numpy() for t in outs[k])
-        assert np.array_equal(g_cid, cid.cpu().numpy()), k
-        assert np.array_equal(g_w, hw.cpu().numpy()), k
-        assert np.array_equal(g_comb.view(np.uint64), scores["combined_score"][:n].cpu().numpy().view(np.uint64)), k
 
 
 @pytest.mark.parametrize("depth,rs,lag", [(3, 2, 0), (4, 2, 3), (4, 3, 0)])

@@ -3,7 +3,7 @@ import os, sys
 import numpy as np, torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from rogtk_amd import device as D, synth
-D.set_global_mode(int(os.environ.get("MODE", "0")))
+
 for n in [int(x) for x in os.environ.get("NS", "10000000,80000000").split(",")]:
     L = 12
     codes = torch.from_numpy(synth.umi_codes(n, L).view(np.int32)).cuda()

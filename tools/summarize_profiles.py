@@ -66,9 +66,6 @@ def main():
                      "KB*1024; FETCH_SIZE doubled (gfx950 reports half of wide streaming reads, "
                      "MI355X_MICROARCH.md HBM section); WRITE_SIZE exact for 16-B/lane streaming stores",
            "kernels": kernels}
-    sap = [k for k in kernels if k.startswith("k_score_assign_prev")]
-    if sap:  # bench.py --assign-prev-fused: the score launch that also assigns the previous batch
-        out["score_assign_prev_hbm_bytes_per_launch"] = kernels[sap[0]]["hbm_bytes"]
     asg = [k for k in kernels if k.startswith("k_assign")]
     if asg:  # bench.py's roofline.dominant reads this when k_assign takes the most time
         out["assign_hbm_bytes_per_launch"] = kernels[asg[0]]["hbm_bytes"]

@@ -38,6 +38,7 @@ def main():
     lo, hi = len(starts) // 10, len(starts) - 1 - len(starts) // 10
     per = defaultdict(lambda: defaultdict(list))
     kern = defaultdict(lambda: defaultdict(list))
+    offs = defaultdict(lambda: defaultdict(list))  # (start, end) of each launch, us after the step start
     for i in range(lo, hi):
         t0, t1 = starts[i], starts[i + 1]
         by_stream = defaultdict(list)
@@ -51,14 +52,21 @@ def main():
             per[name]["busy_us"].append(busy / 1e3)
             per[name]["span_us"].append(span / 1e3)
             per[name]["kernels"].append(len(ks))
+            seen = defaultdict(int)
             for b, e, _, n in ks:
                 kern[name][n].append((e - b) / 1e3)
+                offs[name][f"{n}#{seen[n]}"].append(((b - t0) / 1e3, (e - t0) / 1e3))
+                seen[n] += 1
         per["step"]["us"].append((t1 - t0) / 1e3)
     med = lambda xs: round(statistics.median(xs), 2)
     out = {"steps": hi - lo, "main_stream": main_s,
            "per_step": {k: {kk: med(vv) for kk, vv in v.items()} for k, v in per.items()},
            "kernels_us": {s: {n: [med(v), len(v) // max(hi - lo, 1)] for n, v in sorted(d.items())}
-                          for s, d in kern.items()}}
+                          for s, d in kern.items()},
+           # median start / end of each launch (n-th of its name in the step) after the step's score start
+           "offsets_us": {s: {n: [med([a for a, _ in v]), med([b for _, b in v])] for n, v in
+                              sorted(d.items(), key=lambda kv: statistics.median(a for a, _ in kv[1]))}
+                          for s, d in offs.items()}}
     print(json.dumps(out, indent=1))
     if len(sys.argv) > 2:
         json.dump(out, open(sys.argv[2], "w"), indent=1)
