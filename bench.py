@@ -407,6 +407,43 @@ def c3_workload(n: int = 100_000_000, steps: int = 3, warmup: int = 1, k: int = 
     return out
 
 
+# the single kernels of the C2 step profiled on their own (besides score / assign)
+STEP_KERNELS = ("k_slice_bucket", "k_slice_mark", "k_or_partials", "k_scan_rt", "k_local_cc", "k_hook_g", "k_jump",
+                "k_roots_check", "k_word_label")
+
+
+def kernel_bytes(kernel: str, n: int, L: int, n_distinct: int, score_bpr: float) -> float:
+    """Algorithmic HBM bytes of one launch (SURVEY §8(d) per-unit figures): n rows, the 4^L
+    code space (bitmap 4^L / 8 B, rank table 16 B per 64 codes, word labels 4 + 8 B per 64
+    codes), n_distinct present codes (4 B of f each). Rows: score 56.125 B, assign 8 B (code
+    in, id out), slice bucket 8 B (code in, segment out), slice mark 4 B + 8 chunk partial
+    bitmaps; resolve kernels: the tables they must read or write once."""
+    words = 4 ** L // 64
+    bm = 4 ** L // 8
+    return {"k_score_packed": n * score_bpr, "k_assign": n * 8.0, "k_slice_bucket": n * 8.0,
+            "k_slice_mark": n * 4.0 + 8 * bm, "k_or_partials": 9.0 * bm, "k_scan_rt": bm + words * 16.0,
+            "k_local_cc": words * 20.0 + n_distinct * 4.125, "k_hook_g": words * 20.0,
+            "k_jump": n_distinct * 8.0, "k_roots_check": n_distinct * 4.125,
+            "k_word_label": words * 32.0 + n_distinct * 4.0}.get(kernel, 0.0)
+
+
+def kernel_traffic(kernel: str, reads_per_launch: int):
+    """Corrected PMC HBM bytes per launch of `kernel` from the latest committed summary made
+    at the same reads per launch (its most-launched instance), or None."""
+    for path in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))):
+        try:
+            with open(path) as f:
+                j = json.load(f)
+        except Exception:
+            continue
+        if j.get("reads_per_launch", 10_000_000) != reads_per_launch:
+            continue
+        hits = [v for k, v in j.get("kernels", {}).items() if k == kernel or k.startswith(kernel + "<")]
+        if hits:
+            return max(hits, key=lambda v: v.get("launches_counted", 0)).get("hbm_bytes")
+    return None
+
+
 def load_traffic(reads_per_launch: int, fused: bool = False, key: str = None):
     """Per-launch HBM bytes of k_score_packed (its fused score + assign instance when
     `fused`; another kernel's by `key`) from the latest committed PMC summary made at the
@@ -554,12 +591,15 @@ def main():
     # Outside the timed region: a few more pipelined steps with every kernel bracketed,
     # for the per-phase breakdown (kernels_us; these steps are not timed).
     breakdown = {}
+    per_kernel = {}
     if not args.no_profile:
+        pipe.drain()  # the window then holds exactly w batches' kernels
         torch.cuda.synchronize()
         D.profile_select(None)
         D.profile_reset()
         D.profile_enable(True)
-        for _ in range(min(args.steps, 5)):
+        w = min(args.steps, 5)
+        for _ in range(w):
             step()
         pipe.drain()
         torch.cuda.synchronize()
@@ -569,6 +609,15 @@ def main():
             ms, launches = D.profile_read(k)
             if launches:
                 breakdown[k] = round(1000.0 * ms / launches, 2)
+        # every kernel of the step on its own dispatch-packet events (as rocprofv3's kernel
+        # trace: from the packet's start, so a kernel whose workgroups wait for CU room counts
+        # that wait), per launch and per step (all launches of one batch)
+        for name, k in (("k_score_packed", "score_packed"), ("k_assign", "cluster_assign")) + tuple(
+                (x, x) for x in STEP_KERNELS):
+            ms, launches = D.profile_read(k)
+            if launches:
+                per_kernel[name] = {"avg_us": round(1000.0 * ms / launches, 2), "launches_per_step": launches / w,
+                                    "per_step_us": round(1000.0 * ms / w, 2)}
     # Outside the timed region: the same score kernel launched alone (nothing else on
     # the GPU), so its duration is the kernel's own, not the pipeline-shared one.
     iso = None
@@ -622,23 +671,25 @@ def main():
         roof["step"] = {"algorithmic_bytes": int(step_bytes), "achieved": round(step_bytes / (el / args.steps) / 1e9, 1),
                         "frac": round(step_bytes / (el / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
                         "note": "whole pipelined step (all kernels, ms_per_step) vs SURVEY §8d's algorithmic bytes"}
-        # the kernel with the largest share of the step's device time among the two that
-        # stream every row (the resolve kernels move a few MB each): its §8(d) bytes and
-        # its corrected PMC traffic
-        cands = {roof["kernel"]: (kernels["score_packed"]["avg_us"], bpr, roof["traffic"])}
-        if "cluster_assign" in kernels and not args.fused_assign:
-            a_traffic, _ = load_traffic(count, key="assign_hbm_bytes_per_launch")
-            cands["k_assign"] = (kernels["cluster_assign"]["avg_us"], 8.0, a_traffic)
-        dk = max(cands, key=lambda k: cands[k][0])
-        d_us, d_bpr, d_traffic = cands[dk]
-        d_ach = count * d_bpr / (d_us * 1e-6) / 1e9
-        roof["dominant"] = {"kernel": dk, "avg_us": round(d_us, 2), "bytes_per_read": d_bpr,
-                            "algorithmic_bytes_per_launch": int(count * d_bpr), "achieved": round(d_ach, 1),
-                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(d_ach / HBM_PEAK_GBS, 4),
-                            "traffic": d_traffic,
-                            "traffic_ratio": round(d_traffic / (count * d_bpr), 3) if d_traffic else None,
-                            "per_step_us": {k: round(v[0], 2) for k, v in cands.items()},
-                            "timing": "HIP events on the kernel's dispatch packet, every launch of the timed region"}
+        # the kernel with the largest share of the step's device time among ALL kernels of the
+        # step (per_kernel: dispatch-packet events, untimed steps), against its §8(d) bytes
+        # (kernel_bytes) and its corrected PMC traffic from the latest committed summary
+        if per_kernel:
+            dk = max(per_kernel, key=lambda k: per_kernel[k]["per_step_us"])
+            d = per_kernel[dk]
+            d_bytes = kernel_bytes(dk, count, L, stats["n_distinct"], bpr)
+            d_ach = d_bytes / (d["avg_us"] * 1e-6) / 1e9
+            d_traffic = (traffic if dk == "k_score_packed" else kernel_traffic(dk, count))
+            roof["dominant"] = {"kernel": dk, "avg_us": d["avg_us"], "per_step_us": d["per_step_us"],
+                                "launches_per_step": d["launches_per_step"],
+                                "algorithmic_bytes_per_launch": int(d_bytes), "achieved": round(d_ach, 1),
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(d_ach / HBM_PEAK_GBS, 4),
+                                "traffic": d_traffic,
+                                "traffic_ratio": round(d_traffic / d_bytes, 3) if d_traffic else None,
+                                "per_step_us_all": {k: v["per_step_us"] for k, v in
+                                                    sorted(per_kernel.items(), key=lambda kv: -kv[1]["per_step_us"])},
+                                "timing": "HIP events on each kernel's dispatch packet, 5 untimed pipelined steps "
+                                          "after the timed region"}
         if iso:
             a_iso = count * bpr / (iso * 1e-6) / 1e9
             roof["isolated"] = {"avg_us": round(iso, 2), "achieved": round(a_iso, 1),
@@ -692,6 +743,7 @@ def main():
         "c3": c3,
         "cpu_baseline": cpu,
         "kernels_us": breakdown,
+        "kernels_per_step": per_kernel,
     }
     print(json.dumps(line), flush=True)
     if world > 1:

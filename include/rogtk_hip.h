@@ -351,10 +351,14 @@ int rogtk_kmer_spectrum_dev(const int64_t* offsets, const uint8_t* values, const
  * (block_words 8 only) says no 16-mer at an aligned position 16 j occurs again in the row,
  * so no k-mer with k_eff 32 occurs twice; the spectrum call then skips groups of fewer
  * such rows than min_coverage (nothing valid). block_words = rogtk_read_block_words(max_len):
- * 8, 16 or 32 (rows up to 224 / 480 / 992 bases), 0 when the column is too long. */
+ * 8, 16 or 32 (rows up to 224 / 480 / 992 bases), 0 when the column is too long.
+ * max_len (device int64, nullable; round 5): receives the column's longest row in bytes
+ * (a per-wave reduction inside the pack kernel, zeroed on `stream` first), so a caller
+ * without a bound packs at a guessed block size and repacks only when a row did not fit
+ * (the spectrum call rejects rows longer than its max_len on the device as well). */
 int rogtk_read_block_words(int64_t max_len);
 int rogtk_pack_reads(const int64_t* offsets, const uint8_t* values, const uint8_t* validity, int64_t validity_offset,
-                     int64_t n, int block_words, uint64_t* blocks, void* stream);
+                     int64_t n, int block_words, uint64_t* blocks, int64_t* max_len, void* stream);
 /* rogtk_kmer_spectrum_dev over a column packed by rogtk_pack_reads (same outputs,
  * bit-exact): each grouped row is staged from its block (whole 64-B lines) instead of
  * its ASCII bytes. offsets / values stay needed (capacities, the radix path). */

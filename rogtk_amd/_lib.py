@@ -167,7 +167,7 @@ SIGNATURES = {
     "rogtk_stream_wait_event": [_vp, _vp],
     "rogtk_event_query": [_vp, _P_I32],
     "rogtk_event_synchronize": [_vp],
-    "rogtk_pack_reads": [_vp, _vp, _vp, _i64, _i64, _i32, _vp, _vp],
+    "rogtk_pack_reads": [_vp, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp],
     "rogtk_kmer_spectrum_blocks": [_vp, _i32, _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _i64, _vp,
                                    _vp, _vp, _vp, _vp, _P_I64, _vp],
     "rogtk_kmer_spectrum_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i32, _i32, _i64, _i64, _vp,

@@ -38,7 +38,9 @@ const char* const kKernelNames[K_COUNT_] = {
     "cluster_bitmap", "cluster_scan",   "cluster_compact", "cluster_union",
     "cluster_flatten", "cluster_label", "cluster_assign", "cluster_irregular",
     "bam_fields",     "bam_scan",       "bam_fill",      "pack_reads",
-    "row_gather",     "kmer_lds",      "cluster_resolve", "kmer_minimizer"};
+    "row_gather",     "kmer_lds",      "cluster_resolve", "kmer_minimizer",
+    "k_slice_bucket", "k_slice_mark",  "k_or_partials",  "k_scan_rt",
+    "k_local_cc",     "k_hook_g",      "k_jump",         "k_roots_check", "k_word_label"};
 
 namespace {
 std::atomic<bool> g_prof{false};

@@ -461,15 +461,13 @@ __device__ __forceinline__ uint64_t multi_of4(uint64_t a, uint64_t b, uint64_t c
 }
 
 // ---------------------------------------------------------------- local CC
-// One workgroup owns 4^7 consecutive codes (256 bitmap words): every Hamming-1
-// edge at positions 0..6 stays inside it, so the whole union-find for those
-// positions runs in LDS. Positions 0..2 live inside one 64-bit word: their
-// components come from a bit-parallel BFS on the word mask (no atomics); positions
-// 3..6 unite whole word components that intersect (CAS union-find). Outputs are per
-// word (UR[w] = the shared local root of word w when all its codes are in one local
-// component, the common case once the code space is dense), the live vertices as bits
-// of index space (lroot, zeroed before: the local roots and the codes of the other
-// words), and f over index space for the live vertices.
+// One workgroup owns a tile of 4^LP consecutive codes (4^LP / 64 bitmap words): every
+// Hamming-1 edge at positions 0..LP-1 stays inside it, so the components over those
+// positions are found in LDS (local_cc_tile below). Outputs are per word (UR[w] = the
+// shared local root of word w when all its codes are in one local component, the common
+// case once the code space is dense), the live vertices as bits of index space (lroot,
+// zeroed before: the local roots and the codes of the other words), and f over index space
+// for the live vertices.
 #ifdef ROGTK_LCC_TIMING  // experiment builds (tools/lcc_timing.py): per-phase clocks of k_local_cc
 __device__ unsigned long long g_lcc_clk[8];
 #define LCC_T(k) do { __syncthreads(); if (threadIdx.x == 0) { const unsigned long long now_ = wall_clock64(); \
@@ -500,9 +498,8 @@ __device__ __forceinline__ uint32_t lfind(uint32_t* lf, uint32_t x) {
 }
 
 __device__ __forceinline__ void lunite(uint32_t* lf, uint32_t a, uint32_t b) {
-#ifdef ROGTK_LCC_NOUNITE
-    if (a == b + 100000u) lf[0] = 0;  // keeps the call sites alive
-    return;
+#ifdef ROGTK_LCC_COUNT
+    atomicAdd(&g_lcc_clk[6], 1ull);
 #endif
     for (;;) {
         a = lfind(lf, a);
@@ -517,6 +514,9 @@ __device__ __forceinline__ void lunite(uint32_t* lf, uint32_t a, uint32_t b) {
         if (__hip_atomic_compare_exchange_strong(lf + a, &expected, b, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_WORKGROUP))
             return;
+#ifdef ROGTK_LCC_COUNT
+        atomicAdd(&g_lcc_clk[7], 1ull);
+#endif
         a = expected;
     }
 }
@@ -553,43 +553,6 @@ __device__ __forceinline__ uint64_t word_component(uint64_t m, uint64_t seed_bit
     return word_component_any(m, seed_bit, dims);
 }
 
-// In-word components of one word, as phase 1 of k_local_cc leaves them: up to
-// kWordComps components of two or more codes (masks); every other code is a
-// singleton unless the word overflowed the list (then components come from BFS).
-constexpr int kWordComps = 4;
-struct WordComps {
-    uint64_t m;
-    uint64_t c[kWordComps];
-    int n;       // listed components; -1: overflow
-    bool one;    // the whole word is one component
-};
-
-__device__ __forceinline__ uint64_t comp_of(const WordComps& w, uint64_t seed_bit, int dims) {
-    if (w.one) return w.m;
-    if (w.n < 0) return word_component(w.m, seed_bit, dims);
-    uint64_t r = seed_bit;
-#pragma unroll
-    for (int k = 0; k < kWordComps; ++k)
-        if (k < w.n && (w.c[k] & seed_bit)) r = w.c[k];
-    return r;
-}
-
-// the union of the components of w that contain a bit of seed
-__device__ __forceinline__ uint64_t comps_any(const WordComps& w, uint64_t seed, int dims) {
-    if (!seed) return 0;
-    if (w.one) return w.m;
-    if (w.n < 0) return word_component_any(w.m, seed, dims);
-    uint64_t covered = 0, r = 0;
-#pragma unroll
-    for (int k = 0; k < kWordComps; ++k)
-        if (k < w.n) {
-            covered |= w.c[k];
-            if (w.c[k] & seed) r |= w.c[k];
-        }
-    return r | (seed & ~covered);
-}
-
-
 // The union-find runs over LOCAL RANKS (index - gbase) of the present codes, not over
 // local codes: a tile of nloc present codes needs nloc LDS slots. Instances:
 //  * LP = 8 (tiles of 4^8 codes = 1024 words, one thread per word, CAP 8192 ranks): when
@@ -603,231 +566,236 @@ __device__ __forceinline__ uint64_t comps_any(const WordComps& w, uint64_t seed,
 // dense 68 -> 51 us; the LP = 8 tiling now takes those spaces, so it was dropped - its
 // empty launch cost ~5 us of every resolve.)
 
-// One tile of TW words at word `base` (the body of k_local_cc / k_local_cc_loop).
-template <int CAP, int TW, int LP>
+// Pairs of present codes of word mask m that differ only at in-word position q (bit stride
+// 4^q) by d in 1..3 (the lower code's digit + d <= 3): bit b set <=> codes b and b + d * 4^q.
+__device__ __forceinline__ uint64_t inword_pairs(uint64_t m, int q, int d) {
+    const uint64_t keep = q == 0 ? (d == 1 ? 0x7777777777777777ull : d == 2 ? 0x3333333333333333ull
+                                                                            : 0x1111111111111111ull)
+                        : q == 1 ? (d == 1 ? 0x0FFF0FFF0FFF0FFFull : d == 2 ? 0x00FF00FF00FF00FFull
+                                                                            : 0x000F000F000F000Full)
+                                 : (d == 1 ? 0x0000FFFFFFFFFFFFull : d == 2 ? 0x00000000FFFFFFFFull
+                                                                            : 0x000000000000FFFFull);
+    return m & (m >> (d << (2 * q))) & keep;
+}
+
+// One tile of TW words at word `base` (the body of k_local_cc), NT threads, WPT = TW / NT
+// consecutive words per thread. Edge-centric (round 5): every Hamming-1 edge of the tile
+// (positions 0..lpos-1) between local ranks, except that a word whose codes already form
+// one component over the in-word positions (a BFS from its first code reaches all of them)
+// is a single vertex: its codes point at its first code, and a pair of such words that share
+// a bit is one edge. The edges go to an LDS list and are resolved by uniform hook + jump
+// rounds (round 4 united in-word component lists with one union-find chain per pair: 48 us
+// per workgroup at C2, most of it divergent, dependent LDS chains; the outputs are
+// identical):
+//   1. ranks (block scan), word masks, one-component flags, lf[r] = r (or the word's first
+//      code); 2a. the edge list; 2b. hook + jump rounds until no edge crosses two roots;
+//   3. outputs; 4. the live bits of index space by ballots over the codes' live marks
+//      (lf bit 31).
+// Roots are the smallest local rank of each component (hooks put the larger root under
+// the smaller), so the labels are those of the global phase's smallest-vertex rule.
+template <int CAP, int TW, int LP, int NT, int ECAP>
 __device__ __forceinline__ void local_cc_tile(const int64_t base, const uint4* __restrict__ RT, int64_t words, int L,
-                                              uint32_t* __restrict__ f, uint32_t* __restrict__ D,
-                                              uint32_t* __restrict__ UR, uint64_t* __restrict__ lroot,
-                                              int64_t rwords, int64_t max_distinct,
+                                              uint32_t* __restrict__ f, uint32_t* __restrict__ UR,
+                                              uint64_t* __restrict__ lroot, int64_t rwords, int64_t max_distinct,
                                               unsigned long long* __restrict__ stats) {
-    constexpr int kLrb = CAP / 64 + 2;
+    constexpr int WPT = TW / NT;
+    static_assert(WPT * NT == TW && WPT >= 1, "words per thread");
+    constexpr uint32_t kLive = 0x80000000u;
     __shared__ uint64_t wb[TW];
-    __shared__ uint64_t wcm[kWordComps][TW];  // listed component masks per word
     __shared__ uint32_t lpre[TW];
-    __shared__ uint32_t lf[CAP];  // by local rank; valid at the first code of each in-word component
-    __shared__ int8_t wcn[TW];    // listed components (-1 overflow)
-    __shared__ uint8_t wone[TW];  // the word's codes form one in-word component
-    __shared__ uint64_t lrb[kLrb];  // local-root bits of the block's index range
-    __shared__ uint32_t s_wave[TW / 64];
-    const int t = threadIdx.x;
+    __shared__ uint8_t wone[TW];
+    __shared__ uint32_t lf[CAP];  // by local rank: parent, then root | kLive
+    __shared__ uint32_t edges[ECAP];  // a | b << 16 (local ranks < 2^16)
+    __shared__ uint32_t s_wave[NT / 64];
+    __shared__ uint32_t s_ch[2];
+    const int t = threadIdx.x, lane = t & 63;
 #ifdef ROGTK_LCC_TIMING
     const unsigned long long t_entry_ = wall_clock64();
     unsigned long long t_last_ = t_entry_;
 #endif
     const int nw = (int)min<int64_t>(TW, words - base);
-    const uint4 e = t < nw ? RT[base + t] : make_uint4(0, 0, 0, 0);
-    const uint64_t m = rt_word(e);
-    uint32_t nloc;
-    const uint32_t ex = block_excl_scan<TW>((uint32_t)__popcll(m), s_wave, nloc);
-    for (int k = t; k < kLrb; k += TW) lrb[k] = 0;
-    const int lpos = L < LP ? L : LP;
-    wb[t] = m;
-    lpre[t] = ex;
-    const uint32_t gbase = RT[base].z;
-    const int indims = lpos < 3 ? lpos : 3;  // positions inside one 64-code word
-    // 1. components inside each word (positions 0..2): bit-parallel BFS on the word's
-    //    mask, once; each component is represented by its first code (lf[rank] = rank)
-    WordComps mine;
-    mine.m = m;
-    {
-        uint64_t rem = m;
-        int ncomp = 0, nl = 0;
+    const int w0 = t * WPT;
+    uint64_t m[WPT];
+    uint32_t tsum = 0;
 #pragma unroll
-        for (int k = 0; k < kWordComps; ++k) mine.c[k] = 0;
-        while (rem) {
-            const int b0 = __ffsll((long long)rem) - 1;
-            const uint64_t c = word_component(m, 1ull << b0, indims);
-            rem &= ~c;
-            const uint32_t r0 = ex + (uint32_t)__popcll(m & ((1ull << b0) - 1ull));
-            lf[r0] = r0;
-            ++ncomp;
-            if (c & (c - 1)) {  // two or more codes
-                if (nl < kWordComps) {
-#pragma unroll
-                    for (int k = 0; k < kWordComps; ++k)
-                        if (k == nl) mine.c[k] = c;
-                }
-                ++nl;
-            }
-        }
-        mine.n = nl > kWordComps ? -1 : nl;
-        mine.one = ncomp == 1;
-#pragma unroll
-        for (int k = 0; k < kWordComps; ++k) wcm[k][t] = mine.c[k];
-        wcn[t] = (int8_t)mine.n;
-        wone[t] = mine.one;
+    for (int i = 0; i < WPT; ++i) {
+        m[i] = w0 + i < nw ? rt_word(RT[base + w0 + i]) : 0ull;
+        tsum += (uint32_t)__popcll(m[i]);
     }
+    uint32_t nloc;
+    uint32_t ex[WPT];
+    ex[0] = block_excl_scan<NT>(tsum, s_wave, nloc);
+#pragma unroll
+    for (int i = 1; i < WPT; ++i) ex[i] = ex[i - 1] + (uint32_t)__popcll(m[i - 1]);
+    const uint32_t gbase = RT[base].z;
+    if (nloc > (uint32_t)CAP) {  // the scan's tiling choice rules this out
+        if (t == 0) stats[S_OVERFLOW] = 1;
+        return;
+    }
+    const int lpos = L < LP ? L : LP;
+    const int indims = lpos < 3 ? lpos : 3;  // positions inside one 64-code word
+    bool one[WPT];
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+        const int cnt = __popcll(m[i]);
+        one[i] = cnt <= 1 || (indims > 0 && word_component(m[i], m[i] & (~m[i] + 1ull), indims) == m[i]);
+        wb[w0 + i] = m[i];
+        lpre[w0 + i] = ex[i];
+        wone[w0 + i] = one[i];
+        for (int j = 0; j < cnt; ++j) lf[ex[i] + j] = one[i] ? ex[i] : ex[i] + j;
+    }
+    if (t < 2) s_ch[t] = 0;
     __syncthreads();
     LCC_T(0);
-    // 2. positions 3..lpos-1 join words 4^(p-3) apart: codes at the same bit of the 4
-    //    words of a group differ only at p, so two word components that share a bit
-    //    are adjacent; unite every intersecting pair of components (by the local rank
-    //    of each component's first code)
-    for (int task = t, per = nw >> 2; per > 0 && task < (lpos - 3) * per; task += TW) {
-        {
-            const int p = 3 + task / per, g = task % per, s2 = 2 * p - 6, stride = 1 << s2;
-            const int w0 = ((g >> s2) << (s2 + 2)) | (g & (stride - 1));
-            WordComps wv[4];
-            uint32_t lp[4];
-            bool all_one = true;
+    // 2a. the tile's edges: in-word pairs of the words that are not one component, then the
+    //     cross-word pairs at positions 3..lpos-1 (word w and w + d * 4^(p-3), same bit; one
+    //     edge between two one-component words), as (a | b << 16) over local ranks into the
+    //     edge list, or, past its capacity, united at once (lunite)
+    auto rank_of = [](uint32_t pre, uint64_t mask, int b) {
+        return pre + (uint32_t)__popcll(mask & ((1ull << b) - 1ull));
+    };
+    auto for_edges = [&](auto&& emit) {
 #pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                const int w = w0 + v * stride;
-                wv[v].m = wb[w];
-                wv[v].one = wone[w];
-                wv[v].n = wcn[w];
-                lp[v] = lpre[w];
-#pragma unroll
-                for (int k = 0; k < kWordComps; ++k) wv[v].c[k] = wcm[k][w];
-                all_one &= wv[v].one || wv[v].m == 0;
-            }
-            if (all_one) {
-                // each word is one component: unite every word with the first word of its
-                // linked group (<= 3 unites instead of one per linked pair; a dense tile
-                // links all 6 pairs of most groups)
-                uint32_t adj[4];
-#pragma unroll
-                for (int a = 0; a < 4; ++a) {
-                    adj[a] = 1u << a;
-#pragma unroll
-                    for (int b = 0; b < 4; ++b)
-                        if (b != a && (wv[a].m & wv[b].m)) adj[a] |= 1u << b;
-                }
-#pragma unroll
-                for (int it = 0; it < 2; ++it)  // closure: 4 nodes, diameter <= 3
-#pragma unroll
-                    for (int a = 0; a < 4; ++a) {
-                        uint32_t r = adj[a];
-#pragma unroll
-                        for (int b = 0; b < 4; ++b)
-                            if ((adj[a] >> b) & 1u) r |= adj[b];
-                        adj[a] = r;
-                    }
-#pragma unroll
-                for (int a = 1; a < 4; ++a) {
-                    const int lead = __ffs((int)adj[a]) - 1;
-                    if (lead != a) lunite(lf, lp[lead], lp[a]);  // first code = rank lp
-                }
-            } else {
-#pragma unroll
-                for (int x = 0; x < 3; ++x) {
-                    uint64_t later = 0;
-#pragma unroll
-                    for (int y = x + 1; y < 4; ++y) later |= wv[y].m;
-                    // only components that meet a later word matter
-                    uint64_t rem = comps_any(wv[x], wv[x].m & later, indims);
-                    while (rem) {
-                        const int ba = __ffsll((long long)rem) - 1;
-                        const uint64_t ca = comp_of(wv[x], 1ull << ba, indims);
-                        rem &= ~ca;
-                        const uint32_t ra = lp[x] + (uint32_t)__popcll(wv[x].m & ((1ull << ba) - 1ull));
-#pragma unroll
-                        for (int y = x + 1; y < 4; ++y) {
-                            uint64_t z = ca & wv[y].m;
-                            while (z) {
-                                const uint64_t cb = comp_of(wv[y], z & (~z + 1ull), indims);
-                                z &= ~cb;
-                                const int bb = __ffsll((long long)cb) - 1;
-                                lunite(lf, ra, lp[y] + (uint32_t)__popcll(wv[y].m & ((1ull << bb) - 1ull)));
-                            }
+        for (int i = 0; i < WPT; ++i) {
+            const uint64_t mi = m[i];
+            if (!mi) continue;
+            const int w = w0 + i;
+            if (!one[i]) {
+                for (int q = 0; q < indims; ++q)
+                    for (int d = 1; d <= 3; ++d) {
+                        uint64_t e = inword_pairs(mi, q, d);
+                        while (e) {
+                            const int b = __ffsll((long long)e) - 1;
+                            e &= e - 1;
+                            emit(rank_of(ex[i], mi, b), rank_of(ex[i], mi, b + (d << (2 * q))));
                         }
                     }
+            }
+            for (int p = 3; p < lpos; ++p) {
+                const int sh = 2 * (p - 3);
+                const int a = (w >> sh) & 3;
+                for (int d = 1; a + d <= 3; ++d) {
+                    const int w2 = w + (d << sh);
+                    const uint64_t m2 = wb[w2];
+                    uint64_t z = mi & m2;
+                    if (!z) continue;
+                    const uint32_t pre2 = lpre[w2];
+                    if (one[i] && wone[w2]) {
+                        emit(ex[i], pre2);
+                        continue;
+                    }
+                    while (z) {
+                        const int b = __ffsll((long long)z) - 1;
+                        z &= z - 1;
+                        emit(one[i] ? ex[i] : rank_of(ex[i], mi, b), rank_of(pre2, m2, b));
+                    }
                 }
             }
         }
+    };
+    // the count pass by popcounts (no per-edge loop)
+    uint32_t ecount = 0;
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+        const uint64_t mi = m[i];
+        if (!mi) continue;
+        const int w = w0 + i;
+        if (!one[i])
+            for (int q = 0; q < indims; ++q)
+                for (int d = 1; d <= 3; ++d) ecount += (uint32_t)__popcll(inword_pairs(mi, q, d));
+        for (int p = 3; p < lpos; ++p) {
+            const int sh = 2 * (p - 3);
+            const int a = (w >> sh) & 3;
+            for (int d = 1; a + d <= 3; ++d) {
+                const int w2 = w + (d << sh);
+                const uint64_t z = mi & wb[w2];
+                ecount += one[i] && wone[w2] ? (z ? 1u : 0u) : (uint32_t)__popcll(z);
+            }
+        }
     }
+    uint32_t etot;
+    uint32_t ek = block_excl_scan<NT>(ecount, s_wave, etot);
+    for_edges([&](uint32_t a, uint32_t b) {
+        if (ek < (uint32_t)ECAP) edges[ek] = a | (b << 16);
+        else lunite(lf, a, b);
+        ++ek;
+    });
     __syncthreads();
     LCC_T(1);
-    // 3a. compress: every component root of word t points at its final root (a
-    //     concurrent reader sees the old parent or the final root: both ancestors)
-    {
-        uint64_t rem = m;
-        while (rem) {
-            const int b0 = __ffsll((long long)rem) - 1;
-            rem &= ~comp_of(mine, 1ull << b0, indims);
-            const uint32_t r0 = ex + (uint32_t)__popcll(m & ((1ull << b0) - 1ull));
-            uint32_t root = r0;
+    // 2b. hook + jump rounds over the listed edges (Shiloach-Vishkin in LDS): jump = every
+    //     vertex to its root (stars); hook = for every edge whose ends' roots differ, the
+    //     larger root under the smaller (atomicMin). Parents only ever point at smaller
+    //     vertices, so a component's smallest local rank is never hooked and ends as its
+    //     root. Uniform passes (vertices / edges dealt over the threads) instead of one
+    //     union-find chain per edge; s_ch[r & 1] = some hook in round r (reset a round ahead)
+    const uint32_t ne = min(etot, (uint32_t)ECAP);
+    for (int r = 0;; ++r) {
+        for (uint32_t v = t; v < nloc; v += NT) {
+            uint32_t root = lf[v];
+            if (root == v) continue;
             for (uint32_t q = lds_ld(lf + root); q != root; q = lds_ld(lf + root)) root = q;
-            if (root != r0) __hip_atomic_store(lf + r0, root, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(lf + v, root, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+        __syncthreads();
+        if (t == 0) s_ch[(r + 1) & 1] = 0;  // every thread read it after the previous round's barrier
+        bool ch = false;
+        for (uint32_t j = t; j < ne; j += NT) {
+            const uint32_t ed = edges[j];
+            const uint32_t ra = lds_ld(lf + (ed & 0xFFFFu)), rb = lds_ld(lf + (ed >> 16));
+            if (ra != rb) {
+                atomicMin(lf + max(ra, rb), min(ra, rb));
+                ch = true;
+            }
+        }
+        if (ch) s_ch[r & 1] = 1;
+        __syncthreads();
+        if (!s_ch[r & 1]) break;  // no hook: the jump above left stars
     }
-    __syncthreads();
     LCC_T(2);
-    // 3b. outputs of word t, per in-word component (lf[first] is now the final root):
-    //     UR = the word's shared local root (global index) or kNone, the live bits,
-    //     f[local root] = itself, f[i] = its local root for the codes of words without
-    //     a shared root (the only ones the rounds read by code). (No index -> code table:
-    //     the labels run per word, k_word_label.)
+    // 3b. outputs of this thread's words: UR = the word's shared local root (global index)
+    //     or kNone; f[root] = root; the codes of a word without a shared root are all live
+    //     with f[i] = their root (the global rounds read them by code); live codes marked
     if (t == 0 && (int64_t)gbase + nloc > max_distinct) stats[S_OVERFLOW] = 1;
-    if (t < nw) {
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+        const int w = w0 + i;
+        if (w >= nw) continue;
+        const int cnt = __popcll(m[i]);
         uint32_t first = kNone;
         bool uniform = true;
-        uint64_t rem = m;
-        while (rem) {
-            const int b0 = __ffsll((long long)rem) - 1;
-            rem &= ~comp_of(mine, 1ull << b0, indims);
-            const uint32_t r0 = ex + (uint32_t)__popcll(m & ((1ull << b0) - 1ull));
-            const uint32_t root = lf[r0];
-            const uint32_t rr = gbase + root;
-            if (first == kNone) first = rr;
-            uniform &= rr == first;
-            if (root == r0) {
-                if ((int64_t)rr < max_distinct) f[rr] = rr;
-                const uint32_t k = (gbase & 63u) + root;  // bit of the block's staging
-                atomicOr((unsigned long long*)&lrb[k >> 6], 1ull << (k & 63));
+        for (int j = 0; j < cnt; ++j) {
+            const uint32_t root = lf[ex[i] + j];
+            if (j == 0) first = root;
+            uniform &= root == first;
+        }
+        for (int j = 0; j < cnt; ++j) {
+            const uint32_t r = ex[i] + j, root = lf[r];
+            const int64_t gi = (int64_t)gbase + r;
+            if (root == r || !uniform) {
+                if (gi < max_distinct) f[gi] = gbase + root;
+                lf[r] = root | kLive;
             }
         }
-        if (m && !uniform) {
-            // codes of a word whose components keep different roots: f[i] = root index,
-            // and all of them are live (the rounds read them by code, so jumps keep them
-            // pointing at their root)
-            {
-                const uint32_t k0 = (gbase & 63u) + ex, cnt = (uint32_t)__popcll(m);
-                const uint32_t off = k0 & 63u;
-                const uint64_t range = cnt == 64 ? ~0ull : ((1ull << cnt) - 1ull);
-                atomicOr((unsigned long long*)&lrb[k0 >> 6], range << off);
-                if (off + cnt > 64) atomicOr((unsigned long long*)&lrb[(k0 >> 6) + 1], range >> (64 - off));
-            }
-            uint64_t r2 = m;
-            while (r2) {
-                const int b0 = __ffsll((long long)r2) - 1;
-                uint64_t cc = comp_of(mine, 1ull << b0, indims);
-                r2 &= ~cc;
-                const uint32_t rr = gbase + lf[ex + (uint32_t)__popcll(m & ((1ull << b0) - 1ull))];
-                while (cc) {
-                    const int b = __ffsll((long long)cc) - 1;
-                    cc &= cc - 1;
-                    const int64_t gi = (int64_t)gbase + ex + (uint32_t)__popcll(m & ((1ull << b) - 1ull));
-                    if (gi < max_distinct) f[gi] = rr;
-                }
-            }
-        }
-        UR[base + t] = (m && uniform) ? first : kNone;
+        UR[base + w] = (cnt && uniform) ? gbase + first : kNone;
     }
     __syncthreads();
-    // index-space live words: the block owns the interior words of its range; the
-    // first and last are shared with the neighbouring blocks (atomic OR, zeroed before)
+    // 4. index-space live words: the block owns the interior words of its range; the first
+    //    and last are shared with the neighbouring blocks (atomic OR, zeroed before)
     {
-        const uint32_t nlw = nloc ? ((gbase & 63u) + nloc + 63u) / 64u : 0u;
-        const int64_t w0 = (int64_t)(gbase >> 6);
-        for (uint32_t k = t; k < nlw; k += TW) {
-            const int64_t w = w0 + k;
-            if (w >= rwords) break;
-            const uint64_t v = lrb[k];
-            if (k == 0 || k == nlw - 1) {
-                if (v) atomicOr((unsigned long long*)(lroot + w), (unsigned long long)v);
-            } else {
-                lroot[w] = v;
+        const uint32_t off = gbase & 63u;
+        const uint32_t nlw = nloc ? (off + nloc + 63u) / 64u : 0u;
+        const int64_t lw0 = (int64_t)(gbase >> 6);
+        for (uint32_t k = t >> 6; k < nlw; k += NT / 64) {
+            const int64_t w = lw0 + k;
+            const int64_t r = (int64_t)k * 64 + lane - off;
+            const bool live = r >= 0 && r < (int64_t)nloc && (lf[r] & kLive);
+            const uint64_t v = __ballot(live);
+            if (lane == 0 && w < rwords) {
+                if (k == 0 || k == nlw - 1) {
+                    if (v) atomicOr((unsigned long long*)(lroot + w), (unsigned long long)v);
+                } else {
+                    lroot[w] = v;
+                }
             }
         }
     }
@@ -840,13 +808,15 @@ __device__ __forceinline__ void local_cc_tile(const int64_t base, const uint4* _
 #endif
 }
 
-template <int CAP, int TW, int LP>
-__global__ __launch_bounds__(TW) void k_local_cc(const uint4* __restrict__ RT, int64_t words, int L,
-                                                 uint32_t* __restrict__ f, uint32_t* __restrict__ D,
-                                                 uint32_t* __restrict__ UR, uint64_t* __restrict__ lroot,
-                                                 int64_t rwords, int64_t max_distinct,
-                                                 unsigned long long* __restrict__ stats, bool any_cap = false,
-                                                 bool alone = false) {
+#ifndef ROGTK_LCC_NT8
+#define ROGTK_LCC_NT8 1024  // threads of an 8-position local-CC workgroup (experiments)
+#endif
+template <int CAP, int TW, int LP, int NT = TW>
+__global__ __launch_bounds__(NT) void k_local_cc(const uint4* __restrict__ RT, int64_t words, int L,
+                                                 uint32_t* __restrict__ f, uint32_t* __restrict__ UR,
+                                                 uint64_t* __restrict__ lroot, int64_t rwords,
+                                                 int64_t max_distinct, unsigned long long* __restrict__ stats,
+                                                 bool any_cap = false, bool alone = false) {
     // the other tiling, or the other 8-position instance (any_cap: this one takes both caps)
     const bool mine = ((int)stats[S_P0] == 8 ? 8 : 7) == LP &&
                       (LP != 8 || any_cap || (int)stats[S_LCAP] == (CAP > kLocal8Cap ? 1 : 0));
@@ -855,7 +825,13 @@ __global__ __launch_bounds__(TW) void k_local_cc(const uint4* __restrict__ RT, i
         if (alone && blockIdx.x == 0 && threadIdx.x == 0) stats[S_REDO] = 1;
         return;
     }
-    local_cc_tile<CAP, TW, LP>((int64_t)blockIdx.x * TW, RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats);
+    // edge-list capacity (edges past it are united at once): C2's sparse 4^8 tiles list ~0.8
+    // edges per code; the 7-position tiling takes dense spaces, whose words are mostly one
+    // component each (at most ~1.5 edges per word and position); 3072 keeps that instance at
+    // 2 workgroups per CU
+    constexpr int kEcap = LP == 7 ? 3072 : CAP >= 16384 ? 12288 : 8192;
+    local_cc_tile<CAP, TW, LP, NT, kEcap>((int64_t)blockIdx.x * TW, RT, words, L, f, UR, lroot, rwords, max_distinct,
+                                          stats);
 }
 
 // ROGTK_LOCAL8=0: never the 8-position local tiling (A/B)
@@ -881,34 +857,22 @@ inline bool local8_big_enabled() {
 // <= 8192 codes per tile; 1: 8 positions, <= 16384; 2: 7 positions), launched alone (one
 // launch instead of three: the others exit at once, but each costs a kernel boundary on
 // the resolve chain); it flags S_REDO when the bitmap needs another one. -1: all.
-inline void launch_local_cc(const uint4* RT, int64_t words, int L, uint32_t* f, uint32_t* D, uint32_t* UR,
-                            uint64_t* lroot, int64_t rwords, int64_t max_distinct, unsigned long long* stats,
-                            hipStream_t s, int choice = -1) {
-    if (choice >= 0) {
-        const int64_t tiles8 = (words + kLocal8Words - 1) / kLocal8Words;
-        if (choice == 0)
-            hipLaunchKernelGGL((k_local_cc<kLocal8Cap, kLocal8Words, 8>), dim3((unsigned)tiles8), dim3(kLocal8Words), 0,
-                               s, RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats, false, true);
-        else if (choice == 1)
-            hipLaunchKernelGGL((k_local_cc<kLocal8BigCap, kLocal8Words, 8>), dim3((unsigned)tiles8),
-                               dim3(kLocal8Words), 0, s, RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats,
-                               true, true);
-        else
-            hipLaunchKernelGGL((k_local_cc<kLocalCodes, kLocalWords, 7>),
-                               dim3((unsigned)((words + kLocalWords - 1) / kLocalWords)), dim3(kBlock), 0, s, RT,
-                               words, L, f, D, UR, lroot, rwords, max_distinct, stats, false, true);
-        return;
-    }
-    if (L >= 8 && local8_enabled()) {
-        const unsigned tiles8 = (unsigned)((words + kLocal8Words - 1) / kLocal8Words);
-        hipLaunchKernelGGL((k_local_cc<kLocal8Cap, kLocal8Words, 8>), dim3(tiles8), dim3(kLocal8Words), 0, s, RT,
-                           words, L, f, D, UR, lroot, rwords, max_distinct, stats, false, false);
-        if (local8_big_enabled())
-            hipLaunchKernelGGL((k_local_cc<kLocal8BigCap, kLocal8Words, 8>), dim3(tiles8), dim3(kLocal8Words), 0, s,
-                               RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats, false, false);
-    }
-    hipLaunchKernelGGL((k_local_cc<kLocalCodes, kLocalWords, 7>), dim3((unsigned)((words + kLocalWords - 1) / kLocalWords)),
-                       dim3(kBlock), 0, s, RT, words, L, f, D, UR, lroot, rwords, max_distinct, stats, false, false);
+inline void launch_local_cc(const uint4* RT, int64_t words, int L, uint32_t* f, uint32_t* UR, uint64_t* lroot,
+                            int64_t rwords, int64_t max_distinct, unsigned long long* stats, hipStream_t s,
+                            int choice = -1) {
+    constexpr int kNT8 = ROGTK_LCC_NT8;
+    const unsigned tiles8 = (unsigned)((words + kLocal8Words - 1) / kLocal8Words);
+    const unsigned tiles7 = (unsigned)((words + kLocalWords - 1) / kLocalWords);
+    const bool alone = choice >= 0;
+    if (alone ? choice == 0 : L >= 8 && local8_enabled())
+        ROGTK_TIMED_LAUNCH(K_K_LOCAL_CC, (k_local_cc<kLocal8Cap, kLocal8Words, 8, kNT8>), dim3(tiles8), dim3(kNT8), 0, s, RT,
+                           words, L, f, UR, lroot, rwords, max_distinct, stats, false, alone);
+    if (alone ? choice == 1 : L >= 8 && local8_enabled() && local8_big_enabled())
+        ROGTK_TIMED_LAUNCH(K_K_LOCAL_CC, (k_local_cc<kLocal8BigCap, kLocal8Words, 8, kNT8>), dim3(tiles8), dim3(kNT8), 0, s, RT,
+                           words, L, f, UR, lroot, rwords, max_distinct, stats, alone, alone);
+    if (alone ? choice == 2 : true)
+        ROGTK_TIMED_LAUNCH(K_K_LOCAL_CC, (k_local_cc<kLocalCodes, kLocalWords, 7>), dim3(tiles7), dim3(kLocalWords), 0, s, RT, words,
+                           L, f, UR, lroot, rwords, max_distinct, stats, false, alone);
 }
 
 // --------------------------------------------------------------- global CC
@@ -1664,9 +1628,9 @@ int enqueue_rounds(const ClusterLayout& cl, const WsPtrs& p, int from, int to, h
     const int pg = grid_for(cl.max_distinct, kPersistentGrid);
     const int64_t tasks = (int64_t)(cl.L - kLocalPos) * (cl.words >> 2);
     for (int k = from; k < to; ++k) {
-        hipLaunchKernelGGL(k_hook_g, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words, cl.L, kLocalPos,
+        ROGTK_TIMED_LAUNCH(K_K_HOOK, k_hook_g, dim3(grid_for(tasks)), dim3(kBlock), 0, s, p.RT, p.UR, cl.words, cl.L, kLocalPos,
                            p.f, p.flags, k, p.active, cl.active_words, (const unsigned long long*)p.stats);
-        hipLaunchKernelGGL(k_jump, dim3(pg), dim3(kBlock), 0, s, p.f, p.lroot, cl.max_distinct, p.stats, p.flags, k);
+        ROGTK_TIMED_LAUNCH(K_K_JUMP, k_jump, dim3(pg), dim3(kBlock), 0, s, p.f, p.lroot, cl.max_distinct, p.stats, p.flags, k);
     }
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
@@ -1685,12 +1649,12 @@ int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
         ProfScope prof(K_FLATTEN, s);
         if (check_round >= 0) {
             const int64_t tasks = (int64_t)(cl.L - kLocalPos) * (cl.words >> 2);
-            hipLaunchKernelGGL(k_roots_check, dim3((unsigned)(cl.rblocks + grid_for(tasks))), dim3(kBlock), 0, s, p.f,
+            ROGTK_TIMED_LAUNCH(K_K_ROOTS, k_roots_check, dim3((unsigned)(cl.rblocks + grid_for(tasks))), dim3(kBlock), 0, s, p.f,
                                p.lroot, cl.max_distinct, cl.rwords, p.rbits, p.rpref, p.rblksum,
                                (const unsigned long long*)p.stats, cl.rblocks, p.RT, p.UR, cl.words, cl.L, kLocalPos,
                                p.flags, check_round, p.active, cl.active_words);
         } else {
-            hipLaunchKernelGGL(k_roots_scan, dim3((unsigned)cl.rblocks), dim3(kBlock), 0, s, p.f, p.lroot,
+            ROGTK_TIMED_LAUNCH(K_K_ROOTS, k_roots_scan, dim3((unsigned)cl.rblocks), dim3(kBlock), 0, s, p.f, p.lroot,
                                cl.max_distinct, cl.rwords, p.rbits, p.rpref, p.rblksum,
                                (const unsigned long long*)p.stats, host_stats, (unsigned long long)epoch);
         }
@@ -1707,7 +1671,7 @@ int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
             const char* e = getenv("ROGTK_WORD_EXC1");
             return e && e[0] == '0' ? 0 : 1;
         }();
-        hipLaunchKernelGGL(k_word_label, dim3(grid_for(cl.words, kPersistentGrid)), dim3(kBlock),
+        ROGTK_TIMED_LAUNCH(K_K_WORD_LABEL, k_word_label, dim3(grid_for(cl.words, kPersistentGrid)), dim3(kBlock),
                            lds_off ? (size_t)(cl.rblocks + 1) * 4 : 0, s, p.f, p.UR, cl.words, p.RT, cl.max_distinct,
                            p.rbits, p.rpref, p.rblkoff, p.wpref, p.G, p.labelcode, p.ilab, exc1_on,
                            lds_off ? p.rblksum : nullptr, (int64_t)cl.rblocks, lds_off ? p.stats : nullptr,
@@ -1727,6 +1691,12 @@ int first_zero(const unsigned int* f, int from, int to) {
 
 }  // namespace
 
+#ifndef ROGTK_ASSIGN_WGS
+#define ROGTK_ASSIGN_WGS 2  // workgroups per CU of k_assign (experiment builds)
+#endif
+#ifndef ROGTK_ASSIGN_G
+#define ROGTK_ASSIGN_G 2  // 4-row groups per lane and trip (experiment builds)
+#endif
 namespace {
 int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, bool word_labels, const uint32_t* codes,
                    const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id, hipStream_t s);
@@ -1767,7 +1737,7 @@ int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bi
     {
         ProfScope prof(K_SCAN, s);
         if (scan_tag) {  // single pass: RT, n_distinct and the tiling in one launch
-            hipLaunchKernelGGL(k_scan_rt, dim3((unsigned)cl.blocks), dim3(kBlock), 0, s, bitmaps, n_bitmaps, cl.words,
+            ROGTK_TIMED_LAUNCH(K_K_SCAN_RT, k_scan_rt, dim3((unsigned)cl.blocks), dim3(kBlock), 0, s, bitmaps, n_bitmaps, cl.words,
                                p.RT, p.lroot, max_distance == 0 ? (int64_t)0 : cl.rwords,
                                p.lb + std::max(cl.blocks, cl.rblocks) + 1, p.lb, scan_tag, p.stats, (int)S_NDISTINCT,
                                max_distance == 0 ? (int)S_NCLUSTERS : -1, local8_enabled() ? cl.L : 0,
@@ -1789,7 +1759,7 @@ int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bi
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     ProfScope prof(K_UNION, s);
-    launch_local_cc(p.RT, cl.words, cl.L, p.f, p.D, p.UR, p.lroot, cl.rwords, cl.max_distinct, p.stats, s, lcc_choice);
+    launch_local_cc(p.RT, cl.words, cl.L, p.f, p.UR, p.lroot, cl.rwords, cl.max_distinct, p.stats, s, lcc_choice);
     if (cl.L <= kLocalPos) {
         if (enqueue_labels(cl, p, s, nullptr)) return -1;
         return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1889,8 +1859,8 @@ int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone) 
         // then the global rounds from round 0
         ProfScope prof(K_UNION, s);
         ROGTK_HIP_CHECK(hipMemsetAsync(p.stats + S_REDO, 0, 8, s));
-        launch_local_cc(p.RT, st.cl.words, st.cl.L, p.f, p.D, p.UR, p.lroot, st.cl.rwords, st.cl.max_distinct,
-                        p.stats, s, -1);
+        launch_local_cc(p.RT, st.cl.words, st.cl.L, p.f, p.UR, p.lroot, st.cl.rwords, st.cl.max_distinct, p.stats, s,
+                        -1);
         ROGTK_HIP_CHECK(hipGetLastError());
         ROGTK_HIP_CHECK(hipMemsetAsync(p.flags, 0, kMaxRounds * sizeof(unsigned int), s));
         std::memset(hflags, 0, kMaxRounds * sizeof(unsigned int));
@@ -2038,6 +2008,12 @@ int launch_cluster_lookup(const ClusterLayout& cl, const uint8_t* ws, const uint
     return ROGTK_OK;
 }
 
+#ifndef ROGTK_ASSIGN_WGS
+#define ROGTK_ASSIGN_WGS 2  // workgroups per CU of k_assign (experiment builds)
+#endif
+#ifndef ROGTK_ASSIGN_G
+#define ROGTK_ASSIGN_G 2  // 4-row groups per lane and trip (experiment builds)
+#endif
 namespace {
 int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, bool word_labels, const uint32_t* codes,
                    const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id, hipStream_t s) {
@@ -2055,9 +2031,9 @@ int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, bool word_labels, c
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
-        return (int64_t)2 * cus;
+        return (int64_t)ROGTK_ASSIGN_WGS * cus;
     }();
-    constexpr int kGroups = 2;
+    constexpr int kGroups = ROGTK_ASSIGN_G;
     const int g = grid_for((n + 4 * kGroups - 1) / (4 * kGroups), cap);
     if (cl.label_by_code)
         hipExtLaunchKernelGGL((k_assign<0, kGroups>), dim3(g), dim3(kBlock), 0, s, prof.start(), prof.stop(), 0, codes,
@@ -2442,13 +2418,13 @@ int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bi
             // chunks of all rows were read once per slice: 16x at L = 12, from L2)
             segs = (const uint32_t*)((uint8_t*)temp + (chunks > 1 ? (int64_t)chunks * words * 8 : 0));
             seglen = (uint32_t*)((uint8_t*)segs + (int64_t)kMaxSlices * nb * kSegCap * 4);
-            hipLaunchKernelGGL((k_slice_bucket<kBucketRows, kBucketThreads>), dim3((unsigned)nb), dim3(kBucketThreads), 0,
+            ROGTK_TIMED_LAUNCH(K_K_SLICE_BUCKET, (k_slice_bucket<kBucketRows, kBucketThreads>), dim3((unsigned)nb), dim3(kBucketThreads), 0,
                                s, codes, regular_bits, n, slog, slices, (uint32_t*)segs, seglen, nb);
         }
-        hipLaunchKernelGGL(k_slice_mark, dim3((unsigned)(slices * chunks)), dim3(kSliceBlock), 0, s, codes, regular_bits,
+        ROGTK_TIMED_LAUNCH(K_K_SLICE_MARK, k_slice_mark, dim3((unsigned)(slices * chunks)), dim3(kSliceBlock), 0, s, codes, regular_bits,
                            n, slog, chunks, chunk_rows, dst, words, segs, (const uint32_t*)seglen, nb, kBucketRows, kSegCap);
         if (chunks > 1)
-            hipLaunchKernelGGL(k_or_partials, dim3(grid_for(words, 4096)), dim3(kBlock), 0, s, dst, chunks, words,
+            ROGTK_TIMED_LAUNCH(K_K_OR_PARTIALS, k_or_partials, dim3(grid_for(words, 4096)), dim3(kBlock), 0, s, dst, chunks, words,
                                bitmap);
         ROGTK_HIP_CHECK(hipGetLastError());
         return ROGTK_OK;

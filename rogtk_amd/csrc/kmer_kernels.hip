@@ -296,7 +296,8 @@ template <int B, int R = 64>
 __global__ __launch_bounds__(R, 3) void k_pack_reads(const int64_t* __restrict__ offsets,
                                                   const uint8_t* __restrict__ values,
                                                   const uint8_t* __restrict__ validity, int64_t voff,
-                                                  int64_t n, uint64_t* __restrict__ blocks) {
+                                                  int64_t n, uint64_t* __restrict__ blocks,
+                                                  unsigned long long* __restrict__ max_len) {
     constexpr int kIn = kPackInBytes * R / kBlock;  // staged bytes: 160 per row
     constexpr int kVin = kIn / 4 / R;               // staged dwords per lane (40)
     // + the funnel shift's 2 zero dwords, a dummy slot, and slack for a word's 9-dword read
@@ -348,6 +349,7 @@ __global__ __launch_bounds__(R, 3) void k_pack_reads(const int64_t* __restrict__
     int64_t a = (int64_t)blockIdx.x * R;
     Offs cur = load_offs(a), nxt = load_offs(a + stride);
     if (a < n) load_bytes(cur.b0, cur.b1);
+    int run_max = 0;  // the longest row of this wave's trips (max_len: one atomic per wave)
     for (; a < n; a += stride) {
         const int nr = (int)min<int64_t>(R, n - a);
         if (tid <= nr) s_off[tid] = cur.o0;
@@ -375,6 +377,7 @@ __global__ __launch_bounds__(R, 3) void k_pack_reads(const int64_t* __restrict__
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) my_len = max(my_len, __shfl_xor(my_len, m, 64));
         const int lmax = __builtin_amdgcn_readfirstlane(my_len);
+        run_max = max(run_max, lmax);
         if (tid < nr) {  // this lane's row, entirely in registers: no cross-lane steps
             const int64_t r = a + tid;
             bool valid = true;
@@ -458,6 +461,7 @@ __global__ __launch_bounds__(R, 3) void k_pack_reads(const int64_t* __restrict__
         cur = nxt;
         nxt = nn;
     }
+    if (max_len && tid == 0 && run_max > 0) atomicMax(max_len, (unsigned long long)run_max);
 }
 
 // One wave per 64 grouped rows: each row's block (B words: B lanes, 64 / B rows per
@@ -2502,18 +2506,19 @@ int rogtk_read_block_words(int64_t max_len) {
 }
 
 int rogtk_pack_reads(const int64_t* offsets, const uint8_t* values, const uint8_t* validity, int64_t validity_offset,
-                     int64_t n, int block_words, uint64_t* blocks, void* stream) {
+                     int64_t n, int block_words, uint64_t* blocks, int64_t* max_len, void* stream) {
     ROGTK_REQUIRE(n >= 0 && (n == 0 || (offsets && values && blocks)), ROGTK_E_INVALID, "pack_reads: NULL argument");
     ROGTK_REQUIRE(block_words == 8 || block_words == 16 || block_words == 32, ROGTK_E_INVALID,
                   "pack_reads: block_words must be 8, 16 or 32 (rogtk_read_block_words)");
-    if (n == 0) return ROGTK_OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (max_len) ROGTK_HIP_CHECK(hipMemsetAsync(max_len, 0, 8, s));
+    if (n == 0) return ROGTK_OK;
     constexpr int kRows = 64;  // one wave per workgroup (k_pack_reads)
     const int g = (int)std::min<int64_t>((n + kRows - 1) / kRows, (int64_t)8192 * 256 / kRows);
     ProfScope prof(K_PACK_READS, s, true);
 #define ROGTK_PACK_LAUNCH(BW)                                                                                       \
     hipExtLaunchKernelGGL((k_pack_reads<BW, kRows>), dim3(g), dim3(kRows), 0, s, prof.start(), prof.stop(), 0, offsets, \
-                          values, validity, validity_offset, n, blocks)
+                          values, validity, validity_offset, n, blocks, (unsigned long long*)max_len)
     if (block_words == 8)
         ROGTK_PACK_LAUNCH(8);
     else if (block_words == 16)

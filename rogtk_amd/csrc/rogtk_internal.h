@@ -7,6 +7,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <functional>
+#include <vector>
 
 #include "../../include/rogtk_hip.h"
 
@@ -55,6 +56,16 @@ enum KernelId {
     K_KMER_LDS,
     K_RESOLVE,  // the whole resolve chain of one batch (first launch to last, its stream)
     K_KMER_MZ,  // the minimizer filter of the k-mer spectra (round 4)
+    // round 5: single kernels of the C2 step, each timed on its own dispatch packet
+    K_K_SLICE_BUCKET,
+    K_K_SLICE_MARK,
+    K_K_OR_PARTIALS,
+    K_K_SCAN_RT,
+    K_K_LOCAL_CC,
+    K_K_HOOK,
+    K_K_JUMP,
+    K_K_ROOTS,
+    K_K_WORD_LABEL,
     K_COUNT_
 };
 extern const char* const kKernelNames[K_COUNT_];
@@ -64,6 +75,14 @@ bool profiling_on();
 // exact = true: the events are not recorded on the stream; the launcher attaches them to
 // the kernel's dispatch packet (hipExtLaunchKernelGGL(..., start(), stop(), ...)), so the
 // elapsed time is the kernel's own execution, as in rocprofv3's kernel trace.
+class ProfScope;
+// One launch with its own exact events (kernel execution time, as rocprofv3's kernel trace)
+// when profiling is on and ID is selected; a plain launch otherwise.
+#define ROGTK_TIMED_LAUNCH(ID, KERNEL, GRID, BLOCK, LDS, S, ...)                                     \
+    do {                                                                                           \
+        ::rogtk::ProfScope pk_(ID, S, true);                                                       \
+        hipExtLaunchKernelGGL(KERNEL, GRID, BLOCK, LDS, S, pk_.start(), pk_.stop(), 0, __VA_ARGS__); \
+    } while (0)
 class ProfScope {
    public:
     ProfScope(KernelId id, hipStream_t stream, bool exact = false);
@@ -249,19 +268,20 @@ int cluster_layout(int L, int64_t max_distinct, ClusterLayout* out);
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
+    std::vector<void*> retired;  // outgrown allocations, freed with the buffer
     ~DevBuf() {
         if (p) hipFree(p);
+        for (void* q : retired) hipFree(q);
     }
-    // A buffer that grows may still be read by kernels enqueued earlier (the BAM device
-    // path never waits for the GPU inside a file): as a guard the device drains before
-    // the old allocation is freed, and a regrown buffer takes 1.5x so that growing stays
-    // rare.
+    // A buffer that grows may still be read by kernels enqueued earlier on any stream (the
+    // BAM device path never waits for the GPU inside a file), so the outgrown allocation is
+    // retired, not freed: no device-wide drain on the host path. A regrown buffer takes
+    // 1.5x, so the retired ones together stay below twice the live one.
     int ensure(size_t bytes) {
         if (bytes <= cap && p) return ROGTK_OK;
         size_t grow = 0;
         if (p) {
-            ROGTK_HIP_CHECK(hipDeviceSynchronize());
-            hipFree(p);
+            retired.push_back(p);
             p = nullptr;
             grow = cap + cap / 2;
             cap = 0;

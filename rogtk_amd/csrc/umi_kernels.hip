@@ -17,6 +17,7 @@
 // order); the file is compiled with -ffp-contract=off so `e -= t` and the combined
 // score are never fused into FMAs; f64 division is IEEE (correctly rounded).
 #include <cstdlib>
+#include <type_traits>
 
 #include <hip/hip_ext.h>
 
@@ -349,8 +350,9 @@ __global__ __launch_bounds__(kBlock) void k_score_packed(const uint32_t* __restr
     // Wave tile of 256 rows; lane l owns rows {2l, 2l+1, 128+2l, 129+2l} so that every
     // 16-B (double2) store instruction of the wave writes 1 KB of contiguous output.
     // grid-stride over 1024-row block tiles (a capped grid keeps fewer waves in flight)
-    for (int64_t tile = blockIdx.x; tile * kBlock * kRowsPerLane < n; tile += gridDim.x)
+    for (int64_t tile = blockIdx.x; tile * kBlock * kRowsPerLane < n; tile += gridDim.x) {
         score_tile<SCORE, HAMD, HAMW, LT, ASG>(tile, codes, regbits, n, P, O, hd, hw, A, s_tab);
+    }
     span_exit(tspan);
 }
 

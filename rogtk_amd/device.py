@@ -205,13 +205,18 @@ class ClusterEngine:
         _lib.call("rogtk_cluster_mark", _p(batch.codes), _p(batch.regular_bits), batch.n, self.umi_len,
                   _p(self.ws), self.max_distinct, _s(stream))
 
+    def mark_temp(self, n: int) -> torch.Tensor:
+        """The scratch of mark_bitmap for n rows (kept, grown on demand)."""
+        need = ctypes.c_int64(0)
+        _lib.call("rogtk_cluster_mark_bitmap_temp_bytes", n, self.umi_len, ctypes.byref(need))
+        if getattr(self, "_mark_temp", None) is None or self._mark_temp.numel() < need.value:
+            self._mark_temp = torch.empty(need.value, dtype=torch.uint8, device=self.local_bitmap.device)
+        return self._mark_temp
+
     def mark_bitmap(self, batch: PackedBatch, stream=None):
         """mark + build_local_bitmap in one: code slices or partition sort + LDS bitmap
         (7 <= L <= 13). Returns local_bitmap."""
-        need = ctypes.c_int64(0)
-        _lib.call("rogtk_cluster_mark_bitmap_temp_bytes", batch.n, self.umi_len, ctypes.byref(need))
-        if getattr(self, "_mark_temp", None) is None or self._mark_temp.numel() < need.value:
-            self._mark_temp = torch.empty(need.value, dtype=torch.uint8, device=self.local_bitmap.device)
+        self.mark_temp(batch.n)
         _lib.call("rogtk_cluster_mark_bitmap", _p(batch.codes), _p(batch.regular_bits), batch.n, self.umi_len,
                   _p(self.local_bitmap), _p(self._mark_temp), self._mark_temp.numel(), _s(stream))
         return self.local_bitmap
@@ -326,19 +331,37 @@ class PackedReads:
     """A read column as fixed-size 2-bit blocks in HBM (rogtk_pack_reads): block_words u64
     per row (meta + bases), so a grouped row is staged as whole 64-B lines."""
 
+    # the block size packed first when the caller gives no bound (rows up to 224 bases, the
+    # short-read case); a column with longer rows is packed again at its own size
+    GUESS_LEN = 224
+
     def __init__(self, offsets: torch.Tensor, values: torch.Tensor, validity: Optional[torch.Tensor] = None,
                  validity_offset: int = 0, max_len: Optional[int] = None, stream=None):
         n = offsets.numel() - 1
-        if max_len is None:
-            max_len = int((offsets[1:] - offsets[:-1]).max().item()) if n else 0
-        self.max_len = int(max_len)
-        self.block_words = int(_lib.hip().rogtk_read_block_words(self.max_len))
-        if self.block_words == 0:
-            raise ValueError(f"reads up to {self.max_len} bases: too long for the block layout (max 992)")
         self.n = n
-        self.blocks = torch.empty(max(n * self.block_words, 1), dtype=torch.int64, device=values.device)
-        _lib.call("rogtk_pack_reads", _p(offsets), _p(values), _p(validity), int(validity_offset), n,
-                  self.block_words, _p(self.blocks), _s(stream))
+        # the longest row comes out of the pack kernel itself (a per-wave reduction into one
+        # device word; no separate pass over the offsets, no torch kernel); read back once
+        self._max_dev = torch.empty(1, dtype=torch.int64, device=values.device)
+        guess = self.GUESS_LEN if max_len is None else int(max_len)
+        self._pack(offsets, values, validity, validity_offset, guess, stream)
+        if max_len is None:
+            got = 0
+            if n:  # one 8-byte read, ordered after the pack on its stream
+                with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
+                    got = int(self._max_dev.cpu()[0])
+            if got > (self.block_words - 1) * 32:  # a row did not fit the guessed blocks
+                self._pack(offsets, values, validity, validity_offset, got, stream)
+            self.max_len = got
+        else:
+            self.max_len = int(max_len)
+
+    def _pack(self, offsets, values, validity, validity_offset, max_len, stream):
+        self.block_words = int(_lib.hip().rogtk_read_block_words(int(max_len)))
+        if self.block_words == 0:
+            raise ValueError(f"reads up to {max_len} bases: too long for the block layout (max 992)")
+        self.blocks = torch.empty(max(self.n * self.block_words, 1), dtype=torch.int64, device=values.device)
+        _lib.call("rogtk_pack_reads", _p(offsets), _p(values), _p(validity), int(validity_offset), self.n,
+                  self.block_words, _p(self.blocks), _p(self._max_dev), _s(stream))
 
 
 def kmer_spectrum_blocks(packed: PackedReads, offsets: torch.Tensor, values: torch.Tensor,

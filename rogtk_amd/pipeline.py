@@ -112,7 +112,11 @@ class UmiPipeline:
         # 0.367-0.369 vs 0.398-0.408 ms/step at 10M reads, interleaved on one box; the score
         # kernel then also runs beside fewer resolve kernels: 99 vs 130 us). (Round 4 also
         # measured the presence mark fused into the score kernel as byte stores + a bitmap
-        # pass: 0.484 vs 0.305 ms/step; removed in round 5.)
+        # pass: 0.484 vs 0.305 ms/step; removed in round 5. Round 5 measured and removed two
+        # more orders: assign(k-1) between mark(k) and score(k), so the local CC runs beside
+        # the assign rather than the score kernel, and the mark's slice ranking folded into
+        # the score kernel (its segments read back by the slice mark): 0.31-0.32 and
+        # 0.346-0.349 vs 0.306 ms/step, the folded score kernel 167 vs 100 us.)
         self.mark_first = mark_first
         # device_events: the cross-stream hand-offs use StreamEvents released at device
         # scope (rogtk_event_*) instead of torch events, whose system-scope release writes

@@ -256,7 +256,9 @@ def test_packed_blocks_match_oracle(lo, hi, bw):
     valid = np.array([x is not None for x in items])
     vbits = torch.from_numpy(np.packbits(np.concatenate([valid, np.zeros(7, bool)]), bitorder="little")).cuda()
     pk = D.PackedReads(off, vals, validity=vbits)
-    assert pk.block_words == bw
+    # the longest row from the pack kernel's own reduction (rows past the guessed 224-base
+    # blocks packed again at their size)
+    assert pk.block_words == bw and pk.max_len == int(lens.max())
     gsel = torch.tensor(go, dtype=torch.int64).cuda()
     col = P.StrCol.from_list(items)
     for k, mc in ((13, 2), (17, 1), (33, 2)):

@@ -47,7 +47,10 @@ def test_launcher_world(tmp_path, world):
 
 
 def test_launcher_failed_rank_fails_launch():
-    assert run_local_ranks(2, _fail_on_rank1, (), timeout=120) == 3
+    # rank 1 exits 3; rank 0, blocked in the barrier, is killed by the launcher or sees the
+    # closed connection and fails first (gloo raises): either way the launch fails, promptly
+    rc = run_local_ranks(2, _fail_on_rank1, (), timeout=120)
+    assert rc in (1, 3)
 
 
 def test_bench_rejects_world_mismatch():

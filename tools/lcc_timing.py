@@ -25,7 +25,8 @@ def read_clk():
     v = list(out)
     wg = max(v[5], 1)
     return {"workgroups": v[5], "phase_us": [round(x / wg * TICK_US, 2) for x in v[:4]],
-            "wg_us": round(v[4] / wg * TICK_US, 2)}
+            "wg_us": round(v[4] / wg * TICK_US, 2),
+            "unites_per_wg": round(v[6] / wg, 1), "cas_retries_per_wg": round(v[7] / wg, 1)}
 
 
 def main():
