@@ -115,6 +115,8 @@ def parse():
                     help="skip the C3 line part (BASELINE configs[2]: 100M reads, k-mer spectra per UMI group; "
                          "runs after C2 on rank 0 of a one-GPU run)")
     ap.add_argument("--c3-reads", type=int, default=100_000_000)
+    ap.add_argument("--no-c3-k16", action="store_true",
+                    help="skip the C3 block at the reference's default k (15 / 10: effective 16), min_coverage 5")
     ap.add_argument("--c3-steps", type=int, default=3)
     return ap.parse_args()
 
@@ -294,14 +296,14 @@ def c3_workload(n: int = 100_000_000, steps: int = 3, warmup: int = 1, k: int = 
     ev = lambda: torch.cuda.Event(enable_timing=True)
     phases = {"cluster": 0.0, "group_by+kmer": 0.0}
     acc = {}
-    path_groups = [0, 0, 0]
+    path_groups = [0, 0, 0, 0]
 
     def step(record):
         e0, e1, e3 = ev(), ev(), ev()
         e0.record()
         D.cluster_batch(eng, batch, cid, 0)
         e1.record()
-        path_groups[:] = [0, 0, 0]
+        path_groups[:] = [0, 0, 0, 0]
         acc.update(valid=0, stats=[], calls=0)
 
         def consume(g0, g1, r):  # per spectrum call
@@ -316,6 +318,8 @@ def c3_workload(n: int = 100_000_000, steps: int = 3, warmup: int = 1, k: int = 
                 cg = ctypes.c_int64(0)
                 _lib.call("rogtk_kmer_certified_groups", ctypes.byref(cg))
                 path_groups[2] += cg.value
+                _lib.call("rogtk_kmer_lds_rows", ctypes.byref(cg))  # rows the LDS kernels inserted
+                path_groups[3] += cg.value
             except Exception:  # an older library (A/B)
                 pass
 
@@ -389,9 +393,12 @@ def c3_workload(n: int = 100_000_000, steps: int = 3, warmup: int = 1, k: int = 
         "data": f"synthetic (synth-v1 reads + UMIs, {n // 10} molecules), generated in {gen_s:.1f} s, "
                 "resident in HBM",
     }
-    if "kmer_lds" in kernels:  # the insert kernel alone: observations per CU clock inside it
-        out["roofline"]["kmer_lds"] = {"bound": "lds", "kernel": "k_kmer_lds<3>", "us": kernels["kmer_lds"],
-                                       "obs_per_cu_clock": round(obs / (kernels["kmer_lds"] * 1e-6) / cu_clk, 3)}
+    if "kmer_lds" in kernels:  # the insert kernels alone: the observations THEY inserted per CU clock
+        lds_obs = path_groups[3] * (RL - k_eff + 1)  # rows of the groups left on the LDS kernels
+        out["lds_rows"] = path_groups[3]
+        out["roofline"]["kmer_lds"] = {"bound": "lds", "kernel": "k_kmer_lds<1|3|4>", "us": kernels["kmer_lds"],
+                                       "observations": lds_obs,
+                                       "obs_per_cu_clock": round(lds_obs / (kernels["kmer_lds"] * 1e-6) / cu_clk, 3)}
     if "pack_reads" in kernels:  # HBM stream: RL bytes in, one 64-B block out per read
         a = n * (RL + 64) / (kernels["pack_reads"] * 1e-6) / 1e9
         out["roofline"]["pack_reads"] = {"bound": "hbm", "kernel": "k_pack_reads", "us": kernels["pack_reads"],
@@ -696,12 +703,17 @@ def main():
                                 "frac": round(a_iso / HBM_PEAK_GBS, 4), "launches": args.iso_launches,
                                 "note": "same kernel, same batch, launched alone after the timed region"}
     sort_mark = pipe.sort_mark
-    c3 = None
+    c3 = c3_k16 = None
     if world == 1 and not args.no_c3 and args.emulate_ranks == 1:
         del pipe, batch, codes
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
         c3 = c3_workload(args.c3_reads, steps=args.c3_steps, warmup=1)
+        if not args.no_c3_k16:
+            # the reference's own operating point: assemble_sequences defaults k = 10 and the
+            # docstring's k = 15 (rogtk/__init__.py:106-107, 211-212), both effective 16
+            # (fracture.rs:246-256), min_coverage 5
+            c3_k16 = c3_workload(args.c3_reads, steps=args.c3_steps, warmup=1, k=15, min_coverage=5)
     e2e = None
     if not args.no_end_to_end and args.emulate_ranks == 1:
         e2e = end_to_end(codes_h[: min(count, 10_000_000)], L, md)
@@ -741,6 +753,7 @@ def main():
         "settle": {"seconds": args.settle_seconds, "steps": settle_steps} if settle_steps else None,
         "end_to_end": e2e,
         "c3": c3,
+        "c3_k16": c3_k16,
         "cpu_baseline": cpu,
         "kernels_us": breakdown,
         "kernels_per_step": per_kernel,

@@ -380,6 +380,15 @@ int rogtk_kmer_path_stats(int64_t* out2);
  * (round 4: every row with observations certified free of repeated aligned 16-mers by
  * rogtk_pack_reads, fewer such rows than min_coverage, k_eff 32: nothing valid). */
 int rogtk_kmer_certified_groups(int64_t* out);
+/* Round 5, measurement: rows of the last call's groups that the LDS kernels processed
+ * (LDS-path groups not taken off by a certificate or the minimizer filter), so a caller
+ * can count the k-mer observations those kernels inserted. */
+int rogtk_kmer_lds_rows(int64_t* out);
+/* Round 5, tests only: decisions (device, n_groups bytes; NULL / 0 turns it off) receives,
+ * for each group of the next calls (indices of the call) that the minimizer filter
+ * examined, 1 = emptied (no k-mer can be valid), 2 = kept, 3 = kept (too many minimizers
+ * to decide); other bytes are left as they were. Calls with more groups write nothing. */
+int rogtk_kmer_debug_filter(uint8_t* decisions, int64_t n_groups);
 int rogtk_kmer_spectrum_host(const void* offsets, int offset_width, const uint8_t* values,
                              int64_t values_len, const uint8_t* validity, int64_t validity_offset,
                              int64_t n_rows, const int64_t* group_offsets, int64_t n_groups, int k,

@@ -158,6 +158,8 @@ SIGNATURES = {
                                 _vp, _P_I64, _vp],
     "rogtk_kmer_path_stats": [_P_I64],
     "rogtk_kmer_certified_groups": [_P_I64],
+    "rogtk_kmer_lds_rows": [_P_I64],
+    "rogtk_kmer_debug_filter": [_vp, _i64],
     "rogtk_read_block_words": [_i64],
     "rogtk_host_alloc": [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)],
     "rogtk_host_free": [_vp],

@@ -1347,6 +1347,9 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
 
 // The minimizer filter (below): on unless ROGTK_KMER_MZ=0 or rogtk_kmer_set_filter(0)
 std::atomic<int> g_kmer_mz{-1};
+// tests only (rogtk_kmer_debug_filter): per group of a call, the filter's decision
+uint8_t* g_mz_debug = nullptr;
+int64_t g_mz_debug_groups = 0;
 inline bool kmer_mz_on() {
     int v = g_kmer_mz.load(std::memory_order_relaxed);
     if (v < 0) {
@@ -1396,7 +1399,8 @@ __global__ __launch_bounds__(64 * kMzWaves) void k_minimizer_filter(const GroupD
                                                                      int64_t min_cov,
                                                                      const int32_t* __restrict__ row_len, int stride,
                                                                      const uint64_t* __restrict__ packed,
-                                                                     const unsigned long long* __restrict__ gstat) {
+                                                                     const unsigned long long* __restrict__ gstat,
+                                                                     uint8_t* __restrict__ dbg) {
     constexpr int NW = 7;       // B = 8 blocks: at most 7 base words (224 bases) per row
     constexpr int NH = 2 * NW;  // 32-bit half-words: 16 positions each
     __shared__ unsigned long long s_key[kMzWaves][kMzSlots];
@@ -1665,6 +1669,9 @@ __global__ __launch_bounds__(64 * kMzWaves) void k_minimizer_filter(const GroupD
         if (!gave_up) {
             const uint32_t reach = (split ? reach_split : scan_reach_all()) | keep;
             if (lane < cb.ng && !((reach >> lane) & 1u)) gsmall[cb.g] = kClsEmpty;
+            if (dbg && lane < cb.ng) dbg[cb.g] = ((reach >> lane) & 1u) ? 2 : 1;  // tests: kept / emptied
+        } else if (dbg && lane < cb.ng) {
+            dbg[cb.g] = 3;  // gave up: kept
         }
         for (int i = lane; i < kMzSlots; i += 64) {  // the table for the next batch
             key[i] = kNone;
@@ -1680,30 +1687,34 @@ __global__ __launch_bounds__(64 * kMzWaves) void k_minimizer_filter(const GroupD
 // LDS kernels) and on the global path, counted on the device (no G-byte copy to the host)
 __global__ __launch_bounds__(kBlock) void k_path_counts(const uint8_t* __restrict__ gk, int K, int64_t G,
                                                         const uint8_t* __restrict__ gsmall,
+                                                        const GroupDesc* __restrict__ gdesc,
                                                         unsigned long long* __restrict__ out2) {
-    unsigned long long lds = 0, glob = 0, cert = 0;
+    unsigned long long lds = 0, glob = 0, cert = 0, lrows = 0;
     for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < G; g += (int64_t)gridDim.x * kBlock) {
         if (gk[g] != K) continue;
         if (gsmall && gsmall[g]) ++lds;
         else ++glob;
         if (gsmall && gsmall[g] == kClsEmpty) ++cert;
+        else if (gsmall && gsmall[g]) lrows += (unsigned long long)gdesc[g].nrows;  // rows the LDS kernels insert
     }
     for (int m = 32; m > 0; m >>= 1) {
         lds += __shfl_xor(lds, m);
         glob += __shfl_xor(glob, m);
         cert += __shfl_xor(cert, m);
+        lrows += __shfl_xor(lrows, m);
     }
     // one atomic per workgroup and counter (per wave, 3 x 16K atomics on the same three
     // words serialised at L2: 0.4 ms at 8.17M groups)
-    __shared__ unsigned long long s3[kWavesPerBlock][3];
+    __shared__ unsigned long long s3[kWavesPerBlock][4];
     const int wv = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
         s3[wv][0] = lds;
         s3[wv][1] = glob;
         s3[wv][2] = cert;
+        s3[wv][3] = lrows;
     }
     __syncthreads();
-    if (threadIdx.x < 3) {
+    if (threadIdx.x < 4) {
         unsigned long long v = 0;
         for (int w = 0; w < kWavesPerBlock; ++w) v += s3[w][threadIdx.x];
         if (v) atomicAdd(out2 + threadIdx.x, v);  // out2[2]: of the LDS ones, empty by a certificate
@@ -1859,6 +1870,7 @@ struct KmerCtx {
     bool lds_path = true;  // rogtk_kmer_set_path(): tests force the global path
     int64_t last_lds_groups = 0, last_global_groups = 0;  // rogtk_kmer_path_stats()
     int64_t last_cert_groups = 0;                         // rogtk_kmer_certified_groups()
+    int64_t last_lds_rows = 0;                            // rogtk_kmer_lds_rows()
     ~KmerCtx() {
         if (stream) hipStreamDestroy(stream);
     }
@@ -2009,7 +2021,7 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
         hipExtLaunchKernelGGL(k_minimizer_filter, dim3((unsigned)std::min<int64_t>((chunks + kMzWaves - 1) / kMzWaves, 4096)),
                               dim3(64 * kMzWaves), 0, s, prof.start(), prof.stop(), 0, c->gdesc.as<GroupDesc>(), G,
                               c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(), stride,
-                              c->packed.as<uint64_t>(), gstat);
+                              c->packed.as<uint64_t>(), gstat, g_mz_debug_groups >= G ? g_mz_debug : nullptr);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     if (lds) {
@@ -2022,12 +2034,12 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
     }
     if (lds) {
         // one workgroup per small group, straight from the packed rows
-        hipLaunchKernelGGL((k_kmer_lds<1, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)), dim3(kLdsBlock), 0, s,
+        ROGTK_TIMED_LAUNCH(K_KMER_LDS, (k_kmer_lds<1, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 65536)), dim3(kLdsBlock), 0, s,
                            c->gdesc.as<GroupDesc>(), G,
                            c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
                            c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
                            c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
-        hipLaunchKernelGGL((k_kmer_lds<4, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 8192)), dim3(kLdsBlock), 0, s,
+        ROGTK_TIMED_LAUNCH(K_KMER_LDS, (k_kmer_lds<4, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 8192)), dim3(kLdsBlock), 0, s,
                            c->gdesc.as<GroupDesc>(), G,
                            c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
                            c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
@@ -2036,16 +2048,18 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
     // the groups per path first: with none on the global path (the usual C3 call, every
     // group in LDS or certified empty) its row drop and observation scan are skipped
     if (int rc = c->scal.ensure(64)) return rc;
-    ROGTK_HIP_CHECK(hipMemsetAsync(c->scal.p, 0, 24, s));
+    ROGTK_HIP_CHECK(hipMemsetAsync(c->scal.p, 0, 32, s));
     hipLaunchKernelGGL(k_path_counts, dim3(grid_for(G, 1024)), dim3(kBlock), 0, s, in.gk, K, G,
                        (c->lds_path && K <= 32) ? c->gsmall.as<uint8_t>() : nullptr,
+                       (c->lds_path && K <= 32) ? c->gdesc.as<GroupDesc>() : nullptr,
                        c->scal.as<unsigned long long>());
-    int64_t last[5] = {0, 0, 0, 0, 0};
-    ROGTK_HIP_CHECK(hipMemcpyAsync(&last[2], c->scal.p, 24, hipMemcpyDeviceToHost, s));
+    int64_t last[6] = {0, 0, 0, 0, 0, 0};
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&last[2], c->scal.p, 32, hipMemcpyDeviceToHost, s));
     ROGTK_HIP_CHECK(hipStreamSynchronize(s));
     c->last_lds_groups += last[2];
     c->last_global_groups += last[3];
     c->last_cert_groups += last[4];
+    c->last_lds_rows += last[5];
     if (last[3] == 0) return ROGTK_OK;
     if (lds) {
         hipLaunchKernelGGL(k_drop_small_rows, dim3(grid_for(n_rows)), dim3(kBlock), 0, s, c->row_group.as<uint32_t>(),
@@ -2195,6 +2209,21 @@ int rogtk_kmer_certified_groups(int64_t* out) {
     return ROGTK_OK;
 }
 
+int rogtk_kmer_lds_rows(int64_t* out) {
+    ROGTK_REQUIRE(out, ROGTK_E_INVALID, "kmer_lds_rows: NULL");
+    KmerCtx* c = nullptr;
+    if (int rc = kmer_ctx(&c)) return rc;
+    *out = c->last_lds_rows;
+    return ROGTK_OK;
+}
+
+int rogtk_kmer_debug_filter(uint8_t* decisions, int64_t n_groups) {
+    ROGTK_REQUIRE(!decisions == !n_groups && n_groups >= 0, ROGTK_E_INVALID, "kmer_debug_filter: buffer and size");
+    g_mz_debug = decisions;
+    g_mz_debug_groups = n_groups;
+    return ROGTK_OK;
+}
+
 int rogtk_kmer_path_stats(int64_t* out2) {
     ROGTK_REQUIRE(out2, ROGTK_E_INVALID, "kmer_path_stats: NULL");
     KmerCtx* c = nullptr;
@@ -2315,7 +2344,7 @@ int rogtk_kmer_spectrum_host(const void* offsets, int offset_width, const uint8_
     ROGTK_HIP_CHECK(hipMemcpyAsync(c->cap_off.p, cap_off.data(), (G + 1) * 8, hipMemcpyHostToDevice, s));
     ROGTK_HIP_CHECK(hipMemsetAsync(c->gstat.p, 0, G * 5 * 8, s));
     ROGTK_HIP_CHECK(hipMemsetAsync(c->gcount.p, 0, G * 8, s));
-    c->last_lds_groups = c->last_global_groups = c->last_cert_groups = 0;
+    c->last_lds_groups = c->last_global_groups = c->last_cert_groups = c->last_lds_rows = 0;
     const KIn in{c->offsets.as<int64_t>(), c->values.as<uint8_t>(), validity ? c->validity.as<uint8_t>() : nullptr,
                  0, nullptr, c->go.as<int64_t>(), c->gk.as<uint8_t>(), c->cap_off.as<int64_t>(),
                  c->gstat.as<unsigned long long>(), c->gcount.as<int64_t>()};
@@ -2453,7 +2482,7 @@ int spectrum_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* v
     if (int rc = c->t_kmer.ensure((size_t)tcap * 16)) return rc;
     if (int rc = c->t_ext.ensure((size_t)tcap)) return rc;
     if (int rc = c->t_cnt.ensure((size_t)tcap * 2)) return rc;
-    c->last_lds_groups = c->last_global_groups = c->last_cert_groups = 0;
+    c->last_lds_groups = c->last_global_groups = c->last_cert_groups = c->last_lds_rows = 0;
     if (K && n_rows > 0) {
         KIn in{offsets, values, validity, validity_offset, rows, group_offsets, c->gk.as<uint8_t>(),
                c->cap_off.as<int64_t>(), c->gstat.as<unsigned long long>(), c->gcount.as<int64_t>()};

@@ -4,6 +4,8 @@
   (rogtk_amd.launch); on a one-GPU box they share cuda:0 over gloo
   (ROGTK_DIST_BACKEND=gloo, tests only). The JSON line must report the world size the
   process group saw.
+* C2 weak scaling at N = 8 (10M reads per rank): one rank's ids against the oracle over the
+  union of the 8 shards, at 12 bp (one cluster) and 13 bp (36,893 clusters).
 * C4 = 500M reads over 8 GPUs: one rank's 62.5M-read shard runs through UmiPipeline
   exactly as bench.py --workload C4 --gpus 8 runs it per rank, against the all-gathered
   bitmaps of all 8 shards (the other 7 built on the same GPU). Every output is compared:
@@ -45,15 +47,10 @@ def test_bench_launcher_two_ranks():
     assert line["value"] > 0 and line["scaling"] == "weak"
 
 
-@pytest.mark.timeout(900)
-def test_c4_rank_of_8_against_the_union():
-    """C4 at N = 8 (500M reads, 62.5M per rank), emulated on one GPU exactly as each rank
-    runs it: rank 3's shard goes through UmiPipeline (bench.py's defaults) with the
-    exchange returning the all-gathered bitmaps of all 8 shards (the other 7 built here,
-    ~95% of the 4^12 codes present in their union). Every output is compared: all 7 H1
-    fields and the Hamming-within bits on the rank's distinct codes (a regular row's scores
-    are a function of its code), and the ids against the oracle's union-find over the
-    union's distinct codes (ids depend only on the global distinct set)."""
+def _rank_of_world(n_total, world, rank, L, scores=True):
+    """Rank `rank` of `world` emulated on one GPU exactly as it runs under bench.py: its shard
+    through UmiPipeline (bench.py's defaults) with the exchange returning the all-gathered
+    bitmaps of every shard (the others built here). Returns (codes_h, slot outputs, stats)."""
     import torch
 
     import bench
@@ -63,34 +60,78 @@ def test_c4_rank_of_8_against_the_union():
     from rogtk_amd import synth
     from rogtk_amd.pipeline import UmiPipeline
 
-    n_total, world, rank, L = 500_000_000, 8, 3, 12
     dev = torch.device("cuda", 0)
     bitmaps = [bench.emulated_shard_bitmap(n_total, r, world, L, dev) if r != rank else None for r in range(world)]
     start, count = RD.shard_range(n_total, rank, world)
-    assert count == 62_500_000
     codes_h = synth.umi_codes(n_total, L, start=start, count=count)
     codes = torch.from_numpy(codes_h.view(np.int32)).to(dev)
     batch = D.PackedBatch(codes, L)
-    gathered = torch.zeros(world * bitmaps[0].numel(), dtype=bitmaps[0].dtype, device=dev)
+    nw = next(b for b in bitmaps if b is not None).numel()
+    gathered = torch.zeros(world * nw, dtype=torch.int64, device=dev)
     for r in range(world):
         if r != rank:
-            gathered[r * bitmaps[0].numel():(r + 1) * bitmaps[0].numel()].copy_(bitmaps[r])
+            gathered[r * nw:(r + 1) * nw].copy_(bitmaps[r])
 
     def exchange(bm):  # the all-gather of rank `rank`: its own bitmap in its slot
-        gathered[rank * bm.numel():(rank + 1) * bm.numel()].copy_(bm)
+        gathered[rank * nw:(rank + 1) * nw].copy_(bm)
         return gathered, world
 
     pipe = UmiPipeline(L, min(n_total, 4 ** L), count, dev, depth=2, target=b"ACGTACGTACGT", max_distance=1,
-                       score_alone=True, exchange=exchange)
+                       score_alone=True, exchange=exchange, with_scores=scores)
     slot = pipe.submit(batch)
     pipe.drain()
     torch.cuda.synchronize()
-    got = {f: slot.scores[f][:count].cpu().numpy() for f in P.FIELDS}
-    cid = slot.cid[:count].cpu().numpy().view(np.uint32)
-    within = np.unpackbits(slot.within.cpu().numpy().view(np.uint8), bitorder="little")[:count].astype(bool)
+    out = {"cid": slot.cid[:count].cpu().numpy().view(np.uint32)}
+    if scores:
+        out.update({f: slot.scores[f][:count].cpu().numpy() for f in P.FIELDS})
+        out["within"] = np.unpackbits(slot.within.cpu().numpy().view(np.uint8), bitorder="little")[:count].astype(bool)
     stats = slot.eng.stats()
     del pipe, slot, batch, codes, gathered, bitmaps
     torch.cuda.empty_cache()
+    return codes_h, out, stats
+
+
+def _union_codes(n_total, world, L):
+    """The sorted distinct codes of all `world` shards, from a host presence array (no sort
+    of the n_total codes)."""
+    from rogtk_amd import dist as RD
+    from rogtk_amd import synth
+
+    present = np.zeros(4 ** L, dtype=bool)
+    for r in range(world):
+        s0, c0 = RD.shard_range(n_total, r, world)
+        present[synth.umi_codes(n_total, L, start=s0, count=c0)] = True
+    return np.flatnonzero(present).astype(np.uint32)
+
+
+def _check_union_ids(codes_h, cid, stats, union, L):
+    from oracle import pyoracle as P
+    from rogtk_amd import synth
+
+    threads = min(16, os.cpu_count() or 1)
+    rc, _, rk, _ = P.umi_cluster(P.StrCol.from_fixed(synth.codes_to_ascii(union, L)), L, 1, threads=threads)
+    assert stats["n_distinct"] == len(union)
+    assert stats["n_clusters"] == rk and stats["overflow"] == 0
+    assert np.array_equal(cid, rc[np.searchsorted(union, codes_h)])
+    return rk
+
+
+@pytest.mark.timeout(600)
+def test_c4_rank_of_8_against_the_union():
+    """C4 at N = 8 (500M reads, 62.5M per rank), emulated on one GPU exactly as each rank
+    runs it: rank 3's shard goes through UmiPipeline (bench.py's defaults) with the
+    exchange returning the all-gathered bitmaps of all 8 shards (the other 7 built here,
+    ~95% of the 4^12 codes present in their union). Every output is compared: all 7 H1
+    fields and the Hamming-within bits on the rank's distinct codes (a regular row's scores
+    are a function of its code), and the ids against the oracle's union-find over the
+    union's distinct codes (ids depend only on the global distinct set). At this density
+    the union is one cluster: the non-degenerate N = 8 ids are the C2 test below."""
+    from oracle import pyoracle as P
+    from rogtk_amd import synth
+
+    n_total, world, rank, L = 500_000_000, 8, 3, 12
+    codes_h, got, stats = _rank_of_world(n_total, world, rank, L)
+    assert len(codes_h) == 62_500_000
     print(f"C4 rank {rank} of {world} on GPU done: {stats}", flush=True)
     # H1 / H2 on the rank's distinct codes
     uniq, inv = np.unique(codes_h, return_inverse=True)
@@ -104,17 +145,29 @@ def test_c4_rank_of_8_against_the_union():
         else:
             assert np.array_equal(g.view(np.uint32), r.astype(np.uint32)[inv]), f
     _, rw, _ = P.hamming(ucol, b"ACGTACGTACGT", 1)
-    assert np.array_equal(within, rw[inv])
-    del ucol, ref
-    # H3 over the union of the 8 shards' distinct codes
-    union = uniq
-    for r in range(world):
-        if r != rank:
-            s0, c0 = RD.shard_range(n_total, r, world)
-            union = np.union1d(union, np.unique(synth.umi_codes(n_total, L, start=s0, count=c0)))
-    assert stats["n_distinct"] == len(union) and len(union) > 0.9 * 4 ** L
-    threads = min(16, os.cpu_count() or 1)
-    rc, _, rk, _ = P.umi_cluster(P.StrCol.from_fixed(synth.codes_to_ascii(union, L)), L, 1, threads=threads)
-    print(f"oracle H3 on the union's {len(union)} distinct codes done", flush=True)
-    assert stats["n_clusters"] == rk and stats["overflow"] == 0
-    assert np.array_equal(cid, rc[np.searchsorted(union, codes_h)])
+    assert np.array_equal(got["within"], rw[inv])
+    del ucol, ref, uniq, inv
+    union = _union_codes(n_total, world, L)
+    assert len(union) > 0.9 * 4 ** L
+    _check_union_ids(codes_h, got["cid"], stats, union, L)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("L,min_clusters", [(12, 1), (13, 10_000)])
+def test_c2_weak_scaling_rank_of_8_union(L, min_clusters):
+    """C2 weak scaling at N = 8 (what bench.py --gpus 8 runs: 10M reads per rank, 80M in all),
+    rank 5 emulated on one GPU against the all-gathered bitmaps of the 8 shards; the ids
+    against the oracle's union-find over the union's distinct codes. At 12 bp the union is
+    41% of the code space and Hamming-1 joins all of it into ONE cluster (6.94M codes; a
+    site percolation far above threshold: 36 neighbours per code), so the same shards with
+    13-bp UMIs (12.6% dense, 36,893 clusters, the largest 8.41M codes) pin the merge where
+    the answer is not degenerate."""
+    n_total, world, rank = 80_000_000, 8, 5
+    codes_h, got, stats = _rank_of_world(n_total, world, rank, L, scores=False)
+    assert len(codes_h) == 10_000_000
+    print(f"C2 x8 rank {rank}, {L} bp: {stats}", flush=True)
+    union = _union_codes(n_total, world, L)
+    rk = _check_union_ids(codes_h, got["cid"], stats, union, L)
+    assert rk >= min_clusters
+    if L == 13:
+        assert rk > 10_000 and len(np.unique(got["cid"])) > 10_000

@@ -10,10 +10,12 @@ groups, k = 17 -> effective 32, min_coverage 20 as rogtk/__init__.py:212) -> eve
 * 1M reads (~111k groups) plus injected groups that force every size class and hand-off:
   15 / 40 / 100 unrelated reads (distinct k-mers past class 3's and class 1's tables),
   250 and 700 reads of one template (class 4 and the global radix path), compared in full.
-* 100M reads (the C3 configuration, 11 spectrum calls): size-independent properties over
-  every group (n_sequences, node/terminal/isolated counts recomputed from the returned exts,
-  counts >= min_coverage, ascending k-mers), 300 random groups compared in full with the
-  oracle, and bitwise determinism of a second run.
+* 100M reads (the C3 configuration, 1 and 11 spectrum calls): size-independent properties
+  over every group (n_sequences, node/terminal/isolated counts recomputed from the returned
+  exts, counts >= min_coverage, ascending k-mers), the groups the minimizer filter decided
+  (emptied and kept) and 300 random groups compared in full with the oracle, and one digest
+  of every output for one call, 10M-row calls and the path without the repeat certificate
+  and the minimizer filter (round 5).
 """
 from __future__ import annotations
 
@@ -159,10 +161,9 @@ def _props(calls, min_cov):
     return nseq, groups, int(digest.item())
 
 
-def test_c3_full_size_100m_properties():
+def _c3_100m_inputs():
     import torch
 
-    from oracle import pyoracle as P
     from rogtk_amd import device as D
     from rogtk_amd import synth
 
@@ -173,51 +174,133 @@ def test_c3_full_size_100m_properties():
     for a in range(0, n, chunk):
         b = min(n, a + chunk)
         values[a * RL:b * RL] = torch.from_numpy(synth.reads(n, RL, start=a, count=b - a).reshape(-1)).cuda()
-    print("C3 100M: reads in HBM", flush=True)
     codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
     offsets = torch.arange(0, (n + 1) * RL, RL, dtype=torch.int64, device="cuda")
     eng = D.ClusterEngine(UL, min(n, 4 ** UL), "cuda")
     cid = torch.empty(n, dtype=torch.int32, device="cuda")
+    D.cluster_batch(eng, D.PackedBatch(codes, UL), cid, 0)
+    return n, values, offsets, cid
+
+
+def c3_100m_digest():
+    """(properties + digest, groups, calls) of the default C3 path at 100M reads, one spectrum
+    call; the knob child below runs it under other environments."""
+    import torch
+
+    from rogtk_amd import device as D
+
+    n, values, offsets, cid = _c3_100m_inputs()
+    rows, go, G, calls = D.group_spectra(offsets, values, cid, K, MINCOV, batch_rows=100_000_000)
+    torch.cuda.synchronize()
+    return _props(calls, MINCOV) + (G, len(calls))
+
+
+KNOB_CHILD = r"""
+import importlib.util, json, sys
+sys.path.insert(0, {root!r})
+spec = importlib.util.spec_from_file_location("c3t", {path!r})
+m = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(m)
+print("DIGEST " + json.dumps(list(m.c3_100m_digest())), flush=True)
+"""
+
+
+def _oracle_groups(pick, rows_h, goh, values, n, calls):
+    """Groups `pick` (indices of one run's groups) in full against the oracle."""
+    from oracle import pyoracle as P
+    import torch
+
+    sub_rows, sub_go = [], [0]
+    for g in pick:
+        rr = rows_h[goh[g]:goh[g + 1]]
+        sub_rows.append(rr)
+        sub_go.append(sub_go[-1] + len(rr))
+    sub_rows = np.concatenate(sub_rows)
+    reads_sub = values.view(n, RL)[torch.from_numpy(sub_rows).cuda()].cpu().numpy()
+    ref = P.kmer_spectrum(P.StrCol.from_fixed(reads_sub), K, MINCOV, False, np.array(sub_go), threads=THREADS)
+    starts = np.concatenate([[0], np.cumsum([len(c[2]["stats"]) for c in calls])])
+    nonempty = 0
+    for j, g in enumerate(pick):
+        ci = int(np.searchsorted(starts, g, side="right")) - 1
+        r = calls[ci][2]
+        lg = g - starts[ci]
+        eo = r["entry_offsets"][lg:lg + 2].cpu().numpy()
+        a, b = int(eo[0]), int(eo[1])
+        ra, rb = int(ref["group_offsets"][j]), int(ref["group_offsets"][j + 1])
+        assert np.array_equal(r["stats"][lg].cpu().numpy(), ref["stats"][j]), g
+        km = r["kmers"][a:b].cpu().numpy().view(np.uint64)
+        assert np.array_equal(km[:, 0], ref["kmer_hi"][ra:rb]) and np.array_equal(km[:, 1], ref["kmer_lo"][ra:rb]), g
+        assert np.array_equal(r["exts"][a:b].cpu().numpy(), ref["exts"][ra:rb]), g
+        assert np.array_equal(r["counts"][a:b].cpu().numpy().view(np.uint16), ref["counts"][ra:rb]), g
+        nonempty += rb > ra
+    return nonempty
+
+
+def test_c3_full_size_100m_properties():
+    """C3 at full size (100M reads): properties of every group, the groups the minimizer
+    filter decided (>= 1000 it emptied and every one / >= 1000 it kept) plus 300 random
+    groups in full against the oracle, a digest of every output identical for one call and
+    10M-row calls, and identical to the path without the repeat certificate and the
+    minimizer filter (ROGTK_KMER_CERT=0 ROGTK_KMER_MZ=0, a child process)."""
+    import json
+    import subprocess
+    import sys
+
+    import torch
+
+    from rogtk_amd import _lib
+    from rogtk_amd import device as D
+
+    n, values, offsets, cid = _c3_100m_inputs()
+    print("C3 100M: reads in HBM", flush=True)
     results = []
     for run in range(2):  # one spectrum call (the default), then calls of 10M rows
-        D.cluster_batch(eng, D.PackedBatch(codes, UL), cid, 0)
-        rows, go, G, calls = D.group_spectra(offsets, values, cid, K, MINCOV,
-                                             batch_rows=100_000_000 if run == 0 else 10_000_000)
-        torch.cuda.synchronize()
+        dec = None
+        if run == 0:  # the minimizer filter's decision per group (tests-only hook)
+            dec = torch.zeros(n + 1, dtype=torch.uint8, device="cuda")
+            _lib.call("rogtk_kmer_debug_filter", D._p(dec), n + 1)
+        try:
+            rows, go, G, calls = D.group_spectra(offsets, values, cid, K, MINCOV,
+                                                 batch_rows=100_000_000 if run == 0 else 10_000_000)
+            torch.cuda.synchronize()
+        finally:
+            _lib.call("rogtk_kmer_debug_filter", None, 0)
         results.append(_props(calls, MINCOV) + (G, len(calls)))
         print(f"C3 100M run {run}: {results[-1]}", flush=True)
         if run == 0:
-            # 300 random groups in full against the oracle
             rng = np.random.default_rng(3)
             goh = go.cpu().numpy()
-            pick = np.sort(rng.choice(G, size=300, replace=False))
             rows_h = rows.cpu().numpy()
-            sub_rows, sub_go = [], [0]
-            for g in pick:
-                rr = rows_h[goh[g]:goh[g + 1]]
-                sub_rows.append(rr)
-                sub_go.append(sub_go[-1] + len(rr))
-            sub_rows = np.concatenate(sub_rows)
-            reads_sub = values.view(n, RL)[torch.from_numpy(sub_rows).cuda()].cpu().numpy()
-            ref = P.kmer_spectrum(P.StrCol.from_fixed(reads_sub), K, MINCOV, False, np.array(sub_go), threads=THREADS)
-            starts = np.concatenate([[0], np.cumsum([len(c[2]["stats"]) for c in calls])])
-            for j, g in enumerate(pick):
-                ci = int(np.searchsorted(starts, g, side="right")) - 1
-                r = calls[ci][2]
-                lg = g - starts[ci]
-                eo = r["entry_offsets"][lg:lg + 2].cpu().numpy()
-                a, b = int(eo[0]), int(eo[1])
-                ra, rb = int(ref["group_offsets"][j]), int(ref["group_offsets"][j + 1])
-                assert np.array_equal(r["stats"][lg].cpu().numpy(), ref["stats"][j])
-                km = r["kmers"][a:b].cpu().numpy().view(np.uint64)
-                assert np.array_equal(km[:, 0], ref["kmer_hi"][ra:rb]) and np.array_equal(km[:, 1], ref["kmer_lo"][ra:rb])
-                assert np.array_equal(r["exts"][a:b].cpu().numpy(), ref["exts"][ra:rb])
-                assert np.array_equal(r["counts"][a:b].cpu().numpy().view(np.uint16), ref["counts"][ra:rb])
+            d = dec[:G].cpu().numpy()
+            emptied, kept = np.flatnonzero(d == 1), np.flatnonzero(d >= 2)
+            print(f"filter: {len(emptied)} emptied, {len(kept)} kept", flush=True)
+            assert len(emptied) >= 1000 and len(kept) >= 1
+            pick_k = np.sort(rng.choice(kept, size=min(len(kept), 1500), replace=False))
+            ne = min(len(emptied), max(1500, 2000 - len(pick_k)))
+            pick_e = np.sort(rng.choice(emptied, size=ne, replace=False))
+            assert len(pick_e) + len(pick_k) >= 2000
+            # every emptied group's output is empty (stats say node_count 0); checked in full
+            # against the oracle for the sample
+            assert _oracle_groups(pick_e, rows_h, goh, values, n, calls) == 0
+            nk = _oracle_groups(pick_k, rows_h, goh, values, n, calls)
+            print(f"kept groups with valid k-mers: {nk} of {len(pick_k)}", flush=True)
+            _oracle_groups(np.sort(rng.choice(G, size=300, replace=False)), rows_h, goh, values, n, calls)
         del calls, rows, go
     # bitwise deterministic and independent of the call split (digest of every output array)
     assert results[0][:4] == results[1][:4]
     nseq, groups, _, G, ncalls = results[0]
     assert nseq == n and groups == G and ncalls == 1 and results[1][4] >= 10
+    del values, offsets, cid
+    torch.cuda.empty_cache()
+    # the same outputs without the certificate and the filter (every group through the LDS /
+    # global kernels): a child process, the knobs being read once per process
+    env = dict(os.environ, ROGTK_KMER_CERT="0", ROGTK_KMER_MZ="0")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-u", "-c", KNOB_CHILD.format(root=root, path=os.path.abspath(__file__))],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    child = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("DIGEST ")][-1][7:])
+    assert tuple(child) == results[0], (child, results[0])
 
 
 @pytest.mark.parametrize("lo,hi,bw", [(0, 150, 8), (100, 420, 16), (300, 990, 32)])

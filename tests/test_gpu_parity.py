@@ -580,8 +580,7 @@ def test_local_cc_prediction_redo(rg, deferred, poison):
     sizes = [900_000, 3_400_000, 5_500_000, 900_000, 900_000]
     eng = D.ClusterEngine(12, max(sizes), "cuda")
     for i, n_codes in enumerate(sizes):
-        rng = np.random.default_rng(1000 + i)
-        codes_h = rng.integers(0, 4 ** 12, n_codes, dtype=np.uint32)
+        codes_h, rc, rk = _redo_batch(i, n_codes)
         codes = torch.from_numpy(codes_h.view(np.int32)).cuda()
         batch = D.PackedBatch(codes, 12)
         cid = torch.empty(n_codes, dtype=torch.int32, device="cuda")
@@ -593,9 +592,23 @@ def test_local_cc_prediction_redo(rg, deferred, poison):
         eng.sync()
         stats = eng.stats()
         torch.cuda.synchronize()
-        rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, 12)), 12, 1)
         assert stats["n_clusters"] == rk and stats["error"] == 0, i
         assert np.array_equal(cid.cpu().numpy().view(np.uint32), rc), i
+
+
+_REDO_CACHE = {}
+
+
+def _redo_batch(i, n_codes):
+    """Batch i of the redo test and its oracle ids (the same for every parametrisation)."""
+    if i not in _REDO_CACHE:
+        from rogtk_amd import synth
+
+        codes_h = np.random.default_rng(1000 + i).integers(0, 4 ** 12, n_codes, dtype=np.uint32)
+        rc, _, rk, _ = P().umi_cluster(P().StrCol.from_fixed(synth.codes_to_ascii(codes_h, 12)), 12, 1,
+                                       threads=min(16, os.cpu_count() or 1))
+        _REDO_CACHE[i] = (codes_h, rc, rk)
+    return _REDO_CACHE[i]
 
 
 @pytest.mark.parametrize("shards", [2, 4, 8])
