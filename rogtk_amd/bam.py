@@ -30,7 +30,9 @@ results.
 from __future__ import annotations
 
 import ctypes
+from concurrent.futures import ThreadPoolExecutor
 import os
+import time
 from typing import Iterator, List, Optional, Sequence
 
 import numpy as np
@@ -552,25 +554,50 @@ def bams_umi_cluster(bam_paths: Sequence[str], umi_len: int = 12, max_distance: 
     W = RD.world(group)
     r = torch.distributed.get_rank(group) if W > 1 else 0
     paths = list(bam_paths)
+    tm = [("start", time.perf_counter())] if os.environ.get("ROGTK_BAM_TIMING") == "1" else None
     ranges = _umi_ranges(paths, ranges_per_file or W, split)
     mine = [j for j in range(len(ranges)) if j % W == r]
     dev = torch.device("cuda", torch.cuda.current_device())
-    res = {}  # range index -> (column, names, skip used, tail)
+    res = {}  # range index -> (column, names, skip used, tail, error)
+    # this rank's ranges decode concurrently (round 5): one host thread per range, each with
+    # its own reader (its share of the inflate threads) and its own device stream, as the
+    # reference hands its segments to a worker pool (bam_htslib.rs:665-725)
+    per_reader = max(1, (n_threads or 16) // max(len(mine), 1)) if len(mine) > 1 else n_threads
 
     def decode(j, skip):
+        torch.cuda.set_device(dev)  # a worker thread starts on the process's default device
+        t0 = time.perf_counter()
         fi, i, c0, c1 = ranges[j]
+        if skip is None:
+            skip = 0 if i == 0 else bam_find_record(paths[fi], c0)
         try:
-            col, nm, tail = bam_umis_dev(paths[fi], umi_len, source, sep, mode, n_threads, with_names=True,
+            col, nm, tail = bam_umis_dev(paths[fi], umi_len, source, sep, mode, per_reader, with_names=True,
                                          rng=None if (c0 == 0 and c1 < 0) else (c0, c1, skip), return_tail=True)
-        except _lib.RogtkError:
+            res[j] = (col, nm, skip, tail, None)
+            if tm is not None:
+                print(f"range {j}: {t0 - tm[0][1]:.4f} .. {time.perf_counter() - tm[0][1]:.4f} s, {col[3]} rows",
+                      flush=True)
+        except _lib.RogtkError as e:
             if ranges[j][1] == 0:
                 raise  # a range that starts with the header: a real error
-            col, nm, tail = None, None, -3  # a wrong guess can frame garbage: decode again below
-        res[j] = (col, nm, skip, tail)
+            # a wrong guess can frame garbage: decoded again below; kept to re-raise if the
+            # guess turns out right (then the error is the file's)
+            res[j] = (None, None, skip, -3, e)
 
-    for j in mine:
-        fi, i, c0, c1 = ranges[j]
-        decode(j, 0 if i == 0 else bam_find_record(paths[fi], c0))
+    def decode_all(jobs):
+        if len(jobs) == 1:
+            decode(*jobs[0])
+            return
+        with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
+            for f in [ex.submit(decode, j, skip) for j, skip in jobs]:
+                f.result()
+        torch.cuda.synchronize(dev)  # the workers' streams, before the columns are used here
+
+    if tm is not None:
+        tm.append(("split", time.perf_counter()))
+    decode_all([(j, None) for j in mine])
+    if tm is not None:
+        tm.append(("decode", time.perf_counter()))
     # check every guessed skip against the previous range's tail (exact once that range's
     # own start is); at most len(ranges) rounds, one in practice
     for _ in range(len(ranges)):
@@ -583,11 +610,12 @@ def bams_umi_cluster(bam_paths: Sequence[str], umi_len: int = 12, max_distance: 
             t = tt.cpu()
         bad = [j for j in range(len(ranges))
                if ranges[j][1] > 0 and (t[j, 0] != t[j - 1, 1] or t[j - 1, 1] < 0)]
+        for j in mine:  # a failed range whose start was right: the error is real
+            if res[j][4] is not None and ranges[j][1] > 0 and t[j - 1, 1] >= 0 and t[j, 0] == t[j - 1, 1]:
+                raise res[j][4]
         if not bad:
             break
-        for j in bad:
-            if j in mine and t[j - 1, 1] >= 0:
-                decode(j, int(t[j - 1, 1]))
+        decode_all([(j, int(t[j - 1, 1])) for j in bad if j in mine and t[j - 1, 1] >= 0])
     else:
         raise _lib.RogtkError(_lib.ROGTK_E_INVALID, "bam ranges: record boundaries did not settle")
     parts = [res[j][0] for j in mine]
@@ -595,10 +623,38 @@ def bams_umi_cluster(bam_paths: Sequence[str], umi_len: int = 12, max_distance: 
     srcs = [pa.array([paths[ranges[j][0]]] * res[j][0][3], pa.string()) for j in mine]
     off, val, vw, n = _concat_dev([p[0] for p in parts], [p[1] for p in parts], [p[2] for p in parts],
                                   [p[3] for p in parts], dev) if parts else _concat_dev([], [], [], [], dev)
-    cid, k = RD.umi_cluster_sharded(off, val, n, umi_len, max_distance, validity=vw.view(torch.uint8), group=group)
+    if tm is not None:
+        torch.cuda.synchronize(dev)
+        tm.append(("settle+concat", time.perf_counter()))
+    if W == 1:  # no exchange: the single-GPU H3 on the whole column (same ids)
+        cid, k = _cluster_dev(off, val, vw, n, umi_len, max_distance)
+    else:
+        cid, k = RD.umi_cluster_sharded(off, val, n, umi_len, max_distance, validity=vw.view(torch.uint8),
+                                        group=group)
+    if tm is not None:
+        torch.cuda.synchronize(dev)
+        tm.append(("cluster", time.perf_counter()))
     nm = pa.concat_arrays(names) if names else pa.array([], pa.string())
     src = pa.concat_arrays(srcs) if srcs else pa.array([], pa.string())
-    return _umi_table(off, val, vw, n, nm, cid, k, {"source": src})
+    out = _umi_table(off, val, vw, n, nm, cid, k, {"source": src})
+    if tm is not None:
+        tm.append(("table", time.perf_counter()))
+        print("bams_umi_cluster timing (s): " + ", ".join(f"{a}={b - tm[i][1]:.4f}" for i, (a, b) in
+                                                         enumerate(tm[1:])), flush=True)
+    return out
+
+
+def _cluster_dev(off, val, vw, n, umi_len, max_distance):
+    """rogtk_umi_cluster_dev on a device UMI column: (cluster_id int32 tensor, n_clusters)."""
+    import torch
+
+    stream = torch.cuda.current_stream()
+    cid = torch.empty(max(n, 1), dtype=torch.int32, device=off.device)
+    ncl = ctypes.c_int64(0)
+    _lib.call("rogtk_umi_cluster_dev", ctypes.c_void_p(off.data_ptr()), ctypes.c_void_p(val.data_ptr()),
+              ctypes.c_void_p(vw.data_ptr()), n, int(umi_len), int(max_distance), ctypes.c_void_p(cid.data_ptr()),
+              ctypes.byref(ncl), ctypes.c_void_p(stream.cuda_stream))
+    return cid, ncl.value
 
 
 def bam_umi_cluster(bam_path: str, umi_len: int = 12, max_distance: int = 1, source: str = "sequence",
@@ -606,13 +662,6 @@ def bam_umi_cluster(bam_path: str, umi_len: int = 12, max_distance: int = 1, sou
     """Config C5: BAM -> GPU decode -> UMI column -> H3 cluster ids (and the UMI).
     Returns a Table {name, umi, cluster_id} with the H3 semantics of umi_cluster
     (DESIGN.md §4): dense ids, regular UMIs first, irregular ones after, null -> null."""
-    import torch
-
     (off, val, vw, n), names = bam_umis_dev(bam_path, umi_len, source, sep, mode, n_threads, with_names=True)
-    stream = torch.cuda.current_stream()
-    cid = torch.empty(max(n, 1), dtype=torch.int32, device=off.device)
-    ncl = ctypes.c_int64(0)
-    _lib.call("rogtk_umi_cluster_dev", ctypes.c_void_p(off.data_ptr()), ctypes.c_void_p(val.data_ptr()),
-              ctypes.c_void_p(vw.data_ptr()), n, int(umi_len), int(max_distance), ctypes.c_void_p(cid.data_ptr()),
-              ctypes.byref(ncl), ctypes.c_void_p(stream.cuda_stream))
-    return _umi_table(off, val, vw, n, names, cid, ncl.value)
+    cid, ncl = _cluster_dev(off, val, vw, n, umi_len, max_distance)
+    return _umi_table(off, val, vw, n, names, cid, ncl)

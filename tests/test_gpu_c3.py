@@ -55,7 +55,7 @@ def _inject(reads, codes, rng):
                     reads[r, int(rng.integers(RL))] = acgt[int(rng.integers(4))]
 
 
-def _run_c3(codes_h, reads_h, min_cov=MINCOV, batch_rows=10_000_000, packed="auto"):
+def _run_c3(codes_h, reads_h, min_cov=MINCOV, batch_rows=10_000_000, packed="auto", k=K):
     import torch
 
     from rogtk_amd import device as D
@@ -67,7 +67,7 @@ def _run_c3(codes_h, reads_h, min_cov=MINCOV, batch_rows=10_000_000, packed="aut
     eng = D.ClusterEngine(UL, min(n, 4 ** UL), "cuda")
     cid = torch.empty(n, dtype=torch.int32, device="cuda")
     D.cluster_batch(eng, D.PackedBatch(codes, UL), cid, 0)
-    rows, go, G, calls = D.group_spectra(offsets, values, cid, K, min_cov, batch_rows=batch_rows, packed=packed)
+    rows, go, G, calls = D.group_spectra(offsets, values, cid, k, min_cov, batch_rows=batch_rows, packed=packed)
     torch.cuda.synchronize()
     return rows, go, G, calls
 
@@ -90,10 +90,13 @@ def _concat(calls, G):
             "group_offsets": np.concatenate(eo), "stats": np.concatenate(st)}
 
 
-@pytest.mark.parametrize("min_cov,batch_rows,packed,filt", [(MINCOV, 10_000_000, "auto", 0), (2, 200_000, "auto", 0),
-                                                             (MINCOV, 10_000_000, None, 0),
-                                                             (MINCOV, 10_000_000, "auto", 1), (3, 200_000, "auto", 1)])
-def test_c3_path_1m_vs_oracle(min_cov, batch_rows, packed, filt):
+@pytest.mark.parametrize("k,min_cov,batch_rows,packed,filt", [
+    (K, MINCOV, 10_000_000, "auto", 0), (K, 2, 200_000, "auto", 0), (K, MINCOV, 10_000_000, None, 0),
+    (K, MINCOV, 10_000_000, "auto", 1), (K, 3, 200_000, "auto", 1),
+    # the reference's defaults: k = 15 (docstring) and 10 (assemble_sequences), effective 16,
+    # min_coverage 5 (rogtk/__init__.py:106-107, 211-212)
+    (15, 5, 10_000_000, "auto", 1), (10, 5, 200_000, "auto", 1), (15, 5, 10_000_000, None, 1)])
+def test_c3_path_1m_vs_oracle(k, min_cov, batch_rows, packed, filt):
     """packed "auto": rows staged from the 2-bit block column (rogtk_pack_reads); None: from
     the ASCII bytes. filt: with the minimizer filter (rogtk_kmer_set_filter)."""
     from oracle import pyoracle as P
@@ -109,7 +112,7 @@ def test_c3_path_1m_vs_oracle(min_cov, batch_rows, packed, filt):
     _lib.call("rogtk_kmer_set_path", 1)
     _lib.call("rogtk_kmer_set_filter", filt)
     try:
-        rows, go, G, calls = _run_c3(codes_h, reads_h, min_cov, batch_rows, packed)
+        rows, go, G, calls = _run_c3(codes_h, reads_h, min_cov, batch_rows, packed, k)
     finally:
         _lib.call("rogtk_kmer_set_filter", 1)
     ps = (ctypes.c_int64 * 2)()
@@ -120,12 +123,13 @@ def test_c3_path_1m_vs_oracle(min_cov, batch_rows, packed, filt):
     goh = np.concatenate([starts, [n]]).astype(np.int64)
     assert G == len(starts) and np.array_equal(go.cpu().numpy(), goh)
     got = _concat(calls, G)
-    ref = P.kmer_spectrum(P.StrCol.from_fixed(reads_h[order]), K, min_cov, False, goh, threads=THREADS)
+    ref = P.kmer_spectrum(P.StrCol.from_fixed(reads_h[order]), k, min_cov, False, goh, threads=THREADS)
     assert np.array_equal(got["group_offsets"], ref["group_offsets"])
     assert np.array_equal(got["stats"], ref["stats"])
     for f in ("kmer_hi", "kmer_lo", "exts", "counts"):
         assert np.array_equal(got[f], ref[f]), f
     assert G > 100_000 and len(calls) >= (1 if batch_rows >= n else 5)
+    assert (got["stats"][:, 0] == (16 if k <= 16 else 32)).all()
 
 
 def _props(calls, min_cov):

@@ -103,7 +103,8 @@ def main():
     c5_s = time.perf_counter() - t
     assert tab.num_rows == n
     # the same file cut into 4 ranges at BGZF block starts (what 4 ranks would each decode),
-    # here all on one GPU one after another: rows and ids identical to the whole-file run
+    # here all on one GPU, decoded concurrently (one host thread, reader and stream per
+    # range): rows and ids identical to the whole-file run
     t = time.perf_counter()
     tab4 = B.bams_umi_cluster([args.path], umi_len=umi_len, max_distance=1, source="sequence", mode=args.mode,
                               n_threads=args.threads, ranges_per_file=4)
@@ -143,7 +144,8 @@ def main():
         "c5_4_ranges": {"records_per_s": n / c5r_s, "wall_s": round(c5r_s, 3),
                         "path": "bams_umi_cluster(ranges_per_file=4) on one GPU: the file cut at BGZF block "
                                 "starts, each range's first record found and checked against the previous "
-                                "range's tail, ranges decoded one after another; ids equal the whole-file run"},
+                                "range's tail, the ranges decoded concurrently (a host thread, reader and stream "
+                                "each, the inflate threads shared out); ids equal the whole-file run"},
         "cpu_baseline": cpu,
         "cores_available": os.cpu_count(),
     }

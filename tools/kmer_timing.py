@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Experiment: per-phase clocks of k_kmer_lds (needs the ROGTK_KMER_TIMING build of the
 library in place of rogtk_amd/librogtk_hip.so; see tools/kmer_timing.sh). Runs
-tools/bench_kmer.py's step once more after its own run and prints the phase split."""
+tools/bench_kmer.py's step once more after its own run (extra arguments are passed to it)
+and prints the phase split."""
 import ctypes
 import os
 import runpy
@@ -12,7 +13,7 @@ sys.path.insert(0, ROOT)
 from rogtk_amd import _lib  # noqa: E402
 
 buf = (ctypes.c_ulonglong * 8)()
-sys.argv = [os.path.join(ROOT, "tools", "bench_kmer.py"), "--steps", "1", "--warmup", "1"]
+sys.argv = [os.path.join(ROOT, "tools", "bench_kmer.py"), "--steps", "1", "--warmup", "1"] + sys.argv[1:]
 _lib.call("rogtk_kmer_timing", buf)
 runpy.run_path(sys.argv[0], run_name="__main__")
 _lib.call("rogtk_kmer_timing", buf)

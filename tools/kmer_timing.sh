@@ -4,4 +4,4 @@
 set -eu
 cd "$GRAFT_REPO_ROOT"
 cp tools/ab/kt.so rogtk_amd/librogtk_hip.so
-timeout -k 10 180 python3 tools/kmer_timing.py
+timeout -k 10 180 python3 tools/kmer_timing.py "$@"
