@@ -130,18 +130,30 @@ FIELDS = ("shannon_entropy", "linguistic_complexity", "homopolymer_fraction",
           "dinucleotide_entropy", "longest_homopolymer_run", "dust_score", "combined_score")
 
 
-def umi_complexity(col: StrCol, dinuc_order: int = 0) -> dict:
-    """Oracle H1 over a column. Returns dict field -> numpy array (+ 'valid')."""
+def umi_complexity(col: StrCol, dinuc_order: int = 0, threads: int = 1) -> dict:
+    """Oracle H1 over a column. Returns dict field -> numpy array (+ 'valid'). threads > 1
+    runs row ranges on host threads (the C loop is per row; identical results)."""
     L = lib()
     n = col.n
     out = {f: np.zeros(n, dtype=np.uint32 if f == "longest_homopolymer_run" else np.float64) for f in FIELDS}
     o, v, val = col._ptrs()
-    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)
-    L.oracle_umi_complexity_batch(o, 8, v, val, 0, n, dinuc_order,
-                                  vp(out["shannon_entropy"]), vp(out["linguistic_complexity"]),
-                                  vp(out["homopolymer_fraction"]), vp(out["dinucleotide_entropy"]),
-                                  vp(out["longest_homopolymer_run"]), vp(out["dust_score"]),
-                                  vp(out["combined_score"]))
+
+    def run(a, b):
+        at = lambda arr: ctypes.c_void_p(arr.ctypes.data + a * arr.itemsize)
+        L.oracle_umi_complexity_batch(ctypes.c_void_p(col.offsets.ctypes.data + 8 * a), 8, v, val, a, b - a,
+                                      dinuc_order, at(out["shannon_entropy"]), at(out["linguistic_complexity"]),
+                                      at(out["homopolymer_fraction"]), at(out["dinucleotide_entropy"]),
+                                      at(out["longest_homopolymer_run"]), at(out["dust_score"]),
+                                      at(out["combined_score"]))
+
+    if threads <= 1 or n < 1 << 16:
+        run(0, n)
+    else:
+        from concurrent.futures import ThreadPoolExecutor
+        cuts = np.linspace(0, n, threads + 1).astype(np.int64)
+        with ThreadPoolExecutor(threads) as ex:
+            for f in [ex.submit(run, int(cuts[i]), int(cuts[i + 1])) for i in range(threads)]:
+                f.result()
     out["valid"] = col.valid_mask()
     return out
 

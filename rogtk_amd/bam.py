@@ -472,6 +472,8 @@ def bam_umis_dev(bam_path: str, umi_len: int = 12, source: str = "sequence", sep
                     names.append_strings(b.offsets[0], b.values[0], n, name_bound)
             r.check(stream)
             tail = r.tail()
+            if os.environ.get("ROGTK_BAM_TIMING") == "1":
+                print(f"reader {rng}: {r.timers()}", flush=True)
         out = umi.finish(), (names.to_host_strings() if names is not None else None)
     caller.wait_stream(stream)
     if stream is not caller:  # the column is used on the caller's stream from here on
@@ -613,6 +615,9 @@ def bams_umi_cluster(bam_paths: Sequence[str], umi_len: int = 12, max_distance: 
         for j in mine:  # a failed range whose start was right: the error is real
             if res[j][4] is not None and ranges[j][1] > 0 and t[j - 1, 1] >= 0 and t[j, 0] == t[j - 1, 1]:
                 raise res[j][4]
+        if tm is not None:
+            print(f"settle: skips {[int(t[j, 0]) for j in range(len(ranges))]}, tails "
+                  f"{[int(t[j, 1]) for j in range(len(ranges))]}, redo {bad}", flush=True)
         if not bad:
             break
         decode_all([(j, int(t[j - 1, 1])) for j in bad if j in mine and t[j - 1, 1] >= 0])

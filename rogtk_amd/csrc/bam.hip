@@ -401,8 +401,40 @@ inline double now_s() {
 
 // One cached pinned stream buffer, handed from a closed reader to the next one opened
 // (page-locking hundreds of MB costs more than decoding them).
+// Stream buffers of closed readers, reused by the next ones (a pinned allocation of the
+// size a file's stream needs costs ~0.2 s): a pool, so the concurrent range readers of one
+// file (rogtk_amd/bam.py bams_umi_cluster) each find one after the first call (round 5;
+// one cached buffer left three of four range readers growing their own)
+constexpr size_t kPinPool = 8;
 std::mutex g_pin_mu;
-PinnedBuf g_pin_cache;
+std::vector<PinnedBuf*> g_pin_pool;
+
+void pin_take(PinnedBuf& b) {  // the largest pooled buffer, if any
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    if (g_pin_pool.empty()) return;
+    auto best = std::max_element(g_pin_pool.begin(), g_pin_pool.end(),
+                                 [](const PinnedBuf* x, const PinnedBuf* y) { return x->cap < y->cap; });
+    std::swap(b.p, (*best)->p);
+    std::swap(b.cap, (*best)->cap);
+    delete *best;
+    g_pin_pool.erase(best);
+}
+
+void pin_give(PinnedBuf& b) {  // back to the pool (the smallest pooled one freed when full)
+    if (!b.p) return;
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    if (g_pin_pool.size() >= kPinPool) {
+        auto small = std::min_element(g_pin_pool.begin(), g_pin_pool.end(),
+                                      [](const PinnedBuf* x, const PinnedBuf* y) { return x->cap < y->cap; });
+        if ((*small)->cap >= b.cap) return;  // b is freed by its owner
+        delete *small;
+        g_pin_pool.erase(small);
+    }
+    auto* keep = new PinnedBuf();
+    std::swap(keep->p, b.p);
+    std::swap(keep->cap, b.cap);
+    g_pin_pool.push_back(keep);
+}
 
 struct Bgzf {
     // diagnostics (rogtk_bam_timers), seconds on the caller's thread: t_read file reads,
@@ -737,13 +769,7 @@ struct BamReader {
     ~BamReader() {
         z.stop_ahead();  // the read-ahead thread uses the file and the stream buffer
         if (z.f) fclose(z.f);
-        {
-            std::lock_guard<std::mutex> lk(g_pin_mu);
-            if (z.buf.cap > g_pin_cache.cap) {
-                std::swap(z.buf.p, g_pin_cache.p);
-                std::swap(z.buf.cap, g_pin_cache.cap);
-            }
-        }
+        pin_give(z.buf);
         if (copied) (void)hipEventDestroy(copied);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -1172,11 +1198,7 @@ int rogtk_bam_open_range(const char* path, int n_threads, int64_t c_begin, int64
     std::unique_ptr<BamReader> R(new BamReader());
     R->z.f = fopen(path, "rb");
     ROGTK_REQUIRE(R->z.f, ROGTK_E_INVALID, "Failed to open BAM file '%s'", path);
-    {
-        std::lock_guard<std::mutex> lk(g_pin_mu);
-        std::swap(R->z.buf.p, g_pin_cache.p);
-        std::swap(R->z.buf.cap, g_pin_cache.cap);
-    }
+    pin_take(R->z.buf);
     R->z.threads = n_threads > 0 ? n_threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     ROGTK_HIP_CHECK(hipGetDevice(&R->device));
     ROGTK_HIP_CHECK(hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking));

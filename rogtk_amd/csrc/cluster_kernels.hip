@@ -811,8 +811,15 @@ __device__ __forceinline__ void local_cc_tile(const int64_t base, const uint4* _
 #ifndef ROGTK_LCC_NT8
 #define ROGTK_LCC_NT8 1024  // threads of an 8-position local-CC workgroup (experiments)
 #endif
+// The 8192-code 1024-thread instance's VGPRs capped for 7 waves per SIMD (<= 72; the 8192-code instance
+// compiles to 63 with no spills, against 79 uncapped), so its workgroups fit beside more of the
+// concurrent kernels' waves (round 5, interleaved: 0.3085-0.3106 vs 0.3116-0.3147 ms/step)
+#ifndef ROGTK_LCC_WPE
+#define ROGTK_LCC_WPE 7
+#endif
+#define ROGTK_LCC_ATTR(CAP, NT) __attribute__((amdgpu_waves_per_eu(NT == 1024 && CAP <= 8192 ? ROGTK_LCC_WPE : 1, 8)))
 template <int CAP, int TW, int LP, int NT = TW>
-__global__ __launch_bounds__(NT) void k_local_cc(const uint4* __restrict__ RT, int64_t words, int L,
+__global__ __launch_bounds__(NT) ROGTK_LCC_ATTR(CAP, NT) void k_local_cc(const uint4* __restrict__ RT, int64_t words, int L,
                                                  uint32_t* __restrict__ f, uint32_t* __restrict__ UR,
                                                  uint64_t* __restrict__ lroot, int64_t rwords,
                                                  int64_t max_distinct, unsigned long long* __restrict__ stats,

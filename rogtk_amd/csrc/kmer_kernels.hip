@@ -761,6 +761,10 @@ __global__ __launch_bounds__(kBlock) void k_pack(const uint64_t* __restrict__ t_
 // compacted, bitonic-sorted and censored by binary search, all in LDS. The all-ones
 // key (TTT..T at k = 32) equals the empty marker and gets a dedicated slot.
 constexpr int kLdsBlock = 512;  // 8 waves per group workgroup (16 per CU for class 1; 1024 measured slower)
+#ifndef ROGTK_KMER_RANKSORT
+#define ROGTK_KMER_RANKSORT 1  // 65..512 valid entries by a rank sort (0: bitonic; experiment builds)
+#endif
+constexpr bool kRankSort = ROGTK_KMER_RANKSORT;
 
 // Size classes, tried in the order 3, 1, 4; larger groups take the global radix-sort
 // path. Class 3 (<= 192 rows, <= 576 words, a 2048-slot table for up to 1472 distinct
@@ -848,8 +852,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
     int32_t* const m_w = m_nobs + kLdsRows;
     uint64_t* const vkey = ubuf;                                       // after the inserts
     uint32_t* const vinfo = reinterpret_cast<uint32_t*>(ubuf + kLdsObs);  // count | exts << 16 | pad << 31
-    __shared__ uint32_t scan[kWaves];
-    __shared__ uint32_t s_claimed, s_term, s_iso, s_over, s_hit;
+    __shared__ uint32_t s_claimed, s_term, s_iso, s_over, s_hit, s_nv;
     // s_hit: some k-mer's count reached min_cov during the inserts (counts grow by one per
     // insert, so one insert sees exactly min_cov). Without it nothing is valid and the
     // CountFilter pass, its scan and a barrier are skipped (most groups at the usual floor)
@@ -999,6 +1002,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
         const bool hit = s_hit;
         if (kBounded) {
             const bool over = s_over;
+            if (tid == 0) s_nv = 0;  // every thread read the previous group's count before its first barrier
             __syncthreads();  // every thread has read the flags before they are cleared
             if (over) {
                 // the claimed list is incomplete: clear the whole table; the group goes
@@ -1028,33 +1032,36 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
             }
             continue;
         }
-        // CountFilter + compaction over the claimed slots: wave-shuffle scan, one
-        // barrier for the per-wave totals
-        const uint32_t per = (ncl + TB - 1) / TB;
-        const uint32_t c0 = min(ncl, tid * per), c1 = min(ncl, c0 + per);
-        uint32_t mine = 0;
-        for (uint32_t i = c0; i < c1; ++i) {
-            const uint32_t c = tinfo[cl_at(i)] & 0xFFFFFFu;
-            if ((int64_t)min(c, 0xFFFFu) >= min_cov) ++mine;
-        }
-        uint32_t incl = 0;
-        if (__ballot(mine != 0)) {  // most waves (and most groups, at the usual coverage floors) pass nothing
-            incl = mine;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t v = __shfl_up(incl, off);
-                if (lane >= off) incl += v;
+        // CountFilter + compaction in one pass over the claimed slots (round 5: the sorts
+        // below order the valid entries, so their order here is free): each wave reserves
+        // its valid entries' places with one LDS atomic (round 4 counted them in a pass of
+        // its own, then scanned)
+        for (uint32_t i0 = 0; i0 < ncl; i0 += TB) {  // a uniform trip count (ballots)
+            const uint32_t i = i0 + tid;
+            uint32_t sl = 0, info = 0;
+            bool v = false;
+            if (i < ncl) {
+                sl = cl_at(i);
+                info = tinfo[sl];
+                v = (int64_t)min(info & 0xFFFFFFu, 0xFFFFu) >= min_cov;
+            }
+            const uint64_t m = __ballot(v);
+            if (!m) continue;
+            const int leader = __ffsll((unsigned long long)m) - 1;
+            uint32_t wb = 0;
+            if (lane == leader) wb = atomicAdd(&s_nv, (uint32_t)__popcll(m));
+            wb = __shfl(wb, leader);
+            if (v) {
+                const uint32_t w = wb + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                if (w < (uint32_t)kLdsObs) {
+                    vkey[w] = sl == kLdsSlots ? kEmpty : tkey[sl];
+                    vinfo[w] = min(info & 0xFFFFFFu, 0xFFFFu) | ((info >> 24) << 16);
+                }
             }
         }
-        if (lane == 63) scan[wave] = incl;
         __syncthreads();
         KT(3);
-        uint32_t wbase = 0, nv = 0;
-#pragma unroll
-        for (int w2 = 0; w2 < kWaves; ++w2) {
-            if (w2 < wave) wbase += scan[w2];
-            nv += scan[w2];
-        }
+        const uint32_t nv = s_nv;
         if (nv == 0) {
             // nothing passed CountFilter: reset the touched slots and record the empty
             // group, no compaction, sort or further barrier (the next group's first
@@ -1078,21 +1085,23 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
             }
             continue;
         }
-        uint32_t w = wbase + incl - mine;
-        for (uint32_t i = c0; i < c1; ++i) {
-            const uint32_t sl = cl_at(i);
-            const uint32_t info = tinfo[sl];
-            const uint32_t c = info & 0xFFFFFFu;
-            if ((int64_t)min(c, 0xFFFFu) >= min_cov) {
-                vkey[w] = sl == kLdsSlots ? kEmpty : tkey[sl];
-                vinfo[w] = min(c, 0xFFFFu) | ((info >> 24) << 16);
-                ++w;
-            }
-        }
-        __syncthreads();
         KT(4);
-        // reset the touched slots for the next group (the table is not read again here)
-        reset_claimed();
+        // the censoring below finds a k-mer's neighbours in the hash table itself (a probe
+        // or two, round 5) instead of by binary search over the sorted valid entries (eight
+        // dependent LDS reads per extension); the touched slots are reset after it
+        auto valid_at = [&](uint64_t nb) -> bool {
+            uint32_t sl = kLdsSlots;
+            if (nb != kEmpty) {
+                sl = (uint32_t)((nb * 0x9E3779B97F4A7C15ull) >> (64 - hbits));
+                while (true) {
+                    const unsigned long long k = tkey[sl];
+                    if (k == nb) break;
+                    if (k == kEmpty) return false;
+                    sl = (sl + 1) & (kLdsSlots - 1);
+                }
+            }
+            return (int64_t)min(tinfo[sl] & 0xFFFFFFu, 0xFFFFu) >= min_cov;
+        };
         const int64_t base = cap_off[g];
         if (nv <= 64) {
             // small valid set: wave 0 sorts it in registers (bitonic over shuffles),
@@ -1130,13 +1139,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
                         if (!((e >> bit) & 1u)) continue;
                         const uint64_t bb = (uint64_t)(bit & 3);
                         const uint64_t nb = bit < 4 ? (key >> 2) | (bb << (2 * K - 2)) : ((key << 2) | bb) & kmask;
-                        uint32_t a = 0, c = nv;
-                        while (a < c) {
-                            const uint32_t m = (a + c) >> 1;
-                            if (vkey[m] < nb) a = m + 1;
-                            else c = m;
-                        }
-                        if (a < nv && vkey[a] == nb) ne |= 1u << bit;
+                        if (valid_at(nb)) ne |= 1u << bit;
                     }
                     const int64_t o = base + lane;
                     t_kmer[2 * o] = 0;
@@ -1156,12 +1159,43 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
                 }
             }
             __syncthreads();
+            reset_claimed();  // the next group's first barrier orders these before its inserts
             KT(5);
             continue;
         }
         uint32_t P = 2;
         while (P < nv) P <<= 1;
-        if (P == 128) {
+        if (nv <= (uint32_t)TB && kRankSort) {
+            // 65..TB valid entries (round 5; C3 at k_eff 16, min_coverage 5: ~157 per group):
+            // a rank sort instead of a bitonic network - thread i counts the keys below its
+            // own (distinct: one table slot each), every wave reading the same vkey[j] at once
+            // (an LDS broadcast), then stores its entry at that rank: two barriers instead of
+            // one per bitonic stage (36 at 256 entries)
+            uint64_t myk = 0;
+            uint32_t myi = 0, rank = 0;
+            if ((uint32_t)tid < nv) {
+                myk = vkey[tid];
+                myi = vinfo[tid];
+                uint32_t j = 0;
+                if (K <= 16) {  // 32-bit keys: the low dwords only (half the LDS reads)
+                    const uint32_t* const vk = reinterpret_cast<const uint32_t*>(vkey);
+                    const uint32_t mk = (uint32_t)myk;
+                    for (; j + 4 <= nv; j += 4)
+                        rank += (vk[2 * j] < mk) + (vk[2 * j + 2] < mk) + (vk[2 * j + 4] < mk) + (vk[2 * j + 6] < mk);
+                    for (; j < nv; ++j) rank += vk[2 * j] < mk;
+                } else {
+                    for (; j + 4 <= nv; j += 4)
+                        rank += (vkey[j] < myk) + (vkey[j + 1] < myk) + (vkey[j + 2] < myk) + (vkey[j + 3] < myk);
+                    for (; j < nv; ++j) rank += vkey[j] < myk;
+                }
+            }
+            __syncthreads();  // every key read before the entries move
+            if ((uint32_t)tid < nv) {
+                vkey[rank] = myk;
+                vinfo[rank] = myi;
+            }
+            __syncthreads();
+        } else if (P == 128) {
             // 65..128 valid entries (a family of min_cov or more reads, e.g. C3's uncertified
             // groups: a 150-bp template has 119 k-mers): wave 0 sorts them in registers, two
             // per lane (element lane and 64 + lane: partners j < 64 by shuffles, j = 64 inside
@@ -1239,8 +1273,12 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
             }
         }
         }
-        // remove_censored_exts + output at the group's capacity offset
-        for (uint32_t i = tid; i < nv; i += TB) {
+        // remove_censored_exts + output at the group's capacity offset (terminal / isolated
+        // counts by ballots: one LDS atomic per wave, not per entry)
+        for (uint32_t i0 = 0; i0 < nv; i0 += TB) {
+            const uint32_t i = i0 + tid;
+            bool term = false, iso = false;
+            if (i < nv) {
             const uint64_t key = vkey[i];
             const uint32_t info = vinfo[i];
             const uint32_t e = (info >> 16) & 0xFFu;
@@ -1249,13 +1287,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
                 if (!((e >> bit) & 1u)) continue;
                 const uint64_t bb = (uint64_t)(bit & 3);
                 const uint64_t nb = bit < 4 ? (key >> 2) | (bb << (2 * K - 2)) : ((key << 2) | bb) & kmask;
-                uint32_t a = 0, c = nv;
-                while (a < c) {
-                    const uint32_t m = (a + c) >> 1;
-                    if (vkey[m] < nb) a = m + 1;
-                    else c = m;
-                }
-                if (a < nv && vkey[a] == nb) ne |= 1u << bit;
+                if (valid_at(nb)) ne |= 1u << bit;
             }
             const int64_t o = base + i;
             t_kmer[2 * o] = 0;
@@ -1263,10 +1295,17 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
             t_ext[o] = (uint8_t)ne;
             t_cnt[o] = (uint16_t)(info & 0xFFFFu);
             const bool l0 = (ne & 0xFu) == 0, r0b = (ne >> 4) == 0;
-            if (l0 || r0b) atomicAdd(&s_term, 1u);
-            if (l0 && r0b) atomicAdd(&s_iso, 1u);
+            term = l0 || r0b;
+            iso = l0 && r0b;
+            }
+            const uint64_t tb = __ballot(term), ib = __ballot(iso);
+            if (lane == 0) {
+                if (tb) atomicAdd(&s_term, (uint32_t)__popcll(tb));
+                if (ib) atomicAdd(&s_iso, (uint32_t)__popcll(ib));
+            }
         }
         __syncthreads();
+        reset_claimed();  // the barrier below orders these before the next group's inserts
         if (tid == 0) {
             gcount[g] = nv;
             gstat[5 * g + 3] = s_term;

@@ -50,10 +50,12 @@ def test_bench_launcher_two_ranks():
 def _rank_of_world(n_total, world, rank, L, scores=True):
     """Rank `rank` of `world` emulated on one GPU exactly as it runs under bench.py: its shard
     through UmiPipeline (bench.py's defaults) with the exchange returning the all-gathered
-    bitmaps of every shard (the others built here). Returns (codes_h, slot outputs, stats)."""
+    bitmaps of every shard (the others built here, as bench.emulated_shard_bitmap does).
+    Returns (codes_h, slot outputs, stats, union): union = the sorted distinct codes of all
+    shards, from a presence array torch fills on the device (index_put; none of the
+    library's kernels), each shard's codes generated once."""
     import torch
 
-    import bench
     from oracle import pyoracle as P
     from rogtk_amd import device as D
     from rogtk_amd import dist as RD
@@ -61,16 +63,26 @@ def _rank_of_world(n_total, world, rank, L, scores=True):
     from rogtk_amd.pipeline import UmiPipeline
 
     dev = torch.device("cuda", 0)
-    bitmaps = [bench.emulated_shard_bitmap(n_total, r, world, L, dev) if r != rank else None for r in range(world)]
+    present = torch.zeros(4 ** L, dtype=torch.bool, device=dev)
+    nw = 4 ** L // 64
+    gathered = torch.zeros(world * nw, dtype=torch.int64, device=dev)
+    for r in range(world):
+        if r == rank:
+            continue
+        s0, c0 = RD.shard_range(n_total, r, world)
+        cr = torch.from_numpy(synth.umi_codes(n_total, L, start=s0, count=c0).view(np.int32)).to(dev)
+        present[cr.long()] = True
+        eng = D.ClusterEngine(L, min(n_total, 4 ** L), dev)
+        eng.mark(D.PackedBatch(cr, L))
+        gathered[r * nw:(r + 1) * nw].copy_(eng.build_local_bitmap())
+        del cr, eng
     start, count = RD.shard_range(n_total, rank, world)
     codes_h = synth.umi_codes(n_total, L, start=start, count=count)
     codes = torch.from_numpy(codes_h.view(np.int32)).to(dev)
+    present[codes.long()] = True
+    union = torch.nonzero(present).flatten().to(torch.int64).cpu().numpy().astype(np.uint32)
+    del present
     batch = D.PackedBatch(codes, L)
-    nw = next(b for b in bitmaps if b is not None).numel()
-    gathered = torch.zeros(world * nw, dtype=torch.int64, device=dev)
-    for r in range(world):
-        if r != rank:
-            gathered[r * nw:(r + 1) * nw].copy_(bitmaps[r])
 
     def exchange(bm):  # the all-gather of rank `rank`: its own bitmap in its slot
         gathered[rank * nw:(rank + 1) * nw].copy_(bm)
@@ -86,22 +98,9 @@ def _rank_of_world(n_total, world, rank, L, scores=True):
         out.update({f: slot.scores[f][:count].cpu().numpy() for f in P.FIELDS})
         out["within"] = np.unpackbits(slot.within.cpu().numpy().view(np.uint8), bitorder="little")[:count].astype(bool)
     stats = slot.eng.stats()
-    del pipe, slot, batch, codes, gathered, bitmaps
+    del pipe, slot, batch, codes, gathered
     torch.cuda.empty_cache()
-    return codes_h, out, stats
-
-
-def _union_codes(n_total, world, L):
-    """The sorted distinct codes of all `world` shards, from a host presence array (no sort
-    of the n_total codes)."""
-    from rogtk_amd import dist as RD
-    from rogtk_amd import synth
-
-    present = np.zeros(4 ** L, dtype=bool)
-    for r in range(world):
-        s0, c0 = RD.shard_range(n_total, r, world)
-        present[synth.umi_codes(n_total, L, start=s0, count=c0)] = True
-    return np.flatnonzero(present).astype(np.uint32)
+    return codes_h, out, stats, union
 
 
 def _check_union_ids(codes_h, cid, stats, union, L):
@@ -130,13 +129,19 @@ def test_c4_rank_of_8_against_the_union():
     from rogtk_amd import synth
 
     n_total, world, rank, L = 500_000_000, 8, 3, 12
-    codes_h, got, stats = _rank_of_world(n_total, world, rank, L)
+    codes_h, got, stats, union = _rank_of_world(n_total, world, rank, L)
     assert len(codes_h) == 62_500_000
     print(f"C4 rank {rank} of {world} on GPU done: {stats}", flush=True)
-    # H1 / H2 on the rank's distinct codes
-    uniq, inv = np.unique(codes_h, return_inverse=True)
+    # H1 / H2 on the rank's distinct codes (distinct set and row -> distinct index from a
+    # presence array: no sort of the 62.5M codes)
+    pres = np.zeros(4 ** L, dtype=bool)
+    pres[codes_h] = True
+    uniq = np.flatnonzero(pres).astype(np.uint32)
+    inv = (np.cumsum(pres, dtype=np.int64) - 1)[codes_h]
+    del pres
+    threads = min(16, os.cpu_count() or 1)
     ucol = P.StrCol.from_fixed(synth.codes_to_ascii(uniq, L))
-    ref = P.umi_complexity(ucol)
+    ref = P.umi_complexity(ucol, threads=threads)
     for f in P.FIELDS:
         r = ref[f]
         g = got[f]
@@ -147,7 +152,6 @@ def test_c4_rank_of_8_against_the_union():
     _, rw, _ = P.hamming(ucol, b"ACGTACGTACGT", 1)
     assert np.array_equal(got["within"], rw[inv])
     del ucol, ref, uniq, inv
-    union = _union_codes(n_total, world, L)
     assert len(union) > 0.9 * 4 ** L
     _check_union_ids(codes_h, got["cid"], stats, union, L)
 
@@ -163,10 +167,9 @@ def test_c2_weak_scaling_rank_of_8_union(L, min_clusters):
     13-bp UMIs (12.6% dense, 36,893 clusters, the largest 8.41M codes) pin the merge where
     the answer is not degenerate."""
     n_total, world, rank = 80_000_000, 8, 5
-    codes_h, got, stats = _rank_of_world(n_total, world, rank, L, scores=False)
+    codes_h, got, stats, union = _rank_of_world(n_total, world, rank, L, scores=False)
     assert len(codes_h) == 10_000_000
     print(f"C2 x8 rank {rank}, {L} bp: {stats}", flush=True)
-    union = _union_codes(n_total, world, L)
     rk = _check_union_ids(codes_h, got["cid"], stats, union, L)
     assert rk >= min_clusters
     if L == 13:

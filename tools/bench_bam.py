@@ -105,10 +105,16 @@ def main():
     # the same file cut into 4 ranges at BGZF block starts (what 4 ranks would each decode),
     # here all on one GPU, decoded concurrently (one host thread, reader and stream per
     # range): rows and ids identical to the whole-file run
-    t = time.perf_counter()
-    tab4 = B.bams_umi_cluster([args.path], umi_len=umi_len, max_distance=1, source="sequence", mode=args.mode,
-                              n_threads=args.threads, ranges_per_file=4)
-    c5r_s = time.perf_counter() - t
+    # twice: the first call also allocates the range readers' pinned stream buffers (a pool
+    # the library keeps, as the whole-file reader's above was by the decode run); the second
+    # is the steady state a rank decoding file after file sees
+    c5r_cold = None
+    for _ in range(2):
+        t = time.perf_counter()
+        tab4 = B.bams_umi_cluster([args.path], umi_len=umi_len, max_distance=1, source="sequence", mode=args.mode,
+                                  n_threads=args.threads, ranges_per_file=4)
+        c5r_s = time.perf_counter() - t
+        c5r_cold = c5r_s if c5r_cold is None else c5r_cold
     assert tab4.num_rows == n
     assert tab4.column("cluster_id").equals(tab.column("cluster_id"))
 
@@ -142,6 +148,7 @@ def main():
                            "path": "bam_umi_cluster: one reader, batches decoded and UMIs appended on the device "
                                    "with no host sync inside the file, then H3"},
         "c5_4_ranges": {"records_per_s": n / c5r_s, "wall_s": round(c5r_s, 3),
+                        "first_call": {"records_per_s": n / c5r_cold, "wall_s": round(c5r_cold, 3)},
                         "path": "bams_umi_cluster(ranges_per_file=4) on one GPU: the file cut at BGZF block "
                                 "starts, each range's first record found and checked against the previous "
                                 "range's tail, the ranges decoded concurrently (a host thread, reader and stream "
