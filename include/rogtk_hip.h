@@ -359,6 +359,20 @@ int rogtk_kmer_spectrum_dev(const int64_t* offsets, const uint8_t* values, const
 int rogtk_read_block_words(int64_t max_len);
 int rogtk_pack_reads(const int64_t* offsets, const uint8_t* values, const uint8_t* validity, int64_t validity_offset,
                      int64_t n, int block_words, uint64_t* blocks, int64_t* max_len, void* stream);
+/* Round 5: the longest row of a column (max of offsets[i + 1] - offsets[i], i < n) into
+ * *max_len on the host (a reduction kernel on `stream` and one 8-byte read; synchronises). */
+int rogtk_max_row_len(const int64_t* offsets, int64_t n, int64_t* max_len, void* stream);
+/* Round 5: rogtk_kmer_spectrum_dev with the grouped rows packed straight from their ASCII
+ * bytes (k_pack_gather: the 2-bit packing and the repeat certificate of rogtk_pack_reads
+ * fused with the grouped staging of rogtk_kmer_spectrum_blocks; same outputs, bit-exact),
+ * for columns whose rows are at most 224 bases (max_len, or < 0 to compute it over the
+ * first n_column rows; ROGTK_E_UNSUPPORTED past 224). values_len: readable bytes of values. */
+int rogtk_kmer_spectrum_fused(const int64_t* offsets, const uint8_t* values, int64_t values_len,
+                              const uint8_t* validity, int64_t validity_offset, const int64_t* rows, int64_t n_rows,
+                              const int64_t* group_offsets, int64_t n_groups, int k, int64_t min_coverage,
+                              int64_t capacity, uint64_t* kmers, uint8_t* exts, uint16_t* counts,
+                              int64_t* entry_offsets, int64_t* group_stats, int64_t* n_entries, int64_t max_len,
+                              int64_t n_column, void* stream);
 /* rogtk_kmer_spectrum_dev over a column packed by rogtk_pack_reads (same outputs,
  * bit-exact): each grouped row is staged from its block (whole 64-B lines) instead of
  * its ASCII bytes. offsets / values stay needed (capacities, the radix path). */

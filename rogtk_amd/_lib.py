@@ -170,6 +170,9 @@ SIGNATURES = {
     "rogtk_event_query": [_vp, _P_I32],
     "rogtk_event_synchronize": [_vp],
     "rogtk_pack_reads": [_vp, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp],
+    "rogtk_max_row_len": [_vp, _i64, _P_I64, _vp],
+    "rogtk_kmer_spectrum_fused": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _i64, _vp, _vp, _vp,
+                                  _vp, _vp, _P_I64, _i64, _i64, _vp],
     "rogtk_kmer_spectrum_blocks": [_vp, _i32, _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _i64, _vp,
                                    _vp, _vp, _vp, _vp, _P_I64, _vp],
     "rogtk_kmer_spectrum_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i32, _i32, _i64, _i64, _vp,

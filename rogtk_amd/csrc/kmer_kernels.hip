@@ -537,6 +537,156 @@ __global__ __launch_bounds__(kBlock) void k_row_gather(const uint64_t* __restric
     }
 }
 
+// Round 5: grouped rows packed straight from their ASCII bytes (no block column): the
+// per-row packing and repeat certificate of k_pack_reads fused with k_row_gather's staging,
+// for calls whose rows fit NW words (NW = 5: <= 160 bases, 7: <= 224; the caller knows a
+// bound). A wave per 64 consecutive grouped rows, one workgroup per wave: each row's bytes
+// come by ONE coalesced load instruction of the wave (lane l takes the row's dword l; 16
+// rows' loads in flight before their LDS stores), staged in LDS at a fixed slot per row;
+// then each lane packs and certifies its own row from its slot, as k_pack_reads does from
+// its trip's bytes (a lane loading its own row's bytes took 19 ms for 100M rows, every
+// load instruction touching 64 rows' lines). Outputs as k_row_gather: the row's S words at
+// packed[r * S], its length / observation count, and per group the ok rows and the
+// uncertified rows with observations (gstat[5 g + 1], [5 g + 2]). Saves the block column's
+// 64-B write and re-read per row and one kernel per call (k_pack_reads + k_row_gather).
+template <int NW>
+__global__ __launch_bounds__(64, 3) void k_pack_gather(const int64_t* __restrict__ offsets,
+                                                      const uint8_t* __restrict__ values,
+                                                      const uint8_t* __restrict__ validity, int64_t voff,
+                                                      int64_t vlen,
+                                                      const int64_t* __restrict__ rows, int64_t n_rows, int K, int S,
+                                                      const uint8_t* __restrict__ gk,
+                                                      const uint32_t* __restrict__ row_group,
+                                                      uint64_t* __restrict__ packed, int64_t* __restrict__ row_obs,
+                                                      int32_t* __restrict__ row_len,
+                                                      unsigned long long* __restrict__ gstat,
+                                                      unsigned long long* __restrict__ long_rows) {
+    constexpr int kSlot = 8 * NW + 1;  // dwords per row slot: 32 NW bytes + 3 of alignment + the 9-dword reads
+    __shared__ uint32_t stg[64 * kSlot];
+    const int lane = threadIdx.x;
+    const bool cert = K >= 31 && K <= 32;  // k_group_classify reads the certificate only there
+    for (int64_t rb = (int64_t)blockIdx.x * 64; rb < n_rows; rb += (int64_t)gridDim.x * 64) {
+        const int64_t r = rb + lane;
+        const bool live = r < n_rows;
+        const int64_t pr = live ? (rows ? rows[r] : r) : 0;
+        const uint32_t my_g = live ? row_group[r] : 0u;
+        bool valid = live;
+        if (live && validity) {
+            const int64_t bit = voff + pr;
+            valid = (validity[bit >> 3] >> (bit & 7)) & 1;
+        }
+        const bool inK = valid && gk[my_g] == K;
+        int64_t st = 0;
+        int len = 0;
+        if (live) {
+            st = offsets[pr];
+            len = (int)min<int64_t>(offsets[pr + 1] - st, 1 << 30);
+        }
+        const int clen = min(len, 32 * NW);
+        const int64_t a4 = st & ~3ll;
+        const int rel = (int)(st & 3);
+        const int ndw = inK ? (rel + clen + 3) >> 2 : 0;  // dwords of the row's slot to load
+        // the rows' bytes into their slots: row i by one load instruction of the wave
+        for (int i0 = 0; i0 < 64; i0 += 16) {
+            uint32_t v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int i = i0 + u;
+                const int ni = __builtin_amdgcn_readlane(ndw, i);
+                const int64_t ai = ((int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(a4 >> 32), i) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((int)a4, i);
+                v[u] = 0;
+                if (lane < ni) {
+                    const int64_t at = ai + 4 * lane;
+                    if (at + 4 <= vlen) {
+                        v[u] = *reinterpret_cast<const uint32_t*>(values + at);
+                    } else {  // the buffer's last bytes: none read past values_len
+                        for (int b = 0; b < 4; ++b)
+                            if (at + b < vlen) v[u] |= (uint32_t)values[at + b] << (8 * b);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (lane < kSlot) stg[(i0 + u) * kSlot + lane] = v[u];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        int my_len = inK ? clen : 0;  // the certificate's loop bound (wave-uniform)
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) my_len = max(my_len, __shfl_xor(my_len, m, 64));
+        const int lmax = __builtin_amdgcn_readfirstlane(my_len);
+        const int used = inK ? (clen + 31) >> 5 : 0;
+        const uint32_t sh = (uint32_t)rel * 8;
+        const uint32_t* const slot = stg + lane * kSlot;
+        uint64_t wd[NW];
+        uint32_t bad = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            uint64_t acc = 0;
+            if (w < used) {
+                uint32_t t9[9];
+#pragma unroll
+                for (int i = 0; i < 9; ++i) t9[i] = slot[8 * w + i];  // past the row: masked below
+                uint32_t by[8];
+#pragma unroll
+                for (int d = 0; d < 8; ++d) {
+                    const int j = w * 32 + d * 4;  // first byte of these 4
+                    const int left = len - j;
+                    uint32_t x = __builtin_amdgcn_alignbit(t9[d + 1], t9[d], sh);
+                    const uint32_t inmask = left >= 4 ? 0xFFFFFFFFu : left <= 0 ? 0u : (1u << (8 * left)) - 1u;
+                    x = (x & inmask) | (0x41414141u & ~inmask);  // past the end: 'A' (code 0, valid)
+                    uint32_t nb;
+                    by[d] = pack4(x, nb);
+                    bad |= nb;
+                }
+                const uint32_t hi = (((by[0] << 8) | by[1]) << 16) | ((by[2] << 8) | by[3]);
+                const uint32_t lo = (((by[4] << 8) | by[5]) << 16) | ((by[6] << 8) | by[7]);
+                acc = ((uint64_t)hi << 32) | lo;
+            }
+            wd[w] = acc;
+        }
+        const bool ok = inK && bad == 0 && len <= 32 * NW;
+        const bool use = ok && len >= K;
+        const bool norep = cert && use && !may_repeat16(wd, len, lmax);
+        if (live) {
+#pragma unroll
+            for (int w = 0; w < NW; ++w)
+                if (w < S) packed[r * S + w] = wd[w];
+            // a row longer than S words would read the next row's bases: counted, the call fails
+            if (inK && len > 32 * S) atomicAdd(long_rows, 1ull);
+            row_obs[r] = use ? (int64_t)len - K + 1 : 0;
+            row_len[r] = use ? (int32_t)len : 0;
+        }
+        const uint64_t okbits = __ballot(ok), unc = __ballot(use && !norep);
+        if (live) {  // n_sequences: the first lane of each run of same-group rows adds the run's ok rows
+            const uint32_t g_prev = __shfl_up(my_g, 1);
+            const uint64_t heads = __ballot(lane == 0 || my_g != g_prev);
+            if ((heads >> lane) & 1ull) {
+                const uint64_t above = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
+                const uint64_t run = (above ? (above & (0ull - above)) - 1ull : ~0ull) & (~0ull << lane);
+                const int cnt = __popcll(okbits & run);
+                if (cnt) atomicAdd(gstat + 5 * (int64_t)my_g + 1, (unsigned long long)cnt);
+                const int ucnt = __popcll(unc & run);
+                if (ucnt) atomicAdd(gstat + 5 * (int64_t)my_g + 2, (unsigned long long)ucnt);
+            }
+        }
+        __builtin_amdgcn_s_barrier();  // the slots are rewritten by the next trip
+    }
+}
+
+// the longest row of a column (rogtk_kmer_spectrum_fused without a bound): one atomic per wave
+__global__ __launch_bounds__(kBlock) void k_max_row_len(const int64_t* __restrict__ offsets, int64_t n,
+                                                        unsigned long long* __restrict__ out) {
+    int64_t m = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+        m = max(m, offsets[i + 1] - offsets[i]);
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) m = max(m, (int64_t)__shfl_xor(m, s, 64));
+    if ((threadIdx.x & 63) == 0 && m > 0) atomicMax(out, (unsigned long long)m);
+}
+
 // row -> group map: one wave per group writes its rows' group id (coalesced)
 // 16 lanes per group (no shuffles: segments run independently)
 __global__ __launch_bounds__(kBlock) void k_row_groups(const int64_t* __restrict__ go, int64_t G,
@@ -1982,6 +2132,8 @@ struct KIn {
     int S = 0;                         // 2-bit words per row to stage: ceil(max_len / 32) <= B - 1
     int64_t* cap_fill = nullptr;       // != NULL: per-group capacities computed here (into this
                                        // scratch, then cap_off) from the staged rows' observations
+    bool fused = false;                // stage from the ASCII bytes by k_pack_gather (S words per row)
+    int64_t vlen = 0;                  // fused: readable bytes of values
 };
 
 template <int OW, bool WIDE>
@@ -2000,8 +2152,21 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
     const int wgrid = grid_for((n_rows + kWavesPerBlock - 1) / kWavesPerBlock * kBlock, 16384);
     hipLaunchKernelGGL(k_row_groups, dim3(grid_for(G * 16, 16384)), dim3(kBlock), 0, s, go, G,
                        c->row_group.as<uint32_t>());
-    const int stride = in.blocks ? in.S : 0;  // staged words per row (0: compact, woff)
-    if (in.blocks) {
+    const int stride = (in.blocks || in.fused) ? in.S : 0;  // staged words per row (0: compact, woff)
+    if (in.fused) {
+        // round 5: packed from the ASCII bytes in group order (k_pack_gather), no block column
+        if (int rc = c->packed.ensure((size_t)std::max<int64_t>(n_rows * stride, 1) * 8)) return rc;
+        ProfScope prof(K_ROW_GATHER, s, true);
+        const int pgrid = (int)std::min<int64_t>((n_rows + 63) / 64, (int64_t)8192 * 256 / 64);
+#define ROGTK_PG(NW)                                                                                              \
+    hipExtLaunchKernelGGL(k_pack_gather<NW>, dim3(pgrid), dim3(64), 0, s, prof.start(), prof.stop(), 0, in.offsets,  \
+                          in.values, in.validity, in.voff, in.vlen, in.rows, n_rows, K, stride, in.gk,                \
+                          c->row_group.as<uint32_t>(), c->packed.as<uint64_t>(), c->row_obs.as<int64_t>(),            \
+                          c->row_len.as<int32_t>(), gstat, c->long_rows.as<unsigned long long>())
+        if (stride <= 5) ROGTK_PG(5);
+        else ROGTK_PG(7);
+#undef ROGTK_PG
+    } else if (in.blocks) {
         // stage from the packed column: each grouped row's block as whole lines, its bases
         // at a fixed stride (row r at packed[r * S]: no offsets, no scan)
         if (int rc = c->packed.ensure((size_t)std::max<int64_t>(n_rows * stride, 1) * 8)) return rc;
@@ -2481,7 +2646,7 @@ int spectrum_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* v
                  const int64_t* rows, int64_t n_rows, const int64_t* group_offsets, int64_t n_groups, int k,
                  int64_t min_coverage, int64_t capacity, uint64_t* kmers, uint8_t* exts, uint16_t* counts,
                  int64_t* entry_offsets, int64_t* group_stats, int64_t* n_entries, void* stream,
-                 const uint64_t* blocks, int B, int S) {
+                 const uint64_t* blocks, int B, int S, bool fused = false, int64_t vlen = 0) {
     ROGTK_REQUIRE(offsets && values && group_offsets && entry_offsets && group_stats && n_entries, ROGTK_E_INVALID,
                   "kmer_dev: NULL argument");
     ROGTK_REQUIRE(n_rows >= 0 && n_groups >= 1 && min_coverage >= 0, ROGTK_E_INVALID,
@@ -2504,7 +2669,7 @@ int spectrum_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* v
     ROGTK_HIP_CHECK(hipMemsetAsync(c->long_rows.p, 0, 8, s));
     unsigned long long long_rows = 0;
     int64_t tcap = 0;
-    if (blocks) {
+    if (blocks || fused) {
         // block path: a row holds at most 32 S bases, so at most 32 S - K + 1 observations;
         // the per-group capacities follow from the staged rows (run_class, cap_fill)
         tcap = valid_cap(n_rows * std::max<int64_t>(0, 32 * (int64_t)S - (K ? K : 64) + 1), min_coverage);
@@ -2528,7 +2693,9 @@ int spectrum_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* v
         in.blocks = blocks;
         in.B = B;
         in.S = S;
-        if (blocks) in.cap_fill = c->caps.as<int64_t>();
+        in.fused = fused;
+        in.vlen = vlen;
+        if (blocks || fused) in.cap_fill = c->caps.as<int64_t>();
         if (int rc = run_any<8>(c, in, n_rows, G, K, min_coverage, s, nullptr)) return rc;
     }
     if (int rc = cub_exsum_i64(c, c->gcount.as<int64_t>(), entry_offsets, G, s)) return rc;
@@ -2596,6 +2763,44 @@ int rogtk_pack_reads(const int64_t* offsets, const uint8_t* values, const uint8_
 #undef ROGTK_PACK_LAUNCH
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
+}
+
+int rogtk_max_row_len(const int64_t* offsets, int64_t n, int64_t* max_len, void* stream) {
+    ROGTK_REQUIRE(max_len && n >= 0 && (n == 0 || offsets), ROGTK_E_INVALID, "max_row_len: NULL argument");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    KmerCtx* c = nullptr;
+    if (int rc = kmer_ctx(&c)) return rc;
+    if (int rc = c->scal.ensure(64)) return rc;
+    ROGTK_HIP_CHECK(hipMemsetAsync(c->scal.p, 0, 8, s));
+    if (n > 0)
+        hipLaunchKernelGGL(k_max_row_len, dim3((unsigned)std::min<int64_t>((n + kBlock - 1) / kBlock, 4096)),
+                           dim3(kBlock), 0, s, offsets, n, c->scal.as<unsigned long long>());
+    unsigned long long m = 0;
+    ROGTK_HIP_CHECK(hipMemcpyAsync(&m, c->scal.p, 8, hipMemcpyDeviceToHost, s));
+    ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    *max_len = (int64_t)m;
+    return ROGTK_OK;
+}
+
+int rogtk_kmer_spectrum_fused(const int64_t* offsets, const uint8_t* values, int64_t values_len,
+                              const uint8_t* validity, int64_t validity_offset, const int64_t* rows, int64_t n_rows,
+                              const int64_t* group_offsets, int64_t n_groups, int k, int64_t min_coverage,
+                              int64_t capacity, uint64_t* kmers, uint8_t* exts, uint16_t* counts,
+                              int64_t* entry_offsets, int64_t* group_stats, int64_t* n_entries, int64_t max_len,
+                              int64_t n_column, void* stream) {
+    ROGTK_REQUIRE(offsets && values && values_len >= 0, ROGTK_E_INVALID, "kmer_fused: NULL argument");
+    ROGTK_REQUIRE(((uintptr_t)values & 15u) == 0, ROGTK_E_UNSUPPORTED,
+                  "kmer_fused: values must be 16-byte aligned (16-B loads; use the block column)");
+    if (max_len < 0) {  // the column's longest row: one pass over its offsets and one 8-byte read
+        ROGTK_REQUIRE(n_column >= 0, ROGTK_E_INVALID, "kmer_fused: max_len < 0 needs n_column");
+        if (int rc = rogtk_max_row_len(offsets, n_column, &max_len, stream)) return rc;
+    }
+    ROGTK_REQUIRE(max_len <= 224, ROGTK_E_UNSUPPORTED,
+                  "kmer_fused: rows up to %lld bases; the fused staging takes <= 224 (use the block column)",
+                  (long long)max_len);
+    return spectrum_dev(offsets, values, validity, validity_offset, rows, n_rows, group_offsets, n_groups, k,
+                        min_coverage, capacity, kmers, exts, counts, entry_offsets, group_stats, n_entries, stream,
+                        nullptr, 8, (int)std::max<int64_t>(1, (max_len + 31) / 32), true, values_len);
 }
 
 int rogtk_kmer_spectrum_blocks(const uint64_t* blocks, int block_words, int64_t max_len, const int64_t* offsets,

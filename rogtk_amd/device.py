@@ -327,6 +327,36 @@ def kmer_spectrum_dev(offsets: torch.Tensor, values: torch.Tensor, group_offsets
     return {"kmers": km[:n], "exts": ex[:n], "counts": cn[:n], "entry_offsets": eo, "stats": st}
 
 
+def max_row_len(offsets: torch.Tensor, stream=None) -> int:
+    """The longest row of an int64-offsets column (rogtk_max_row_len: a reduction kernel and
+    one 8-byte read)."""
+    m = ctypes.c_int64(0)
+    _lib.call("rogtk_max_row_len", _p(offsets), max(offsets.numel() - 1, 0), ctypes.byref(m), _s(stream))
+    return int(m.value)
+
+
+def kmer_spectrum_fused(offsets: torch.Tensor, values: torch.Tensor, group_offsets: torch.Tensor, k: int,
+                        min_coverage: int, capacity: int, max_len: int, rows: Optional[torch.Tensor] = None,
+                        validity: Optional[torch.Tensor] = None, validity_offset: int = 0, stream=None):
+    """kmer_spectrum_dev with the grouped rows packed straight from their ASCII bytes
+    (rogtk_kmer_spectrum_fused; rows of at most 224 bases): same outputs, bit-exact."""
+    dev = values.device
+    G = group_offsets.numel() - 1
+    n_rows = rows.numel() if rows is not None else offsets.numel() - 1
+    cap = max(int(capacity), 1)
+    km = torch.empty((cap, 2), dtype=torch.int64, device=dev)
+    ex = torch.empty(cap, dtype=torch.uint8, device=dev)
+    cn = torch.empty(cap, dtype=torch.int16, device=dev)
+    eo = torch.empty(G + 1, dtype=torch.int64, device=dev)
+    st = torch.empty((G, 5), dtype=torch.int64, device=dev)
+    m = ctypes.c_int64(0)
+    _lib.call("rogtk_kmer_spectrum_fused", _p(offsets), _p(values), values.numel(), _p(validity),
+              int(validity_offset), _p(rows), n_rows, _p(group_offsets), G, int(k), int(min_coverage), cap, _p(km),
+              _p(ex), _p(cn), _p(eo), _p(st), ctypes.byref(m), int(max_len), offsets.numel() - 1, _s(stream))
+    n = int(m.value)
+    return {"kmers": km[:n], "exts": ex[:n], "counts": cn[:n], "entry_offsets": eo, "stats": st}
+
+
 class PackedReads:
     """A read column as fixed-size 2-bit blocks in HBM (rogtk_pack_reads): block_words u64
     per row (meta + bases), so a grouped row is staged as whole 64-B lines."""
@@ -400,20 +430,31 @@ def group_spectra(offsets: torch.Tensor, values: torch.Tensor, keys: torch.Tenso
     dict for groups g0..g1-1) copied to its own size so the next call can reuse the
     capacity; else consume(g0, g1, result) is called per call (the result's buffers are
     reused afterwards) and calls is empty.
-    packed: "auto" packs the column once into 2-bit blocks (PackedReads) when its reads
-    fit the block layout, and every call stages from the blocks; a PackedReads to reuse;
-    None for the ASCII staging path."""
+    packed: "auto" stages every call's grouped rows straight from their ASCII bytes with
+    the 2-bit packing and repeat certificate fused in (kmer_spectrum_fused, round 5) when the
+    rows fit 224 bases, else packs the column once into 2-bit blocks (PackedReads) that every
+    call stages from; "fused" / "blocks" force one of the two; a PackedReads to reuse; None
+    for the ASCII staging path (no certificate)."""
+    if isinstance(packed, PackedReads):
+        max_len = packed.max_len
+    else:  # the longest row by a reduction kernel (no torch kernel, one 8-byte read)
+        max_len = max_row_len(offsets, stream=stream)
     if isinstance(packed, str):
-        try:
-            packed = PackedReads(offsets, values, stream=stream)
-        except ValueError:
-            packed = None
+        mode = ("fused" if max_len <= 224 and values.data_ptr() % 16 == 0 else "blocks") if packed == "auto" \
+            else packed
+        if mode not in ("fused", "blocks"):
+            raise ValueError("packed must be 'auto', 'fused', 'blocks', a PackedReads or None")
+        packed = "fused"
+        if mode == "blocks":
+            try:
+                packed = PackedReads(offsets, values, max_len=max_len, stream=stream)
+            except ValueError:
+                packed = None
     rows, go, G = group_by_key(keys, stream=stream)
     if G == 0:
         return rows, go, G, []
     # output capacity per call: rows x (longest row - 3) bounds the valid entries (each
     # row adds at most len - 3 k-mers, k_eff >= 4)
-    max_len = packed.max_len if packed is not None else int((offsets[1:] - offsets[:-1]).max().item())
     per_row = max(0, max_len - 3)
     n_grouped = rows.numel()
     if n_grouped <= batch_rows:  # one call: no copy of the group offsets to the host
@@ -431,7 +472,10 @@ def group_spectra(offsets: torch.Tensor, values: torch.Tensor, keys: torch.Tenso
         a, b = bounds[g0], bounds[g1]
         r = rows[a:b]
         cap = (b - a) * per_row // max(int(min_coverage), 1)
-        if packed is not None:
+        if packed == "fused":
+            res = kmer_spectrum_fused(offsets, values, go[g0:g1 + 1] - a, k, min_coverage, cap, max_len, rows=r,
+                                      stream=stream)
+        elif packed is not None:
             res = kmer_spectrum_blocks(packed, offsets, values, go[g0:g1 + 1] - a, k, min_coverage, cap, rows=r,
                                        stream=stream)
         else:

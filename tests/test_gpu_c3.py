@@ -92,13 +92,17 @@ def _concat(calls, G):
 
 @pytest.mark.parametrize("k,min_cov,batch_rows,packed,filt", [
     (K, MINCOV, 10_000_000, "auto", 0), (K, 2, 200_000, "auto", 0), (K, MINCOV, 10_000_000, None, 0),
-    (K, MINCOV, 10_000_000, "auto", 1), (K, 3, 200_000, "auto", 1),
+    (K, MINCOV, 10_000_000, "auto", 1), (K, 3, 200_000, "auto", 1), (K, MINCOV, 10_000_000, "blocks", 1),
+    (K, 2, 200_000, "blocks", 0),
     # the reference's defaults: k = 15 (docstring) and 10 (assemble_sequences), effective 16,
     # min_coverage 5 (rogtk/__init__.py:106-107, 211-212)
-    (15, 5, 10_000_000, "auto", 1), (10, 5, 200_000, "auto", 1), (15, 5, 10_000_000, None, 1)])
+    (15, 5, 10_000_000, "auto", 1), (10, 5, 200_000, "auto", 1), (15, 5, 10_000_000, None, 1),
+    (15, 5, 10_000_000, "blocks", 1)])
 def test_c3_path_1m_vs_oracle(k, min_cov, batch_rows, packed, filt):
-    """packed "auto": rows staged from the 2-bit block column (rogtk_pack_reads); None: from
-    the ASCII bytes. filt: with the minimizer filter (rogtk_kmer_set_filter)."""
+    """packed "auto" (150-bp rows: "fused"): rows packed from their ASCII bytes in group
+    order with the certificate (rogtk_kmer_spectrum_fused); "blocks": staged from the 2-bit
+    block column (rogtk_pack_reads); None: from the ASCII bytes without a certificate.
+    filt: with the minimizer filter (rogtk_kmer_set_filter)."""
     from oracle import pyoracle as P
     from rogtk_amd import _lib
     from rogtk_amd import synth
@@ -264,8 +268,10 @@ def test_c3_full_size_100m_properties():
             dec = torch.zeros(n + 1, dtype=torch.uint8, device="cuda")
             _lib.call("rogtk_kmer_debug_filter", D._p(dec), n + 1)
         try:
+            # run 0: the default (fused staging), one call; run 1: the block column, 10M-row calls
             rows, go, G, calls = D.group_spectra(offsets, values, cid, K, MINCOV,
-                                                 batch_rows=100_000_000 if run == 0 else 10_000_000)
+                                                 batch_rows=100_000_000 if run == 0 else 10_000_000,
+                                                 packed="auto" if run == 0 else "blocks")
             torch.cuda.synchronize()
         finally:
             _lib.call("rogtk_kmer_debug_filter", None, 0)
@@ -348,12 +354,21 @@ def test_packed_blocks_match_oracle(lo, hi, bw):
     assert pk.block_words == bw and pk.max_len == int(lens.max())
     gsel = torch.tensor(go, dtype=torch.int64).cuda()
     col = P.StrCol.from_list(items)
+    fused = hi <= 224  # the fused staging (rogtk_kmer_spectrum_fused) takes rows up to 224 bases
+    if not fused:
+        with pytest.raises(_lib.RogtkError, match="224"):
+            D.kmer_spectrum_fused(off, vals, gsel, 17, 1, 1, -1, validity=vbits)
     for k, mc in ((13, 2), (17, 1), (33, 2)):
         ref = P.kmer_spectrum(col, k, mc, False, np.array(go), threads=THREADS)
-        for path in (1, 0):
+        for path, fz in ((1, False), (0, False), (1, True), (0, True)):
+            if fz and not fused:
+                continue
             _lib.call("rogtk_kmer_set_path", path)
             cap = int(np.clip(lens - 3, 0, None).sum())
-            got = D.kmer_spectrum_blocks(pk, off, vals, gsel, k, mc, cap, validity=vbits)
+            if fz:
+                got = D.kmer_spectrum_fused(off, vals, gsel, k, mc, cap, -1, validity=vbits)
+            else:
+                got = D.kmer_spectrum_blocks(pk, off, vals, gsel, k, mc, cap, validity=vbits)
             torch.cuda.synchronize()
             km = got["kmers"].cpu().numpy().view(np.uint64)
             assert np.array_equal(got["entry_offsets"].cpu().numpy(), ref["group_offsets"]), (k, path)
@@ -482,9 +497,12 @@ def test_repeat_certificate_spectra(mc):
     gsel = torch.tensor(go, dtype=torch.int64).cuda()
     col = P.StrCol.from_list(items)
     _lib.call("rogtk_kmer_set_path", 1)
-    for k in (17, 31):
+    for k, fz in ((17, False), (31, False), (17, True), (31, True)):
         ref = P.kmer_spectrum(col, k, mc, False, np.array(go), threads=THREADS)
-        got = D.kmer_spectrum_blocks(pk, off, vals, gsel, k, mc, int(np.clip(lens - 3, 0, None).sum()))
+        cap = int(np.clip(lens - 3, 0, None).sum())
+        # the block path, and the fused staging (certificate computed in k_pack_gather)
+        got = (D.kmer_spectrum_fused(off, vals, gsel, k, mc, cap, -1) if fz else
+               D.kmer_spectrum_blocks(pk, off, vals, gsel, k, mc, cap))
         torch.cuda.synchronize()
         km = got["kmers"].cpu().numpy().view(np.uint64)
         assert np.array_equal(got["entry_offsets"].cpu().numpy(), ref["group_offsets"]), k
@@ -557,11 +575,15 @@ def test_minimizer_filter_spectra(mc):
     gsel = torch.tensor(go, dtype=torch.int64).cuda()
     col = P.StrCol.from_list(items)
     _lib.call("rogtk_kmer_set_path", 1)
-    for k, filt in ((17, 1), (31, 1), (17, 0)):
+    for k, filt, fz in ((17, 1, False), (31, 1, False), (17, 0, False), (17, 1, True), (31, 1, True)):
         ref = P.kmer_spectrum(col, k, mc, False, np.array(go), threads=THREADS)
         _lib.call("rogtk_kmer_set_filter", filt)
         try:
-            got = D.kmer_spectrum_blocks(pk, off, vals, gsel, k, mc, int(np.clip(lens - 3, 0, None).sum()))
+            cap = int(np.clip(lens - 3, 0, None).sum())
+            if fz:  # the fused staging: the certificate computed in k_pack_gather
+                got = D.kmer_spectrum_fused(off, vals, gsel, k, mc, cap, -1)
+            else:
+                got = D.kmer_spectrum_blocks(pk, off, vals, gsel, k, mc, cap)
             torch.cuda.synchronize()
         finally:
             _lib.call("rogtk_kmer_set_filter", 1)
