@@ -1335,7 +1335,10 @@ __device__ __forceinline__ uint32_t word_label_of(const uint32_t* __restrict__ w
     return decode_word_label(wlab[c >> 6], wexc, c);
 }
 
-// MODE 0: labelcode[code]; MODE 1: flab[rank(code)] (labels by index, ilab).
+// MODE 0: labelcode[code]; MODE 1: flab[rank(code)] (labels by index, ilab); MODE 2 (exact
+// ids, max_distance 0, round 5): the rank itself, from the 16-B-per-64-codes rank table (4 MB
+// at L = 12, cache-resident) instead of a gather from the 4^L-entry label table (C3's H3:
+// 100M rows 1.8 ms).
 // wlab / wexc (max_distance 1 only, else NULL): per 64 codes the label of the word's most
 // frequent component (1 MB at L = 12, L2-resident) and, for flagged words only, the mask
 // of its other codes (2 MB): only exception codes gather from the 4^L-entry table.
@@ -1379,7 +1382,8 @@ __global__ __launch_bounds__(kBlock) void k_assign(const uint32_t* __restrict__ 
                     const uint32_t wl = wlab ? word_label_of(wlab, wexc, c[g][k]) : kNone;
                     id[g][k] = wl != kNone ? wl
                                : MODE == 0 ? labelcode[c[g][k]]
-                                           : flab[rt_rank(RT[c[g][k] >> 6], c[g][k])];
+                               : MODE == 1 ? flab[rt_rank(RT[c[g][k] >> 6], c[g][k])]
+                                           : rt_rank(RT[c[g][k] >> 6], c[g][k]);
                 }
             }
 #pragma unroll
@@ -1601,6 +1605,7 @@ struct ResolveState {
     int rounds = 0;  // hook rounds the last resolve needed (the converged round included)
     int needed = 0;  // the same, kept across launches (adaptive speculative rounds)
     bool word_labels = false;  // wpref holds word labels (max_distance 1)
+    bool exact = false;        // max_distance 0: the ids are the codes' ranks
     uint32_t scan_tag = 0;     // the last k_scan_rt launch's look-back tag (1..2^30-1)
     int lcc_choice = -1;       // the local-CC instance of the last resolve (launch_local_cc)
     bool checked = false;      // flags[launched] holds a read-only check round (k_roots_check)
@@ -1705,7 +1710,7 @@ int first_zero(const unsigned int* f, int from, int to) {
 #define ROGTK_ASSIGN_G 2  // 4-row groups per lane and trip (experiment builds)
 #endif
 namespace {
-int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, bool word_labels, const uint32_t* codes,
+int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, int labels, const uint32_t* codes,
                    const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id, hipStream_t s);
 int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone = nullptr);
 }  // namespace
@@ -1800,6 +1805,7 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
     st.rounds = 0;
     st.cl = cl;
     st.word_labels = max_distance == 1;
+    st.exact = max_distance == 0;
     int spec = g_spec_rounds.load();
     if (g_spec_adaptive.load() && st.needed > spec) spec = std::min(st.needed + 1, kMaxRounds);
     const bool rounds = max_distance == 1 && cl.L > kLocalPos;
@@ -1893,7 +1899,7 @@ int finish_locked(const void* ws, ResolveState& st, hipStream_t s, int* redone) 
     if (int rc = enqueue_labels(st.cl, p, s, nullptr)) return rc;
     if (st.deferred.on) {  // the assign that ran on the speculative labels, again
         st.deferred.on = false;
-        return enqueue_assign(st.cl, p, st.word_labels, st.deferred.codes, st.deferred.regbits, st.deferred.n,
+        return enqueue_assign(st.cl, p, st.word_labels ? 1 : st.exact ? 2 : 0, st.deferred.codes, st.deferred.regbits, st.deferred.n,
                               st.deferred.cid, s);
     }
     return ROGTK_OK;
@@ -1938,12 +1944,12 @@ int launch_cluster_assign(const ClusterLayout& cl, const uint8_t* ws, const uint
     if (!deferred)
         if (int rc = cluster_finish(ws, s)) return rc;
     WsPtrs p = ws_ptrs(cl, const_cast<uint8_t*>(ws));
-    bool wl = false;
+    int wl = 0;
     {
         std::lock_guard<std::mutex> lk(g_rs_mu);
         auto it = g_rs.find(ws);
         if (it != g_rs.end()) {
-            wl = it->second.word_labels;
+            wl = it->second.word_labels ? 1 : it->second.exact ? 2 : 0;
             if (deferred && it->second.pending) {
                 auto& d = it->second.deferred;
                 d.on = true;
@@ -2022,11 +2028,11 @@ int launch_cluster_lookup(const ClusterLayout& cl, const uint8_t* ws, const uint
 #define ROGTK_ASSIGN_G 2  // 4-row groups per lane and trip (experiment builds)
 #endif
 namespace {
-int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, bool word_labels, const uint32_t* codes,
+int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, int labels, const uint32_t* codes,
                    const uint64_t* regular_bits, int64_t n, uint32_t* cluster_id, hipStream_t s) {
     if (n <= 0) return ROGTK_OK;
-    const uint32_t* wlab = word_labels ? p.wpref : nullptr;
-    const uint64_t* wexc = word_labels ? p.G : nullptr;
+    const uint32_t* wlab = labels == 1 ? p.wpref : nullptr;
+    const uint64_t* wexc = labels == 1 ? p.G : nullptr;
     ProfScope prof(K_ASSIGN, s, true);  // events on the dispatch packet (kernel time only)
     // Two workgroups per CU, grid-stride: assign runs beside the next batch's resolve,
     // whose hook rounds are latency-bound; a full grid of gathers (40k waves at 10M rows)
@@ -2042,7 +2048,10 @@ int enqueue_assign(const ClusterLayout& cl, const WsPtrs& p, bool word_labels, c
     }();
     constexpr int kGroups = ROGTK_ASSIGN_G;
     const int g = grid_for((n + 4 * kGroups - 1) / (4 * kGroups), cap);
-    if (cl.label_by_code)
+    if (labels == 2)  // exact ids: the ranks
+        hipExtLaunchKernelGGL((k_assign<2, kGroups>), dim3(g), dim3(kBlock), 0, s, prof.start(), prof.stop(), 0, codes,
+                              regular_bits, n, p.labelcode, p.ilab, p.RT, wlab, wexc, cluster_id);
+    else if (cl.label_by_code)
         hipExtLaunchKernelGGL((k_assign<0, kGroups>), dim3(g), dim3(kBlock), 0, s, prof.start(), prof.stop(), 0, codes,
                               regular_bits, n, p.labelcode, p.D, p.RT, wlab, wexc, cluster_id);
     else

@@ -284,9 +284,12 @@ def cluster_batch(engine: ClusterEngine, batch: PackedBatch, cluster_id: torch.T
     """mark -> local bitmap -> (all-gather over ranks) -> resolve -> assign."""
     from .dist import gather_bitmaps
 
-    if not marked:
-        engine.mark(batch, stream)
-    local = engine.build_local_bitmap(stream)
+    if not marked and 7 <= batch.umi_len <= 13:  # the presence bitmap in one call (code slices / sort)
+        local = engine.mark_bitmap(batch, stream)
+    else:
+        if not marked:
+            engine.mark(batch, stream)
+        local = engine.build_local_bitmap(stream)
     bitmaps, nb = gather_bitmaps(local, group)
     engine.resolve(bitmaps, nb, max_distance, stream)
     engine.assign(batch, cluster_id, stream)

@@ -29,6 +29,8 @@ else
     rc=$?; echo "c3 trace rc=$rc"; find $O/c3trace -name '*kernel_trace.csv' -delete; [ $rc -eq 0 ] || exit $rc
     timeout -k 10 240 python3 tools/bench_kmer.py --reads 100000000 --steps 3 --warmup 1 > $O/c3.log 2>&1
     rc=$?; echo "c3 rc=$rc"; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 300 python3 tools/bench_kmer.py --reads 100000000 --k 15 --min-coverage 5 --steps 3 --warmup 1 > $O/c3_k16.log 2>&1
+    rc=$?; echo "c3 k16 rc=$rc"; [ $rc -eq 0 ] || exit $rc
     timeout -k 10 240 python3 bench.py --workload C4 --emulate-ranks 8 --steps 20 --warmup 3 --no-cpu-baseline > $O/c4_emul8.log 2>&1
     rc=$?; echo "c4 rc=$rc"; [ $rc -eq 0 ] || exit $rc
     timeout -k 10 300 python3 tools/bench_bam.py > $O/c5.log 2>&1
