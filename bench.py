@@ -323,8 +323,10 @@ def c3_workload(n: int = 100_000_000, steps: int = 3, warmup: int = 1, k: int = 
             except Exception:  # an older library (A/B)
                 pass
 
+        # max_len: the generator's read length (a bound the caller knows; the device still
+        # rejects a longer row), so no reduction over the offsets runs in the step
         _, _, G, _ = D.group_spectra(offsets, reads, cid, k, min_coverage, batch_rows=br, consume=consume,
-                                     packed=None if ascii else "auto")
+                                     packed=None if ascii else "auto", max_len=RL)
         e3.record()
         torch.cuda.synchronize()
         if record:

@@ -561,8 +561,13 @@ __global__ __launch_bounds__(64, 3) void k_pack_gather(const int64_t* __restrict
                                                       int32_t* __restrict__ row_len,
                                                       unsigned long long* __restrict__ gstat,
                                                       unsigned long long* __restrict__ long_rows) {
-    constexpr int kSlot = 8 * NW + 1;  // dwords per row slot: 32 NW bytes + 3 of alignment + the 9-dword reads
-    __shared__ uint32_t stg[64 * kSlot];
+    // dwords per row slot: the row's 16-B chunks from the aligned address below its first
+    // byte (<= 32 NW + 15 bytes), which also covers the 9-dword reads below
+    constexpr int kChunks = (32 * NW + 15 + 15) / 16;
+    constexpr int kSlot = 4 * kChunks;
+    static_assert(kSlot >= 8 * NW + 4, "slot covers the word reads");
+    __shared__ uint4 stg4[64 * kChunks];
+    const uint32_t* const stg = reinterpret_cast<const uint32_t*>(stg4);
     const int lane = threadIdx.x;
     const bool cert = K >= 31 && K <= 32;  // k_group_classify reads the certificate only there
     for (int64_t rb = (int64_t)blockIdx.x * 64; rb < n_rows; rb += (int64_t)gridDim.x * 64) {
@@ -583,32 +588,36 @@ __global__ __launch_bounds__(64, 3) void k_pack_gather(const int64_t* __restrict
             len = (int)min<int64_t>(offsets[pr + 1] - st, 1 << 30);
         }
         const int clen = min(len, 32 * NW);
-        const int64_t a4 = st & ~3ll;
-        const int rel = (int)(st & 3);
-        const int ndw = inK ? (rel + clen + 3) >> 2 : 0;  // dwords of the row's slot to load
-        // the rows' bytes into their slots: row i by one load instruction of the wave
+        const int64_t a16 = st & ~15ll;
+        const int rel = (int)(st & 15);
+        const int nch = inK ? (rel + clen + 15) >> 4 : 0;  // 16-B chunks of the row's slot to load
+        // the rows' chunks into their slots: 16 lanes per row, 4 rows per load instruction,
+        // 16 rows' loads in flight before their LDS stores
+        const int sub = lane >> 4, c = lane & 15;
         for (int i0 = 0; i0 < 64; i0 += 16) {
-            uint32_t v[16];
+            uint4 v[4];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int i = i0 + u;
-                const int ni = __builtin_amdgcn_readlane(ndw, i);
-                const int64_t ai = ((int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(a4 >> 32), i) << 32) |
-                                   (uint32_t)__builtin_amdgcn_readlane((int)a4, i);
-                v[u] = 0;
-                if (lane < ni) {
-                    const int64_t at = ai + 4 * lane;
-                    if (at + 4 <= vlen) {
-                        v[u] = *reinterpret_cast<const uint32_t*>(values + at);
+            for (int u = 0; u < 4; ++u) {
+                const int row = i0 + 4 * u + sub;
+                const int64_t ar = __shfl(a16, row);
+                const int nr = __shfl(nch, row);
+                v[u] = make_uint4(0, 0, 0, 0);
+                if (c < nr) {
+                    const int64_t at = ar + 16 * c;
+                    if (at + 16 <= vlen) {
+                        v[u] = *reinterpret_cast<const uint4*>(values + at);
                     } else {  // the buffer's last bytes: none read past values_len
-                        for (int b = 0; b < 4; ++b)
-                            if (at + b < vlen) v[u] |= (uint32_t)values[at + b] << (8 * b);
+                        uint32_t t4[4] = {0, 0, 0, 0};
+#pragma unroll
+                        for (int b = 0; b < 16; ++b)
+                            if (at + b < vlen) t4[b >> 2] |= (uint32_t)values[at + b] << (8 * (b & 3));
+                        v[u] = make_uint4(t4[0], t4[1], t4[2], t4[3]);
                     }
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 16; ++u)
-                if (lane < kSlot) stg[(i0 + u) * kSlot + lane] = v[u];
+            for (int u = 0; u < 4; ++u)
+                if (c < kChunks) stg4[(i0 + 4 * u + sub) * kChunks + c] = v[u];
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_s_barrier();
@@ -618,8 +627,8 @@ __global__ __launch_bounds__(64, 3) void k_pack_gather(const int64_t* __restrict
         for (int m = 32; m >= 1; m >>= 1) my_len = max(my_len, __shfl_xor(my_len, m, 64));
         const int lmax = __builtin_amdgcn_readfirstlane(my_len);
         const int used = inK ? (clen + 31) >> 5 : 0;
-        const uint32_t sh = (uint32_t)rel * 8;
-        const uint32_t* const slot = stg + lane * kSlot;
+        const uint32_t sh = (uint32_t)(rel & 3) * 8;
+        const uint32_t* const slot = stg + lane * kSlot + (rel >> 2);
         uint64_t wd[NW];
         uint32_t bad = 0;
 #pragma unroll

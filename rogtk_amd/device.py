@@ -420,7 +420,8 @@ def kmer_spectrum_blocks(packed: PackedReads, offsets: torch.Tensor, values: tor
 
 
 def group_spectra(offsets: torch.Tensor, values: torch.Tensor, keys: torch.Tensor, k: int, min_coverage: int,
-                  batch_rows: int = 100_000_000, consume=None, stream=None, packed="auto"):
+                  batch_rows: int = 100_000_000, consume=None, stream=None, packed="auto",
+                  max_len: Optional[int] = None):
     """The C3 front end after H3 (rogtk/__init__.py:206-214: group_by('umi') then
     assemble per group): rows grouped by key (stable; e.g. H3 cluster ids), then k-mer
     spectra (filter_kmers + CountFilter + censored exts, fracture.rs:105-116) over runs of
@@ -437,10 +438,12 @@ def group_spectra(offsets: torch.Tensor, values: torch.Tensor, keys: torch.Tenso
     the 2-bit packing and repeat certificate fused in (kmer_spectrum_fused, round 5) when the
     rows fit 224 bases, else packs the column once into 2-bit blocks (PackedReads) that every
     call stages from; "fused" / "blocks" force one of the two; a PackedReads to reuse; None
-    for the ASCII staging path (no certificate)."""
+    for the ASCII staging path (no certificate). max_len: a bound on the rows' lengths the
+    caller knows (e.g. the sequencer's read length; rows past it fail the call on the device
+    check), else the longest row is found by a reduction kernel (one 8-byte read)."""
     if isinstance(packed, PackedReads):
         max_len = packed.max_len
-    else:  # the longest row by a reduction kernel (no torch kernel, one 8-byte read)
+    elif max_len is None:  # the longest row by a reduction kernel (no torch kernel, one 8-byte read)
         max_len = max_row_len(offsets, stream=stream)
     if isinstance(packed, str):
         mode = ("fused" if max_len <= 224 and values.data_ptr() % 16 == 0 else "blocks") if packed == "auto" \
