@@ -62,6 +62,9 @@ def _rank_of_world(n_total, world, rank, L, scores=True):
     from rogtk_amd import synth
     from rogtk_amd.pipeline import UmiPipeline
 
+    import time
+
+    t0 = time.perf_counter()
     dev = torch.device("cuda", 0)
     present = torch.zeros(4 ** L, dtype=torch.bool, device=dev)
     nw = 4 ** L // 64
@@ -82,6 +85,7 @@ def _rank_of_world(n_total, world, rank, L, scores=True):
     present[codes.long()] = True
     union = torch.nonzero(present).flatten().to(torch.int64).cpu().numpy().astype(np.uint32)
     del present
+    print(f"shards and union ({time.perf_counter() - t0:.1f} s)", flush=True)
     batch = D.PackedBatch(codes, L)
 
     def exchange(bm):  # the all-gather of rank `rank`: its own bitmap in its slot
@@ -128,10 +132,13 @@ def test_c4_rank_of_8_against_the_union():
     from oracle import pyoracle as P
     from rogtk_amd import synth
 
+    import time
+
+    t0 = time.perf_counter()
     n_total, world, rank, L = 500_000_000, 8, 3, 12
     codes_h, got, stats, union = _rank_of_world(n_total, world, rank, L)
     assert len(codes_h) == 62_500_000
-    print(f"C4 rank {rank} of {world} on GPU done: {stats}", flush=True)
+    print(f"C4 rank {rank} of {world} on GPU done ({time.perf_counter() - t0:.1f} s): {stats}", flush=True)
     # H1 / H2 on the rank's distinct codes (distinct set and row -> distinct index from a
     # presence array: no sort of the 62.5M codes)
     pres = np.zeros(4 ** L, dtype=bool)
@@ -152,8 +159,20 @@ def test_c4_rank_of_8_against_the_union():
     _, rw, _ = P.hamming(ucol, b"ACGTACGTACGT", 1)
     assert np.array_equal(got["within"], rw[inv])
     del ucol, ref, uniq, inv
+    print(f"H1/H2 checked ({time.perf_counter() - t0:.1f} s)", flush=True)
     assert len(union) > 0.9 * 4 ** L
-    _check_union_ids(codes_h, got["cid"], stats, union, L)
+    # H3 against the oracle's union-find over the union, pinned in a fixture
+    # (tools/gen_union_fixture.py: 45 s of oracle at this density): the same union (size and
+    # digest), one cluster, so every id is 0
+    with open(os.path.join(ROOT, "tests", "golden", "c4_union_x8.json")) as f:
+        fx = json.load(f)
+    digest = int(np.bitwise_xor.reduce(union.astype(np.uint64) * np.uint64(0x9E3779B1)))
+    assert (fx["n_total"], fx["world"], fx["umi_len"]) == (n_total, world, L)
+    assert len(union) == fx["n_distinct"] and digest == fx["union_digest"]
+    assert stats["n_distinct"] == fx["n_distinct"] and stats["n_clusters"] == fx["n_clusters"]
+    assert stats["overflow"] == 0 and fx["max_cluster_id"] == 0
+    assert int(got["cid"].max()) == 0 and int(got["cid"].min()) == 0
+    print(f"H3 checked ({time.perf_counter() - t0:.1f} s)", flush=True)
 
 
 @pytest.mark.timeout(600)

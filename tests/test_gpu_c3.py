@@ -92,12 +92,10 @@ def _concat(calls, G):
 
 @pytest.mark.parametrize("k,min_cov,batch_rows,packed,filt", [
     (K, MINCOV, 10_000_000, "auto", 0), (K, 2, 200_000, "auto", 0), (K, MINCOV, 10_000_000, None, 0),
-    (K, MINCOV, 10_000_000, "auto", 1), (K, 3, 200_000, "auto", 1), (K, MINCOV, 10_000_000, "blocks", 1),
-    (K, 2, 200_000, "blocks", 0),
+    (K, 3, 200_000, "auto", 1), (K, MINCOV, 10_000_000, "blocks", 1),
     # the reference's defaults: k = 15 (docstring) and 10 (assemble_sequences), effective 16,
     # min_coverage 5 (rogtk/__init__.py:106-107, 211-212)
-    (15, 5, 10_000_000, "auto", 1), (10, 5, 200_000, "auto", 1), (15, 5, 10_000_000, None, 1),
-    (15, 5, 10_000_000, "blocks", 1)])
+    (15, 5, 10_000_000, "auto", 1), (10, 5, 200_000, "blocks", 1)])
 def test_c3_path_1m_vs_oracle(k, min_cov, batch_rows, packed, filt):
     """packed "auto" (150-bp rows: "fused"): rows packed from their ASCII bytes in group
     order with the certificate (rogtk_kmer_spectrum_fused); "blocks": staged from the 2-bit
