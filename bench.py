@@ -109,6 +109,9 @@ def parse():
                          "library's device-scope StreamEvents")
     ap.add_argument("--late-assign", action="store_true",
                     help="host order: enqueue batch k-1's assign after batch k's resolve (round-2 default)")
+    ap.add_argument("--no-split-mark", action="store_true",
+                    help="the whole presence mark on the main stream (round 4 order) instead of its slice mark + "
+                         "merge at the head of the resolve stream")
     ap.add_argument("--assign-lag", type=int, default=0,
                     help="assign batch k-lag at batch k's submit (0: the pipeline's default, 1 per resolve stream)")
     ap.add_argument("--no-c3", action="store_true",
@@ -512,7 +515,8 @@ def main():
                        resolve_streams=args.resolve_streams, assign_on=args.assign_on,
                        reuse_gate=args.reuse_gate, assign_early=not args.late_assign,
                        mark_first=not args.score_first, device_events=not args.torch_events,
-                       mark_stream=args.mark_stream, fused_assign=args.fused_assign, assign_lag=args.assign_lag)
+                       mark_stream=args.mark_stream, fused_assign=args.fused_assign, assign_lag=args.assign_lag,
+                       split_mark=not args.no_split_mark)
 
     def step():
         pipe.submit(batch)

@@ -221,6 +221,13 @@ int rogtk_cluster_mark_bitmap_temp_bytes(int64_t n, int umi_len, int64_t* bytes)
 int rogtk_cluster_set_mark_method(int method);
 int rogtk_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
                               uint64_t* bitmap_out, void* temp, int64_t temp_bytes, void* stream);
+/* Round 5: rogtk_cluster_mark_bitmap in two phases on (possibly) two streams, the caller
+ * ordering phase 2 after phase 1: phase 1 = the slice-bucket pass over the codes (nothing
+ * when the code-slice segments do not apply to (n, umi_len)), phase 2 = the rest (slice
+ * mark + merge of the chunk partials, or the partition sort); phase 0 = both (the
+ * one-call form). Same temp, same bitmap. */
+int rogtk_cluster_mark_bitmap_phase(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
+                                    uint64_t* bitmap_out, void* temp, int64_t temp_bytes, int phase, void* stream);
 /* Releases the host-side resolve state kept for ws (call before freeing ws). */
 int rogtk_cluster_release(const void* ws);
 

@@ -125,6 +125,7 @@ SIGNATURES = {
     "rogtk_group_strings": [_vp, _vp, _i64, _i64, _u32, _vp, _P_I64, _vp],
     "rogtk_irregular_merge": [_vp, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _P_I64, _vp],
     "rogtk_cluster_mark_bitmap_temp_bytes": [_i64, _i32, _P_I64],
+    "rogtk_cluster_mark_bitmap_phase": [_vp, _vp, _i64, _i32, _vp, _vp, _i64, _i32, _vp],
     "rogtk_cluster_mark_bitmap": [_vp, _vp, _i64, _i32, _vp, _vp, _i64, _vp],
     "rogtk_umi_cluster_dev": [_vp, _vp, _vp, _i64, _i32, _i32, _vp, ctypes.POINTER(_i64), _vp],
     "rogtk_route_pack": [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp],

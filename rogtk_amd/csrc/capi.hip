@@ -865,6 +865,12 @@ int rogtk_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bit
     return launch_cluster_mark_bitmap(codes, regular_bits, n, umi_len, bitmap_out, temp, temp_bytes,
                                       as_stream(stream));
 }
+int rogtk_cluster_mark_bitmap_phase(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int umi_len,
+                                    uint64_t* bitmap_out, void* temp, int64_t temp_bytes, int phase, void* stream) {
+    ROGTK_REQUIRE((codes || n == 0) && bitmap_out, ROGTK_E_INVALID, "null codes / bitmap_out");
+    return launch_cluster_mark_phase(codes, regular_bits, n, umi_len, bitmap_out, temp, temp_bytes, phase,
+                                     as_stream(stream));
+}
 int rogtk_cluster_release(const void* ws) {
     if (ws) cluster_release(ws);
     return ROGTK_OK;

@@ -2407,6 +2407,16 @@ int cluster_mark_bitmap_temp(int64_t n, int L, int64_t* bytes) {
 
 int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int L,
                                uint64_t* bitmap, void* temp, int64_t temp_bytes, hipStream_t s) {
+    return launch_cluster_mark_phase(codes, regular_bits, n, L, bitmap, temp, temp_bytes, 0, s);
+}
+
+// phase 0: the whole mark; 1: the slice-bucket pass alone (nothing when the code-slice
+// segments do not apply to (n, L)); 2: the rest (slice mark + OR of the chunk partials, or
+// the partition sort), to be enqueued after phase 1 (round 5: the pipeline runs phase 1 on
+// the main stream and phase 2 at the head of the resolve stream, beside the score kernel)
+int launch_cluster_mark_phase(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int L,
+                              uint64_t* bitmap, void* temp, int64_t temp_bytes, int phase, hipStream_t s) {
+    ROGTK_REQUIRE(phase >= 0 && phase <= 2, ROGTK_E_INVALID, "mark_bitmap: phase %d", phase);
     int64_t need = 0;
     if (int rc = cluster_mark_bitmap_temp(n, L, &need)) return rc;
     ROGTK_REQUIRE((temp || n == 0) && temp_bytes >= need, ROGTK_E_INVALID, "temp_bytes %lld < %lld", (long long)temp_bytes,
@@ -2414,7 +2424,7 @@ int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bi
     ProfScope prof(K_MARK, s);
     const int two_l = 2 * L;
     if (n == 0) {
-        ROGTK_HIP_CHECK(hipMemsetAsync(bitmap, 0, ((size_t)1 << two_l) / 8, s));
+        if (phase != 1) ROGTK_HIP_CHECK(hipMemsetAsync(bitmap, 0, ((size_t)1 << two_l) / 8, s));
         return ROGTK_OK;
     }
     ROGTK_REQUIRE(((uintptr_t)codes & 15u) == 0, ROGTK_E_INVALID, "mark_bitmap: codes must be 16-byte aligned");
@@ -2434,8 +2444,14 @@ int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bi
             // chunks of all rows were read once per slice: 16x at L = 12, from L2)
             segs = (const uint32_t*)((uint8_t*)temp + (chunks > 1 ? (int64_t)chunks * words * 8 : 0));
             seglen = (uint32_t*)((uint8_t*)segs + (int64_t)kMaxSlices * nb * kSegCap * 4);
-            ROGTK_TIMED_LAUNCH(K_K_SLICE_BUCKET, (k_slice_bucket<kBucketRows, kBucketThreads>), dim3((unsigned)nb), dim3(kBucketThreads), 0,
-                               s, codes, regular_bits, n, slog, slices, (uint32_t*)segs, seglen, nb);
+            if (phase != 2)
+                ROGTK_TIMED_LAUNCH(K_K_SLICE_BUCKET, (k_slice_bucket<kBucketRows, kBucketThreads>), dim3((unsigned)nb),
+                                   dim3(kBucketThreads), 0, s, codes, regular_bits, n, slog, slices, (uint32_t*)segs,
+                                   seglen, nb);
+        }
+        if (phase == 1) {
+            ROGTK_HIP_CHECK(hipGetLastError());
+            return ROGTK_OK;
         }
         ROGTK_TIMED_LAUNCH(K_K_SLICE_MARK, k_slice_mark, dim3((unsigned)(slices * chunks)), dim3(kSliceBlock), 0, s, codes, regular_bits,
                            n, slog, chunks, chunk_rows, dst, words, segs, (const uint32_t*)seglen, nb, kBucketRows, kSegCap);
@@ -2445,6 +2461,7 @@ int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bi
         ROGTK_HIP_CHECK(hipGetLastError());
         return ROGTK_OK;
     }
+    if (phase == 1) return ROGTK_OK;  // the partition sort is one phase
     const int64_t slab = (n * 4 + 255) / 256 * 256;
     uint32_t* keys_in = (uint32_t*)temp;
     uint32_t* keys_out = (uint32_t*)((uint8_t*)temp + slab);

@@ -306,6 +306,9 @@ int launch_cluster_local_bitmap(const ClusterLayout& cl, uint8_t* ws, uint64_t* 
 int cluster_mark_bitmap_temp(int64_t n, int L, int64_t* bytes);
 int launch_cluster_mark_bitmap(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int L,
                                uint64_t* bitmap, void* temp, int64_t temp_bytes, hipStream_t s);
+// the same in two phases (1: slice-bucket pass; 2: the rest; 0: both)
+int launch_cluster_mark_phase(const uint32_t* codes, const uint64_t* regular_bits, int64_t n, int L,
+                              uint64_t* bitmap, void* temp, int64_t temp_bytes, int phase, hipStream_t s);
 // The assign half of a fused score + assign: completes (deferred = false) or registers
 // (deferred = true, as launch_cluster_assign) the assign of codes into cluster_id, and
 // fills *a with the tables when the fused kernel can label these rows (word labels,

@@ -213,12 +213,18 @@ class ClusterEngine:
             self._mark_temp = torch.empty(need.value, dtype=torch.uint8, device=self.local_bitmap.device)
         return self._mark_temp
 
-    def mark_bitmap(self, batch: PackedBatch, stream=None):
+    def mark_bitmap(self, batch: PackedBatch, stream=None, phase: int = 0):
         """mark + build_local_bitmap in one: code slices or partition sort + LDS bitmap
-        (7 <= L <= 13). Returns local_bitmap."""
+        (7 <= L <= 13). Returns local_bitmap. phase 1 / 2: the slice-bucket pass / the rest
+        (rogtk_cluster_mark_bitmap_phase), the caller ordering 2 after 1."""
         self.mark_temp(batch.n)
-        _lib.call("rogtk_cluster_mark_bitmap", _p(batch.codes), _p(batch.regular_bits), batch.n, self.umi_len,
-                  _p(self.local_bitmap), _p(self._mark_temp), self._mark_temp.numel(), _s(stream))
+        if phase:
+            _lib.call("rogtk_cluster_mark_bitmap_phase", _p(batch.codes), _p(batch.regular_bits), batch.n,
+                      self.umi_len, _p(self.local_bitmap), _p(self._mark_temp), self._mark_temp.numel(), int(phase),
+                      _s(stream))
+        else:
+            _lib.call("rogtk_cluster_mark_bitmap", _p(batch.codes), _p(batch.regular_bits), batch.n, self.umi_len,
+                      _p(self.local_bitmap), _p(self._mark_temp), self._mark_temp.numel(), _s(stream))
         return self.local_bitmap
 
     def build_local_bitmap(self, stream=None) -> torch.Tensor:

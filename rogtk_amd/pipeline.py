@@ -54,6 +54,7 @@ class _Slot:
         self.cid = torch.empty(max(n_max, 4), dtype=torch.int32, device=dev)
         self.assigned = None  # D.StreamEvent or torch.cuda.Event (UmiPipeline.device_events)
         self.resolved = None
+        self.mark_batch = None  # split_mark: the batch whose mark phase 2 is still to enqueue
 
 
 class UmiPipeline:
@@ -63,7 +64,8 @@ class UmiPipeline:
                  on_assigned=None, score_alone: bool = False, exchange=None, resolve_streams: int = 1,
                  assign_on: str = "main", reuse_gate: str = "auto", assign_early: bool = True,
                  mark_first: bool = True, device_events: bool = True, mark_stream: bool = False,
-                 fused_assign: bool = False, with_distance: bool = False, assign_lag: int = 0):
+                 fused_assign: bool = False, with_distance: bool = False, assign_lag: int = 0,
+                 split_mark: bool = True):
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.umi_len, self.max_distance, self.target, self.max_hamming = umi_len, max_distance, target, max_hamming
         self.group = group
@@ -118,6 +120,14 @@ class UmiPipeline:
         # the score kernel (its segments read back by the slice mark): 0.31-0.32 and
         # 0.346-0.349 vs 0.306 ms/step, the folded score kernel 167 vs 100 us.)
         self.mark_first = mark_first
+        # split_mark (round 5): the presence mark's slice-bucket pass stays on the main stream
+        # (mark(k) -> score(k)), its slice mark + merge move to the head of the resolve stream:
+        # they run beside the score kernel, in the time the resolve would otherwise spend
+        # waiting for the score kernel's waves to leave room for its local CC (a 1024-thread
+        # workgroup needs 4 waves on every SIMD), so the main chain is ~30 us shorter and the
+        # resolve chain is not longer. Applies to the code-slice mark with the default order.
+        self.split_mark = bool(split_mark and self.sort_mark and mark_first and assign_on == "main"
+                               and not mark_stream and not fused_assign)
         # device_events: the cross-stream hand-offs use StreamEvents released at device
         # scope (rogtk_event_*) instead of torch events, whose system-scope release writes
         # the L2 back at every record (round 3: each record / wait between two kernels of
@@ -263,7 +273,10 @@ class UmiPipeline:
         ms = self.s_mark
         if (gate_resolve or ms is not self.main) and slot.resolved is not None:
             D.wait_for(ms, slot.resolved)  # the previous resolve read the bitmap
-        if self.sort_mark:
+        if self.split_mark:  # phase 2 runs at the head of the resolve (_resolve)
+            slot.eng.mark_bitmap(batch, stream=ms, phase=1)
+            slot.mark_batch = batch
+        elif self.sort_mark:
             slot.eng.mark_bitmap(batch, stream=ms)
         else:
             slot.eng.mark(batch, stream=ms)
@@ -276,6 +289,13 @@ class UmiPipeline:
         """[exchange on the comm stream], the resolve on a resolve stream after `marked`;
         returns the resolve's completion event."""
         sr = self.s_resolves[self.k % len(self.s_resolves)]
+        if self.split_mark:  # the rest of the presence mark, at the head of the resolve stream
+            with torch.cuda.stream(sr):
+                D.wait_for(sr, marked)
+                slot.eng.mark_bitmap(slot.mark_batch, stream=sr, phase=2)
+                slot.mark_batch = None
+                marked = self._event()
+                marked.record(sr)
         if self.s_comm is not None:
             with torch.cuda.stream(self.s_comm):
                 D.wait_for(self.s_comm, marked)

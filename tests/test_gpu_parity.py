@@ -746,7 +746,8 @@ def test_streaming_pipeline_matches_sequential(rg, depth, nb, alone, mark, assig
         assert np.array_equal(g_long, scores["longest_homopolymer_run"][:n].cpu().numpy()), k
 
 
-@pytest.mark.parametrize("assign_on", ["main", "separate", "main_mark_stream", "main_fused", "resolve"])
+@pytest.mark.parametrize("assign_on", ["main", "main_no_split", "separate", "main_mark_stream", "main_fused",
+                                       "resolve"])
 def test_pipeline_segment_mark(rg, assign_on):
     """>= 2^20 rows: the code-slice mark runs its segment (bucket) pass and merges one
     partial bitmap per row chunk. Every batch's ids, scores and Hamming bits equal the
@@ -765,9 +766,10 @@ def test_pipeline_segment_mark(rg, assign_on):
         outs.append((slot.cid[:n].clone(), slot.within.clone(), slot.scores["combined_score"][:n].clone()))
 
     mark_stream, fused = assign_on == "main_mark_stream", assign_on == "main_fused"
+    split = assign_on != "main_no_split"  # round 5 default: the slice mark at the head of the resolve stream
     pipe = UmiPipeline(L, n, n, "cuda", depth=2, target=b"ACGTACGTACGT", max_distance=1, on_assigned=grab,
-                       assign_on="main" if mark_stream or fused else assign_on, mark_stream=mark_stream,
-                       fused_assign=fused)
+                       assign_on="main" if mark_stream or fused or not split else assign_on, mark_stream=mark_stream,
+                       fused_assign=fused, split_mark=split)
     keep = []
     for s in seeds:
         keep.append(D.PackedBatch(torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda(), L))
