@@ -1004,7 +1004,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
     __shared__ unsigned long long tkey[kLdsSlots + 1];
     __shared__ uint32_t tinfo[kLdsSlots + 1];  // count (bits 0..23) | exts << 24
     __shared__ uint16_t claimed[C::kClaim + 1];  // slots first touched by this group
-    __shared__ uint64_t ubuf[C::kUnionWords];
+    __shared__ __attribute__((aligned(16))) uint64_t ubuf[C::kUnionWords];
     uint64_t* const words = ubuf;                                      // the group's packed rows
     int32_t* const m_len = reinterpret_cast<int32_t*>(ubuf + kLdsWords + 1);
     int32_t* const m_nobs = m_len + kLdsRows;
@@ -1335,18 +1335,29 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
             if ((uint32_t)tid < nv) {
                 myk = vkey[tid];
                 myi = vinfo[tid];
-                uint32_t j = 0;
-                if (K <= 16) {  // 32-bit keys: the low dwords only (half the LDS reads)
-                    const uint32_t* const vk = reinterpret_cast<const uint32_t*>(vkey);
+            }
+            if (K <= 16) {
+                // 32-bit keys: packed densely over the front of vkey first (every u64 key read
+                // above), so one 16-B broadcast read gives 4 of them; pads compare as the
+                // largest key and count for nobody
+                uint32_t* const vk = reinterpret_cast<uint32_t*>(vkey);
+                const uint32_t n4 = (nv + 3) & ~3u;
+                __syncthreads();
+                if ((uint32_t)tid < n4) vk[tid] = (uint32_t)tid < nv ? (uint32_t)myk : 0xFFFFFFFFu;
+                __syncthreads();
+                if ((uint32_t)tid < nv) {
                     const uint32_t mk = (uint32_t)myk;
-                    for (; j + 4 <= nv; j += 4)
-                        rank += (vk[2 * j] < mk) + (vk[2 * j + 2] < mk) + (vk[2 * j + 4] < mk) + (vk[2 * j + 6] < mk);
-                    for (; j < nv; ++j) rank += vk[2 * j] < mk;
-                } else {
-                    for (; j + 4 <= nv; j += 4)
-                        rank += (vkey[j] < myk) + (vkey[j + 1] < myk) + (vkey[j + 2] < myk) + (vkey[j + 3] < myk);
-                    for (; j < nv; ++j) rank += vkey[j] < myk;
+                    const uint4* const v4 = reinterpret_cast<const uint4*>(vk);
+                    for (uint32_t j = 0; j < n4 / 4; ++j) {
+                        const uint4 q = v4[j];
+                        rank += (q.x < mk) + (q.y < mk) + (q.z < mk) + (q.w < mk);
+                    }
                 }
+            } else if ((uint32_t)tid < nv) {
+                uint32_t j = 0;
+                for (; j + 4 <= nv; j += 4)
+                    rank += (vkey[j] < myk) + (vkey[j + 1] < myk) + (vkey[j + 2] < myk) + (vkey[j + 3] < myk);
+                for (; j < nv; ++j) rank += vkey[j] < myk;
             }
             __syncthreads();  // every key read before the entries move
             if ((uint32_t)tid < nv) {
