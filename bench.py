@@ -53,7 +53,8 @@ TARGET = b"ACGTACGTACGT"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100,
+                    help="timed steps (the pipeline fills and drains once per timed region: 100 steps amortise that to ~1%%)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=("C2", "C4"), default="C2",
                     help="C2: 10M reads per GPU (weak scaling); C4: 500M reads over all GPUs (strong scaling)")

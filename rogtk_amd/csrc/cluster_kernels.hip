@@ -2152,12 +2152,19 @@ __global__ __launch_bounds__(kPartBlock) void k_part_bitmap(const uint32_t* __re
 // the slices of one chunk are the workgroups b = s * chunks + c, which share the XCD
 // c % 8 under the round-robin placement (measured exact; speed only), so their repeated
 // reads of the chunk hit that XCD's L2. No sort, no scattered global stores.
-constexpr int kSliceBlock = 1024;
+#ifndef ROGTK_SLICE_BLOCK
+#define ROGTK_SLICE_BLOCK 1024
+#endif
+constexpr int kSliceBlock = ROGTK_SLICE_BLOCK;
 constexpr int kSliceChunks = 8;    // a multiple of the 8 XCDs (round 3: 8 vs 16 chunks 0.318-0.327 vs 0.322-0.345 ms/step)
-constexpr int kSliceLog2 = 20;     // codes per slice (LDS bits)
-constexpr int kMaxSlices = 16;     // 4^12 / 2^20
+#ifndef ROGTK_SLICE_LOG2
+#define ROGTK_SLICE_LOG2 20
+#endif
+constexpr int kSliceLog2 = ROGTK_SLICE_LOG2;  // codes per slice (LDS bits)
+constexpr int kSliceBits = 24 - kSliceLog2;   // log2 of the slices of 4^12
+constexpr int kMaxSlices = 1 << kSliceBits;
 constexpr int kBucketRows = 8192;  // rows per segment workgroup (8 per lane; default)
-constexpr int kSegCap = kBucketRows / 4;  // codes per (slice, workgroup) segment: 4x the mean share at 16 slices
+constexpr int kSegCap = kBucketRows * 4 / kMaxSlices;  // codes per (slice, workgroup) segment: 4x the mean share
 
 // Segment mode (segs != nullptr, written by k_slice_bucket): workgroup (s, c) reads only
 // slice s's segments of the bucket workgroups of chunk c (every code is read once in
@@ -2170,7 +2177,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_mark(const uint32_t* __re
                                                             const uint32_t* __restrict__ seglen = nullptr,
                                                             int nbuckets = 0, int bucket_rows = kBucketRows,
                                                             int seg_cap = kSegCap) {
-    __shared__ uint32_t sbits[(1u << kSliceLog2) / 32];  // 128 KB: the slice's bits (2^slice_log2 used)
+    __shared__ uint32_t sbits[(1u << kSliceLog2) / 32];  // 128 KB at 2^20: the slice's bits (2^slice_log2 used)
     const int c = blockIdx.x % chunks, sl = blockIdx.x / chunks;
     const uint32_t sw32 = (1u << slice_log2) >> 5;
     for (uint32_t k = threadIdx.x; k < sw32; k += kSliceBlock) sbits[k] = 0;
@@ -2260,7 +2267,7 @@ __global__ __launch_bounds__(kBucketThreads) void k_slice_bucket(const uint32_t*
                                                          int slice_log2, int nslices, uint32_t* __restrict__ segs,
                                                          uint32_t* __restrict__ seglen, int nbuckets) {
     __shared__ unsigned int cnt[kMaxSlices], lbase[kMaxSlices + 1];
-    constexpr int kSegCap = kBucketRows / 4;  // 4x the mean share at 16 slices
+    constexpr int kSegCap = kBucketRows * 4 / kMaxSlices;  // 4x the mean share
     __shared__ uint32_t stage[kBucketRows];
     const int t = threadIdx.x, lane = t & 63;
     if (t < kMaxSlices) cnt[t] = 0;
@@ -2299,7 +2306,7 @@ __global__ __launch_bounds__(kBucketThreads) void k_slice_bucket(const uint32_t*
             const bool ok = ((regs[u] >> k) & 1u) && sl < (uint32_t)nslices;
             uint64_t peers = __ballot(ok);
 #pragma unroll
-            for (int bit = 0; bit < 4; ++bit) {
+            for (int bit = 0; bit < kSliceBits; ++bit) {
                 const uint64_t b = __ballot((sl >> bit) & 1u);
                 peers &= ((sl >> bit) & 1u) ? b : ~b;
             }

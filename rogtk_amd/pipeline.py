@@ -126,7 +126,7 @@ class UmiPipeline:
         # waiting for the score kernel's waves to leave room for its local CC (a 1024-thread
         # workgroup needs 4 waves on every SIMD), so the main chain is ~30 us shorter and the
         # resolve chain is not longer. Applies to the code-slice mark with the default order.
-        self.split_mark = bool(split_mark and self.sort_mark and mark_first and assign_on == "main"
+        self.split_mark = bool(split_mark and self.sort_mark and mark_first and assign_on in ("main", "separate")
                                and not mark_stream and not fused_assign)
         # device_events: the cross-stream hand-offs use StreamEvents released at device
         # scope (rogtk_event_*) instead of torch events, whose system-scope release writes

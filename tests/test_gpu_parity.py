@@ -1087,10 +1087,12 @@ def test_level2_transfers_pinned_and_pageable(rg):
     assert nk.value == k_p and np.array_equal(_np(cid_p).astype(np.uint32), cid)
 
 
-@pytest.mark.parametrize("depth,rs,lag", [(3, 2, 0), (4, 2, 3), (4, 3, 0)])
-def test_pipeline_resolve_streams(rg, depth, rs, lag):
+@pytest.mark.parametrize("depth,rs,lag,assign_on", [(3, 2, 0, "main"), (4, 2, 3, "main"), (4, 3, 0, "main"),
+                                                    (2, 1, 0, "separate"), (3, 2, 0, "separate")])
+def test_pipeline_resolve_streams(rg, depth, rs, lag, assign_on):
     """resolve_streams > 1 (consecutive batches resolve on different streams) with the
-    default schedule, and with assign_lag: every batch's ids, scores and Hamming bits,
+    default schedule, with assign_lag, and with the assign on a stream of its own (the split
+    mark then spans three streams): every batch's ids, scores and Hamming bits,
     taken at its on_assigned hook, equal the sequential device path."""
     import torch
 
@@ -1106,7 +1108,8 @@ def test_pipeline_resolve_streams(rg, depth, rs, lag):
         outs.append((slot.cid[:n].clone(), slot.within.clone(), slot.scores["combined_score"][:n].clone()))
 
     pipe = UmiPipeline(L, n, n, "cuda", depth=depth, target=b"ACGTACGTACGT", max_distance=1, on_assigned=grab,
-                       resolve_streams=rs, assign_lag=lag)
+                       resolve_streams=rs, assign_lag=lag, assign_on=assign_on)
+    assert pipe.split_mark
     keep = []
     for s in seeds:
         keep.append(D.PackedBatch(torch.from_numpy(synth.umi_codes(n, L, seed=s).view(np.int32)).cuda(), L))
