@@ -1135,14 +1135,16 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
                             slot = (slot + 1) & (kLdsSlots - 1);
                         }
                     }
-                    const uint32_t cnt0 = atomicAdd(&tinfo[slot], 1u) & 0xFFFFFFu;
+                    const uint32_t old = atomicAdd(&tinfo[slot], 1u);
+                    const uint32_t cnt0 = old & 0xFFFFFFu;
                     if (cnt0 == 0) {
                         const uint32_t ci = atomicAdd(&s_claimed, 1u);
                         if (!kBounded || ci < (uint32_t)C::kClaim) claimed[ci] = (uint16_t)slot;
                         else s_over = 1;  // more distinct k-mers than the table takes
                     }
                     if (cnt0 + 1 == hit_at) s_hit = 1;
-                    if (e) atomicOr(&tinfo[slot], e << 24);
+                    // the extension bits only when one is new (the count's old value carries them)
+                    if (e & ~(old >> 24)) atomicOr(&tinfo[slot], e << 24);
                 }
             }
         }
@@ -1324,14 +1326,18 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
         }
         uint32_t P = 2;
         while (P < nv) P <<= 1;
+        // rank sort: every thread keeps its own entry and writes it at its rank (the
+        // censoring reads the hash table, not the sorted order), so the entries never move
+        bool direct = false;
+        uint64_t myk = 0;
+        uint32_t myi = 0, rank = 0;
         if (nv <= (uint32_t)TB && kRankSort) {
             // 65..TB valid entries (round 5; C3 at k_eff 16, min_coverage 5: ~157 per group):
             // a rank sort instead of a bitonic network - thread i counts the keys below its
             // own (distinct: one table slot each), every wave reading the same vkey[j] at once
-            // (an LDS broadcast), then stores its entry at that rank: two barriers instead of
-            // one per bitonic stage (36 at 256 entries)
-            uint64_t myk = 0;
-            uint32_t myi = 0, rank = 0;
+            // (an LDS broadcast), then writes its entry out at that rank: two barriers instead
+            // of one per bitonic stage (36 at 256 entries)
+            direct = true;
             if ((uint32_t)tid < nv) {
                 myk = vkey[tid];
                 myi = vinfo[tid];
@@ -1359,12 +1365,6 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
                     rank += (vkey[j] < myk) + (vkey[j + 1] < myk) + (vkey[j + 2] < myk) + (vkey[j + 3] < myk);
                 for (; j < nv; ++j) rank += vkey[j] < myk;
             }
-            __syncthreads();  // every key read before the entries move
-            if ((uint32_t)tid < nv) {
-                vkey[rank] = myk;
-                vinfo[rank] = myi;
-            }
-            __syncthreads();
         } else if (P == 128) {
             // 65..128 valid entries (a family of min_cov or more reads, e.g. C3's uncertified
             // groups: a 150-bp template has 119 k-mers): wave 0 sorts them in registers, two
@@ -1449,8 +1449,8 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
             const uint32_t i = i0 + tid;
             bool term = false, iso = false;
             if (i < nv) {
-            const uint64_t key = vkey[i];
-            const uint32_t info = vinfo[i];
+            const uint64_t key = direct ? myk : vkey[i];
+            const uint32_t info = direct ? myi : vinfo[i];
             const uint32_t e = (info >> 16) & 0xFFu;
             uint32_t ne = 0;
             for (int bit = 0; bit < 8; ++bit) {
@@ -1459,7 +1459,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
                 const uint64_t nb = bit < 4 ? (key >> 2) | (bb << (2 * K - 2)) : ((key << 2) | bb) & kmask;
                 if (valid_at(nb)) ne |= 1u << bit;
             }
-            const int64_t o = base + i;
+            const int64_t o = base + (direct ? rank : i);
             t_kmer[2 * o] = 0;
             t_kmer[2 * o + 1] = key;
             t_ext[o] = (uint8_t)ne;
