@@ -68,6 +68,11 @@ int rogtk_event_record(void* ev, void* stream);
 int rogtk_stream_wait_event(void* stream, void* ev);
 int rogtk_event_query(void* ev, int* done);
 int rogtk_event_synchronize(void* ev);
+/* rogtk_event_attach_next: the next kernel this thread launches records `ev` on its own
+ * dispatch packet (no marker packet on the stream); rogtk_event_attach_done: *taken = 1 if
+ * one did (else the caller records it), and disarms. */
+int rogtk_event_attach_next(void* ev);
+int rogtk_event_attach_done(int* taken);
 
 /*
  * Output set of UMI complexity scoring: ComplexityScore (umi_score.rs:5-13)

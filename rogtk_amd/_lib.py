@@ -167,6 +167,8 @@ SIGNATURES = {
     "rogtk_event_create": [_i32, ctypes.POINTER(ctypes.c_void_p)],
     "rogtk_event_destroy": [_vp],
     "rogtk_event_record": [_vp, _vp],
+    "rogtk_event_attach_next": [_vp],
+    "rogtk_event_attach_done": [_vp],
     "rogtk_stream_wait_event": [_vp, _vp],
     "rogtk_event_query": [_vp, _P_I32],
     "rogtk_event_synchronize": [_vp],

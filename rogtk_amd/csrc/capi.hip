@@ -589,6 +589,31 @@ int check_host_col(const HostCol& h) {
 
 }  // namespace
 
+namespace rogtk {
+namespace detail_attach {
+thread_local hipEvent_t t_attached = nullptr;  // rogtk_event_attach_next
+thread_local bool t_attach_taken = false;
+}  // namespace
+void arm_attached_event(hipEvent_t e) {
+    detail_attach::t_attached = e;
+    detail_attach::t_attach_taken = false;
+}
+bool attached_event_taken() { return detail_attach::t_attach_taken; }
+void set_attached_taken() {
+    detail_attach::t_attached = nullptr;
+    detail_attach::t_attach_taken = true;
+}
+hipEvent_t take_attached_event() {
+    using namespace detail_attach;
+    hipEvent_t e = t_attached;
+    if (e) {
+        t_attached = nullptr;
+        t_attach_taken = true;
+    }
+    return e;
+}
+}  // namespace rogtk
+
 extern "C" {
 
 const char* rogtk_version(void) { return "rogtk-amd 0.1.0 (gfx950)"; }
@@ -1125,6 +1150,20 @@ int rogtk_event_create(int flags, void** out) {
 int rogtk_event_destroy(void* ev) {
     if (!ev) return ROGTK_OK;
     ROGTK_HIP_CHECK(hipEventDestroy((hipEvent_t)ev));
+    return ROGTK_OK;
+}
+
+int rogtk_event_attach_next(void* ev) {
+    rogtk::detail_attach::t_attached = (hipEvent_t)ev;
+    rogtk::detail_attach::t_attach_taken = false;
+    return ROGTK_OK;
+}
+
+int rogtk_event_attach_done(int* taken) {
+    ROGTK_REQUIRE(taken, ROGTK_E_INVALID, "event_attach_done: NULL argument");
+    *taken = rogtk::detail_attach::t_attach_taken ? 1 : 0;
+    rogtk::detail_attach::t_attached = nullptr;
+    rogtk::detail_attach::t_attach_taken = false;
     return ROGTK_OK;
 }
 

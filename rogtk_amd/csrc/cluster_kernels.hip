@@ -1648,6 +1648,10 @@ int enqueue_rounds(const ClusterLayout& cl, const WsPtrs& p, int from, int to, h
     return ROGTK_OK;
 }
 
+// rogtk_cluster_resolve's completion event, armed by its caller (rogtk_event_attach_next):
+// recorded on k_word_label's dispatch packet, or by a marker after the resolve's launches
+thread_local hipEvent_t t_resolve_fin = nullptr;
+
 // host_stats != nullptr: k_roots_scan also publishes the stats block (the resolve's
 // first labels pass; never the re-run after extra rounds, which the host waits for)
 // check_round >= 0: the read-only check of that hook round runs inside the roots scan's
@@ -1683,12 +1687,16 @@ int enqueue_labels(const ClusterLayout& cl, const WsPtrs& p, hipStream_t s,
             const char* e = getenv("ROGTK_WORD_EXC1");
             return e && e[0] == '0' ? 0 : 1;
         }();
+        // the resolve's completion event (armed by the caller, taken at rogtk_cluster_resolve's
+        // entry) rides on this last launch's dispatch packet
+        if (t_resolve_fin) arm_attached_event(t_resolve_fin);
         ROGTK_TIMED_LAUNCH(K_K_WORD_LABEL, k_word_label, dim3(grid_for(cl.words, kPersistentGrid)), dim3(kBlock),
                            lds_off ? (size_t)(cl.rblocks + 1) * 4 : 0, s, p.f, p.UR, cl.words, p.RT, cl.max_distinct,
                            p.rbits, p.rpref, p.rblkoff, p.wpref, p.G, p.labelcode, p.ilab, exc1_on,
                            lds_off ? p.rblksum : nullptr, (int64_t)cl.rblocks, lds_off ? p.stats : nullptr,
                            (const unsigned long long*)p.stats, check_round >= 0 ? host_stats : nullptr,
                            (unsigned long long)epoch);
+        if (t_resolve_fin && attached_event_taken()) t_resolve_fin = nullptr;
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     return ROGTK_OK;
@@ -1794,10 +1802,14 @@ int enqueue_resolve(const ClusterLayout& cl, const WsPtrs& p, const uint64_t* bi
 int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t* bitmaps, int n_bitmaps,
                            int max_distance, hipStream_t s) {
     WsPtrs p = ws_ptrs(cl, ws);
+    hipEvent_t fin = take_attached_event();  // armed by the caller: recorded at the end
     std::lock_guard<std::mutex> lk(g_rs_mu);
     ResolveState& st = g_rs[ws];
     if (st.pending && st.deferred.on) {  // a deferred assign must see its resolve complete first
-        if (int rc = finish_locked(ws, st, s)) return rc;
+        if (int rc = finish_locked(ws, st, s)) {
+            if (fin) (void)hipEventRecord(fin, s);
+            return rc;
+        }
     }
     ProfScope prof_chain(K_RESOLVE, s);
     st.pending = false;
@@ -1823,9 +1835,15 @@ int launch_cluster_resolve(const ClusterLayout& cl, uint8_t* ws, const uint64_t*
     // one local-CC instance, the previous resolve's (checked on the device: S_REDO)
     const int choice = rounds && lcc_predict_enabled() ? st.lcc_choice : -1;
     bool checked = false;
+    t_resolve_fin = fin;
     const int launched = enqueue_resolve(cl, p, bitmaps, n_bitmaps, max_distance, spec,
                                          rounds ? (unsigned long long*)st.hstats_dev : nullptr, st.epoch + 1, s, tag,
                                          choice, &checked);
+    if (t_resolve_fin) {  // no k_word_label took it (or the launch failed): a marker
+        (void)hipEventRecord(t_resolve_fin, s);
+        t_resolve_fin = nullptr;
+    }
+    if (fin) set_attached_taken();  // recorded either way (rogtk_event_attach_done says so)
     ROGTK_REQUIRE(launched >= 0, ROGTK_E_HIP, "cluster: resolve launch failed (%s)", hipGetErrorString(hipGetLastError()));
     if (rounds) {
         ++st.epoch;  // the sequence number k_roots_scan / k_word_label publish (passed at enqueue)

@@ -78,11 +78,23 @@ bool profiling_on();
 class ProfScope;
 // One launch with its own exact events (kernel execution time, as rocprofv3's kernel trace)
 // when profiling is on and ID is selected; a plain launch otherwise.
+// A stream-ordering event armed by rogtk_event_attach_next rides on the next such launch's
+// dispatch packet instead of a marker packet of its own (when that launch is not being
+// timed; a timed launch records it right behind).
 #define ROGTK_TIMED_LAUNCH(ID, KERNEL, GRID, BLOCK, LDS, S, ...)                                     \
     do {                                                                                           \
         ::rogtk::ProfScope pk_(ID, S, true);                                                       \
-        hipExtLaunchKernelGGL(KERNEL, GRID, BLOCK, LDS, S, pk_.start(), pk_.stop(), 0, __VA_ARGS__); \
+        hipEvent_t att_ = ::rogtk::take_attached_event();                                          \
+        hipExtLaunchKernelGGL(KERNEL, GRID, BLOCK, LDS, S, pk_.start(), pk_.stop() ? pk_.stop() : att_, 0, \
+                              __VA_ARGS__);                                                        \
+        if (att_ && pk_.stop()) (void)hipEventRecord(att_, S);                                     \
     } while (0)
+// the event armed on this thread (cleared), or nullptr; arm_attached_event re-arms one for
+// the next launch, attached_event_taken: whether the last armed one rode on a launch
+hipEvent_t take_attached_event();
+void arm_attached_event(hipEvent_t e);
+bool attached_event_taken();
+void set_attached_taken();
 class ProfScope {
    public:
     ProfScope(KernelId id, hipStream_t stream, bool exact = false);

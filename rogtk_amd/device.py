@@ -51,6 +51,17 @@ class StreamEvent:
     def record(self, stream: Optional[torch.cuda.Stream] = None):
         _lib.call("rogtk_event_record", self._ev, _s(stream))
 
+    def attach_next(self):
+        """Record this event on the dispatch packet of the next kernel this thread launches
+        through the library (no marker packet of its own); attach_done() says whether one
+        did, and disarms."""
+        _lib.call("rogtk_event_attach_next", self._ev)
+
+    def attach_done(self) -> bool:
+        taken = ctypes.c_int32(0)
+        _lib.call("rogtk_event_attach_done", ctypes.byref(taken))
+        return bool(taken.value)
+
     def wait(self, stream: Optional[torch.cuda.Stream] = None):
         """`stream` waits for this event's last record."""
         _lib.call("rogtk_stream_wait_event", _s(stream), self._ev)

@@ -274,8 +274,19 @@ class UmiPipeline:
         if (gate_resolve or ms is not self.main) and slot.resolved is not None:
             D.wait_for(ms, slot.resolved)  # the previous resolve read the bitmap
         if self.split_mark:  # phase 2 runs at the head of the resolve (_resolve)
-            slot.eng.mark_bitmap(batch, stream=ms, phase=1)
+            marked = self._event()
+            if isinstance(marked, D.StreamEvent):
+                # the bucket pass's own dispatch packet records the event (no marker packet
+                # between it and the score kernel)
+                marked.attach_next()
+                slot.eng.mark_bitmap(batch, stream=ms, phase=1)
+                if not marked.attach_done():
+                    marked.record(ms)
+            else:
+                slot.eng.mark_bitmap(batch, stream=ms, phase=1)
+                marked.record(ms)
             slot.mark_batch = batch
+            return marked
         elif self.sort_mark:
             slot.eng.mark_bitmap(batch, stream=ms)
         else:
@@ -294,8 +305,11 @@ class UmiPipeline:
                 D.wait_for(sr, marked)
                 slot.eng.mark_bitmap(slot.mark_batch, stream=sr, phase=2)
                 slot.mark_batch = None
-                marked = self._event()
-                marked.record(sr)
+                # the resolve below is on this stream: an event only for the comm stream
+                marked = None
+                if self.s_comm is not None:
+                    marked = self._event()
+                    marked.record(sr)
         if self.s_comm is not None:
             with torch.cuda.stream(self.s_comm):
                 D.wait_for(self.s_comm, marked)
@@ -303,7 +317,8 @@ class UmiPipeline:
                 gathered = self._event()
                 gathered.record(self.s_comm)
         with torch.cuda.stream(sr):
-            D.wait_for(sr, marked)
+            if marked is not None:
+                D.wait_for(sr, marked)
             if (gate_resolve or self.s_mark is not self.main) and slot.assigned is not None:
                 D.wait_for(sr, slot.assigned)  # assign(k - depth) reads the tables rewritten here
             if self.s_comm is not None:
@@ -311,9 +326,16 @@ class UmiPipeline:
                 bitmaps.record_stream(sr)  # allocated on the comm stream
             else:
                 bitmaps, nb = self.exchange(slot.eng.local_bitmap)
-            slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr)
             resolved = self._event()
-            resolved.record(sr)
+            if isinstance(resolved, D.StreamEvent):
+                # recorded on the resolve's last kernel's dispatch packet
+                resolved.attach_next()
+                slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr)
+                if not resolved.attach_done():
+                    resolved.record(sr)
+            else:
+                slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr)
+                resolved.record(sr)
         return resolved
 
     def _settle(self, slot: _Slot, stream=None):

@@ -1123,3 +1123,34 @@ def test_pipeline_resolve_streams(rg, depth, rs, lag, assign_on):
         assert np.array_equal(g_cid, cid.cpu().numpy()), k
         assert np.array_equal(g_w, hw.cpu().numpy()), k
         assert np.array_equal(g_comb.view(np.uint64), scores["combined_score"][:n].cpu().numpy().view(np.uint64)), k
+
+
+def test_events_ride_on_dispatch_packets(rg):
+    """rogtk_event_attach_next: the slice-bucket pass and the resolve's last kernel record
+    the pipeline's hand-off events on their own dispatch packets. A second stream that waits
+    only for those events sees the finished mark / resolve: its ids equal the plain path's."""
+    import torch
+
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+
+    n, L = 2_000_003, 12
+    batch = D.PackedBatch(torch.from_numpy(synth.umi_codes(n, L, seed=synth.DEFAULT_SEED + 5).view(np.int32)).cuda(), L)
+    _, _, _, _, cid_ref, _ = _device_run(n, seed=synth.DEFAULT_SEED + 5)
+    eng = D.ClusterEngine(L, n, "cuda")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    marked = D.StreamEvent()
+    marked.attach_next()
+    eng.mark_bitmap(batch, stream=s1, phase=1)
+    assert marked.attach_done()  # the bucket pass took it (10M-row segment mode applies at 2M)
+    marked.wait(s2)
+    eng.mark_bitmap(batch, stream=s2, phase=2)
+    resolved = D.StreamEvent()
+    resolved.attach_next()
+    eng.resolve(eng.local_bitmap, 1, 1, stream=s2)
+    assert resolved.attach_done()
+    resolved.wait(s1)
+    cid = torch.empty(n, dtype=torch.int32, device="cuda")
+    eng.assign(batch, cid, stream=s1)
+    torch.cuda.synchronize()
+    assert np.array_equal(cid.cpu().numpy(), cid_ref.cpu().numpy())

@@ -71,6 +71,20 @@ def test_argument_errors_cross_the_abi_as_status_codes():
     assert lib.rogtk_profile_read(b"nope", ctypes.byref(ctypes.c_double()), ctypes.byref(ctypes.c_int64())) == 1
 
 
+def test_event_attach_disarms_without_a_launch():
+    """rogtk_event_attach_next arms an event for the next library launch of this thread;
+    with no launch in between, attach_done reports it untaken (the caller then records it)
+    and disarms, so a later launch cannot pick up a stale event. No HIP call is made."""
+    from rogtk_amd import _lib
+
+    lib = _lib.hip()
+    taken = ctypes.c_int32(7)
+    assert lib.rogtk_event_attach_next(ctypes.c_void_p(0x1000)) == 0
+    assert lib.rogtk_event_attach_done(ctypes.byref(taken)) == 0 and taken.value == 0
+    assert lib.rogtk_event_attach_done(ctypes.byref(taken)) == 0 and taken.value == 0
+    assert lib.rogtk_event_attach_done(None) == _lib.ROGTK_E_INVALID
+
+
 def test_synth_is_deterministic_and_shardable():
     from rogtk_amd import synth
 
