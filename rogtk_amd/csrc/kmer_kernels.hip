@@ -570,54 +570,86 @@ __global__ __launch_bounds__(64, 3) void k_pack_gather(const int64_t* __restrict
     const uint32_t* const stg = reinterpret_cast<const uint32_t*>(stg4);
     const int lane = threadIdx.x;
     const bool cert = K >= 31 && K <= 32;  // k_group_classify reads the certificate only there
-    for (int64_t rb = (int64_t)blockIdx.x * 64; rb < n_rows; rb += (int64_t)gridDim.x * 64) {
+    // Software pipeline over the wave's trips: during trip t the loads of trip t + 1's
+    // offsets, validity byte and group k (their row index and group came a trip earlier)
+    // and of trip t + 2's row index and group are in flight, so a trip waits for its row
+    // bytes only (round 5: three dependent round trips per trip before)
+    const int64_t rstride = (int64_t)gridDim.x * 64;
+    auto l1 = [&](int64_t r, int64_t& pr, uint32_t& g) {
+        pr = 0;
+        g = 0;
+        if (r < n_rows) {
+            pr = rows ? rows[r] : r;
+            g = row_group[r];
+        }
+    };
+    auto l2 = [&](int64_t r, int64_t pr, uint32_t g, int64_t& o0, int64_t& o1, uint32_t& vb, uint32_t& gv) {
+        o0 = o1 = 0;
+        vb = 1;
+        gv = 0xFFFFFFFFu;
+        if (r < n_rows) {
+            o0 = offsets[pr];
+            o1 = offsets[pr + 1];
+            if (validity) {
+                const int64_t bit = voff + pr;
+                vb = (uint32_t)(validity[bit >> 3] >> (bit & 7));
+            }
+            gv = gk[g];
+        }
+    };
+    int64_t c_pr, n_pr, c_o0, c_o1;
+    uint32_t c_g, n_g, c_vb, c_gv;
+    {
+        const int64_t r = (int64_t)blockIdx.x * 64 + lane;
+        l1(r, c_pr, c_g);
+        l1(r + rstride, n_pr, n_g);
+        l2(r, c_pr, c_g, c_o0, c_o1, c_vb, c_gv);
+    }
+    for (int64_t rb = (int64_t)blockIdx.x * 64; rb < n_rows; rb += rstride) {
         const int64_t r = rb + lane;
         const bool live = r < n_rows;
-        const int64_t pr = live ? (rows ? rows[r] : r) : 0;
-        const uint32_t my_g = live ? row_group[r] : 0u;
-        bool valid = live;
-        if (live && validity) {
-            const int64_t bit = voff + pr;
-            valid = (validity[bit >> 3] >> (bit & 7)) & 1;
-        }
-        const bool inK = valid && gk[my_g] == K;
-        int64_t st = 0;
-        int len = 0;
-        if (live) {
-            st = offsets[pr];
-            len = (int)min<int64_t>(offsets[pr + 1] - st, 1 << 30);
-        }
+        const uint32_t my_g = c_g;
+        const bool valid = live && (c_vb & 1u);
+        const bool inK = valid && c_gv == (uint32_t)K;
+        const int64_t st = live ? c_o0 : 0;
+        const int len = live ? (int)min<int64_t>(c_o1 - c_o0, 1 << 30) : 0;
+        // trip t + 1's second level, trip t + 2's first (consumed a trip later)
+        c_pr = n_pr;
+        c_g = n_g;
+        l2(r + rstride, c_pr, c_g, c_o0, c_o1, c_vb, c_gv);
+        l1(r + 2 * rstride, n_pr, n_g);
         const int clen = min(len, 32 * NW);
         const int64_t a16 = st & ~15ll;
         const int rel = (int)(st & 15);
         const int nch = inK ? (rel + clen + 15) >> 4 : 0;  // 16-B chunks of the row's slot to load
         // the rows' chunks into their slots: 16 lanes per row, 4 rows per load instruction,
-        // 16 rows' loads in flight before their LDS stores
+        // all 64 rows' loads in flight before their LDS stores (a row whose chunks end within
+        // 16 B of the buffer's end takes the byte-wise path after them)
         const int sub = lane >> 4, c = lane & 15;
-        for (int i0 = 0; i0 < 64; i0 += 16) {
-            uint4 v[4];
+        uint4 v[16];
+        bool tail[16];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int row = i0 + 4 * u + sub;
-                const int64_t ar = __shfl(a16, row);
-                const int nr = __shfl(nch, row);
-                v[u] = make_uint4(0, 0, 0, 0);
-                if (c < nr) {
-                    const int64_t at = ar + 16 * c;
-                    if (at + 16 <= vlen) {
-                        v[u] = *reinterpret_cast<const uint4*>(values + at);
-                    } else {  // the buffer's last bytes: none read past values_len
-                        uint32_t t4[4] = {0, 0, 0, 0};
+        for (int u = 0; u < 16; ++u) {
+            const int row = 4 * u + sub;
+            const int64_t ar = __shfl(a16, row);
+            const int nr = __shfl(nch, row);
+            const int64_t at = ar + 16 * c;
+            v[u] = make_uint4(0, 0, 0, 0);
+            tail[u] = c < nr && at + 16 > vlen;
+            if (c < nr && !tail[u]) v[u] = *reinterpret_cast<const uint4*>(values + at);
+        }
 #pragma unroll
-                        for (int b = 0; b < 16; ++b)
-                            if (at + b < vlen) t4[b >> 2] |= (uint32_t)values[at + b] << (8 * (b & 3));
-                        v[u] = make_uint4(t4[0], t4[1], t4[2], t4[3]);
-                    }
+        for (int u = 0; u < 16; ++u) {
+            if (__builtin_amdgcn_ballot_w64(tail[u])) {  // wave-uniform: the shuffle needs every lane
+                const int64_t at = __shfl(a16, 4 * u + sub) + 16 * c;
+                if (tail[u]) {  // the buffer's last bytes: none read past values_len
+                    uint32_t t4[4] = {0, 0, 0, 0};
+                    for (int b = 0; b < 16; ++b)
+                        if (at + b < vlen) t4[b >> 2] |= (uint32_t)values[at + b] << (8 * (b & 3));
+                    v[u] = make_uint4(t4[0], t4[1], t4[2], t4[3]);
                 }
             }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (c < kChunks) stg4[(i0 + 4 * u + sub) * kChunks + c] = v[u];
+            if (c < kChunks) stg4[(4 * u + sub) * kChunks + c] = v[u];
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_s_barrier();
