@@ -124,6 +124,10 @@ def parse():
     ap.add_argument("--no-c3-k16", action="store_true",
                     help="skip the C3 block at the reference's default k (15 / 10: effective 16), min_coverage 5")
     ap.add_argument("--c3-steps", type=int, default=3)
+    ap.add_argument("--no-h5", action="store_true",
+                    help="skip the H5 block (every group of a 10M-read C3-style run assembled: GPU spectra + "
+                         "host assembly threads, round 6)")
+    ap.add_argument("--h5-reads", type=int, default=10_000_000)
     return ap.parse_args()
 
 
@@ -354,11 +358,11 @@ def c3_workload(n: int = 100_000_000, steps: int = 3, warmup: int = 1, k: int = 
     obs = n * (RL - k_eff + 1)  # k-mer observations per step (every read is ACGT, full length)
     kernels = {}
     if profile:
-        sel = ("pack_reads", "row_gather", "kmer_lds", "kmer_minimizer")
+        sel = ("pack_reads", "pack_gather", "row_gather", "kmer_wave", "kmer_lds", "kmer_minimizer")
         try:
             D.profile_select(",".join(sel))
         except Exception:  # a library without these kernel names (A/B of older builds)
-            sel = sel[:3]
+            sel = ("pack_reads", "row_gather", "kmer_lds", "kmer_minimizer")
             try:
                 D.profile_select(",".join(sel))
             except Exception:
@@ -376,9 +380,9 @@ def c3_workload(n: int = 100_000_000, steps: int = 3, warmup: int = 1, k: int = 
     cu_clk = 256 * 2.4e9  # MI355X: 256 CUs at 2.4 GHz
     peak = HBM_PEAK_GBS
     # Algorithmic HBM bytes per read: the ASCII read once, its UMI code read and
-    # its cluster id written (RL + 8). As built: pack (RL in, one 64-B block out), grouped
-    # gather (64-B block in, 40 B staged + 12 B of row metadata).
-    alg_b, staged_b = RL + 8, RL + 64 + 64 + 40 + 12
+    # its cluster id written (RL + 8). As built (round 5: fused pack + grouped staging): the
+    # row and its index / offsets / group in, the packed words and row metadata out.
+    alg_b, staged_b = RL + 8, RL + 8 + 16 + 4 + 8 * -(-RL // 32) + 8 + 4
     ach = lambda b: n * b / step_s / 1e9
     out = {
         "workload": f"C3: {n // 1_000_000}M reads x {RL} bp, 12-bp UMI; H3 exact ids -> group_by -> k-mer "
@@ -401,17 +405,31 @@ def c3_workload(n: int = 100_000_000, steps: int = 3, warmup: int = 1, k: int = 
         "data": f"synthetic (synth-v1 reads + UMIs, {n // 10} molecules), generated in {gen_s:.1f} s, "
                 "resident in HBM",
     }
-    if "kmer_lds" in kernels:  # the insert kernels alone: the observations THEY inserted per CU clock
+    if "kmer_lds" in kernels or "kmer_wave" in kernels:
+        # the insert kernels alone (the wave-per-group class 2 at k_eff <= 16, round 6, and the
+        # workgroup classes 3 / 1 / 4): the observations THEY inserted per CU clock
         lds_obs = path_groups[3] * (RL - k_eff + 1)  # rows of the groups left on the LDS kernels
+        us = kernels.get("kmer_wave", 0.0) + kernels.get("kmer_lds", 0.0)
         out["lds_rows"] = path_groups[3]
-        out["roofline"]["kmer_lds"] = {"bound": "lds", "kernel": "k_kmer_lds<1|3|4>", "us": kernels["kmer_lds"],
+        out["roofline"]["kmer_lds"] = {"bound": "lds", "kernel": "k_kmer_wave + k_kmer_lds<1|3|4>"
+                                       if "kmer_wave" in kernels else "k_kmer_lds<1|3|4>", "us": round(us, 1),
                                        "observations": lds_obs,
-                                       "obs_per_cu_clock": round(lds_obs / (kernels["kmer_lds"] * 1e-6) / cu_clk, 3)}
+                                       "obs_per_cu_clock": round(lds_obs / (us * 1e-6) / cu_clk, 3)}
     if "pack_reads" in kernels:  # HBM stream: RL bytes in, one 64-B block out per read
         a = n * (RL + 64) / (kernels["pack_reads"] * 1e-6) / 1e9
         out["roofline"]["pack_reads"] = {"bound": "hbm", "kernel": "k_pack_reads", "us": kernels["pack_reads"],
                                          "bytes_per_read": RL + 64, "achieved": round(a, 1), "peak": peak,
                                          "unit": "GB/s", "frac": round(a / peak, 4)}
+    if "pack_gather" in kernels:
+        # k_pack_gather (round 5; its own profile name in round 6): per grouped row, in: the
+        # RL-byte ASCII row, its row index (8 B), offsets (16 B) and group id (4 B); out: S
+        # packed words (8 B each), observation count (8 B) and length (4 B). DESIGN §3b
+        S = -(-RL // 32)
+        bpr = RL + 8 + 16 + 4 + 8 * S + 8 + 4
+        a = n * bpr / (kernels["pack_gather"] * 1e-6) / 1e9
+        out["roofline"]["pack_gather"] = {"bound": "hbm", "kernel": "k_pack_gather", "us": kernels["pack_gather"],
+                                          "bytes_per_read": bpr, "achieved": round(a, 1), "peak": peak,
+                                          "unit": "GB/s", "frac": round(a / peak, 4)}
     if "row_gather" in kernels:  # 64-B block in, 40 B staged + 12 B of row metadata out
         a = n * (64 + 40 + 12) / (kernels["row_gather"] * 1e-6) / 1e9
         out["roofline"]["row_gather"] = {"bound": "hbm", "kernel": "k_row_gather", "us": kernels["row_gather"],
@@ -420,6 +438,92 @@ def c3_workload(n: int = 100_000_000, steps: int = 3, warmup: int = 1, k: int = 
     del reads, codes, offsets, batch, eng, cid
     torch.cuda.empty_cache()
     return out
+
+
+def h5_workload(n: int = 10_000_000, k: int = 10, min_coverage: int = 5, method: str = "compression",
+                read_len: int = 150, steps: int = 2, cpu_groups: int = 200) -> dict:
+    """H5 over a C3-style run (round 6): n synthetic 150-bp reads with 12-bp UMIs in HBM,
+    exact H3 ids (the caller's group_by('umi')), then EVERY group assembled with
+    assemble_sequences' defaults (k = 10, min_coverage 5, rogtk/__init__.py:104-116; method
+    compression, largest contig as the expression asks, expressions.rs:751): the groups' k-mer
+    spectra on the GPU at min_coverage (device.group_spectra: the preliminary graphs), the
+    graphs assembled on host threads (rogtk_assemble_groups_host). Beside it, on samples of
+    the same groups: the per-group C ABI call (rogtk_assemble_host, its own spectrum round
+    trip per group) and the Python restatement (oracle/pyassembly.py, 1 core)."""
+    from rogtk_amd import assembly as AS
+
+    RL, L = read_len, 12
+    dev = torch.device("cuda", torch.cuda.current_device())
+    codes = torch.from_numpy(synth.umi_codes(n, L).view(np.int32)).to(dev)
+    reads_h = synth.reads(n, RL)
+    values = torch.from_numpy(reads_h.reshape(-1)).to(dev)
+    offsets = torch.arange(0, (n + 1) * RL, RL, dtype=torch.int64, device=dev)
+    eng = D.ClusterEngine(L, min(n, 4 ** L), dev)
+    cid = torch.empty(n, dtype=torch.int32, device=dev)
+    D.cluster_batch(eng, D.PackedBatch(codes, L), cid, 0)
+    torch.cuda.synchronize()
+    threads = host_threads()
+    phase = {"spectra_s": 0.0, "assemble_s": 0.0}
+
+    def step():
+        outs = []
+
+        def consume(g0, g1, r):
+            t0 = time.perf_counter()
+            outs.append(AS.assemble_groups(r, method, n_threads=threads))
+            phase["assemble_s"] += time.perf_counter() - t0
+
+        t0 = time.perf_counter()
+        rows, go, G, _ = D.group_spectra(offsets, values, cid, k, min_coverage, batch_rows=n, consume=consume)
+        torch.cuda.synchronize()
+        phase["spectra_s"] += time.perf_counter() - t0
+        return rows, go, G, outs
+
+    step()  # warm-up: buffers, pinned staging
+    phase.update(spectra_s=0.0, assemble_s=0.0)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        rows, go, G, outs = step()
+    el = (time.perf_counter() - t0) / steps
+    arr = pa_concat([a for a, _ in outs])
+    nc = np.concatenate([c for _, c in outs])
+    rows_h, goh = rows.cpu().numpy(), go.cpu().numpy()
+    rng = np.random.default_rng(5)
+    pick = np.sort(rng.choice(G, size=min(G, cpu_groups), replace=False))
+    groups = [[bytes(reads_h[r]) for r in rows_h[goh[g]:goh[g + 1]]] for g in pick]
+    import pyarrow as pa
+    import rogtk_amd as rg
+    got = arr.to_pylist()
+    t1 = time.perf_counter()
+    per_group = [rg.assemble_sequences(pa.array(items, type=pa.large_binary()), k, min_coverage, method)
+                 for items in groups]
+    t_per = time.perf_counter() - t1
+    from oracle import pyassembly as PA
+    t2 = time.perf_counter()
+    ref = ["\n".join(PA.assemble(items, k, min_coverage, method, None, None, True, None, False)) for items in groups]
+    t_cpu = time.perf_counter() - t2
+    same = sum(got[g] == a == b for g, a, b in zip(pick, per_group, ref))
+    del values, codes, offsets, cid, eng
+    torch.cuda.empty_cache()
+    spec_s = phase["spectra_s"] / steps - phase["assemble_s"] / steps
+    return {"workload": f"H5: {n // 1_000_000}M reads x {RL} bp, 12-bp UMI; H3 exact ids -> every group's de Bruijn "
+                        f"assembly, k={k}, min_coverage {min_coverage}, method {method}, largest contig "
+                        f"(assemble_sequences defaults)",
+            "groups": int(G), "groups_per_s": round(G / el, 1), "ms_per_step": round(1000 * el, 2), "steps": steps,
+            "contigs": int(nc.sum()), "groups_with_contig": int((nc > 0).sum()),
+            "split_ms": {"gpu_spectra": round(1000 * spec_s, 2), "host_assembly": round(1000 * phase["assemble_s"] / steps, 2)},
+            "host_threads": threads,
+            "per_group_abi": {"groups_per_s": round(len(pick) / t_per, 1), "sample_groups": len(pick),
+                              "path": "rogtk_assemble_host per group (one GPU spectrum round trip per group)"},
+            "cpu_baseline": {"value": round(len(pick) / t_cpu, 1), "unit": "groups/s", "cores": 1, "kind": "port",
+                             "sample": f"{len(pick)} random groups of the same run, oracle/pyassembly.py (pure "
+                                       f"Python restatement of fracture.rs + djfind.rs), {t_cpu:.1f} s"},
+            "sample_identical": f"{same} of {len(pick)} groups: batched == per-group ABI == Python restatement"}
+
+
+def pa_concat(arrs):
+    import pyarrow as pa
+    return pa.concat_arrays(arrs) if arrs else pa.array([], type=pa.large_string())
 
 
 # the single kernels of the C2 step profiled on their own (besides score / assign)
@@ -729,6 +833,9 @@ def main():
             # docstring's k = 15 (rogtk/__init__.py:106-107, 211-212), both effective 16
             # (fracture.rs:246-256), min_coverage 5
             c3_k16 = c3_workload(args.c3_reads, steps=args.c3_steps, warmup=1, k=15, min_coverage=5)
+    h5 = None
+    if world == 1 and not args.no_h5 and args.emulate_ranks == 1:
+        h5 = h5_workload(args.h5_reads)
     e2e = None
     if not args.no_end_to_end and args.emulate_ranks == 1:
         e2e = end_to_end(codes_h[: min(count, 10_000_000)], L, md)
@@ -769,6 +876,7 @@ def main():
         "end_to_end": e2e,
         "c3": c3,
         "c3_k16": c3_k16,
+        "h5": h5,
         "cpu_baseline": cpu,
         "kernels_us": breakdown,
         "kernels_per_step": per_kernel,

@@ -335,8 +335,9 @@ int rogtk_umi_cluster_dev(const int64_t* offsets, const uint8_t* values, const u
 int rogtk_kmer_capacity(const void* offsets, int offset_width, int64_t n_rows, int64_t* capacity);
 /* Path selection for the calling thread (default 1): groups with <= 2048 k-mer
  * observations, rows <= 2048 bases and k_eff <= 32 run entirely in LDS (one
- * workgroup per group); 0 sends every group through the global radix-sort path.
- * Results are identical; tests use this to cover both paths. */
+ * wave per group for k_eff <= 16 and <= 64 rows, round 6; one workgroup per group
+ * otherwise); 2: the LDS path without the wave class; 0 sends every group through
+ * the global radix-sort path. Results are identical; tests use this to cover the paths. */
 int rogtk_kmer_set_path(int lds_small_groups);
 /* The minimizer filter (round 4; process-wide, default on, ROGTK_KMER_MZ=0 turns it off): on the
  * block path, class-3 groups whose rows all carry the repeat certificate are checked for a
@@ -462,6 +463,25 @@ int rogtk_assembly_optimize_host(const void* offsets, int offset_width, const ui
                                  const char* end_anchor, int64_t start_k, int64_t start_min_coverage,
                                  int64_t max_iterations, int explore_k, int prioritize_length, char* contig,
                                  int64_t contig_cap, int64_t* contig_len, uint32_t* out4);
+/* Round 6: H5 over every group of a k-mer spectrum call at once (the C3 path's device
+ * spectra copied to the host, or any rogtk_kmer_spectrum_* output at the assembly's
+ * min_coverage: its entries are exactly the preliminary graph of fracture.rs:343-348, valid
+ * k-mers with exts censored to valid neighbours). Assembles every group on n_threads host
+ * threads (0: 16) with the method / anchors / only_largest / min_length of
+ * rogtk_assemble_host and returns a result handle: per group one string, its contigs
+ * joined by '\n' (expressions.rs:695-760). Groups whose stats say k_eff 0 (k > 64) or no
+ * valid sequence get an empty string and 0 contigs. Replaces a per-group
+ * rogtk_assemble_host call (each its own spectrum round trip) for a polars
+ * group_by(...).agg(assemble_sequences) over many groups (rogtk/__init__.py:206-214). */
+int rogtk_assemble_groups_host(const uint64_t* kmers, const uint8_t* exts, const uint16_t* counts,
+                               const int64_t* entry_offsets, const int64_t* group_stats, int64_t n_groups,
+                               const char* method, const char* start_anchor, const char* end_anchor,
+                               int only_largest, int64_t min_length, int n_threads, void** result);
+/* Sizes of a result (n_groups, bytes of all strings), then its contents: offsets[n_groups + 1]
+ * (int64, Arrow LargeUtf8), values, n_contigs[n_groups] (each pointer nullable); free it. */
+int rogtk_assembly_result_sizes(const void* result, int64_t* n_groups, int64_t* values_len);
+int rogtk_assembly_result_copy(const void* result, int64_t* offsets, char* values, int64_t* n_contigs);
+int rogtk_assembly_result_free(void* result);
 
 /* ============ paired FASTQ ingest (host C++, zlib) ============
  * parse_paired_fastqs (src/lib.rs:232-428) as a streaming reader of Arrow string

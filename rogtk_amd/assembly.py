@@ -8,6 +8,8 @@ reference (rogtk/__init__.py -> src/expressions.rs)          rogtk_amd
 (:158-234 -> expressions.rs:770-849)
 ``sweep_assembly_params(...)`` (:236-287 -> :880-955)          ``sweep_assembly_params(...)``
 ``optimize_assembly(...)`` (:289-323 -> fracture_opt.rs:283)   ``optimize_assembly(...)``
+``df.group_by(key).agg(assemble_sequences(...))``              ``assemble_groups(...)`` /
+(:206-214, one plugin call per group)                          ``assemble_column_groups(...)`` (round 6)
 ===========================================================  ==============================
 
 Each call is one polars group (the reference registers them ``returns_scalar``).
@@ -149,3 +151,65 @@ def optimize_assembly(column: ColumnLike, method: str = "shortest_path", start_a
             raise
         return {"contig": buf.raw[: need.value].decode(), "k": out4[0], "min_coverage": out4[1],
                 "length": out4[2], "input_sequences": out4[3]}
+
+
+def assemble_groups(spectrum: dict, method: str = "compression", start_anchor: Optional[str] = None,
+                    end_anchor: Optional[str] = None, min_length: Optional[int] = None, only_largest: bool = True,
+                    n_threads: int = 0):
+    """Batched H5 (round 6): every group of one k-mer spectrum result (a device or host
+    dict of rogtk_amd.device.kmer_spectrum_* / a group_spectra call: kmers, exts, counts,
+    entry_offsets, stats) assembled at once on host threads (rogtk_assemble_groups_host).
+    The spectrum must be taken at the assembly's min_coverage: its entries are then the
+    preliminary graph of each group (fracture.rs:343-348). Returns (LargeString array of
+    one string per group - its contigs joined by '\\n', as assemble_sequences_expr's row -,
+    int64 contig counts). only_largest=True is what the expression asks for
+    (expressions.rs:751)."""
+    def host(t, dt):
+        a = t.cpu().numpy() if hasattr(t, "cpu") else np.asarray(t)
+        return np.ascontiguousarray(a.view(dt) if a.dtype != dt and a.dtype.itemsize == np.dtype(dt).itemsize else a,
+                                    dtype=dt)
+    km = host(spectrum["kmers"], np.uint64).reshape(-1)
+    ex = host(spectrum["exts"], np.uint8)
+    cn = host(spectrum["counts"], np.uint16)
+    eo = host(spectrum["entry_offsets"], np.int64)
+    st = host(spectrum["stats"], np.int64).reshape(-1)
+    G = len(eo) - 1
+    p = lambda a: ctypes.c_void_p(a.ctypes.data) if a.size else None
+    h = ctypes.c_void_p()
+    _lib.call("rogtk_assemble_groups_host", p(km), p(ex), p(cn), p(eo), p(st), G, _enc(method), _enc(start_anchor),
+              _enc(end_anchor), int(bool(only_largest)), -1 if min_length is None else int(min_length),
+              int(n_threads), ctypes.byref(h))
+    try:
+        ng, nb = ctypes.c_int64(0), ctypes.c_int64(0)
+        _lib.call("rogtk_assembly_result_sizes", h, ctypes.byref(ng), ctypes.byref(nb))
+        offs = np.zeros(int(ng.value) + 1, np.int64)
+        vals = np.zeros(max(int(nb.value), 1), np.uint8)
+        nc = np.zeros(max(int(ng.value), 1), np.int64)
+        _lib.call("rogtk_assembly_result_copy", h, p(offs), p(vals), p(nc))
+    finally:
+        _lib.call("rogtk_assembly_result_free", h)
+    arr = pa.Array.from_buffers(pa.large_string(), int(ng.value), [None, pa.py_buffer(offs), pa.py_buffer(vals)])
+    return arr, nc[: int(ng.value)]
+
+
+def assemble_column_groups(offsets, values, keys, k: int = 10, min_coverage: int = 5, method: str = "compression",
+                           start_anchor: Optional[str] = None, end_anchor: Optional[str] = None,
+                           min_length: Optional[int] = None, only_largest: bool = True, n_threads: int = 0,
+                           batch_rows: int = 10_000_000):
+    """A device read column grouped by `keys` (e.g. H3 cluster ids: the caller's
+    group_by('umi'), rogtk/__init__.py:206-214) and assembled per group: the k-mer spectra
+    of all groups on the GPU (device.group_spectra at min_coverage), then assemble_groups
+    per spectrum call. Returns (rows in group order, group offsets, strings per group,
+    contig counts)."""
+    from . import device as D
+
+    outs, counts = [], []
+
+    def consume(g0, g1, r):
+        a, c = assemble_groups(r, method, start_anchor, end_anchor, min_length, only_largest, n_threads)
+        outs.append(a)
+        counts.append(c)
+
+    rows, go, G, _ = D.group_spectra(offsets, values, keys, k, min_coverage, batch_rows=batch_rows, consume=consume)
+    arr = pa.concat_arrays(outs) if outs else pa.array([], type=pa.large_string())
+    return rows, go, arr, (np.concatenate(counts) if counts else np.zeros(0, np.int64))

@@ -25,10 +25,12 @@
 //   sweep      expressions.rs:880-955;  optimize  fracture_opt.rs:120-282
 // Graph export (DOT / CSV files, export_graphs) is a file side effect and out of scope.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <map>
 #include <set>
+#include <thread>
 #include <string>
 #include <utility>
 #include <vector>
@@ -460,6 +462,30 @@ int parse_method(const char* method, const char* sa, const char* ea, int* out) {
     return ROGTK_OK;
 }
 
+// fracture.rs:343-464 from the preliminary graph on: the method's contigs, min_length,
+// only_largest (max_by_key: the last longest)
+void assemble_graph(const Graph& g, int method, const std::string& sa, const std::string& ea, int only_largest,
+                    int64_t min_length, std::vector<std::string>* out) {
+    out->clear();
+    std::vector<std::string> cs;
+    if (method == M_COMPRESSION) {
+        cs = compress(g);
+    } else {
+        const PetGraph pg = to_petgraph(g);
+        std::string c;
+        const bool ok = method == M_SHORTEST ? path_assembly(g, pg, sa, ea, &c) : auto_path_assembly(g, pg, &c);
+        if (ok) cs.push_back(c);
+    }
+    for (auto& c : cs)
+        if ((int64_t)c.size() >= std::max<int64_t>(min_length, 0)) out->push_back(c);
+    if (out->empty() || !only_largest) return;
+    size_t best = 0;  // max_by_key: the last maximum
+    for (size_t i = 1; i < out->size(); ++i)
+        if ((*out)[i].size() >= (*out)[best].size()) best = i;
+    std::string keep = (*out)[best];
+    out->assign(1, keep);
+}
+
 // assemble_sequences (fracture.rs:188-280) over a prepared group with a spectrum cache
 struct Assembler {
     GroupCol col;
@@ -479,24 +505,7 @@ struct Assembler {
         }
         const Spectrum& s = it->second;
         if (s.nseq == 0) return ROGTK_OK;  // no valid sequences
-        const Graph g = make_graph(s, min_cov);
-        std::vector<std::string> cs;
-        if (method == M_COMPRESSION) {
-            cs = compress(g);
-        } else {
-            const PetGraph pg = to_petgraph(g);
-            std::string c;
-            const bool ok = method == M_SHORTEST ? path_assembly(g, pg, sa, ea, &c) : auto_path_assembly(g, pg, &c);
-            if (ok) cs.push_back(c);
-        }
-        for (auto& c : cs)
-            if ((int64_t)c.size() >= std::max<int64_t>(min_length, 0)) out->push_back(c);
-        if (out->empty() || !only_largest) return ROGTK_OK;
-        size_t best = 0;  // max_by_key: the last maximum
-        for (size_t i = 1; i < out->size(); ++i)
-            if ((*out)[i].size() >= (*out)[best].size()) best = i;
-        std::string keep = (*out)[best];
-        out->assign(1, keep);
+        assemble_graph(make_graph(s, min_cov), method, sa, ea, only_largest, min_length, out);
         return ROGTK_OK;
     }
 };
@@ -508,6 +517,14 @@ int copy_out(const std::string& s, char* out, int64_t cap, int64_t* len) {
     if (out && !s.empty()) std::memcpy(out, s.data(), s.size());
     return ROGTK_OK;
 }
+
+// The batched H5 result (rogtk_assemble_groups_host): one string per group, the group's
+// contigs joined by '\n' (assemble_sequences_expr's output row, expressions.rs:695-760).
+struct AssemblyResult {
+    std::vector<int64_t> offsets;  // n_groups + 1
+    std::string values;
+    std::vector<int64_t> n_contigs;  // per group
+};
 
 }  // namespace
 }  // namespace rogtk
@@ -689,6 +706,91 @@ int rogtk_assembly_optimize_host(const void* offsets, int offset_width, const ui
     out4[2] = (uint32_t)r.contig.size();
     out4[3] = nin;
     return copy_out(r.contig, contig, contig_cap, contig_len);
+}
+
+// Round 6: H5 over every group of a spectrum call at once. The device spectra at the
+// call's min_coverage are the preliminary graphs (CountFilter + exts censored to valid
+// neighbours = make_graph of the min_coverage 0 spectrum, fracture.rs:343-348), so each
+// group's graph is its entry slice; groups are assembled on n_threads host threads
+// (atomic work counter, 64 groups per take), each writing its own string.
+int rogtk_assemble_groups_host(const uint64_t* kmers, const uint8_t* exts, const uint16_t* counts,
+                               const int64_t* entry_offsets, const int64_t* group_stats, int64_t n_groups,
+                               const char* method, const char* start_anchor, const char* end_anchor,
+                               int only_largest, int64_t min_length, int n_threads, void** result) {
+    ROGTK_REQUIRE(result, ROGTK_E_INVALID, "assemble_groups: result is NULL");
+    *result = nullptr;
+    ROGTK_REQUIRE(n_groups >= 0 && (n_groups == 0 || (entry_offsets && group_stats)), ROGTK_E_INVALID,
+                  "assemble_groups: bad groups");
+    const int64_t total = n_groups ? entry_offsets[n_groups] : 0;
+    ROGTK_REQUIRE(total == 0 || (kmers && exts && counts), ROGTK_E_INVALID, "assemble_groups: NULL spectrum arrays");
+    int m = 0;
+    if (int rc = parse_method(method, start_anchor, end_anchor, &m)) return rc;
+    const std::string sa(start_anchor ? start_anchor : ""), ea(end_anchor ? end_anchor : "");
+    std::vector<std::string> per((size_t)n_groups);
+    std::vector<int64_t> nc((size_t)n_groups, 0);
+    std::atomic<int64_t> next{0};
+    auto work = [&]() {
+        std::vector<std::string> cs;
+        for (;;) {
+            const int64_t g0 = next.fetch_add(64);
+            if (g0 >= n_groups) return;
+            for (int64_t g = g0; g < std::min<int64_t>(n_groups, g0 + 64); ++g) {
+                const int K = (int)group_stats[5 * g];
+                if (K <= 0 || group_stats[5 * g + 1] == 0) continue;  // k > 64 / no valid sequences
+                Graph gr;
+                gr.K = K;
+                gr.mask = K == 64 ? ~(u128)0 : (((u128)1 << (2 * K)) - 1);
+                const int64_t a = entry_offsets[g], b = entry_offsets[g + 1];
+                gr.km.resize((size_t)(b - a));
+                for (int64_t i = a; i < b; ++i) gr.km[i - a] = ((u128)kmers[2 * i] << 64) | kmers[2 * i + 1];
+                gr.ex.assign(exts + a, exts + b);
+                gr.cov.assign(counts + a, counts + b);
+                assemble_graph(gr, m, sa, ea, only_largest, min_length, &cs);
+                nc[g] = (int64_t)cs.size();
+                std::string& o = per[g];
+                for (size_t i = 0; i < cs.size(); ++i) {
+                    if (i) o.push_back('\n');
+                    o += cs[i];
+                }
+            }
+        }
+    };
+    const int T = std::max(1, std::min<int>(n_threads > 0 ? n_threads : 16, (int)((n_groups + 63) / 64)));
+    std::vector<std::thread> pool;
+    for (int t = 1; t < T; ++t) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+    auto* r = new AssemblyResult();
+    r->offsets.resize((size_t)n_groups + 1);
+    r->offsets[0] = 0;
+    for (int64_t g = 0; g < n_groups; ++g) r->offsets[g + 1] = r->offsets[g] + (int64_t)per[g].size();
+    r->values.reserve((size_t)r->offsets[n_groups]);
+    for (auto& x : per) r->values += x;
+    r->n_contigs = std::move(nc);
+    *result = r;
+    return ROGTK_OK;
+}
+
+int rogtk_assembly_result_sizes(const void* result, int64_t* n_groups, int64_t* values_len) {
+    ROGTK_REQUIRE(result && n_groups && values_len, ROGTK_E_INVALID, "assembly_result_sizes: NULL argument");
+    const auto* r = static_cast<const AssemblyResult*>(result);
+    *n_groups = (int64_t)r->n_contigs.size();
+    *values_len = (int64_t)r->values.size();
+    return ROGTK_OK;
+}
+
+int rogtk_assembly_result_copy(const void* result, int64_t* offsets, char* values, int64_t* n_contigs) {
+    ROGTK_REQUIRE(result, ROGTK_E_INVALID, "assembly_result_copy: NULL result");
+    const auto* r = static_cast<const AssemblyResult*>(result);
+    if (offsets) std::memcpy(offsets, r->offsets.data(), r->offsets.size() * 8);
+    if (values && !r->values.empty()) std::memcpy(values, r->values.data(), r->values.size());
+    if (n_contigs && !r->n_contigs.empty()) std::memcpy(n_contigs, r->n_contigs.data(), r->n_contigs.size() * 8);
+    return ROGTK_OK;
+}
+
+int rogtk_assembly_result_free(void* result) {
+    delete static_cast<AssemblyResult*>(result);
+    return ROGTK_OK;
 }
 
 }  // extern "C"

@@ -40,7 +40,8 @@ const char* const kKernelNames[K_COUNT_] = {
     "bam_fields",     "bam_scan",       "bam_fill",      "pack_reads",
     "row_gather",     "kmer_lds",      "cluster_resolve", "kmer_minimizer",
     "k_slice_bucket", "k_slice_mark",  "k_or_partials",  "k_scan_rt",
-    "k_local_cc",     "k_hook_g",      "k_jump",         "k_roots_check", "k_word_label"};
+    "k_local_cc",     "k_hook_g",      "k_jump",         "k_roots_check", "k_word_label",
+    "pack_gather",    "kmer_wave"};
 
 namespace {
 std::atomic<bool> g_prof{false};

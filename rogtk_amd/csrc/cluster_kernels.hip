@@ -2212,20 +2212,39 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_mark(const uint32_t* __re
         r0 = (int64_t)b0 * bucket_rows;
         r1 = min(n, (int64_t)b1 * bucket_rows);
         if (!__syncthreads_or(over)) {
-            // one wave per segment: 256 codes per pass of 16-B loads
+            // a wave takes kSegInFlight segments at a time (256 codes of each per pass of 16-B
+            // loads), all their loads in flight before the LDS atomics: one segment at a time
+            // left a wave ~2 dependent HBM round trips per segment (~10 segments per wave at
+            // 10M rows, ~60 at 62.5M: the C4 rank's 736 us, round 6)
+            constexpr int kSegInFlight = 8;
+            constexpr int kWaves = kSliceBlock / 64;
             const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-            for (int b = b0 + wave; b < b1; b += kSliceBlock / 64) {
-                const uint32_t len = seglen[(int64_t)sl * nbuckets + b];
-                const uint32_t* seg = segs + ((int64_t)sl * nbuckets + b) * seg_cap;
-                for (uint32_t i = 4 * lane; i < len; i += 256) {
-                    const uint4 v = *reinterpret_cast<const uint4*>(seg + i);
-                    const uint32_t cc[4] = {v.x, v.y, v.z, v.w};
+            for (int bb = b0 + wave; bb < b1; bb += kWaves * kSegInFlight) {
+                uint32_t len[kSegInFlight];
+                uint32_t mx = 0;
 #pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        if (i + k < len) {
-                            const uint32_t bb = cc[k] & smask;
-                            atomicOr(&sbits[bb >> 5], 1u << (bb & 31));
-                        }
+                for (int u = 0; u < kSegInFlight; ++u) {
+                    const int b = bb + u * kWaves;
+                    len[u] = b < b1 ? seglen[(int64_t)sl * nbuckets + b] : 0u;
+                    mx = max(mx, len[u]);
+                }
+                for (uint32_t i = 4 * lane; i < mx; i += 256) {
+                    uint4 v[kSegInFlight];
+#pragma unroll
+                    for (int u = 0; u < kSegInFlight; ++u) {
+                        const uint32_t* seg = segs + ((int64_t)sl * nbuckets + bb + u * kWaves) * seg_cap;
+                        v[u] = i < len[u] ? *reinterpret_cast<const uint4*>(seg + i) : make_uint4(0, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int u = 0; u < kSegInFlight; ++u) {
+                        const uint32_t cc[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                        for (int k = 0; k < 4; ++k)
+                            if (i + k < len[u]) {
+                                const uint32_t b2 = cc[k] & smask;
+                                atomicOr(&sbits[b2 >> 5], 1u << (b2 & 31));
+                            }
+                    }
                 }
             }
             r1 = r0;  // no row pass

@@ -1525,6 +1525,355 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
 #endif
 }
 
+// ------------------------------------------------------ wave-per-group path (round 6)
+// Class 2 (k_eff <= 16, <= 64 rows, <= kWaveWords packed words): ONE wave per group, with
+// a wave-private LDS hash table and no workgroup barrier. The workgroup kernel above holds
+// 8 waves per group through barrier-separated phases in which most waves idle (a C3 group
+// at k_eff 16: ~1,650 observations, ~157 valid k-mers, ~30k clocks per group); here each
+// wave runs its own group start to end, so the CU interleaves up to 12 groups' inserts.
+//   * slot = key << 32 | count << 8 | exts (k_eff <= 16: 32-bit keys); empty = key bits all
+//     ones with count 0 (a real entry has count >= 1, so the all-T key needs no special slot);
+//   * insert: one 64-bit CAS claims an empty slot or returns the owner; a repeat whose
+//     extension bits are already set is a non-returning 64-bit add of 1 << 8, else a CAS loop
+//     (the observations of one trip are consecutive positions: distinct k-mers, few retries);
+//   * the observations of a group are dealt flat over the lanes (lane l of trip t takes
+//     observation 64 t + l of the group, walking the rows' observation counts), so a 135-k-mer
+//     row costs 2.1 trips instead of 3;
+//   * CountFilter: a scan of the table compacts the valid entries (ballot prefix) into the
+//     words' LDS (the words are dead by then); a rank sort (each lane counts the keys below
+//     its entries, every lane reading the same 16 B at once) gives each entry its output
+//     place; censoring probes the table itself; terminal / isolated counts by ballots.
+// A group with more than kWaveClaim distinct or kWaveValid valid k-mers moves to class 3
+// (launched after this kernel): the outputs never depend on the path.
+// The next group's descriptor and packed words are loaded into registers while the current
+// group is processed (the descriptor two groups ahead), so a group waits on HBM only when
+// its chunk of 64 groups starts.
+#ifndef ROGTK_KMER_WAVE
+#define ROGTK_KMER_WAVE 1  // 0: no class 2 (experiment builds: the workgroup kernels take every group)
+#endif
+constexpr bool kWavePath = ROGTK_KMER_WAVE;
+constexpr int kWaveSlots = 1024;   // table slots per wave (8 KB)
+constexpr int kWaveClaim = 768;    // distinct k-mers (the table stays <= 75% + one trip full)
+constexpr int kWaveRows = 64;      // one row per lane
+constexpr int kWaveWords = 192;    // packed words (38 rows of <= 160 bases at stride 5)
+constexpr int kWaveValid = 512;    // valid k-mers (compacted to the table's front; keys bucketed behind them)
+constexpr int kWaveWG = 2;         // waves per workgroup (24.5 KB of LDS: 6 workgroups per CU)
+constexpr int kWaveWPL = (kWaveWords + 63) / 64;  // prefetched words per lane
+constexpr unsigned long long kWEmpty = 0xFFFFFFFF00000000ull;
+
+__device__ __forceinline__ void wave_lds_sync() {  // the wave's LDS writes before its reads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t wave_hash(uint32_t key) {
+    // xor-fold + one 24-bit multiply (full rate; a 32-bit mul_lo is quarter rate, and this
+    // kernel is bound by issue): k-mers of consecutive positions are shifts of each other
+    const uint32_t x = key ^ (key >> 14) ^ (key >> 25);
+    return (__umul24(x & 0xFFFFFFu, 0x9E3779u) >> 12) & (kWaveSlots - 1);
+}
+
+__global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_kmer_wave(const GroupDesc* __restrict__ gdesc, int64_t G,
+                                                           uint8_t* __restrict__ gsmall, int K, int64_t min_cov,
+                                                           const int32_t* __restrict__ row_len,
+                                                           const int64_t* __restrict__ woff, int stride,
+                                                           const uint64_t* __restrict__ packed,
+                                                           const int64_t* __restrict__ cap_off,
+                                                           uint64_t* __restrict__ t_kmer, uint8_t* __restrict__ t_ext,
+                                                           uint16_t* __restrict__ t_cnt, int64_t* __restrict__ gcount,
+                                                           unsigned long long* __restrict__ gstat) {
+    constexpr int kBuf = kWaveWords;
+    static_assert(kWaveValid * 8 + kWaveValid * 4 <= kWaveSlots * 8, "entries + bucketed keys fit the table");
+    __shared__ unsigned long long s_tab[kWaveWG][kWaveSlots];
+    __shared__ __attribute__((aligned(16))) uint64_t s_buf[kWaveWG][kBuf + 2];
+    __shared__ uint32_t s_cnt[kWaveWG][64];  // the rank sort's bucket counts
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    unsigned long long* const T = s_tab[wv];
+    uint64_t* const W = s_buf[wv];
+    uint32_t* const C = s_cnt[wv];
+    const uint32_t kmask = K >= 16 ? 0xFFFFFFFFu : (1u << (2 * K)) - 1u;
+    const int bsh = 2 * K >= 6 ? 2 * K - 6 : 0;  // the rank sort's bucket: the key's top 6 bits
+    for (int i = lane; i < kWaveSlots; i += 64) T[i] = kWEmpty;
+    const int64_t n_chunks = (G + 63) >> 6;
+    const int64_t nw = (int64_t)gridDim.x * kWaveWG;
+    int64_t ch = (int64_t)blockIdx.x * kWaveWG + wv;
+    uint64_t own = ch < n_chunks ? __ballot((ch << 6) + lane < G && gsmall[(ch << 6) + lane] == 2) : 0ull;
+    // the next group of this class for this wave (-1: none); loads the chunk's classes as needed
+    auto next_group = [&]() -> int64_t {
+        while (true) {
+            if (own) {
+                const int i = __ffsll((unsigned long long)own) - 1;
+                own &= own - 1;
+                return (ch << 6) + i;
+            }
+            ch += nw;
+            if (ch >= n_chunks) return -1;
+            own = __ballot((ch << 6) + lane < G && gsmall[(ch << 6) + lane] == 2);
+        }
+    };
+    // prefetch state of the next group: its row (lane) and packed words in registers
+    int32_t p_len = 0, p_wo = 0;
+    uint64_t p_words[kWaveWPL];
+    auto load_group = [&](const GroupDesc& dd) {
+        p_len = 0;
+        p_wo = 0;
+        if (lane < dd.nrows) {
+            p_len = row_len[dd.r0 + lane];
+            p_wo = stride ? lane * stride : (int32_t)(woff[dd.r0 + lane] - dd.w0);
+        }
+#pragma unroll
+        for (int j = 0; j < kWaveWPL; ++j) {
+            const int i = lane + 64 * j;
+            p_words[j] = i < dd.nwords ? packed[dd.w0 + i] : 0ull;
+        }
+    };
+    // descriptors by a VECTOR load (lane k < 6 takes dword k, readlane after): a scalar load
+    // would share lgkmcnt with the LDS operations, and every LDS wait of the group before it
+    // would wait for the prefetch too
+    auto desc_load = [&](int64_t gg) -> uint32_t {
+        return gg >= 0 && lane < 6 ? reinterpret_cast<const uint32_t*>(gdesc + gg)[lane] : 0u;
+    };
+    auto desc_get = [&](uint32_t dw) -> GroupDesc {
+        GroupDesc o;
+        o.r0 = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dw, 1) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)dw, 0));
+        o.w0 = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dw, 3) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)dw, 2));
+        o.nrows = __builtin_amdgcn_readlane((int)dw, 4);
+        o.nwords = __builtin_amdgcn_readlane((int)dw, 5);
+        return o;
+    };
+    static_assert(sizeof(GroupDesc) == 24, "GroupDesc: 6 dwords");
+    int64_t g = next_group();
+    GroupDesc d = desc_get(desc_load(g));
+    if (g >= 0) load_group(d);
+    int64_t g1 = g >= 0 ? next_group() : -1;
+    uint32_t dw1 = desc_load(g1);
+#ifdef ROGTK_KMER_TIMING
+    const int tid = lane;
+    unsigned long long kt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, kt_last = wall_clock64();
+#endif
+    for (; g >= 0;) {
+        const int nrows = d.nrows, nwords = d.nwords;
+        // this group's rows: lane r holds row r's observation count, length and word offset
+        const int c_len = p_len, c_wo = p_wo;
+        const int c_nobs = lane < nrows && c_len ? max(c_len - K + 1, 0) : 0;
+#pragma unroll
+        for (int j = 0; j < kWaveWPL; ++j) {
+            const int i = lane + 64 * j;
+            if (i < nwords) W[i] = p_words[j];
+        }
+        if (lane == 0) W[nwords] = 0;  // the second word of a k-mer in the last word
+        wave_lds_sync();
+        // the next group's rows and words in flight while this group is processed, and the
+        // descriptor of the one after it
+        GroupDesc d1{0, 0, 0, 0};
+        if (g1 >= 0) {
+            d1 = desc_get(dw1);
+            load_group(d1);
+        }
+        const int64_t g2 = g1 >= 0 ? next_group() : -1;
+        const uint32_t dw2 = desc_load(g2);
+        KT(0);
+        // inserts, one pass: lane task = (row, segment), spr = floor(64 / rows) segments
+        // per row of Ls = ceil(longest / spr) positions (a C3 group of ~12 rows of 135
+        // observations: 60 lanes of 27 steps). Each lane starts its segment at a rotation of
+        // its row (7 r mod its length) and wraps, so the rows' lanes - copies of one template -
+        // insert different k-mers in a step instead of all hitting one slot
+        int maxn = c_nobs;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) maxn = max(maxn, __shfl_xor(maxn, m));
+        const int spr = nrows > 0 ? max(1, 64 / nrows) : 1;
+        const int Ls = (maxn + spr - 1) / spr;
+        const int r = lane / spr;
+        const int seg = lane - r * spr;
+        const int rs = r < nrows ? r : 0;
+        const int nobs_r = __shfl(c_nobs, rs), len_r = __shfl(c_len, rs), wo_r = __shfl(c_wo, rs);
+        const int pst = seg * Ls;
+        const int nst = r < nrows ? min(max(nobs_r - pst, 0), Ls) : 0;
+        const int rot = nst > 0 ? (7 * r) % nst : 0;
+        // the base before the segment (left extension of its first k-mer) and the one before
+        // the rotated start: later steps take the previous k-mer's first base
+        auto base_at = [&](int q) -> uint32_t {  // base q of the lane's row (q >= 0)
+            return (uint32_t)(W[wo_r + (q >> 5)] >> (62 - 2 * (q & 31))) & 3u;
+        };
+        const uint32_t wrapb = nst > 0 && pst > 0 ? base_at(pst - 1) : 0u;
+        uint32_t prevb = nst > 0 && pst + rot > 0 ? base_at(pst + rot - 1) : 0u;
+        uint32_t claims = 0;
+        bool over = false;
+        for (int t = 0; t < Ls; ++t) {
+            const bool act = t < nst;
+            int j = t + rot;
+            j -= j >= nst ? nst : 0;
+            const int p = pst + j;
+            bool fresh = false;
+            if (act) {
+                const int wi = wo_r + (p >> 5);
+                const uint64_t w0 = W[wi], w1 = W[wi + 1];
+                const int o = 2 * (p & 31);
+                const uint64_t win = o ? (w0 << o) | (w1 >> (64 - o)) : w0;
+                const uint32_t key = (uint32_t)(win >> (64 - 2 * K)) & kmask;
+                const uint32_t lb = j == 0 ? wrapb : prevb;
+                uint32_t e = p > 0 ? 1u << lb : 0u;
+                if (p + K < len_r) e |= 1u << (4 + ((uint32_t)(win >> (62 - 2 * K)) & 3u));
+                prevb = (uint32_t)(win >> 62);
+                uint32_t h = wave_hash(key);
+                const unsigned long long mine = ((unsigned long long)key << 32) | (1ull << 8) | e;
+#if defined(ROGTK_WAVE_EXP) && ROGTK_WAVE_EXP == 1
+                T[h] = mine;  // (timing experiment: no atomics)
+                fresh = (h & 7) == 0;
+                if (true) continue;
+#endif
+#if defined(ROGTK_WAVE_EXP) && ROGTK_WAVE_EXP == 2
+                if (h != 0xFFFFFFFFu) continue;  // (timing experiment: no table access)
+#endif
+                unsigned long long v;
+                while (true) {
+                    v = atomicCAS(&T[h], kWEmpty, mine);
+                    if (v == kWEmpty || (uint32_t)(v >> 32) == key) break;
+                    h = (h + 1) & (kWaveSlots - 1);
+                }
+                fresh = v == kWEmpty;
+                if (!fresh) {
+                    if ((e & ~(uint32_t)v & 0xFFu) == 0) {
+                        atomicAdd(&T[h], 1ull << 8);  // no new extension: count only
+                    } else {
+                        while (true) {
+                            const unsigned long long w2 = atomicCAS(&T[h], v, (v + (1ull << 8)) | e);
+                            if (w2 == v) break;
+                            v = w2;
+                        }
+                    }
+                }
+            }
+            claims += (uint32_t)__popcll(__ballot(fresh));
+            if (claims > (uint32_t)kWaveClaim) {
+                over = true;
+                break;
+            }
+        }
+        wave_lds_sync();
+        KT(1);
+        // CountFilter: the valid entries compacted IN PLACE to the front of the table (key << 32 |
+        // count | exts << 16; a chunk's 64 slots are read before any entry is written, and entries
+        // only move down); the table is rebuilt empty after the group, and the censoring below
+        // looks neighbours up in the bucketed keys instead of the hash table
+        uint32_t nv = 0;
+        if (!over) {
+            for (int s0 = 0; s0 < kWaveSlots; s0 += 64) {
+                const unsigned long long v = T[s0 + lane];
+                const uint32_t cnt = (uint32_t)(v >> 8) & 0xFFFFFFu;
+                const bool ok = v != kWEmpty && (int64_t)min(cnt, 0xFFFFu) >= min_cov;
+                const uint64_t bm = __ballot(ok);
+                const uint32_t at = nv + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
+                if (ok && at < (uint32_t)kWaveValid)
+                    T[at] = (v & 0xFFFFFFFF00000000ull) | min(cnt, 0xFFFFu) | ((uint64_t)(v & 0xFFu) << 16);
+                nv += (uint32_t)__popcll(bm);
+            }
+            if (nv > (uint32_t)kWaveValid) over = true;
+        }
+        uint32_t term = 0, iso = 0;
+        if (!over && nv > 0) {
+            // rank sort by buckets: the key's top 6 bits pick one of 64 buckets, an LDS atomic
+            // gives each entry its place in its bucket (kept in the entry's bits 24..31), a wave
+            // scan the buckets' starts; the bucketed keys K2 (behind the entries) give an
+            // entry's rank (its bucket's start + the keys of its bucket below it) and the
+            // censoring's neighbour lookups (a valid neighbour is one of K2's keys)
+            uint32_t* const K2 = reinterpret_cast<uint32_t*>(T + kWaveValid);
+            C[lane] = 0;
+            wave_lds_sync();
+            KT(2);
+            bool deep = false;  // a bucket past 255 entries (adversarial keys): class 3
+            for (uint32_t i = lane; i < nv; i += 64) {
+                const unsigned long long v = T[i];
+                const uint32_t li = atomicAdd(&C[(uint32_t)(v >> 32) >> bsh & 63u], 1u);
+                deep |= li > 255u;
+                T[i] = v | ((unsigned long long)min(li, 255u) << 24);
+            }
+            if (__ballot(deep)) {
+                over = true;
+            } else {
+                wave_lds_sync();
+                const uint32_t bc = C[lane];
+                uint32_t incl = bc;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const uint32_t t = __shfl_up(incl, off);
+                    if (lane >= off) incl += t;
+                }
+                const uint32_t bstart = incl - bc;
+                for (uint32_t i = lane; i < nv; i += 64) {
+                    const unsigned long long v = T[i];
+                    const uint32_t b = (uint32_t)(v >> 32) >> bsh & 63u;
+                    K2[(uint32_t)__shfl((int)bstart, (int)b) + ((uint32_t)(v >> 24) & 0xFFu)] = (uint32_t)(v >> 32);
+                }
+                wave_lds_sync();
+                KT(3);
+                const int64_t base = cap_off[g];
+                for (uint32_t i0 = 0; i0 < nv; i0 += 64) {
+                    const uint32_t i = i0 + lane;
+                    const bool live = i < nv;
+                    const unsigned long long v = live ? T[i] : 0ull;
+                    const uint32_t key = (uint32_t)(v >> 32);
+                    const uint32_t b = key >> bsh & 63u;
+                    const uint32_t at = (uint32_t)__shfl((int)bstart, (int)b), bn = (uint32_t)__shfl((int)bc, (int)b);
+                    bool tm = false, is = false;
+                    if (live) {
+                        uint32_t rank = at;
+                        for (uint32_t m = 0; m < bn; ++m) rank += K2[at + m] < key;
+                        const uint32_t ex = (uint32_t)(v >> 16) & 0xFFu;
+                        uint32_t nx = 0;
+                        for (int bit = 0; bit < 8; ++bit) {
+                            if (!((ex >> bit) & 1u)) continue;
+                            const uint32_t bb = (uint32_t)(bit & 3);
+                            const uint32_t nb = bit < 4 ? (key >> 2) | (bb << (2 * K - 2)) : ((key << 2) | bb) & kmask;
+                            const uint32_t b2 = nb >> bsh & 63u;
+                            const uint32_t a2 = (uint32_t)__shfl((int)bstart, (int)b2),
+                                           n2 = (uint32_t)__shfl((int)bc, (int)b2);
+                            for (uint32_t m = 0; m < n2; ++m)
+                                if (K2[a2 + m] == nb) {
+                                    nx |= 1u << bit;
+                                    break;
+                                }
+                        }
+                        const int64_t o = base + rank;
+                        t_kmer[2 * o] = 0;
+                        t_kmer[2 * o + 1] = key;
+                        t_ext[o] = (uint8_t)nx;
+                        t_cnt[o] = (uint16_t)(v & 0xFFFFu);
+                        const bool l0 = (nx & 0xFu) == 0, r0b = (nx >> 4) == 0;
+                        tm = l0 || r0b;
+                        is = l0 && r0b;
+                    }
+                    term += (uint32_t)__popcll(__ballot(tm));
+                    iso += (uint32_t)__popcll(__ballot(is));
+                }
+            }
+        }
+        if (over && lane == 0) gsmall[g] = 3;  // more than the wave path takes: class 3 (launched next) redoes it
+        KT(4);
+        if (lane == 0 && !over) {
+            gcount[g] = nv;
+            gstat[5 * g + 3] = term;
+            gstat[5 * g + 4] = iso;
+        }
+        wave_lds_sync();
+        for (int i = lane; i < kWaveSlots; i += 64) T[i] = kWEmpty;
+        wave_lds_sync();
+        KT(5);
+        g = g1;
+        d = d1;
+        g1 = g2;
+        dw1 = dw2;
+    }
+#ifdef ROGTK_KMER_TIMING
+    KT(6);
+    if (lane == 0)
+        for (int k = 0; k < 8; ++k) atomicAdd(&g_kmer_clk[k], kt_acc[k]);
+#endif
+}
+
 // Per group of effective k K: observation, row and packed-word totals decide the path.
 // 16 lanes per group (a C3 group has ~10 rows: a wave per group left most lanes idle);
 // caps != NULL: also the group's output capacity (valid_cap of its observations)
@@ -1539,7 +1888,7 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
                                                            const int64_t* __restrict__ woff, int stride,
                                                            uint8_t* __restrict__ gsmall, GroupDesc* __restrict__ gdesc,
                                                            int64_t* __restrict__ caps, int64_t min_cov,
-                                                           const unsigned long long* __restrict__ gstat = nullptr) {
+                                                           const unsigned long long* __restrict__ gstat, int wave) {
     const int sub = threadIdx.x & (kClsLanes - 1);
     const int64_t step = (int64_t)gridDim.x * (kBlock / kClsLanes);
     // every segment of a wave runs the same number of trips (the shuffles need the lanes)
@@ -1576,7 +1925,8 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
         if (K <= 32 && obs > 0 && empty) {
             cls = kClsEmpty;
         } else if (K <= 32 && obs > 0) {
-            if (nrows <= LdsCfg<3>::kRows && words <= LdsCfg<3>::kWords) cls = 3;
+            if (wave && K <= 16 && nrows <= kWaveRows && words <= kWaveWords) cls = 2;
+            else if (nrows <= LdsCfg<3>::kRows && words <= LdsCfg<3>::kWords) cls = 3;
             else if (nrows <= LdsCfg<1>::kRows && words <= LdsCfg<1>::kWords) cls = 1;
             else if (nrows <= LdsCfg<4>::kRows && words <= LdsCfg<4>::kWords) cls = 4;
         }
@@ -2109,9 +2459,26 @@ struct KmerCtx {
     DevBuf v_lo, v_hi, v_grp, v_ext, v_cnt, t_kmer, t_ext, t_cnt, o_kmer, o_ext, o_cnt, cub, gsmall, caps, scal;
     DevBuf long_rows;  // block path: grouped rows longer than the staging stride (an error)
     bool lds_path = true;  // rogtk_kmer_set_path(): tests force the global path
+    bool wave_path = true;  // rogtk_kmer_set_path(2): the LDS path without class 2 (tests)
     int64_t last_lds_groups = 0, last_global_groups = 0;  // rogtk_kmer_path_stats()
     int64_t last_cert_groups = 0;                         // rogtk_kmer_certified_groups()
     int64_t last_lds_rows = 0;                            // rogtk_kmer_lds_rows()
+    // the retired allocations of every buffer; a device-wide sync first when there are any
+    // (an earlier call's kernels may still read them on another stream; buffers regrow only
+    // while the calls' sizes grow, so steady-state calls find nothing to free)
+    void reclaim() {
+        DevBuf* const all[] = {&offsets, &values, &validity, &go, &gk, &cap_off, &gstat, &gstart, &gcount, &out_off,
+                               &row_group, &row_obs, &obs_off, &row_len, &row_words, &woff, &packed, &row_st,
+                               &raw_len, &gdesc, &key_lo, &key_hi, &ext, &grp, &idx, &perm_a, &perm_b, &tmp_u64,
+                               &tmp_u32, &s_lo, &s_hi, &s_ext, &s_grp, &head, &rid, &r_valid, &r_first, &r_ext,
+                               &r_cnt, &vpos, &v_lo, &v_hi, &v_grp, &v_ext, &v_cnt, &t_kmer, &t_ext, &t_cnt,
+                               &o_kmer, &o_ext, &o_cnt, &cub, &gsmall, &caps, &scal, &long_rows};
+        bool any = false;
+        for (DevBuf* b : all) any |= !b->retired.empty();
+        if (!any) return;
+        (void)hipDeviceSynchronize();
+        for (DevBuf* b : all) b->reclaim();
+    }
     ~KmerCtx() {
         if (stream) hipStreamDestroy(stream);
     }
@@ -2208,7 +2575,7 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
     if (in.fused) {
         // round 5: packed from the ASCII bytes in group order (k_pack_gather), no block column
         if (int rc = c->packed.ensure((size_t)std::max<int64_t>(n_rows * stride, 1) * 8)) return rc;
-        ProfScope prof(K_ROW_GATHER, s, true);
+        ProfScope prof(K_PACK_GATHER, s, true);
         const int pgrid = (int)std::min<int64_t>((n_rows + 63) / 64, (int64_t)8192 * 256 / 64);
 #define ROGTK_PG(NW)                                                                                              \
     hipExtLaunchKernelGGL(k_pack_gather<NW>, dim3(pgrid), dim3(64), 0, s, prof.start(), prof.stop(), 0, in.offsets,  \
@@ -2260,7 +2627,7 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
         hipLaunchKernelGGL(k_group_classify, dim3(grid_for(G * kClsLanes, 16384)), dim3(kBlock), 0, s, go, G, in.gk,
                            K, c->row_obs.as<int64_t>(), c->row_words.as<int64_t>(), c->woff.as<int64_t>(), stride,
                            c->gsmall.as<uint8_t>(), c->gdesc.as<GroupDesc>(), in.cap_fill, min_cov,
-                           stride && kmer_cert_on() ? gstat : nullptr);
+                           stride && kmer_cert_on() ? gstat : nullptr, (int)(kWavePath && c->wave_path && K <= 16));
     } else if (in.cap_fill) {
         hipLaunchKernelGGL(k_group_caps_obs, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, go, G,
                            c->row_obs.as<int64_t>(), min_cov, in.cap_fill);
@@ -2279,6 +2646,14 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
                               c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(), stride,
                               c->packed.as<uint64_t>(), gstat, g_mz_debug_groups >= G ? g_mz_debug : nullptr);
         ROGTK_HIP_CHECK(hipGetLastError());
+    }
+    if (lds && kWavePath && c->wave_path && K <= 16) {
+        // class 2 first: its overflowing groups become class 3 for the launch below
+        const int64_t chunks = (G + 63) / 64;
+        ROGTK_TIMED_LAUNCH(K_KMER_WAVE, k_kmer_wave, dim3((unsigned)std::min<int64_t>((chunks + kWaveWG - 1) / kWaveWG, 65536)),
+                           dim3(64 * kWaveWG), 0, s, c->gdesc.as<GroupDesc>(), G, c->gsmall.as<uint8_t>(), K, min_cov,
+                           c->row_len.as<int32_t>(), c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(), in.cap_off,
+                           c->t_kmer.as<uint64_t>(), c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
     }
     if (lds) {
         ProfScope prof(K_KMER_LDS, s, true);
@@ -2312,6 +2687,7 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
     int64_t last[6] = {0, 0, 0, 0, 0, 0};
     ROGTK_HIP_CHECK(hipMemcpyAsync(&last[2], c->scal.p, 32, hipMemcpyDeviceToHost, s));
     ROGTK_HIP_CHECK(hipStreamSynchronize(s));
+    c->reclaim();
     c->last_lds_groups += last[2];
     c->last_global_groups += last[3];
     c->last_cert_groups += last[4];
@@ -2439,6 +2815,7 @@ int rogtk_kmer_set_path(int lds_small_groups) {
     KmerCtx* c = nullptr;
     if (int rc = kmer_ctx(&c)) return rc;
     c->lds_path = lds_small_groups != 0;
+    c->wave_path = lds_small_groups == 1;
     return ROGTK_OK;
 }
 

@@ -66,6 +66,10 @@ enum KernelId {
     K_K_JUMP,
     K_K_ROOTS,
     K_K_WORD_LABEL,
+    // round 6: the fused pack + grouped staging of C3 (was timed as K_ROW_GATHER) and the
+    // wave-per-group k-mer kernel
+    K_PACK_GATHER,
+    K_KMER_WAVE,
     K_COUNT_
 };
 extern const char* const kKernelNames[K_COUNT_];
@@ -303,6 +307,13 @@ struct DevBuf {
         ROGTK_HIP_CHECK(hipMalloc(&p, want));
         cap = want;
         return ROGTK_OK;
+    }
+    // Frees the outgrown allocations (a long-lived context otherwise keeps up to
+    // ~2x its live buffers in HBM). Only where the caller has synchronised every stream that
+    // used them (hipFree does not wait for kernels still reading them).
+    void reclaim() {
+        for (void* q : retired) hipFree(q);
+        retired.clear();
     }
     template <class T>
     T* as() const { return reinterpret_cast<T*>(p); }

@@ -31,6 +31,8 @@ wait for batch k-1's flags moves onto the critical cycle: 0.487 vs 0.430 ms/step
 """
 from __future__ import annotations
 
+import os
+
 from collections import deque
 from typing import Optional
 
@@ -162,6 +164,11 @@ class UmiPipeline:
         # so it overlaps the previous batch's resolve instead of lengthening the resolve
         # stream's chain (a substituted exchange may reuse one buffer: it stays in line)
         self.s_comm = torch.cuda.Stream(dev) if exchange is None and dist_collective(group) else None
+        if self.s_comm is not None:
+            #  with a comm stream the split mark would hold batch k's all-gather
+            # behind resolve(k - 1) (phase 2 sits on the resolve stream): the whole mark stays
+            # on the main stream, so the all-gather overlaps the previous resolve
+            self.split_mark = False
         self.last_scored: Optional[torch.cuda.Event] = None
         self.k = 0
         self.last_assigned: Optional[torch.cuda.Event] = None
@@ -261,6 +268,13 @@ class UmiPipeline:
     def _event(self):
         return D.StreamEvent() if self.device_events else torch.cuda.Event()
 
+    def _attach_event(self):
+        """An event recorded by a kernel's own dispatch packet (the split mark's bucket pass,
+        the resolve's last kernel), which another stream waits for."""
+        if not self.device_events:
+            return torch.cuda.Event()
+        return D.StreamEvent(device_scope=os.environ.get("ROGTK_ATTACH_SYS", "0") != "1")
+
     def _score(self, slot: _Slot, batch: D.PackedBatch):
         D.score_packed(batch, slot.scores, self.target, self.max_hamming, slot.dist, slot.within, stream=self.main)
         if self.score_alone and self.s_assign is not self.main:
@@ -274,13 +288,16 @@ class UmiPipeline:
         if (gate_resolve or ms is not self.main) and slot.resolved is not None:
             D.wait_for(ms, slot.resolved)  # the previous resolve read the bitmap
         if self.split_mark:  # phase 2 runs at the head of the resolve (_resolve)
-            marked = self._event()
+            marked = self._attach_event()
             if isinstance(marked, D.StreamEvent):
                 # the bucket pass's own dispatch packet records the event (no marker packet
-                # between it and the score kernel)
+                # between it and the score kernel); disarmed whatever happens
                 marked.attach_next()
-                slot.eng.mark_bitmap(batch, stream=ms, phase=1)
-                if not marked.attach_done():
+                try:
+                    slot.eng.mark_bitmap(batch, stream=ms, phase=1)
+                finally:
+                    taken = marked.attach_done()
+                if not taken:
                     marked.record(ms)
             else:
                 slot.eng.mark_bitmap(batch, stream=ms, phase=1)
@@ -326,12 +343,15 @@ class UmiPipeline:
                 bitmaps.record_stream(sr)  # allocated on the comm stream
             else:
                 bitmaps, nb = self.exchange(slot.eng.local_bitmap)
-            resolved = self._event()
+            resolved = self._attach_event()
             if isinstance(resolved, D.StreamEvent):
                 # recorded on the resolve's last kernel's dispatch packet
                 resolved.attach_next()
-                slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr)
-                if not resolved.attach_done():
+                try:
+                    slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr)
+                finally:
+                    taken = resolved.attach_done()
+                if not taken:
                     resolved.record(sr)
             else:
                 slot.eng.resolve(bitmaps, nb, self.max_distance, stream=sr)

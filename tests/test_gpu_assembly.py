@@ -125,3 +125,55 @@ def test_method_errors(rg):
         rg.assemble_sequences(_col(REF_SEQS), 13, 1, "bogus")
     got = rg.assemble_sequences_with_anchors(_col(REF_SEQS), ["GAGACTGCATGG"], ["TTTAGTGAGGGT"], k=13, min_coverage=1)
     assert got == "GAGACTGCATGGGCTGGTGGGCGTCCGTCTGCTTTAGTGAGGGT"
+
+
+def _c3_groups(n, seed_rows=None):
+    """n synth-v1 150-bp reads with 12-bp UMIs on the device, their exact H3 ids (the
+    caller's group_by('umi'), rogtk/__init__.py:206-214)."""
+    import torch
+
+    from rogtk_amd import device as D
+    from rogtk_amd import synth
+
+    codes = torch.from_numpy(synth.umi_codes(n, 12).view(np.int32)).cuda()
+    reads_h = synth.reads(n, 150)
+    values = torch.from_numpy(reads_h.reshape(-1)).cuda()
+    offsets = torch.arange(0, (n + 1) * 150, 150, dtype=torch.int64, device="cuda")
+    eng = D.ClusterEngine(12, min(n, 4 ** 12), "cuda")
+    cid = torch.empty(n, dtype=torch.int32, device="cuda")
+    D.cluster_batch(eng, D.PackedBatch(codes, 12), cid, 0)
+    return reads_h, values, offsets, cid
+
+
+@pytest.mark.parametrize("k,mc,method,n,sample", [(15, 5, "compression", 1_000_000, 2000),
+                                                  (10, 5, "shortest_path_auto", 200_000, 400),
+                                                  (17, 3, "compression", 200_000, 400)])
+def test_batched_groups_match_per_group(rg, k, mc, method, n, sample):
+    """Round 6, batched H5 (rogtk_assemble_groups_host over a whole group_spectra result):
+    every group's string identical to the per-group rogtk_assemble_host call (its own GPU
+    spectrum at min_coverage 0, CountFilter + censoring on the host) on a sample of the C3
+    groups (the largest ones included), and to the Python restatement on a smaller one."""
+    import torch
+
+    from rogtk_amd import assembly as AS
+
+    reads_h, values, offsets, cid = _c3_groups(n)
+    rows, go, arr, nc = AS.assemble_column_groups(offsets, values, cid, k, mc, method)
+    torch.cuda.synchronize()
+    G = len(go) - 1
+    assert len(arr) == G and len(nc) == G
+    rows_h, goh = rows.cpu().numpy(), go.cpu().numpy()
+    sizes = np.diff(goh)
+    rng = np.random.default_rng(k + mc)
+    pick = np.unique(np.concatenate([rng.choice(G, size=sample, replace=False), np.argsort(sizes)[-50:]]))
+    got = arr.to_pylist()
+    nonempty = 0
+    for j, g in enumerate(pick):
+        items = [bytes(reads_h[r]) for r in rows_h[goh[g]:goh[g + 1]]]
+        want = rg.assemble_sequences(_col(items), k, mc, method)
+        assert got[g] == want, (g, len(items))
+        assert nc[g] == (want.count("\n") + 1 if want else 0)
+        nonempty += bool(want)
+        if j < 60:  # the Python restatement (only_largest, as the expression)
+            assert got[g] == "\n".join(A().assemble(items, k, mc, method, None, None, True, None, False)), g
+    assert nonempty > len(pick) // 2

@@ -9,7 +9,10 @@ groups, k = 17 -> effective 32, min_coverage 20 as rogtk/__init__.py:212) -> eve
 
 * 1M reads (~111k groups) plus injected groups that force every size class and hand-off:
   15 / 40 / 100 unrelated reads (distinct k-mers past class 3's and class 1's tables),
-  250 and 700 reads of one template (class 4 and the global radix path), compared in full.
+  250 and 700 reads of one template (class 4 and the global radix path), 3 / 4 clean
+  templates (the wave class's sort bound), compared in full; k_eff 8 / 16 / 32.
+* 100M reads at k = 15, min_coverage 5 (the reference's default, round 6): properties,
+  2,600 groups vs the oracle, digest against the path without the wave class.
 * 100M reads (the C3 configuration, 1 and 11 spectrum calls): size-independent properties
   over every group (n_sequences, node/terminal/isolated counts recomputed from the returned
   exts, counts >= min_coverage, ascending k-mers), the groups the minimizer filter decided
@@ -29,14 +32,22 @@ RL, UL, K, MINCOV = 150, 12, 17, 20
 THREADS = min(16, os.cpu_count() or 1)
 
 
+INJECT = ((15, "random"), (40, "random"), (100, "random"), (250, "template"), (700, "template"),
+          (18, "multi3"), (24, "multi4"), (64, "multi4"), (65, "template"))
+
+
 def _inject(reads, codes, rng):
-    """Overwrite rows with groups of chosen shapes (fresh UMI codes)."""
+    """Overwrite rows with groups of chosen shapes (fresh UMI codes): random rows (distinct
+    k-mers past the wave class's and class 3's / class 1's tables), one template (class 4, the
+    global radix path, and 65 rows: one past the wave class), and 3 / 4 templates of 6 clean
+    copies each (k_eff 16, min_coverage <= 6: ~405 / ~540 valid k-mers, the latter past the
+    wave class's 512-entry sort; 64 rows: the wave class's row bound)."""
     n = len(codes)
     acgt = np.frombuffer(b"ACGT", np.uint8)
-    rows = rng.choice(n, size=15 + 40 + 100 + 250 + 700, replace=False)
+    rows = rng.choice(n, size=sum(sz for sz, _ in INJECT), replace=False)
     at = 0
     used = set(np.unique(codes).tolist())
-    for size, kind in ((15, "random"), (40, "random"), (100, "random"), (250, "template"), (700, "template")):
+    for size, kind in INJECT:
         sel = rows[at:at + size]
         at += size
         c = int(rng.integers(0, 4 ** UL))
@@ -46,6 +57,10 @@ def _inject(reads, codes, rng):
         codes[sel] = c
         if kind == "random":
             reads[sel] = acgt[rng.integers(0, 4, size=(size, RL))]
+        elif kind.startswith("multi"):
+            tpls = acgt[rng.integers(0, 4, size=(int(kind[5:]), RL))]
+            for j, r in enumerate(sel):
+                reads[r] = tpls[j % len(tpls)]
         else:
             tpl = acgt[rng.integers(0, 4, size=RL + 60)]
             for j, r in enumerate(sel):
@@ -90,17 +105,19 @@ def _concat(calls, G):
             "group_offsets": np.concatenate(eo), "stats": np.concatenate(st)}
 
 
-@pytest.mark.parametrize("k,min_cov,batch_rows,packed,filt", [
-    (K, MINCOV, 10_000_000, "auto", 0), (K, 2, 200_000, "auto", 0), (K, MINCOV, 10_000_000, None, 0),
-    (K, 3, 200_000, "auto", 1), (K, MINCOV, 10_000_000, "blocks", 1),
+@pytest.mark.parametrize("k,min_cov,batch_rows,packed,filt,path", [
+    (K, MINCOV, 10_000_000, "auto", 0, 1), (K, 2, 200_000, "auto", 0, 1), (K, MINCOV, 10_000_000, None, 0, 1),
+    (K, 3, 200_000, "auto", 1, 1), (K, MINCOV, 10_000_000, "blocks", 1, 1),
     # the reference's defaults: k = 15 (docstring) and 10 (assemble_sequences), effective 16,
-    # min_coverage 5 (rogtk/__init__.py:106-107, 211-212)
-    (15, 5, 10_000_000, "auto", 1), (10, 5, 200_000, "blocks", 1)])
-def test_c3_path_1m_vs_oracle(k, min_cov, batch_rows, packed, filt):
+    # min_coverage 5 (rogtk/__init__.py:106-107, 211-212): the wave-per-group class (round 6),
+    # and the same without it (path 2: the workgroup kernels take those groups)
+    (15, 5, 10_000_000, "auto", 1, 1), (10, 5, 200_000, "blocks", 1, 1), (15, 5, 10_000_000, "auto", 1, 2),
+    (15, 3, 10_000_000, None, 1, 1), (7, 6, 10_000_000, "auto", 1, 1)])
+def test_c3_path_1m_vs_oracle(k, min_cov, batch_rows, packed, filt, path):
     """packed "auto" (150-bp rows: "fused"): rows packed from their ASCII bytes in group
     order with the certificate (rogtk_kmer_spectrum_fused); "blocks": staged from the 2-bit
     block column (rogtk_pack_reads); None: from the ASCII bytes without a certificate.
-    filt: with the minimizer filter (rogtk_kmer_set_filter)."""
+    filt: with the minimizer filter (rogtk_kmer_set_filter). path: rogtk_kmer_set_path."""
     from oracle import pyoracle as P
     from rogtk_amd import _lib
     from rogtk_amd import synth
@@ -111,12 +128,13 @@ def test_c3_path_1m_vs_oracle(k, min_cov, batch_rows, packed, filt):
     codes_h = synth.umi_codes(n, UL).copy()
     reads_h = synth.reads(n, RL).copy()
     _inject(reads_h, codes_h, rng)
-    _lib.call("rogtk_kmer_set_path", 1)
+    _lib.call("rogtk_kmer_set_path", path)
     _lib.call("rogtk_kmer_set_filter", filt)
     try:
         rows, go, G, calls = _run_c3(codes_h, reads_h, min_cov, batch_rows, packed, k)
     finally:
         _lib.call("rogtk_kmer_set_filter", 1)
+        _lib.call("rogtk_kmer_set_path", 1)
     ps = (ctypes.c_int64 * 2)()
     _lib.call("rogtk_kmer_path_stats", ps)
     order = np.argsort(codes_h, kind="stable")
@@ -131,10 +149,10 @@ def test_c3_path_1m_vs_oracle(k, min_cov, batch_rows, packed, filt):
     for f in ("kmer_hi", "kmer_lo", "exts", "counts"):
         assert np.array_equal(got[f], ref[f]), f
     assert G > 100_000 and len(calls) >= (1 if batch_rows >= n else 5)
-    assert (got["stats"][:, 0] == (16 if k <= 16 else 32)).all()
+    assert (got["stats"][:, 0] == (8 if k <= 8 else 16 if k <= 16 else 32)).all()
 
 
-def _props(calls, min_cov):
+def _props(calls, min_cov, k_eff=32):
     """Size-independent properties of one run; returns (sum n_sequences, groups, a digest)."""
     import torch
 
@@ -147,14 +165,14 @@ def _props(calls, min_cov):
         ex = r["exts"].cpu().numpy()
         cn = r["counts"].cpu().numpy().view(np.uint16)
         km = r["kmers"].cpu().numpy().view(np.uint64)
-        assert (st[:, 0] == 32).all()
+        assert (st[:, 0] == k_eff).all()
         assert np.array_equal(st[:, 2], np.diff(eo))  # node_count = entries
         l0, r0 = (ex & 0xF) == 0, (ex >> 4) == 0
         gid = np.repeat(np.arange(len(eo) - 1), np.diff(eo))
         assert np.array_equal(np.bincount(gid, weights=(l0 | r0), minlength=len(eo) - 1).astype(np.int64), st[:, 3])
         assert np.array_equal(np.bincount(gid, weights=(l0 & r0), minlength=len(eo) - 1).astype(np.int64), st[:, 4])
         assert (cn >= min_cov).all()
-        if len(km) > 1:  # ascending k-mers within a group (k_eff 32: the lo word)
+        if len(km) > 1:  # ascending k-mers within a group (k_eff <= 32: the lo word)
             same = gid[1:] == gid[:-1]
             assert (km[1:, 1][same] > km[:-1, 1][same]).all()
         nseq += int(st[:, 1].sum())
@@ -211,7 +229,7 @@ print("DIGEST " + json.dumps(list(m.c3_100m_digest())), flush=True)
 """
 
 
-def _oracle_groups(pick, rows_h, goh, values, n, calls):
+def _oracle_groups(pick, rows_h, goh, values, n, calls, k=K, min_cov=MINCOV):
     """Groups `pick` (indices of one run's groups) in full against the oracle."""
     from oracle import pyoracle as P
     import torch
@@ -223,7 +241,7 @@ def _oracle_groups(pick, rows_h, goh, values, n, calls):
         sub_go.append(sub_go[-1] + len(rr))
     sub_rows = np.concatenate(sub_rows)
     reads_sub = values.view(n, RL)[torch.from_numpy(sub_rows).cuda()].cpu().numpy()
-    ref = P.kmer_spectrum(P.StrCol.from_fixed(reads_sub), K, MINCOV, False, np.array(sub_go), threads=THREADS)
+    ref = P.kmer_spectrum(P.StrCol.from_fixed(reads_sub), k, min_cov, False, np.array(sub_go), threads=THREADS)
     starts = np.concatenate([[0], np.cumsum([len(c[2]["stats"]) for c in calls])])
     nonempty = 0
     for j, g in enumerate(pick):
@@ -309,6 +327,58 @@ def test_c3_full_size_100m_properties():
     assert r.returncode == 0, r.stderr[-3000:]
     child = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("DIGEST ")][-1][7:])
     assert tuple(child) == results[0], (child, results[0])
+
+
+def test_c3_full_size_100m_k15():
+    """C3 at the reference's default operating point at full size: 100M reads, k = 15
+    (effective 16, rogtk/__init__.py:211-212, fracture.rs:246-256), min_coverage 5 - nearly
+    every group has valid k-mers and runs the wave-per-group kernel (round 6). Properties of
+    every group; 2,000 random groups plus the 300 with the most rows and the 300 with the
+    most valid k-mers in full against the oracle; one digest of every output identical for
+    one call on the default path and for 10M-row calls without the wave class
+    (rogtk_kmer_set_path(2): the workgroup kernels take every LDS group)."""
+    import torch
+
+    from rogtk_amd import _lib
+    from rogtk_amd import device as D
+
+    k, mc = 15, 5
+    n, values, offsets, cid = _c3_100m_inputs()
+    print("C3 100M k=15: reads in HBM", flush=True)
+    results = []
+    for run in range(2):
+        _lib.call("rogtk_kmer_set_path", 1 if run == 0 else 2)
+        try:
+            rows, go, G, calls = D.group_spectra(offsets, values, cid, k, mc,
+                                                 batch_rows=100_000_000 if run == 0 else 10_000_000)
+            torch.cuda.synchronize()
+        finally:
+            _lib.call("rogtk_kmer_set_path", 1)
+        results.append(_props(calls, mc, 16) + (G, len(calls)))
+        print(f"C3 100M k=15 run {run}: {results[-1]}", flush=True)
+        if run == 0:
+            rng = np.random.default_rng(15)
+            goh = go.cpu().numpy()
+            rows_h = rows.cpu().numpy()
+            sizes = np.diff(goh)
+            eo = calls[0][2]["entry_offsets"].cpu().numpy()
+            nvalid = np.diff(eo)
+            assert (nvalid > 0).mean() > 0.75  # the operating point: most groups have valid k-mers (UMI-error
+            # singletons and families below 5 reads have none)
+            big = np.argsort(sizes, kind="stable")[-300:]
+            rich = np.argsort(nvalid, kind="stable")[-300:]
+            pick = np.unique(np.concatenate([rng.choice(G, size=2000, replace=False), big, rich]))
+            assert len(pick) >= 2000 and nvalid[rich].min() > 200
+            ne = _oracle_groups(pick, rows_h, goh, values, n, calls, k, mc)
+            print(f"C3 100M k=15: {len(pick)} groups vs oracle, {ne} with valid k-mers; "
+                  f"largest group {sizes.max()} rows, most valid {nvalid.max()}", flush=True)
+            assert ne >= 1500
+        del calls, rows, go
+    assert results[0][:4] == results[1][:4]
+    nseq, groups, _, G, ncalls = results[0]
+    assert nseq == n and groups == G and ncalls == 1 and results[1][4] >= 10
+    del values, offsets, cid
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("lo,hi,bw", [(0, 150, 8), (100, 420, 16), (300, 990, 32)])
