@@ -409,6 +409,39 @@ constexpr size_t kPinPool = 8;
 std::mutex g_pin_mu;
 std::vector<PinnedBuf*> g_pin_pool;
 
+// Round 6: the pool is warmed when the first reader of a process opens: kPinWarm buffers
+// (concurrent range readers: one per range of a rank, bams_umi_cluster) of the size stream
+// buffers reach (g_pin_hint: the largest pinned so far, at least kPinWarmBytes), pinned by one
+// thread each, joined before the open returns (concurrent opens wait in call_once), so the
+// range readers of a rank's first call take pooled buffers instead of page-locking and
+// growing their own inside the call.
+constexpr size_t kPinWarm = 4;
+constexpr size_t kPinWarmBytes = (size_t)256 << 20;
+size_t g_pin_hint = 0;  // the largest stream buffer pinned so far (guarded by g_pin_mu)
+std::once_flag g_pin_warm_once;
+
+void pin_note(size_t cap) {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    g_pin_hint = std::max(g_pin_hint, cap);
+}
+
+void pin_warm(size_t n, size_t bytes) {
+    std::vector<PinnedBuf*> got(n, nullptr);
+    std::vector<std::thread> th;
+    for (size_t i = 0; i < n; ++i)
+        th.emplace_back([&got, i, bytes] {
+            auto* b = new PinnedBuf();
+            if (b->ensure(bytes) == ROGTK_OK) got[i] = b;  // (ensure pins 1.5x bytes)
+            else delete b;
+        });
+    for (auto& t : th) t.join();
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    for (PinnedBuf* b : got) {
+        if (b && g_pin_pool.size() < kPinPool) g_pin_pool.push_back(b);
+        else delete b;
+    }
+}
+
 void pin_take(PinnedBuf& b) {  // the largest pooled buffer, if any
     std::lock_guard<std::mutex> lk(g_pin_mu);
     if (g_pin_pool.empty()) return;
@@ -712,6 +745,7 @@ struct Bgzf {
                     err = "pinned host allocation failed";
                     return false;
                 }
+                pin_note(nb.cap);
                 if (keep) memcpy(nb.p, buf.p + keep_from, keep);
                 std::swap(buf.p, nb.p);
                 std::swap(buf.cap, nb.cap);
@@ -1198,6 +1232,14 @@ int rogtk_bam_open_range(const char* path, int n_threads, int64_t c_begin, int64
     std::unique_ptr<BamReader> R(new BamReader());
     R->z.f = fopen(path, "rb");
     ROGTK_REQUIRE(R->z.f, ROGTK_E_INVALID, "Failed to open BAM file '%s'", path);
+    std::call_once(g_pin_warm_once, [] {
+        size_t hint;
+        {
+            std::lock_guard<std::mutex> lk(g_pin_mu);
+            hint = std::max(g_pin_hint, kPinWarmBytes);
+        }
+        pin_warm(kPinWarm, hint);
+    });
     pin_take(R->z.buf);
     R->z.threads = n_threads > 0 ? n_threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     ROGTK_HIP_CHECK(hipGetDevice(&R->device));

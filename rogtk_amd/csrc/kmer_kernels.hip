@@ -1803,10 +1803,14 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
                     if (lane >= off) incl += t;
                 }
                 const uint32_t bstart = incl - bc;
+                // each bucket's start and count in LDS (the lookups below run under divergent
+                // control flow, where a cross-lane read of an inactive lane is not defined)
+                C[lane] = bstart | (bc << 16);
+                wave_lds_sync();
                 for (uint32_t i = lane; i < nv; i += 64) {
                     const unsigned long long v = T[i];
                     const uint32_t b = (uint32_t)(v >> 32) >> bsh & 63u;
-                    K2[(uint32_t)__shfl((int)bstart, (int)b) + ((uint32_t)(v >> 24) & 0xFFu)] = (uint32_t)(v >> 32);
+                    K2[(C[b] & 0xFFFFu) + ((uint32_t)(v >> 24) & 0xFFu)] = (uint32_t)(v >> 32);
                 }
                 wave_lds_sync();
                 KT(3);
@@ -1817,9 +1821,9 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
                     const unsigned long long v = live ? T[i] : 0ull;
                     const uint32_t key = (uint32_t)(v >> 32);
                     const uint32_t b = key >> bsh & 63u;
-                    const uint32_t at = (uint32_t)__shfl((int)bstart, (int)b), bn = (uint32_t)__shfl((int)bc, (int)b);
                     bool tm = false, is = false;
                     if (live) {
+                        const uint32_t q = C[b], at = q & 0xFFFFu, bn = q >> 16;
                         uint32_t rank = at;
                         for (uint32_t m = 0; m < bn; ++m) rank += K2[at + m] < key;
                         const uint32_t ex = (uint32_t)(v >> 16) & 0xFFu;
@@ -1829,8 +1833,7 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
                             const uint32_t bb = (uint32_t)(bit & 3);
                             const uint32_t nb = bit < 4 ? (key >> 2) | (bb << (2 * K - 2)) : ((key << 2) | bb) & kmask;
                             const uint32_t b2 = nb >> bsh & 63u;
-                            const uint32_t a2 = (uint32_t)__shfl((int)bstart, (int)b2),
-                                           n2 = (uint32_t)__shfl((int)bc, (int)b2);
+                            const uint32_t q2 = C[b2], a2 = q2 & 0xFFFFu, n2 = q2 >> 16;
                             for (uint32_t m = 0; m < n2; ++m)
                                 if (K2[a2 + m] == nb) {
                                     nx |= 1u << bit;
