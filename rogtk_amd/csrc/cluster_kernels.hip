@@ -480,12 +480,14 @@ constexpr int kLocalCodes = kLocalWords * 64;  // 16384
 constexpr int kLocalPos = 7;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
-// LDS union-find (coherent inside the workgroup): path-halving find, CAS hook of
-// the larger root under the smaller, so a local component's root is its smallest code.
+// relaxed workgroup-scope LDS load (the SV rounds below read parents other threads hook)
 __device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// LDS union-find (coherent inside the workgroup; the dense 7-position tiles): path-halving
+// find, CAS hook of the larger root under the smaller, so a component's root is its
+// smallest local rank, as the SV rounds' rule
 __device__ __forceinline__ uint32_t lfind(uint32_t* lf, uint32_t x) {
     for (;;) {
         const uint32_t p = lds_ld(lf + x);
@@ -498,9 +500,6 @@ __device__ __forceinline__ uint32_t lfind(uint32_t* lf, uint32_t x) {
 }
 
 __device__ __forceinline__ void lunite(uint32_t* lf, uint32_t a, uint32_t b) {
-#ifdef ROGTK_LCC_COUNT
-    atomicAdd(&g_lcc_clk[6], 1ull);
-#endif
     for (;;) {
         a = lfind(lf, a);
         b = lfind(lf, b);
@@ -514,13 +513,9 @@ __device__ __forceinline__ void lunite(uint32_t* lf, uint32_t a, uint32_t b) {
         if (__hip_atomic_compare_exchange_strong(lf + a, &expected, b, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_WORKGROUP))
             return;
-#ifdef ROGTK_LCC_COUNT
-        atomicAdd(&g_lcc_clk[7], 1ull);
-#endif
         a = expected;
     }
 }
-
 
 // Hamming-1 neighbours inside a 64-code word (positions 0..dims-1 of the code =
 // bit strides 1, 4, 16 in groups of 4): any bit set in a group of 4 spreads to all 4.
@@ -650,7 +645,7 @@ __device__ __forceinline__ void local_cc_tile(const int64_t base, const uint4* _
     // 2a. the tile's edges: in-word pairs of the words that are not one component, then the
     //     cross-word pairs at positions 3..lpos-1 (word w and w + d * 4^(p-3), same bit; one
     //     edge between two one-component words), as (a | b << 16) over local ranks into the
-    //     edge list, or, past its capacity, united at once (lunite)
+    //     edge list (past its capacity: in batches, 2b)
     auto rank_of = [](uint32_t pre, uint64_t mask, int b) {
         return pre + (uint32_t)__popcll(mask & ((1ull << b) - 1ull));
     };
@@ -714,42 +709,53 @@ __device__ __forceinline__ void local_cc_tile(const int64_t base, const uint4* _
         }
     }
     uint32_t etot;
-    uint32_t ek = block_excl_scan<NT>(ecount, s_wave, etot);
-    for_edges([&](uint32_t a, uint32_t b) {
-        if (ek < (uint32_t)ECAP) edges[ek] = a | (b << 16);
-        else lunite(lf, a, b);
-        ++ek;
-    });
-    __syncthreads();
-    LCC_T(1);
+    const uint32_t ek0 = block_excl_scan<NT>(ecount, s_wave, etot);
     // 2b. hook + jump rounds over the listed edges (Shiloach-Vishkin in LDS): jump = every
     //     vertex to its root (stars); hook = for every edge whose ends' roots differ, the
     //     larger root under the smaller (atomicMin). Parents only ever point at smaller
     //     vertices, so a component's smallest local rank is never hooked and ends as its
     //     root. Uniform passes (vertices / edges dealt over the threads) instead of one
-    //     union-find chain per edge; s_ch[r & 1] = some hook in round r (reset a round ahead)
-    const uint32_t ne = min(etot, (uint32_t)ECAP);
-    for (int r = 0;; ++r) {
-        for (uint32_t v = t; v < nloc; v += NT) {
-            uint32_t root = lf[v];
-            if (root == v) continue;
-            for (uint32_t q = lds_ld(lf + root); q != root; q = lds_ld(lf + root)) root = q;
-            __hip_atomic_store(lf + v, root, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+    //     union-find chain per edge; s_ch[r & 1] = some hook in round r (reset a round ahead).
+    //     More edges than the list holds (dense tiles: words that are not one component list
+    //     an edge per shared bit) go through in batches of ECAP, the edges re-enumerated per
+    //     batch (round 6: the overflow used to be united by one union-find chain per edge,
+    //     dependent LDS CAS loops: 525 us of local CC per step at 8 emulated ranks)
+    int r = 0;
+    for (uint32_t e0 = 0; e0 < etot || e0 == 0; e0 += (uint32_t)ECAP) {
+        if (e0) __syncthreads();  // the previous batch's rounds read the list
+        uint32_t ek = ek0;
+        for_edges([&](uint32_t a, uint32_t b) {
+            if (ek >= e0 && ek - e0 < (uint32_t)ECAP) edges[ek - e0] = a | (b << 16);
+            ++ek;
+        });
         __syncthreads();
-        if (t == 0) s_ch[(r + 1) & 1] = 0;  // every thread read it after the previous round's barrier
-        bool ch = false;
-        for (uint32_t j = t; j < ne; j += NT) {
-            const uint32_t ed = edges[j];
-            const uint32_t ra = lds_ld(lf + (ed & 0xFFFFu)), rb = lds_ld(lf + (ed >> 16));
-            if (ra != rb) {
-                atomicMin(lf + max(ra, rb), min(ra, rb));
-                ch = true;
+        if (e0 == 0) LCC_T(1);
+        const uint32_t ne = min(etot - min(etot, e0), (uint32_t)ECAP);
+        for (;; ++r) {
+            for (uint32_t v = t; v < nloc; v += NT) {
+                uint32_t root = lf[v];
+                if (root == v) continue;
+                for (uint32_t q = lds_ld(lf + root); q != root; q = lds_ld(lf + root)) root = q;
+                __hip_atomic_store(lf + v, root, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            __syncthreads();
+            if (t == 0) s_ch[(r + 1) & 1] = 0;  // every thread read it after the previous round's barrier
+            bool ch = false;
+            for (uint32_t j = t; j < ne; j += NT) {
+                const uint32_t ed = edges[j];
+                const uint32_t ra = lds_ld(lf + (ed & 0xFFFFu)), rb = lds_ld(lf + (ed >> 16));
+                if (ra != rb) {
+                    atomicMin(lf + max(ra, rb), min(ra, rb));
+                    ch = true;
+                }
+            }
+            if (ch) s_ch[r & 1] = 1;
+            __syncthreads();
+            if (!s_ch[r & 1]) {
+                ++r;
+                break;  // no hook: the jump above left stars
             }
         }
-        if (ch) s_ch[r & 1] = 1;
-        __syncthreads();
-        if (!s_ch[r & 1]) break;  // no hook: the jump above left stars
     }
     LCC_T(2);
     // 3b. outputs of this thread's words: UR = the word's shared local root (global index)
@@ -808,6 +814,251 @@ __device__ __forceinline__ void local_cc_tile(const int64_t base, const uint4* _
 #endif
 }
 
+// The 7-position instance (tiles of 4^7 codes, one 64-code word per thread) for DENSE spaces
+// (round 6: the union bitmap of several ranks, 25-41% of the codes present). A word's
+// vertices are its in-word components (up to kComp; a word with more, i.e. scattered codes,
+// keeps one vertex per code as local_cc_tile does): every code points at its component's
+// first code, so no in-word edge is listed, a pair of words sharing bits lists one edge per
+// pair of their components that share one, and the jumps visit the representatives only.
+// local_cc_tile's per-code edges for a dense tile (every word that is not ONE component, 21%
+// at 41% density, listed an edge per shared bit) took 146 us per workgroup, 380-525 us of
+// local CC per step at 8 emulated ranks. Outputs as local_cc_tile.
+constexpr int kComp = 4;
+template <int CAP, int TW, int ECAP>
+__device__ __forceinline__ void local_cc_tile7(const int64_t base, const uint4* __restrict__ RT, int64_t words, int L,
+                                               uint32_t* __restrict__ f, uint32_t* __restrict__ UR,
+                                               uint64_t* __restrict__ lroot, int64_t rwords, int64_t max_distinct,
+                                               unsigned long long* __restrict__ stats) {
+    constexpr int NT = TW;
+    constexpr uint32_t kLive = 0x80000000u;
+    __shared__ uint64_t wb[TW];
+    __shared__ uint64_t wc[kComp][TW];  // component masks of the words with 1..kComp components
+    __shared__ uint32_t lpre[TW];
+    __shared__ uint8_t wk[TW];  // components (1..kComp), or 0: one vertex per code
+    __shared__ uint32_t lf[CAP];
+    __shared__ uint32_t s_wave[NT / 64];
+    const int t = threadIdx.x, lane = t & 63;
+#ifdef ROGTK_LCC_TIMING
+    const unsigned long long t_entry_ = wall_clock64();
+    unsigned long long t_last_ = t_entry_;
+#endif
+    const int nw = (int)min<int64_t>(TW, words - base);
+    const int w = t;
+    const uint64_t m = w < nw ? rt_word(RT[base + w]) : 0ull;
+    uint32_t nloc;
+    const uint32_t ex = block_excl_scan<NT>((uint32_t)__popcll(m), s_wave, nloc);
+    const uint32_t gbase = RT[base].z;
+    if (nloc > (uint32_t)CAP) {
+        if (t == 0) stats[S_OVERFLOW] = 1;
+        return;
+    }
+    const int lpos = L < 7 ? L : 7;
+    const int indims = lpos < 3 ? lpos : 3;
+    auto rank_of = [](uint32_t pre, uint64_t mask, int b) {
+        return pre + (uint32_t)__popcll(mask & ((1ull << b) - 1ull));
+    };
+    // 1. components, ranks, parents
+    uint64_t comp[kComp];
+    int nc = 0;
+    {
+        uint64_t rest = m;
+        while (rest && nc <= kComp) {
+            const uint64_t c = indims > 0 ? word_component(m, rest & (~rest + 1ull), indims) : (rest & (~rest + 1ull));
+            if (nc < kComp) comp[nc] = c;
+            ++nc;
+            rest &= ~c;
+        }
+    }
+    const int kind = nc > kComp ? 0 : nc;
+    uint32_t rep[kComp];
+#pragma unroll
+    for (int q = 0; q < kComp; ++q) {
+        rep[q] = 0;
+        if (q < kind) {
+            rep[q] = rank_of(ex, m, __ffsll((long long)comp[q]) - 1);
+            wc[q][w] = comp[q];
+        }
+    }
+    wb[w] = m;
+    lpre[w] = ex;
+    wk[w] = (uint8_t)kind;
+    if (kind == 0) {
+        const int cnt = __popcll(m);
+        for (int j = 0; j < cnt; ++j) lf[ex + j] = ex + j;
+    } else {
+#pragma unroll
+        for (int q = 0; q < kComp; ++q) {
+            if (q >= kind) break;
+            uint64_t x = comp[q];
+            while (x) {
+                const int b = __ffsll((long long)x) - 1;
+                x &= x - 1;
+                lf[rank_of(ex, m, b)] = rep[q];
+            }
+        }
+    }
+    __syncthreads();
+    LCC_T(0);
+    // 2. unions, straight into the LDS union-find: the in-word pairs of per-code words, then
+    //    positions 3..lpos-1 as tasks of one group of 4 words {w0 + v 4^(p-3)} each (codes at
+    //    one bit of a group differ only at p): components of two words that share a bit are
+    //    united; a group of one-component words unites each word with the first word of its
+    //    linked group (<= 3 unions instead of one per linked pair; round 4's dense rule)
+    auto rep_in = [&](int w2, uint64_t m2, uint32_t pre2, int k2, int b) -> uint32_t {
+        if (k2 == 0) return rank_of(pre2, m2, b);
+        for (int q = 0; q < k2; ++q) {
+            const uint64_t c = wc[q][w2];
+            if ((c >> b) & 1ull) return rank_of(pre2, m2, __ffsll((long long)c) - 1);
+        }
+        return rank_of(pre2, m2, b);  // (not reached: the components cover the word)
+    };
+    if (kind == 0 && m)
+        for (int q = 0; q < indims; ++q)
+            for (int d = 1; d <= 3; ++d) {
+                uint64_t e = inword_pairs(m, q, d);
+                while (e) {
+                    const int b = __ffsll((long long)e) - 1;
+                    e &= e - 1;
+                    lunite(lf, rank_of(ex, m, b), rank_of(ex, m, b + (d << (2 * q))));
+                }
+            }
+    const int per = nw >> 2;
+    for (int task = t; per > 0 && task < (lpos - 3) * per; task += NT) {
+        const int p = 3 + task / per, g = task % per, s2 = 2 * p - 6, stride = 1 << s2;
+        const int wg0 = ((g >> s2) << (s2 + 2)) | (g & (stride - 1));
+        uint64_t mv[4];
+        uint32_t pv[4];
+        int kv[4];
+        bool all_one = true;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int wv = wg0 + v * stride;
+            mv[v] = wb[wv];
+            pv[v] = lpre[wv];
+            kv[v] = wk[wv];
+            all_one &= kv[v] == 1 || mv[v] == 0;
+        }
+        if (all_one) {
+            uint32_t adj[4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                adj[a] = 1u << a;
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if (b != a && (mv[a] & mv[b])) adj[a] |= 1u << b;
+            }
+#pragma unroll
+            for (int it = 0; it < 2; ++it)  // closure: 4 nodes, diameter <= 3
+#pragma unroll
+                for (int a = 0; a < 4; ++a) {
+                    uint32_t rr = adj[a];
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        if ((adj[a] >> b) & 1u) rr |= adj[b];
+                    adj[a] = rr;
+                }
+#pragma unroll
+            for (int a = 1; a < 4; ++a) {
+                const int lead = __ffs((int)adj[a]) - 1;
+                if (lead != a) lunite(lf, pv[lead], pv[a]);  // a one-component word's vertex: its first code
+            }
+        } else {
+#pragma unroll
+            for (int x = 0; x < 3; ++x)
+#pragma unroll
+                for (int y = x + 1; y < 4; ++y) {
+                    uint64_t z = mv[x] & mv[y];
+                    if (!z) continue;
+                    const int wx = wg0 + x * stride, wy = wg0 + y * stride;
+                    if (kv[x] > 0 && kv[y] > 0) {
+                        for (int qx = 0; qx < kv[x]; ++qx) {
+                            const uint64_t cx = wc[qx][wx];
+                            if (!(cx & z)) continue;
+                            for (int qy = 0; qy < kv[y]; ++qy) {
+                                const uint64_t cy = wc[qy][wy];
+                                if (cx & cy)
+                                    lunite(lf, rank_of(pv[x], mv[x], __ffsll((long long)cx) - 1),
+                                           rank_of(pv[y], mv[y], __ffsll((long long)cy) - 1));
+                            }
+                        }
+                    } else {
+                        while (z) {
+                            const int b = __ffsll((long long)z) - 1;
+                            z &= z - 1;
+                            lunite(lf, rep_in(wx, mv[x], pv[x], kv[x], b), rep_in(wy, mv[y], pv[y], kv[y], b));
+                        }
+                    }
+                }
+        }
+    }
+    __syncthreads();
+    LCC_T(1);
+    if (kind == 0) {
+        const int cnt = __popcll(m);
+        for (int j = 0; j < cnt; ++j) lf[ex + j] = lfind(lf, ex + j);
+    } else {
+#pragma unroll
+        for (int q = 0; q < kComp; ++q)
+            if (q < kind) lf[rep[q]] = lfind(lf, rep[q]);
+    }
+    __syncthreads();
+    LCC_T(2);
+    // 3. outputs of this thread's word: a code's root is lf[its representative] (stars: the
+    //    representatives were jumped last; codes of a component still point at theirs)
+    if (t == 0 && (int64_t)gbase + nloc > max_distinct) stats[S_OVERFLOW] = 1;
+    if (w < nw) {
+        const int cnt = __popcll(m);
+        uint32_t first = kNone;
+        bool uniform = true;
+        for (int j = 0; j < cnt; ++j) {
+            const uint32_t root = lf[lf[ex + j]] & ~kLive;  // (another thread may mark a root live)
+            if (j == 0) first = root;
+            uniform &= root == first;
+        }
+        // f first, then the live marks (a mark would hide the representative's root)
+        for (int j = 0; j < cnt; ++j) {
+            const uint32_t rr = ex + j, root = lf[lf[rr]] & ~kLive;
+            const int64_t gi = (int64_t)gbase + rr;
+            if (root == rr || !uniform) {
+                if (gi < max_distinct) f[gi] = gbase + root;
+            }
+        }
+        for (int j = 0; j < cnt; ++j) {
+            const uint32_t rr = ex + j;
+            const uint32_t root = lf[lf[rr] & ~kLive] & ~kLive;
+            if (root == rr || !uniform) lf[rr] = root | kLive;
+        }
+        UR[base + w] = (cnt && uniform) ? gbase + first : kNone;
+    }
+    __syncthreads();
+    // 4. index-space live words (as local_cc_tile)
+    {
+        const uint32_t off = gbase & 63u;
+        const uint32_t nlw = nloc ? (off + nloc + 63u) / 64u : 0u;
+        const int64_t lw0 = (int64_t)(gbase >> 6);
+        for (uint32_t k = t >> 6; k < nlw; k += NT / 64) {
+            const int64_t lw = lw0 + k;
+            const int64_t rr = (int64_t)k * 64 + lane - off;
+            const bool live = rr >= 0 && rr < (int64_t)nloc && (lf[rr] & kLive);
+            const uint64_t v = __ballot(live);
+            if (lane == 0 && lw < rwords) {
+                if (k == 0 || k == nlw - 1) {
+                    if (v) atomicOr((unsigned long long*)(lroot + lw), (unsigned long long)v);
+                } else {
+                    lroot[lw] = v;
+                }
+            }
+        }
+    }
+    LCC_T(3);
+#ifdef ROGTK_LCC_TIMING
+    if (threadIdx.x == 0) {
+        atomicAdd(&g_lcc_clk[4], wall_clock64() - t_entry_);
+        atomicAdd(&g_lcc_clk[5], 1ull);
+    }
+#endif
+}
+
 #ifndef ROGTK_LCC_NT8
 #define ROGTK_LCC_NT8 1024  // threads of an 8-position local-CC workgroup (experiments)
 #endif
@@ -832,13 +1083,17 @@ __global__ __launch_bounds__(NT) ROGTK_LCC_ATTR(CAP, NT) void k_local_cc(const u
         if (alone && blockIdx.x == 0 && threadIdx.x == 0) stats[S_REDO] = 1;
         return;
     }
-    // edge-list capacity (edges past it are united at once): C2's sparse 4^8 tiles list ~0.8
-    // edges per code; the 7-position tiling takes dense spaces, whose words are mostly one
-    // component each (at most ~1.5 edges per word and position); 3072 keeps that instance at
-    // 2 workgroups per CU
-    constexpr int kEcap = LP == 7 ? 3072 : CAP >= 16384 ? 12288 : 8192;
-    local_cc_tile<CAP, TW, LP, NT, kEcap>((int64_t)blockIdx.x * TW, RT, words, L, f, UR, lroot, rwords, max_distinct,
-                                          stats);
+    // edge-list capacity (more edges go through in batches): C2's sparse 4^8 tiles list ~0.8
+    // edges per code; the 7-position tiling takes dense spaces, whose words are few
+    // components each (~1.3 edges per word pair: ~2,000 per tile at 41% density, two
+    // batches); 1024 keeps that instance at 2 workgroups per CU
+    constexpr int kEcap = LP == 7 ? 1024 : CAP >= 16384 ? 12288 : 8192;
+    if constexpr (LP == 7 && NT == TW)
+        local_cc_tile7<CAP, TW, kEcap>((int64_t)blockIdx.x * TW, RT, words, L, f, UR, lroot, rwords, max_distinct,
+                                       stats);
+    else
+        local_cc_tile<CAP, TW, LP, NT, kEcap>((int64_t)blockIdx.x * TW, RT, words, L, f, UR, lroot, rwords,
+                                              max_distinct, stats);
 }
 
 // ROGTK_LOCAL8=0: never the 8-position local tiling (A/B)

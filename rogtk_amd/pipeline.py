@@ -31,8 +31,6 @@ wait for batch k-1's flags moves onto the critical cycle: 0.487 vs 0.430 ms/step
 """
 from __future__ import annotations
 
-import os
-
 from collections import deque
 from typing import Optional
 
@@ -270,10 +268,14 @@ class UmiPipeline:
 
     def _attach_event(self):
         """An event recorded by a kernel's own dispatch packet (the split mark's bucket pass,
-        the resolve's last kernel), which another stream waits for."""
+        the resolve's last kernel), which another stream waits for. Created WITHOUT
+        hipEventDisableSystemFence: as the stop event of a dispatch, a
+        device-scope event may leave the packet without the agent-scope release that makes
+        the kernel's L2 lines visible to a consumer on another XCD; interleaved A/B (round 6,
+        profiles/r06_event_scope_ab.txt): 0.2843-0.2883 vs 0.2851-0.29 ms/step, sustained equal."""
         if not self.device_events:
             return torch.cuda.Event()
-        return D.StreamEvent(device_scope=os.environ.get("ROGTK_ATTACH_SYS", "0") != "1")
+        return D.StreamEvent(device_scope=False)
 
     def _score(self, slot: _Slot, batch: D.PackedBatch):
         D.score_packed(batch, slot.scores, self.target, self.max_hamming, slot.dist, slot.within, stream=self.main)
