@@ -53,9 +53,10 @@ TARGET = b"ACGTACGTACGT"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100,
-                    help="timed steps (the pipeline fills and drains once per timed region: 100 steps amortise that to ~1%%)")
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20,
+                    help="timed steps (the driver's 20: the pipeline fills and drains once per timed region, ~5%% "
+                         "of 20 steps; 'sustained' reports the steady state)")
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=("C2", "C4"), default="C2",
                     help="C2: 10M reads per GPU (weak scaling); C4: 500M reads over all GPUs (strong scaling)")
     ap.add_argument("--reads-per-gpu", type=int, default=None,
