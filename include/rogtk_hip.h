@@ -642,6 +642,15 @@ int rogtk_bam_umi_append(const rogtk_bam_batch* batch, int64_t n, int source, in
 int rogtk_bam_append_strings(const int64_t* src_offsets, const uint8_t* src_values, int64_t n, int64_t* offsets,
                              uint8_t* values, int64_t values_cap, int64_t row_base, int64_t* base,
                              unsigned long long* overflow, void* stream);
+/* Round 6: k device string columns (int64 offsets from 0, n_i + 1 entries; values; validity
+ * bitmaps) concatenated in order into out_offsets (sum n_i + 1), out_values (values_cap
+ * bytes; rows past it counted in *overflow, a device u64) and out_validity, with the running
+ * byte count in *base (a device int64): no host synchronisation. Arrays of device pointers
+ * on the host. */
+int rogtk_concat_strings_dev(int k, const int64_t* const* offsets, const uint8_t* const* values,
+                             const uint64_t* const* validity, const int64_t* counts, int64_t* out_offsets,
+                             uint8_t* out_values, int64_t values_cap, uint64_t* out_validity, int64_t* base,
+                             unsigned long long* overflow, void* stream);
 /* Raw record bytes of the reader's current batch (bounds a device batch's columns: name
  * <= 3 x bytes + 7 per record, sequence / qualities <= bytes). */
 int rogtk_bam_batch_bytes(void* reader, int64_t* bytes);

@@ -186,6 +186,7 @@ SIGNATURES = {
                                   ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, _i64, _vp, _vp, _vp, _P_I64],
     "rogtk_assembly_optimize_host": [_vp, _i32, _vp, _i64, _vp, _i64, _i64, ctypes.c_char_p, ctypes.c_char_p,
                                      ctypes.c_char_p, _i64, _i64, _i64, _i32, _i32, _vp, _i64, _P_I64, _vp],
+    "rogtk_concat_strings_dev": [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
     "rogtk_assemble_groups_host": [_vp, _vp, _vp, _vp, _vp, _i64, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                    _i32, _i64, _i32, _vp],
     "rogtk_assembly_result_sizes": [_vp, _P_I64, _P_I64],

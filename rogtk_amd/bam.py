@@ -217,7 +217,7 @@ def iter_bam_batches(bam_path: str, batch_size: int = 50000, include_sequence: b
 
 def _with_source(rb: pa.RecordBatch, source: str, schema: pa.Schema) -> pa.RecordBatch:
     """add_source_file_column (bam.rs:634-643)."""
-    col = pa.array([source] * rb.num_rows, type=pa.string())
+    col = _repeat_str(source, rb.num_rows)
     return pa.RecordBatch.from_arrays(list(rb.columns) + [col], schema=schema)
 
 
@@ -482,7 +482,22 @@ def bam_umis_dev(bam_path: str, umi_len: int = 12, source: str = "sequence", sep
     return out + (tail,) if return_tail else out
 
 
+def _repeat_str(s: str, n: int) -> pa.Array:
+    """A string column of n copies of s, built from buffers (round 6: pa.array over a
+    Python list of 1M strings cost a fresh process ~0.6 s the first time, most of a rank's
+    first bams_umi_cluster call)."""
+    b = s.encode()
+    big = n * len(b) >= 2 ** 31
+    offs = np.arange(n + 1, dtype=np.int64 if big else np.int32) * len(b)
+    arr = pa.Array.from_buffers(pa.large_string() if big else pa.string(), n,
+                                [None, pa.py_buffer(offs), pa.py_buffer(b * n)])
+    return arr.cast(pa.string()) if big else arr
+
+
 def _concat_dev(offs, vals, valids, counts, dev):
+    """The ranges' device UMI columns concatenated in order (rogtk_concat_strings_dev: the
+    library's own kernels, no host sync; round 6 - torch's cat and bit kernels cost a fresh
+    process ~0.5 s of module loading in its first call)."""
     import torch
     n = sum(counts)
     if n == 0:
@@ -490,23 +505,19 @@ def _concat_dev(offs, vals, valids, counts, dev):
         return z, torch.zeros(1, dtype=torch.uint8, device=dev), torch.zeros(1, dtype=torch.int64, device=dev), 0
     if len(offs) == 1:
         return offs[0], vals[0], valids[0], n
-    base = 0
-    parts = []
-    for o, v in zip(offs, vals):
-        parts.append(o[:-1] + base)
-        base += v.numel()
-    off = torch.cat(parts + [torch.tensor([base], dtype=torch.int64, device=dev)])
-    val = torch.cat(vals)
-    # validity: unpack to bools, concatenate, repack into little-endian words
-    bools = []
-    for w, c in zip(valids, counts):
-        bits = ((w.view(torch.uint8).unsqueeze(1) >> torch.arange(8, device=dev, dtype=torch.uint8)) & 1)
-        bools.append(bits.reshape(-1)[:c])
-    allb = torch.cat(bools)
-    pad = (-allb.numel()) % 64
-    allb = torch.cat([allb, torch.zeros(pad, dtype=torch.uint8, device=dev)]).view(-1, 8)
-    packed = (allb << torch.arange(8, device=dev, dtype=torch.uint8)).sum(1, dtype=torch.uint8)
-    return off, val, packed.view(torch.int64), n
+    cap = sum(int(v.numel()) for v in vals)
+    off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    val = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+    vw = torch.empty((n + 63) // 64, dtype=torch.int64, device=dev)
+    scratch = torch.empty(2, dtype=torch.int64, device=dev)  # running byte count, overflow
+    k = len(offs)
+    P = ctypes.c_void_p * k
+    _lib.call("rogtk_concat_strings_dev", k, P(*[o.data_ptr() for o in offs]), P(*[v.data_ptr() for v in vals]),
+              P(*[w.data_ptr() for w in valids]), (ctypes.c_int64 * k)(*[int(c) for c in counts]),
+              ctypes.c_void_p(off.data_ptr()), ctypes.c_void_p(val.data_ptr()), cap, ctypes.c_void_p(vw.data_ptr()),
+              ctypes.c_void_p(scratch.data_ptr()), ctypes.c_void_p(scratch.data_ptr() + 8),
+              ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+    return off, val, vw, n
 
 
 def _umi_table(off, val, vw, n, names, cid, n_clusters, extra=None) -> pa.Table:
@@ -625,7 +636,7 @@ def bams_umi_cluster(bam_paths: Sequence[str], umi_len: int = 12, max_distance: 
         raise _lib.RogtkError(_lib.ROGTK_E_INVALID, "bam ranges: record boundaries did not settle")
     parts = [res[j][0] for j in mine]
     names = [res[j][1] if res[j][1] is not None else pa.array([], pa.string()) for j in mine]
-    srcs = [pa.array([paths[ranges[j][0]]] * res[j][0][3], pa.string()) for j in mine]
+    srcs = [_repeat_str(paths[ranges[j][0]], res[j][0][3]) for j in mine]
     off, val, vw, n = _concat_dev([p[0] for p in parts], [p[1] for p in parts], [p[2] for p in parts],
                                   [p[3] for p in parts], dev) if parts else _concat_dev([], [], [], [], dev)
     if tm is not None:

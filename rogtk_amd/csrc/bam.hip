@@ -1495,6 +1495,59 @@ int rogtk_bam_append_strings(const int64_t* src_offsets, const uint8_t* src_valu
     return ROGTK_OK;
 }
 
+namespace {
+// dst bits [row_base, row_base + n) = src bits [0, n) (dst zeroed before; a part's first word
+// may hold the previous part's last bits: ORed, the rest stored whole)
+__global__ __launch_bounds__(256) void k_bits_append(const uint64_t* __restrict__ src, int64_t n, uint64_t* dst,
+                                                     int64_t row_base) {
+    const int64_t w0 = row_base >> 6, w1 = (row_base + n - 1) >> 6;
+    const int64_t w = w0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n <= 0 || w > w1) return;
+    const int64_t lo = max<int64_t>(64 * w, row_base), hi = min<int64_t>(64 * w + 64, row_base + n);
+    const int64_t s0 = lo - row_base;  // first source bit
+    const int len = (int)(hi - lo);
+    const int sh = (int)(s0 & 63);
+    uint64_t v = src[s0 >> 6] >> sh;
+    if (sh && sh + len > 64) v |= src[(s0 >> 6) + 1] << (64 - sh);
+    if (len < 64) v &= (1ull << len) - 1ull;
+    v <<= (int)(lo - 64 * w);
+    if (w == w0) atomicOr((unsigned long long*)(dst + w), (unsigned long long)v);
+    else dst[w] = v;
+}
+}  // namespace
+
+// Round 6: k device string columns (int64 offsets from 0, values, validity bits) into one,
+// in order, with the library's own kernels (rogtk_amd.bam's range concatenation: torch's
+// cat / bit kernels cost their first call ~0.5 s of module loading in a fresh process)
+int rogtk_concat_strings_dev(int k, const int64_t* const* offsets, const uint8_t* const* values,
+                             const uint64_t* const* validity, const int64_t* counts, int64_t* out_offsets,
+                             uint8_t* out_values, int64_t values_cap, uint64_t* out_validity, int64_t* base,
+                             unsigned long long* overflow, void* stream) {
+    ROGTK_REQUIRE(k >= 0 && (k == 0 || (offsets && values && validity && counts)) && out_offsets && out_values &&
+                      out_validity && base && overflow,
+                  ROGTK_E_INVALID, "concat strings: bad arguments");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int64_t n = 0;
+    for (int i = 0; i < k; ++i) n += counts[i];
+    ROGTK_HIP_CHECK(hipMemsetAsync(out_validity, 0, (size_t)std::max<int64_t>((n + 63) / 64, 1) * 8, s));
+    ROGTK_HIP_CHECK(hipMemsetAsync(base, 0, 8, s));
+    ROGTK_HIP_CHECK(hipMemsetAsync(overflow, 0, 8, s));
+    ROGTK_HIP_CHECK(hipMemsetAsync(out_offsets, 0, 8, s));
+    int64_t row = 0;
+    for (int i = 0; i < k; ++i) {
+        if (counts[i] == 0) continue;
+        if (int rc = rogtk_bam_append_strings(offsets[i], values[i], counts[i], out_offsets, out_values, values_cap,
+                                              row, base, overflow, stream))
+            return rc;
+        const int64_t words = ((row + counts[i] - 1) >> 6) - (row >> 6) + 1;
+        hipLaunchKernelGGL(k_bits_append, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, validity[i], counts[i],
+                           out_validity, row);
+        ROGTK_HIP_CHECK(hipGetLastError());
+        row += counts[i];
+    }
+    return ROGTK_OK;
+}
+
 int rogtk_bam_batch_bytes(void* reader, int64_t* bytes) {
     ROGTK_REQUIRE(reader && bytes, ROGTK_E_INVALID, "bam: NULL argument");
     auto* R = static_cast<BamReader*>(reader);
