@@ -1587,13 +1587,13 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
     static_assert(kWaveValid * 8 + kWaveValid * 4 <= kWaveSlots * 8, "entries + bucketed keys fit the table");
     __shared__ unsigned long long s_tab[kWaveWG][kWaveSlots];
     __shared__ __attribute__((aligned(16))) uint64_t s_buf[kWaveWG][kBuf + 2];
-    __shared__ uint32_t s_cnt[kWaveWG][64];  // the rank sort's bucket counts
+    static_assert((kBuf + 2) * 8 >= 256 * 4, "the rank sort's 256 bucket heads fit the words' LDS");
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     unsigned long long* const T = s_tab[wv];
     uint64_t* const W = s_buf[wv];
-    uint32_t* const C = s_cnt[wv];
     const uint32_t kmask = K >= 16 ? 0xFFFFFFFFu : (1u << (2 * K)) - 1u;
-    const int bsh = 2 * K >= 6 ? 2 * K - 6 : 0;  // the rank sort's bucket: the key's top 6 bits
+    // the rank sort's bucket: the key's top 8 bits, and never its last base (bsh >= 2)
+    const int bsh = 2 * K - 8 >= 2 ? 2 * K - 8 : 2;
     for (int i = lane; i < kWaveSlots; i += 64) T[i] = kWEmpty;
     const int64_t n_chunks = (G + 63) >> 6;
     const int64_t nw = (int64_t)gridDim.x * kWaveWG;
@@ -1698,36 +1698,47 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
         auto base_at = [&](int q) -> uint32_t {  // base q of the lane's row (q >= 0)
             return (uint32_t)(W[wo_r + (q >> 5)] >> (62 - 2 * (q & 31))) & 3u;
         };
+        auto win_at = [&](int q) -> uint64_t {  // bases q .. q + 31 of the lane's row
+            const int wi = wo_r + (q >> 5);
+            const uint64_t w0 = W[wi], w1 = W[wi + 1];
+            const int o = 2 * (q & 31);
+            return o ? (w0 << o) | (w1 >> (64 - o)) : w0;
+        };
+        // a rolling window: win holds the 32 bases from the lane's position p and nwd the
+        // packed word that supplies base p + 32, so a step shifts one base in and reads LDS
+        // once per 32 positions (the CAS is the trip's only LDS access on its chain); the
+        // segment's start state is kept for the wrap of the rotation
         const uint32_t wrapb = nst > 0 && pst > 0 ? base_at(pst - 1) : 0u;
         uint32_t prevb = nst > 0 && pst + rot > 0 ? base_at(pst + rot - 1) : 0u;
+        uint64_t win = 0, nwd = 0, win_s = 0, nwd_s = 0;
+        int p = pst + rot;
+        if (nst > 0) {
+            win_s = win_at(pst);
+            nwd_s = W[wo_r + (pst >> 5) + 1];
+            win = rot ? win_at(p) : win_s;
+            nwd = rot ? W[wo_r + (p >> 5) + 1] : nwd_s;
+        }
         uint32_t claims = 0;
         bool over = false;
         for (int t = 0; t < Ls; ++t) {
-            const bool act = t < nst;
-            int j = t + rot;
-            j -= j >= nst ? nst : 0;
-            const int p = pst + j;
             bool fresh = false;
-            if (act) {
-                const int wi = wo_r + (p >> 5);
-                const uint64_t w0 = W[wi], w1 = W[wi + 1];
-                const int o = 2 * (p & 31);
-                const uint64_t win = o ? (w0 << o) | (w1 >> (64 - o)) : w0;
+            if (t < nst) {
                 const uint32_t key = (uint32_t)(win >> (64 - 2 * K)) & kmask;
-                const uint32_t lb = j == 0 ? wrapb : prevb;
-                uint32_t e = p > 0 ? 1u << lb : 0u;
+                uint32_t e = p > 0 ? 1u << prevb : 0u;
                 if (p + K < len_r) e |= 1u << (4 + ((uint32_t)(win >> (62 - 2 * K)) & 3u));
                 prevb = (uint32_t)(win >> 62);
                 uint32_t h = wave_hash(key);
                 const unsigned long long mine = ((unsigned long long)key << 32) | (1ull << 8) | e;
-#if defined(ROGTK_WAVE_EXP) && ROGTK_WAVE_EXP == 1
-                T[h] = mine;  // (timing experiment: no atomics)
-                fresh = (h & 7) == 0;
-                if (true) continue;
-#endif
-#if defined(ROGTK_WAVE_EXP) && ROGTK_WAVE_EXP == 2
-                if (h != 0xFFFFFFFFu) continue;  // (timing experiment: no table access)
-#endif
+                // the next position's window (its LDS word read, if any, overlaps the CAS)
+                const int o = p & 31;
+                win = (win << 2) | ((nwd >> (62 - 2 * o)) & 3u);
+                if (o == 31) nwd = W[wo_r + ((p + 1) >> 5) + 1];
+                if (++p == pst + nst) {
+                    p = pst;
+                    win = win_s;
+                    nwd = nwd_s;
+                    prevb = wrapb;
+                }
                 unsigned long long v;
                 while (true) {
                     v = atomicCAS(&T[h], kWEmpty, mine);
@@ -1775,19 +1786,22 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
         }
         uint32_t term = 0, iso = 0;
         if (!over && nv > 0) {
-            // rank sort by buckets: the key's top 6 bits pick one of 64 buckets, an LDS atomic
-            // gives each entry its place in its bucket (kept in the entry's bits 24..31), a wave
-            // scan the buckets' starts; the bucketed keys K2 (behind the entries) give an
-            // entry's rank (its bucket's start + the keys of its bucket below it) and the
-            // censoring's neighbour lookups (a valid neighbour is one of K2's keys)
+            // rank sort by buckets: the key's top 8 bits pick one of 256 buckets (an entry's
+            // bucket holds ~1 key at C3's ~150 valid k-mers), an LDS atomic gives each entry its
+            // place in its bucket (kept in the entry's bits 24..31), a wave scan the buckets'
+            // starts; the bucketed keys K2 (behind the entries) give an entry's rank (its
+            // bucket's start + the keys of its bucket below it) and the censoring's neighbour
+            // lookups (a valid neighbour is one of K2's keys). bsh >= 2, so the four right
+            // neighbours of a key share a bucket: one scan decides its four right bits.
             uint32_t* const K2 = reinterpret_cast<uint32_t*>(T + kWaveValid);
-            C[lane] = 0;
+            uint32_t* const C = reinterpret_cast<uint32_t*>(W);  // the words are dead by now
+            reinterpret_cast<uint4*>(C)[lane] = make_uint4(0u, 0u, 0u, 0u);
             wave_lds_sync();
             KT(2);
             bool deep = false;  // a bucket past 255 entries (adversarial keys): class 3
             for (uint32_t i = lane; i < nv; i += 64) {
                 const unsigned long long v = T[i];
-                const uint32_t li = atomicAdd(&C[(uint32_t)(v >> 32) >> bsh & 63u], 1u);
+                const uint32_t li = atomicAdd(&C[(uint32_t)(v >> 32) >> bsh & 255u], 1u);
                 deep |= li > 255u;
                 T[i] = v | ((unsigned long long)min(li, 255u) << 24);
             }
@@ -1795,48 +1809,66 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
                 over = true;
             } else {
                 wave_lds_sync();
-                const uint32_t bc = C[lane];
+                const uint4 c4 = reinterpret_cast<const uint4*>(C)[lane];  // buckets 4 lane .. 4 lane + 3
+                const uint32_t bc = c4.x + c4.y + c4.z + c4.w;
                 uint32_t incl = bc;
 #pragma unroll
                 for (int off = 1; off < 64; off <<= 1) {
                     const uint32_t t = __shfl_up(incl, off);
                     if (lane >= off) incl += t;
                 }
-                const uint32_t bstart = incl - bc;
                 // each bucket's start and count in LDS (the lookups below run under divergent
                 // control flow, where a cross-lane read of an inactive lane is not defined)
-                C[lane] = bstart | (bc << 16);
+                uint32_t st = incl - bc;
+                uint4 o4;
+                o4.x = st | (c4.x << 16);
+                st += c4.x;
+                o4.y = st | (c4.y << 16);
+                st += c4.y;
+                o4.z = st | (c4.z << 16);
+                st += c4.z;
+                o4.w = st | (c4.w << 16);
+                reinterpret_cast<uint4*>(C)[lane] = o4;
                 wave_lds_sync();
                 for (uint32_t i = lane; i < nv; i += 64) {
                     const unsigned long long v = T[i];
-                    const uint32_t b = (uint32_t)(v >> 32) >> bsh & 63u;
+                    const uint32_t b = (uint32_t)(v >> 32) >> bsh & 255u;
                     K2[(C[b] & 0xFFFFu) + ((uint32_t)(v >> 24) & 0xFFu)] = (uint32_t)(v >> 32);
                 }
                 wave_lds_sync();
                 KT(3);
                 const int64_t base = cap_off[g];
+                const uint32_t kmask2 = kmask >> 2;
                 for (uint32_t i0 = 0; i0 < nv; i0 += 64) {
                     const uint32_t i = i0 + lane;
                     const bool live = i < nv;
                     const unsigned long long v = live ? T[i] : 0ull;
                     const uint32_t key = (uint32_t)(v >> 32);
-                    const uint32_t b = key >> bsh & 63u;
                     bool tm = false, is = false;
                     if (live) {
-                        const uint32_t q = C[b], at = q & 0xFFFFu, bn = q >> 16;
+                        const uint32_t ex = (uint32_t)(v >> 16) & 0xFFu;
+                        // the three bucket heads first (independent reads), then the scans
+                        const uint32_t q = C[key >> bsh & 255u];
+                        const uint32_t qr = C[((key << 2) & kmask) >> bsh & 255u];
+                        const uint32_t at = q & 0xFFFFu, bn = q >> 16;
                         uint32_t rank = at;
                         for (uint32_t m = 0; m < bn; ++m) rank += K2[at + m] < key;
-                        const uint32_t ex = (uint32_t)(v >> 16) & 0xFFu;
                         uint32_t nx = 0;
-                        for (int bit = 0; bit < 8; ++bit) {
-                            if (!((ex >> bit) & 1u)) continue;
-                            const uint32_t bb = (uint32_t)(bit & 3);
-                            const uint32_t nb = bit < 4 ? (key >> 2) | (bb << (2 * K - 2)) : ((key << 2) | bb) & kmask;
-                            const uint32_t b2 = nb >> bsh & 63u;
-                            const uint32_t q2 = C[b2], a2 = q2 & 0xFFFFu, n2 = q2 >> 16;
+                        if (ex >> 4) {
+                            const uint32_t ar = qr & 0xFFFFu, nr = qr >> 16, lo = key & kmask2;
+                            for (uint32_t m = 0; m < nr; ++m) {
+                                const uint32_t k2 = K2[ar + m];
+                                if ((k2 >> 2) == lo) nx |= 16u << (k2 & 3u);
+                            }
+                            nx &= ex & 0xF0u;
+                        }
+                        for (uint32_t lb = ex & 0xFu; lb; lb &= lb - 1) {
+                            const uint32_t bb = (uint32_t)__builtin_ctz(lb);
+                            const uint32_t nb = (key >> 2) | (bb << (2 * K - 2));
+                            const uint32_t q2 = C[nb >> bsh & 255u], a2 = q2 & 0xFFFFu, n2 = q2 >> 16;
                             for (uint32_t m = 0; m < n2; ++m)
                                 if (K2[a2 + m] == nb) {
-                                    nx |= 1u << bit;
+                                    nx |= 1u << bb;
                                     break;
                                 }
                         }
