@@ -1530,19 +1530,18 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
 // a wave-private LDS hash table and no workgroup barrier. The workgroup kernel above holds
 // 8 waves per group through barrier-separated phases in which most waves idle (a C3 group
 // at k_eff 16: ~1,650 observations, ~157 valid k-mers, ~30k clocks per group); here each
-// wave runs its own group start to end, so the CU interleaves up to 12 groups' inserts.
-//   * slot = key << 32 | count << 8 | exts (k_eff <= 16: 32-bit keys); empty = key bits all
-//     ones with count 0 (a real entry has count >= 1, so the all-T key needs no special slot);
-//   * insert: one 64-bit CAS claims an empty slot or returns the owner; a repeat whose
-//     extension bits are already set is a non-returning 64-bit add of 1 << 8, else a CAS loop
-//     (the observations of one trip are consecutive positions: distinct k-mers, few retries);
-//   * the observations of a group are dealt flat over the lanes (lane l of trip t takes
-//     observation 64 t + l of the group, walking the rows' observation counts), so a 135-k-mer
-//     row costs 2.1 trips instead of 3;
-//   * CountFilter: a scan of the table compacts the valid entries (ballot prefix) into the
-//     words' LDS (the words are dead by then); a rank sort (each lane counts the keys below
-//     its entries, every lane reading the same 16 B at once) gives each entry its output
-//     place; censoring probes the table itself; terminal / isolated counts by ballots.
+// wave runs its own group start to end, so the CU interleaves up to 16 groups' inserts.
+//   * table: 32-bit keys TK (k_eff <= 16) beside 32-bit count << 8 | exts TV; empty = all-ones
+//     key, so the all-T 16-mer counts in a slot of its own (TV[kWaveSlots]);
+//   * insert: a 32-bit CAS claims an empty key slot or finds the key, a returning add counts
+//     it, and an OR follows only when the add's old value lacks one of its extension bits
+//     (half the LDS dwords of a 64-bit slot's CAS + add);
+//   * lane task = (row, segment of the row), each segment started at a rotation of its row so
+//     the rows' lanes - copies of one template - hit different k-mers in a trip; a lane rolls
+//     a 32-base window along its segment (one packed word read per step, ahead of its CAS);
+//   * CountFilter: a scan of the table compacts the valid entries (ballot prefix) in place; a
+//     rank sort by 256 key buckets gives each entry its output place; censoring looks the
+//     neighbours up in the bucketed keys; terminal / isolated counts by ballots.
 // A group with more than kWaveClaim distinct or kWaveValid valid k-mers moves to class 3
 // (launched after this kernel): the outputs never depend on the path.
 // The next group's descriptor and packed words are loaded into registers while the current
@@ -1559,7 +1558,7 @@ constexpr int kWaveWords = 192;    // packed words (38 rows of <= 160 bases at s
 constexpr int kWaveValid = 512;    // valid k-mers (compacted to the table's front; keys bucketed behind them)
 constexpr int kWaveWG = 2;         // waves per workgroup (24.5 KB of LDS: 6 workgroups per CU)
 constexpr int kWaveWPL = (kWaveWords + 63) / 64;  // prefetched words per lane
-constexpr unsigned long long kWEmpty = 0xFFFFFFFF00000000ull;
+constexpr uint32_t kWEmpty = 0xFFFFFFFFu;  // an empty key slot (the all-T 16-mer has a counter of its own)
 
 __device__ __forceinline__ void wave_lds_sync() {  // the wave's LDS writes before its reads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1570,8 +1569,12 @@ __device__ __forceinline__ void wave_lds_sync() {  // the wave's LDS writes befo
 __device__ __forceinline__ uint32_t wave_hash(uint32_t key) {
     // xor-fold + one 24-bit multiply (full rate; a 32-bit mul_lo is quarter rate, and this
     // kernel is bound by issue): k-mers of consecutive positions are shifts of each other
+    // (the compiler turns __umul24 of a masked operand into a quarter-rate v_mul_lo_u32;
+    // the 24-bit multiply is spelled out)
     const uint32_t x = key ^ (key >> 14) ^ (key >> 25);
-    return (__umul24(x & 0xFFFFFFu, 0x9E3779u) >> 12) & (kWaveSlots - 1);
+    uint32_t m;
+    asm("v_mul_u32_u24 %0, %1, %2" : "=v"(m) : "v"(x), "v"(0x9E3779u));
+    return (m >> 12) & (kWaveSlots - 1);
 }
 
 __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_kmer_wave(const GroupDesc* __restrict__ gdesc, int64_t G,
@@ -1584,17 +1587,24 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
                                                            uint16_t* __restrict__ t_cnt, int64_t* __restrict__ gcount,
                                                            unsigned long long* __restrict__ gstat) {
     constexpr int kBuf = kWaveWords;
-    static_assert(kWaveValid * 8 + kWaveValid * 4 <= kWaveSlots * 8, "entries + bucketed keys fit the table");
-    __shared__ unsigned long long s_tab[kWaveWG][kWaveSlots];
+    static_assert(2 * kWaveValid <= kWaveSlots, "entries + bucketed keys fit the key table");
+    // per wave: keys TK[kWaveSlots], then count | exts TV[kWaveSlots + 1] (TV[kWaveSlots]: the
+    // all-T key at k_eff 16, whose key equals the empty mark)
+    __shared__ uint32_t s_tab[kWaveWG][2 * kWaveSlots + 4];
     __shared__ __attribute__((aligned(16))) uint64_t s_buf[kWaveWG][kBuf + 2];
     static_assert((kBuf + 2) * 8 >= 256 * 4, "the rank sort's 256 bucket heads fit the words' LDS");
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    unsigned long long* const T = s_tab[wv];
+    uint32_t* const TK = s_tab[wv];
+    uint32_t* const TV = TK + kWaveSlots;
     uint64_t* const W = s_buf[wv];
     const uint32_t kmask = K >= 16 ? 0xFFFFFFFFu : (1u << (2 * K)) - 1u;
     // the rank sort's bucket: the key's top 8 bits, and never its last base (bsh >= 2)
     const int bsh = 2 * K - 8 >= 2 ? 2 * K - 8 : 2;
-    for (int i = lane; i < kWaveSlots; i += 64) T[i] = kWEmpty;
+    for (int i = lane; i < kWaveSlots; i += 64) {
+        TK[i] = kWEmpty;
+        TV[i] = 0u;
+    }
+    if (lane == 0) TV[kWaveSlots] = 0u;
     const int64_t n_chunks = (G + 63) >> 6;
     const int64_t nw = (int64_t)gridDim.x * kWaveWG;
     int64_t ch = (int64_t)blockIdx.x * kWaveWG + wv;
@@ -1705,18 +1715,17 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
             return o ? (w0 << o) | (w1 >> (64 - o)) : w0;
         };
         // a rolling window: win holds the 32 bases from the lane's position p and nwd the
-        // packed word that supplies base p + 32, so a step shifts one base in and reads LDS
-        // once per 32 positions (the CAS is the trip's only LDS access on its chain); the
-        // segment's start state is kept for the wrap of the rotation
+        // packed word that supplies base p + 32, so a step shifts one base in; the next
+        // position's word is read before the trip's CAS, whose wait covers it (no LDS read
+        // of its own on the trip's chain). The segment's start window is kept for the wrap.
         const uint32_t wrapb = nst > 0 && pst > 0 ? base_at(pst - 1) : 0u;
         uint32_t prevb = nst > 0 && pst + rot > 0 ? base_at(pst + rot - 1) : 0u;
-        uint64_t win = 0, nwd = 0, win_s = 0, nwd_s = 0;
+        uint64_t win = 0, nwd = 0, win_s = 0;
         int p = pst + rot;
         if (nst > 0) {
             win_s = win_at(pst);
-            nwd_s = W[wo_r + (pst >> 5) + 1];
             win = rot ? win_at(p) : win_s;
-            nwd = rot ? W[wo_r + (p >> 5) + 1] : nwd_s;
+            nwd = W[wo_r + (p >> 5) + 1];
         }
         uint32_t claims = 0;
         bool over = false;
@@ -1726,37 +1735,28 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
                 const uint32_t key = (uint32_t)(win >> (64 - 2 * K)) & kmask;
                 uint32_t e = p > 0 ? 1u << prevb : 0u;
                 if (p + K < len_r) e |= 1u << (4 + ((uint32_t)(win >> (62 - 2 * K)) & 3u));
-                prevb = (uint32_t)(win >> 62);
                 uint32_t h = wave_hash(key);
-                const unsigned long long mine = ((unsigned long long)key << 32) | (1ull << 8) | e;
-                // the next position's window (its LDS word read, if any, overlaps the CAS)
-                const int o = p & 31;
-                win = (win << 2) | ((nwd >> (62 - 2 * o)) & 3u);
-                if (o == 31) nwd = W[wo_r + ((p + 1) >> 5) + 1];
-                if (++p == pst + nst) {
-                    p = pst;
-                    win = win_s;
-                    nwd = nwd_s;
-                    prevb = wrapb;
-                }
-                unsigned long long v;
-                while (true) {
-                    v = atomicCAS(&T[h], kWEmpty, mine);
-                    if (v == kWEmpty || (uint32_t)(v >> 32) == key) break;
-                    h = (h + 1) & (kWaveSlots - 1);
-                }
-                fresh = v == kWEmpty;
-                if (!fresh) {
-                    if ((e & ~(uint32_t)v & 0xFFu) == 0) {
-                        atomicAdd(&T[h], 1ull << 8);  // no new extension: count only
-                    } else {
-                        while (true) {
-                            const unsigned long long w2 = atomicCAS(&T[h], v, (v + (1ull << 8)) | e);
-                            if (w2 == v) break;
-                            v = w2;
-                        }
+                const bool wrap = p + 1 == pst + nst;
+                const int pn = wrap ? pst : p + 1;
+                const uint64_t nwd_n = W[wo_r + (pn >> 5) + 1];
+                // claim or find the key's slot (a 32-bit CAS), then count it: a returning add
+                // whose old value shows whether the extension bits are new (then an OR)
+                uint32_t hv = kWaveSlots;
+                if (key != kWEmpty) {
+                    uint32_t v = atomicCAS(&TK[h], kWEmpty, key);
+                    while (v != kWEmpty && v != key) {
+                        h = (h + 1) & (kWaveSlots - 1);
+                        v = atomicCAS(&TK[h], kWEmpty, key);
                     }
+                    fresh = v == kWEmpty;
+                    hv = h;
                 }
+                const uint32_t old = atomicAdd(&TV[hv], 1u << 8);
+                if (e & ~old & 0xFFu) atomicOr(&TV[hv], e);
+                prevb = wrap ? wrapb : (uint32_t)(win >> 62);
+                win = wrap ? win_s : (win << 2) | ((nwd >> (62 - 2 * (p & 31))) & 3u);
+                nwd = nwd_n;
+                p = pn;
             }
             claims += (uint32_t)__popcll(__ballot(fresh));
             if (claims > (uint32_t)kWaveClaim) {
@@ -1766,21 +1766,31 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
         }
         wave_lds_sync();
         KT(1);
-        // CountFilter: the valid entries compacted IN PLACE to the front of the table (key << 32 |
+        // CountFilter: the valid entries compacted IN PLACE to the front of the two arrays (key;
         // count | exts << 16; a chunk's 64 slots are read before any entry is written, and entries
         // only move down); the table is rebuilt empty after the group, and the censoring below
         // looks neighbours up in the bucketed keys instead of the hash table
         uint32_t nv = 0;
         if (!over) {
             for (int s0 = 0; s0 < kWaveSlots; s0 += 64) {
-                const unsigned long long v = T[s0 + lane];
-                const uint32_t cnt = (uint32_t)(v >> 8) & 0xFFFFFFu;
-                const bool ok = v != kWEmpty && (int64_t)min(cnt, 0xFFFFu) >= min_cov;
+                const uint32_t k = TK[s0 + lane], v = TV[s0 + lane];
+                const uint32_t cnt = v >> 8;
+                const bool ok = k != kWEmpty && (int64_t)min(cnt, 0xFFFFu) >= min_cov;
                 const uint64_t bm = __ballot(ok);
                 const uint32_t at = nv + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
-                if (ok && at < (uint32_t)kWaveValid)
-                    T[at] = (v & 0xFFFFFFFF00000000ull) | min(cnt, 0xFFFFu) | ((uint64_t)(v & 0xFFu) << 16);
+                if (ok && at < (uint32_t)kWaveValid) {
+                    TK[at] = k;
+                    TV[at] = min(cnt, 0xFFFFu) | ((v & 0xFFu) << 16);
+                }
                 nv += (uint32_t)__popcll(bm);
+            }
+            const uint32_t vt = TV[kWaveSlots];  // the all-T key (the largest key: it ranks last)
+            if ((int64_t)min(vt >> 8, 0xFFFFu) >= min_cov && vt >= (1u << 8)) {
+                if (lane == 0 && nv < (uint32_t)kWaveValid) {
+                    TK[nv] = kWEmpty;
+                    TV[nv] = min(vt >> 8, 0xFFFFu) | ((vt & 0xFFu) << 16);
+                }
+                ++nv;
             }
             if (nv > (uint32_t)kWaveValid) over = true;
         }
@@ -1793,17 +1803,16 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
             // bucket's start + the keys of its bucket below it) and the censoring's neighbour
             // lookups (a valid neighbour is one of K2's keys). bsh >= 2, so the four right
             // neighbours of a key share a bucket: one scan decides its four right bits.
-            uint32_t* const K2 = reinterpret_cast<uint32_t*>(T + kWaveValid);
+            uint32_t* const K2 = TK + kWaveValid;
             uint32_t* const C = reinterpret_cast<uint32_t*>(W);  // the words are dead by now
             reinterpret_cast<uint4*>(C)[lane] = make_uint4(0u, 0u, 0u, 0u);
             wave_lds_sync();
             KT(2);
             bool deep = false;  // a bucket past 255 entries (adversarial keys): class 3
             for (uint32_t i = lane; i < nv; i += 64) {
-                const unsigned long long v = T[i];
-                const uint32_t li = atomicAdd(&C[(uint32_t)(v >> 32) >> bsh & 255u], 1u);
+                const uint32_t li = atomicAdd(&C[TK[i] >> bsh & 255u], 1u);
                 deep |= li > 255u;
-                T[i] = v | ((unsigned long long)min(li, 255u) << 24);
+                TV[i] |= min(li, 255u) << 24;
             }
             if (__ballot(deep)) {
                 over = true;
@@ -1831,9 +1840,8 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
                 reinterpret_cast<uint4*>(C)[lane] = o4;
                 wave_lds_sync();
                 for (uint32_t i = lane; i < nv; i += 64) {
-                    const unsigned long long v = T[i];
-                    const uint32_t b = (uint32_t)(v >> 32) >> bsh & 255u;
-                    K2[(C[b] & 0xFFFFu) + ((uint32_t)(v >> 24) & 0xFFu)] = (uint32_t)(v >> 32);
+                    const uint32_t k = TK[i];
+                    K2[(C[k >> bsh & 255u] & 0xFFFFu) + (TV[i] >> 24)] = k;
                 }
                 wave_lds_sync();
                 KT(3);
@@ -1842,8 +1850,7 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
                 for (uint32_t i0 = 0; i0 < nv; i0 += 64) {
                     const uint32_t i = i0 + lane;
                     const bool live = i < nv;
-                    const unsigned long long v = live ? T[i] : 0ull;
-                    const uint32_t key = (uint32_t)(v >> 32);
+                    const uint32_t key = live ? TK[i] : 0u, v = live ? TV[i] : 0u;
                     bool tm = false, is = false;
                     if (live) {
                         const uint32_t ex = (uint32_t)(v >> 16) & 0xFFu;
@@ -1894,7 +1901,11 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
             gstat[5 * g + 4] = iso;
         }
         wave_lds_sync();
-        for (int i = lane; i < kWaveSlots; i += 64) T[i] = kWEmpty;
+        for (int i = lane; i < kWaveSlots; i += 64) {
+            TK[i] = kWEmpty;
+            TV[i] = 0u;
+        }
+        if (lane == 0) TV[kWaveSlots] = 0u;
         wave_lds_sync();
         KT(5);
         g = g1;

@@ -33,7 +33,7 @@ THREADS = min(16, os.cpu_count() or 1)
 
 
 INJECT = ((15, "random"), (40, "random"), (100, "random"), (250, "template"), (700, "template"),
-          (18, "multi3"), (24, "multi4"), (64, "multi4"), (65, "template"))
+          (18, "multi3"), (24, "multi4"), (64, "multi4"), (65, "template"), (20, "polyT"))
 
 
 def _inject(reads, codes, rng):
@@ -41,7 +41,8 @@ def _inject(reads, codes, rng):
     k-mers past the wave class's and class 3's / class 1's tables), one template (class 4, the
     global radix path, and 65 rows: one past the wave class), and 3 / 4 templates of 6 clean
     copies each (k_eff 16, min_coverage <= 6: ~405 / ~540 valid k-mers, the latter past the
-    wave class's 512-entry sort; 64 rows: the wave class's row bound)."""
+    wave class's 512-entry sort; 64 rows: the wave class's row bound), and one template with
+    a 90-base run of T (the all-T 16-mer, whose key is the wave table's empty mark)."""
     n = len(codes)
     acgt = np.frombuffer(b"ACGT", np.uint8)
     rows = rng.choice(n, size=sum(sz for sz, _ in INJECT), replace=False)
@@ -63,6 +64,8 @@ def _inject(reads, codes, rng):
                 reads[r] = tpls[j % len(tpls)]
         else:
             tpl = acgt[rng.integers(0, 4, size=RL + 60)]
+            if kind == "polyT":
+                tpl[40:130] = ord("T")
             for j, r in enumerate(sel):
                 a = int(rng.integers(0, 60))
                 reads[r] = tpl[a:a + RL]
