@@ -1588,14 +1588,16 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
                                                            unsigned long long* __restrict__ gstat) {
     constexpr int kBuf = kWaveWords;
     static_assert(2 * kWaveValid <= kWaveSlots, "entries + bucketed keys fit the key table");
-    // per wave: keys TK[kWaveSlots], then count | exts TV[kWaveSlots + 1] (TV[kWaveSlots]: the
-    // all-T key at k_eff 16, whose key equals the empty mark)
-    __shared__ uint32_t s_tab[kWaveWG][2 * kWaveSlots + 4];
+    // per wave: keys TK[kWaveSlots + 1], then count | exts TV[kWaveSlots + 1]. Slot kWaveSlots
+    // is the all-T key's at k_eff 16 (its key equals the empty mark): TK[kWaveSlots] stays
+    // empty, so its CAS finds "empty" at once and its count lands in TV[kWaveSlots]
+    constexpr int kTV = kWaveSlots + 4;
+    __shared__ uint32_t s_tab[kWaveWG][kTV + kWaveSlots + 4];
     __shared__ __attribute__((aligned(16))) uint64_t s_buf[kWaveWG][kBuf + 2];
     static_assert((kBuf + 2) * 8 >= 256 * 4, "the rank sort's 256 bucket heads fit the words' LDS");
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t* const TK = s_tab[wv];
-    uint32_t* const TV = TK + kWaveSlots;
+    uint32_t* const TV = TK + kTV;
     uint64_t* const W = s_buf[wv];
     const uint32_t kmask = K >= 16 ? 0xFFFFFFFFu : (1u << (2 * K)) - 1u;
     // the rank sort's bucket: the key's top 8 bits, and never its last base (bsh >= 2)
@@ -1604,7 +1606,10 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
         TK[i] = kWEmpty;
         TV[i] = 0u;
     }
-    if (lane == 0) TV[kWaveSlots] = 0u;
+    if (lane == 0) {
+        TK[kWaveSlots] = kWEmpty;
+        TV[kWaveSlots] = 0u;
+    }
     const int64_t n_chunks = (G + 63) >> 6;
     const int64_t nw = (int64_t)gridDim.x * kWaveWG;
     int64_t ch = (int64_t)blockIdx.x * kWaveWG + wv;
@@ -1695,7 +1700,8 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) maxn = max(maxn, __shfl_xor(maxn, m));
         const int spr = nrows > 0 ? max(1, 64 / nrows) : 1;
-        const int Ls = (maxn + spr - 1) / spr;
+        // (uniform: the trip loop and its exit stay scalar branches)
+        const int Ls = __builtin_amdgcn_readfirstlane((maxn + spr - 1) / spr);
         const int r = lane / spr;
         const int seg = lane - r * spr;
         const int rs = r < nrows ? r : 0;
@@ -1741,20 +1747,21 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
                 const uint64_t nwd_n = W[wo_r + (pn >> 5) + 1];
                 // claim or find the key's slot (a 32-bit CAS), then count it: a returning add
                 // whose old value shows whether the extension bits are new (then an OR)
-                uint32_t hv = kWaveSlots;
-                if (key != kWEmpty) {
-                    uint32_t v = atomicCAS(&TK[h], kWEmpty, key);
-                    while (v != kWEmpty && v != key) {
-                        h = (h + 1) & (kWaveSlots - 1);
-                        v = atomicCAS(&TK[h], kWEmpty, key);
-                    }
-                    fresh = v == kWEmpty;
-                    hv = h;
+                const bool allt = key == kWEmpty;
+                h = allt ? (uint32_t)kWaveSlots : h;
+                uint32_t v = atomicCAS(&TK[h], kWEmpty, key);
+                while (v != kWEmpty && v != key) {
+                    h = (h + 1) & (kWaveSlots - 1);
+                    v = atomicCAS(&TK[h], kWEmpty, key);
                 }
-                const uint32_t old = atomicAdd(&TV[hv], 1u << 8);
-                if (e & ~old & 0xFFu) atomicOr(&TV[hv], e);
+                fresh = v == kWEmpty && !allt;
+                const uint32_t old = atomicAdd(&TV[h], 1u << 8);
+                if (e & ~old & 0xFFu) atomicOr(&TV[h], e);
+                // the next position (a wrap restarts the segment): selects by masks, no branch
+                const uint64_t wm = 0ull - (uint64_t)wrap;
+                const uint64_t nxt = (win << 2) | ((nwd >> (62 - 2 * (p & 31))) & 3u);
                 prevb = wrap ? wrapb : (uint32_t)(win >> 62);
-                win = wrap ? win_s : (win << 2) | ((nwd >> (62 - 2 * (p & 31))) & 3u);
+                win = (nxt & ~wm) | (win_s & wm);
                 nwd = nwd_n;
                 p = pn;
             }
