@@ -1552,7 +1552,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
 #endif
 constexpr bool kWavePath = ROGTK_KMER_WAVE;
 constexpr int kWaveSlots = 1024;   // table slots per wave (8 KB)
-constexpr int kWaveClaim = 768;    // distinct k-mers (the table stays <= 75% + one trip full)
+constexpr int kWaveClaim = 768;    // distinct k-mers (checked every 2 trips: <= 896 of 1024 slots)
 constexpr int kWaveRows = 64;      // one row per lane
 constexpr int kWaveWords = 192;    // packed words (38 rows of <= 160 bases at stride 5)
 constexpr int kWaveValid = 512;    // valid k-mers (compacted to the table's front; keys bucketed behind them)
@@ -1735,8 +1735,9 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
         }
         uint32_t claims = 0;
         bool over = false;
-        for (int t = 0; t < Ls; ++t) {
-            bool fresh = false;
+        // one insert step of the lane's segment; returns the wave's new claims
+        auto step = [&](int t) -> uint32_t {
+            uint32_t v = 0u, allt = 1u;  // (a lane past its segment claims nothing)
             if (t < nst) {
                 const uint32_t key = (uint32_t)(win >> (64 - 2 * K)) & kmask;
                 uint32_t e = p > 0 ? 1u << prevb : 0u;
@@ -1747,14 +1748,13 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
                 const uint64_t nwd_n = W[wo_r + (pn >> 5) + 1];
                 // claim or find the key's slot (a 32-bit CAS), then count it: a returning add
                 // whose old value shows whether the extension bits are new (then an OR)
-                const bool allt = key == kWEmpty;
+                allt = key == kWEmpty;
                 h = allt ? (uint32_t)kWaveSlots : h;
-                uint32_t v = atomicCAS(&TK[h], kWEmpty, key);
+                v = atomicCAS(&TK[h], kWEmpty, key);
                 while (v != kWEmpty && v != key) {
                     h = (h + 1) & (kWaveSlots - 1);
                     v = atomicCAS(&TK[h], kWEmpty, key);
                 }
-                fresh = v == kWEmpty && !allt;
                 const uint32_t old = atomicAdd(&TV[h], 1u << 8);
                 if (e & ~old & 0xFFu) atomicOr(&TV[h], e);
                 // the next position (a wrap restarts the segment): selects by masks, no branch
@@ -1765,7 +1765,13 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
                 nwd = nwd_n;
                 p = pn;
             }
-            claims += (uint32_t)__popcll(__ballot(fresh));
+            return (uint32_t)__popcll(__ballot((v == kWEmpty) & (allt == 0u)));
+        };
+        // the claim bound is checked every second step: <= 768 + 128 keys stay below the
+        // table's 1024 slots, so probing always ends
+        for (int t = 0; t < Ls; t += 2) {
+            claims += step(t);
+            if (t + 1 < Ls) claims += step(t + 1);
             if (claims > (uint32_t)kWaveClaim) {
                 over = true;
                 break;
