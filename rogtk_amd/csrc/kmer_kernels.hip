@@ -923,22 +923,56 @@ __global__ __launch_bounds__(kBlock) void k_censor(const uint64_t* __restrict__ 
     }
 }
 
-// dense packing: one wave per group copies its entries to the final offsets
+// dense packing: one wave per group copies its entries to the final offsets, up to 256
+// entries per trip with all their loads issued before the first store (a C3 group at k_eff
+// 16 has ~157 valid k-mers: one trip instead of three dependent ones); V16: the k-mer pairs
+// as one 16-B access (both arrays 16-B aligned)
+template <bool V16>
 __global__ __launch_bounds__(kBlock) void k_pack(const uint64_t* __restrict__ t_kmer, const uint8_t* __restrict__ t_ext,
                                                  const uint16_t* __restrict__ t_cnt, int64_t G,
                                                  const int64_t* __restrict__ cap_off,
                                                  const int64_t* __restrict__ gcount,
                                                  const int64_t* __restrict__ out_off, uint64_t* __restrict__ kmer,
                                                  uint8_t* __restrict__ ext, uint16_t* __restrict__ cnt) {
+    constexpr int kU = 4;
     const int lane = threadIdx.x & 63;
     const int64_t waves = (int64_t)gridDim.x * kWavesPerBlock;
     for (int64_t g = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); g < G; g += waves) {
         const int64_t n = gcount[g], s = cap_off[g], d = out_off[g];
-        for (int64_t t = lane; t < n; t += 64) {
-            kmer[2 * (d + t)] = t_kmer[2 * (s + t)];
-            kmer[2 * (d + t) + 1] = t_kmer[2 * (s + t) + 1];
-            ext[d + t] = t_ext[s + t];
-            cnt[d + t] = t_cnt[s + t];
+        for (int64_t t0 = 0; t0 < n; t0 += 64 * kU) {
+            uint64_t k0[kU], k1[kU];
+            uint8_t e[kU];
+            uint16_t c[kU];
+#pragma unroll
+            for (int j = 0; j < kU; ++j) {
+                const int64_t t = t0 + lane + 64 * j;
+                if (t < n) {
+                    if constexpr (V16) {
+                        const ulonglong2 v = reinterpret_cast<const ulonglong2*>(t_kmer)[s + t];
+                        k0[j] = v.x;
+                        k1[j] = v.y;
+                    } else {
+                        k0[j] = t_kmer[2 * (s + t)];
+                        k1[j] = t_kmer[2 * (s + t) + 1];
+                    }
+                    e[j] = t_ext[s + t];
+                    c[j] = t_cnt[s + t];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kU; ++j) {
+                const int64_t t = t0 + lane + 64 * j;
+                if (t < n) {
+                    if constexpr (V16) {
+                        reinterpret_cast<ulonglong2*>(kmer)[d + t] = make_ulonglong2(k0[j], k1[j]);
+                    } else {
+                        kmer[2 * (d + t)] = k0[j];
+                        kmer[2 * (d + t) + 1] = k1[j];
+                    }
+                    ext[d + t] = e[j];
+                    cnt[d + t] = c[j];
+                }
+            }
         }
     }
 }
@@ -3058,7 +3092,7 @@ int rogtk_kmer_spectrum_host(const void* offsets, int offset_width, const uint8_
         if (int rc = c->o_ext.ensure((size_t)total)) return rc;
         if (int rc = c->o_cnt.ensure((size_t)total * 2)) return rc;
         ROGTK_HIP_CHECK(hipMemcpyAsync(c->out_off.p, entry_offsets, (G + 1) * 8, hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_pack, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, c->t_kmer.as<uint64_t>(),
+        hipLaunchKernelGGL(k_pack<true>, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, c->t_kmer.as<uint64_t>(),
                            c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), G, c->cap_off.as<int64_t>(),
                            c->gcount.as<int64_t>(), c->out_off.as<int64_t>(), c->o_kmer.as<uint64_t>(),
                            c->o_ext.as<uint8_t>(), c->o_cnt.as<uint16_t>());
@@ -3200,9 +3234,15 @@ int spectrum_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* v
                   (long long)*n_entries, (long long)capacity);
     if (*n_entries > 0) {
         ROGTK_REQUIRE(kmers && exts && counts, ROGTK_E_INVALID, "kmer_dev: output arrays are NULL");
-        hipLaunchKernelGGL(k_pack, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, c->t_kmer.as<uint64_t>(),
-                           c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), G, c->cap_off.as<int64_t>(),
-                           c->gcount.as<int64_t>(), entry_offsets, kmers, exts, counts);
+        // the caller's k-mer array may sit at any 8-B offset of its buffer
+        if (((uintptr_t)kmers & 15u) == 0)
+            hipLaunchKernelGGL(k_pack<true>, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, c->t_kmer.as<uint64_t>(),
+                               c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), G, c->cap_off.as<int64_t>(),
+                               c->gcount.as<int64_t>(), entry_offsets, kmers, exts, counts);
+        else
+            hipLaunchKernelGGL(k_pack<false>, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, c->t_kmer.as<uint64_t>(),
+                               c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), G, c->cap_off.as<int64_t>(),
+                               c->gcount.as<int64_t>(), entry_offsets, kmers, exts, counts);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     return ROGTK_OK;
