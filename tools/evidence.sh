@@ -27,6 +27,8 @@ else
     rm -rf gpurun_out/prof_bench
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/c3trace -o run --output-format csv -- python3 tools/bench_kmer.py --reads 100000000 --steps 2 --warmup 1 > $O/c3_trace.log 2>&1
     rc=$?; echo "c3 trace rc=$rc"; find $O/c3trace -name '*kernel_trace.csv' -delete; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/c3k16trace -o run --output-format csv -- python3 tools/bench_kmer.py --reads 100000000 --k 15 --min-coverage 5 --steps 2 --warmup 1 > $O/c3k16_trace.log 2>&1
+    rc=$?; echo "c3 k16 trace rc=$rc"; find $O/c3k16trace -name '*kernel_trace.csv' -delete; [ $rc -eq 0 ] || exit $rc
     timeout -k 10 240 python3 tools/bench_kmer.py --reads 100000000 --steps 3 --warmup 1 > $O/c3.log 2>&1
     rc=$?; echo "c3 rc=$rc"; [ $rc -eq 0 ] || exit $rc
     timeout -k 10 300 python3 tools/bench_kmer.py --reads 100000000 --k 15 --min-coverage 5 --steps 3 --warmup 1 > $O/c3_k16.log 2>&1
