@@ -1581,17 +1581,23 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
 // The next group's descriptor and packed words are loaded into registers while the current
 // group is processed (the descriptor two groups ahead), so a group waits on HBM only when
 // its chunk of 64 groups starts.
-#ifndef ROGTK_KMER_WAVE
-#define ROGTK_KMER_WAVE 1  // 0: no class 2 (experiment builds: the workgroup kernels take every group)
-#endif
-constexpr bool kWavePath = ROGTK_KMER_WAVE;
-constexpr int kWaveSlots = 1024;   // table slots per wave (8 KB)
-constexpr int kWaveClaim = 768;    // distinct k-mers (checked every 2 trips: <= 896 of 1024 slots)
-constexpr int kWaveRows = 64;      // one row per lane
-constexpr int kWaveWords = 192;    // packed words (38 rows of <= 160 bases at stride 5)
-constexpr int kWaveValid = 512;    // valid k-mers (compacted to the table's front; keys bucketed behind them)
-constexpr int kWaveWG = 2;         // waves per workgroup (24.5 KB of LDS: 6 workgroups per CU)
-constexpr int kWaveWPL = (kWaveWords + 63) / 64;  // prefetched words per lane
+// Two instances: 1024 slots (class 2), and 2048 (class 6) for the groups past class 2's
+// claim bound or packed words: at C3's UMI collision rate a group of 22-38 rows often holds
+// 2-3 molecules' reads, past 768 distinct k-mers (~7% of the k_eff-16 work went to the
+// workgroup kernel before the big instance)
+constexpr int kWaveRows = 64;       // one row per lane
+constexpr uint8_t kClsWaveBig = 6;  // the 2048-slot instance's class
+template <int SLOTS>
+struct WaveCfg {
+    static constexpr int kSlots = SLOTS;          // table slots per wave (8 / 16 KB)
+    static constexpr int kClaim = SLOTS * 3 / 4;  // distinct k-mers (checked every 2 trips: <= 7/8 of the slots)
+    static constexpr int kValid = SLOTS / 2;      // valid k-mers (compacted to the front; keys bucketed behind them)
+    static constexpr int kWords = SLOTS == 1024 ? 192 : 320;  // packed words (38 / 64 rows at stride 5)
+    static constexpr int kWG = SLOTS == 1024 ? 2 : 1;          // waves per workgroup (8 workgroups per CU)
+    static constexpr int kWPL = (kWords + 63) / 64;            // prefetched words per lane
+    static constexpr uint8_t kCls = SLOTS == 1024 ? 2 : kClsWaveBig;
+};
+constexpr int kWaveWords = WaveCfg<1024>::kWords, kWaveBigWords = WaveCfg<2048>::kWords;
 constexpr uint32_t kWEmpty = 0xFFFFFFFFu;  // an empty key slot (the all-T 16-mer has a counter of its own)
 
 __device__ __forceinline__ void wave_lds_sync() {  // the wave's LDS writes before its reads
@@ -1600,6 +1606,7 @@ __device__ __forceinline__ void wave_lds_sync() {  // the wave's LDS writes befo
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+template <int SLOTS>
 __device__ __forceinline__ uint32_t wave_hash(uint32_t key) {
     // xor-fold + one 24-bit multiply (full rate; a 32-bit mul_lo is quarter rate, and this
     // kernel is bound by issue): k-mers of consecutive positions are shifts of each other
@@ -1608,10 +1615,11 @@ __device__ __forceinline__ uint32_t wave_hash(uint32_t key) {
     const uint32_t x = key ^ (key >> 14) ^ (key >> 25);
     uint32_t m;
     asm("v_mul_u32_u24 %0, %1, %2" : "=v"(m) : "v"(x), "v"(0x9E3779u));
-    return (m >> 12) & (kWaveSlots - 1);
+    return (m >> 12) & (SLOTS - 1);
 }
 
-__global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_kmer_wave(const GroupDesc* __restrict__ gdesc, int64_t G,
+template <int SLOTS>
+__global__ __launch_bounds__(64 * WaveCfg<SLOTS>::kWG) __attribute__((amdgpu_waves_per_eu(SLOTS == 1024 ? 4 : 2, 8))) void k_kmer_wave(const GroupDesc* __restrict__ gdesc, int64_t G,
                                                            uint8_t* __restrict__ gsmall, int K, int64_t min_cov,
                                                            const int32_t* __restrict__ row_len,
                                                            const int64_t* __restrict__ woff, int stride,
@@ -1620,7 +1628,10 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
                                                            uint64_t* __restrict__ t_kmer, uint8_t* __restrict__ t_ext,
                                                            uint16_t* __restrict__ t_cnt, int64_t* __restrict__ gcount,
                                                            unsigned long long* __restrict__ gstat) {
-    constexpr int kBuf = kWaveWords;
+    using WC = WaveCfg<SLOTS>;
+    constexpr int kWaveSlots = WC::kSlots, kWaveClaim = WC::kClaim, kWaveValid = WC::kValid, kWaveWG = WC::kWG,
+                  kWaveWPL = WC::kWPL;
+    constexpr int kBuf = WC::kWords;
     static_assert(2 * kWaveValid <= kWaveSlots, "entries + bucketed keys fit the key table");
     // per wave: keys TK[kWaveSlots + 1], then count | exts TV[kWaveSlots + 1]. Slot kWaveSlots
     // is the all-T key's at k_eff 16 (its key equals the empty mark): TK[kWaveSlots] stays
@@ -1647,7 +1658,7 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
     const int64_t n_chunks = (G + 63) >> 6;
     const int64_t nw = (int64_t)gridDim.x * kWaveWG;
     int64_t ch = (int64_t)blockIdx.x * kWaveWG + wv;
-    uint64_t own = ch < n_chunks ? __ballot((ch << 6) + lane < G && gsmall[(ch << 6) + lane] == 2) : 0ull;
+    uint64_t own = ch < n_chunks ? __ballot((ch << 6) + lane < G && gsmall[(ch << 6) + lane] == WC::kCls) : 0ull;
     // the next group of this class for this wave (-1: none); loads the chunk's classes as needed
     auto next_group = [&]() -> int64_t {
         while (true) {
@@ -1658,7 +1669,7 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
             }
             ch += nw;
             if (ch >= n_chunks) return -1;
-            own = __ballot((ch << 6) + lane < G && gsmall[(ch << 6) + lane] == 2);
+            own = __ballot((ch << 6) + lane < G && gsmall[(ch << 6) + lane] == WC::kCls);
         }
     };
     // prefetch state of the next group: its row (lane) and packed words in registers
@@ -1776,7 +1787,7 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
                 const uint32_t key = (uint32_t)(win >> (64 - 2 * K)) & kmask;
                 uint32_t e = p > 0 ? 1u << prevb : 0u;
                 if (p + K < len_r) e |= 1u << (4 + ((uint32_t)(win >> (62 - 2 * K)) & 3u));
-                uint32_t h = wave_hash(key);
+                uint32_t h = wave_hash<SLOTS>(key);
                 const bool wrap = p + 1 == pst + nst;
                 const int pn = wrap ? pst : p + 1;
                 const uint64_t nwd_n = W[wo_r + (pn >> 5) + 1];
@@ -1940,7 +1951,8 @@ __global__ __launch_bounds__(64 * kWaveWG) __attribute__((amdgpu_waves_per_eu(4,
                 }
             }
         }
-        if (over && lane == 0) gsmall[g] = 3;  // more than the wave path takes: class 3 (launched next) redoes it
+        // more than this instance takes: the 2048-slot instance (launched next) or class 3 redoes it
+        if (over && lane == 0) gsmall[g] = SLOTS == 1024 && nwords <= kWaveBigWords ? kClsWaveBig : 3;
         KT(4);
         if (lane == 0 && !over) {
             gcount[g] = nv;
@@ -2019,6 +2031,7 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
             cls = kClsEmpty;
         } else if (K <= 32 && obs > 0) {
             if (wave && K <= 16 && nrows <= kWaveRows && words <= kWaveWords) cls = 2;
+            else if (wave && K <= 16 && nrows <= kWaveRows && words <= kWaveBigWords) cls = kClsWaveBig;
             else if (nrows <= LdsCfg<3>::kRows && words <= LdsCfg<3>::kWords) cls = 3;
             else if (nrows <= LdsCfg<1>::kRows && words <= LdsCfg<1>::kWords) cls = 1;
             else if (nrows <= LdsCfg<4>::kRows && words <= LdsCfg<4>::kWords) cls = 4;
@@ -2720,7 +2733,7 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
         hipLaunchKernelGGL(k_group_classify, dim3(grid_for(G * kClsLanes, 16384)), dim3(kBlock), 0, s, go, G, in.gk,
                            K, c->row_obs.as<int64_t>(), c->row_words.as<int64_t>(), c->woff.as<int64_t>(), stride,
                            c->gsmall.as<uint8_t>(), c->gdesc.as<GroupDesc>(), in.cap_fill, min_cov,
-                           stride && kmer_cert_on() ? gstat : nullptr, (int)(kWavePath && c->wave_path && K <= 16));
+                           stride && kmer_cert_on() ? gstat : nullptr, (int)(c->wave_path && K <= 16));
     } else if (in.cap_fill) {
         hipLaunchKernelGGL(k_group_caps_obs, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, go, G,
                            c->row_obs.as<int64_t>(), min_cov, in.cap_fill);
@@ -2740,13 +2753,20 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
                               c->packed.as<uint64_t>(), gstat, g_mz_debug_groups >= G ? g_mz_debug : nullptr);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
-    if (lds && kWavePath && c->wave_path && K <= 16) {
-        // class 2 first: its overflowing groups become class 3 for the launch below
+    if (lds && c->wave_path && K <= 16) {
+        // classes 2 and 6 first: their overflowing groups become class 3 for the launch below
         const int64_t chunks = (G + 63) / 64;
-        ROGTK_TIMED_LAUNCH(K_KMER_WAVE, k_kmer_wave, dim3((unsigned)std::min<int64_t>((chunks + kWaveWG - 1) / kWaveWG, 65536)),
-                           dim3(64 * kWaveWG), 0, s, c->gdesc.as<GroupDesc>(), G, c->gsmall.as<uint8_t>(), K, min_cov,
-                           c->row_len.as<int32_t>(), c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(), in.cap_off,
-                           c->t_kmer.as<uint64_t>(), c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
+        ROGTK_TIMED_LAUNCH(K_KMER_WAVE, k_kmer_wave<1024>,
+                           dim3((unsigned)std::min<int64_t>((chunks + WaveCfg<1024>::kWG - 1) / WaveCfg<1024>::kWG, 65536)),
+                           dim3(64 * WaveCfg<1024>::kWG), 0, s, c->gdesc.as<GroupDesc>(), G, c->gsmall.as<uint8_t>(), K,
+                           min_cov, c->row_len.as<int32_t>(), c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(),
+                           in.cap_off, c->t_kmer.as<uint64_t>(), c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(),
+                           in.gcount, gstat);
+        ROGTK_TIMED_LAUNCH(K_KMER_WAVE, k_kmer_wave<2048>, dim3((unsigned)std::min<int64_t>(chunks, 16384)),
+                           dim3(64 * WaveCfg<2048>::kWG), 0, s, c->gdesc.as<GroupDesc>(), G, c->gsmall.as<uint8_t>(), K,
+                           min_cov, c->row_len.as<int32_t>(), c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(),
+                           in.cap_off, c->t_kmer.as<uint64_t>(), c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(),
+                           in.gcount, gstat);
     }
     if (lds) {
         ProfScope prof(K_KMER_LDS, s, true);
