@@ -875,7 +875,7 @@ __global__ __launch_bounds__(kBlock) void k_censor(const uint64_t* __restrict__ 
                                                    const int64_t* __restrict__ cap_off,
                                                    uint64_t* __restrict__ o_kmer, uint8_t* __restrict__ o_ext,
                                                    uint16_t* __restrict__ o_cnt,
-                                                   unsigned long long* __restrict__ gstat) {
+                                                   unsigned long long* __restrict__ gstat, int lo_only) {
     const uint64_t mask = (WIDE || K == 32) ? ~0ull : ((1ull << (2 * K)) - 1ull);
     for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < nv; j += (int64_t)gridDim.x * kBlock) {
         const uint32_t g = v_grp[j];
@@ -913,8 +913,12 @@ __global__ __launch_bounds__(kBlock) void k_censor(const uint64_t* __restrict__ 
             if (found) ne |= (uint8_t)(1u << bit);
         }
         const int64_t o = cap_off[g] + (j - a0);
-        o_kmer[2 * o] = hi;
-        o_kmer[2 * o + 1] = lo;
+        if (lo_only) {
+            o_kmer[o] = lo;
+        } else {
+            o_kmer[2 * o] = hi;
+            o_kmer[2 * o + 1] = lo;
+        }
         o_ext[o] = ne;
         o_cnt[o] = v_cnt[j];
         const bool l0 = (ne & 0xF) == 0, r0 = (ne >> 4) == 0;
@@ -926,8 +930,9 @@ __global__ __launch_bounds__(kBlock) void k_censor(const uint64_t* __restrict__ 
 // dense packing: one wave per group copies its entries to the final offsets, up to 256
 // entries per trip with all their loads issued before the first store (a C3 group at k_eff
 // 16 has ~157 valid k-mers: one trip instead of three dependent ones); V16: the k-mer pairs
-// as one 16-B access (both arrays 16-B aligned)
-template <bool V16>
+// as one 16-B access (both arrays 16-B aligned); LO: the staged k-mers are one word each
+// (k_eff <= 32), the high word written as 0 here
+template <bool V16, bool LO>
 __global__ __launch_bounds__(kBlock) void k_pack(const uint64_t* __restrict__ t_kmer, const uint8_t* __restrict__ t_ext,
                                                  const uint16_t* __restrict__ t_cnt, int64_t G,
                                                  const int64_t* __restrict__ cap_off,
@@ -947,7 +952,10 @@ __global__ __launch_bounds__(kBlock) void k_pack(const uint64_t* __restrict__ t_
             for (int j = 0; j < kU; ++j) {
                 const int64_t t = t0 + lane + 64 * j;
                 if (t < n) {
-                    if constexpr (V16) {
+                    if constexpr (LO) {
+                        k0[j] = 0ull;
+                        k1[j] = t_kmer[s + t];
+                    } else if constexpr (V16) {
                         const ulonglong2 v = reinterpret_cast<const ulonglong2*>(t_kmer)[s + t];
                         k0[j] = v.x;
                         k1[j] = v.y;
@@ -1060,7 +1068,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
                                                      const int64_t* __restrict__ cap_off,
                                                      uint64_t* __restrict__ t_kmer, uint8_t* __restrict__ t_ext,
                                                      uint16_t* __restrict__ t_cnt, int64_t* __restrict__ gcount,
-                                                     unsigned long long* __restrict__ gstat) {
+                                                     unsigned long long* __restrict__ gstat, int lo_only) {
     using C = LdsCfg<CLS>;
     constexpr int kWaves = TB / 64;
     // every class takes groups of any observation count: their distinct k-mers are
@@ -1369,8 +1377,12 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
                         if (valid_at(nb)) ne |= 1u << bit;
                     }
                     const int64_t o = base + lane;
-                    t_kmer[2 * o] = 0;
-                    t_kmer[2 * o + 1] = key;
+                    if (lo_only) {
+                        t_kmer[o] = key;
+                    } else {
+                        t_kmer[2 * o] = 0;
+                        t_kmer[2 * o + 1] = key;
+                    }
                     t_ext[o] = (uint8_t)ne;
                     t_cnt[o] = (uint16_t)(info & 0xFFFFu);
                     const bool l0 = (ne & 0xFu) == 0, r0b = (ne >> 4) == 0;
@@ -1526,8 +1538,12 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
                 if (valid_at(nb)) ne |= 1u << bit;
             }
             const int64_t o = base + (direct ? rank : i);
-            t_kmer[2 * o] = 0;
-            t_kmer[2 * o + 1] = key;
+            if (lo_only) {
+                t_kmer[o] = key;
+            } else {
+                t_kmer[2 * o] = 0;
+                t_kmer[2 * o + 1] = key;
+            }
             t_ext[o] = (uint8_t)ne;
             t_cnt[o] = (uint16_t)(info & 0xFFFFu);
             const bool l0 = (ne & 0xFu) == 0, r0b = (ne >> 4) == 0;
@@ -1627,7 +1643,7 @@ __global__ __launch_bounds__(64 * WaveCfg<SLOTS>::kWG) __attribute__((amdgpu_wav
                                                            const int64_t* __restrict__ cap_off,
                                                            uint64_t* __restrict__ t_kmer, uint8_t* __restrict__ t_ext,
                                                            uint16_t* __restrict__ t_cnt, int64_t* __restrict__ gcount,
-                                                           unsigned long long* __restrict__ gstat) {
+                                                           unsigned long long* __restrict__ gstat, int lo_only) {
     using WC = WaveCfg<SLOTS>;
     constexpr int kWaveSlots = WC::kSlots, kWaveClaim = WC::kClaim, kWaveValid = WC::kValid, kWaveWG = WC::kWG,
                   kWaveWPL = WC::kWPL;
@@ -1938,8 +1954,12 @@ __global__ __launch_bounds__(64 * WaveCfg<SLOTS>::kWG) __attribute__((amdgpu_wav
                                 }
                         }
                         const int64_t o = base + rank;
-                        t_kmer[2 * o] = 0;
-                        t_kmer[2 * o + 1] = key;
+                        if (lo_only) {
+                            t_kmer[o] = key;
+                        } else {
+                            t_kmer[2 * o] = 0;
+                            t_kmer[2 * o + 1] = key;
+                        }
                         t_ext[o] = (uint8_t)nx;
                         t_cnt[o] = (uint16_t)(v & 0xFFFFu);
                         const bool l0 = (nx & 0xFu) == 0, r0b = (nx >> 4) == 0;
@@ -2566,6 +2586,9 @@ struct KmerCtx {
     DevBuf long_rows;  // block path: grouped rows longer than the staging stride (an error)
     bool lds_path = true;  // rogtk_kmer_set_path(): tests force the global path
     bool wave_path = true;  // rogtk_kmer_set_path(2): the LDS path without class 2 (tests)
+    // the staged k-mers of this call: one word per entry (every group's k_eff <= 32: the
+    // high word is 0 and k_pack writes it) or two (a group of k_eff 64 in the call)
+    bool lo_only = true;
     int64_t last_lds_groups = 0, last_global_groups = 0;  // rogtk_kmer_path_stats()
     int64_t last_cert_groups = 0;                         // rogtk_kmer_certified_groups()
     int64_t last_lds_rows = 0;                            // rogtk_kmer_lds_rows()
@@ -2761,12 +2784,12 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
                            dim3(64 * WaveCfg<1024>::kWG), 0, s, c->gdesc.as<GroupDesc>(), G, c->gsmall.as<uint8_t>(), K,
                            min_cov, c->row_len.as<int32_t>(), c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(),
                            in.cap_off, c->t_kmer.as<uint64_t>(), c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(),
-                           in.gcount, gstat);
+                           in.gcount, gstat, c->lo_only ? 1 : 0);
         ROGTK_TIMED_LAUNCH(K_KMER_WAVE, k_kmer_wave<2048>, dim3((unsigned)std::min<int64_t>(chunks, 16384)),
                            dim3(64 * WaveCfg<2048>::kWG), 0, s, c->gdesc.as<GroupDesc>(), G, c->gsmall.as<uint8_t>(), K,
                            min_cov, c->row_len.as<int32_t>(), c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(),
                            in.cap_off, c->t_kmer.as<uint64_t>(), c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(),
-                           in.gcount, gstat);
+                           in.gcount, gstat, c->lo_only ? 1 : 0);
     }
     if (lds) {
         ProfScope prof(K_KMER_LDS, s, true);
@@ -2774,7 +2797,7 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
                               dim3(kLdsBlock), 0, s, prof.start(), prof.stop(), 0, c->gdesc.as<GroupDesc>(), G,
                               c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
                               c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
-                              c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
+                              c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat, c->lo_only ? 1 : 0);
     }
     if (lds) {
         // one workgroup per small group, straight from the packed rows
@@ -2782,12 +2805,12 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
                            c->gdesc.as<GroupDesc>(), G,
                            c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
                            c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
-                           c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
+                           c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat, c->lo_only ? 1 : 0);
         ROGTK_TIMED_LAUNCH(K_KMER_LDS, (k_kmer_lds<4, kLdsBlock>), dim3((unsigned)std::min<int64_t>((G + 63) / 64, 8192)), dim3(kLdsBlock), 0, s,
                            c->gdesc.as<GroupDesc>(), G,
                            c->gsmall.as<uint8_t>(), K, min_cov, c->row_len.as<int32_t>(),
                            c->woff.as<int64_t>(), stride, c->packed.as<uint64_t>(), in.cap_off, c->t_kmer.as<uint64_t>(),
-                           c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat);
+                           c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), in.gcount, gstat, c->lo_only ? 1 : 0);
     }
     // the groups per path first: with none on the global path (the usual C3 call, every
     // group in LDS or certified empty) its row drop and observation scan are skipped
@@ -2905,7 +2928,7 @@ int run_class(KmerCtx* c, const KIn& in, int64_t n_rows, int64_t G, int K, int64
                        c->v_hi.as<uint64_t>(), c->v_grp.as<uint32_t>(), c->v_ext.as<uint8_t>(),
                        c->v_cnt.as<uint16_t>(), nv, K, c->gstart.as<int64_t>(), in.gcount,
                        in.cap_off, c->t_kmer.as<uint64_t>(), c->t_ext.as<uint8_t>(),
-                       c->t_cnt.as<uint16_t>(), gstat);
+                       c->t_cnt.as<uint16_t>(), gstat, c->lo_only ? 1 : 0);
     ROGTK_HIP_CHECK(hipGetLastError());
     return ROGTK_OK;
 }
@@ -3094,6 +3117,7 @@ int rogtk_kmer_spectrum_host(const void* offsets, int offset_width, const uint8_
     const KIn in{c->offsets.as<int64_t>(), c->values.as<uint8_t>(), validity ? c->validity.as<uint8_t>() : nullptr,
                  0, nullptr, c->go.as<int64_t>(), c->gk.as<uint8_t>(), c->cap_off.as<int64_t>(),
                  c->gstat.as<unsigned long long>(), c->gcount.as<int64_t>()};
+    c->lo_only = !present[64];
     for (int K : {4, 8, 16, 32, 64}) {
         if (!present[K] || n_rows == 0) continue;
         if (int rc = run_any<8>(c, in, n_rows, G, K, min_coverage, s, &gk)) return rc;
@@ -3112,7 +3136,8 @@ int rogtk_kmer_spectrum_host(const void* offsets, int offset_width, const uint8_
         if (int rc = c->o_ext.ensure((size_t)total)) return rc;
         if (int rc = c->o_cnt.ensure((size_t)total * 2)) return rc;
         ROGTK_HIP_CHECK(hipMemcpyAsync(c->out_off.p, entry_offsets, (G + 1) * 8, hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_pack<true>, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, c->t_kmer.as<uint64_t>(),
+        auto pack = c->lo_only ? k_pack<true, true> : k_pack<true, false>;
+        hipLaunchKernelGGL(pack, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, c->t_kmer.as<uint64_t>(),
                            c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), G, c->cap_off.as<int64_t>(),
                            c->gcount.as<int64_t>(), c->out_off.as<int64_t>(), c->o_kmer.as<uint64_t>(),
                            c->o_ext.as<uint8_t>(), c->o_cnt.as<uint16_t>());
@@ -3238,6 +3263,7 @@ int spectrum_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* v
         in.fused = fused;
         in.vlen = vlen;
         if (blocks || fused) in.cap_fill = c->caps.as<int64_t>();
+        c->lo_only = K <= 32;
         if (int rc = run_any<8>(c, in, n_rows, G, K, min_coverage, s, nullptr)) return rc;
     }
     if (int rc = cub_exsum_i64(c, c->gcount.as<int64_t>(), entry_offsets, G, s)) return rc;
@@ -3255,14 +3281,12 @@ int spectrum_dev(const int64_t* offsets, const uint8_t* values, const uint8_t* v
     if (*n_entries > 0) {
         ROGTK_REQUIRE(kmers && exts && counts, ROGTK_E_INVALID, "kmer_dev: output arrays are NULL");
         // the caller's k-mer array may sit at any 8-B offset of its buffer
-        if (((uintptr_t)kmers & 15u) == 0)
-            hipLaunchKernelGGL(k_pack<true>, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, c->t_kmer.as<uint64_t>(),
-                               c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), G, c->cap_off.as<int64_t>(),
-                               c->gcount.as<int64_t>(), entry_offsets, kmers, exts, counts);
-        else
-            hipLaunchKernelGGL(k_pack<false>, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, c->t_kmer.as<uint64_t>(),
-                               c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), G, c->cap_off.as<int64_t>(),
-                               c->gcount.as<int64_t>(), entry_offsets, kmers, exts, counts);
+        const bool v16 = ((uintptr_t)kmers & 15u) == 0;
+        auto pack = c->lo_only ? (v16 ? k_pack<true, true> : k_pack<false, true>)
+                               : (v16 ? k_pack<true, false> : k_pack<false, false>);
+        hipLaunchKernelGGL(pack, dim3(grid_for(G * 64, 16384)), dim3(kBlock), 0, s, c->t_kmer.as<uint64_t>(),
+                           c->t_ext.as<uint8_t>(), c->t_cnt.as<uint16_t>(), G, c->cap_off.as<int64_t>(),
+                           c->gcount.as<int64_t>(), entry_offsets, kmers, exts, counts);
         ROGTK_HIP_CHECK(hipGetLastError());
     }
     return ROGTK_OK;
