@@ -180,6 +180,85 @@ Graph make_graph(const Spectrum& s, int64_t min_cov) {
 inline int popc4(unsigned x) { return __builtin_popcount(x & 0xFu); }
 inline int ctz4(unsigned x) { return __builtin_ctz(x & 0xFu); }
 
+// compress()'s walks without building every contig: the last longest path of at least
+// min_len bases (assemble_graph's min_length + only_largest: max_by_key keeps the last
+// maximum), as a string; false when none qualifies. Scratch buffers are per thread (the
+// batched H5 calls it once per group). Same seeds, same order, same walks as compress().
+// Neighbours by an open-addressing table of the group's k-mers (built once per group)
+// instead of Graph::find's binary search: the walks look up ~2 neighbours per node.
+struct KmerIndex {
+    std::vector<u128> key;
+    std::vector<int32_t> at;  // -1: empty
+    uint64_t mask = 0;
+    static uint64_t hash(u128 x) {
+        const uint64_t h = (uint64_t)x ^ (uint64_t)(x >> 64) * 0x9E3779B97F4A7C15ull;
+        return (h ^ (h >> 29)) * 0xBF58476D1CE4E5B9ull;
+    }
+    void build(const Graph& g) {
+        size_t cap = 16;
+        while (cap < 2 * (size_t)g.size()) cap <<= 1;
+        key.resize(cap);
+        at.assign(cap, -1);
+        mask = cap - 1;
+        for (int64_t i = 0; i < g.size(); ++i) {
+            uint64_t h = hash(g.km[i]) & mask;
+            while (at[h] >= 0) h = (h + 1) & mask;
+            key[h] = g.km[i];
+            at[h] = (int32_t)i;
+        }
+    }
+    int64_t find(u128 x) const {
+        for (uint64_t h = hash(x) & mask;; h = (h + 1) & mask) {
+            if (at[h] < 0) return -1;
+            if (key[h] == x) return at[h];
+        }
+    }
+};
+
+bool compress_largest(const Graph& g, int64_t min_len, std::string* out) {
+    thread_local std::vector<char> avail;
+    thread_local std::vector<int64_t> lpath, rpath, best;
+    thread_local KmerIndex ix;
+    const int64_t n = g.size();
+    avail.assign((size_t)n, 1);
+    ix.build(g);
+    int64_t best_len = -1;
+    for (int64_t seed = 0; seed < n; ++seed) {
+        if (!avail[seed]) continue;
+        avail[seed] = 0;
+        lpath.clear();
+        rpath.clear();
+        for (int64_t cur = seed;;) {  // extend left
+            const unsigned l = g.ex[cur] & 0xFu;
+            if (popc4(l) != 1) break;
+            const int64_t nx = ix.find(g.ext_left(g.km[cur], ctz4(l)));
+            if (nx < 0 || !avail[nx] || popc4(g.ex[nx] >> 4) != 1) break;
+            avail[nx] = 0;
+            lpath.push_back(nx);
+            cur = nx;
+        }
+        for (int64_t cur = seed;;) {  // extend right
+            const unsigned r = g.ex[cur] >> 4;
+            if (popc4(r) != 1) break;
+            const int64_t nx = ix.find(g.ext_right(g.km[cur], ctz4(r)));
+            if (nx < 0 || !avail[nx] || popc4(g.ex[nx] & 0xFu) != 1) break;
+            avail[nx] = 0;
+            rpath.push_back(nx);
+            cur = nx;
+        }
+        const int64_t len = g.K + (int64_t)(lpath.size() + rpath.size());
+        if (len < min_len || len < best_len) continue;
+        best_len = len;
+        best.assign(lpath.rbegin(), lpath.rend());
+        best.push_back(seed);
+        best.insert(best.end(), rpath.begin(), rpath.end());
+    }
+    if (best_len < 0) return false;
+    *out = g.seq(best[0]);
+    for (size_t i = 1; i < best.size(); ++i) out->push_back("ACGT"[(int)(g.km[best[i]] & 3)]);
+    return true;
+}
+
 // ---------------------------------------------------- compression (fracture.rs:351-383)
 std::vector<std::string> compress(const Graph& g) {
     const int64_t n = g.size();
@@ -731,13 +810,13 @@ int rogtk_assemble_groups_host(const uint64_t* kmers, const uint8_t* exts, const
     std::atomic<int64_t> next{0};
     auto work = [&]() {
         std::vector<std::string> cs;
+        Graph gr;  // reused across the thread's groups (no allocation once grown)
         for (;;) {
             const int64_t g0 = next.fetch_add(64);
             if (g0 >= n_groups) return;
             for (int64_t g = g0; g < std::min<int64_t>(n_groups, g0 + 64); ++g) {
                 const int K = (int)group_stats[5 * g];
                 if (K <= 0 || group_stats[5 * g + 1] == 0) continue;  // k > 64 / no valid sequences
-                Graph gr;
                 gr.K = K;
                 gr.mask = K == 64 ? ~(u128)0 : (((u128)1 << (2 * K)) - 1);
                 const int64_t a = entry_offsets[g], b = entry_offsets[g + 1];
@@ -745,6 +824,11 @@ int rogtk_assemble_groups_host(const uint64_t* kmers, const uint8_t* exts, const
                 for (int64_t i = a; i < b; ++i) gr.km[i - a] = ((u128)kmers[2 * i] << 64) | kmers[2 * i + 1];
                 gr.ex.assign(exts + a, exts + b);
                 gr.cov.assign(counts + a, counts + b);
+                if (m == M_COMPRESSION && only_largest) {  // the expression's default: one string
+                    std::string& o = per[g];
+                    nc[g] = compress_largest(gr, std::max<int64_t>(min_length, 0), &o) ? 1 : 0;
+                    continue;
+                }
                 assemble_graph(gr, m, sa, ea, only_largest, min_length, &cs);
                 nc[g] = (int64_t)cs.size();
                 std::string& o = per[g];
