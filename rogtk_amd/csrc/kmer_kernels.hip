@@ -1598,7 +1598,7 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
 // group is processed (the descriptor two groups ahead), so a group waits on HBM only when
 // its chunk of 64 groups starts.
 // Two instances: 1024 slots (class 2), and 2048 (class 6) for the groups past class 2's
-// claim bound or packed words: at C3's UMI collision rate a group of 22-38 rows often holds
+// claim bound or packed words (39..64 rows of 150 bases): at C3's UMI collision rate a group of 22-38 rows often holds
 // 2-3 molecules' reads, past 768 distinct k-mers (~7% of the k_eff-16 work went to the
 // workgroup kernel before the big instance)
 constexpr int kWaveRows = 64;       // one row per lane
@@ -2051,6 +2051,7 @@ __global__ __launch_bounds__(kBlock) void k_group_classify(const int64_t* __rest
             cls = kClsEmpty;
         } else if (K <= 32 && obs > 0) {
             if (wave && K <= 16 && nrows <= kWaveRows && words <= kWaveWords) cls = 2;
+            else if (wave && K <= 16 && nrows <= kWaveRows && words <= kWaveBigWords) cls = kClsWaveBig;
             else if (wave && K <= 16 && nrows <= kWaveRows && words <= kWaveBigWords) cls = kClsWaveBig;
             else if (nrows <= LdsCfg<3>::kRows && words <= LdsCfg<3>::kWords) cls = 3;
             else if (nrows <= LdsCfg<1>::kRows && words <= LdsCfg<1>::kWords) cls = 1;
