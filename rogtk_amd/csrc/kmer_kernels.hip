@@ -994,10 +994,7 @@ __global__ __launch_bounds__(kBlock) void k_pack(const uint64_t* __restrict__ t_
 // compacted, bitonic-sorted and censored by binary search, all in LDS. The all-ones
 // key (TTT..T at k = 32) equals the empty marker and gets a dedicated slot.
 constexpr int kLdsBlock = 512;  // 8 waves per group workgroup (16 per CU for class 1; 1024 measured slower)
-#ifndef ROGTK_KMER_RANKSORT
-#define ROGTK_KMER_RANKSORT 1  // 65..512 valid entries by a rank sort (0: bitonic; experiment builds)
-#endif
-constexpr bool kRankSort = ROGTK_KMER_RANKSORT;
+constexpr bool kRankSort = true;  // 65..512 valid entries by a rank sort (round 5; bitonic above)
 
 // Size classes, tried in the order 3, 1, 4; larger groups take the global radix-sort
 // path. Class 3 (<= 192 rows, <= 576 words, a 2048-slot table for up to 1472 distinct

@@ -548,11 +548,7 @@ int launch_score_packed(const uint32_t* codes, const uint64_t* regular_bits, int
     // exact: the profiling events ride on the dispatch packet (kernel execution time only,
     // comparable with rocprofv3's kernel trace; bench.py's roofline.frac)
     ProfScope prof(K_SCORE_PACKED, s, true);
-#ifdef ROGTK_SCORE_WGS  // experiment builds: grid-stride over WGS workgroups per CU
-    const int g = std::min(grid_for((n + kRowsPerLane - 1) / kRowsPerLane), ROGTK_SCORE_WGS * 256);
-#else
     const int g = grid_for((n + kRowsPerLane - 1) / kRowsPerLane);
-#endif
     const int sel = (score ? 4 : 0) | (hamd ? 2 : 0) | (hamw ? 1 : 0);
     // profiling: the kernel's own execution span from in-kernel clocks (NULL otherwise)
     uint64_t* tspan = span_begin(K_SCORE_PACKED, g, s);
