@@ -2320,12 +2320,17 @@ __global__ __launch_bounds__(64 * kMzWaves) void k_minimizer_filter(const GroupD
             total = __builtin_amdgcn_readfirstlane(total);
             // the lists of the lanes in `sel` into the table; with a cap on the claims
             // (none is needed while the keys inserted stay within kMzClaim)
+            // each lane walks its list from its own rotation: the rows of one group (copies of
+            // one molecule) hold the same minimizers in the same order, and lanes adding the
+            // same key in one step serialise on its slot
+            const int rot = nn > 0 ? (5 * lane) % nn : 0;
             auto insert = [&](bool sel, bool capped) {
                 uint32_t claimed_here = 0;
                 for (int k = 0; k < nmax; ++k) {
                     bool fresh = false;
                     if (sel && k < nn) {
-                        const uint32_t m = lst[k];
+                        const int kk0 = k + rot;
+                        const uint32_t m = lst[kk0 >= nn ? kk0 - nn : kk0];
                         const unsigned long long kk = ((unsigned long long)cj << 32) | m;
                         uint32_t slot = ((m ^ (uint32_t)cj * 0x85EBCA77u) * 0x9E3779B1u) >> 23;  // 512 slots
                         while (true) {
