@@ -1596,14 +1596,14 @@ __global__ __launch_bounds__(TB, CLS == 3 ? 8 : 1) void k_kmer_lds(const GroupDe
 // its chunk of 64 groups starts.
 // Two instances: 1024 slots (class 2), and 2048 (class 6) for the groups past class 2's
 // claim bound or packed words (39..64 rows of 150 bases): at C3's UMI collision rate a group of 22-38 rows often holds
-// 2-3 molecules' reads, past 768 distinct k-mers (~7% of the k_eff-16 work went to the
+// 2-3 molecules' reads, past 768-832 distinct k-mers (~7% of the k_eff-16 work went to the
 // workgroup kernel before the big instance)
 constexpr int kWaveRows = 64;       // one row per lane
 constexpr uint8_t kClsWaveBig = 6;  // the 2048-slot instance's class
 template <int SLOTS>
 struct WaveCfg {
     static constexpr int kSlots = SLOTS;          // table slots per wave (8 / 16 KB)
-    static constexpr int kClaim = SLOTS * 3 / 4;  // distinct k-mers (checked every 2 trips: <= 7/8 of the slots)
+    static constexpr int kClaim = SLOTS * 13 / 16;  // distinct k-mers (checked every 2 trips: <= 15/16 of the slots)
     static constexpr int kValid = SLOTS / 2;      // valid k-mers (compacted to the front; keys bucketed behind them)
     static constexpr int kWords = SLOTS == 1024 ? 192 : 320;  // packed words (38 / 64 rows at stride 5)
     static constexpr int kWG = SLOTS == 1024 ? 2 : 1;          // waves per workgroup (8 workgroups per CU)
@@ -1825,7 +1825,7 @@ __global__ __launch_bounds__(64 * WaveCfg<SLOTS>::kWG) __attribute__((amdgpu_wav
             }
             return (uint32_t)__popcll(__ballot((v == kWEmpty) & (allt == 0u)));
         };
-        // the claim bound is checked every second step: <= 768 + 128 keys stay below the
+        // the claim bound is checked every second step: <= 13/16 + 128 keys stay below the
         // table's 1024 slots, so probing always ends
         for (int t = 0; t < Ls; t += 2) {
             claims += step(t);
