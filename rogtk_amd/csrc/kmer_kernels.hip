@@ -1784,12 +1784,13 @@ __global__ __launch_bounds__(64 * WaveCfg<SLOTS>::kWG) __attribute__((amdgpu_wav
         // of its own on the trip's chain). The segment's start window is kept for the wrap.
         const uint32_t wrapb = nst > 0 && pst > 0 ? base_at(pst - 1) : 0u;
         uint32_t prevb = nst > 0 && pst + rot > 0 ? base_at(pst + rot - 1) : 0u;
-        uint64_t win = 0, nwd = 0, win_s = 0;
+        uint32_t key = 0u, key_s = 0u;
+        uint64_t aw = 0;
         int p = pst + rot;
         if (nst > 0) {
-            win_s = win_at(pst);
-            win = rot ? win_at(p) : win_s;
-            nwd = W[wo_r + (p >> 5) + 1];
+            key_s = (uint32_t)(win_at(pst) >> (64 - 2 * K)) & kmask;
+            key = rot ? (uint32_t)(win_at(p) >> (64 - 2 * K)) & kmask : key_s;
+            aw = W[wo_r + ((p + K) >> 5)];
         }
         uint32_t claims = 0;
         bool over = false;
@@ -1797,30 +1798,30 @@ __global__ __launch_bounds__(64 * WaveCfg<SLOTS>::kWG) __attribute__((amdgpu_wav
         auto step = [&](int t) -> uint32_t {
             uint32_t v = 0u, allt = 1u;  // (a lane past its segment claims nothing)
             if (t < nst) {
-                const uint32_t key = (uint32_t)(win >> (64 - 2 * K)) & kmask;
+                const uint32_t rb = (uint32_t)(aw >> (62 - 2 * ((p + K) & 31))) & 3u;  // base p+K
                 uint32_t e = p > 0 ? 1u << prevb : 0u;
-                if (p + K < len_r) e |= 1u << (4 + ((uint32_t)(win >> (62 - 2 * K)) & 3u));
+                if (p + K < len_r) e |= 16u << rb;
                 uint32_t h = wave_hash<SLOTS>(key);
                 const bool wrap = p + 1 == pst + nst;
                 const int pn = wrap ? pst : p + 1;
-                const uint64_t nwd_n = W[wo_r + (pn >> 5) + 1];
+                const uint64_t aw_n = W[wo_r + ((pn + K) >> 5)];
                 // claim or find the key's slot (a 32-bit CAS), then count it: a returning add
                 // whose old value shows whether the extension bits are new (then an OR)
                 allt = key == kWEmpty;
                 h = allt ? (uint32_t)kWaveSlots : h;
                 v = atomicCAS(&TK[h], kWEmpty, key);
-                while (v != kWEmpty && v != key) {
+                // one combined test (bitwise: no branch per condition)
+                for (uint32_t miss = (uint32_t)(v != kWEmpty) & (uint32_t)(v != key); miss;
+                     miss = (uint32_t)(v != kWEmpty) & (uint32_t)(v != key)) {
                     h = (h + 1) & (kWaveSlots - 1);
                     v = atomicCAS(&TK[h], kWEmpty, key);
                 }
                 const uint32_t old = atomicAdd(&TV[h], 1u << 8);
                 if (e & ~old & 0xFFu) atomicOr(&TV[h], e);
                 // the next position (a wrap restarts the segment): selects by masks, no branch
-                const uint64_t wm = 0ull - (uint64_t)wrap;
-                const uint64_t nxt = (win << 2) | ((nwd >> (62 - 2 * (p & 31))) & 3u);
-                prevb = wrap ? wrapb : (uint32_t)(win >> 62);
-                win = (nxt & ~wm) | (win_s & wm);
-                nwd = nwd_n;
+                prevb = wrap ? wrapb : key >> (2 * K - 2);
+                key = wrap ? key_s : ((key << 2) | rb) & kmask;
+                aw = aw_n;
                 p = pn;
             }
             return (uint32_t)__popcll(__ballot((v == kWEmpty) & (allt == 0u)));
