@@ -1945,11 +1945,9 @@ __global__ __launch_bounds__(64 * WaveCfg<SLOTS>::kWG) __attribute__((amdgpu_wav
                             const uint32_t bb = (uint32_t)__builtin_ctz(lb);
                             const uint32_t nb = (key >> 2) | (bb << (2 * K - 2));
                             const uint32_t q2 = C[nb >> bsh & 255u], a2 = q2 & 0xFFFFu, n2 = q2 >> 16;
-                            for (uint32_t m = 0; m < n2; ++m)
-                                if (K2[a2 + m] == nb) {
-                                    nx |= 1u << bb;
-                                    break;
-                                }
+                            uint32_t hit = 0u;  // (no early exit: a bucket holds ~1 key)
+                            for (uint32_t m = 0; m < n2; ++m) hit |= (uint32_t)(K2[a2 + m] == nb);
+                            nx |= hit << bb;
                         }
                         const int64_t o = base + rank;
                         if (lo_only) {
