@@ -1795,9 +1795,9 @@ __global__ __launch_bounds__(64 * WaveCfg<SLOTS>::kWG) __attribute__((amdgpu_wav
         uint32_t claims = 0;
         bool over = false;
         // one insert step of the lane's segment; returns the wave's new claims
-        auto step = [&](int t) -> uint32_t {
+        auto step = [&](int t, auto check) -> uint32_t {
             uint32_t v = 0u, allt = 1u;  // (a lane past its segment claims nothing)
-            if (t < nst) {
+            if (!decltype(check)::value || t < nst) {
                 const uint32_t rb = (uint32_t)(aw >> (62 - 2 * ((p + K) & 31))) & 3u;  // base p+K
                 uint32_t e = p > 0 ? 1u << prevb : 0u;
                 if (p + K < len_r) e |= 16u << rb;
@@ -1828,9 +1828,31 @@ __global__ __launch_bounds__(64 * WaveCfg<SLOTS>::kWG) __attribute__((amdgpu_wav
         };
         // the claim bound is checked every second step: <= 13/16 + 128 keys stay below the
         // table's 1024 slots, so probing always ends
-        for (int t = 0; t < Ls; t += 2) {
-            claims += step(t);
-            if (t + 1 < Ls) claims += step(t + 1);
+        // trips every row's lanes take (the shortest segment of a row: its last one) run
+        // inside one exec mask of the rows' lanes, without a per-trip segment test
+        int lmin = r < nrows ? nst : 1 << 30;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) lmin = min(lmin, __shfl_xor(lmin, m));
+        const int L0 = __builtin_amdgcn_readfirstlane(min(lmin, Ls)) & ~1;  // even: checks stay paired
+        using kNoCheck = std::integral_constant<bool, false>;
+        using kCheck = std::integral_constant<bool, true>;
+        int t = 0;
+        if (r < nrows) {
+            for (; t < L0; t += 2) {
+                claims += step(t, kNoCheck{});
+                claims += step(t + 1, kNoCheck{});
+                if (claims > (uint32_t)kWaveClaim) {
+                    over = true;
+                    break;
+                }
+            }
+        }
+        t = __builtin_amdgcn_readfirstlane(t);
+        over = __builtin_amdgcn_readfirstlane((int)over) != 0;
+        claims = __builtin_amdgcn_readfirstlane(claims);
+        for (; !over && t < Ls; t += 2) {
+            claims += step(t, kCheck{});
+            if (t + 1 < Ls) claims += step(t + 1, kCheck{});
             if (claims > (uint32_t)kWaveClaim) {
                 over = true;
                 break;
