@@ -1953,11 +1953,20 @@ __global__ __launch_bounds__(64 * WaveCfg<SLOTS>::kWG) __attribute__((amdgpu_wav
                         const uint32_t qr = C[((key << 2) & kmask) >> bsh & 255u];
                         const uint32_t at = q & 0xFFFFu, bn = q >> 16;
                         uint32_t rank = at;
-                        for (uint32_t m = 0; m < bn; ++m) rank += K2[at + m] < key;
+                        // the first 4 keys of a bucket by predicated reads (a bucket holds ~1
+                        // key; the key table's pad keeps the reads in bounds), a loop past them
+#pragma unroll
+                        for (uint32_t m = 0; m < 4; ++m) rank += (uint32_t)(m < bn) & (uint32_t)(K2[at + m] < key);
+                        for (uint32_t m = 4; m < bn; ++m) rank += K2[at + m] < key;
                         uint32_t nx = 0;
-                        if (ex >> 4) {
+                        {
                             const uint32_t ar = qr & 0xFFFFu, nr = qr >> 16, lo = key & kmask2;
-                            for (uint32_t m = 0; m < nr; ++m) {
+#pragma unroll
+                            for (uint32_t m = 0; m < 4; ++m) {
+                                const uint32_t k2 = K2[ar + m];
+                                nx |= ((uint32_t)(m < nr) & (uint32_t)((k2 >> 2) == lo)) << (4 + (k2 & 3u));
+                            }
+                            for (uint32_t m = 4; m < nr; ++m) {
                                 const uint32_t k2 = K2[ar + m];
                                 if ((k2 >> 2) == lo) nx |= 16u << (k2 & 3u);
                             }
