@@ -1972,7 +1972,22 @@ __global__ __launch_bounds__(64 * WaveCfg<SLOTS>::kWG) __attribute__((amdgpu_wav
                             }
                             nx &= ex & 0xF0u;
                         }
-                        for (uint32_t lb = ex & 0xFu; lb; lb &= lb - 1) {
+                        // left neighbours: the first set bit (nearly always the only one)
+                        // straight-line with predicated reads, any further bits by a loop
+                        uint32_t lb = ex & 0xFu;
+                        {
+                            const uint32_t bb = (uint32_t)__builtin_ctz(lb | 0x10u) & 3u;
+                            const uint32_t nb = (key >> 2) | (bb << (2 * K - 2));
+                            const uint32_t q2 = C[nb >> bsh & 255u], a2 = q2 & 0xFFFFu;
+                            const uint32_t n2 = lb ? q2 >> 16 : 0u;
+                            uint32_t hit = 0u;
+#pragma unroll
+                            for (uint32_t m = 0; m < 4; ++m) hit |= (uint32_t)(m < n2) & (uint32_t)(K2[a2 + m] == nb);
+                            for (uint32_t m = 4; m < n2; ++m) hit |= (uint32_t)(K2[a2 + m] == nb);
+                            nx |= hit << bb;
+                            lb &= lb - 1;
+                        }
+                        for (; lb; lb &= lb - 1) {
                             const uint32_t bb = (uint32_t)__builtin_ctz(lb);
                             const uint32_t nb = (key >> 2) | (bb << (2 * K - 2));
                             const uint32_t q2 = C[nb >> bsh & 255u], a2 = q2 & 0xFFFFu, n2 = q2 >> 16;
