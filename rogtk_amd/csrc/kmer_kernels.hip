@@ -1817,7 +1817,7 @@ __global__ __launch_bounds__(64 * WaveCfg<SLOTS>::kWG) __attribute__((amdgpu_wav
                     v = atomicCAS(&TK[h], kWEmpty, key);
                 }
                 const uint32_t old = atomicAdd(&TV[h], 1u << 8);
-                if (e & ~old & 0xFFu) atomicOr(&TV[h], e);
+                atomicOr(&TV[h], e & ~old & 0xFFu);  // (no branch: an OR of 0 changes nothing)
                 // the next position (a wrap restarts the segment): selects by masks, no branch
                 prevb = wrap ? wrapb : key >> (2 * K - 2);
                 key = wrap ? key_s : ((key << 2) | rb) & kmask;
